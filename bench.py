@@ -1,0 +1,228 @@
+#!/usr/bin/env python3
+"""bench.py — merged changes/sec of the batched CRDT merge on MI355X.
+
+Workload (BASELINE.json configs[3], "C4"): per GPU, 1M documents x 8 actors x
+8 changes (64 changes/doc, 1-2 map sets per change), documents drawn from one
+global stream of base58 doc ids and sharded by FNV-1a64(docId) % world_size
+(weak scaling: every rank merges its own 1M-document shard; the merge has no
+cross-document exchange, so the timed step has no collective).
+
+A step = one cold ``Backend.applyChanges(Backend.init(), changes)`` of every
+document in the shard (what ``DocBackend.init`` / ``applyRemoteChanges`` hand
+Automerge, src/DocBackend.ts:144-185) plus the DocBackend clock bookkeeping:
+history order, allDeps, clocks, heads, map registers with conflicts and
+counters.  Inputs are resident in HBM before the timed region.
+
+Prints ONE JSON line (rank 0).  ``value`` = changes that entered history over
+all ranks / max-over-ranks wall time of the K timed steps.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def _dist():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--docs", type=int, default=1_000_000, help="documents per GPU")
+    ap.add_argument("--config", default="C4")
+    ap.add_argument("--cpu-sample-docs", type=int, default=200_000)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--check-docs", type=int, default=20_000, help="docs checked against the oracle")
+    args = ap.parse_args()
+
+    ws, rank, local = _dist()
+    import torch
+    import torch.distributed as dist
+    if ws > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from hypermerge_amd import synth
+    from hypermerge_amd.columnar import CBatch, CResults, Results
+    from hypermerge_amd.engine import Engine
+
+    t0 = time.time()
+    cfg = synth.config(args.config, n_docs=args.docs, shard=rank, n_shards=ws)
+    batch = synth.generate(cfg, threads=min(16, os.cpu_count() or 1))
+    gen_s = time.time() - t0
+
+    eng = Engine(local)
+
+    def to_dev(a: np.ndarray) -> torch.Tensor:
+        t = torch.from_numpy(a.view(np.uint8).reshape(-1)).to(dev)
+        return t
+
+    S = batch.a_stride
+    nd, nc, no = batch.n_docs, len(batch.changes), len(batch.ops)
+    nr = int(batch.docs["n_regs"].sum())
+    d_docs, d_ch, d_dp, d_op = (to_dev(x) for x in (batch.docs, batch.changes, batch.deps, batch.ops))
+    u8 = dict(dtype=torch.uint8, device=dev)
+    r_docs = torch.zeros(nd * 32, **u8)
+    r_clock = torch.zeros(nd * S, dtype=torch.int32, device=dev)
+    r_bclock = torch.zeros(nd * S, dtype=torch.int32, device=dev)
+    r_heads = torch.zeros(nd * S, dtype=torch.int32, device=dev)
+    r_hist = torch.zeros(nc, dtype=torch.int32, device=dev)
+    r_ad = torch.zeros(nc * S, dtype=torch.int32, device=dev)
+    r_regs = torch.zeros(nr * 16, **u8)
+    r_surv = torch.zeros(no * 16, **u8)
+    hc = batch.c_struct()
+    cb = CBatch(hc.n_docs, hc.n_changes, hc.n_deps, hc.n_ops, hc.n_regs, hc.a_stride,
+                hc.max_changes, hc.max_ops, hc.max_regs, hc.max_objs,
+                d_docs.data_ptr(), d_ch.data_ptr(), d_dp.data_ptr(), d_op.data_ptr(), None)
+    cr = CResults(r_docs.data_ptr(), r_clock.data_ptr(), r_bclock.data_ptr(), r_heads.data_ptr(),
+                  r_hist.data_ptr(), r_ad.data_ptr(), r_regs.data_ptr(), r_surv.data_ptr())
+    stream = torch.cuda.Stream(dev)          # a real stream: the C-ABI treats handle 0 as "engine stream"
+    torch.cuda.set_stream(stream)
+    sptr = stream.cuda_stream
+
+    def step():
+        eng.merge_device(cb, cr, sptr)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t_start = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t_start
+    ev_ms = ev0.elapsed_time(ev1)
+    # per-launch kernel duration: HIP events on the launch stream, one extra timed launch
+    klist = []
+    for _ in range(max(3, min(args.steps, 10))):
+        step()
+        klist.append(eng.last_kernel_ms()[0])
+    kern_ms = float(np.mean(klist))
+
+    # pull results back once for counting + spot parity
+    from hypermerge_amd.columnar import DOC_RESULT_DT
+    docs_res = r_docs.cpu().numpy().view(DOC_RESULT_DT)
+    applied = int(docs_res["hist_len"].astype(np.int64).sum())
+    unsupported = int((docs_res["status"] == 16).sum())
+    errors = int(((docs_res["status"] != 0) & (docs_res["status"] != 16)).sum())
+
+    if ws > 1:
+        t_app = torch.tensor([float(applied)], dtype=torch.float64, device=dev)
+        dist.all_reduce(t_app, op=dist.ReduceOp.SUM)
+        t_time = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(t_time, op=dist.ReduceOp.MAX)
+        applied_all, wall_max = float(t_app.item()), float(t_time.item())
+    else:
+        applied_all, wall_max = float(applied), wall
+
+    value = applied_all * args.steps / wall_max
+    ms_per_step = wall_max * 1000.0 / args.steps
+    # roofline of the dominant kernel (merge_small_kernel): algorithmic bytes per launch
+    full = Results(docs_res, None, None, None, None, None, None, None)
+    alg_bytes = batch.algorithmic_bytes(full)
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+
+    # spot parity against the oracle on a sample (checker only; not timed)
+    parity = None
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        import oracle.oracle as O
+        from hypermerge_amd.columnar import Batch
+        k = min(args.check_docs, nd)
+        sub = _subbatch(batch, k)
+        g = eng.merge(sub)
+        o = O.merge(sub, threads=min(16, os.cpu_count() or 1))
+        parity = bool(_same(sub, g, o))
+        ns = min(args.cpu_sample_docs, nd)
+        cs = _subbatch(batch, ns)
+        t = time.perf_counter()
+        oc = O.merge(cs, threads=1)
+        dt = time.perf_counter() - t
+        cpu = {"value": float(oc.docs["hist_len"].sum()) / dt, "unit": "changes/s", "cores": 1, "kind": "port",
+               "sample": f"oracle/oracle.c (C restatement, single thread) on the first {ns} docs "
+                         f"({int(oc.docs['hist_len'].sum())} changes) of this rank's {args.config} shard, {dt:.2f}s"}
+
+    if rank == 0:
+        line = {
+            "metric": "merged changes/sec (1M docs×8 actors) at 1/2/4/8 GPUs + % HBM roofline",
+            "value": value, "unit": "changes/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u32", "data": "synthetic (seeded gossip feeds, hypermerge_amd/csrc/synth.cpp)",
+            "config": {"workload": f"{args.config}: {nd} docs/GPU x {batch.docs['n_actors'].max()} actors x "
+                                   f"{nc // max(nd, 1)} changes/doc, map LWW sets", "docs_per_gpu": nd,
+                       "changes_per_gpu": nc, "ops_per_gpu": no, "parallelism": f"doc-shard{ws}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": achieved / PEAK_HBM_GBS, "traffic": None,
+                         "kernel": "merge_small_kernel", "kernel_ms": kern_ms, "alg_bytes": alg_bytes},
+            "cpu_baseline": cpu,
+            "parity_sample_ok": parity, "unsupported_docs": unsupported, "error_docs": errors,
+            "gen_s": round(gen_s, 2), "event_ms_per_step": ev_ms / args.steps,
+        }
+        print(json.dumps(line), flush=True)
+    if ws > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+def _subbatch(b, k):
+    """First k documents of a batch as a self-contained batch."""
+    from hypermerge_amd.columnar import Batch
+    docs = b.docs[:k].copy()
+    nc = int(docs["change_off"][-1] + docs["n_changes"][-1]) if k else 0
+    no = int(docs["op_off"][-1] + docs["n_ops"][-1]) if k else 0
+    ch = b.changes[:nc].copy()
+    nd = int(ch["dep_off"][-1] + ch["n_deps"][-1]) if nc else 0
+    return Batch(docs, ch, b.deps[:nd].copy(), b.ops[:no].copy(), b.a_stride)
+
+
+def _same(b, g, o) -> bool:
+    ok = (g.docs["status"] != 16)
+    if not np.array_equal(g.docs["status"][ok], o.docs["status"][ok]):
+        return False
+    good = ok & (o.docs["status"] == 0)
+    S = b.a_stride
+    for f in ("clock", "back_clock", "heads"):
+        if not np.array_equal(getattr(g, f)[np.repeat(good, S)], getattr(o, f)[np.repeat(good, S)]):
+            return False
+    cm = np.repeat(good, b.docs["n_changes"])
+    if not np.array_equal(g.hist[cm], o.hist[cm]) or not np.array_equal(g.all_deps[np.repeat(cm, S)], o.all_deps[np.repeat(cm, S)]):
+        return False
+    rm = np.repeat(good, b.docs["n_regs"])
+    if not np.array_equal(g.regs[rm], o.regs[rm]):
+        return False
+    sm = np.zeros(len(b.ops), bool)
+    for d in np.nonzero(good)[0]:
+        s0 = int(b.docs["op_off"][d]); sm[s0:s0 + int(o.docs["n_surv"][d])] = True
+    return bool(np.array_equal(g.surv[sm], o.surv[sm]))
+
+
+if __name__ == "__main__":
+    sys.exit(main())

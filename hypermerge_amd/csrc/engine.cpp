@@ -1,0 +1,241 @@
+// engine.cpp — the C-ABI of include/hypermerge_amd.h (host side of the engine).
+//
+// Owns the HIP device, stream, events and staging buffers; sizes and launches
+// the merge kernels.  No C++ exception crosses the ABI: every entry point
+// catches and returns an hm_status.  There is no CPU fallback: if the HIP
+// library cannot run, calls fail with HM_ERR_DEVICE.
+#include <hip/hip_runtime.h>
+#include <cstring>
+#include <string>
+#include <vector>
+#include <algorithm>
+#include <new>
+#include "../../include/hypermerge_amd.h"
+#include "merge_kernels.h"
+
+struct hm_engine {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[4] = {};
+    float last_ms[2] = {0, 0};
+    int n_last = 0;
+    int num_cus = 256;
+    std::string err;
+    void *dbuf = nullptr;
+    size_t dbuf_size = 0;
+};
+
+namespace {
+
+int fail(hm_engine *e, int status, const std::string &msg) {
+    if (e) e->err = msg;
+    return status;
+}
+
+int hip_fail(hm_engine *e, hipError_t r, const char *what) {
+    return fail(e, HM_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(r));
+}
+
+#define HIPCHK(e, call)                                   \
+    do {                                                  \
+        hipError_t _r = (call);                           \
+        if (_r != hipSuccess) return hip_fail(e, _r, #call); \
+    } while (0)
+
+struct Caps { uint32_t opl, regs, objs; };
+
+Caps launch_caps(const hm_batch *b) {
+    Caps c;
+    uint32_t mo = b->max_ops;
+    c.opl = mo <= 64 ? 1 : (mo <= 128 ? 2 : 4);
+    c.regs = std::max<uint32_t>(1, std::min<uint32_t>(b->max_regs, 1024));
+    c.regs = (c.regs + 15) & ~15u;
+    c.objs = std::max<uint32_t>(1, std::min<uint32_t>(b->max_objs, 256));
+    c.objs = (c.objs + 15) & ~15u;
+    return c;
+}
+
+int launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, hipStream_t s) {
+    Caps c = launch_caps(b);
+    SmallParams p;
+    p.docs = b->docs; p.changes = b->changes; p.deps = b->deps; p.ops = b->ops; p.min_clock = b->min_clock;
+    p.res_docs = o->docs; p.res_clock = o->clock; p.res_back_clock = o->back_clock; p.res_heads = o->heads;
+    p.res_hist = o->hist; p.res_all_deps = o->all_deps; p.res_regs = o->regs; p.res_surv = o->surv;
+    p.n_docs = b->n_docs; p.a_stride = b->a_stride; p.cap_regs = c.regs; p.cap_objs = c.objs;
+    if (b->n_docs == 0) { e->n_last = 0; return HM_OK; }
+    // persistent grid: enough resident 1-wave workgroups to fill every CU
+    size_t lds = hm_small_lds_bytes(c.opl, c.regs, c.objs);
+    uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, (160 * 1024) / std::max<size_t>(lds, 1)));
+    uint32_t grid = std::min<uint32_t>(b->n_docs, (uint32_t)e->num_cus * per_cu * 2);
+    HIPCHK(e, hipEventRecord(e->ev[0], s));
+    hipError_t r = hm_launch_small(p, c.opl, grid, s);
+    if (r != hipSuccess) return hip_fail(e, r, "merge_small_kernel launch");
+    HIPCHK(e, hipEventRecord(e->ev[1], s));
+    e->n_last = 1;
+    return HM_OK;
+}
+
+int check_batch(hm_engine *e, const hm_batch *b) {
+    if (!b || b->a_stride == 0 || b->a_stride > 64) return fail(e, HM_ERR_INVALID, "a_stride must be in [1,64]");
+    if (b->n_docs && !b->docs) return fail(e, HM_ERR_INVALID, "docs table missing");
+    return HM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t hm_abi_version(void) { return HM_ABI_VERSION; }
+
+const char *hm_status_message(int status) {
+    switch (status) {
+    case HM_OK: return "ok";
+    case HM_ERR_INCONSISTENT_SEQ: return "Inconsistent reuse of sequence number";
+    case HM_ERR_UNKNOWN_OBJECT: return "Modification of unknown object";
+    case HM_ERR_DUPLICATE_OBJECT: return "Duplicate creation of object";
+    case HM_ERR_DUPLICATE_ELEM: return "Duplicate list element ID";
+    case HM_ERR_MISSING_ELEM: return "Missing index entry for list element";
+    case HM_ERR_UNSUPPORTED: return "document outside the engine envelope";
+    case HM_ERR_INVALID: return "invalid batch";
+    case HM_ERR_DEVICE: return "HIP device error";
+    case HM_ERR_NOMEM: return "out of memory";
+    default: return "unknown status";
+    }
+}
+
+int hm_engine_create(const hm_config *cfg, hm_engine **out) {
+    if (!out) return HM_ERR_INVALID;
+    *out = nullptr;
+    hm_engine *e = new (std::nothrow) hm_engine();
+    if (!e) return HM_ERR_NOMEM;
+    e->device = cfg ? cfg->device : 0;
+    int n = 0;
+    hipError_t r = hipGetDeviceCount(&n);
+    if (r != hipSuccess || n <= e->device) { delete e; return HM_ERR_DEVICE; }
+    if (hipSetDevice(e->device) != hipSuccess) { delete e; return HM_ERR_DEVICE; }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, e->device) == hipSuccess) e->num_cus = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { delete e; return HM_ERR_DEVICE; }
+    for (auto &ev : e->ev)
+        if (hipEventCreate(&ev) != hipSuccess) { delete e; return HM_ERR_DEVICE; }
+    *out = e;
+    return HM_OK;
+}
+
+void hm_engine_destroy(hm_engine *e) {
+    if (!e) return;
+    hipSetDevice(e->device);
+    if (e->dbuf) hipFree(e->dbuf);
+    for (auto &ev : e->ev) if (ev) hipEventDestroy(ev);
+    if (e->stream) hipStreamDestroy(e->stream);
+    delete e;
+}
+
+const char *hm_engine_last_error(const hm_engine *e) { return e ? e->err.c_str() : "no engine"; }
+
+size_t hm_scratch_bytes(const hm_batch *) { return 0; }
+
+int hm_merge_device(hm_engine *e, const hm_batch *b, const hm_results *o, void *scratch, void *stream) {
+    (void)scratch;
+    try {
+        if (!e || !o) return HM_ERR_INVALID;
+        int st = check_batch(e, b);
+        if (st) return st;
+        if (b->n_docs && (!b->max_changes && !b->max_ops && !b->max_regs && !b->max_objs))
+            return fail(e, HM_ERR_INVALID, "device batches must carry max_* launch hints");
+        HIPCHK(e, hipSetDevice(e->device));
+        return launch_merge(e, b, o, stream ? (hipStream_t)stream : e->stream);
+    } catch (...) {
+        return fail(e, HM_ERR_DEVICE, "exception in hm_merge_device");
+    }
+}
+
+int hm_merge_host(hm_engine *e, const hm_batch *hb, const hm_results *ho) {
+    try {
+        if (!e || !hb || !ho) return HM_ERR_INVALID;
+        int st = check_batch(e, hb);
+        if (st) return st;
+        HIPCHK(e, hipSetDevice(e->device));
+        hm_batch b = *hb;
+        if (!b.max_changes && !b.max_ops && !b.max_regs && !b.max_objs)
+            for (uint32_t d = 0; d < b.n_docs; d++) {
+                b.max_changes = std::max(b.max_changes, hb->docs[d].n_changes);
+                b.max_ops = std::max(b.max_ops, hb->docs[d].n_ops);
+                b.max_regs = std::max(b.max_regs, hb->docs[d].n_regs);
+                b.max_objs = std::max(b.max_objs, hb->docs[d].n_objs);
+            }
+        const size_t S = b.a_stride;
+        struct Seg { size_t bytes; size_t off; };
+        auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+        size_t sz[13] = {
+            b.n_docs * sizeof(hm_doc_row), b.n_changes * sizeof(hm_change_row), b.n_deps * sizeof(hm_dep_row),
+            b.n_ops * sizeof(hm_op_row), hb->min_clock ? b.n_docs * S * 4 : 0,
+            b.n_docs * sizeof(hm_doc_result), b.n_docs * S * 4, b.n_docs * S * 4, b.n_docs * S * 4,
+            b.n_changes * 4, b.n_changes * S * 4, b.n_regs * sizeof(hm_reg_result), b.n_ops * sizeof(hm_surv_result)};
+        size_t off[13], total = 0;
+        for (int i = 0; i < 13; i++) { off[i] = total; total += al(sz[i] ? sz[i] : 1); }
+        if (total > e->dbuf_size) {
+            if (e->dbuf) hipFree(e->dbuf);
+            e->dbuf = nullptr; e->dbuf_size = 0;
+            if (hipMalloc(&e->dbuf, total) != hipSuccess) return fail(e, HM_ERR_NOMEM, "hipMalloc staging");
+            e->dbuf_size = total;
+        }
+        char *base = (char *)e->dbuf;
+        auto P = [&](int i) { return (void *)(base + off[i]); };
+        hipStream_t s = e->stream;
+        const void *src[5] = {hb->docs, hb->changes, hb->deps, hb->ops, hb->min_clock};
+        for (int i = 0; i < 5; i++)
+            if (sz[i]) HIPCHK(e, hipMemcpyAsync(P(i), src[i], sz[i], hipMemcpyHostToDevice, s));
+        b.docs = (const hm_doc_row *)P(0); b.changes = (const hm_change_row *)P(1);
+        b.deps = (const hm_dep_row *)P(2); b.ops = (const hm_op_row *)P(3);
+        b.min_clock = hb->min_clock ? (const uint32_t *)P(4) : nullptr;
+        hm_results d;
+        d.docs = (hm_doc_result *)P(5); d.clock = (uint32_t *)P(6); d.back_clock = (uint32_t *)P(7);
+        d.heads = (uint32_t *)P(8); d.hist = (int32_t *)P(9); d.all_deps = (uint32_t *)P(10);
+        d.regs = (hm_reg_result *)P(11); d.surv = (hm_surv_result *)P(12);
+        // the survivor table is only defined on [0, n_surv) per doc: zero it for stable host views
+        if (sz[12]) HIPCHK(e, hipMemsetAsync(P(12), 0, sz[12], s));
+        st = launch_merge(e, &b, &d, s);
+        if (st) return st;
+        void *dst[8] = {ho->docs, ho->clock, ho->back_clock, ho->heads, ho->hist, ho->all_deps, ho->regs, ho->surv};
+        for (int i = 0; i < 8; i++)
+            if (sz[5 + i] && dst[i]) HIPCHK(e, hipMemcpyAsync(dst[i], P(5 + i), sz[5 + i], hipMemcpyDeviceToHost, s));
+        HIPCHK(e, hipStreamSynchronize(s));
+        return HM_OK;
+    } catch (...) {
+        return fail(e, HM_ERR_DEVICE, "exception in hm_merge_host");
+    }
+}
+
+int hm_last_kernel_ms(hm_engine *e, float *ms, int max_kernels) {
+    if (!e || !ms) return 0;
+    int n = std::min(max_kernels, e->n_last);
+    for (int i = 0; i < n; i++) {
+        if (hipEventSynchronize(e->ev[2 * i + 1]) != hipSuccess) return 0;
+        if (hipEventElapsedTime(&ms[i], e->ev[2 * i], e->ev[2 * i + 1]) != hipSuccess) return 0;
+    }
+    return n;
+}
+
+int hm_clock_cmp_device(hm_engine *e, const uint32_t *a, const uint32_t *b, uint8_t *out, uint32_t n_docs,
+                        uint32_t a_stride, void *stream) {
+    if (!e) return HM_ERR_INVALID;
+    hipError_t r = hm_launch_clock(0, a, b, out, n_docs, a_stride, stream ? (hipStream_t)stream : e->stream);
+    return r == hipSuccess ? HM_OK : hip_fail(e, r, "clock_cmp");
+}
+
+int hm_clock_union_device(hm_engine *e, const uint32_t *a, const uint32_t *b, uint32_t *c, uint32_t n_docs,
+                          uint32_t a_stride, void *stream) {
+    if (!e) return HM_ERR_INVALID;
+    hipError_t r = hm_launch_clock(1, a, b, c, n_docs, a_stride, stream ? (hipStream_t)stream : e->stream);
+    return r == hipSuccess ? HM_OK : hip_fail(e, r, "clock_union");
+}
+
+int hm_clock_intersection_device(hm_engine *e, const uint32_t *a, const uint32_t *b, uint32_t *c,
+                                 uint32_t n_docs, uint32_t a_stride, void *stream) {
+    if (!e) return HM_ERR_INVALID;
+    hipError_t r = hm_launch_clock(2, a, b, c, n_docs, a_stride, stream ? (hipStream_t)stream : e->stream);
+    return r == hipSuccess ? HM_OK : hip_fail(e, r, "clock_intersection");
+}
+
+}  // extern "C"

@@ -1,0 +1,693 @@
+// merge_kernels.hip — CDNA4 (gfx950) kernels of the batched CRDT merge.
+//
+// merge_small_kernel: one wavefront per document ("small" envelope: <= 64
+// changes, <= 8 actors, <= 64*OPL ops, registers/objects bounded by the
+// launch's LDS carve).  Everything a document needs lives in registers and
+// LDS; each input row is read from HBM once (coalesced) and each output row
+// written once, so the kernel is HBM-bound.  No MFMA:
+// nothing here is a dense contraction.
+//
+// Stages inside the wave (reference semantics in brackets; restated in
+// SURVEY.md Appendix A from Automerge 0.12.2-beta.0 backend/op_set.js, which
+// is not vendored — yarn.lock:178-185):
+//
+//  K1  causal readiness + history order      [addChange / applyQueuedOps / causallyReady]
+//      fast path: every change is ready on arrival (first-arrival table in
+//      LDS + one ballot) => history = arrival order minus duplicates;
+//      slow path: exact emulation of the queue passes with wave-uniform
+//      control (per-lane SWAR readiness, ballot, find-first after the cursor).
+//  K1b transitive deps                       [transitiveDeps -> allDeps]
+//      64-bit ancestor sets over history positions, built by a push in
+//      history order (v_readlane of the finished lane, OR into dependents);
+//      allDeps[c][a] = popcount(anc(c) & chain(a)) for a cold merge.
+//  K1c clocks                                [opSet.clock, opSet.deps; DocBackend.updateClock
+//                                             src/DocBackend.ts:135-142; Clock.cmp src/Clock.ts:27-38]
+//  K2  map registers                         [applyAssign / updateMapKey]
+//      survivors of (obj,key) = set/link ops whose change is not an ancestor
+//      of any set/del/link on the register (LDS 64-bit OR per register);
+//      order = actor rank descending; equal-actor ties (one change) follow the
+//      flip of sortBy(actor).reverse() after every assign; counter `inc`s add
+//      to the counter sets that are their ancestors (LDS int64 atomics).
+//
+// Errors are per document: the earliest (history position, op) error wins —
+// the throw that would abort that document's Backend.applyChanges.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/hypermerge_amd.h"
+#include "merge_kernels.h"
+
+#define WAVE 64
+#define NA_MAX 8
+#define NDEP_MAX 512
+typedef unsigned long long u64;
+#if defined(__HIP_DEVICE_COMPILE__)
+#define LDS __attribute__((address_space(3)))   // explicit LDS pointers -> ds_* (not flat_*) instructions
+#else
+#define LDS
+#endif
+
+namespace hm {
+
+__device__ __forceinline__ u64 readlane64(u64 v, int l) {
+    const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((u64)hi << 32) | lo;
+}
+__device__ __forceinline__ uint32_t shfl32(uint32_t v, int src) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
+}
+__device__ __forceinline__ u64 shfl64(u64 v, int src) {
+    return ((u64)shfl32((uint32_t)(v >> 32), src) << 32) | shfl32((uint32_t)v, src);
+}
+__device__ __forceinline__ u64 wave_or64(u64 v) {
+    for (int o = 1; o < WAVE; o <<= 1) v |= shfl64(v, (int)(threadIdx.x ^ o));
+    return v;
+}
+// exclusive prefix sum across the wave; *total = sum over all lanes
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t *total) {
+    const uint32_t lane = threadIdx.x;
+    uint32_t x = v;
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const uint32_t y = shfl32(x, (int)(lane >= (uint32_t)o ? lane - o : lane));
+        if (lane >= (uint32_t)o) x += y;
+    }
+    *total = (uint32_t)__builtin_amdgcn_readlane((int)x, WAVE - 1);
+    return x - v;
+}
+__device__ __forceinline__ void wave_sync() { __syncthreads(); }   // 1-wave workgroup: cheap
+
+// error key: (history position, op index + 1, arrival index, code); the first throw is the min
+__device__ __forceinline__ u64 err_key(uint32_t h, uint32_t op_plus1, uint32_t arr, uint32_t code) {
+    return ((u64)h << 40) | ((u64)(op_plus1 & 0xFFFF) << 24) | ((u64)(arr & 0xFFFF) << 8) | code;
+}
+
+struct SmallLds {
+    LDS u64 *anc, *chain, *segor, *survabs, *errkey, *opval;
+    LDS int64_t *survsum;
+    LDS uint32_t *first, *base, *bclock, *headv, *objslot, *segcnt, *survcnt, *regoff, *regobj, *insmin;
+    LDS uint32_t *flags, *deps, *opmeta, *segoff, *segfill, *seglist, *survp;
+    LDS int32_t *hist_of;
+    LDS uint16_t *survtmp, *survop, *opbase, *opreg;
+    LDS uint8_t *h2a, *chactor, *opchg, *objtype;
+};
+
+// LDS carve, identical for the host size query and the device pointers.
+template <typename L_t, typename P>
+__host__ __device__ inline size_t small_carve(P base, uint32_t NOp, uint32_t NR, uint32_t NO, L_t *L) {
+    size_t o = 0;
+#define TAKE(f, T, cnt) do { L->f = (decltype(L->f))(base + o); o = (o + (size_t)(cnt) * sizeof(T) + 15) & ~(size_t)15; } while (0)
+    TAKE(anc, u64, 64);          TAKE(chain, u64, NA_MAX);     TAKE(segor, u64, NR);
+    TAKE(survabs, u64, NOp);     TAKE(errkey, u64, 1);         TAKE(opval, u64, NOp);
+    TAKE(survsum, int64_t, NOp);
+    TAKE(first, uint32_t, NA_MAX * 64); TAKE(base, uint32_t, NA_MAX * 3);
+    TAKE(objslot, uint32_t, NO); TAKE(segcnt, uint32_t, NR);   TAKE(survcnt, uint32_t, NR);
+    TAKE(regoff, uint32_t, NR);  TAKE(regobj, uint32_t, NR);   TAKE(insmin, uint32_t, NR);
+    TAKE(flags, uint32_t, 1);    TAKE(deps, uint32_t, NDEP_MAX); TAKE(opmeta, uint32_t, NOp);
+    TAKE(segoff, uint32_t, NR);  TAKE(segfill, uint32_t, NR);  TAKE(seglist, uint32_t, NOp);
+    TAKE(survp, uint32_t, NOp);  TAKE(hist_of, int32_t, 64);
+    TAKE(survtmp, uint16_t, NOp); TAKE(survop, uint16_t, NOp); TAKE(opbase, uint16_t, 64);
+    TAKE(opreg, uint16_t, NOp);
+    TAKE(h2a, uint8_t, 64);      TAKE(chactor, uint8_t, 64);   TAKE(opchg, uint8_t, NOp);
+    TAKE(objtype, uint8_t, NO);
+#undef TAKE
+    L->bclock = L->base + NA_MAX;
+    L->headv = L->base + 2 * NA_MAX;
+    return o;
+}
+
+template <typename T> struct Id { typedef T type; };
+template <typename T> __device__ __forceinline__ T lds_or(LDS T *p, typename Id<T>::type v) { return __atomic_fetch_or(p, v, __ATOMIC_RELAXED); }
+template <typename T> __device__ __forceinline__ T lds_min(LDS T *p, typename Id<T>::type v) { return __atomic_fetch_min(p, v, __ATOMIC_RELAXED); }
+template <typename T> __device__ __forceinline__ T lds_max(LDS T *p, typename Id<T>::type v) { return __atomic_fetch_max(p, v, __ATOMIC_RELAXED); }
+template <typename T> __device__ __forceinline__ T lds_add(LDS T *p, typename Id<T>::type v) { return __atomic_fetch_add(p, v, __ATOMIC_RELAXED); }
+
+enum : uint32_t { FL_UNSUPPORTED = 1u };
+enum Outcome { OUT_OK = 0, OUT_ERROR = 1, OUT_UNSUPPORTED = 2 };
+
+__device__ __forceinline__ void need_set(uint32_t &lo, uint32_t &hi, uint32_t a, uint32_t v) {
+    const uint32_t sh = (a & 3) * 8;
+    if (a < 4) { const uint32_t cur = (lo >> sh) & 0xFF; if (v > cur) lo = (lo & ~(0xFFu << sh)) | (v << sh); }
+    else       { const uint32_t cur = (hi >> sh) & 0xFF; if (v > cur) hi = (hi & ~(0xFFu << sh)) | (v << sh); }
+}
+
+// opmeta layout: action | datatype << 8 | vtag << 16 | applied << 24
+__device__ __forceinline__ uint32_t meta_action(uint32_t m) { return m & 0xFF; }
+__device__ __forceinline__ uint32_t meta_dtype(uint32_t m) { return (m >> 8) & 0xFF; }
+__device__ __forceinline__ uint32_t meta_vtag(uint32_t m) { return (m >> 16) & 0xFF; }
+
+// tie order key of an assign at position p on its register: odd p first (p descending),
+// then even p ascending ("append, then reverse" after every assign)
+__device__ __forceinline__ uint32_t tie_order(uint32_t pc) { return (pc & 1) ? (0x10000u - pc) : (0x20000u + pc); }
+
+// Merge one document with the whole wave.  Every return is wave-uniform.
+template <int OPL>
+__device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const SmallLds &L, uint32_t d,
+                                                   const hm_doc_row &doc) {
+    constexpr uint32_t NOp = WAVE * OPL;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t S = p.a_stride;
+    const uint32_t n = doc.n_changes, A = doc.n_actors, m = doc.n_ops, R = doc.n_regs, O = doc.n_objs;
+    hm_doc_result *dres = p.res_docs + d;
+
+    // ---------------- K1: load changes (lane = arrival index) ----------------
+    const bool act = lane < n;
+    hm_change_row c = {};
+    if (act) c = p.changes[doc.change_off + lane];
+    for (uint32_t i = lane; i < NA_MAX * 64; i += WAVE) L.first[i] = 0xFFFFFFFFu;
+    if (lane < NA_MAX) { L.base[lane] = 0xFFFFFFFFu; L.bclock[lane] = 0; L.headv[lane] = 0; L.chain[lane] = 0; }
+    if (lane == 0) { *L.errkey = ~0ull; *L.flags = 0; }
+    // the document's deps are one contiguous range: stage it in LDS with coalesced loads
+    const uint32_t dep_lo = n ? (uint32_t)__builtin_amdgcn_readlane((int)c.dep_off, 0) : 0;
+    const uint32_t dep_hi = n ? (uint32_t)__builtin_amdgcn_readlane((int)(c.dep_off + c.n_deps), (int)(n - 1)) : 0;
+    const uint32_t ndep = dep_hi - dep_lo;
+    if (n && (dep_hi < dep_lo || ndep > NDEP_MAX)) return OUT_UNSUPPORTED;
+    for (uint32_t i = lane; i < ndep; i += WAVE) {
+        const hm_dep_row dp = p.deps[dep_lo + i];
+        L.deps[i] = (dp.seq < (1u << 24) && dp.actor < 256) ? (((uint32_t)dp.actor << 24) | dp.seq) : 0xFFFFFFFFu;
+    }
+    wave_sync();
+    const uint32_t actor = c.actor, seq = c.seq;
+    const uint32_t my_dep0 = c.dep_off - dep_lo;
+    if (act) {
+        if (actor >= A || seq == 0 || c.dep_off < dep_lo || my_dep0 + c.n_deps > ndep) lds_or(L.flags, FL_UNSUPPORTED);
+        else { lds_min(&L.base[actor], seq); lds_max(&L.bclock[actor], seq); }
+        L.chactor[lane] = (uint8_t)actor;
+        L.opbase[lane] = (uint16_t)(c.op_first - doc.op_off);
+        if (c.op_first < doc.op_off || c.op_first - doc.op_off + c.n_ops > m) lds_or(L.flags, FL_UNSUPPORTED);
+    }
+    wave_sync();
+    if (*L.flags & FL_UNSUPPORTED) return OUT_UNSUPPORTED;
+    const uint32_t mybase = act ? L.base[actor] : 0;
+    const uint32_t slot = seq - mybase;
+    if (act) {
+        if (slot >= 64) lds_or(L.flags, FL_UNSUPPORTED);
+        else lds_min(&L.first[actor * 64 + slot], lane);
+        const uint32_t o0 = c.op_first - doc.op_off;       // ops -> arrival index of their change
+        for (uint32_t j = 0; j < c.n_ops; j++) L.opchg[o0 + j] = (uint8_t)lane;
+    }
+    wave_sync();
+    if (*L.flags & FL_UNSUPPORTED) return OUT_UNSUPPORTED;
+
+    const uint32_t first_me = act ? L.first[actor * 64 + slot] : lane;
+    const bool dup = act && first_me != lane;
+    const uint32_t cid_first = shfl32(c.content_id, (int)(first_me & 63));
+    // per-actor clock requirement relative to the batch's first seq of that actor,
+    // packed as bytes (0x7F = never satisfiable in this batch)
+    uint32_t need_lo = 0, need_hi = 0;
+    u64 dmask = 0;                       // direct deps in arrival-index space (fast path)
+    uint32_t pred_arr = 0xFFu;
+    bool ok = true;                      // ready on arrival
+    if (act) {
+        for (uint32_t j = 0; j < c.n_deps; j++) {
+            const uint32_t pk = L.deps[my_dep0 + j];
+            const uint32_t a = pk >> 24, s = pk & 0xFFFFFF;
+            if (pk == 0xFFFFFFFFu || a >= A) { lds_or(L.flags, FL_UNSUPPORTED); continue; }
+            if (a == actor || s == 0) continue;                // deps.set(actor, seq-1) overrides
+            const uint32_t b = L.base[a];
+            if (b == 0xFFFFFFFFu || s < b || s - b >= 64) { need_set(need_lo, need_hi, a, 0x7F); ok = false; continue; }
+            need_set(need_lo, need_hi, a, s - b + 1);
+            const uint32_t f = L.first[a * 64 + (s - b)];
+            if (f >= lane) ok = false; else dmask |= 1ull << f;
+        }
+        const uint32_t ps = seq - 1;
+        if (ps != 0) {
+            if (ps < mybase) { need_set(need_lo, need_hi, actor, 0x7F); ok = false; }
+            else {
+                need_set(need_lo, need_hi, actor, ps - mybase + 1);
+                const uint32_t f = L.first[actor * 64 + (ps - mybase)];
+                if (f >= lane) ok = false; else { dmask |= 1ull << f; pred_arr = f; }
+            }
+        }
+        if (dup && cid_first != c.content_id) ok = false;      // mismatched duplicate: exact path
+    }
+    wave_sync();
+    if (*L.flags & FL_UNSUPPORTED) return OUT_UNSUPPORTED;
+
+    int32_t hist = -1;
+    uint32_t H = 0;
+    if (__ballot(act && !ok) == 0) {
+        // every change was ready on arrival: history = arrival order minus duplicates
+        const u64 appl = __ballot(act && !dup);
+        if (act) hist = dup ? -2 : (int32_t)__popcll(appl & ((1ull << lane) - 1));
+        H = (uint32_t)__popcll(appl);
+    } else {
+        // ---- exact emulation of addChange / applyQueuedOps (wave-uniform control) ----
+        for (uint32_t i = lane; i < NA_MAX * 64; i += WAVE) L.first[i] = 0xFFFFFFFFu;   // -> applied lane
+        wave_sync();
+        uint32_t crel_lo = 0, crel_hi = 0;      // relative applied clock per actor (bytes)
+        u64 queued = 0;
+        bool stop = false;
+        for (uint32_t i = 0; i < n && !stop; i++) {
+            queued |= 1ull << i;
+            u64 above = 0;
+            bool first_pass = true;             // pass 1 can only apply the new change
+            for (;;) {                          // passes
+                bool progress = false;
+                for (;;) {                      // one pass: first ready change after the cursor
+                    const uint32_t x0 = ((crel_lo | 0x80808080u) - need_lo) & 0x80808080u;
+                    const uint32_t x1 = ((crel_hi | 0x80808080u) - need_hi) & 0x80808080u;
+                    u64 r = __ballot(act && x0 == 0x80808080u && x1 == 0x80808080u) & queued;
+                    r &= first_pass ? (1ull << i) : above;
+                    if (!r) break;
+                    const uint32_t j = (uint32_t)__builtin_ctzll(r);
+                    const uint32_t aj = (uint32_t)__builtin_amdgcn_readlane((int)actor, (int)j);
+                    const uint32_t sj = (uint32_t)__builtin_amdgcn_readlane((int)slot, (int)j);
+                    const uint32_t sh = (aj & 3) * 8;
+                    const uint32_t cur = (((aj < 4) ? crel_lo : crel_hi) >> sh) & 0xFF;
+                    queued &= ~(1ull << j);
+                    progress = true;
+                    above = (j >= 63) ? 0 : (~0ull << (j + 1));
+                    if (sj + 1 <= cur) {                         // seq <= clock: already applied
+                        const uint32_t k = L.first[aj * 64 + sj];
+                        const uint32_t ck = (uint32_t)__builtin_amdgcn_readlane((int)c.content_id, (int)k);
+                        const uint32_t cj = (uint32_t)__builtin_amdgcn_readlane((int)c.content_id, (int)j);
+                        if (lane == j) hist = -2;
+                        if (ck != cj) {                          // 'Inconsistent reuse of sequence number'
+                            if (lane == 0) lds_min(L.errkey, err_key(H, 0, j, HM_ERR_INCONSISTENT_SEQ));
+                            stop = true;
+                            break;
+                        }
+                        if (first_pass) break;
+                        continue;
+                    }
+                    if (aj < 4) crel_lo = (crel_lo & ~(0xFFu << sh)) | ((sj + 1) << sh);
+                    else        crel_hi = (crel_hi & ~(0xFFu << sh)) | ((sj + 1) << sh);
+                    if (lane == 0) L.first[aj * 64 + sj] = j;
+                    if (lane == j) hist = (int32_t)H;
+                    H++;
+                    if (first_pass) break;
+                }
+                if (stop || !progress) break;
+                first_pass = false;
+                above = ~0ull;
+            }
+        }
+        wave_sync();
+        // direct deps over the *applied* lanes
+        dmask = 0; pred_arr = 0xFFu;
+        if (act && hist >= 0) {
+            for (uint32_t j = 0; j < c.n_deps; j++) {
+                const uint32_t pk = L.deps[my_dep0 + j];
+                const uint32_t a = pk >> 24, s = pk & 0xFFFFFF;
+                if (a == actor || s == 0) continue;
+                dmask |= 1ull << L.first[a * 64 + (s - L.base[a])];
+            }
+            if (seq - 1 != 0) { pred_arr = L.first[actor * 64 + (seq - 1 - mybase)]; dmask |= 1ull << pred_arr; }
+        }
+    }
+
+    // ---------------- K1b: ancestor sets in history order ----------------
+    if (act) L.hist_of[lane] = hist;
+    if (act && hist >= 0) L.h2a[hist] = (uint8_t)lane;
+    wave_sync();
+    const bool hv = lane < H;
+    const uint32_t ai = hv ? L.h2a[lane] : 0;            // arrival index at history position `lane`
+    const u64 dm_arr = shfl64(dmask, (int)ai);
+    const uint32_t hactor = shfl32(actor, (int)ai);
+    const uint32_t hseq = shfl32(seq, (int)ai);
+    const uint32_t hpred = shfl32(pred_arr, (int)ai);
+    u64 D = 0, Dnp = 0;                                   // direct deps; without the own predecessor
+    if (hv) {
+        u64 x = dm_arr;
+        while (x) {
+            const uint32_t j = (uint32_t)__builtin_ctzll(x);
+            x &= x - 1;
+            const u64 bit = 1ull << (uint32_t)L.hist_of[j];
+            D |= bit;
+            if (j != hpred) Dnp |= bit;
+        }
+    }
+    u64 anc = 0;
+    for (uint32_t k = 0; k < H; k++) {                    // lane k is final when the push reaches it
+        const u64 ak = readlane64(anc, (int)k) | (1ull << k);
+        if ((D >> k) & 1) anc |= ak;
+    }
+    if (hv) L.anc[lane] = anc;
+    for (uint32_t a = 0; a < A; a++) {
+        const u64 ch = __ballot(hv && hactor == a);
+        if (lane == 0) L.chain[a] = ch;
+    }
+    wave_sync();
+    // transitiveDeps folds the deps map in key order with `.set(actor, seq)`: that equals
+    // the closure unless one listed dep is an ancestor of another (never for heads deps).
+    if (hv && Dnp) {
+        bool bad = false;
+        u64 x = Dnp;
+        while (x) {
+            const uint32_t j = (uint32_t)__builtin_ctzll(x);
+            x &= x - 1;
+            u64 y = D & ~(1ull << j);
+            while (y) {
+                const uint32_t i2 = (uint32_t)__builtin_ctzll(y);
+                y &= y - 1;
+                if ((L.anc[i2] >> j) & 1) bad = true;
+            }
+        }
+        if (bad) lds_or(L.flags, FL_UNSUPPORTED);
+    }
+    const u64 covered = wave_or64(hv ? anc : 0);
+    if (hv && !((covered >> lane) & 1)) L.headv[hactor] = hseq;     // opSet.deps
+    for (uint32_t i = lane; i < O; i += WAVE) { L.objslot[i] = i == 0 ? 0u : 0xFFFFFFFFu; L.objtype[i] = i == 0 ? HM_MAKE_MAP : 0xFF; }
+    for (uint32_t i = lane; i < R; i += WAVE) {
+        L.segor[i] = 0; L.segcnt[i] = 0; L.survcnt[i] = 0; L.insmin[i] = 0xFFFFFFFFu; L.regobj[i] = HM_NONE;
+    }
+    wave_sync();
+
+    // ---------------- K2: ops (lane + 64*t) ----------------
+    uint32_t oreg[OPL], oobj[OPL], opar[OPL], oact[OPL], okey[OPL], oarr[OPL];
+    int32_t oh[OPL];
+#pragma unroll
+    for (int t = 0; t < OPL; t++) {
+        const uint32_t k = lane + WAVE * t;
+        oh[t] = -1; okey[t] = 0; oarr[t] = 0; oreg[t] = 0; oobj[t] = 0; opar[t] = 0; oact[t] = 0xFF;
+        if (k < m) {
+            const hm_op_row o = p.ops[doc.op_off + k];
+            const uint32_t ch = L.opchg[k];
+            oarr[t] = ch; oh[t] = L.hist_of[ch];
+            oreg[t] = o.reg; oobj[t] = o.obj; opar[t] = o.parent; oact[t] = o.action;
+            okey[t] = ((uint32_t)(oh[t] < 0 ? 0 : oh[t]) << 16) | (k - L.opbase[ch]);
+            L.opmeta[k] = (uint32_t)o.action | ((uint32_t)o.datatype << 8) | ((uint32_t)o.vtag << 16) |
+                          ((oh[t] >= 0 ? 1u : 0u) << 24);
+            L.opval[k] = o.value;
+            L.opreg[k] = (uint16_t)(o.reg < 0xFFFFu ? o.reg : 0xFFFFu);
+            if (oh[t] >= 0) {
+                const uint32_t a = o.action;
+                if (a <= HM_MAKE_TEXT) {
+                    if (o.obj >= O) lds_or(L.flags, FL_UNSUPPORTED);
+                    else lds_min(&L.objslot[o.obj], okey[t] + 1);
+                } else if (a <= HM_INC) {
+                    if (o.reg >= R || (a == HM_INS && o.parent != HM_HEAD && o.parent >= R))
+                        lds_or(L.flags, FL_UNSUPPORTED);
+                    else if (o.obj < O) {
+                        L.regobj[o.reg] = o.obj;
+                        if (a == HM_INS) lds_min(&L.insmin[o.reg], okey[t] + 1);
+                        else {
+                            lds_add(&L.segcnt[o.reg], 1u);
+                            if (a != HM_INC) lds_or(&L.segor[o.reg], L.anc[oh[t]]);
+                        }
+                    }
+                } else lds_or(L.flags, FL_UNSUPPORTED);
+            }
+        }
+    }
+    wave_sync();
+    // objects: the earliest make op creates, later ones throw 'Duplicate creation of object'
+#pragma unroll
+    for (int t = 0; t < OPL; t++)
+        if (oh[t] >= 0 && oact[t] <= HM_MAKE_TEXT && oobj[t] < O) {
+            if (L.objslot[oobj[t]] != okey[t] + 1)
+                lds_min(L.errkey, err_key((uint32_t)oh[t], (okey[t] & 0xFFFF) + 1, oarr[t], HM_ERR_DUPLICATE_OBJECT));
+            else L.objtype[oobj[t]] = (uint8_t)oact[t];
+        }
+    wave_sync();
+    uint32_t sslot[OPL];
+    bool surv[OPL];
+    bool has_list = false;
+#pragma unroll
+    for (int t = 0; t < OPL; t++) {
+        surv[t] = false; sslot[t] = 0;
+        if (oh[t] < 0 || oact[t] < HM_INS || oact[t] > HM_INC || oreg[t] >= R) continue;
+        const uint32_t os = oobj[t] < O ? L.objslot[oobj[t]] : 0xFFFFFFFFu;
+        if (os == 0xFFFFFFFFu || os > okey[t]) {       // 'Modification of unknown object'
+            lds_min(L.errkey, err_key((uint32_t)oh[t], (okey[t] & 0xFFFF) + 1, oarr[t], HM_ERR_UNKNOWN_OBJECT));
+            continue;
+        }
+        const uint32_t ot = L.objtype[oobj[t]];
+        const bool is_list = ot == HM_MAKE_LIST || ot == HM_MAKE_TEXT;
+        if (oact[t] == HM_INS) {
+            has_list = true;
+            if (L.insmin[oreg[t]] != okey[t] + 1)     // 'Duplicate list element ID'
+                lds_min(L.errkey, err_key((uint32_t)oh[t], (okey[t] & 0xFFFF) + 1, oarr[t], HM_ERR_DUPLICATE_ELEM));
+            if (opar[t] != HM_HEAD && !(L.insmin[opar[t]] <= okey[t]))
+                lds_or(L.flags, FL_UNSUPPORTED);
+            continue;
+        }
+        has_list |= is_list;
+        if (oact[t] == HM_SET || oact[t] == HM_LINK) {
+            if (is_list && !(L.insmin[oreg[t]] <= okey[t]))   // 'Missing index entry for list element'
+                lds_min(L.errkey, err_key((uint32_t)oh[t], (okey[t] & 0xFFFF) + 1, oarr[t], HM_ERR_MISSING_ELEM));
+            if (!((L.segor[oreg[t]] >> oh[t]) & 1)) {
+                surv[t] = true;
+                sslot[t] = lds_add(&L.survcnt[oreg[t]], 1u);
+            }
+        }
+    }
+    if (__ballot(has_list)) lds_or(L.flags, FL_UNSUPPORTED);   // RGA order: not in this kernel yet
+    wave_sync();
+    if (*L.errkey != ~0ull) return OUT_ERROR;                    // the first throw wins
+    if (*L.flags & FL_UNSUPPORTED) return OUT_UNSUPPORTED;
+
+    // survivor offsets: exclusive scan over register ids
+    uint32_t total = 0;
+    for (uint32_t r0 = 0; r0 < R; r0 += WAVE) {
+        const uint32_t r = r0 + lane;
+        uint32_t tot;
+        const uint32_t ex = wave_excl_scan(r < R ? L.survcnt[r] : 0u, &tot);
+        if (r < R) L.regoff[r] = total + ex;
+        total += tot;
+    }
+    wave_sync();
+#pragma unroll
+    for (int t = 0; t < OPL; t++)
+        if (surv[t]) { sslot[t] += L.regoff[oreg[t]]; L.survtmp[sslot[t]] = (uint16_t)(lane + WAVE * t); }
+    wave_sync();
+    // rank: actor rank descending ...
+    uint32_t rank[OPL];
+    bool tie[OPL];
+#pragma unroll
+    for (int t = 0; t < OPL; t++) {
+        rank[t] = 0; tie[t] = false;
+        if (!surv[t]) continue;
+        const uint32_t k = lane + WAVE * t, reg = oreg[t];
+        const uint32_t my_a = L.chactor[oarr[t]];
+        const uint32_t b0 = L.regoff[reg], cnt = L.survcnt[reg];
+        for (uint32_t q = 0; q < cnt; q++) {
+            const uint32_t k2 = L.survtmp[b0 + q];
+            if (k2 == k) continue;
+            const uint32_t a2 = L.chactor[L.opchg[k2]];
+            if (a2 > my_a) rank[t]++;
+            else if (a2 == my_a) tie[t] = true;
+        }
+    }
+    bool anytie = false;
+#pragma unroll
+    for (int t = 0; t < OPL; t++) anytie |= tie[t];
+    if (__ballot(anytie)) {
+        // ... equal actors (ops of one change): p = assigns applied on the register before
+        // the op; per-register assign lists (CSR) give p in O(register length)
+        uint32_t tot2 = 0;
+        for (uint32_t r0 = 0; r0 < R; r0 += WAVE) {
+            const uint32_t r = r0 + lane;
+            uint32_t tt;
+            const uint32_t ex = wave_excl_scan(r < R ? L.segcnt[r] : 0u, &tt);
+            if (r < R) { L.segoff[r] = tot2 + ex; L.segfill[r] = 0; }
+            tot2 += tt;
+        }
+        wave_sync();
+#pragma unroll
+        for (int t = 0; t < OPL; t++)
+            if (oh[t] >= 0 && oact[t] >= HM_SET && oact[t] <= HM_INC && oreg[t] < R)
+                L.seglist[L.segoff[oreg[t]] + lds_add(&L.segfill[oreg[t]], 1u)] = okey[t];
+        wave_sync();
+#pragma unroll
+        for (int t = 0; t < OPL; t++) {
+            if (!tie[t]) continue;
+            const uint32_t s0 = L.segoff[oreg[t]], sc = L.segcnt[oreg[t]];
+            uint32_t pc = 0;
+            for (uint32_t q = 0; q < sc; q++) pc += L.seglist[s0 + q] < okey[t] ? 1u : 0u;
+            L.survp[sslot[t]] = tie_order(pc);
+        }
+        wave_sync();
+#pragma unroll
+        for (int t = 0; t < OPL; t++) {
+            if (!tie[t]) continue;
+            const uint32_t k = lane + WAVE * t, reg = oreg[t];
+            const uint32_t my_a = L.chactor[oarr[t]], my_t = L.survp[sslot[t]];
+            const bool odd_n = L.segcnt[reg] & 1;      // the group is reversed after an odd count
+            const uint32_t b0 = L.regoff[reg], cnt = L.survcnt[reg];
+            for (uint32_t q = 0; q < cnt; q++) {
+                const uint32_t k2 = L.survtmp[b0 + q];
+                if (k2 == k || L.chactor[L.opchg[k2]] != my_a) continue;
+                const uint32_t t2 = L.survp[b0 + q];
+                if (odd_n ? (t2 > my_t) : (t2 < my_t)) rank[t]++;
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < OPL; t++) {
+        if (!surv[t]) continue;
+        const uint32_t pos = L.regoff[oreg[t]] + rank[t];
+        L.survop[pos] = (uint16_t)(lane + WAVE * t);
+        L.survsum[pos] = 0;
+        L.survabs[pos] = 0;
+    }
+    wave_sync();
+    // counters: an inc adds to every surviving counter set that is its ancestor
+    bool float_counter = false;
+#pragma unroll
+    for (int t = 0; t < OPL; t++) {
+        if (oh[t] < 0 || oact[t] != HM_INC) continue;
+        const uint32_t k = lane + WAVE * t;
+        const uint32_t reg = oreg[t], b0 = L.regoff[reg], cnt = L.survcnt[reg];
+        const u64 an = L.anc[oh[t]];
+        const uint32_t my_vtag = meta_vtag(L.opmeta[k]);
+        const int64_t v = (int64_t)L.opval[k];
+        for (uint32_t q = 0; q < cnt; q++) {
+            const uint32_t k2 = L.survop[b0 + q];
+            const uint32_t m2 = L.opmeta[k2];
+            const uint32_t vt2 = meta_vtag(m2);
+            if (meta_action(m2) != HM_SET || meta_dtype(m2) != HM_DT_COUNTER || (vt2 != HM_V_INT && vt2 != HM_V_FLOAT)) continue;
+            if (!((an >> L.hist_of[L.opchg[k2]]) & 1)) continue;
+            if (vt2 != HM_V_INT || my_vtag != HM_V_INT) { float_counter = true; continue; }
+            lds_add((LDS u64 *)&L.survsum[b0 + q], (unsigned long long)v);
+            lds_add((LDS u64 *)&L.survabs[b0 + q], (unsigned long long)(v < 0 ? -v : v));
+        }
+    }
+    if (__ballot(float_counter)) lds_or(L.flags, FL_UNSUPPORTED);   // f64 counters need the ordered sum
+    wave_sync();
+    if (*L.flags & FL_UNSUPPORTED) return OUT_UNSUPPORTED;
+
+    // ---------------- outputs ----------------
+    bool inexact = false;
+    for (uint32_t q = lane; q < total; q += WAVE) {
+        const uint32_t k = L.survop[q], mt = L.opmeta[k];
+        hm_surv_result sr;
+        sr.op = k; sr.vtag = meta_vtag(mt); sr.value = L.opval[k];
+        if (meta_action(mt) == HM_SET && meta_dtype(mt) == HM_DT_COUNTER && sr.vtag == HM_V_INT) {
+            const int64_t b = (int64_t)sr.value;
+            inexact |= L.survabs[q] + (u64)(b < 0 ? -b : b) > (1ull << 53);   // JS number exactness
+            sr.value = (u64)(b + L.survsum[q]);
+        }
+        p.res_surv[doc.op_off + q] = sr;
+    }
+    if (__ballot(inexact)) return OUT_UNSUPPORTED;
+    for (uint32_t r = lane; r < R; r += WAVE) {
+        hm_reg_result rr;
+        rr.n_surv = L.survcnt[r]; rr.surv_off = L.regoff[r]; rr.list_index = -1; rr.obj = L.regobj[r];
+        p.res_regs[doc.reg_off + r] = rr;
+    }
+    // allDeps rows, coalesced: word w = (change w/S, actor w%S)
+    for (uint32_t w = lane; w < n * S; w += WAVE) {
+        const uint32_t ci = w / S, a = w - ci * S;
+        const int32_t h = L.hist_of[ci];
+        uint32_t v = 0;
+        if (h >= 0 && a < A) v = (uint32_t)__popcll(L.anc[h] & L.chain[a]);
+        p.res_all_deps[(size_t)doc.change_off * S + w] = v;
+    }
+    uint32_t bc = 0, mc = 0;
+    if (lane < S) {
+        const bool ar = lane < A;
+        p.res_clock[(size_t)d * S + lane] = ar ? (uint32_t)__popcll(L.chain[lane]) : 0u;
+        p.res_heads[(size_t)d * S + lane] = ar ? L.headv[lane] : 0u;
+        bc = ar ? L.bclock[lane] : 0u;
+        p.res_back_clock[(size_t)d * S + lane] = bc;              // DocBackend.clock (queued included)
+        if (p.min_clock) mc = p.min_clock[(size_t)d * S + lane];
+    }
+    const bool aGTE = __ballot(lane < S && bc < mc) == 0;
+    const bool bGTE = __ballot(lane < S && mc < bc) == 0;
+    const u64 q = __ballot(act && hist == -1);
+    if (act) p.res_hist[doc.change_off + lane] = hist;
+    if (lane == 0) {
+        hm_doc_result r = {};
+        r.status = HM_OK; r.err_change = HM_NONE; r.err_op = HM_NONE;
+        r.hist_len = H; r.n_queued = (uint32_t)__popcll(q); r.n_surv = total;
+        r.min_cmp = p.min_clock ? ((aGTE && bGTE) ? 0u : (aGTE ? 1u : (bGTE ? 2u : 3u))) : 0u;
+        *dres = r;
+    }
+    return OUT_OK;
+}
+
+template <int OPL>
+__global__ __launch_bounds__(WAVE) void merge_small_kernel(SmallParams p) {
+    extern __shared__ __align__(16) uint8_t lds_raw[];
+    SmallLds L;
+    small_carve((LDS uint8_t *)lds_raw, WAVE * OPL, p.cap_regs, p.cap_objs, &L);
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t d = blockIdx.x; d < p.n_docs; d += gridDim.x) {
+        const hm_doc_row doc = p.docs[d];
+        const bool in_env = doc.n_changes <= 64 && doc.n_actors <= NA_MAX && doc.n_ops <= WAVE * OPL &&
+                            doc.n_regs <= p.cap_regs && doc.n_objs <= p.cap_objs && doc.n_objs >= 1;
+        const Outcome oc = in_env ? merge_doc_small<OPL>(p, L, d, doc) : OUT_UNSUPPORTED;
+        hm_doc_result *dres = p.res_docs + d;
+        if (oc == OUT_ERROR) {
+            // an Automerge throw aborted this document's Backend.applyChanges
+            const u64 ek = *L.errkey;
+            if (lane == 0) {
+                hm_doc_result r = {};
+                r.status = (int32_t)(ek & 0xFF);
+                r.err_change = (uint32_t)((ek >> 8) & 0xFFFF);
+                const uint32_t opp1 = (uint32_t)((ek >> 24) & 0xFFFF);
+                r.err_op = opp1 ? opp1 - 1 : HM_NONE;
+                *dres = r;
+            }
+        } else if (oc == OUT_UNSUPPORTED) {
+            if (lane == 0) {
+                hm_doc_result r = {};
+                r.status = HM_ERR_UNSUPPORTED; r.err_change = HM_NONE; r.err_op = HM_NONE;
+                *dres = r;
+            }
+        }
+        wave_sync();
+    }
+}
+
+// ---------------- Clock algebra over dense rows (src/Clock.ts) ----------------
+// cmp: 64/S rows per wave, one lane per entry, two ballots (gte(a,b), gte(b,a))
+__global__ void clock_cmp_kernel(const uint32_t *a, const uint32_t *b, uint8_t *out, uint32_t n_docs, uint32_t S) {
+    const uint32_t lane = threadIdx.x & 63, wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t rows_per_wave = WAVE / S;
+    const uint32_t row = wave * rows_per_wave + lane / S, col = lane % S;
+    const bool v = row < n_docs && lane < rows_per_wave * S;
+    const uint32_t x = v ? a[(size_t)row * S + col] : 0, y = v ? b[(size_t)row * S + col] : 0;
+    const u64 lt = __ballot(v && x < y), gt = __ballot(v && y < x);
+    if (v && col == 0) {
+        const u64 mask = (S >= 64 ? ~0ull : ((1ull << S) - 1)) << lane;
+        const bool aGTE = (lt & mask) == 0, bGTE = (gt & mask) == 0;
+        out[row] = (aGTE && bGTE) ? 0 : (aGTE ? 1 : (bGTE ? 2 : 3));
+    }
+}
+__global__ void clock_union_kernel(const uint32_t *a, const uint32_t *b, uint32_t *c, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        c[i] = a[i] > b[i] ? a[i] : b[i];
+}
+__global__ void clock_intersection_kernel(const uint32_t *a, const uint32_t *b, uint32_t *c, size_t n) {
+    // Math.min(c1||0, c2||0), kept only when > 0 (zero == absent in a dense row)
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        c[i] = a[i] < b[i] ? a[i] : b[i];
+}
+
+}  // namespace hm
+
+// ---------------- host-side launchers ----------------
+size_t hm_small_lds_bytes(uint32_t opl, uint32_t cap_regs, uint32_t cap_objs) {
+    hm::SmallLds L;
+    return hm::small_carve((uintptr_t)0, 64 * opl, cap_regs, cap_objs, &L);
+}
+
+hipError_t hm_launch_small(const SmallParams &p, uint32_t opl, uint32_t grid, hipStream_t s) {
+    const size_t lds = hm_small_lds_bytes(opl, p.cap_regs, p.cap_objs);
+    switch (opl) {
+    case 1: hipLaunchKernelGGL(hm::merge_small_kernel<1>, dim3(grid), dim3(WAVE), lds, s, p); break;
+    case 2: hipLaunchKernelGGL(hm::merge_small_kernel<2>, dim3(grid), dim3(WAVE), lds, s, p); break;
+    default: hipLaunchKernelGGL(hm::merge_small_kernel<4>, dim3(grid), dim3(WAVE), lds, s, p); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t hm_launch_clock(int which, const uint32_t *a, const uint32_t *b, void *out, uint32_t n_docs,
+                           uint32_t S, hipStream_t s) {
+    if (which == 0) {
+        if (S == 0 || S > 64) return hipErrorInvalidValue;
+        const uint32_t rows_per_wave = 64 / S;
+        const uint32_t waves = (n_docs + rows_per_wave - 1) / rows_per_wave;
+        const uint32_t blocks = (waves + 3) / 4;
+        hipLaunchKernelGGL(hm::clock_cmp_kernel, dim3(blocks ? blocks : 1), dim3(256), 0, s, a, b, (uint8_t *)out, n_docs, S);
+    } else {
+        const size_t n = (size_t)n_docs * S;
+        uint32_t blocks = (uint32_t)((n + 255) / 256);
+        if (blocks > 8192) blocks = 8192;
+        if (which == 1) hipLaunchKernelGGL(hm::clock_union_kernel, dim3(blocks ? blocks : 1), dim3(256), 0, s, a, b, (uint32_t *)out, n);
+        else hipLaunchKernelGGL(hm::clock_intersection_kernel, dim3(blocks ? blocks : 1), dim3(256), 0, s, a, b, (uint32_t *)out, n);
+    }
+    return hipGetLastError();
+}

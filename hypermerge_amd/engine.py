@@ -1,0 +1,111 @@
+"""ctypes binding of the C-ABI in include/hypermerge_amd.h (libhmgpu.so).
+
+This is the Python face of the boundary; the Node face is hypermerge_amd/js
+(N-API).  There is no CPU fallback: if the HIP library or a GPU is missing,
+``Engine()`` raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+from .columnar import Batch, Results, CBatch, CResults
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(_HERE, "_lib", "libhmgpu.so")
+
+# every symbol include/hypermerge_amd.h declares
+EXPORTS = ("hm_abi_version", "hm_status_message", "hm_engine_create", "hm_engine_destroy",
+           "hm_engine_last_error", "hm_merge_host", "hm_scratch_bytes", "hm_merge_device",
+           "hm_last_kernel_ms", "hm_clock_cmp_device", "hm_clock_union_device",
+           "hm_clock_intersection_device")
+
+_lib = None
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            raise EngineError(f"{LIB} is missing: run __graft_entry__.build() (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB)
+        L.hm_abi_version.restype = ctypes.c_uint32
+        L.hm_status_message.argtypes = [ctypes.c_int]
+        L.hm_status_message.restype = ctypes.c_char_p
+        L.hm_engine_create.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]
+        L.hm_engine_destroy.argtypes = [ctypes.c_void_p]
+        L.hm_engine_last_error.argtypes = [ctypes.c_void_p]
+        L.hm_engine_last_error.restype = ctypes.c_char_p
+        L.hm_merge_host.argtypes = [ctypes.c_void_p, ctypes.POINTER(CBatch), ctypes.POINTER(CResults)]
+        L.hm_merge_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(CBatch), ctypes.POINTER(CResults),
+                                      ctypes.c_void_p, ctypes.c_void_p]
+        L.hm_scratch_bytes.argtypes = [ctypes.POINTER(CBatch)]
+        L.hm_scratch_bytes.restype = ctypes.c_size_t
+        L.hm_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
+        for f in ("hm_clock_cmp_device", "hm_clock_union_device", "hm_clock_intersection_device"):
+            getattr(L, f).argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 3 + [ctypes.c_uint32] * 2 + [ctypes.c_void_p]
+        _lib = L
+    return _lib
+
+
+class _Config(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("flags", ctypes.c_int)]
+
+
+class Engine:
+    def __init__(self, device: int = 0):
+        L = lib()
+        h = ctypes.c_void_p()
+        cfg = _Config(device, 0)
+        st = L.hm_engine_create(ctypes.byref(cfg), ctypes.byref(h))
+        if st != 0:
+            raise EngineError(f"hm_engine_create failed: {L.hm_status_message(st).decode()}")
+        self._h = h
+        self._L = L
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.hm_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, st: int, what: str) -> None:
+        if st != 0:
+            msg = self._L.hm_engine_last_error(self._h).decode()
+            raise EngineError(f"{what}: {self._L.hm_status_message(st).decode()} ({msg})")
+
+    def merge(self, batch: Batch, results: Optional[Results] = None) -> Results:
+        """Host batch -> GPU merge -> host results (synchronous)."""
+        if results is None:
+            results = Results.alloc(batch)
+        cb, cr = batch.c_struct(), results.c_struct()
+        self._check(self._L.hm_merge_host(self._h, ctypes.byref(cb), ctypes.byref(cr)), "hm_merge_host")
+        return results
+
+    def merge_device(self, cbatch: CBatch, cresults: CResults, stream: int = 0) -> None:
+        """Device-resident merge: every pointer in the structs is a device pointer."""
+        self._check(self._L.hm_merge_device(self._h, ctypes.byref(cbatch), ctypes.byref(cresults), None,
+                                            ctypes.c_void_p(stream) if stream else None), "hm_merge_device")
+
+    def last_kernel_ms(self) -> Sequence[float]:
+        buf = (ctypes.c_float * 4)()
+        n = self._L.hm_last_kernel_ms(self._h, buf, 4)
+        return [float(buf[i]) for i in range(n)]
+
+    def clock_op(self, which: str, a_ptr: int, b_ptr: int, out_ptr: int, n_docs: int, a_stride: int,
+                 stream: int = 0) -> None:
+        f = {"cmp": self._L.hm_clock_cmp_device, "union": self._L.hm_clock_union_device,
+             "intersection": self._L.hm_clock_intersection_device}[which]
+        self._check(f(self._h, a_ptr, b_ptr, out_ptr, n_docs, a_stride, stream or None), f"clock_{which}")

@@ -1,0 +1,232 @@
+/*
+ * hypermerge_amd.h — C-ABI boundary of the MI355X batched CRDT merge engine.
+ *
+ * The engine replaces the L5 -> L0 edge of hypermerge: everything that
+ * Automerge 0.12's `Backend.applyChanges(state, changes)` computes when
+ * `DocBackend.applyRemoteChanges` / `DocBackend.init` hand it a batch of
+ * decoded `Change` objects, plus the vector-clock bookkeeping around it.
+ *
+ *   reference call sites replaced (paths relative to the reference repo):
+ *     src/DocBackend.ts:115-117  applyRemoteChanges(changes)  -> remoteChangesQ
+ *     src/DocBackend.ts:169-185  Backend.applyChanges(back, changes) + updateClock
+ *     src/DocBackend.ts:144-167  init(changes): Backend.applyChanges(Backend.init(), changes)
+ *     src/DocBackend.ts:135-142  updateClock (clock includes queued changes)
+ *     src/DocBackend.ts:90-100   testMinimumClockSatisfied -> Clock.cmp
+ *     src/Clock.ts:13-38,87-113  gte / cmp / union / intersection
+ *     src/RepoBackend.ts:570-579 MaterializeMsg (history-prefix replay)
+ *   Automerge 0.12.2-beta.0 (yarn.lock:178-185; NOT vendored) backend/op_set.js:
+ *     addChange/applyQueuedOps/causallyReady, applyChange/transitiveDeps,
+ *     applyAssign (map registers, counters, conflicts), applyInsert +
+ *     updateListElement (RGA lists/text).  Restated in SURVEY.md Appendix A.
+ *
+ * A batch is columnar: plain little-endian tables, no strings.  Strings
+ * (actor ids, object UUIDs, keys, string values) are interned by the host
+ * encoder; the engine only needs their identity, except actor ids, whose
+ * JS UTF-16 string order is encoded as the per-document actor *rank*.
+ *
+ * No C++ exception crosses this boundary.  Every call returns an hm_status;
+ * per-document failures are reported per document (hm_doc_result.status),
+ * never as a whole-batch failure (the reference aborts only the throwing
+ * document's applyChanges; SURVEY.md §5, §8b "Errors").
+ */
+#ifndef HYPERMERGE_AMD_H
+#define HYPERMERGE_AMD_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HM_ABI_VERSION 1u
+
+/* ------------------------------------------------------------------ */
+/* Status codes                                                        */
+/* ------------------------------------------------------------------ */
+typedef enum {
+    HM_OK = 0,
+    /* per-document Automerge errors (the message each maps to is what the
+     * reference would throw; see hm_status_message) */
+    HM_ERR_INCONSISTENT_SEQ = 1,   /* 'Inconsistent reuse of sequence number <seq> by <actor>' */
+    HM_ERR_UNKNOWN_OBJECT = 2,     /* 'Modification of unknown object <obj>' */
+    HM_ERR_DUPLICATE_OBJECT = 3,   /* 'Duplicate creation of object <obj>' */
+    HM_ERR_DUPLICATE_ELEM = 4,     /* 'Duplicate list element ID <elemId>' */
+    HM_ERR_MISSING_ELEM = 5,       /* 'Missing index entry for list element <elemId>' */
+    /* engine-side limits / preconditions (not reference errors) */
+    HM_ERR_UNSUPPORTED = 16,       /* document outside the engine's supported envelope */
+    /* call-level errors */
+    HM_ERR_INVALID = 32,           /* malformed batch (bad offsets, sizes) */
+    HM_ERR_DEVICE = 33,            /* HIP runtime failure */
+    HM_ERR_NOMEM = 34
+} hm_status;
+
+/* ------------------------------------------------------------------ */
+/* Op actions / datatypes / value tags (Automerge 0.12 op vocabulary)   */
+/* ------------------------------------------------------------------ */
+enum {
+    HM_MAKE_MAP = 0, HM_MAKE_TABLE = 1, HM_MAKE_LIST = 2, HM_MAKE_TEXT = 3,
+    HM_INS = 4, HM_SET = 5, HM_DEL = 6, HM_LINK = 7, HM_INC = 8
+};
+enum { HM_DT_NONE = 0, HM_DT_COUNTER = 1, HM_DT_TIMESTAMP = 2 };
+enum {
+    HM_V_NULL = 0, HM_V_FALSE = 1, HM_V_TRUE = 2,
+    HM_V_INT = 3,    /* integral JS number, |v| < 2^53, stored as int64 */
+    HM_V_FLOAT = 4,  /* any other JS number, stored as IEEE-754 f64 bits */
+    HM_V_STR = 5,    /* string-pool id */
+    HM_V_OBJ = 6     /* doc-local object id (link target) */
+};
+#define HM_HEAD 0xFFFFFFFFu      /* ins parent '_head' */
+#define HM_NONE 0xFFFFFFFFu
+
+/* ------------------------------------------------------------------ */
+/* Columnar batch tables                                               */
+/* ------------------------------------------------------------------ */
+
+/* One row per document (32 B). */
+typedef struct {
+    uint32_t change_off;  /* first row of this doc in changes[] */
+    uint32_t n_changes;   /* changes handed to applyChanges, in array (arrival) order */
+    uint32_t op_off;      /* first row of this doc in ops[]; ops are grouped by change, in op order */
+    uint32_t n_ops;
+    uint32_t reg_off;     /* first row of this doc in the per-register output table */
+    uint32_t n_regs;      /* registers = interned (obj, key) pairs; for lists key = elemId */
+    uint32_t n_objs;      /* interned object ids, 0 = ROOT '00000000-0000-0000-0000-000000000000' */
+    uint16_t n_actors;    /* actor ranks 0..n_actors-1 (rank = order of the actor id strings) */
+    uint16_t flags;       /* reserved, 0 */
+} hm_doc_row;
+
+/* One row per change (24 B), in the order the changes are handed over. */
+typedef struct {
+    uint16_t actor;       /* actor rank within the doc */
+    uint16_t n_deps;
+    uint32_t seq;         /* 1-based */
+    uint32_t dep_off;     /* first row in deps[] (global) */
+    uint32_t n_ops;       /* ops of this change: rows [op_first, op_first+n_ops) */
+    uint32_t op_first;    /* global op row */
+    uint32_t content_id;  /* equal <=> the two changes are deep-equal (host-interned) */
+} hm_change_row;
+
+/* One row per dependency entry (8 B), in the change's `deps` key order. */
+typedef struct {
+    uint16_t actor;
+    uint16_t pad;
+    uint32_t seq;
+} hm_dep_row;
+
+/* One row per op (32 B). */
+typedef struct {
+    uint32_t obj;         /* doc-local object id the op modifies (make*: the created object) */
+    uint32_t reg;         /* set/del/link/inc: register of (obj,key); ins: register of the new element */
+    uint32_t parent;      /* ins: register of the predecessor element, or HM_HEAD */
+    uint32_t elem;        /* ins: element counter */
+    uint8_t  action;      /* HM_MAKE_* / HM_INS / HM_SET / HM_DEL / HM_LINK / HM_INC */
+    uint8_t  datatype;    /* HM_DT_* */
+    uint8_t  vtag;        /* HM_V_* */
+    uint8_t  pad;
+    uint32_t key;         /* string-pool id of the map key (rendering only) */
+    uint64_t value;       /* int64 / f64 bits / string id / object id, by vtag */
+} hm_op_row;
+
+typedef struct {
+    uint32_t n_docs, n_changes, n_deps, n_ops, n_regs;
+    uint32_t a_stride;    /* >= max n_actors; stride of every per-actor output row */
+    /* per-document maxima over the batch (launch sizing hints); 0 = unknown,
+     * computed by the engine from the doc table */
+    uint32_t max_changes, max_ops, max_regs, max_objs;
+    const hm_doc_row    *docs;
+    const hm_change_row *changes;
+    const hm_dep_row    *deps;
+    const hm_op_row     *ops;
+    const uint32_t      *min_clock;  /* optional [n_docs*a_stride] minimumClock (0 = absent) or NULL */
+} hm_batch;
+
+/* ------------------------------------------------------------------ */
+/* Results                                                             */
+/* ------------------------------------------------------------------ */
+typedef struct {          /* 32 B */
+    int32_t  status;      /* hm_status for this document */
+    uint32_t err_change;  /* doc-local change index where the first error fired (HM_NONE if ok) */
+    uint32_t err_op;      /* op index within that change, HM_NONE for change-level errors */
+    uint32_t hist_len;    /* opSet.history.size after the merge */
+    uint32_t n_queued;    /* changes left in opSet.queue (causally blocked) */
+    uint32_t n_surv;      /* survivors written for this doc */
+    uint32_t min_cmp;     /* Clock.cmp(DocBackend.clock, minimumClock): 0 EQ 1 GT 2 LT 3 CONCUR */
+    uint32_t pad;
+} hm_doc_result;
+
+typedef struct {          /* 16 B per register */
+    uint32_t n_surv;      /* surviving ops (winner + conflicts) */
+    uint32_t surv_off;    /* doc-local offset into the survivor table (doc base = docs[d].op_off) */
+    int32_t  list_index;  /* list/text element: index among visible elements, else -1 */
+    uint32_t obj;         /* object the register belongs to (HM_NONE if never touched) */
+} hm_reg_result;
+
+typedef struct {          /* 16 B per survivor, winner first then conflicts */
+    uint32_t op;          /* doc-local op index (ops[docs[d].op_off + op]) */
+    uint32_t vtag;        /* value tag of the resolved value (counters may turn INT -> FLOAT) */
+    uint64_t value;       /* resolved value (counter: base + causally-later incs) */
+} hm_surv_result;
+
+typedef struct {
+    hm_doc_result  *docs;       /* [n_docs] */
+    uint32_t       *clock;      /* [n_docs*a_stride] opSet.clock (applied changes only) */
+    uint32_t       *back_clock; /* [n_docs*a_stride] DocBackend.clock (max over handed changes, quirk) */
+    uint32_t       *heads;      /* [n_docs*a_stride] opSet.deps (0 = no entry) */
+    int32_t        *hist;       /* [n_changes] history position, -1 queued, -2 duplicate (no-op) */
+    uint32_t       *all_deps;   /* [n_changes*a_stride] opSet.states[actor][seq-1].allDeps (0 if not applied) */
+    hm_reg_result  *regs;       /* [n_regs] */
+    hm_surv_result *surv;       /* [n_ops] */
+} hm_results;
+
+/* ------------------------------------------------------------------ */
+/* Engine                                                              */
+/* ------------------------------------------------------------------ */
+typedef struct hm_engine hm_engine;
+
+typedef struct {
+    int device;           /* HIP device ordinal */
+    int flags;            /* reserved, 0 */
+} hm_config;
+
+/* Version of the ABI compiled into the library. */
+uint32_t hm_abi_version(void);
+const char *hm_status_message(int status);
+
+int  hm_engine_create(const hm_config *cfg, hm_engine **out);
+void hm_engine_destroy(hm_engine *e);
+const char *hm_engine_last_error(const hm_engine *e);
+
+/* Host batch -> device -> merge -> host results (synchronous).  All host
+ * buffers are owned by the caller; the engine stages copies. */
+int hm_merge_host(hm_engine *e, const hm_batch *batch, const hm_results *out);
+
+/* Device-resident merge: every pointer in `batch` and `out` is a device
+ * pointer on the engine's device; work is enqueued on `stream` (hipStream_t,
+ * NULL = the engine's stream) and the call returns without synchronising.
+ * `scratch` is device memory of at least hm_scratch_bytes(batch) bytes. */
+size_t hm_scratch_bytes(const hm_batch *batch);
+int hm_merge_device(hm_engine *e, const hm_batch *batch, const hm_results *out,
+                    void *scratch, void *stream);
+
+/* Per-kernel launch timing of the last hm_merge_* call on `stream`,
+ * measured with HIP events on that stream (ms).  Returns number filled. */
+int hm_last_kernel_ms(hm_engine *e, float *ms, int max_kernels);
+
+/* ------------------------------------------------------------------ */
+/* Clock algebra (src/Clock.ts) over dense per-doc rows (a_stride wide) */
+/* ------------------------------------------------------------------ */
+/* out[d] = Clock.cmp(a[d], b[d]) coded 0 EQ, 1 GT, 2 LT, 3 CONCUR  (src/Clock.ts:27-38) */
+int hm_clock_cmp_device(hm_engine *e, const uint32_t *a, const uint32_t *b, uint8_t *out,
+                        uint32_t n_docs, uint32_t a_stride, void *stream);
+/* c[d] = Clock.union(a[d], b[d]) elementwise max (src/Clock.ts:87-95) */
+int hm_clock_union_device(hm_engine *e, const uint32_t *a, const uint32_t *b, uint32_t *c,
+                          uint32_t n_docs, uint32_t a_stride, void *stream);
+/* c[d] = Clock.intersection(a[d], b[d]) elementwise min, zeros dropped (src/Clock.ts:103-113) */
+int hm_clock_intersection_device(hm_engine *e, const uint32_t *a, const uint32_t *b, uint32_t *c,
+                                 uint32_t n_docs, uint32_t a_stride, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HYPERMERGE_AMD_H */
