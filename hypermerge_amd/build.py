@@ -1,0 +1,56 @@
+"""Native build of the package (no cmake): hipcc for the gfx950 library,
+g++ for the synthetic-feed generator.  Outputs go to hypermerge_amd/_lib/
+in-tree so they travel to the GPU box with the repo snapshot."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIBDIR = os.path.join(HERE, "_lib")
+CSRC = os.path.join(HERE, "csrc")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("HM_OFFLOAD_ARCH", "gfx950")
+
+GPU_SRCS = ["merge_kernels.hip", "engine.cpp"]
+GPU_DEPS = GPU_SRCS + ["merge_kernels.h", "../../include/hypermerge_amd.h"]
+
+
+def _stale(out: str, deps) -> bool:
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(os.path.join(CSRC, d)) > t for d in deps)
+
+
+def _run(cmd) -> None:
+    print("+", " ".join(cmd), file=sys.stderr, flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def build_gpu(force: bool = False) -> str:
+    out = os.path.join(LIBDIR, "libhmgpu.so")
+    if force or _stale(out, GPU_DEPS):
+        os.makedirs(LIBDIR, exist_ok=True)
+        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+              "-o", out] + [os.path.join(CSRC, s) for s in GPU_SRCS])
+    return out
+
+
+def build_synth(force: bool = False) -> str:
+    out = os.path.join(LIBDIR, "libhmsynth.so")
+    if force or _stale(out, ["synth.cpp", "../../include/hypermerge_amd.h"]):
+        os.makedirs(LIBDIR, exist_ok=True)
+        _run(["g++", "-O2", "-std=c++17", "-Wall", "-fPIC", "-shared", "-pthread", "-o", out,
+              os.path.join(CSRC, "synth.cpp")])
+    return out
+
+
+def build_all(force: bool = False) -> None:
+    build_gpu(force)
+    build_synth(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

@@ -1,0 +1,92 @@
+"""HIP engine vs the CPU restatement, bit-exact, on the same seeded inputs
+(called through the C-ABI).  Documents the engine reports as UNSUPPORTED are
+outside its current envelope (counted, and required to be zero for the
+configs in scope)."""
+import numpy as np
+import pytest
+
+from hypermerge_amd import synth
+from hypermerge_amd.columnar import encode
+from hypermerge_amd.render import canonical_json
+import oracle.oracle as O
+
+from kat_cases import CASES
+
+pytestmark = pytest.mark.gpu
+
+
+def assert_same(b, g, o, allow_unsupported=False):
+    gs, os_ = g.docs["status"], o.docs["status"]
+    unsup = gs == 16
+    if not allow_unsupported:
+        assert not unsup.any(), f"{int(unsup.sum())} docs outside the engine envelope"
+    live = ~unsup
+    np.testing.assert_array_equal(gs[live], os_[live])
+    err = live & (os_ != 0)
+    for f in ("err_change", "err_op"):
+        np.testing.assert_array_equal(g.docs[f][err], o.docs[f][err])
+    ok = live & (os_ == 0)
+    for f in ("hist_len", "n_queued", "n_surv", "min_cmp"):
+        np.testing.assert_array_equal(g.docs[f][ok], o.docs[f][ok], err_msg=f)
+    S = b.a_stride
+    for f in ("clock", "back_clock", "heads"):
+        np.testing.assert_array_equal(getattr(g, f)[np.repeat(ok, S)], getattr(o, f)[np.repeat(ok, S)], err_msg=f)
+    cm = np.repeat(ok, b.docs["n_changes"])
+    np.testing.assert_array_equal(g.hist[cm], o.hist[cm])
+    np.testing.assert_array_equal(g.all_deps[np.repeat(cm, S)], o.all_deps[np.repeat(cm, S)])
+    rm = np.repeat(ok, b.docs["n_regs"])
+    np.testing.assert_array_equal(g.regs[rm], o.regs[rm])
+    sm = np.zeros(len(b.ops), bool)
+    for d in np.nonzero(ok)[0]:
+        s0 = int(b.docs["op_off"][d])
+        sm[s0: s0 + int(o.docs["n_surv"][d])] = True
+    np.testing.assert_array_equal(g.surv[sm], o.surv[sm])
+    return int(unsup.sum())
+
+
+@pytest.mark.parametrize("name,n,extra", [
+    ("C4", 20000, {}),
+    ("C2", 20000, {}),
+    ("C4", 4000, {"arrival": 1}),                          # loadDocument actor-major order: blocked changes
+    ("C2", 4000, {"arrival": 2, "shuffle_pct": 25}),       # out-of-order delivery
+    ("C2", 2000, {"del_pct": 20}),
+    ("C4", 2000, {"actors": 3, "changes_per_actor": 20}),
+])
+def test_synthetic_parity(engine, name, n, extra):
+    b = synth.generate(synth.config(name, n_docs=n, **extra))
+    assert_same(b, engine.merge(b), O.merge(b, threads=8))
+
+
+def test_full_size_c4_properties(engine):
+    """BASELINE size (1M docs): size-independent properties, no oracle run."""
+    b = synth.generate(synth.config("C4", n_docs=1_000_000))
+    g = engine.merge(b)
+    assert (g.docs["status"] == 0).all()
+    assert int(g.docs["hist_len"].sum()) == len(b.changes)          # every change applied once
+    S = b.a_stride
+    clk = g.clock.reshape(-1, S)
+    assert (clk.sum(1) == 64).all()                                  # clock = changes per actor
+    # history is a permutation of 0..n-1 per document
+    h = g.hist.reshape(-1, 64)
+    assert (np.sort(h, 1) == np.arange(64)).all()
+    # idempotence: merging again gives identical results
+    g2 = engine.merge(b)
+    for f in ("docs", "clock", "heads", "hist", "all_deps", "regs", "surv"):
+        np.testing.assert_array_equal(getattr(g, f), getattr(g2, f))
+
+
+@pytest.mark.parametrize("name,changes,expect", CASES, ids=[c[0] for c in CASES])
+def test_known_answers_on_gpu(engine, name, changes, expect):
+    b = encode([changes])
+    g, o = engine.merge(b), O.merge(b)
+    if g.docs["status"][0] == 16:
+        pytest.skip("outside the small-document envelope (lists/RGA)")
+    assert canonical_json(b, g, 0) == canonical_json(b, o, 0)
+
+
+def test_empty_and_single(engine):
+    from hypermerge_amd.columnar import ROOT_ID as R
+    docs = [[], [{"actor": "a", "seq": 1, "deps": {}, "ops": []}],
+            [{"actor": "a", "seq": 1, "deps": {}, "ops": [{"action": "set", "obj": R, "key": "k", "value": 1}]}]]
+    b = encode(docs)
+    assert_same(b, engine.merge(b), O.merge(b))
