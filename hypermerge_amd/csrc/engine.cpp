@@ -42,7 +42,7 @@ int hip_fail(hm_engine *e, hipError_t r, const char *what) {
         if (_r != hipSuccess) return hip_fail(e, _r, #call); \
     } while (0)
 
-struct Caps { uint32_t opl, regs, objs; };
+struct Caps { uint32_t opl, regs, objs; bool lists; };
 
 Caps launch_caps(const hm_batch *b) {
     Caps c;
@@ -52,6 +52,7 @@ Caps launch_caps(const hm_batch *b) {
     c.regs = (c.regs + 15) & ~15u;
     c.objs = std::max<uint32_t>(1, std::min<uint32_t>(b->max_objs, 256));
     c.objs = (c.objs + 15) & ~15u;
+    c.lists = (b->doc_flags & HM_DOC_HAS_LISTS) != 0;
     return c;
 }
 
@@ -64,11 +65,11 @@ int launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, hipStream
     p.n_docs = b->n_docs; p.a_stride = b->a_stride; p.cap_regs = c.regs; p.cap_objs = c.objs;
     if (b->n_docs == 0) { e->n_last = 0; return HM_OK; }
     // persistent grid: enough resident 1-wave workgroups to fill every CU
-    size_t lds = hm_small_lds_bytes(c.opl, c.regs, c.objs);
+    size_t lds = hm_small_lds_bytes(c.opl, c.regs, c.objs, c.lists);
     uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, (160 * 1024) / std::max<size_t>(lds, 1)));
     uint32_t grid = std::min<uint32_t>(b->n_docs, (uint32_t)e->num_cus * per_cu * 2);
     HIPCHK(e, hipEventRecord(e->ev[0], s));
-    hipError_t r = hm_launch_small(p, c.opl, grid, s);
+    hipError_t r = hm_launch_small(p, c.opl, c.lists, grid, s);
     if (r != hipSuccess) return hip_fail(e, r, "merge_small_kernel launch");
     HIPCHK(e, hipEventRecord(e->ev[1], s));
     e->n_last = 1;
@@ -163,6 +164,7 @@ int hm_merge_host(hm_engine *e, const hm_batch *hb, const hm_results *ho) {
                 b.max_ops = std::max(b.max_ops, hb->docs[d].n_ops);
                 b.max_regs = std::max(b.max_regs, hb->docs[d].n_regs);
                 b.max_objs = std::max(b.max_objs, hb->docs[d].n_objs);
+                b.doc_flags |= hb->docs[d].flags;
             }
         const size_t S = b.a_stride;
         struct Seg { size_t bytes; size_t off; };

@@ -19,8 +19,8 @@ struct SmallParams {
     uint32_t cap_regs, cap_objs;     // LDS carve of this launch
 };
 
-size_t hm_small_lds_bytes(uint32_t opl, uint32_t cap_regs, uint32_t cap_objs);
-hipError_t hm_launch_small(const SmallParams &p, uint32_t opl, uint32_t grid, hipStream_t s);
+size_t hm_small_lds_bytes(uint32_t opl, uint32_t cap_regs, uint32_t cap_objs, bool lists);
+hipError_t hm_launch_small(const SmallParams &p, uint32_t opl, bool lists, uint32_t grid, hipStream_t s);
 // which: 0 cmp (out uint8_t*), 1 union, 2 intersection (out uint32_t*)
 hipError_t hm_launch_clock(int which, const uint32_t *a, const uint32_t *b, void *out, uint32_t n_docs,
                            uint32_t S, hipStream_t s);

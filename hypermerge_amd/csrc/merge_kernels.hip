@@ -89,11 +89,14 @@ struct SmallLds {
     LDS int32_t *hist_of;
     LDS uint16_t *survtmp, *survop, *opbase, *opreg;
     LDS uint8_t *h2a, *chactor, *opchg, *objtype;
+    // K3 (RGA lists); carved only for launches with list documents
+    LDS uint32_t *nins, *pcount, *poff, *pfill, *nodekey, *tour0, *tour1, *listbase;
+    LDS uint16_t *nodeop, *nodepi, *regnode, *plist, *fc, *ns, *listid;
 };
 
 // LDS carve, identical for the host size query and the device pointers.
 template <typename L_t, typename P>
-__host__ __device__ inline size_t small_carve(P base, uint32_t NOp, uint32_t NR, uint32_t NO, L_t *L) {
+__host__ __device__ inline size_t small_carve(P base, uint32_t NOp, uint32_t NR, uint32_t NO, bool lists, L_t *L) {
     size_t o = 0;
 #define TAKE(f, T, cnt) do { L->f = (decltype(L->f))(base + o); o = (o + (size_t)(cnt) * sizeof(T) + 15) & ~(size_t)15; } while (0)
     TAKE(anc, u64, 64);          TAKE(chain, u64, NA_MAX);     TAKE(segor, u64, NR);
@@ -109,6 +112,15 @@ __host__ __device__ inline size_t small_carve(P base, uint32_t NOp, uint32_t NR,
     TAKE(opreg, uint16_t, NOp);
     TAKE(h2a, uint8_t, 64);      TAKE(chactor, uint8_t, 64);   TAKE(opchg, uint8_t, NOp);
     TAKE(objtype, uint8_t, NO);
+    if (lists) {
+        const uint32_t NP = NR + NO, NE = 2 * (NOp + NO);
+        TAKE(nins, uint32_t, 1);      TAKE(pcount, uint32_t, NP);  TAKE(poff, uint32_t, NP);
+        TAKE(pfill, uint32_t, NP);    TAKE(nodekey, uint32_t, NOp); TAKE(tour0, uint32_t, NE);
+        TAKE(tour1, uint32_t, NE);    TAKE(listbase, uint32_t, NO + 1);
+        TAKE(nodeop, uint16_t, NOp);  TAKE(nodepi, uint16_t, NOp); TAKE(regnode, uint16_t, NR);
+        TAKE(plist, uint16_t, NOp);   TAKE(fc, uint16_t, NP);      TAKE(ns, uint16_t, NOp);
+        TAKE(listid, uint16_t, NO);
+    }
 #undef TAKE
     L->bclock = L->base + NA_MAX;
     L->headv = L->base + 2 * NA_MAX;
@@ -139,8 +151,155 @@ __device__ __forceinline__ uint32_t meta_vtag(uint32_t m) { return (m >> 16) & 0
 // then even p ascending ("append, then reverse" after every assign)
 __device__ __forceinline__ uint32_t tie_order(uint32_t pc) { return (pc & 1) ? (0x10000u - pc) : (0x20000u + pc); }
 
-// Merge one document with the whole wave.  Every return is wave-uniform.
+
+// ---------------- K3: RGA document order (applyInsert, updateListElement, getPrevious) ----------------
+// The applied `ins` ops of a list form a tree (parent = the elemId inserted after, or
+// '_head'); siblings are ordered by lamportCompare (elem, actor) DESCENDING and the list
+// is the pre-order of that tree restricted to visible elements (a non-empty survivor
+// set).  Pre-order comes from an Euler tour ranked by pointer jumping in LDS.
+// Writes the visible index of every element register into L.insmin (as int32, -1 hidden).
 template <int OPL>
+__device__ __forceinline__ void rga_order(const SmallLds &L, uint32_t R, uint32_t O,
+                                          const uint32_t (&oreg)[OPL], const uint32_t (&oobj)[OPL],
+                                          const uint32_t (&opar)[OPL], const uint32_t (&oact)[OPL],
+                                          const uint32_t (&oelem)[OPL], const uint32_t (&oarr)[OPL],
+                                          const int32_t (&oh)[OPL]) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t NP = R + O;
+    constexpr uint32_t END = 0xFFFFu;
+    for (uint32_t i = lane; i < NP; i += WAVE) { L.pcount[i] = 0; L.pfill[i] = 0; L.fc[i] = 0xFFFFu; }
+    for (uint32_t i = lane; i < R; i += WAVE) L.regnode[i] = 0xFFFFu;
+    if (lane == 0) *L.nins = 0;
+    // compact ids of the list/text objects
+    uint32_t nl = 0;
+    for (uint32_t o0 = 0; o0 < O; o0 += WAVE) {
+        const uint32_t o = o0 + lane;
+        const uint32_t ot = o < O ? L.objtype[o] : 0xFFu;
+        const bool isl = ot == HM_MAKE_LIST || ot == HM_MAKE_TEXT;
+        const u64 mk = __ballot(isl);
+        if (o < O) L.listid[o] = isl ? (uint16_t)(nl + __popcll(mk & ((1ull << lane) - 1))) : (uint16_t)0xFFFFu;
+        nl += (uint32_t)__popcll(mk);
+    }
+    wave_sync();
+    // nodes = applied ins ops
+#pragma unroll
+    for (int t = 0; t < OPL; t++) {
+        if (oh[t] < 0 || oact[t] != HM_INS) continue;
+        const uint32_t i = lds_add(L.nins, 1u);
+        const uint32_t pi = opar[t] == HM_HEAD ? R + oobj[t] : opar[t];
+        L.nodeop[i] = (uint16_t)(lane + WAVE * t);
+        L.nodepi[i] = (uint16_t)pi;
+        L.nodekey[i] = (oelem[t] << 8) | L.chactor[oarr[t]];
+        L.regnode[oreg[t]] = (uint16_t)i;
+        lds_add(&L.pcount[pi], 1u);
+    }
+    wave_sync();
+    const uint32_t N = *L.nins;
+    // children of every parent (CSR over parent slots: element registers, then list heads)
+    uint32_t tot = 0;
+    for (uint32_t r0 = 0; r0 < NP; r0 += WAVE) {
+        const uint32_t r = r0 + lane;
+        uint32_t tt;
+        const uint32_t ex = wave_excl_scan(r < NP ? L.pcount[r] : 0u, &tt);
+        if (r < NP) L.poff[r] = tot + ex;
+        tot += tt;
+    }
+    wave_sync();
+    for (uint32_t i = lane; i < N; i += WAVE) {
+        const uint32_t pi = L.nodepi[i];
+        L.plist[L.poff[pi] + lds_add(&L.pfill[pi], 1u)] = (uint16_t)i;
+    }
+    wave_sync();
+    // sibling order: next sibling = the largest smaller key; the largest key is the first child
+    for (uint32_t i = lane; i < N; i += WAVE) {
+        const uint32_t pi = L.nodepi[i], key = L.nodekey[i];
+        const uint32_t q0 = L.poff[pi], qn = L.pcount[pi];
+        uint32_t best = 0xFFFFu, bkey = 0;
+        bool firstc = true;
+        for (uint32_t q = 0; q < qn; q++) {
+            const uint32_t j = L.plist[q0 + q], kj = L.nodekey[j];
+            if (kj > key) firstc = false;
+            else if (kj < key && (best == 0xFFFFu || kj > bkey)) { best = j; bkey = kj; }
+        }
+        L.ns[i] = (uint16_t)best;
+        if (firstc) L.fc[pi] = (uint16_t)i;
+    }
+    wave_sync();
+    // Euler tour: down(i) = 2i (value 1), up(i) = 2i+1; list head h = N + listid: 2h, 2h+1 (end)
+    const uint32_t E = 2 * (N + nl);
+    for (uint32_t i = lane; i < N; i += WAVE) {
+        const uint32_t reg = L.opreg[L.nodeop[i]];
+        const uint32_t hd = N + L.listid[L.regobj[reg]];
+        const uint32_t f = L.fc[reg];
+        const uint32_t sd = f != 0xFFFFu ? 2 * f : 2 * i + 1;
+        const uint32_t pi = L.nodepi[i];
+        const uint32_t su = L.ns[i] != 0xFFFFu ? 2u * L.ns[i] : (pi >= R ? 2 * hd + 1 : 2u * L.regnode[pi] + 1);
+        L.tour0[2 * i] = (sd << 16) | 1u;
+        L.tour0[2 * i + 1] = su << 16;
+    }
+    for (uint32_t o = lane; o < O; o += WAVE) {
+        const uint32_t l = L.listid[o];
+        if (l == 0xFFFFu) continue;
+        const uint32_t h = N + l, f = L.fc[R + o];
+        L.tour0[2 * h] = (f != 0xFFFFu ? 2 * f : 2 * h + 1) << 16;
+        L.tour0[2 * h + 1] = END << 16;
+    }
+    wave_sync();
+    LDS uint32_t *cur = L.tour0, *nxt = L.tour1;
+    const uint32_t rounds = E ? 32 - __builtin_clz(E) : 0;
+    for (uint32_t rd = 0; rd < rounds; rd++) {
+        for (uint32_t e = lane; e < E; e += WAVE) {
+            uint32_t x = cur[e];
+            const uint32_t nx = x >> 16;
+            if (nx != END) { const uint32_t y = cur[nx]; x = (y & 0xFFFF0000u) | ((x & 0xFFFFu) + (y & 0xFFFFu)); }
+            nxt[e] = x;
+        }
+        wave_sync();
+        LDS uint32_t *tmp = cur; cur = nxt; nxt = tmp;
+    }
+    // list sizes -> base positions; pre-order position of every node
+    uint32_t lb = 0;
+    for (uint32_t l0 = 0; l0 < nl; l0 += WAVE) {
+        const uint32_t l = l0 + lane;
+        uint32_t tt;
+        const uint32_t ex = wave_excl_scan(l < nl ? (cur[2 * (N + l)] & 0xFFFFu) : 0u, &tt);
+        if (l < nl) L.listbase[l] = lb + ex;
+        lb += tt;
+    }
+    wave_sync();
+    for (uint32_t i = lane; i < N; i += WAVE) {
+        const uint32_t reg = L.opreg[L.nodeop[i]];
+        const uint32_t l = L.listid[L.regobj[reg]];
+        const uint32_t total = cur[2 * (N + l)] & 0xFFFFu;
+        const uint32_t pos = L.listbase[l] + total - (cur[2 * i] & 0xFFFFu);
+        L.seglist[pos] = L.survcnt[reg] > 0 ? 1u : 0u;       // visible = non-empty survivor set
+        L.nodekey[i] = pos;
+        L.insmin[reg] = 0xFFFFFFFFu;                          // -> list index (or -1)
+    }
+    wave_sync();
+    uint32_t vc = 0;
+    for (uint32_t q0 = 0; q0 < N; q0 += WAVE) {
+        const uint32_t q = q0 + lane;
+        uint32_t tt;
+        const uint32_t ex = wave_excl_scan(q < N ? L.seglist[q] : 0u, &tt);
+        if (q < N) L.survp[q] = vc + ex;
+        vc += tt;
+    }
+    wave_sync();
+    for (uint32_t i = lane; i < N; i += WAVE) {
+        const uint32_t reg = L.opreg[L.nodeop[i]];
+        const uint32_t pos = L.nodekey[i];
+        if (L.seglist[pos]) {
+            const uint32_t l = L.listid[L.regobj[reg]];
+            const uint32_t first_pos = L.listbase[l];
+            L.insmin[reg] = L.survp[pos] - (first_pos < N ? L.survp[first_pos] : vc);
+        }
+    }
+    wave_sync();
+}
+
+// Merge one document with the whole wave.  Every return is wave-uniform.
+template <int OPL, bool LISTS>
 __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const SmallLds &L, uint32_t d,
                                                    const hm_doc_row &doc) {
     constexpr uint32_t NOp = WAVE * OPL;
@@ -354,17 +513,18 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     wave_sync();
 
     // ---------------- K2: ops (lane + 64*t) ----------------
-    uint32_t oreg[OPL], oobj[OPL], opar[OPL], oact[OPL], okey[OPL], oarr[OPL];
+    uint32_t oreg[OPL], oobj[OPL], opar[OPL], oact[OPL], okey[OPL], oarr[OPL], oelem[OPL];
     int32_t oh[OPL];
 #pragma unroll
     for (int t = 0; t < OPL; t++) {
         const uint32_t k = lane + WAVE * t;
-        oh[t] = -1; okey[t] = 0; oarr[t] = 0; oreg[t] = 0; oobj[t] = 0; opar[t] = 0; oact[t] = 0xFF;
+        oh[t] = -1; okey[t] = 0; oarr[t] = 0; oreg[t] = 0; oobj[t] = 0; opar[t] = 0; oact[t] = 0xFF; oelem[t] = 0;
         if (k < m) {
             const hm_op_row o = p.ops[doc.op_off + k];
             const uint32_t ch = L.opchg[k];
             oarr[t] = ch; oh[t] = L.hist_of[ch];
-            oreg[t] = o.reg; oobj[t] = o.obj; opar[t] = o.parent; oact[t] = o.action;
+            oreg[t] = o.reg; oobj[t] = o.obj; opar[t] = o.parent; oact[t] = o.action; oelem[t] = o.elem;
+            if (o.action == HM_INS && o.elem >= (1u << 24)) lds_or(L.flags, FL_UNSUPPORTED);
             okey[t] = ((uint32_t)(oh[t] < 0 ? 0 : oh[t]) << 16) | (k - L.opbase[ch]);
             L.opmeta[k] = (uint32_t)o.action | ((uint32_t)o.datatype << 8) | ((uint32_t)o.vtag << 16) |
                           ((oh[t] >= 0 ? 1u : 0u) << 24);
@@ -432,7 +592,8 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
             }
         }
     }
-    if (__ballot(has_list)) lds_or(L.flags, FL_UNSUPPORTED);   // RGA order: not in this kernel yet
+    const bool doc_lists = __ballot(has_list) != 0;
+    if (!LISTS && doc_lists) lds_or(L.flags, FL_UNSUPPORTED);   // launched without the K3 carve
     wave_sync();
     if (*L.errkey != ~0ull) return OUT_ERROR;                    // the first throw wins
     if (*L.flags & FL_UNSUPPORTED) return OUT_UNSUPPORTED;
@@ -522,6 +683,9 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         L.survabs[pos] = 0;
     }
     wave_sync();
+    if constexpr (LISTS) {
+        if (doc_lists) rga_order<OPL>(L, R, O, oreg, oobj, opar, oact, oelem, oarr, oh);
+    }
     // counters: an inc adds to every surviving counter set that is its ancestor
     bool float_counter = false;
 #pragma unroll
@@ -563,7 +727,8 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     if (__ballot(inexact)) return OUT_UNSUPPORTED;
     for (uint32_t r = lane; r < R; r += WAVE) {
         hm_reg_result rr;
-        rr.n_surv = L.survcnt[r]; rr.surv_off = L.regoff[r]; rr.list_index = -1; rr.obj = L.regobj[r];
+        rr.n_surv = L.survcnt[r]; rr.surv_off = L.regoff[r]; rr.obj = L.regobj[r];
+        rr.list_index = (LISTS && doc_lists) ? (int32_t)L.insmin[r] : -1;
         p.res_regs[doc.reg_off + r] = rr;
     }
     // allDeps rows, coalesced: word w = (change w/S, actor w%S)
@@ -597,17 +762,17 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     return OUT_OK;
 }
 
-template <int OPL>
+template <int OPL, bool LISTS>
 __global__ __launch_bounds__(WAVE) void merge_small_kernel(SmallParams p) {
     extern __shared__ __align__(16) uint8_t lds_raw[];
     SmallLds L;
-    small_carve((LDS uint8_t *)lds_raw, WAVE * OPL, p.cap_regs, p.cap_objs, &L);
+    small_carve((LDS uint8_t *)lds_raw, WAVE * OPL, p.cap_regs, p.cap_objs, LISTS, &L);
     const uint32_t lane = threadIdx.x;
     for (uint32_t d = blockIdx.x; d < p.n_docs; d += gridDim.x) {
         const hm_doc_row doc = p.docs[d];
         const bool in_env = doc.n_changes <= 64 && doc.n_actors <= NA_MAX && doc.n_ops <= WAVE * OPL &&
                             doc.n_regs <= p.cap_regs && doc.n_objs <= p.cap_objs && doc.n_objs >= 1;
-        const Outcome oc = in_env ? merge_doc_small<OPL>(p, L, d, doc) : OUT_UNSUPPORTED;
+        const Outcome oc = in_env ? merge_doc_small<OPL, LISTS>(p, L, d, doc) : OUT_UNSUPPORTED;
         hm_doc_result *dres = p.res_docs + d;
         if (oc == OUT_ERROR) {
             // an Automerge throw aborted this document's Backend.applyChanges
@@ -659,18 +824,20 @@ __global__ void clock_intersection_kernel(const uint32_t *a, const uint32_t *b, 
 }  // namespace hm
 
 // ---------------- host-side launchers ----------------
-size_t hm_small_lds_bytes(uint32_t opl, uint32_t cap_regs, uint32_t cap_objs) {
+size_t hm_small_lds_bytes(uint32_t opl, uint32_t cap_regs, uint32_t cap_objs, bool lists) {
     hm::SmallLds L;
-    return hm::small_carve((uintptr_t)0, 64 * opl, cap_regs, cap_objs, &L);
+    return hm::small_carve((uintptr_t)0, 64 * opl, cap_regs, cap_objs, lists, &L);
 }
 
-hipError_t hm_launch_small(const SmallParams &p, uint32_t opl, uint32_t grid, hipStream_t s) {
-    const size_t lds = hm_small_lds_bytes(opl, p.cap_regs, p.cap_objs);
-    switch (opl) {
-    case 1: hipLaunchKernelGGL(hm::merge_small_kernel<1>, dim3(grid), dim3(WAVE), lds, s, p); break;
-    case 2: hipLaunchKernelGGL(hm::merge_small_kernel<2>, dim3(grid), dim3(WAVE), lds, s, p); break;
-    default: hipLaunchKernelGGL(hm::merge_small_kernel<4>, dim3(grid), dim3(WAVE), lds, s, p); break;
+hipError_t hm_launch_small(const SmallParams &p, uint32_t opl, bool lists, uint32_t grid, hipStream_t s) {
+    const size_t lds = hm_small_lds_bytes(opl, p.cap_regs, p.cap_objs, lists);
+#define HM_LAUNCH(O_, L_) hipLaunchKernelGGL((hm::merge_small_kernel<O_, L_>), dim3(grid), dim3(WAVE), lds, s, p)
+    if (lists) {
+        switch (opl) { case 1: HM_LAUNCH(1, true); break; case 2: HM_LAUNCH(2, true); break; default: HM_LAUNCH(4, true); }
+    } else {
+        switch (opl) { case 1: HM_LAUNCH(1, false); break; case 2: HM_LAUNCH(2, false); break; default: HM_LAUNCH(4, false); }
     }
+#undef HM_LAUNCH
     return hipGetLastError();
 }
 

@@ -101,7 +101,7 @@ struct DocOut {
     std::vector<hm_change_row> ch;
     std::vector<hm_dep_row> dp;
     std::vector<hm_op_row> op;
-    uint32_t n_regs = 0, n_objs = 1, n_actors = 0;
+    uint32_t n_regs = 0, n_objs = 1, n_actors = 0, flags = 0;
 };
 
 struct Gen {
@@ -279,7 +279,7 @@ struct Gen {
             maxel[a].push_back(std::max(prev, cmax));
             produce(a, std::move(ops));
         }
-        d.n_regs = regs; d.n_objs = 2;
+        d.n_regs = regs; d.n_objs = 2; d.flags = HM_DOC_HAS_LISTS;
     }
 
     // ---------------- kind 2: nested maps + lists (C5) ----------------
@@ -381,7 +381,7 @@ struct Gen {
             maxel[a].push_back(std::max(prev, cmax));
             produce(a, std::move(o2));
         }
-        d.n_regs = regs; d.n_objs = nobj;
+        d.n_regs = regs; d.n_objs = nobj; d.flags = HM_DOC_HAS_LISTS;
     }
 
     void run(DocOut &d) {
@@ -488,7 +488,7 @@ void *hm_synth_generate(const hm_synth_config *cfg) {
             row.change_off = (uint32_t)o->ch.size(); row.n_changes = (uint32_t)d.ch.size();
             row.op_off = (uint32_t)o->op.size(); row.n_ops = (uint32_t)d.op.size();
             row.reg_off = (uint32_t)o->n_regs; row.n_regs = d.n_regs; row.n_objs = d.n_objs;
-            row.n_actors = (uint16_t)d.n_actors; row.flags = 0;
+            row.n_actors = (uint16_t)d.n_actors; row.flags = (uint16_t)d.flags;
             uint32_t dbase = (uint32_t)o->dp.size(), obase = row.op_off;
             for (auto ch : d.ch) { ch.dep_off += dbase; ch.op_first += obase; o->ch.push_back(ch); }
             o->dp.insert(o->dp.end(), d.dp.begin(), d.dp.end());

@@ -35,6 +35,13 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB):
             raise EngineError(f"{LIB} is missing: run __graft_entry__.build() (no CPU fallback exists)")
+        # PyTorch-ROCm bundles its own libamdhip64.so.7 (same soname as /opt/rocm's).  Whichever
+        # loads first serves the whole process, so let torch's load first: then device pointers
+        # and streams from torch tensors are valid in this library's calls.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB)
         L.hm_abi_version.restype = ctypes.c_uint32
         L.hm_status_message.argtypes = [ctypes.c_int]

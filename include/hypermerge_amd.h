@@ -93,8 +93,9 @@ typedef struct {
     uint32_t n_regs;      /* registers = interned (obj, key) pairs; for lists key = elemId */
     uint32_t n_objs;      /* interned object ids, 0 = ROOT '00000000-0000-0000-0000-000000000000' */
     uint16_t n_actors;    /* actor ranks 0..n_actors-1 (rank = order of the actor id strings) */
-    uint16_t flags;       /* reserved, 0 */
+    uint16_t flags;       /* HM_DOC_* bits set by the encoder */
 } hm_doc_row;
+#define HM_DOC_HAS_LISTS 1u   /* the doc creates a list/text object (launch sizing hint only) */
 
 /* One row per change (24 B), in the order the changes are handed over. */
 typedef struct {
@@ -134,6 +135,8 @@ typedef struct {
     /* per-document maxima over the batch (launch sizing hints); 0 = unknown,
      * computed by the engine from the doc table */
     uint32_t max_changes, max_ops, max_regs, max_objs;
+    uint32_t doc_flags;   /* OR of every docs[d].flags (launch hint; 0 when unknown -> computed) */
+    uint32_t pad;
     const hm_doc_row    *docs;
     const hm_change_row *changes;
     const hm_dep_row    *deps;

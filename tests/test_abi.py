@@ -37,7 +37,7 @@ def test_abi_version_and_messages():
 
 def test_struct_layouts_match_header():
     from hypermerge_amd import columnar as C
-    assert ctypes.sizeof(C.CBatch) == 10 * 4 + 5 * 8
+    assert ctypes.sizeof(C.CBatch) == 12 * 4 + 5 * 8
     assert ctypes.sizeof(C.CResults) == 8 * 8
 
 

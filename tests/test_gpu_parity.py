@@ -51,6 +51,8 @@ def assert_same(b, g, o, allow_unsupported=False):
     ("C2", 4000, {"arrival": 2, "shuffle_pct": 25}),       # out-of-order delivery
     ("C2", 2000, {"del_pct": 20}),
     ("C4", 2000, {"actors": 3, "changes_per_actor": 20}),
+    ("C5", 4000, {}),                                      # nested maps + lists, blocked + duplicate changes
+    ("C5", 2000, {"arrival": 1, "dup_pct": 0}),
 ])
 def test_synthetic_parity(engine, name, n, extra):
     b = synth.generate(synth.config(name, n_docs=n, **extra))
@@ -79,8 +81,7 @@ def test_full_size_c4_properties(engine):
 def test_known_answers_on_gpu(engine, name, changes, expect):
     b = encode([changes])
     g, o = engine.merge(b), O.merge(b)
-    if g.docs["status"][0] == 16:
-        pytest.skip("outside the small-document envelope (lists/RGA)")
+    assert g.docs["status"][0] != 16, "outside the engine envelope"
     assert canonical_json(b, g, 0) == canonical_json(b, o, 0)
 
 
