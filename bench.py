@@ -81,7 +81,7 @@ def main() -> int:
     nr = int(batch.docs["n_regs"].sum())
     d_docs, d_ch, d_dp, d_op = (to_dev(x) for x in (batch.docs, batch.changes, batch.deps, batch.ops))
     u8 = dict(dtype=torch.uint8, device=dev)
-    r_docs = torch.zeros(nd * 32, **u8)
+    r_docs = torch.zeros(nd * 32, **u8)   # hm_doc_result rows
     r_clock = torch.zeros(nd * S, dtype=torch.int32, device=dev)
     r_bclock = torch.zeros(nd * S, dtype=torch.int32, device=dev)
     r_heads = torch.zeros(nd * S, dtype=torch.int32, device=dev)

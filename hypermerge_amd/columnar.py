@@ -44,9 +44,9 @@ STATUS = {0: "OK", 1: "INCONSISTENT_SEQ", 2: "UNKNOWN_OBJECT", 3: "DUPLICATE_OBJ
           4: "DUPLICATE_ELEM", 5: "MISSING_ELEM", 16: "UNSUPPORTED", 32: "INVALID",
           33: "DEVICE", 34: "NOMEM"}
 
-DOC_DT = np.dtype([("change_off", "<u4"), ("n_changes", "<u4"), ("op_off", "<u4"),
-                   ("n_ops", "<u4"), ("reg_off", "<u4"), ("n_regs", "<u4"),
-                   ("n_objs", "<u4"), ("n_actors", "<u2"), ("flags", "<u2")])
+DOC_DT = np.dtype([("change_off", "<u4"), ("n_changes", "<u4"), ("dep_off", "<u4"), ("n_deps", "<u4"),
+                   ("op_off", "<u4"), ("n_ops", "<u4"), ("reg_off", "<u4"), ("n_regs", "<u4"),
+                   ("n_objs", "<u4"), ("n_actors", "<u2"), ("flags", "<u2"), ("reserved", "<u4", (2,))])
 CHANGE_DT = np.dtype([("actor", "<u2"), ("n_deps", "<u2"), ("seq", "<u4"), ("dep_off", "<u4"),
                       ("n_ops", "<u4"), ("op_first", "<u4"), ("content_id", "<u4")])
 DEP_DT = np.dtype([("actor", "<u2"), ("pad", "<u2"), ("seq", "<u4")])
@@ -59,7 +59,7 @@ DOC_RESULT_DT = np.dtype([("status", "<i4"), ("err_change", "<u4"), ("err_op", "
 REG_RESULT_DT = np.dtype([("n_surv", "<u4"), ("surv_off", "<u4"), ("list_index", "<i4"),
                           ("obj", "<u4")])
 SURV_RESULT_DT = np.dtype([("op", "<u4"), ("vtag", "<u4"), ("value", "<u8")])
-assert DOC_DT.itemsize == 32 and CHANGE_DT.itemsize == 24 and DEP_DT.itemsize == 8
+assert DOC_DT.itemsize == 48 and CHANGE_DT.itemsize == 24 and DEP_DT.itemsize == 8
 assert OP_DT.itemsize == 32 and DOC_RESULT_DT.itemsize == 32
 assert REG_RESULT_DT.itemsize == 16 and SURV_RESULT_DT.itemsize == 16
 
@@ -249,7 +249,7 @@ class BatchBuilder:
                 reg_list.append((o, key))
             return regs[(o, key)]
 
-        change_off, op_off = len(self._changes), len(self._ops)
+        change_off, op_off, dep_off0 = len(self._changes), len(self._ops), len(self._deps)
         for c in changes:
             a = rank[c["actor"]]
             deps = c.get("deps") or {}
@@ -282,9 +282,9 @@ class BatchBuilder:
                                   op_first, self._content[ck]))
         n_regs = len(reg_list)
         has_lists = any(o[4] in (MAKE_LIST, MAKE_TEXT) for o in self._ops[op_off:])
-        self._docs.append((change_off, len(changes), op_off, len(self._ops) - op_off,
-                           self._reg_off, n_regs, len(obj_list), len(ranked),
-                           DOC_HAS_LISTS if has_lists else 0))
+        self._docs.append((change_off, len(changes), dep_off0, len(self._deps) - dep_off0,
+                           op_off, len(self._ops) - op_off, self._reg_off, n_regs, len(obj_list), len(ranked),
+                           DOC_HAS_LISTS if has_lists else 0, (0, 0)))
         self._reg_off += n_regs
         self._max_actors = max(self._max_actors, len(ranked))
         self._doc_actors.append(ranked)

@@ -36,6 +36,12 @@
 #include "../../include/hypermerge_amd.h"
 #include "merge_kernels.h"
 
+#ifndef HM_ABLATE
+#define HM_ABLATE 0     // dev-only timing builds: 1 skip ancestor push, 2 stop after K1, 4 stop after K2 survivors
+#endif
+#ifndef HM_WAVES_PER_EU
+#define HM_WAVES_PER_EU 5   // occupancy target for the register allocator (93 VGPRs, no spills)
+#endif
 #define WAVE 64
 #define NA_MAX 8
 #define NDEP_MAX 512
@@ -82,12 +88,13 @@ __device__ __forceinline__ u64 err_key(uint32_t h, uint32_t op_plus1, uint32_t a
 }
 
 struct SmallLds {
-    LDS u64 *anc, *chain, *segor, *survabs, *errkey, *opval;
+    LDS u64 *anc, *chain, *segor, *survabs, *errkey;
+    LDS hm_op_row *ops;             // the document's op rows, staged from the prefetch registers
     LDS int64_t *survsum;
     LDS uint32_t *first, *base, *bclock, *headv, *objslot, *segcnt, *survcnt, *regoff, *regobj, *insmin;
-    LDS uint32_t *flags, *deps, *opmeta, *segoff, *segfill, *seglist, *survp;
+    LDS uint32_t *flags, *deps, *segoff, *segfill, *seglist, *survp;
     LDS int32_t *hist_of;
-    LDS uint16_t *survtmp, *survop, *opbase, *opreg;
+    LDS uint16_t *survtmp, *survop, *opbase;
     LDS uint8_t *h2a, *chactor, *opchg, *objtype;
     // K3 (RGA lists); carved only for launches with list documents
     LDS uint32_t *nins, *pcount, *poff, *pfill, *nodekey, *tour0, *tour1, *listbase;
@@ -100,16 +107,15 @@ __host__ __device__ inline size_t small_carve(P base, uint32_t NOp, uint32_t NR,
     size_t o = 0;
 #define TAKE(f, T, cnt) do { L->f = (decltype(L->f))(base + o); o = (o + (size_t)(cnt) * sizeof(T) + 15) & ~(size_t)15; } while (0)
     TAKE(anc, u64, 64);          TAKE(chain, u64, NA_MAX);     TAKE(segor, u64, NR);
-    TAKE(survabs, u64, NOp);     TAKE(errkey, u64, 1);         TAKE(opval, u64, NOp);
+    TAKE(survabs, u64, NOp);     TAKE(errkey, u64, 1);         TAKE(ops, hm_op_row, NOp);
     TAKE(survsum, int64_t, NOp);
     TAKE(first, uint32_t, NA_MAX * 64); TAKE(base, uint32_t, NA_MAX * 3);
     TAKE(objslot, uint32_t, NO); TAKE(segcnt, uint32_t, NR);   TAKE(survcnt, uint32_t, NR);
     TAKE(regoff, uint32_t, NR);  TAKE(regobj, uint32_t, NR);   TAKE(insmin, uint32_t, NR);
-    TAKE(flags, uint32_t, 1);    TAKE(deps, uint32_t, NDEP_MAX); TAKE(opmeta, uint32_t, NOp);
+    TAKE(flags, uint32_t, 1);    TAKE(deps, uint32_t, NDEP_MAX);
     TAKE(segoff, uint32_t, NR);  TAKE(segfill, uint32_t, NR);  TAKE(seglist, uint32_t, NOp);
     TAKE(survp, uint32_t, NOp);  TAKE(hist_of, int32_t, 64);
     TAKE(survtmp, uint16_t, NOp); TAKE(survop, uint16_t, NOp); TAKE(opbase, uint16_t, 64);
-    TAKE(opreg, uint16_t, NOp);
     TAKE(h2a, uint8_t, 64);      TAKE(chactor, uint8_t, 64);   TAKE(opchg, uint8_t, NOp);
     TAKE(objtype, uint8_t, NO);
     if (lists) {
@@ -142,10 +148,6 @@ __device__ __forceinline__ void need_set(uint32_t &lo, uint32_t &hi, uint32_t a,
     else       { const uint32_t cur = (hi >> sh) & 0xFF; if (v > cur) hi = (hi & ~(0xFFu << sh)) | (v << sh); }
 }
 
-// opmeta layout: action | datatype << 8 | vtag << 16 | applied << 24
-__device__ __forceinline__ uint32_t meta_action(uint32_t m) { return m & 0xFF; }
-__device__ __forceinline__ uint32_t meta_dtype(uint32_t m) { return (m >> 8) & 0xFF; }
-__device__ __forceinline__ uint32_t meta_vtag(uint32_t m) { return (m >> 16) & 0xFF; }
 
 // tie order key of an assign at position p on its register: odd p first (p descending),
 // then even p ascending ("append, then reverse" after every assign)
@@ -228,7 +230,7 @@ __device__ __forceinline__ void rga_order(const SmallLds &L, uint32_t R, uint32_
     // Euler tour: down(i) = 2i (value 1), up(i) = 2i+1; list head h = N + listid: 2h, 2h+1 (end)
     const uint32_t E = 2 * (N + nl);
     for (uint32_t i = lane; i < N; i += WAVE) {
-        const uint32_t reg = L.opreg[L.nodeop[i]];
+        const uint32_t reg = L.ops[L.nodeop[i]].reg;
         const uint32_t hd = N + L.listid[L.regobj[reg]];
         const uint32_t f = L.fc[reg];
         const uint32_t sd = f != 0xFFFFu ? 2 * f : 2 * i + 1;
@@ -268,7 +270,7 @@ __device__ __forceinline__ void rga_order(const SmallLds &L, uint32_t R, uint32_
     }
     wave_sync();
     for (uint32_t i = lane; i < N; i += WAVE) {
-        const uint32_t reg = L.opreg[L.nodeop[i]];
+        const uint32_t reg = L.ops[L.nodeop[i]].reg;
         const uint32_t l = L.listid[L.regobj[reg]];
         const uint32_t total = cur[2 * (N + l)] & 0xFFFFu;
         const uint32_t pos = L.listbase[l] + total - (cur[2 * i] & 0xFFFFu);
@@ -287,7 +289,7 @@ __device__ __forceinline__ void rga_order(const SmallLds &L, uint32_t R, uint32_
     }
     wave_sync();
     for (uint32_t i = lane; i < N; i += WAVE) {
-        const uint32_t reg = L.opreg[L.nodeop[i]];
+        const uint32_t reg = L.ops[L.nodeop[i]].reg;
         const uint32_t pos = L.nodekey[i];
         if (L.seglist[pos]) {
             const uint32_t l = L.listid[L.regobj[reg]];
@@ -298,30 +300,89 @@ __device__ __forceinline__ void rga_order(const SmallLds &L, uint32_t R, uint32_
     wave_sync();
 }
 
-// Merge one document with the whole wave.  Every return is wave-uniform.
-template <int OPL, bool LISTS>
-__device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const SmallLds &L, uint32_t d,
-                                                   const hm_doc_row &doc) {
-    constexpr uint32_t NOp = WAVE * OPL;
-    const uint32_t lane = threadIdx.x;
-    const uint32_t S = p.a_stride;
-    const uint32_t n = doc.n_changes, A = doc.n_actors, m = doc.n_ops, R = doc.n_regs, O = doc.n_objs;
-    hm_doc_result *dres = p.res_docs + d;
 
-    // ---------------- K1: load changes (lane = arrival index) ----------------
+// FC(h)[x]: latest seq of actor x among change h's ancestors and itself (cold merge)
+__device__ __forceinline__ uint32_t fc_of(const SmallLds &L, uint32_t h, uint32_t x) {
+    return (uint32_t)__popcll((L.anc[h] | (1ull << h)) & L.chain[x]);
+}
+// history position of the applied change (a, s) (s >= 1, in this batch)
+__device__ __forceinline__ uint32_t hpos_of(const SmallLds &L, uint32_t a, uint32_t s) {
+    return (uint32_t)L.hist_of[L.first[a * 64 + (s - L.base[a])]];
+}
+// Does the literal transitiveDeps fold differ from the closure for this change?
+__device__ __noinline__ bool fold_differs(const SmallLds &L, uint32_t dep0, uint32_t nd, uint32_t actor, uint32_t seq) {
+    // entries of deps.set(actor, seq-1) in key order, seq 0 skipped (reduce ignores them)
+    uint32_t ex[NA_MAX + 1], es[NA_MAX + 1], eh[NA_MAX + 1], k = 0;
+    bool own = false;
+    for (uint32_t j = 0; j < nd && k < NA_MAX; j++) {
+        const uint32_t pk = L.deps[dep0 + j];
+        uint32_t a = pk >> 24, sq = pk & 0xFFFFFF;
+        if (a == actor) { sq = seq - 1; own = true; }
+        if (sq == 0) continue;
+        ex[k] = a; es[k] = sq; eh[k] = hpos_of(L, a, sq); k++;
+    }
+    if (!own && seq > 1) { ex[k] = actor; es[k] = seq - 1; eh[k] = hpos_of(L, actor, seq - 1); k++; }
+    for (uint32_t j = 0; j < k; j++) {
+        uint32_t before = 0, after = 0;
+        for (uint32_t i = 0; i < k; i++) {
+            if (i == j) continue;
+            const uint32_t f = fc_of(L, eh[i], ex[j]);
+            if (i < j) before = before > f ? before : f; else after = after > f ? after : f;
+        }
+        if (before > (es[j] > after ? es[j] : after)) return true;
+    }
+    return false;
+}
+
+// Rows of the NEXT document, loaded into registers before the current document's
+// output stores (loads and stores share vmcnt on CDNA: loads issued first are not
+// held up by the stores), then staged to LDS at the top of the next iteration.
+template <int OPL>
+struct Prefetch {
+    hm_change_row c;          // lane < n_changes
+    hm_op_row op[OPL];        // lane + 64 t < n_ops
+    hm_dep_row dp[2];         // lane + 64 t < n_deps (the rest, if any, is loaded on use)
+};
+template <int OPL>
+__device__ __forceinline__ void prefetch_doc(const SmallParams &p, const hm_doc_row &doc, Prefetch<OPL> &pf) {
+    const uint32_t lane = threadIdx.x;
+    if (lane < doc.n_changes) pf.c = p.changes[doc.change_off + lane];
+#pragma unroll
+    for (int t = 0; t < OPL; t++)
+        if (lane + WAVE * t < doc.n_ops) pf.op[t] = p.ops[doc.op_off + lane + WAVE * t];
+#pragma unroll
+    for (int t = 0; t < 2; t++)
+        if (lane + WAVE * t < doc.n_deps) pf.dp[t] = p.deps[doc.dep_off + lane + WAVE * t];
+}
+// what the output phase needs besides LDS
+struct DocState {
+    int32_t hist;             // per arrival lane
+    uint32_t H, total;
+    bool doc_lists;
+};
+
+// Merge one document with the whole wave (no global stores).  Every return is wave-uniform.
+template <int OPL, bool LISTS>
+__device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const SmallLds &L, const hm_doc_row &doc,
+                                                   const Prefetch<OPL> &pf, DocState &st) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t n = doc.n_changes, A = doc.n_actors, m = doc.n_ops, R = doc.n_regs, O = doc.n_objs;
+    st.hist = -1; st.H = 0; st.total = 0; st.doc_lists = false;
+
+    // ---------------- stage the prefetched rows (lane = arrival index) ----------------
     const bool act = lane < n;
     hm_change_row c = {};
-    if (act) c = p.changes[doc.change_off + lane];
+    if (act) c = pf.c;
     for (uint32_t i = lane; i < NA_MAX * 64; i += WAVE) L.first[i] = 0xFFFFFFFFu;
     if (lane < NA_MAX) { L.base[lane] = 0xFFFFFFFFu; L.bclock[lane] = 0; L.headv[lane] = 0; L.chain[lane] = 0; }
     if (lane == 0) { *L.errkey = ~0ull; *L.flags = 0; }
-    // the document's deps are one contiguous range: stage it in LDS with coalesced loads
-    const uint32_t dep_lo = n ? (uint32_t)__builtin_amdgcn_readlane((int)c.dep_off, 0) : 0;
-    const uint32_t dep_hi = n ? (uint32_t)__builtin_amdgcn_readlane((int)(c.dep_off + c.n_deps), (int)(n - 1)) : 0;
-    const uint32_t ndep = dep_hi - dep_lo;
-    if (n && (dep_hi < dep_lo || ndep > NDEP_MAX)) return OUT_UNSUPPORTED;
+#pragma unroll
+    for (int t = 0; t < OPL; t++)
+        if (lane + WAVE * t < m) L.ops[lane + WAVE * t] = pf.op[t];
+    const uint32_t dep_lo = doc.dep_off, ndep = doc.n_deps;
+    if (ndep > NDEP_MAX) return OUT_UNSUPPORTED;
     for (uint32_t i = lane; i < ndep; i += WAVE) {
-        const hm_dep_row dp = p.deps[dep_lo + i];
+        const hm_dep_row dp = i < 2 * WAVE ? pf.dp[i >= WAVE ? 1 : 0] : p.deps[dep_lo + i];
         L.deps[i] = (dp.seq < (1u << 24) && dp.actor < 256) ? (((uint32_t)dp.actor << 24) | dp.seq) : 0xFFFFFFFFu;
     }
     wave_sync();
@@ -356,11 +417,13 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     u64 dmask = 0;                       // direct deps in arrival-index space (fast path)
     uint32_t pred_arr = 0xFFu;
     bool ok = true;                      // ready on arrival
+    bool own_row = false;                // the deps map lists the change's own actor
     if (act) {
         for (uint32_t j = 0; j < c.n_deps; j++) {
             const uint32_t pk = L.deps[my_dep0 + j];
             const uint32_t a = pk >> 24, s = pk & 0xFFFFFF;
             if (pk == 0xFFFFFFFFu || a >= A) { lds_or(L.flags, FL_UNSUPPORTED); continue; }
+            if (a == actor) own_row = true;
             if (a == actor || s == 0) continue;                // deps.set(actor, seq-1) overrides
             const uint32_t b = L.base[a];
             if (b == 0xFFFFFFFFu || s < b || s - b >= 64) { need_set(need_lo, need_hi, a, 0x7F); ok = false; continue; }
@@ -465,7 +528,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     const uint32_t hactor = shfl32(actor, (int)ai);
     const uint32_t hseq = shfl32(seq, (int)ai);
     const uint32_t hpred = shfl32(pred_arr, (int)ai);
-    u64 D = 0, Dnp = 0;                                   // direct deps; without the own predecessor
+    u64 D = 0, Dnp = 0;                                   // direct deps (history space); without own pred
     if (hv) {
         u64 x = dm_arr;
         while (x) {
@@ -476,10 +539,11 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
             if (j != hpred) Dnp |= bit;
         }
     }
-    u64 anc = 0;
-    for (uint32_t k = 0; k < H; k++) {                    // lane k is final when the push reaches it
-        const u64 ak = readlane64(anc, (int)k) | (1ull << k);
-        if ((D >> k) & 1) anc |= ak;
+    u64 anc = 0, covered = 0;                             // covered = union of all ancestor sets
+    for (uint32_t k = 0; k < ((HM_ABLATE & 1) ? 0u : H); k++) {   // lane k is final when the push reaches it
+        const u64 ak = readlane64(anc, (int)k);
+        covered |= ak;
+        if ((D >> k) & 1) anc |= ak | (1ull << k);
     }
     if (hv) L.anc[lane] = anc;
     for (uint32_t a = 0; a < A; a++) {
@@ -487,24 +551,24 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         if (lane == 0) L.chain[a] = ch;
     }
     wave_sync();
-    // transitiveDeps folds the deps map in key order with `.set(actor, seq)`: that equals
-    // the closure unless one listed dep is an ancestor of another (never for heads deps).
-    if (hv && Dnp) {
-        bool bad = false;
+    // transitiveDeps folds deps.set(actor, seq-1) in key order: acc = max(acc, FC(d)); acc[a_d] = s_d.
+    // The `.set` can LOWER acc[a_d] when an earlier entry already knows a later change of a_d;
+    // compare that literal fold with the closure and leave the envelope only when they differ.
+    // Necessary condition (cheap): a listed non-own dep is an ancestor of another listed
+    // non-own dep, or the own actor appears as a deps key (then seq-1 is folded in place).
+    bool suspect = false;
+    if (hv && (Dnp & (Dnp - 1))) {
         u64 x = Dnp;
         while (x) {
-            const uint32_t j = (uint32_t)__builtin_ctzll(x);
+            const uint32_t i2 = (uint32_t)__builtin_ctzll(x);
             x &= x - 1;
-            u64 y = D & ~(1ull << j);
-            while (y) {
-                const uint32_t i2 = (uint32_t)__builtin_ctzll(y);
-                y &= y - 1;
-                if ((L.anc[i2] >> j) & 1) bad = true;
-            }
+            if (L.anc[i2] & Dnp) suspect = true;
         }
-        if (bad) lds_or(L.flags, FL_UNSUPPORTED);
     }
-    const u64 covered = wave_or64(hv ? anc : 0);
+    const uint32_t h_own_row = shfl32(own_row ? 1u : 0u, (int)ai);     // all lanes: bpermute sources
+    const uint32_t h_dep0 = shfl32(my_dep0, (int)ai), h_nd = shfl32(c.n_deps, (int)ai);
+    suspect |= hv && h_own_row != 0;
+    if (suspect && fold_differs(L, h_dep0, h_nd, hactor, hseq)) lds_or(L.flags, FL_UNSUPPORTED);
     if (hv && !((covered >> lane) & 1)) L.headv[hactor] = hseq;     // opSet.deps
     for (uint32_t i = lane; i < O; i += WAVE) { L.objslot[i] = i == 0 ? 0u : 0xFFFFFFFFu; L.objtype[i] = i == 0 ? HM_MAKE_MAP : 0xFF; }
     for (uint32_t i = lane; i < R; i += WAVE) {
@@ -512,6 +576,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     }
     wave_sync();
 
+    if (HM_ABLATE & 2) return OUT_UNSUPPORTED;
     // ---------------- K2: ops (lane + 64*t) ----------------
     uint32_t oreg[OPL], oobj[OPL], opar[OPL], oact[OPL], okey[OPL], oarr[OPL], oelem[OPL];
     int32_t oh[OPL];
@@ -520,16 +585,12 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         const uint32_t k = lane + WAVE * t;
         oh[t] = -1; okey[t] = 0; oarr[t] = 0; oreg[t] = 0; oobj[t] = 0; opar[t] = 0; oact[t] = 0xFF; oelem[t] = 0;
         if (k < m) {
-            const hm_op_row o = p.ops[doc.op_off + k];
+            const hm_op_row o = L.ops[k];
             const uint32_t ch = L.opchg[k];
             oarr[t] = ch; oh[t] = L.hist_of[ch];
             oreg[t] = o.reg; oobj[t] = o.obj; opar[t] = o.parent; oact[t] = o.action; oelem[t] = o.elem;
             if (o.action == HM_INS && o.elem >= (1u << 24)) lds_or(L.flags, FL_UNSUPPORTED);
             okey[t] = ((uint32_t)(oh[t] < 0 ? 0 : oh[t]) << 16) | (k - L.opbase[ch]);
-            L.opmeta[k] = (uint32_t)o.action | ((uint32_t)o.datatype << 8) | ((uint32_t)o.vtag << 16) |
-                          ((oh[t] >= 0 ? 1u : 0u) << 24);
-            L.opval[k] = o.value;
-            L.opreg[k] = (uint16_t)(o.reg < 0xFFFFu ? o.reg : 0xFFFFu);
             if (oh[t] >= 0) {
                 const uint32_t a = o.action;
                 if (a <= HM_MAKE_TEXT) {
@@ -598,6 +659,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     if (*L.errkey != ~0ull) return OUT_ERROR;                    // the first throw wins
     if (*L.flags & FL_UNSUPPORTED) return OUT_UNSUPPORTED;
 
+    if (HM_ABLATE & 4) return OUT_UNSUPPORTED;
     // survivor offsets: exclusive scan over register ids
     uint32_t total = 0;
     for (uint32_t r0 = 0; r0 < R; r0 += WAVE) {
@@ -694,13 +756,12 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         const uint32_t k = lane + WAVE * t;
         const uint32_t reg = oreg[t], b0 = L.regoff[reg], cnt = L.survcnt[reg];
         const u64 an = L.anc[oh[t]];
-        const uint32_t my_vtag = meta_vtag(L.opmeta[k]);
-        const int64_t v = (int64_t)L.opval[k];
+        const uint32_t my_vtag = L.ops[k].vtag;
+        const int64_t v = (int64_t)L.ops[k].value;
         for (uint32_t q = 0; q < cnt; q++) {
             const uint32_t k2 = L.survop[b0 + q];
-            const uint32_t m2 = L.opmeta[k2];
-            const uint32_t vt2 = meta_vtag(m2);
-            if (meta_action(m2) != HM_SET || meta_dtype(m2) != HM_DT_COUNTER || (vt2 != HM_V_INT && vt2 != HM_V_FLOAT)) continue;
+            const uint32_t vt2 = L.ops[k2].vtag;
+            if (L.ops[k2].action != HM_SET || L.ops[k2].datatype != HM_DT_COUNTER || (vt2 != HM_V_INT && vt2 != HM_V_FLOAT)) continue;
             if (!((an >> L.hist_of[L.opchg[k2]]) & 1)) continue;
             if (vt2 != HM_V_INT || my_vtag != HM_V_INT) { float_counter = true; continue; }
             lds_add((LDS u64 *)&L.survsum[b0 + q], (unsigned long long)v);
@@ -711,24 +772,62 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     wave_sync();
     if (*L.flags & FL_UNSUPPORTED) return OUT_UNSUPPORTED;
 
-    // ---------------- outputs ----------------
+    // JS numbers: an integer counter is exact only while |base| + sum|inc| <= 2^53
     bool inexact = false;
     for (uint32_t q = lane; q < total; q += WAVE) {
-        const uint32_t k = L.survop[q], mt = L.opmeta[k];
-        hm_surv_result sr;
-        sr.op = k; sr.vtag = meta_vtag(mt); sr.value = L.opval[k];
-        if (meta_action(mt) == HM_SET && meta_dtype(mt) == HM_DT_COUNTER && sr.vtag == HM_V_INT) {
-            const int64_t b = (int64_t)sr.value;
-            inexact |= L.survabs[q] + (u64)(b < 0 ? -b : b) > (1ull << 53);   // JS number exactness
-            sr.value = (u64)(b + L.survsum[q]);
+        const hm_op_row &o = L.ops[L.survop[q]];
+        if (o.action == HM_SET && o.datatype == HM_DT_COUNTER && o.vtag == HM_V_INT) {
+            const int64_t b = (int64_t)o.value;
+            inexact |= L.survabs[q] + (u64)(b < 0 ? -b : b) > (1ull << 53);
         }
-        p.res_surv[doc.op_off + q] = sr;
     }
     if (__ballot(inexact)) return OUT_UNSUPPORTED;
+    st.hist = hist; st.H = H; st.total = total; st.doc_lists = doc_lists;
+    return OUT_OK;
+}
+
+// Output phase of one document (all reads from LDS; coalesced stores).
+template <bool LISTS>
+__device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallLds &L, uint32_t d,
+                                              const hm_doc_row &doc, Outcome oc, const DocState &st) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t S = p.a_stride;
+    const uint32_t n = doc.n_changes, A = doc.n_actors, R = doc.n_regs;
+    hm_doc_result *dres = p.res_docs + d;
+    if (oc == OUT_ERROR) {
+        // an Automerge throw aborted this document's Backend.applyChanges
+        const u64 ek = *L.errkey;
+        if (lane == 0) {
+            hm_doc_result r = {};
+            r.status = (int32_t)(ek & 0xFF);
+            r.err_change = (uint32_t)((ek >> 8) & 0xFFFF);
+            const uint32_t opp1 = (uint32_t)((ek >> 24) & 0xFFFF);
+            r.err_op = opp1 ? opp1 - 1 : HM_NONE;
+            *dres = r;
+        }
+        return;
+    }
+    if (oc == OUT_UNSUPPORTED) {
+        if (lane == 0) {
+            hm_doc_result r = {};
+            r.status = HM_ERR_UNSUPPORTED; r.err_change = HM_NONE; r.err_op = HM_NONE;
+            *dres = r;
+        }
+        return;
+    }
+    for (uint32_t q = lane; q < st.total; q += WAVE) {
+        const uint32_t k = L.survop[q];
+        const hm_op_row &o = L.ops[k];
+        hm_surv_result sr;
+        sr.op = k; sr.vtag = o.vtag; sr.value = o.value;
+        if (o.action == HM_SET && o.datatype == HM_DT_COUNTER && o.vtag == HM_V_INT)
+            sr.value = (u64)((int64_t)o.value + L.survsum[q]);
+        p.res_surv[doc.op_off + q] = sr;
+    }
     for (uint32_t r = lane; r < R; r += WAVE) {
         hm_reg_result rr;
         rr.n_surv = L.survcnt[r]; rr.surv_off = L.regoff[r]; rr.obj = L.regobj[r];
-        rr.list_index = (LISTS && doc_lists) ? (int32_t)L.insmin[r] : -1;
+        rr.list_index = (LISTS && st.doc_lists) ? (int32_t)L.insmin[r] : -1;
         p.res_regs[doc.reg_off + r] = rr;
     }
     // allDeps rows, coalesced: word w = (change w/S, actor w%S)
@@ -750,49 +849,46 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     }
     const bool aGTE = __ballot(lane < S && bc < mc) == 0;
     const bool bGTE = __ballot(lane < S && mc < bc) == 0;
-    const u64 q = __ballot(act && hist == -1);
-    if (act) p.res_hist[doc.change_off + lane] = hist;
+    const bool act = lane < n;
+    const u64 q = __ballot(act && st.hist == -1);
+    if (act) p.res_hist[doc.change_off + lane] = st.hist;
     if (lane == 0) {
         hm_doc_result r = {};
         r.status = HM_OK; r.err_change = HM_NONE; r.err_op = HM_NONE;
-        r.hist_len = H; r.n_queued = (uint32_t)__popcll(q); r.n_surv = total;
+        r.hist_len = st.H; r.n_queued = (uint32_t)__popcll(q); r.n_surv = st.total;
         r.min_cmp = p.min_clock ? ((aGTE && bGTE) ? 0u : (aGTE ? 1u : (bGTE ? 2u : 3u))) : 0u;
         *dres = r;
     }
-    return OUT_OK;
 }
 
 template <int OPL, bool LISTS>
-__global__ __launch_bounds__(WAVE) void merge_small_kernel(SmallParams p) {
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(HM_WAVES_PER_EU)))
+void merge_small_kernel(SmallParams p) {
     extern __shared__ __align__(16) uint8_t lds_raw[];
     SmallLds L;
     small_carve((LDS uint8_t *)lds_raw, WAVE * OPL, p.cap_regs, p.cap_objs, LISTS, &L);
-    const uint32_t lane = threadIdx.x;
-    for (uint32_t d = blockIdx.x; d < p.n_docs; d += gridDim.x) {
-        const hm_doc_row doc = p.docs[d];
+    uint32_t d = blockIdx.x;
+    if (d >= p.n_docs) return;
+    hm_doc_row doc = p.docs[d];
+    Prefetch<OPL> pf;
+    prefetch_doc<OPL>(p, doc, pf);
+    for (;;) {
+        // software pipeline over this wave's documents: the next row is read now, its
+        // change/op/dep rows are issued before this document's stores
+        const uint32_t dn = d + gridDim.x;
+        const bool more = dn < p.n_docs;
+        hm_doc_row docn = {};
+        if (more) docn = p.docs[dn];
         const bool in_env = doc.n_changes <= 64 && doc.n_actors <= NA_MAX && doc.n_ops <= WAVE * OPL &&
                             doc.n_regs <= p.cap_regs && doc.n_objs <= p.cap_objs && doc.n_objs >= 1;
-        const Outcome oc = in_env ? merge_doc_small<OPL, LISTS>(p, L, d, doc) : OUT_UNSUPPORTED;
-        hm_doc_result *dres = p.res_docs + d;
-        if (oc == OUT_ERROR) {
-            // an Automerge throw aborted this document's Backend.applyChanges
-            const u64 ek = *L.errkey;
-            if (lane == 0) {
-                hm_doc_result r = {};
-                r.status = (int32_t)(ek & 0xFF);
-                r.err_change = (uint32_t)((ek >> 8) & 0xFFFF);
-                const uint32_t opp1 = (uint32_t)((ek >> 24) & 0xFFFF);
-                r.err_op = opp1 ? opp1 - 1 : HM_NONE;
-                *dres = r;
-            }
-        } else if (oc == OUT_UNSUPPORTED) {
-            if (lane == 0) {
-                hm_doc_result r = {};
-                r.status = HM_ERR_UNSUPPORTED; r.err_change = HM_NONE; r.err_op = HM_NONE;
-                *dres = r;
-            }
-        }
+        DocState st;
+        const Outcome oc = in_env ? merge_doc_small<OPL, LISTS>(p, L, doc, pf, st) : OUT_UNSUPPORTED;
+        if (more) prefetch_doc<OPL>(p, docn, pf);
+        write_outputs<LISTS>(p, L, d, doc, oc, st);
         wave_sync();
+        if (!more) break;
+        d = dn;
+        doc = docn;
     }
 }
 

@@ -485,7 +485,9 @@ void *hm_synth_generate(const hm_synth_config *cfg) {
     for (auto &p : parts)
         for (auto &d : p) {
             hm_doc_row row;
+            memset(&row, 0, sizeof(row));
             row.change_off = (uint32_t)o->ch.size(); row.n_changes = (uint32_t)d.ch.size();
+            row.dep_off = (uint32_t)o->dp.size(); row.n_deps = (uint32_t)d.dp.size();
             row.op_off = (uint32_t)o->op.size(); row.n_ops = (uint32_t)d.op.size();
             row.reg_off = (uint32_t)o->n_regs; row.n_regs = d.n_regs; row.n_objs = d.n_objs;
             row.n_actors = (uint16_t)d.n_actors; row.flags = (uint16_t)d.flags;

@@ -15,7 +15,7 @@ import numpy as np
 from .columnar import Batch, Results, CBatch, CResults
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(_HERE, "_lib", "libhmgpu.so")
+LIB = os.environ.get("HMGPU_LIB") or os.path.join(_HERE, "_lib", "libhmgpu.so")
 
 # every symbol include/hypermerge_amd.h declares
 EXPORTS = ("hm_abi_version", "hm_status_message", "hm_engine_create", "hm_engine_destroy",

@@ -83,10 +83,13 @@ enum {
 /* Columnar batch tables                                               */
 /* ------------------------------------------------------------------ */
 
-/* One row per document (32 B). */
+/* One row per document (48 B).  Every input range of a document is in its row,
+ * so all of a document's loads can be issued as soon as the row is read. */
 typedef struct {
     uint32_t change_off;  /* first row of this doc in changes[] */
     uint32_t n_changes;   /* changes handed to applyChanges, in array (arrival) order */
+    uint32_t dep_off;     /* first row of this doc in deps[] (= changes[change_off].dep_off) */
+    uint32_t n_deps;      /* dep rows of all its changes (contiguous) */
     uint32_t op_off;      /* first row of this doc in ops[]; ops are grouped by change, in op order */
     uint32_t n_ops;
     uint32_t reg_off;     /* first row of this doc in the per-register output table */
@@ -94,6 +97,7 @@ typedef struct {
     uint32_t n_objs;      /* interned object ids, 0 = ROOT '00000000-0000-0000-0000-000000000000' */
     uint16_t n_actors;    /* actor ranks 0..n_actors-1 (rank = order of the actor id strings) */
     uint16_t flags;       /* HM_DOC_* bits set by the encoder */
+    uint32_t reserved[2];
 } hm_doc_row;
 #define HM_DOC_HAS_LISTS 1u   /* the doc creates a list/text object (launch sizing hint only) */
 
