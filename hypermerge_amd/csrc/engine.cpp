@@ -15,6 +15,7 @@
 
 struct hm_engine {
     int device = 0;
+    int flags = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[4] = {};
     float last_ms[2] = {0, 0};
@@ -23,6 +24,8 @@ struct hm_engine {
     std::string err;
     void *dbuf = nullptr;
     size_t dbuf_size = 0;
+    void *pool = nullptr;        // merge_large_kernel scratch + deferred-document list
+    size_t pool_size = 0;
 };
 
 namespace {
@@ -63,7 +66,23 @@ int launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, hipStream
     p.res_docs = o->docs; p.res_clock = o->clock; p.res_back_clock = o->back_clock; p.res_heads = o->heads;
     p.res_hist = o->hist; p.res_all_deps = o->all_deps; p.res_regs = o->regs; p.res_surv = o->surv;
     p.n_docs = b->n_docs; p.a_stride = b->a_stride; p.cap_regs = c.regs; p.cap_objs = c.objs;
+    p.general_only = (e->flags & HM_CFG_GENERAL_ONLY) ? 1u : 0u;
     if (b->n_docs == 0) { e->n_last = 0; return HM_OK; }
+    // scratch: [counters 256 B][deferred list n_docs u32][large-kernel pool]
+    const size_t list_bytes = ((size_t)b->n_docs * 4 + 255) & ~(size_t)255;
+    const size_t pool_bytes = hm_large_scratch_bound(b);
+    const size_t need = 256 + list_bytes + pool_bytes;
+    if (need > e->pool_size) {
+        if (e->pool) { HIPCHK(e, hipStreamSynchronize(s)); HIPCHK(e, hipFree(e->pool)); }
+        e->pool = nullptr; e->pool_size = 0;
+        if (hipMalloc(&e->pool, need) != hipSuccess) return fail(e, HM_ERR_NOMEM, "hipMalloc scratch pool");
+        e->pool_size = need;
+    }
+    char *pb = (char *)e->pool;
+    p.defer_count = (uint32_t *)pb;
+    p.defer_list = (uint32_t *)(pb + 256);
+    unsigned long long *pool_used = (unsigned long long *)(pb + 8);
+    HIPCHK(e, hipMemsetAsync(pb, 0, 16, s));
     // persistent grid: enough resident 1-wave workgroups to fill every CU
     size_t lds = hm_small_lds_bytes(c.opl, c.regs, c.objs, c.lists);
     uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, (160 * 1024) / std::max<size_t>(lds, 1)));
@@ -72,7 +91,11 @@ int launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, hipStream
     hipError_t r = hm_launch_small(p, c.opl, c.lists, grid, s);
     if (r != hipSuccess) return hip_fail(e, r, "merge_small_kernel launch");
     HIPCHK(e, hipEventRecord(e->ev[1], s));
-    e->n_last = 1;
+    HIPCHK(e, hipEventRecord(e->ev[2], s));
+    r = hm_launch_large(p, pb + 256 + list_bytes, pool_bytes, pool_used, (uint32_t)e->num_cus * 4, s);
+    if (r != hipSuccess) return hip_fail(e, r, "merge_large_kernel launch");
+    HIPCHK(e, hipEventRecord(e->ev[3], s));
+    e->n_last = 2;
     return HM_OK;
 }
 
@@ -110,6 +133,7 @@ int hm_engine_create(const hm_config *cfg, hm_engine **out) {
     hm_engine *e = new (std::nothrow) hm_engine();
     if (!e) return HM_ERR_NOMEM;
     e->device = cfg ? cfg->device : 0;
+    e->flags = cfg ? cfg->flags : 0;
     int n = 0;
     hipError_t r = hipGetDeviceCount(&n);
     if (r != hipSuccess || n <= e->device) { delete e; return HM_ERR_DEVICE; }
@@ -125,10 +149,11 @@ int hm_engine_create(const hm_config *cfg, hm_engine **out) {
 
 void hm_engine_destroy(hm_engine *e) {
     if (!e) return;
-    hipSetDevice(e->device);
-    if (e->dbuf) hipFree(e->dbuf);
-    for (auto &ev : e->ev) if (ev) hipEventDestroy(ev);
-    if (e->stream) hipStreamDestroy(e->stream);
+    (void)hipSetDevice(e->device);
+    if (e->dbuf) (void)hipFree(e->dbuf);
+    if (e->pool) (void)hipFree(e->pool);
+    for (auto &ev : e->ev) if (ev) (void)hipEventDestroy(ev);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
 }
 
@@ -177,7 +202,7 @@ int hm_merge_host(hm_engine *e, const hm_batch *hb, const hm_results *ho) {
         size_t off[13], total = 0;
         for (int i = 0; i < 13; i++) { off[i] = total; total += al(sz[i] ? sz[i] : 1); }
         if (total > e->dbuf_size) {
-            if (e->dbuf) hipFree(e->dbuf);
+            if (e->dbuf) (void)hipFree(e->dbuf);
             e->dbuf = nullptr; e->dbuf_size = 0;
             if (hipMalloc(&e->dbuf, total) != hipSuccess) return fail(e, HM_ERR_NOMEM, "hipMalloc staging");
             e->dbuf_size = total;

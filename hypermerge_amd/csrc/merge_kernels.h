@@ -17,8 +17,17 @@ struct SmallParams {
     hm_surv_result *res_surv;
     uint32_t n_docs, a_stride;
     uint32_t cap_regs, cap_objs;     // LDS carve of this launch
+    uint32_t *defer_list;            // documents handed to merge_large_kernel
+    uint32_t *defer_count;
+    uint32_t general_only;           // HM_CFG_GENERAL_ONLY: defer every document
 };
 
+// internal: the small kernel hands a document to merge_large_kernel (never returned to callers)
+#define HM_DEFERRED 0x7FFFFFFF
+
+size_t hm_large_scratch_bound(const hm_batch *b);
+hipError_t hm_launch_large(const SmallParams &p, void *pool, size_t pool_bytes, unsigned long long *pool_used,
+                           uint32_t grid, hipStream_t s);
 size_t hm_small_lds_bytes(uint32_t opl, uint32_t cap_regs, uint32_t cap_objs, bool lists);
 hipError_t hm_launch_small(const SmallParams &p, uint32_t opl, bool lists, uint32_t grid, hipStream_t s);
 // which: 0 cmp (out uint8_t*), 1 union, 2 intersection (out uint32_t*)

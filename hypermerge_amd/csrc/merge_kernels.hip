@@ -808,10 +808,12 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
         return;
     }
     if (oc == OUT_UNSUPPORTED) {
+        // outside this kernel's envelope: merge_large_kernel takes the document
         if (lane == 0) {
             hm_doc_result r = {};
-            r.status = HM_ERR_UNSUPPORTED; r.err_change = HM_NONE; r.err_op = HM_NONE;
+            r.status = HM_DEFERRED; r.err_change = HM_NONE; r.err_op = HM_NONE;
             *dres = r;
+            p.defer_list[atomicAdd(p.defer_count, 1u)] = d;
         }
         return;
     }
@@ -880,7 +882,8 @@ void merge_small_kernel(SmallParams p) {
         hm_doc_row docn = {};
         if (more) docn = p.docs[dn];
         const bool in_env = doc.n_changes <= 64 && doc.n_actors <= NA_MAX && doc.n_ops <= WAVE * OPL &&
-                            doc.n_regs <= p.cap_regs && doc.n_objs <= p.cap_objs && doc.n_objs >= 1;
+                            doc.n_regs <= p.cap_regs && doc.n_objs <= p.cap_objs && doc.n_objs >= 1 &&
+                            !p.general_only;
         DocState st;
         const Outcome oc = in_env ? merge_doc_small<OPL, LISTS>(p, L, doc, pf, st) : OUT_UNSUPPORTED;
         if (more) prefetch_doc<OPL>(p, docn, pf);

@@ -1,0 +1,648 @@
+// merge_large.hip — the general merge kernel: one 256-thread workgroup per document,
+// for documents outside merge_small_kernel's envelope (more than 64 changes, more
+// than 8 actors, long op lists, big lists/texts).  Per-document working arrays live
+// in a device scratch pool (bump-allocated by each workgroup); small tables in LDS.
+//
+// Same reference semantics as merge_kernels.hip (Automerge
+// 0.12.2-beta.0 backend/op_set.js, not vendored — yarn.lock:178-185), computed so
+// that long documents parallelise over their changes/ops:
+//   L1  first-arrival table per (actor, seq) -> fast path (every change ready on
+//       arrival: history = arrival order minus duplicates, one block scan) or the exact
+//       queue-pass emulation (wave 0; readiness of 64 queued changes per ballot).
+//   L2  allDeps by the LITERAL transitiveDeps fold in history order (lanes = actors):
+//       acc = max(acc, allDeps(d) + {d}); acc[actor_d] = seq_d, deps in key order.
+//   L3  registers: survivors = set/link ops o with max_{x} allDeps(x)[actor_o] < seq_o
+//       over the register's set/del/link ops x (per-register x per-actor atomicMax);
+//       order, ties and counters as in the small kernel.
+//   L4  RGA order: Euler tour of the insertion tree + pointer jumping (block-wide).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/hypermerge_amd.h"
+#include "merge_kernels.h"
+
+#define LWG 256
+#define LA_MAX 32
+typedef unsigned long long u64;
+
+namespace hml {
+
+__device__ __forceinline__ void bsync() { __syncthreads(); }
+// order one lane's global writes before the wave's next reads (wave-uniform sections)
+__device__ __forceinline__ void wfence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+
+// error key: history position (20 b) | op index + 1 (16 b) | arrival index (20 b) | code (8 b)
+__device__ __forceinline__ u64 err_key(uint32_t h, uint32_t op_plus1, uint32_t arr, uint32_t code) {
+    return ((u64)(h & 0xFFFFF) << 44) | ((u64)(op_plus1 & 0xFFFF) << 28) | ((u64)(arr & 0xFFFFF) << 8) | code;
+}
+
+struct Shared {
+    uint32_t base[LA_MAX], maxs[LA_MAX], tabo[LA_MAX + 1], clock[LA_MAX], bclock[LA_MAX], headv[LA_MAX];
+    uint32_t maxad[LA_MAX];
+    uint32_t flags, all_ok, H, nins, nl, total, lists;
+    u64 errkey;
+    uint32_t scan[LWG / 64 + 1];
+    u64 scratch_base;
+};
+
+enum : uint32_t { LF_UNSUPPORTED = 1u, LF_NOPOOL = 2u };
+
+// exclusive scan of v over the block; returns the prefix, *total = block sum
+__device__ __forceinline__ uint32_t block_excl_scan(Shared &sh, uint32_t v, uint32_t *total) {
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane >= (uint32_t)o ? lane - o : lane) << 2), (int)x);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) sh.scan[w] = x;
+    bsync();
+    uint32_t off = 0, tot = 0;
+    for (uint32_t i = 0; i < LWG / 64; i++) { if (i < w) off += sh.scan[i]; tot += sh.scan[i]; }
+    bsync();
+    *total = tot;
+    return off + x - v;
+}
+// exclusive scan of arr[0..N) in place (chunks of LWG)
+__device__ void scan_array(Shared &sh, uint32_t *arr, uint32_t N, uint32_t *total) {
+    uint32_t carry = 0;
+    for (uint32_t c0 = 0; c0 < N; c0 += LWG) {
+        const uint32_t i = c0 + threadIdx.x;
+        const uint32_t v = i < N ? arr[i] : 0;
+        uint32_t t;
+        const uint32_t ex = block_excl_scan(sh, v, &t);
+        if (i < N) arr[i] = carry + ex;
+        carry += t;
+    }
+    *total = carry;
+    bsync();
+}
+
+struct Scratch {
+    uint32_t *tab, *h2a, *opchg, *segmax, *segcnt, *survcnt, *regoff, *regobj, *segoff, *segfill;
+    uint32_t *survtmp, *survop, *survp, *objtype, *listid, *nodeop, *nodepi, *regnode, *pcount, *poff;
+    uint32_t *pfill, *plist, *fc, *ns, *tour0, *tour1, *tval0, *tval1, *listbase, *pos, *vis;
+    int32_t *hist;
+    u64 *opkey, *insmin, *objslot, *seglist, *nodekey, *survabs;
+    int64_t *survsum;
+};
+
+__host__ __device__ inline size_t large_carve(uintptr_t base, uint32_t n, uint32_t m, uint32_t R, uint32_t O,
+                                              uint32_t A, uint32_t T, Scratch *S) {
+    size_t o = 0;
+    const uint32_t NP = R + O, NE = 2 * (m + O);
+#define TK(f, T_, cnt) do { S->f = (T_ *)(base + o); o = (o + (size_t)(cnt) * sizeof(T_) + 15) & ~(size_t)15; } while (0)
+    TK(opkey, u64, m); TK(insmin, u64, R); TK(objslot, u64, O); TK(seglist, u64, m); TK(nodekey, u64, m);
+    TK(survabs, u64, m); TK(survsum, int64_t, m);
+    TK(tab, uint32_t, T); TK(h2a, uint32_t, n); TK(hist, int32_t, n); TK(opchg, uint32_t, m);
+    TK(segmax, uint32_t, (size_t)R * A); TK(segcnt, uint32_t, R); TK(survcnt, uint32_t, R);
+    TK(regoff, uint32_t, R); TK(regobj, uint32_t, R); TK(segoff, uint32_t, R); TK(segfill, uint32_t, R);
+    TK(survtmp, uint32_t, m); TK(survop, uint32_t, m); TK(survp, uint32_t, m); TK(objtype, uint32_t, O);
+    TK(listid, uint32_t, O); TK(nodeop, uint32_t, m); TK(nodepi, uint32_t, m); TK(regnode, uint32_t, R);
+    TK(pcount, uint32_t, NP); TK(poff, uint32_t, NP); TK(pfill, uint32_t, NP); TK(plist, uint32_t, m);
+    TK(fc, uint32_t, NP); TK(ns, uint32_t, m); TK(tour0, uint32_t, NE); TK(tour1, uint32_t, NE);
+    TK(tval0, uint32_t, NE); TK(tval1, uint32_t, NE);
+    TK(listbase, uint32_t, O + 1); TK(pos, uint32_t, m); TK(vis, uint32_t, m);
+#undef TK
+    return o;
+}
+
+enum Outcome { LOK = 0, LERR = 1, LUNSUP = 2 };
+
+// allDeps row of the applied change at arrival index ci (global, written in history order)
+__device__ __forceinline__ uint32_t *ad_row(const SmallParams &p, const hm_doc_row &doc, uint32_t ci) {
+    return p.res_all_deps + ((size_t)doc.change_off + ci) * p.a_stride;
+}
+
+__device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, const hm_doc_row &doc, uint32_t d,
+                                   uint8_t *pool, u64 pool_bytes, u64 *pool_used, int32_t &H_out) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t n = doc.n_changes, A = doc.n_actors, m = doc.n_ops, R = doc.n_regs, O = doc.n_objs;
+    const uint32_t S = p.a_stride;
+    const hm_change_row *CH = p.changes + doc.change_off;
+    const hm_op_row *OP = p.ops + doc.op_off;
+    if (A > LA_MAX || O < 1 || n >= (1u << 20) || m >= (1u << 24)) return LUNSUP;
+
+    // ---- per-actor seq ranges -> first-arrival table size ----
+    if (tid < LA_MAX) { sh.base[tid] = 0xFFFFFFFFu; sh.maxs[tid] = 0; sh.clock[tid] = 0; sh.bclock[tid] = 0;
+                        sh.headv[tid] = 0; sh.maxad[tid] = 0; }
+    if (tid == 0) { sh.flags = 0; sh.errkey = ~0ull; sh.all_ok = 1; sh.H = 0; sh.nins = 0; sh.total = 0; sh.lists = 0; }
+    bsync();
+    for (uint32_t i = tid; i < n; i += LWG) {
+        const hm_change_row c = CH[i];
+        if (c.actor >= A || c.seq == 0 || c.op_first < doc.op_off || c.op_first - doc.op_off + c.n_ops > m ||
+            c.dep_off < doc.dep_off || c.dep_off - doc.dep_off + c.n_deps > doc.n_deps)
+            atomicOr(&sh.flags, LF_UNSUPPORTED);
+        else { atomicMin(&sh.base[c.actor], c.seq); atomicMax(&sh.maxs[c.actor], c.seq); atomicMax(&sh.bclock[c.actor], c.seq); }
+    }
+    bsync();
+    if (sh.flags) return LUNSUP;
+    if (tid == 0) {
+        uint32_t t = 0;
+        for (uint32_t a = 0; a < A; a++) { sh.tabo[a] = t; if (sh.maxs[a]) t += sh.maxs[a] - sh.base[a] + 1; }
+        sh.tabo[A] = t;
+        if (t > 4 * n + 64) sh.flags |= LF_UNSUPPORTED;    // sparse seqs: leave the envelope
+        // scratch for this document
+        Scratch tmp;
+        const size_t need = large_carve(0, n, m, R, O, A, t, &tmp);
+        const u64 at = atomicAdd(pool_used, (u64)need);
+        if (at + need > pool_bytes) sh.flags |= LF_NOPOOL;
+        sh.scratch_base = (u64)(uintptr_t)(pool + at);
+    }
+    bsync();
+    if (sh.flags) return LUNSUP;
+    const uint32_t T = sh.tabo[A];
+    Scratch X;
+    large_carve((uintptr_t)sh.scratch_base, n, m, R, O, A, T, &X);
+    for (uint32_t i = tid; i < T; i += LWG) X.tab[i] = 0xFFFFFFFFu;
+    bsync();
+    auto slot_of = [&](uint32_t a, uint32_t s) -> uint32_t {     // table index of (a, s) or NONE
+        if (a >= A || s < sh.base[a] || s > sh.maxs[a] || sh.maxs[a] == 0) return 0xFFFFFFFFu;
+        return sh.tabo[a] + (s - sh.base[a]);
+    };
+    for (uint32_t i = tid; i < n; i += LWG) { const hm_change_row c = CH[i]; atomicMin(&X.tab[slot_of(c.actor, c.seq)], i); }
+    for (uint32_t i = tid; i < n; i += LWG) {
+        const hm_change_row c = CH[i];
+        for (uint32_t j = 0; j < c.n_ops; j++) X.opchg[c.op_first - doc.op_off + j] = i;
+    }
+    bsync();
+    // ---- L1 fast path: every dependency arrived earlier ----
+    uint32_t ndup_local = 0;
+    for (uint32_t i = tid; i < n; i += LWG) {
+        const hm_change_row c = CH[i];
+        bool ok = true;
+        for (uint32_t j = 0; j < c.n_deps; j++) {
+            const hm_dep_row dp = p.deps[c.dep_off + j];
+            if (dp.actor >= A) { atomicOr(&sh.flags, LF_UNSUPPORTED); continue; }
+            if (dp.actor == c.actor || dp.seq == 0) continue;
+            const uint32_t sl = slot_of(dp.actor, dp.seq);
+            if (sl == 0xFFFFFFFFu || X.tab[sl] >= i) ok = false;
+        }
+        if (c.seq > 1) { const uint32_t sl = slot_of(c.actor, c.seq - 1); if (sl == 0xFFFFFFFFu || X.tab[sl] >= i) ok = false; }
+        const uint32_t f = X.tab[slot_of(c.actor, c.seq)];
+        if (f != i && CH[f].content_id != c.content_id) ok = false;   // mismatched duplicate: exact path
+        if (!ok) sh.all_ok = 0;
+    }
+    bsync();
+    if (sh.flags) return LUNSUP;
+    if (sh.all_ok) {
+        // history = arrival order minus duplicates (block scan of non-duplicate flags)
+        uint32_t carry = 0;
+        for (uint32_t c0 = 0; c0 < n; c0 += LWG) {
+            const uint32_t i = c0 + tid;
+            bool app = false;
+            if (i < n) { const hm_change_row c = CH[i]; app = X.tab[slot_of(c.actor, c.seq)] == i; }
+            uint32_t tot;
+            const uint32_t ex = block_excl_scan(sh, app ? 1u : 0u, &tot);
+            if (i < n) { X.hist[i] = app ? (int32_t)(carry + ex) : -2; if (app) X.h2a[carry + ex] = i; }
+            carry += tot;
+        }
+        if (tid == 0) sh.H = carry;
+        (void)ndup_local;
+    } else if (wave == 0) {
+        // ---- exact emulation of addChange / applyQueuedOps; wave 0, wave-uniform control ----
+        // hist: -3 not arrived, -1 queued, -2 duplicate (no-op), >= 0 history position
+        for (uint32_t i = lane; i < T; i += 64) X.tab[i] = 0xFFFFFFFFu;       // -> applied arrival index
+        for (uint32_t i = lane; i < n; i += 64) X.hist[i] = -3;
+        wfence();
+        uint32_t H = 0;
+        bool stop = false;
+        // causallyReady: every (a, s) of deps.set(actor, seq-1) has clock[a] >= s
+        auto ready = [&](uint32_t i) -> bool {
+            const hm_change_row c = CH[i];
+            for (uint32_t j = 0; j < c.n_deps; j++) {
+                const hm_dep_row dp = p.deps[c.dep_off + j];
+                if (dp.actor == c.actor) continue;
+                if (sh.clock[dp.actor] < dp.seq) return false;
+            }
+            return sh.clock[c.actor] >= c.seq - 1;
+        };
+        auto apply = [&](uint32_t j) {                     // applyChange, wave-uniform j
+            const hm_change_row c = CH[j];
+            const uint32_t sl = slot_of(c.actor, c.seq);
+            if (c.seq <= sh.clock[c.actor]) {              // already applied: must be identical
+                const uint32_t k = X.tab[sl];
+                if (lane == 0) X.hist[j] = -2;
+                if (CH[k].content_id != c.content_id) {
+                    if (lane == 0) atomicMin(&sh.errkey, err_key(H, 0, j, HM_ERR_INCONSISTENT_SEQ));
+                    stop = true;
+                }
+            } else {
+                if (lane == 0) { sh.clock[c.actor] = c.seq; X.tab[sl] = j; X.hist[j] = (int32_t)H; X.h2a[H] = j; }
+                H++;
+            }
+            wfence();
+        };
+        // first queued + ready change at index >= cursor (among arrived changes <= i)
+        auto find_ready = [&](uint32_t cursor, uint32_t i) -> uint32_t {
+            for (uint32_t q0 = cursor; q0 <= i; q0 += 64) {
+                const uint32_t q = q0 + lane;
+                const bool cand = q <= i && X.hist[q] == -1 && ready(q);
+                const u64 bm = __ballot(cand);
+                if (bm) return q0 + (uint32_t)__builtin_ctzll(bm);
+            }
+            return 0xFFFFFFFFu;
+        };
+        for (uint32_t i = 0; i < n && !stop; i++) {
+            if (lane == 0) X.hist[i] = -1;                 // queue.push(change)
+            wfence();
+            if (!ready(i)) continue;                       // pass 1: only the new change can be ready
+            apply(i);
+            while (!stop) {                                // further passes until one applies nothing
+                bool progress = false;
+                uint32_t cursor = 0;
+                for (;;) {
+                    const uint32_t j = find_ready(cursor, i);
+                    if (j == 0xFFFFFFFFu) break;
+                    apply(j);
+                    progress = true;
+                    cursor = j + 1;
+                    if (stop) break;
+                }
+                if (!progress) break;
+            }
+        }
+        for (uint32_t i = lane; i < n; i += 64) if (X.hist[i] == -3) X.hist[i] = -1;
+        if (lane == 0) sh.H = H;
+    }
+    bsync();
+    const uint32_t H = sh.H;
+    H_out = (int32_t)H;
+
+    // ---- L2: allDeps by the literal fold, history order, lanes = actors (wave 0) ----
+    if (wave == 0) {
+        for (uint32_t h = 0; h < H; h++) {
+            const uint32_t ci = X.h2a[h];
+            const hm_change_row c = CH[ci];
+            uint32_t acc = 0;
+            auto fold = [&](uint32_t a, uint32_t s) {
+                if (s == 0) return;
+                const uint32_t dc = X.tab[slot_of(a, s)];          // the applied change (a, s)
+                const uint32_t t = lane < A ? ad_row(p, doc, dc)[lane] : 0;
+                acc = acc > t ? acc : t;
+                if (lane == a) acc = s;
+            };
+            bool own = false;
+            for (uint32_t j = 0; j < c.n_deps; j++) {
+                const hm_dep_row dp = p.deps[c.dep_off + j];
+                if (dp.actor == c.actor) { own = true; fold(c.actor, c.seq - 1); }
+                else fold(dp.actor, dp.seq);
+            }
+            if (!own) fold(c.actor, c.seq - 1);
+            if (lane < S) ad_row(p, doc, ci)[lane] = lane < A ? acc : 0;
+            if (lane < A) sh.maxad[lane] = sh.maxad[lane] > acc ? sh.maxad[lane] : acc;
+            wfence();                                          // rows are re-read by later changes
+        }
+        // rows of unapplied changes are zero
+        for (uint32_t i = lane; i < n; i += 64)
+            if (X.hist[i] < 0) for (uint32_t a = 0; a < S; a++) ad_row(p, doc, i)[a] = 0;
+    }
+    bsync();
+    // clock / heads: a head survives unless some applied change's allDeps reaches it
+    for (uint32_t h = tid; h < H; h += LWG) {
+        const hm_change_row c = CH[X.h2a[h]];
+        atomicMax(&sh.clock[c.actor], c.seq);
+    }
+    bsync();
+    if (tid < A && sh.clock[tid] && sh.maxad[tid] < sh.clock[tid]) sh.headv[tid] = sh.clock[tid];
+
+    // ---- L3: ops ----
+    for (uint32_t i = tid; i < O; i += LWG) { X.objslot[i] = i == 0 ? 0ull : ~0ull; X.objtype[i] = i == 0 ? HM_MAKE_MAP : 0xFFu; }
+    for (uint32_t i = tid; i < R; i += LWG) {
+        X.segcnt[i] = 0; X.survcnt[i] = 0; X.insmin[i] = ~0ull; X.regobj[i] = HM_NONE; X.segfill[i] = 0;
+        for (uint32_t a = 0; a < A; a++) X.segmax[(size_t)i * A + a] = 0;
+    }
+    bsync();
+    for (uint32_t k = tid; k < m; k += LWG) {
+        const hm_op_row o = OP[k];
+        const uint32_t ci = X.opchg[k];
+        const int32_t h = X.hist[ci];
+        X.opkey[k] = h >= 0 ? (((u64)h << 32) | (k - (CH[ci].op_first - doc.op_off))) : ~0ull;
+        if (h < 0) continue;
+        const u64 key = X.opkey[k];
+        if (o.action <= HM_MAKE_TEXT) {
+            if (o.obj >= O) atomicOr(&sh.flags, LF_UNSUPPORTED); else atomicMin(&X.objslot[o.obj], key + 1);
+        } else if (o.action <= HM_INC) {
+            if (o.reg >= R || (o.action == HM_INS && o.parent != HM_HEAD && o.parent >= R)) { atomicOr(&sh.flags, LF_UNSUPPORTED); continue; }
+            if (o.obj >= O) continue;
+            X.regobj[o.reg] = o.obj;
+            if (o.action == HM_INS) { atomicMin(&X.insmin[o.reg], key + 1); if (o.elem >= (1u << 24)) atomicOr(&sh.flags, LF_UNSUPPORTED); }
+            else {
+                atomicAdd(&X.segcnt[o.reg], 1u);
+                if (o.action != HM_INC) {
+                    const uint32_t *ad = ad_row(p, doc, ci);
+                    for (uint32_t a = 0; a < A; a++) atomicMax(&X.segmax[(size_t)o.reg * A + a], ad[a]);
+                }
+            }
+        } else atomicOr(&sh.flags, LF_UNSUPPORTED);
+    }
+    bsync();
+    if (sh.flags) return LUNSUP;
+    for (uint32_t k = tid; k < m; k += LWG) {
+        const hm_op_row o = OP[k];
+        const u64 key = X.opkey[k];
+        if (key == ~0ull || o.action > HM_MAKE_TEXT || o.obj >= O) continue;
+        const uint32_t ci = X.opchg[k];
+        if (X.objslot[o.obj] != key + 1)
+            atomicMin(&sh.errkey, err_key((uint32_t)(key >> 32), (uint32_t)key + 1, ci, HM_ERR_DUPLICATE_OBJECT));
+        else X.objtype[o.obj] = o.action;
+    }
+    bsync();
+    bool any_list = false;
+    for (uint32_t k = tid; k < m; k += LWG) {
+        const hm_op_row o = OP[k];
+        const u64 key = X.opkey[k];
+        X.survp[k] = 0xFFFFFFFFu;                             // survivor slot (or none)
+        if (key == ~0ull || o.action < HM_INS || o.action > HM_INC || o.reg >= R) continue;
+        const uint32_t ci = X.opchg[k];
+        const u64 os = o.obj < O ? X.objslot[o.obj] : ~0ull;
+        if (os == ~0ull || os > key) {
+            atomicMin(&sh.errkey, err_key((uint32_t)(key >> 32), (uint32_t)key + 1, ci, HM_ERR_UNKNOWN_OBJECT));
+            continue;
+        }
+        const uint32_t ot = X.objtype[o.obj];
+        const bool is_list = ot == HM_MAKE_LIST || ot == HM_MAKE_TEXT;
+        if (o.action == HM_INS) {
+            any_list = true;
+            if (X.insmin[o.reg] != key + 1)
+                atomicMin(&sh.errkey, err_key((uint32_t)(key >> 32), (uint32_t)key + 1, ci, HM_ERR_DUPLICATE_ELEM));
+            if (o.parent != HM_HEAD && !(X.insmin[o.parent] <= key)) atomicOr(&sh.flags, LF_UNSUPPORTED);
+            continue;
+        }
+        any_list |= is_list;
+        if (o.action == HM_SET || o.action == HM_LINK) {
+            if (is_list && !(X.insmin[o.reg] <= key))
+                atomicMin(&sh.errkey, err_key((uint32_t)(key >> 32), (uint32_t)key + 1, ci, HM_ERR_MISSING_ELEM));
+            const hm_change_row c = CH[ci];
+            if (X.segmax[(size_t)o.reg * A + c.actor] < c.seq) X.survp[k] = atomicAdd(&X.survcnt[o.reg], 1u);
+        }
+    }
+    if (any_list) sh.lists = 1;
+    bsync();
+    const bool lists_flag = sh.lists != 0;
+    if (sh.errkey != ~0ull) return LERR;
+    if (sh.flags) return LUNSUP;
+    // survivor offsets
+    for (uint32_t i = tid; i < R; i += LWG) X.regoff[i] = X.survcnt[i];
+    bsync();
+    uint32_t total;
+    scan_array(sh, X.regoff, R, &total);
+    if (tid == 0) sh.total = total;
+    for (uint32_t k = tid; k < m; k += LWG)
+        if (X.survp[k] != 0xFFFFFFFFu) X.survtmp[X.regoff[OP[k].reg] + X.survp[k]] = k;
+    // per-register assign lists (for tie positions)
+    for (uint32_t i = tid; i < R; i += LWG) X.segoff[i] = X.segcnt[i];
+    bsync();
+    uint32_t tot2;
+    scan_array(sh, X.segoff, R, &tot2);
+    for (uint32_t k = tid; k < m; k += LWG) {
+        const hm_op_row o = OP[k];
+        if (X.opkey[k] == ~0ull || o.action < HM_SET || o.action > HM_INC || o.reg >= R) continue;
+        X.seglist[X.segoff[o.reg] + atomicAdd(&X.segfill[o.reg], 1u)] = X.opkey[k];
+    }
+    bsync();
+    // ranks: actor descending; ties (one change) by the sortBy(actor).reverse() flip
+    for (uint32_t k = tid; k < m; k += LWG) {
+        if (X.survp[k] == 0xFFFFFFFFu) continue;
+        const hm_op_row o = OP[k];
+        const uint32_t my_a = CH[X.opchg[k]].actor;
+        const uint32_t b0 = X.regoff[o.reg], cnt = X.survcnt[o.reg];
+        const bool odd_n = X.segcnt[o.reg] & 1;
+        auto tkey = [&](uint32_t kk) -> uint32_t {
+            uint32_t pc = 0;
+            const u64 key = X.opkey[kk];
+            for (uint32_t q = 0; q < X.segcnt[o.reg]; q++) pc += X.seglist[X.segoff[o.reg] + q] < key ? 1u : 0u;
+            return (pc & 1) ? (0x80000000u - pc) : (0x80000000u + pc);
+        };
+        uint32_t rank = 0, my_t = 0;
+        bool have_t = false;
+        for (uint32_t q = 0; q < cnt; q++) {
+            const uint32_t k2 = X.survtmp[b0 + q];
+            if (k2 == k) continue;
+            const uint32_t a2 = CH[X.opchg[k2]].actor;
+            if (a2 > my_a) rank++;
+            else if (a2 == my_a) {
+                if (!have_t) { my_t = tkey(k); have_t = true; }
+                const uint32_t t2 = tkey(k2);
+                if (odd_n ? (t2 > my_t) : (t2 < my_t)) rank++;
+            }
+        }
+        X.survop[b0 + rank] = k;
+        X.survsum[b0 + rank] = 0;
+        X.survabs[b0 + rank] = 0;
+    }
+    bsync();
+    // counters
+    for (uint32_t k = tid; k < m; k += LWG) {
+        const hm_op_row o = OP[k];
+        if (X.opkey[k] == ~0ull || o.action != HM_INC || o.reg >= R) continue;
+        const uint32_t *adi = ad_row(p, doc, X.opchg[k]);
+        const uint32_t b0 = X.regoff[o.reg], cnt = X.survcnt[o.reg];
+        for (uint32_t q = 0; q < cnt; q++) {
+            const uint32_t k2 = X.survop[b0 + q];
+            const hm_op_row o2 = OP[k2];
+            if (o2.action != HM_SET || o2.datatype != HM_DT_COUNTER || (o2.vtag != HM_V_INT && o2.vtag != HM_V_FLOAT)) continue;
+            const hm_change_row c2 = CH[X.opchg[k2]];
+            if (adi[c2.actor] < c2.seq) continue;                 // concurrent inc: no effect
+            if (o2.vtag != HM_V_INT || o.vtag != HM_V_INT) { atomicOr(&sh.flags, LF_UNSUPPORTED); continue; }
+            const int64_t v = (int64_t)o.value;
+            atomicAdd((unsigned long long *)&X.survsum[b0 + q], (unsigned long long)v);
+            atomicAdd((unsigned long long *)&X.survabs[b0 + q], (unsigned long long)(v < 0 ? -v : v));
+        }
+    }
+    bsync();
+    if (sh.flags) return LUNSUP;
+
+    // ---- L4: RGA order ----
+    if (lists_flag) {
+        const uint32_t NP = R + O;
+        for (uint32_t i = tid; i < NP; i += LWG) { X.pcount[i] = 0; X.pfill[i] = 0; X.fc[i] = 0xFFFFFFFFu; }
+        for (uint32_t i = tid; i < R; i += LWG) X.regnode[i] = 0xFFFFFFFFu;
+        for (uint32_t i = tid; i < O; i += LWG) X.listid[i] = (X.objtype[i] == HM_MAKE_LIST || X.objtype[i] == HM_MAKE_TEXT) ? 1u : 0u;
+        bsync();
+        uint32_t nl;
+        scan_array(sh, X.listid, O, &nl);          // exclusive prefix -> compact list id (valid for list objects)
+        for (uint32_t k = tid; k < m; k += LWG) {
+            const hm_op_row o = OP[k];
+            if (X.opkey[k] == ~0ull || o.action != HM_INS) continue;
+            const uint32_t i = atomicAdd(&sh.nins, 1u);
+            const uint32_t pi = o.parent == HM_HEAD ? R + o.obj : o.parent;
+            X.nodeop[i] = k; X.nodepi[i] = pi;
+            X.nodekey[i] = ((u64)o.elem << 8) | CH[X.opchg[k]].actor;
+            X.regnode[o.reg] = i;
+            atomicAdd(&X.pcount[pi], 1u);
+        }
+        bsync();
+        const uint32_t N = sh.nins;
+        for (uint32_t i = tid; i < NP; i += LWG) X.poff[i] = X.pcount[i];
+        bsync();
+        uint32_t tp;
+        scan_array(sh, X.poff, NP, &tp);
+        for (uint32_t i = tid; i < N; i += LWG) { const uint32_t pi = X.nodepi[i]; X.plist[X.poff[pi] + atomicAdd(&X.pfill[pi], 1u)] = i; }
+        bsync();
+        for (uint32_t i = tid; i < N; i += LWG) {
+            const uint32_t pi = X.nodepi[i];
+            const u64 key = X.nodekey[i];
+            uint32_t best = 0xFFFFFFFFu; u64 bkey = 0; bool firstc = true;
+            for (uint32_t q = 0; q < X.pcount[pi]; q++) {
+                const uint32_t j = X.plist[X.poff[pi] + q];
+                const u64 kj = X.nodekey[j];
+                if (kj > key) firstc = false;
+                else if (kj < key && (best == 0xFFFFFFFFu || kj > bkey)) { best = j; bkey = kj; }
+            }
+            X.ns[i] = best;
+            if (firstc) X.fc[pi] = i;
+        }
+        bsync();
+        const uint32_t E = 2 * (N + nl), END = 0xFFFFFFFFu;
+        // tour entries: (next, value) as two arrays packed into u64? keep next in tour0/tour1, values in pos/vis
+        uint32_t *nx0 = X.tour0, *nx1 = X.tour1;
+        uint32_t *va0 = X.tval0, *va1 = X.tval1;
+        for (uint32_t i = tid; i < N; i += LWG) {
+            const hm_op_row o = OP[X.nodeop[i]];
+            const uint32_t hd = N + X.listid[o.obj];
+            const uint32_t f = X.fc[o.reg];
+            const uint32_t pi = X.nodepi[i];
+            nx0[2 * i] = f != 0xFFFFFFFFu ? 2 * f : 2 * i + 1;           va0[2 * i] = 1;
+            nx0[2 * i + 1] = X.ns[i] != 0xFFFFFFFFu ? 2 * X.ns[i] : (pi >= R ? 2 * hd + 1 : 2 * X.regnode[pi] + 1);
+            va0[2 * i + 1] = 0;
+        }
+        for (uint32_t o = tid; o < O; o += LWG) {
+            if (!(X.objtype[o] == HM_MAKE_LIST || X.objtype[o] == HM_MAKE_TEXT)) continue;
+            const uint32_t h = N + X.listid[o], f = X.fc[R + o];
+            nx0[2 * h] = f != 0xFFFFFFFFu ? 2 * f : 2 * h + 1; va0[2 * h] = 0;
+            nx0[2 * h + 1] = END; va0[2 * h + 1] = 0;
+        }
+        bsync();
+        const uint32_t rounds = E ? 32 - __builtin_clz(E) : 0;
+        for (uint32_t rd = 0; rd < rounds; rd++) {
+            for (uint32_t e = tid; e < E; e += LWG) {
+                const uint32_t x = nx0[e];
+                if (x != END) { nx1[e] = nx0[x]; va1[e] = va0[e] + va0[x]; } else { nx1[e] = END; va1[e] = va0[e]; }
+            }
+            bsync();
+            uint32_t *t = nx0; nx0 = nx1; nx1 = t; t = va0; va0 = va1; va1 = t;
+        }
+        for (uint32_t o = tid; o < O; o += LWG) {
+            const bool isl = X.objtype[o] == HM_MAKE_LIST || X.objtype[o] == HM_MAKE_TEXT;
+            if (isl) X.listbase[X.listid[o]] = va0[2 * (N + X.listid[o])];
+        }
+        bsync();
+        uint32_t tl;
+        scan_array(sh, X.listbase, nl, &tl);
+        for (uint32_t i = tid; i < N; i += LWG) {
+            const hm_op_row o = OP[X.nodeop[i]];
+            const uint32_t l = X.listid[o.obj];
+            const uint32_t total_l = va0[2 * (N + l)];
+            const uint32_t ps = X.listbase[l] + total_l - va0[2 * i];
+            X.pos[i] = ps;
+            X.vis[ps] = X.survcnt[o.reg] > 0 ? 1u : 0u;
+            X.insmin[o.reg] = 0xFFFFFFFFull;                     // -> list index or -1
+        }
+        bsync();
+        // exclusive scan of visibility over pre-order positions, kept in survp (free now)
+        for (uint32_t i = tid; i < N; i += LWG) X.survp[i] = X.vis[i];
+        bsync();
+        uint32_t tv;
+        scan_array(sh, X.survp, N, &tv);
+        for (uint32_t i = tid; i < N; i += LWG) {
+            const hm_op_row o = OP[X.nodeop[i]];
+            const uint32_t ps = X.pos[i];
+            if (X.vis[ps]) {
+                const uint32_t l = X.listid[o.obj];
+                X.insmin[o.reg] = X.survp[ps] - X.survp[X.listbase[l]];
+            }
+        }
+        bsync();
+    }
+
+    // ---- outputs ----
+    for (uint32_t q = tid; q < total; q += LWG) {
+        const uint32_t k = X.survop[q];
+        const hm_op_row o = OP[k];
+        hm_surv_result sr; sr.op = k; sr.vtag = o.vtag; sr.value = o.value;
+        if (o.action == HM_SET && o.datatype == HM_DT_COUNTER && o.vtag == HM_V_INT) {
+            const int64_t b = (int64_t)o.value;
+            if (X.survabs[q] + (u64)(b < 0 ? -b : b) > (1ull << 53)) atomicOr(&sh.flags, LF_UNSUPPORTED);
+            sr.value = (u64)(b + X.survsum[q]);
+        }
+        p.res_surv[doc.op_off + q] = sr;
+    }
+    for (uint32_t r = tid; r < R; r += LWG) {
+        hm_reg_result rr;
+        rr.n_surv = X.survcnt[r]; rr.surv_off = X.regoff[r]; rr.obj = X.regobj[r];
+        // list elements carry their visible index (or -1) in insmin after L4
+        rr.list_index = (lists_flag && X.regnode[r] != 0xFFFFFFFFu && X.insmin[r] != 0xFFFFFFFFull) ? (int32_t)X.insmin[r] : -1;
+        p.res_regs[doc.reg_off + r] = rr;
+    }
+    for (uint32_t i = tid; i < n; i += LWG) p.res_hist[doc.change_off + i] = X.hist[i];
+    bsync();
+    if (sh.flags) return LUNSUP;
+    return LOK;
+}
+
+__global__ __launch_bounds__(LWG) void merge_large_kernel(SmallParams p, uint8_t *pool, u64 pool_bytes, u64 *pool_used) {
+    __shared__ Shared sh;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t S = p.a_stride;
+    const uint32_t n_def = *p.defer_count;               // documents the small kernel deferred
+    for (uint32_t di = blockIdx.x; di < n_def; di += gridDim.x) {
+        const uint32_t d = p.defer_list[di];
+        bsync();
+        const hm_doc_row doc = p.docs[d];
+        int32_t H = 0;
+        const Outcome oc = merge_doc_large(p, sh, doc, d, pool, pool_bytes, pool_used, H);
+        bsync();
+        hm_doc_result r = {};
+        r.err_change = HM_NONE; r.err_op = HM_NONE;
+        if (oc == LERR) {
+            const u64 ek = sh.errkey;
+            r.status = (int32_t)(ek & 0xFF);
+            r.err_change = (uint32_t)((ek >> 8) & 0xFFFFF);
+            const uint32_t opp1 = (uint32_t)((ek >> 28) & 0xFFFF);
+            r.err_op = opp1 ? opp1 - 1 : HM_NONE;
+        } else if (oc == LUNSUP) {
+            r.status = HM_ERR_UNSUPPORTED;
+        } else {
+            r.status = HM_OK;
+            r.hist_len = (uint32_t)H;
+            r.n_surv = sh.total;
+            uint32_t q = 0;
+            for (uint32_t i = 0; i < doc.n_changes; i++) q += p.res_hist[doc.change_off + i] == -1 ? 1u : 0u;
+            r.n_queued = q;
+            bool ag = true, bg = true;
+            for (uint32_t a = 0; a < S; a++) {
+                const uint32_t bc = a < doc.n_actors ? sh.bclock[a] : 0u;
+                const uint32_t mc = p.min_clock ? p.min_clock[(size_t)d * S + a] : 0u;
+                if (bc < mc) ag = false;
+                if (mc < bc) bg = false;
+            }
+            r.min_cmp = p.min_clock ? ((ag && bg) ? 0u : (ag ? 1u : (bg ? 2u : 3u))) : 0u;
+        }
+        if (tid < S) {
+            const bool ok = oc == LOK, ar = tid < doc.n_actors;
+            p.res_clock[(size_t)d * S + tid] = ok && ar ? sh.clock[tid] : 0u;
+            p.res_heads[(size_t)d * S + tid] = ok && ar ? sh.headv[tid] : 0u;
+            p.res_back_clock[(size_t)d * S + tid] = ok && ar ? sh.bclock[tid] : 0u;
+        }
+        if (tid == 0) p.res_docs[d] = r;
+        bsync();
+    }
+}
+
+}  // namespace hml
+
+size_t hm_large_scratch_bound(const hm_batch *b) {
+    // linear upper bound of large_carve over every document (T <= 4n + 64 per doc)
+    // (n_objs <= n_ops + 1 per document: objects are created by make ops)
+    hml::Scratch s;
+    const uint32_t A = b->a_stride;
+    size_t per = hml::large_carve(0, b->n_changes, b->n_ops, b->n_regs, b->n_ops + b->n_docs, A,
+                                  4 * b->n_changes + 64 * b->n_docs, &s);
+    return per + (size_t)b->n_docs * 48 * 16 + (1u << 20);
+}
+
+hipError_t hm_launch_large(const SmallParams &p, void *pool, size_t pool_bytes, unsigned long long *pool_used,
+                           uint32_t grid, hipStream_t s) {
+    hipLaunchKernelGGL(hml::merge_large_kernel, dim3(grid), dim3(LWG), 0, s, p, (uint8_t *)pool, (u64)pool_bytes, pool_used);
+    return hipGetLastError();
+}

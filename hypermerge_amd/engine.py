@@ -66,11 +66,14 @@ class _Config(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("flags", ctypes.c_int)]
 
 
+GENERAL_ONLY = 1   # HM_CFG_GENERAL_ONLY
+
+
 class Engine:
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, flags: int = 0):
         L = lib()
         h = ctypes.c_void_p()
-        cfg = _Config(device, 0)
+        cfg = _Config(device, flags)
         st = L.hm_engine_create(ctypes.byref(cfg), ctypes.byref(h))
         if st != 0:
             raise EngineError(f"hm_engine_create failed: {L.hm_status_message(st).decode()}")

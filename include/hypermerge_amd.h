@@ -193,8 +193,9 @@ typedef struct hm_engine hm_engine;
 
 typedef struct {
     int device;           /* HIP device ordinal */
-    int flags;            /* reserved, 0 */
+    int flags;            /* HM_CFG_* */
 } hm_config;
+#define HM_CFG_GENERAL_ONLY 1   /* route every document through the general (workgroup) kernel */
 
 /* Version of the ABI compiled into the library. */
 uint32_t hm_abi_version(void);

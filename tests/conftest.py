@@ -18,3 +18,12 @@ def engine():
     e = Engine(0)
     yield e
     e.close()
+
+
+@pytest.fixture(scope="session")
+def engine_general():
+    """every document through the general (workgroup-per-document) kernel"""
+    from hypermerge_amd.engine import Engine, GENERAL_ONLY
+    e = Engine(0, GENERAL_ONLY)
+    yield e
+    e.close()

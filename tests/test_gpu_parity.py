@@ -59,6 +59,36 @@ def test_synthetic_parity(engine, name, n, extra):
     assert_same(b, engine.merge(b), O.merge(b, threads=8))
 
 
+@pytest.mark.parametrize("name,n,extra", [
+    ("C1", 1, {}),                                         # 1 doc x 10k changes (general kernel)
+    ("C3", 300, {}),                                       # text docs: ~240 changes, ~3.6k ops each
+    ("C3", 60, {"arrival": 2, "shuffle_pct": 20, "dup_pct": 3}),
+    ("C2", 2000, {"dup_pct": 8, "arrival": 2, "shuffle_pct": 20}),   # > 64 changes with duplicates
+    ("C4", 500, {"actors": 12, "changes_per_actor": 10}),  # > 8 actors
+])
+def test_large_documents(engine, name, n, extra):
+    b = synth.generate(synth.config(name, n_docs=n, **extra))
+    assert_same(b, engine.merge(b), O.merge(b, threads=8))
+
+
+@pytest.mark.parametrize("name,n,extra", [
+    ("C4", 3000, {}), ("C2", 3000, {}), ("C5", 2000, {}), ("C4", 1000, {"arrival": 1}),
+    ("C2", 1000, {"arrival": 2, "shuffle_pct": 25, "dup_pct": 5}),
+])
+def test_general_kernel_on_small_docs(engine_general, name, n, extra):
+    """The general kernel alone must agree too (it is the path for long documents)."""
+    b = synth.generate(synth.config(name, n_docs=n, **extra))
+    assert_same(b, engine_general.merge(b), O.merge(b, threads=8))
+
+
+@pytest.mark.parametrize("name,changes,expect", CASES, ids=[c[0] for c in CASES])
+def test_known_answers_general_kernel(engine_general, name, changes, expect):
+    b = encode([changes])
+    g, o = engine_general.merge(b), O.merge(b)
+    assert g.docs["status"][0] != 16, "outside the engine envelope"
+    assert canonical_json(b, g, 0) == canonical_json(b, o, 0)
+
+
 def test_full_size_c4_properties(engine):
     """BASELINE size (1M docs): size-independent properties, no oracle run."""
     b = synth.generate(synth.config("C4", n_docs=1_000_000))
