@@ -91,7 +91,7 @@ def main() -> int:
     r_surv = torch.zeros(no * 16, **u8)
     hc = batch.c_struct()
     cb = CBatch(hc.n_docs, hc.n_changes, hc.n_deps, hc.n_ops, hc.n_regs, hc.a_stride,
-                hc.max_changes, hc.max_ops, hc.max_regs, hc.max_objs, hc.doc_flags, 0,
+                hc.max_changes, hc.max_ops, hc.max_regs, hc.max_objs, hc.doc_flags, hc.max_deps,
                 d_docs.data_ptr(), d_ch.data_ptr(), d_dp.data_ptr(), d_op.data_ptr(), None)
     cr = CResults(r_docs.data_ptr(), r_clock.data_ptr(), r_bclock.data_ptr(), r_heads.data_ptr(),
                   r_hist.data_ptr(), r_ad.data_ptr(), r_regs.data_ptr(), r_surv.data_ptr())

@@ -38,6 +38,7 @@ V_NULL, V_FALSE, V_TRUE, V_INT, V_FLOAT, V_STR, V_OBJ = range(7)
 HEAD = 0xFFFFFFFF
 NONE = 0xFFFFFFFF
 DOC_HAS_LISTS = 1
+DOC_HAS_COUNTERS = 2
 TWO53 = 2 ** 53
 
 STATUS = {0: "OK", 1: "INCONSISTENT_SEQ", 2: "UNKNOWN_OBJECT", 3: "DUPLICATE_OBJECT",
@@ -71,7 +72,7 @@ class CBatch(ctypes.Structure):
                 ("n_regs", ctypes.c_uint32), ("a_stride", ctypes.c_uint32),
                 ("max_changes", ctypes.c_uint32), ("max_ops", ctypes.c_uint32),
                 ("max_regs", ctypes.c_uint32), ("max_objs", ctypes.c_uint32),
-                ("doc_flags", ctypes.c_uint32), ("pad", ctypes.c_uint32),
+                ("doc_flags", ctypes.c_uint32), ("max_deps", ctypes.c_uint32),
                 ("docs", ctypes.c_void_p), ("changes", ctypes.c_void_p),
                 ("deps", ctypes.c_void_p), ("ops", ctypes.c_void_p),
                 ("min_clock", ctypes.c_void_p)]
@@ -141,7 +142,7 @@ class Batch:
         return CBatch(nd, len(self.changes), len(self.deps), len(self.ops),
                       int(self.docs["n_regs"].sum()) if nd else 0, self.a_stride,
                       mx("n_changes"), mx("n_ops"), mx("n_regs"), mx("n_objs"),
-                      int(np.bitwise_or.reduce(self.docs["flags"])) if nd else 0, 0,
+                      int(np.bitwise_or.reduce(self.docs["flags"])) if nd else 0, mx("n_deps"),
                       self.docs.ctypes.data, self.changes.ctypes.data, self.deps.ctypes.data,
                       self.ops.ctypes.data, mc)
 
@@ -282,9 +283,11 @@ class BatchBuilder:
                                   op_first, self._content[ck]))
         n_regs = len(reg_list)
         has_lists = any(o[4] in (MAKE_LIST, MAKE_TEXT) for o in self._ops[op_off:])
+        has_counters = any(o[4] == INC or o[5] == DT_COUNTER for o in self._ops[op_off:])
         self._docs.append((change_off, len(changes), dep_off0, len(self._deps) - dep_off0,
                            op_off, len(self._ops) - op_off, self._reg_off, n_regs, len(obj_list), len(ranked),
-                           DOC_HAS_LISTS if has_lists else 0, (0, 0)))
+                           (DOC_HAS_LISTS if has_lists else 0) | (DOC_HAS_COUNTERS if has_counters else 0),
+                           (0, 0)))
         self._reg_off += n_regs
         self._max_actors = max(self._max_actors, len(ranked))
         self._doc_actors.append(ranked)

@@ -45,17 +45,16 @@ int hip_fail(hm_engine *e, hipError_t r, const char *what) {
         if (_r != hipSuccess) return hip_fail(e, _r, #call); \
     } while (0)
 
-struct Caps { uint32_t opl, regs, objs; bool lists; };
+struct Caps { uint32_t opl, cls; bool lists, counters; };
 
 Caps launch_caps(const hm_batch *b) {
     Caps c;
     uint32_t mo = b->max_ops;
     c.opl = mo <= 64 ? 1 : (mo <= 128 ? 2 : 4);
-    c.regs = std::max<uint32_t>(1, std::min<uint32_t>(b->max_regs, 1024));
-    c.regs = (c.regs + 15) & ~15u;
-    c.objs = std::max<uint32_t>(1, std::min<uint32_t>(b->max_objs, 256));
-    c.objs = (c.objs + 15) & ~15u;
+    // 0 = unknown hint -> the larger class (documents outside it are deferred)
+    c.cls = (b->max_regs && b->max_objs && b->max_deps) ? hm_small_class(b->max_regs, b->max_objs, b->max_deps) : 1u;
     c.lists = (b->doc_flags & HM_DOC_HAS_LISTS) != 0;
+    c.counters = (b->doc_flags & HM_DOC_HAS_COUNTERS) != 0;
     return c;
 }
 
@@ -65,7 +64,8 @@ int launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, hipStream
     p.docs = b->docs; p.changes = b->changes; p.deps = b->deps; p.ops = b->ops; p.min_clock = b->min_clock;
     p.res_docs = o->docs; p.res_clock = o->clock; p.res_back_clock = o->back_clock; p.res_heads = o->heads;
     p.res_hist = o->hist; p.res_all_deps = o->all_deps; p.res_regs = o->regs; p.res_surv = o->surv;
-    p.n_docs = b->n_docs; p.a_stride = b->a_stride; p.cap_regs = c.regs; p.cap_objs = c.objs;
+    p.n_docs = b->n_docs; p.a_stride = b->a_stride; p.cap_regs = 0; p.cap_objs = 0; p.cap_deps = 0;
+    p.counters = c.counters ? 1u : 0u;
     p.general_only = (e->flags & HM_CFG_GENERAL_ONLY) ? 1u : 0u;
     if (b->n_docs == 0) { e->n_last = 0; return HM_OK; }
     // scratch: [counters 256 B][deferred list n_docs u32][large-kernel pool]
@@ -84,11 +84,11 @@ int launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, hipStream
     unsigned long long *pool_used = (unsigned long long *)(pb + 8);
     HIPCHK(e, hipMemsetAsync(pb, 0, 16, s));
     // persistent grid: enough resident 1-wave workgroups to fill every CU
-    size_t lds = hm_small_lds_bytes(c.opl, c.regs, c.objs, c.lists);
+    size_t lds = hm_small_lds_bytes(c.opl, c.cls, c.lists, c.counters);
     uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, (160 * 1024) / std::max<size_t>(lds, 1)));
     uint32_t grid = std::min<uint32_t>(b->n_docs, (uint32_t)e->num_cus * per_cu * 2);
     HIPCHK(e, hipEventRecord(e->ev[0], s));
-    hipError_t r = hm_launch_small(p, c.opl, c.lists, grid, s);
+    hipError_t r = hm_launch_small(p, c.opl, c.cls, c.lists, grid, s);
     if (r != hipSuccess) return hip_fail(e, r, "merge_small_kernel launch");
     HIPCHK(e, hipEventRecord(e->ev[1], s));
     HIPCHK(e, hipEventRecord(e->ev[2], s));
@@ -183,14 +183,16 @@ int hm_merge_host(hm_engine *e, const hm_batch *hb, const hm_results *ho) {
         if (st) return st;
         HIPCHK(e, hipSetDevice(e->device));
         hm_batch b = *hb;
-        if (!b.max_changes && !b.max_ops && !b.max_regs && !b.max_objs)
+        if (!b.max_changes && !b.max_ops && !b.max_regs && !b.max_objs) {
             for (uint32_t d = 0; d < b.n_docs; d++) {
                 b.max_changes = std::max(b.max_changes, hb->docs[d].n_changes);
                 b.max_ops = std::max(b.max_ops, hb->docs[d].n_ops);
                 b.max_regs = std::max(b.max_regs, hb->docs[d].n_regs);
                 b.max_objs = std::max(b.max_objs, hb->docs[d].n_objs);
+                b.max_deps = std::max(b.max_deps, hb->docs[d].n_deps);
                 b.doc_flags |= hb->docs[d].flags;
             }
+        }
         const size_t S = b.a_stride;
         struct Seg { size_t bytes; size_t off; };
         auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };

@@ -16,7 +16,9 @@ struct SmallParams {
     hm_reg_result *res_regs;
     hm_surv_result *res_surv;
     uint32_t n_docs, a_stride;
-    uint32_t cap_regs, cap_objs;     // LDS carve of this launch
+    uint32_t cap_regs, cap_objs;     // LDS carve of this launch (set by the kernel's size class)
+    uint32_t cap_deps;               // dep rows per document the carve holds
+    uint32_t counters;               // the carve has the counter sums (HM_DOC_HAS_COUNTERS)
     uint32_t *defer_list;            // documents handed to merge_large_kernel
     uint32_t *defer_count;
     uint32_t general_only;           // HM_CFG_GENERAL_ONLY: defer every document
@@ -28,8 +30,10 @@ struct SmallParams {
 size_t hm_large_scratch_bound(const hm_batch *b);
 hipError_t hm_launch_large(const SmallParams &p, void *pool, size_t pool_bytes, unsigned long long *pool_used,
                            uint32_t grid, hipStream_t s);
-size_t hm_small_lds_bytes(uint32_t opl, uint32_t cap_regs, uint32_t cap_objs, bool lists);
-hipError_t hm_launch_small(const SmallParams &p, uint32_t opl, bool lists, uint32_t grid, hipStream_t s);
+// small-kernel size class (LDS carve) for a batch's per-document maxima
+uint32_t hm_small_class(uint32_t max_regs, uint32_t max_objs, uint32_t max_deps);
+size_t hm_small_lds_bytes(uint32_t opl, uint32_t cls, bool lists, bool counters);
+hipError_t hm_launch_small(const SmallParams &p, uint32_t opl, uint32_t cls, bool lists, uint32_t grid, hipStream_t s);
 // which: 0 cmp (out uint8_t*), 1 union, 2 intersection (out uint32_t*)
 hipError_t hm_launch_clock(int which, const uint32_t *a, const uint32_t *b, void *out, uint32_t n_docs,
                            uint32_t S, hipStream_t s);

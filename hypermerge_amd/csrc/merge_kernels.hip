@@ -40,11 +40,11 @@
 #define HM_ABLATE 0     // dev-only timing builds: 1 skip ancestor push, 2 stop after K1, 4 stop after K2 survivors
 #endif
 #ifndef HM_WAVES_PER_EU
-#define HM_WAVES_PER_EU 5   // occupancy target for the register allocator (93 VGPRs, no spills)
+#define HM_WAVES_PER_EU 4   // register-allocator target: LDS already caps C4-class launches at ~4.25 waves/SIMD
 #endif
 #define WAVE 64
 #define NA_MAX 8
-#define NDEP_MAX 512
+#define NDEP_MAX 1024                // largest dep table a launch carves
 typedef unsigned long long u64;
 #if defined(__HIP_DEVICE_COMPILE__)
 #define LDS __attribute__((address_space(3)))   // explicit LDS pointers -> ds_* (not flat_*) instructions
@@ -88,38 +88,58 @@ __device__ __forceinline__ u64 err_key(uint32_t h, uint32_t op_plus1, uint32_t a
 }
 
 struct SmallLds {
-    LDS u64 *anc, *chain, *segor, *survabs, *errkey;
-    LDS hm_op_row *ops;             // the document's op rows, staged from the prefetch registers
-    LDS int64_t *survsum;
+    LDS u64 *anc, *chain, *segor, *errkey, *opval;
+    LDS int64_t *survsum;           // counter launches only
+    LDS uint2 *cw0, *cw1, *cw2;     // staged change rows (three 8-byte words, conflict-free)
     LDS uint32_t *first, *base, *bclock, *headv, *objslot, *segcnt, *survcnt, *regoff, *regobj, *insmin;
     LDS uint32_t *flags, *deps, *segoff, *segfill, *seglist, *survp;
+    LDS uint32_t *opmeta;           // action | datatype << 8 | vtag << 16
+    LDS uint32_t *opro;             // reg | obj << 16 (clamped to 0xFFFF: >= any carve)
+    LDS uint32_t *opelem;           // ins element counter (list launches)
     LDS int32_t *hist_of;
-    LDS uint16_t *survtmp, *survop, *opbase;
+    LDS uint16_t *survtmp, *survop, *opbase, *oppar;
     LDS uint8_t *h2a, *chactor, *opchg, *objtype;
     // K3 (RGA lists); carved only for launches with list documents
     LDS uint32_t *nins, *pcount, *poff, *pfill, *nodekey, *tour0, *tour1, *listbase;
     LDS uint16_t *nodeop, *nodepi, *regnode, *plist, *fc, *ns, *listid;
 };
+#define PAR_HEAD 0xFFFFu             // oppar of an insert after '_head'
 
-// LDS carve, identical for the host size query and the device pointers.
+// Size classes of the small kernel's carve (registers, objects, dep rows per document).
+template <int CLS> struct SizeClass;
+template <> struct SizeClass<0> { static constexpr uint32_t NR = 32, NO = 16, ND = 128; };
+template <> struct SizeClass<1> { static constexpr uint32_t NR = 256, NO = 64, ND = 512; };
+
+// LDS carve, identical for the host size query and the device pointers.  Sized per launch
+// (ops, registers, objects, dep rows, lists, counters): LDS is what bounds the number of
+// resident waves per CU, so nothing is carved that the launch's documents cannot use.
+// The kernel instantiates it with compile-time sizes (a size class), so every LDS address
+// folds into a ds_* immediate offset instead of occupying an SGPR.
+// Aliases: seglist/survp live in `first` (dead after K1b), survtmp in `deps` (dead after K1b).
 template <typename L_t, typename P>
-__host__ __device__ inline size_t small_carve(P base, uint32_t NOp, uint32_t NR, uint32_t NO, bool lists, L_t *L) {
+__host__ __device__ inline size_t small_carve(P base, uint32_t NOp, uint32_t NR, uint32_t NO, uint32_t ND,
+                                              bool lists, bool counters, L_t *L) {
     size_t o = 0;
 #define TAKE(f, T, cnt) do { L->f = (decltype(L->f))(base + o); o = (o + (size_t)(cnt) * sizeof(T) + 15) & ~(size_t)15; } while (0)
     TAKE(anc, u64, 64);          TAKE(chain, u64, NA_MAX);     TAKE(segor, u64, NR);
-    TAKE(survabs, u64, NOp);     TAKE(errkey, u64, 1);         TAKE(ops, hm_op_row, NOp);
-    TAKE(survsum, int64_t, NOp);
-    TAKE(first, uint32_t, NA_MAX * 64); TAKE(base, uint32_t, NA_MAX * 3);
+    TAKE(errkey, u64, 1);        TAKE(opval, u64, NOp);
+    TAKE(cw0, uint2, 64);        TAKE(cw1, uint2, 64);         TAKE(cw2, uint2, 64);
+    TAKE(first, uint32_t, NA_MAX * 64 > 2 * NOp ? NA_MAX * 64 : 2 * NOp);
+    L->seglist = L->first; L->survp = L->first + NOp;
+    TAKE(base, uint32_t, NA_MAX * 3);
     TAKE(objslot, uint32_t, NO); TAKE(segcnt, uint32_t, NR);   TAKE(survcnt, uint32_t, NR);
     TAKE(regoff, uint32_t, NR);  TAKE(regobj, uint32_t, NR);   TAKE(insmin, uint32_t, NR);
-    TAKE(flags, uint32_t, 1);    TAKE(deps, uint32_t, NDEP_MAX);
-    TAKE(segoff, uint32_t, NR);  TAKE(segfill, uint32_t, NR);  TAKE(seglist, uint32_t, NOp);
-    TAKE(survp, uint32_t, NOp);  TAKE(hist_of, int32_t, 64);
-    TAKE(survtmp, uint16_t, NOp); TAKE(survop, uint16_t, NOp); TAKE(opbase, uint16_t, 64);
+    TAKE(flags, uint32_t, 1);    TAKE(deps, uint32_t, ND > NOp / 2 ? ND : NOp / 2);
+    L->survtmp = (decltype(L->survtmp))L->deps;
+    TAKE(segoff, uint32_t, NR);  TAKE(segfill, uint32_t, NR);
+    TAKE(opmeta, uint32_t, NOp); TAKE(opro, uint32_t, NOp);
+    TAKE(hist_of, int32_t, 64);
+    TAKE(survop, uint16_t, NOp); TAKE(opbase, uint16_t, 64);   TAKE(oppar, uint16_t, NOp);
     TAKE(h2a, uint8_t, 64);      TAKE(chactor, uint8_t, 64);   TAKE(opchg, uint8_t, NOp);
     TAKE(objtype, uint8_t, NO);
     if (lists) {
         const uint32_t NP = NR + NO, NE = 2 * (NOp + NO);
+        TAKE(opelem, uint32_t, NOp);
         TAKE(nins, uint32_t, 1);      TAKE(pcount, uint32_t, NP);  TAKE(poff, uint32_t, NP);
         TAKE(pfill, uint32_t, NP);    TAKE(nodekey, uint32_t, NOp); TAKE(tour0, uint32_t, NE);
         TAKE(tour1, uint32_t, NE);    TAKE(listbase, uint32_t, NO + 1);
@@ -127,6 +147,7 @@ __host__ __device__ inline size_t small_carve(P base, uint32_t NOp, uint32_t NR,
         TAKE(plist, uint16_t, NOp);   TAKE(fc, uint16_t, NP);      TAKE(ns, uint16_t, NOp);
         TAKE(listid, uint16_t, NO);
     }
+    TAKE(survsum, int64_t, counters ? NOp : 0);       // last: the rest of the carve ignores `counters`
 #undef TAKE
     L->bclock = L->base + NA_MAX;
     L->headv = L->base + 2 * NA_MAX;
@@ -142,10 +163,15 @@ template <typename T> __device__ __forceinline__ T lds_add(LDS T *p, typename Id
 enum : uint32_t { FL_UNSUPPORTED = 1u };
 enum Outcome { OUT_OK = 0, OUT_ERROR = 1, OUT_UNSUPPORTED = 2 };
 
+// raise byte a of the 8-byte packed requirement (lo: actors 0-3, hi: 4-7) to at least v;
+// selects only (a data-dependent reference would push lo/hi to scratch)
 __device__ __forceinline__ void need_set(uint32_t &lo, uint32_t &hi, uint32_t a, uint32_t v) {
     const uint32_t sh = (a & 3) * 8;
-    if (a < 4) { const uint32_t cur = (lo >> sh) & 0xFF; if (v > cur) lo = (lo & ~(0xFFu << sh)) | (v << sh); }
-    else       { const uint32_t cur = (hi >> sh) & 0xFF; if (v > cur) hi = (hi & ~(0xFFu << sh)) | (v << sh); }
+    const uint32_t w = a < 4 ? lo : hi;
+    const uint32_t cur = (w >> sh) & 0xFF;
+    const uint32_t nw = v > cur ? ((w & ~(0xFFu << sh)) | (v << sh)) : w;
+    lo = a < 4 ? nw : lo;
+    hi = a < 4 ? hi : nw;
 }
 
 
@@ -230,7 +256,7 @@ __device__ __forceinline__ void rga_order(const SmallLds &L, uint32_t R, uint32_
     // Euler tour: down(i) = 2i (value 1), up(i) = 2i+1; list head h = N + listid: 2h, 2h+1 (end)
     const uint32_t E = 2 * (N + nl);
     for (uint32_t i = lane; i < N; i += WAVE) {
-        const uint32_t reg = L.ops[L.nodeop[i]].reg;
+        const uint32_t reg = (L.opro[L.nodeop[i]] & 0xFFFFu);
         const uint32_t hd = N + L.listid[L.regobj[reg]];
         const uint32_t f = L.fc[reg];
         const uint32_t sd = f != 0xFFFFu ? 2 * f : 2 * i + 1;
@@ -270,7 +296,7 @@ __device__ __forceinline__ void rga_order(const SmallLds &L, uint32_t R, uint32_
     }
     wave_sync();
     for (uint32_t i = lane; i < N; i += WAVE) {
-        const uint32_t reg = L.ops[L.nodeop[i]].reg;
+        const uint32_t reg = (L.opro[L.nodeop[i]] & 0xFFFFu);
         const uint32_t l = L.listid[L.regobj[reg]];
         const uint32_t total = cur[2 * (N + l)] & 0xFFFFu;
         const uint32_t pos = L.listbase[l] + total - (cur[2 * i] & 0xFFFFu);
@@ -289,7 +315,7 @@ __device__ __forceinline__ void rga_order(const SmallLds &L, uint32_t R, uint32_
     }
     wave_sync();
     for (uint32_t i = lane; i < N; i += WAVE) {
-        const uint32_t reg = L.ops[L.nodeop[i]].reg;
+        const uint32_t reg = (L.opro[L.nodeop[i]] & 0xFFFFu);
         const uint32_t pos = L.nodekey[i];
         if (L.seglist[pos]) {
             const uint32_t l = L.listid[L.regobj[reg]];
@@ -301,16 +327,23 @@ __device__ __forceinline__ void rga_order(const SmallLds &L, uint32_t R, uint32_
 }
 
 
+// The literal-fold check reads only these tables (passed by value: taking the address of
+// the whole SmallLds would push every LDS pointer to scratch).
+struct FoldView {
+    LDS u64 *anc, *chain;
+    LDS uint32_t *first, *base, *deps;
+    LDS int32_t *hist_of;
+};
 // FC(h)[x]: latest seq of actor x among change h's ancestors and itself (cold merge)
-__device__ __forceinline__ uint32_t fc_of(const SmallLds &L, uint32_t h, uint32_t x) {
+__device__ __forceinline__ uint32_t fc_of(FoldView L, uint32_t h, uint32_t x) {
     return (uint32_t)__popcll((L.anc[h] | (1ull << h)) & L.chain[x]);
 }
 // history position of the applied change (a, s) (s >= 1, in this batch)
-__device__ __forceinline__ uint32_t hpos_of(const SmallLds &L, uint32_t a, uint32_t s) {
+__device__ __forceinline__ uint32_t hpos_of(FoldView L, uint32_t a, uint32_t s) {
     return (uint32_t)L.hist_of[L.first[a * 64 + (s - L.base[a])]];
 }
 // Does the literal transitiveDeps fold differ from the closure for this change?
-__device__ __noinline__ bool fold_differs(const SmallLds &L, uint32_t dep0, uint32_t nd, uint32_t actor, uint32_t seq) {
+__device__ __noinline__ bool fold_differs(FoldView L, uint32_t dep0, uint32_t nd, uint32_t actor, uint32_t seq) {
     // entries of deps.set(actor, seq-1) in key order, seq 0 skipped (reduce ignores them)
     uint32_t ex[NA_MAX + 1], es[NA_MAX + 1], eh[NA_MAX + 1], k = 0;
     bool own = false;
@@ -334,25 +367,73 @@ __device__ __noinline__ bool fold_differs(const SmallLds &L, uint32_t dep0, uint
     return false;
 }
 
-// Rows of the NEXT document, loaded into registers before the current document's
-// output stores (loads and stores share vmcnt on CDNA: loads issued first are not
-// held up by the stores), then staged to LDS at the top of the next iteration.
-template <int OPL>
-struct Prefetch {
-    hm_change_row c;          // lane < n_changes
-    hm_op_row op[OPL];        // lane + 64 t < n_ops
-    hm_dep_row dp[2];         // lane + 64 t < n_deps (the rest, if any, is loaded on use)
+// One document's input rows in flight.  They are loaded before the previous document's
+// output stores (loads and stores share vmcnt on CDNA: loads issued first are not held up
+// by the stores) and written to LDS after those stores, so nothing stays live across
+// documents.  Named members only (no arrays): the struct is scalarised into VGPRs.
+struct Rows {
+    uint2 c0, c1, c2;                        // change row, lane < n_changes
+    uint4 a0, b0, a1, b1, a2, b2, a3, b3;    // op rows lane + 64 t (first / second 16 B)
+    uint2 d0, d1;                            // dep rows lane, lane + 64
 };
+__device__ __forceinline__ void load_op(const SmallParams &p, const hm_doc_row &doc, uint32_t k, uint4 &a, uint4 &b) {
+    a = make_uint4(0, 0, 0, 0); b = a;
+    if (k < doc.n_ops) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(p.ops + doc.op_off + k);
+        a = src[0]; b = src[1];
+    }
+}
 template <int OPL>
-__device__ __forceinline__ void prefetch_doc(const SmallParams &p, const hm_doc_row &doc, Prefetch<OPL> &pf) {
+__device__ __forceinline__ Rows load_rows(const SmallParams &p, const hm_doc_row &doc) {
     const uint32_t lane = threadIdx.x;
-    if (lane < doc.n_changes) pf.c = p.changes[doc.change_off + lane];
-#pragma unroll
-    for (int t = 0; t < OPL; t++)
-        if (lane + WAVE * t < doc.n_ops) pf.op[t] = p.ops[doc.op_off + lane + WAVE * t];
-#pragma unroll
-    for (int t = 0; t < 2; t++)
-        if (lane + WAVE * t < doc.n_deps) pf.dp[t] = p.deps[doc.dep_off + lane + WAVE * t];
+    Rows r;
+    r.c0 = r.c1 = r.c2 = r.d0 = r.d1 = make_uint2(0, 0);
+    if (lane < doc.n_changes) {
+        const uint2 *cs = reinterpret_cast<const uint2 *>(p.changes + doc.change_off + lane);
+        r.c0 = cs[0]; r.c1 = cs[1]; r.c2 = cs[2];
+    }
+    load_op(p, doc, lane, r.a0, r.b0);
+    if (OPL > 1) load_op(p, doc, lane + WAVE, r.a1, r.b1);
+    if (OPL > 2) { load_op(p, doc, lane + 2 * WAVE, r.a2, r.b2); load_op(p, doc, lane + 3 * WAVE, r.a3, r.b3); }
+    const hm_dep_row *dp = p.deps + doc.dep_off;
+    if (lane < doc.n_deps) r.d0 = *reinterpret_cast<const uint2 *>(dp + lane);
+    if (lane + WAVE < doc.n_deps) r.d1 = *reinterpret_cast<const uint2 *>(dp + lane + WAVE);
+    return r;
+}
+// dep row -> actor << 24 | seq (all ones: outside the envelope)
+__device__ __forceinline__ uint32_t pack_dep(uint2 w) {
+    const uint32_t a = w.x & 0xFFFF;
+    return (w.y < (1u << 24) && a < 256) ? ((a << 24) | w.y) : 0xFFFFFFFFu;
+}
+template <bool LISTS>
+__device__ __forceinline__ void stage_op(const SmallLds &L, uint32_t k, uint32_t m, uint4 a, uint4 b) {
+    if (k >= m) return;
+    // a = (obj, reg, parent, elem); b = (action | datatype << 8 | vtag << 16, key, value lo, value hi)
+    const uint32_t obj = a.x < 0xFFFFu ? a.x : 0xFFFFu, reg = a.y < 0xFFFFu ? a.y : 0xFFFFu;
+    L.opro[k] = reg | (obj << 16);
+    L.oppar[k] = (uint16_t)(a.z == HM_HEAD ? PAR_HEAD : (a.z < 0xFFFEu ? a.z : 0xFFFEu));
+    L.opmeta[k] = b.x & 0xFFFFFFu;
+    L.opval[k] = ((u64)b.w << 32) | b.z;
+    if (LISTS) L.opelem[k] = a.w;
+}
+template <int OPL, bool LISTS>
+__device__ __forceinline__ void stage_rows(const SmallParams &p, const SmallLds &L, const hm_doc_row &doc, const Rows &r) {
+    const uint32_t lane = threadIdx.x, m = doc.n_ops;
+    if (lane < doc.n_changes) { L.cw0[lane] = r.c0; L.cw1[lane] = r.c1; L.cw2[lane] = r.c2; }
+    stage_op<LISTS>(L, lane, m, r.a0, r.b0);
+    if (OPL > 1) stage_op<LISTS>(L, lane + WAVE, m, r.a1, r.b1);
+    if (OPL > 2) { stage_op<LISTS>(L, lane + 2 * WAVE, m, r.a2, r.b2); stage_op<LISTS>(L, lane + 3 * WAVE, m, r.a3, r.b3); }
+    const uint32_t nd = doc.n_deps < p.cap_deps ? doc.n_deps : p.cap_deps;
+    if (lane < nd) L.deps[lane] = pack_dep(r.d0);
+    if (lane + WAVE < nd) L.deps[lane + WAVE] = pack_dep(r.d1);
+    for (uint32_t i = lane + 2 * WAVE; i < nd; i += WAVE)     // long dep tables: read on demand
+        L.deps[i] = pack_dep(*reinterpret_cast<const uint2 *>(p.deps + doc.dep_off + i));
+}
+__device__ __forceinline__ hm_change_row change_of(uint2 w0, uint2 w1, uint2 w2) {
+    hm_change_row c;
+    c.actor = (uint16_t)(w0.x & 0xFFFF); c.n_deps = (uint16_t)(w0.x >> 16); c.seq = w0.y;
+    c.dep_off = w1.x; c.n_ops = w1.y; c.op_first = w2.x; c.content_id = w2.y;
+    return c;
 }
 // what the output phase needs besides LDS
 struct DocState {
@@ -364,30 +445,30 @@ struct DocState {
 // Merge one document with the whole wave (no global stores).  Every return is wave-uniform.
 template <int OPL, bool LISTS>
 __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const SmallLds &L, const hm_doc_row &doc,
-                                                   const Prefetch<OPL> &pf, DocState &st) {
+                                                   DocState &st) {
     const uint32_t lane = threadIdx.x;
     const uint32_t n = doc.n_changes, A = doc.n_actors, m = doc.n_ops, R = doc.n_regs, O = doc.n_objs;
     st.hist = -1; st.H = 0; st.total = 0; st.doc_lists = false;
 
-    // ---------------- stage the prefetched rows (lane = arrival index) ----------------
+    // ---------------- the staged rows (lane = arrival index) ----------------
     const bool act = lane < n;
-    hm_change_row c = {};
-    if (act) c = pf.c;
+    const hm_change_row c = act ? change_of(L.cw0[lane], L.cw1[lane], L.cw2[lane])
+                                : change_of(make_uint2(0, 0), make_uint2(0, 0), make_uint2(0, 0));
     for (uint32_t i = lane; i < NA_MAX * 64; i += WAVE) L.first[i] = 0xFFFFFFFFu;
     if (lane < NA_MAX) { L.base[lane] = 0xFFFFFFFFu; L.bclock[lane] = 0; L.headv[lane] = 0; L.chain[lane] = 0; }
     if (lane == 0) { *L.errkey = ~0ull; *L.flags = 0; }
-#pragma unroll
-    for (int t = 0; t < OPL; t++)
-        if (lane + WAVE * t < m) L.ops[lane + WAVE * t] = pf.op[t];
     const uint32_t dep_lo = doc.dep_off, ndep = doc.n_deps;
-    if (ndep > NDEP_MAX) return OUT_UNSUPPORTED;
-    for (uint32_t i = lane; i < ndep; i += WAVE) {
-        const hm_dep_row dp = i < 2 * WAVE ? pf.dp[i >= WAVE ? 1 : 0] : p.deps[dep_lo + i];
-        L.deps[i] = (dp.seq < (1u << 24) && dp.actor < 256) ? (((uint32_t)dp.actor << 24) | dp.seq) : 0xFFFFFFFFu;
-    }
     wave_sync();
     const uint32_t actor = c.actor, seq = c.seq;
     const uint32_t my_dep0 = c.dep_off - dep_lo;
+    // layout contract (include/hypermerge_amd.h): op and dep rows are grouped by change in
+    // arrival order without gaps; anything else leaves the envelope
+    const uint32_t op_end = c.op_first + c.n_ops, dep_end = c.dep_off + c.n_deps;
+    const uint32_t prev_op = shfl32(op_end, lane ? (int)lane - 1 : 0), prev_dep = shfl32(dep_end, lane ? (int)lane - 1 : 0);
+    if ((n == 0 && (m || ndep)) ||
+        (act && (c.op_first != (lane ? prev_op : doc.op_off) || c.dep_off != (lane ? prev_dep : dep_lo) ||
+                 (lane == n - 1 && (op_end != doc.op_off + m || dep_end != dep_lo + ndep)))))
+        lds_or(L.flags, FL_UNSUPPORTED);
     if (act) {
         if (actor >= A || seq == 0 || c.dep_off < dep_lo || my_dep0 + c.n_deps > ndep) lds_or(L.flags, FL_UNSUPPORTED);
         else { lds_min(&L.base[actor], seq); lds_max(&L.bclock[actor], seq); }
@@ -568,7 +649,10 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     const uint32_t h_own_row = shfl32(own_row ? 1u : 0u, (int)ai);     // all lanes: bpermute sources
     const uint32_t h_dep0 = shfl32(my_dep0, (int)ai), h_nd = shfl32(c.n_deps, (int)ai);
     suspect |= hv && h_own_row != 0;
-    if (suspect && fold_differs(L, h_dep0, h_nd, hactor, hseq)) lds_or(L.flags, FL_UNSUPPORTED);
+    if (suspect) {
+        const FoldView fv = {L.anc, L.chain, L.first, L.base, L.deps, L.hist_of};
+        if (fold_differs(fv, h_dep0, h_nd, hactor, hseq)) lds_or(L.flags, FL_UNSUPPORTED);
+    }
     if (hv && !((covered >> lane) & 1)) L.headv[hactor] = hseq;     // opSet.deps
     for (uint32_t i = lane; i < O; i += WAVE) { L.objslot[i] = i == 0 ? 0u : 0xFFFFFFFFu; L.objtype[i] = i == 0 ? HM_MAKE_MAP : 0xFF; }
     for (uint32_t i = lane; i < R; i += WAVE) {
@@ -580,37 +664,44 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     // ---------------- K2: ops (lane + 64*t) ----------------
     uint32_t oreg[OPL], oobj[OPL], opar[OPL], oact[OPL], okey[OPL], oarr[OPL], oelem[OPL];
     int32_t oh[OPL];
+    bool counter_ops = false, malformed = false;
 #pragma unroll
     for (int t = 0; t < OPL; t++) {
         const uint32_t k = lane + WAVE * t;
         oh[t] = -1; okey[t] = 0; oarr[t] = 0; oreg[t] = 0; oobj[t] = 0; opar[t] = 0; oact[t] = 0xFF; oelem[t] = 0;
         if (k < m) {
-            const hm_op_row o = L.ops[k];
+            const uint32_t meta = L.opmeta[k], ro = L.opro[k], pr = L.oppar[k];
             const uint32_t ch = L.opchg[k];
             oarr[t] = ch; oh[t] = L.hist_of[ch];
-            oreg[t] = o.reg; oobj[t] = o.obj; opar[t] = o.parent; oact[t] = o.action; oelem[t] = o.elem;
-            if (o.action == HM_INS && o.elem >= (1u << 24)) lds_or(L.flags, FL_UNSUPPORTED);
+            oreg[t] = ro & 0xFFFFu; oobj[t] = ro >> 16; oact[t] = meta & 0xFF;
+            opar[t] = pr == PAR_HEAD ? HM_HEAD : pr;
+            if (LISTS) {
+                oelem[t] = L.opelem[k];
+                if (oact[t] == HM_INS && oelem[t] >= (1u << 24)) lds_or(L.flags, FL_UNSUPPORTED);
+            }
+            counter_ops |= oact[t] == HM_INC || ((meta >> 8) & 0xFF) == HM_DT_COUNTER;
             okey[t] = ((uint32_t)(oh[t] < 0 ? 0 : oh[t]) << 16) | (k - L.opbase[ch]);
-            if (oh[t] >= 0) {
-                const uint32_t a = o.action;
-                if (a <= HM_MAKE_TEXT) {
-                    if (o.obj >= O) lds_or(L.flags, FL_UNSUPPORTED);
-                    else lds_min(&L.objslot[o.obj], okey[t] + 1);
-                } else if (a <= HM_INC) {
-                    if (o.reg >= R || (a == HM_INS && o.parent != HM_HEAD && o.parent >= R))
-                        lds_or(L.flags, FL_UNSUPPORTED);
-                    else if (o.obj < O) {
-                        L.regobj[o.reg] = o.obj;
-                        if (a == HM_INS) lds_min(&L.insmin[o.reg], okey[t] + 1);
-                        else {
-                            lds_add(&L.segcnt[o.reg], 1u);
-                            if (a != HM_INC) lds_or(&L.segor[o.reg], L.anc[oh[t]]);
-                        }
+            // malformed rows (any op, applied or not) put the whole document outside the envelope
+            const uint32_t a = oact[t];
+            const bool bad = a <= HM_MAKE_TEXT ? oobj[t] >= O
+                           : (a <= HM_INC ? (oreg[t] >= R || (a == HM_INS && opar[t] != HM_HEAD && opar[t] >= R)) : true);
+            malformed |= bad;
+            if (oh[t] >= 0 && !bad) {
+                if (a <= HM_MAKE_TEXT) lds_min(&L.objslot[oobj[t]], okey[t] + 1);
+                else if (oobj[t] < O) {
+                    L.regobj[oreg[t]] = oobj[t];
+                    if (a == HM_INS) lds_min(&L.insmin[oreg[t]], okey[t] + 1);
+                    else {
+                        lds_add(&L.segcnt[oreg[t]], 1u);
+                        if (a != HM_INC) lds_or(&L.segor[oreg[t]], L.anc[oh[t]]);
                     }
-                } else lds_or(L.flags, FL_UNSUPPORTED);
+                }
             }
         }
     }
+    if (__ballot(malformed)) return OUT_UNSUPPORTED;
+    // counter sums need the carve's survsum table (launches flagged HM_DOC_HAS_COUNTERS)
+    if (!p.counters && __ballot(counter_ops)) lds_or(L.flags, FL_UNSUPPORTED);
     wave_sync();
     // objects: the earliest make op creates, later ones throw 'Duplicate creation of object'
 #pragma unroll
@@ -639,8 +730,9 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
             has_list = true;
             if (L.insmin[oreg[t]] != okey[t] + 1)     // 'Duplicate list element ID'
                 lds_min(L.errkey, err_key((uint32_t)oh[t], (okey[t] & 0xFFFF) + 1, oarr[t], HM_ERR_DUPLICATE_ELEM));
+            // engine envelope, ordered like a throw: insert after an element not yet inserted
             if (opar[t] != HM_HEAD && !(L.insmin[opar[t]] <= okey[t]))
-                lds_or(L.flags, FL_UNSUPPORTED);
+                lds_min(L.errkey, err_key((uint32_t)oh[t], (okey[t] & 0xFFFF) + 1, oarr[t], HM_ERR_UNSUPPORTED));
             continue;
         }
         has_list |= is_list;
@@ -741,47 +833,46 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         if (!surv[t]) continue;
         const uint32_t pos = L.regoff[oreg[t]] + rank[t];
         L.survop[pos] = (uint16_t)(lane + WAVE * t);
-        L.survsum[pos] = 0;
-        L.survabs[pos] = 0;
+        if (p.counters) L.survsum[pos] = 0;
     }
     wave_sync();
     if constexpr (LISTS) {
         if (doc_lists) rga_order<OPL>(L, R, O, oreg, oobj, opar, oact, oelem, oarr, oh);
     }
-    // counters: an inc adds to every surviving counter set that is its ancestor
-    bool float_counter = false;
+    // counters: an inc adds to every surviving counter set that is its ancestor.
+    // JS numbers: an integer counter is exact only while |base| + sum|inc| <= 2^53; with at
+    // most 256 ops per document, |inc| < 2^44 and |base| < 2^52 guarantee it (larger
+    // values go to merge_large_kernel, which tracks sum|inc| exactly).
+    if (p.counters && __ballot(counter_ops)) {
+        bool outside = false;
 #pragma unroll
-    for (int t = 0; t < OPL; t++) {
-        if (oh[t] < 0 || oact[t] != HM_INC) continue;
-        const uint32_t k = lane + WAVE * t;
-        const uint32_t reg = oreg[t], b0 = L.regoff[reg], cnt = L.survcnt[reg];
-        const u64 an = L.anc[oh[t]];
-        const uint32_t my_vtag = L.ops[k].vtag;
-        const int64_t v = (int64_t)L.ops[k].value;
-        for (uint32_t q = 0; q < cnt; q++) {
-            const uint32_t k2 = L.survop[b0 + q];
-            const uint32_t vt2 = L.ops[k2].vtag;
-            if (L.ops[k2].action != HM_SET || L.ops[k2].datatype != HM_DT_COUNTER || (vt2 != HM_V_INT && vt2 != HM_V_FLOAT)) continue;
-            if (!((an >> L.hist_of[L.opchg[k2]]) & 1)) continue;
-            if (vt2 != HM_V_INT || my_vtag != HM_V_INT) { float_counter = true; continue; }
-            lds_add((LDS u64 *)&L.survsum[b0 + q], (unsigned long long)v);
-            lds_add((LDS u64 *)&L.survabs[b0 + q], (unsigned long long)(v < 0 ? -v : v));
+        for (int t = 0; t < OPL; t++) {
+            if (oh[t] < 0 || oact[t] != HM_INC) continue;
+            const uint32_t k = lane + WAVE * t;
+            const uint32_t reg = oreg[t], b0 = L.regoff[reg], cnt = L.survcnt[reg];
+            const u64 an = L.anc[oh[t]];
+            const uint32_t my_vtag = (L.opmeta[k] >> 16) & 0xFF;
+            const int64_t v = (int64_t)L.opval[k];
+            for (uint32_t q = 0; q < cnt; q++) {
+                const uint32_t k2 = L.survop[b0 + q];
+                const uint32_t m2 = L.opmeta[k2], vt2 = (m2 >> 16) & 0xFF;
+                if ((m2 & 0xFF) != HM_SET || ((m2 >> 8) & 0xFF) != HM_DT_COUNTER || (vt2 != HM_V_INT && vt2 != HM_V_FLOAT)) continue;
+                if (!((an >> L.hist_of[L.opchg[k2]]) & 1)) continue;
+                // f64 counters need the ordered sum
+                if (vt2 != HM_V_INT || my_vtag != HM_V_INT || (u64)(v < 0 ? -v : v) >= (1ull << 44)) { outside = true; continue; }
+                lds_add((LDS u64 *)&L.survsum[b0 + q], (unsigned long long)v);
+            }
         }
-    }
-    if (__ballot(float_counter)) lds_or(L.flags, FL_UNSUPPORTED);   // f64 counters need the ordered sum
-    wave_sync();
-    if (*L.flags & FL_UNSUPPORTED) return OUT_UNSUPPORTED;
-
-    // JS numbers: an integer counter is exact only while |base| + sum|inc| <= 2^53
-    bool inexact = false;
-    for (uint32_t q = lane; q < total; q += WAVE) {
-        const hm_op_row &o = L.ops[L.survop[q]];
-        if (o.action == HM_SET && o.datatype == HM_DT_COUNTER && o.vtag == HM_V_INT) {
-            const int64_t b = (int64_t)o.value;
-            inexact |= L.survabs[q] + (u64)(b < 0 ? -b : b) > (1ull << 53);
+        for (uint32_t q = lane; q < total; q += WAVE) {
+            const uint32_t k = L.survop[q], mt = L.opmeta[k];
+            if ((mt & 0xFF) == HM_SET && ((mt >> 8) & 0xFF) == HM_DT_COUNTER && ((mt >> 16) & 0xFF) == HM_V_INT) {
+                const int64_t b = (int64_t)L.opval[k];
+                outside |= (u64)(b < 0 ? -b : b) >= (1ull << 52);
+            }
         }
+        if (__ballot(outside)) return OUT_UNSUPPORTED;
+        wave_sync();
     }
-    if (__ballot(inexact)) return OUT_UNSUPPORTED;
     st.hist = hist; st.H = H; st.total = total; st.doc_lists = doc_lists;
     return OUT_OK;
 }
@@ -803,6 +894,7 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
             r.err_change = (uint32_t)((ek >> 8) & 0xFFFF);
             const uint32_t opp1 = (uint32_t)((ek >> 24) & 0xFFFF);
             r.err_op = opp1 ? opp1 - 1 : HM_NONE;
+            if (r.status == HM_ERR_UNSUPPORTED) { r.err_change = HM_NONE; r.err_op = HM_NONE; }
             *dres = r;
         }
         return;
@@ -818,12 +910,11 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
         return;
     }
     for (uint32_t q = lane; q < st.total; q += WAVE) {
-        const uint32_t k = L.survop[q];
-        const hm_op_row &o = L.ops[k];
+        const uint32_t k = L.survop[q], mt = L.opmeta[k];
         hm_surv_result sr;
-        sr.op = k; sr.vtag = o.vtag; sr.value = o.value;
-        if (o.action == HM_SET && o.datatype == HM_DT_COUNTER && o.vtag == HM_V_INT)
-            sr.value = (u64)((int64_t)o.value + L.survsum[q]);
+        sr.op = k; sr.vtag = (mt >> 16) & 0xFF; sr.value = L.opval[k];
+        if (p.counters && (mt & 0xFF) == HM_SET && ((mt >> 8) & 0xFF) == HM_DT_COUNTER && sr.vtag == HM_V_INT)
+            sr.value = (u64)((int64_t)sr.value + L.survsum[q]);
         p.res_surv[doc.op_off + q] = sr;
     }
     for (uint32_t r = lane; r < R; r += WAVE) {
@@ -863,33 +954,38 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
     }
 }
 
-template <int OPL, bool LISTS>
+template <int OPL, bool LISTS, int CLS>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(HM_WAVES_PER_EU)))
 void merge_small_kernel(SmallParams p) {
     extern __shared__ __align__(16) uint8_t lds_raw[];
+    typedef SizeClass<CLS> C;
     SmallLds L;
-    small_carve((LDS uint8_t *)lds_raw, WAVE * OPL, p.cap_regs, p.cap_objs, LISTS, &L);
+    small_carve((LDS uint8_t *)lds_raw, WAVE * OPL, C::NR, C::NO, C::ND, LISTS, true, &L);
+    p.cap_regs = C::NR; p.cap_objs = C::NO; p.cap_deps = C::ND;
     uint32_t d = blockIdx.x;
     if (d >= p.n_docs) return;
     hm_doc_row doc = p.docs[d];
-    Prefetch<OPL> pf;
-    prefetch_doc<OPL>(p, doc, pf);
+    stage_rows<OPL, LISTS>(p, L, doc, load_rows<OPL>(p, doc));
+    wave_sync();
     for (;;) {
-        // software pipeline over this wave's documents: the next row is read now, its
-        // change/op/dep rows are issued before this document's stores
+        // software pipeline over this wave's documents: the next document's rows are
+        // loaded before this document's stores and staged to LDS after them
         const uint32_t dn = d + gridDim.x;
         const bool more = dn < p.n_docs;
         hm_doc_row docn = {};
         if (more) docn = p.docs[dn];
         const bool in_env = doc.n_changes <= 64 && doc.n_actors <= NA_MAX && doc.n_ops <= WAVE * OPL &&
                             doc.n_regs <= p.cap_regs && doc.n_objs <= p.cap_objs && doc.n_objs >= 1 &&
-                            !p.general_only;
+                            doc.n_deps <= p.cap_deps && !p.general_only;
         DocState st;
-        const Outcome oc = in_env ? merge_doc_small<OPL, LISTS>(p, L, doc, pf, st) : OUT_UNSUPPORTED;
-        if (more) prefetch_doc<OPL>(p, docn, pf);
+        const Outcome oc = in_env ? merge_doc_small<OPL, LISTS>(p, L, doc, st) : OUT_UNSUPPORTED;
+        Rows next;
+        if (more) next = load_rows<OPL>(p, docn);
         write_outputs<LISTS>(p, L, d, doc, oc, st);
         wave_sync();
         if (!more) break;
+        stage_rows<OPL, LISTS>(p, L, docn, next);
+        wave_sync();
         d = dn;
         doc = docn;
     }
@@ -923,19 +1019,26 @@ __global__ void clock_intersection_kernel(const uint32_t *a, const uint32_t *b, 
 }  // namespace hm
 
 // ---------------- host-side launchers ----------------
-size_t hm_small_lds_bytes(uint32_t opl, uint32_t cap_regs, uint32_t cap_objs, bool lists) {
-    hm::SmallLds L;
-    return hm::small_carve((uintptr_t)0, 64 * opl, cap_regs, cap_objs, lists, &L);
+uint32_t hm_small_class(uint32_t max_regs, uint32_t max_objs, uint32_t max_deps) {
+    typedef hm::SizeClass<0> S;
+    return (max_regs <= S::NR && max_objs <= S::NO && max_deps <= S::ND) ? 0u : 1u;
 }
 
-hipError_t hm_launch_small(const SmallParams &p, uint32_t opl, bool lists, uint32_t grid, hipStream_t s) {
-    const size_t lds = hm_small_lds_bytes(opl, p.cap_regs, p.cap_objs, lists);
-#define HM_LAUNCH(O_, L_) hipLaunchKernelGGL((hm::merge_small_kernel<O_, L_>), dim3(grid), dim3(WAVE), lds, s, p)
-    if (lists) {
-        switch (opl) { case 1: HM_LAUNCH(1, true); break; case 2: HM_LAUNCH(2, true); break; default: HM_LAUNCH(4, true); }
-    } else {
-        switch (opl) { case 1: HM_LAUNCH(1, false); break; case 2: HM_LAUNCH(2, false); break; default: HM_LAUNCH(4, false); }
-    }
+size_t hm_small_lds_bytes(uint32_t opl, uint32_t cls, bool lists, bool counters) {
+    hm::SmallLds L;
+    return cls == 0 ? hm::small_carve((uintptr_t)0, 64 * opl, hm::SizeClass<0>::NR, hm::SizeClass<0>::NO,
+                                      hm::SizeClass<0>::ND, lists, counters, &L)
+                    : hm::small_carve((uintptr_t)0, 64 * opl, hm::SizeClass<1>::NR, hm::SizeClass<1>::NO,
+                                      hm::SizeClass<1>::ND, lists, counters, &L);
+}
+
+hipError_t hm_launch_small(const SmallParams &p, uint32_t opl, uint32_t cls, bool lists, uint32_t grid, hipStream_t s) {
+    const size_t lds = hm_small_lds_bytes(opl, cls, lists, p.counters != 0);
+#define HM_LAUNCH(O_, L_, C_) hipLaunchKernelGGL((hm::merge_small_kernel<O_, L_, C_>), dim3(grid), dim3(WAVE), lds, s, p)
+#define HM_OPL(L_, C_) switch (opl) { case 1: HM_LAUNCH(1, L_, C_); break; case 2: HM_LAUNCH(2, L_, C_); break; default: HM_LAUNCH(4, L_, C_); }
+    if (cls == 0) { if (lists) { HM_OPL(true, 0) } else { HM_OPL(false, 0) } }
+    else          { if (lists) { HM_OPL(true, 1) } else { HM_OPL(false, 1) } }
+#undef HM_OPL
 #undef HM_LAUNCH
     return hipGetLastError();
 }

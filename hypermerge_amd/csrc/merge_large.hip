@@ -127,10 +127,16 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, const hm_do
                         sh.headv[tid] = 0; sh.maxad[tid] = 0; }
     if (tid == 0) { sh.flags = 0; sh.errkey = ~0ull; sh.all_ok = 1; sh.H = 0; sh.nins = 0; sh.total = 0; sh.lists = 0; }
     bsync();
+    if (n == 0 && (m || doc.n_deps)) return LUNSUP;
     for (uint32_t i = tid; i < n; i += LWG) {
         const hm_change_row c = CH[i];
+        // layout contract: op and dep rows grouped by change in arrival order, without gaps
+        const uint32_t op0 = i ? CH[i - 1].op_first + CH[i - 1].n_ops : doc.op_off;
+        const uint32_t dp0 = i ? CH[i - 1].dep_off + CH[i - 1].n_deps : doc.dep_off;
+        const bool last_bad = i == n - 1 && (c.op_first + c.n_ops != doc.op_off + m || c.dep_off + c.n_deps != doc.dep_off + doc.n_deps);
         if (c.actor >= A || c.seq == 0 || c.op_first < doc.op_off || c.op_first - doc.op_off + c.n_ops > m ||
-            c.dep_off < doc.dep_off || c.dep_off - doc.dep_off + c.n_deps > doc.n_deps)
+            c.dep_off < doc.dep_off || c.dep_off - doc.dep_off + c.n_deps > doc.n_deps ||
+            c.op_first != op0 || c.dep_off != dp0 || last_bad)
             atomicOr(&sh.flags, LF_UNSUPPORTED);
         else { atomicMin(&sh.base[c.actor], c.seq); atomicMax(&sh.maxs[c.actor], c.seq); atomicMax(&sh.bclock[c.actor], c.seq); }
     }
@@ -317,12 +323,15 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, const hm_do
         const uint32_t ci = X.opchg[k];
         const int32_t h = X.hist[ci];
         X.opkey[k] = h >= 0 ? (((u64)h << 32) | (k - (CH[ci].op_first - doc.op_off))) : ~0ull;
+        // malformed rows (any op, applied or not) put the whole document outside the envelope
+        const bool bad = o.action <= HM_MAKE_TEXT ? o.obj >= O
+                       : (o.action <= HM_INC ? (o.reg >= R || (o.action == HM_INS && o.parent != HM_HEAD && o.parent >= R)) : true);
+        if (bad) { atomicOr(&sh.flags, LF_UNSUPPORTED); continue; }
         if (h < 0) continue;
         const u64 key = X.opkey[k];
         if (o.action <= HM_MAKE_TEXT) {
-            if (o.obj >= O) atomicOr(&sh.flags, LF_UNSUPPORTED); else atomicMin(&X.objslot[o.obj], key + 1);
-        } else if (o.action <= HM_INC) {
-            if (o.reg >= R || (o.action == HM_INS && o.parent != HM_HEAD && o.parent >= R)) { atomicOr(&sh.flags, LF_UNSUPPORTED); continue; }
+            atomicMin(&X.objslot[o.obj], key + 1);
+        } else {
             if (o.obj >= O) continue;
             X.regobj[o.reg] = o.obj;
             if (o.action == HM_INS) { atomicMin(&X.insmin[o.reg], key + 1); if (o.elem >= (1u << 24)) atomicOr(&sh.flags, LF_UNSUPPORTED); }
@@ -333,7 +342,7 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, const hm_do
                     for (uint32_t a = 0; a < A; a++) atomicMax(&X.segmax[(size_t)o.reg * A + a], ad[a]);
                 }
             }
-        } else atomicOr(&sh.flags, LF_UNSUPPORTED);
+        }
     }
     bsync();
     if (sh.flags) return LUNSUP;
@@ -365,7 +374,9 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, const hm_do
             any_list = true;
             if (X.insmin[o.reg] != key + 1)
                 atomicMin(&sh.errkey, err_key((uint32_t)(key >> 32), (uint32_t)key + 1, ci, HM_ERR_DUPLICATE_ELEM));
-            if (o.parent != HM_HEAD && !(X.insmin[o.parent] <= key)) atomicOr(&sh.flags, LF_UNSUPPORTED);
+            // engine envelope, ordered like a throw: insert after an element not yet inserted
+            if (o.parent != HM_HEAD && !(X.insmin[o.parent] <= key))
+                atomicMin(&sh.errkey, err_key((uint32_t)(key >> 32), (uint32_t)key + 1, ci, HM_ERR_UNSUPPORTED));
             continue;
         }
         any_list |= is_list;
@@ -600,6 +611,7 @@ __global__ __launch_bounds__(LWG) void merge_large_kernel(SmallParams p, uint8_t
             r.err_change = (uint32_t)((ek >> 8) & 0xFFFFF);
             const uint32_t opp1 = (uint32_t)((ek >> 28) & 0xFFFF);
             r.err_op = opp1 ? opp1 - 1 : HM_NONE;
+            if (r.status == HM_ERR_UNSUPPORTED) { r.err_change = HM_NONE; r.err_op = HM_NONE; }
         } else if (oc == LUNSUP) {
             r.status = HM_ERR_UNSUPPORTED;
         } else {

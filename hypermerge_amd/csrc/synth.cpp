@@ -215,7 +215,7 @@ struct Gen {
             }
             produce(a, std::move(ops));
         }
-        d.n_regs = K; d.n_objs = 1;
+        d.n_regs = K; d.n_objs = 1; d.flags = ncounter ? HM_DOC_HAS_COUNTERS : 0;
     }
 
     // ---------------- kind 1: text (C3) ----------------

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define HM_ABI_VERSION 1u
+#define HM_ABI_VERSION 2u
 
 /* ------------------------------------------------------------------ */
 /* Status codes                                                        */
@@ -99,7 +99,8 @@ typedef struct {
     uint16_t flags;       /* HM_DOC_* bits set by the encoder */
     uint32_t reserved[2];
 } hm_doc_row;
-#define HM_DOC_HAS_LISTS 1u   /* the doc creates a list/text object (launch sizing hint only) */
+#define HM_DOC_HAS_LISTS 1u     /* the doc creates a list/text object (launch sizing hint only) */
+#define HM_DOC_HAS_COUNTERS 2u  /* the doc has counter sets or incs (launch sizing hint only) */
 
 /* One row per change (24 B), in the order the changes are handed over. */
 typedef struct {
@@ -140,7 +141,7 @@ typedef struct {
      * computed by the engine from the doc table */
     uint32_t max_changes, max_ops, max_regs, max_objs;
     uint32_t doc_flags;   /* OR of every docs[d].flags (launch hint; 0 when unknown -> computed) */
-    uint32_t pad;
+    uint32_t max_deps;    /* max docs[d].n_deps (launch hint, sizes the LDS dep table) */
     const hm_doc_row    *docs;
     const hm_change_row *changes;
     const hm_dep_row    *deps;

@@ -297,7 +297,7 @@ static void apply_change(docst_t *s, uint32_t ci) {
             if (s->insertion[op->reg] != NONE) { err = HM_ERR_DUPLICATE_ELEM; break; }
             /* engine envelope (not a reference rule): an element must be inserted after
              * an element that already exists; otherwise getPrevious may throw later */
-            if (op->parent != HM_HEAD && s->insertion[op->parent] == NONE) { s->unsupported = 1; break; }
+            if (op->parent != HM_HEAD && s->insertion[op->parent] == NONE) { fail(s, HM_ERR_UNSUPPORTED, ci, j); return; }
             s->reg_obj[op->reg] = op->obj;
             u32_push(&s->following[op->parent == HM_HEAD ? s->doc->n_regs + op->obj : op->parent], k);
             s->insertion[op->reg] = k;
@@ -343,6 +343,15 @@ static void merge_doc(const hm_batch *b, const hm_results *out, uint32_t d) {
     s.op_actor = (uint32_t *)malloc((m ? m : 1) * 4);
     s.kids = (uint32_t *)malloc((m ? m : 1) * 4);
     for (uint32_t k = 0; k < m; k++) { s.op_change[k] = NONE; s.op_actor[k] = 0; }
+    /* engine envelope: op and dep rows grouped by change in arrival order, without gaps
+     * (the layout include/hypermerge_amd.h prescribes) */
+    uint32_t op_next = s.doc->op_off, dep_next = s.doc->dep_off;
+    for (uint32_t i = 0; i < n; i++) {
+        const hm_change_row *c = CH(&s, i);
+        if (c->op_first != op_next || c->dep_off != dep_next) s.unsupported = 1;
+        op_next = c->op_first + c->n_ops; dep_next = c->dep_off + c->n_deps;
+    }
+    if (op_next != s.doc->op_off + m || dep_next != s.doc->dep_off + s.doc->n_deps) s.unsupported = 1;
     for (uint32_t i = 0; i < n; i++) {
         const hm_change_row *c = CH(&s, i);
         if (c->actor >= s.A || c->seq == 0) s.unsupported = 1;
@@ -352,6 +361,16 @@ static void merge_doc(const hm_batch *b, const hm_results *out, uint32_t d) {
             if (k < m) { s.op_change[k] = i; s.op_actor[k] = c->actor; } else s.unsupported = 1;
         }
         out->hist[s.doc->change_off + i] = -1;
+    }
+    /* engine envelope: malformed op rows (ids outside the doc's tables, unknown actions)
+     * put the whole document outside, whatever would throw first */
+    for (uint32_t k = 0; k < m; k++) {
+        const hm_op_row *op = OP(&s, k);
+        if (op->action <= HM_MAKE_TEXT) { if (op->obj >= O) s.unsupported = 1; }
+        else if (op->action <= HM_INC) {
+            if (op->reg >= R) s.unsupported = 1;
+            if (op->action == HM_INS && op->parent != HM_HEAD && op->parent >= R) s.unsupported = 1;
+        } else s.unsupported = 1;
     }
 
     uint32_t qn = 0;

@@ -129,3 +129,53 @@ CASES = [
     ("rga_missing_elem", [ch(A, 1, {}, mk("makeList", "L"), s(f"{A}:9", "q", obj="L"))],
      {"status": "MISSING_ELEM", "error_at": [0, 1]}),
 ]
+
+
+# ---------------------------------------------------------------------------
+# Engine-envelope precedence (not Automerge rules; DESIGN.md "Envelope").
+# An insert after an element that is not yet inserted is ordered like a throw:
+# the first event in (history position, op) order wins.  Malformed rows
+# (ids outside the doc's tables, gaps/overlaps in the change->op/dep layout)
+# put the whole document outside, whatever would throw first.
+# Each case: (name, changes, mutate(batch) or None, expected summary subset).
+# ---------------------------------------------------------------------------
+def _orphan_reg_in_queued(b):
+    # the queued change's op names a register past the doc's table
+    b.ops["reg"][len(b.ops) - 1] = int(b.docs["n_regs"][0]) + 5
+
+
+def _op_gap(b):
+    b.changes["n_ops"][0] = 0          # op 0 belongs to no change
+
+
+def _op_overlap(b):
+    b.changes["op_first"][1] = b.changes["op_first"][0]
+
+
+ENVELOPE_CASES = [
+    ("orphan_insert_after_error",
+     [ch(A, 1, {}, mk("makeList", "L"), ins("L", "_head", 1), mk("makeMap", "M")),
+      ch(A, 2, {}, mk("makeMap", "M")),
+      ch(A, 3, {}, ins("L", "zzzz:99", 5))],
+     None, {"status": "DUPLICATE_OBJECT", "error_at": [1, 0]}),
+    ("orphan_insert_before_error",
+     [ch(A, 1, {}, mk("makeList", "L"), ins("L", "zzzz:99", 1)),
+      ch(A, 2, {}, mk("makeMap", "M"), mk("makeMap", "M"))],
+     None, {"status": "UNSUPPORTED"}),
+    ("orphan_insert_then_error_same_change",
+     [ch(A, 1, {}, mk("makeList", "L"), ins("L", "zzzz:5", 1), mk("makeList", "L"))],
+     None, {"status": "UNSUPPORTED"}),
+    ("duplicate_elem_outranks_orphan_on_same_op",
+     [ch(A, 1, {}, mk("makeList", "L"), ins("L", "_head", 1)),
+      ch(A, 2, {}, ins("L", "zzzz:9", 1))],
+     None, {"status": "DUPLICATE_ELEM", "error_at": [1, 0]}),
+    ("malformed_register_in_queued_change",
+     [ch(A, 1, {}, s("x", 1)), ch(B, 2, {}, s("y", 2))],
+     _orphan_reg_in_queued, {"status": "UNSUPPORTED"}),
+    ("malformed_op_gap",
+     [ch(A, 1, {}, s("x", 1)), ch(A, 2, {}, s("y", 2))],
+     _op_gap, {"status": "UNSUPPORTED"}),
+    ("malformed_op_overlap",
+     [ch(A, 1, {}, s("x", 1)), ch(A, 2, {}, s("y", 2))],
+     _op_overlap, {"status": "UNSUPPORTED"}),
+]

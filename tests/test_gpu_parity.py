@@ -7,10 +7,10 @@ import pytest
 
 from hypermerge_amd import synth
 from hypermerge_amd.columnar import encode
-from hypermerge_amd.render import canonical_json
+from hypermerge_amd.render import canonical_json, doc_summary
 import oracle.oracle as O
 
-from kat_cases import CASES
+from kat_cases import CASES, ENVELOPE_CASES
 
 pytestmark = pytest.mark.gpu
 
@@ -121,3 +121,18 @@ def test_empty_and_single(engine):
             [{"actor": "a", "seq": 1, "deps": {}, "ops": [{"action": "set", "obj": R, "key": "k", "value": 1}]}]]
     b = encode(docs)
     assert_same(b, engine.merge(b), O.merge(b))
+
+
+@pytest.mark.parametrize("general", [False, True], ids=["small", "general"])
+@pytest.mark.parametrize("name,changes,mutate,expect", ENVELOPE_CASES, ids=[c[0] for c in ENVELOPE_CASES])
+def test_envelope_precedence_on_gpu(engine, engine_general, general, name, changes, mutate, expect):
+    """Status (UNSUPPORTED included) and error position equal the oracle's exactly."""
+    b = encode([changes])
+    if mutate:
+        mutate(b)
+    g = (engine_general if general else engine).merge(b)
+    o = O.merge(b)
+    assert canonical_json(b, g, 0) == canonical_json(b, o, 0)
+    got = doc_summary(b, g, 0)
+    for k, v in expect.items():
+        assert got.get(k) == v, (name, k, got)

@@ -7,7 +7,7 @@ from hypermerge_amd.columnar import encode
 from hypermerge_amd.render import doc_summary
 import oracle.oracle as O
 
-from kat_cases import CASES
+from kat_cases import CASES, ENVELOPE_CASES
 
 
 @pytest.mark.parametrize("name,changes,expect", CASES, ids=[c[0] for c in CASES])
@@ -50,3 +50,13 @@ def test_oracle_envelope_flags():
         {"action": "makeList", "obj": "L"}, {"action": "ins", "obj": "L", "key": "a:7", "elem": 8}]}]
     b = encode([changes])
     assert doc_summary(b, O.merge(b), 0)["status"] == "UNSUPPORTED"
+
+
+@pytest.mark.parametrize("name,changes,mutate,expect", ENVELOPE_CASES, ids=[c[0] for c in ENVELOPE_CASES])
+def test_oracle_envelope_precedence(name, changes, mutate, expect):
+    b = encode([changes])
+    if mutate:
+        mutate(b)
+    got = doc_summary(b, O.merge(b), 0)
+    for k, v in expect.items():
+        assert got.get(k) == v, (name, k, got)
