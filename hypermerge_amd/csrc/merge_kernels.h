@@ -19,8 +19,7 @@ struct SmallParams {
     uint32_t cap_regs, cap_objs;     // LDS carve of this launch (set by the kernel's size class)
     uint32_t cap_deps;               // dep rows per document the carve holds
     uint32_t counters;               // the carve has the counter sums (HM_DOC_HAS_COUNTERS)
-    uint32_t *defer_list;            // documents handed to merge_large_kernel
-    uint32_t *defer_count;
+    uint32_t *large_cursor;          // merge_large_kernel's chunk cursor (zeroed before the launch)
     uint32_t general_only;           // HM_CFG_GENERAL_ONLY: defer every document
 };
 

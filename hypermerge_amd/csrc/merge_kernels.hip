@@ -37,7 +37,8 @@
 #include "merge_kernels.h"
 
 #ifndef HM_ABLATE
-#define HM_ABLATE 0     // dev-only timing builds: 1 skip ancestor push, 2 stop after K1, 4 stop after K2 survivors
+#define HM_ABLATE 0     // dev-only timing builds: 1 skip ancestor push, 2 stop after K1, 4 stop after K2 survivors,
+                        // 8 stop right after staging
 #endif
 #ifndef HM_WAVES_PER_EU
 #define HM_WAVES_PER_EU 4   // register-allocator target: LDS already caps C4-class launches at ~4.25 waves/SIMD
@@ -88,7 +89,7 @@ __device__ __forceinline__ u64 err_key(uint32_t h, uint32_t op_plus1, uint32_t a
 }
 
 struct SmallLds {
-    LDS u64 *anc, *chain, *segor, *errkey, *opval;
+    LDS u64 *anc, *chain, *segor, *errkey, *cov, *opval;
     LDS int64_t *survsum;           // counter launches only
     LDS uint2 *cw0, *cw1, *cw2;     // staged change rows (three 8-byte words, conflict-free)
     LDS uint32_t *first, *base, *bclock, *headv, *objslot, *segcnt, *survcnt, *regoff, *regobj, *insmin;
@@ -122,7 +123,7 @@ __host__ __device__ inline size_t small_carve(P base, uint32_t NOp, uint32_t NR,
     size_t o = 0;
 #define TAKE(f, T, cnt) do { L->f = (decltype(L->f))(base + o); o = (o + (size_t)(cnt) * sizeof(T) + 15) & ~(size_t)15; } while (0)
     TAKE(anc, u64, 64);          TAKE(chain, u64, NA_MAX);     TAKE(segor, u64, NR);
-    TAKE(errkey, u64, 1);        TAKE(opval, u64, NOp);
+    TAKE(errkey, u64, 1);        TAKE(cov, u64, 1);            TAKE(opval, u64, NOp);
     TAKE(cw0, uint2, 64);        TAKE(cw1, uint2, 64);         TAKE(cw2, uint2, 64);
     TAKE(first, uint32_t, NA_MAX * 64 > 2 * NOp ? NA_MAX * 64 : 2 * NOp);
     L->seglist = L->first; L->survp = L->first + NOp;
@@ -451,12 +452,13 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     st.hist = -1; st.H = 0; st.total = 0; st.doc_lists = false;
 
     // ---------------- the staged rows (lane = arrival index) ----------------
+    if (HM_ABLATE & 8) return OUT_UNSUPPORTED;
     const bool act = lane < n;
     const hm_change_row c = act ? change_of(L.cw0[lane], L.cw1[lane], L.cw2[lane])
                                 : change_of(make_uint2(0, 0), make_uint2(0, 0), make_uint2(0, 0));
     for (uint32_t i = lane; i < NA_MAX * 64; i += WAVE) L.first[i] = 0xFFFFFFFFu;
     if (lane < NA_MAX) { L.base[lane] = 0xFFFFFFFFu; L.bclock[lane] = 0; L.headv[lane] = 0; L.chain[lane] = 0; }
-    if (lane == 0) { *L.errkey = ~0ull; *L.flags = 0; }
+    if (lane == 0) { *L.errkey = ~0ull; *L.flags = 0; *L.cov = 0; }
     const uint32_t dep_lo = doc.dep_off, ndep = doc.n_deps;
     wave_sync();
     const uint32_t actor = c.actor, seq = c.seq;
@@ -620,18 +622,33 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
             if (j != hpred) Dnp |= bit;
         }
     }
-    u64 anc = 0, covered = 0;                             // covered = union of all ancestor sets
-    for (uint32_t k = 0; k < ((HM_ABLATE & 1) ? 0u : H); k++) {   // lane k is final when the push reaches it
-        const u64 ak = readlane64(anc, (int)k);
-        covered |= ak;
-        if ((D >> k) & 1) anc |= ak | (1ull << k);
+    // covered = union of all ancestor sets = union of the direct deps (every ancestor is
+    // some change's direct dep); chains = history positions of each actor
+    if (hv) { lds_or(L.cov, D); lds_or(&L.chain[hactor], 1ull << lane); }
+    // ancestors-or-self, pushed in history order: lane k is final when the sweep reaches it.
+    // Per step: v_readlane of lane k, bit k of D as an all-ones mask (v_bfe_i32), v_and_or.
+    // Positions below 32 only have low-word ancestors.
+    uint32_t alo = hv && lane < 32 ? 1u << lane : 0u, ahi = hv && lane >= 32 ? 1u << (lane - 32) : 0u;
+    {
+        const uint32_t Hs = (HM_ABLATE & 1) ? 0u : (uint32_t)__builtin_amdgcn_readfirstlane((int)H);
+        const uint32_t Dlo = (uint32_t)D, Dhi = (uint32_t)(D >> 32);
+        const uint32_t H1 = Hs < 32 ? Hs : 32;
+#define PUSH_LO(k) alo |= (uint32_t)__builtin_amdgcn_readlane((int)alo, (int)(k)) & (uint32_t)__builtin_amdgcn_sbfe((int)Dlo, (k), 1)
+#define PUSH_HI(k) do { const uint32_t m_ = (uint32_t)__builtin_amdgcn_sbfe((int)Dhi, (k) - 32, 1);          \
+                        alo |= (uint32_t)__builtin_amdgcn_readlane((int)alo, (int)(k)) & m_;              \
+                        ahi |= (uint32_t)__builtin_amdgcn_readlane((int)ahi, (int)(k)) & m_; } while (0)
+        uint32_t k = 0;                                   // wave-uniform: manual 4x unroll
+        for (; k + 4 <= H1; k += 4) { PUSH_LO(k); PUSH_LO(k + 1); PUSH_LO(k + 2); PUSH_LO(k + 3); }
+        for (; k < H1; k++) PUSH_LO(k);
+        for (k = 32; k + 2 <= Hs; k += 2) { PUSH_HI(k); PUSH_HI(k + 1); }
+        for (; k < Hs; k++) PUSH_HI(k);
+#undef PUSH_LO
+#undef PUSH_HI
     }
+    const u64 anc = hv ? ((((u64)ahi << 32) | alo) & ~(1ull << lane)) : 0ull;   // strict ancestors
     if (hv) L.anc[lane] = anc;
-    for (uint32_t a = 0; a < A; a++) {
-        const u64 ch = __ballot(hv && hactor == a);
-        if (lane == 0) L.chain[a] = ch;
-    }
     wave_sync();
+    const u64 covered = *L.cov;
     // transitiveDeps folds deps.set(actor, seq-1) in key order: acc = max(acc, FC(d)); acc[a_d] = s_d.
     // The `.set` can LOWER acc[a_d] when an earlier entry already knows a later change of a_d;
     // compare that literal fold with the closure and leave the envelope only when they differ.
@@ -900,12 +917,11 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
         return;
     }
     if (oc == OUT_UNSUPPORTED) {
-        // outside this kernel's envelope: merge_large_kernel takes the document
+        // outside this kernel's envelope: merge_large_kernel finds the status and takes the document
         if (lane == 0) {
             hm_doc_result r = {};
             r.status = HM_DEFERRED; r.err_change = HM_NONE; r.err_op = HM_NONE;
             *dres = r;
-            p.defer_list[atomicAdd(p.defer_count, 1u)] = d;
         }
         return;
     }
@@ -923,13 +939,20 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
         rr.list_index = (LISTS && st.doc_lists) ? (int32_t)L.insmin[r] : -1;
         p.res_regs[doc.reg_off + r] = rr;
     }
-    // allDeps rows, coalesced: word w = (change w/S, actor w%S)
-    for (uint32_t w = lane; w < n * S; w += WAVE) {
-        const uint32_t ci = w / S, a = w - ci * S;
-        const int32_t h = L.hist_of[ci];
-        uint32_t v = 0;
-        if (h >= 0 && a < A) v = (uint32_t)__popcll(L.anc[h] & L.chain[a]);
-        p.res_all_deps[(size_t)doc.change_off * S + w] = v;
+    // allDeps rows: lane = arrival index writes its change's row (zeros if not applied;
+    // chain[a] is empty for a >= A)
+    if (lane < n) {
+        const u64 an = st.hist >= 0 ? L.anc[st.hist] : 0ull;
+        uint32_t *row = p.res_all_deps + (size_t)(doc.change_off + lane) * S;
+        if (S == 8 || S == 4) {
+            uint32_t v[NA_MAX];
+#pragma unroll
+            for (int a = 0; a < NA_MAX; a++) v[a] = (uint32_t)__popcll(an & L.chain[a]);
+            reinterpret_cast<uint4 *>(row)[0] = make_uint4(v[0], v[1], v[2], v[3]);
+            if (S == 8) reinterpret_cast<uint4 *>(row)[1] = make_uint4(v[4], v[5], v[6], v[7]);
+        } else {
+            for (uint32_t a = 0; a < S; a++) row[a] = a < NA_MAX ? (uint32_t)__popcll(an & L.chain[a]) : 0u;
+        }
     }
     uint32_t bc = 0, mc = 0;
     if (lane < S) {

@@ -595,9 +595,22 @@ __global__ __launch_bounds__(LWG) void merge_large_kernel(SmallParams p, uint8_t
     __shared__ Shared sh;
     const uint32_t tid = threadIdx.x;
     const uint32_t S = p.a_stride;
-    const uint32_t n_def = *p.defer_count;               // documents the small kernel deferred
-    for (uint32_t di = blockIdx.x; di < n_def; di += gridDim.x) {
-        const uint32_t d = p.defer_list[di];
+    // Deferred documents carry status HM_DEFERRED (written by merge_small_kernel).  Workgroups
+    // claim chunks of LWG result rows from a cursor, compact the deferred ones in LDS and
+    // merge them: one atomic per chunk instead of one per document.
+    __shared__ uint32_t chunk_docs[LWG];
+    __shared__ uint32_t chunk_id, chunk_n;
+    for (;;) {
+        if (tid == 0) { chunk_id = atomicAdd(p.large_cursor, 1u); chunk_n = 0; }
+        bsync();
+        const size_t c0 = (size_t)chunk_id * LWG;
+        if (c0 >= p.n_docs) break;
+        if (c0 + tid < p.n_docs && p.res_docs[c0 + tid].status == HM_DEFERRED)
+            chunk_docs[atomicAdd(&chunk_n, 1u)] = (uint32_t)(c0 + tid);
+        bsync();
+        const uint32_t cn = chunk_n;
+        for (uint32_t ci = 0; ci < cn; ci++) {
+        const uint32_t d = chunk_docs[ci];
         bsync();
         const hm_doc_row doc = p.docs[d];
         int32_t H = 0;
@@ -637,6 +650,8 @@ __global__ __launch_bounds__(LWG) void merge_large_kernel(SmallParams p, uint8_t
             p.res_back_clock[(size_t)d * S + tid] = ok && ar ? sh.bclock[tid] : 0u;
         }
         if (tid == 0) p.res_docs[d] = r;
+        bsync();
+        }
         bsync();
     }
 }
