@@ -13,8 +13,8 @@ CSRC = os.path.join(HERE, "csrc")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("HM_OFFLOAD_ARCH", "gfx950")
 
-GPU_SRCS = ["merge_kernels.hip", "merge_large.hip", "engine.cpp"]
-GPU_DEPS = GPU_SRCS + ["merge_kernels.h", "../../include/hypermerge_amd.h"]
+GPU_SRCS = ["merge_kernels.hip", "merge_large.hip", "store_kernels.hip", "engine.cpp", "store.cpp"]
+GPU_DEPS = GPU_SRCS + ["merge_kernels.h", "store_kernels.h", "engine_internal.h", "../../include/hypermerge_amd.h"]
 
 
 def _stale(out: str, deps) -> bool:
@@ -30,11 +30,18 @@ def _run(cmd) -> None:
 
 
 def build_gpu(force: bool = False) -> str:
+    """One object per source (compiled in parallel), then one shared library."""
     out = os.path.join(LIBDIR, "libhmgpu.so")
     if force or _stale(out, GPU_DEPS):
-        os.makedirs(LIBDIR, exist_ok=True)
-        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-              "-o", out] + [os.path.join(CSRC, s) for s in GPU_SRCS])
+        from concurrent.futures import ThreadPoolExecutor
+        objdir = os.path.join(LIBDIR, "obj")
+        os.makedirs(objdir, exist_ok=True)
+        flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall"]
+        objs = [os.path.join(objdir, s + ".o") for s in GPU_SRCS]
+        with ThreadPoolExecutor(min(8, len(GPU_SRCS))) as ex:
+            list(ex.map(lambda so: _run([HIPCC] + flags + ["-c", "-o", so[1], os.path.join(CSRC, so[0])]),
+                        zip(GPU_SRCS, objs)))
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs)
     return out
 
 

@@ -309,3 +309,71 @@ def encode(docs: Sequence[Sequence[Dict[str, Any]]], a_stride: Optional[int] = N
     for d in docs:
         bb.add_doc(d)
     return bb.build(a_stride)
+
+
+def decode_doc(b: Batch, d: int) -> List[Dict[str, Any]]:
+    """Columnar rows of document d -> Automerge 0.12 ``Change`` dicts (test/bench
+    utility: turns synthetic feeds into the JSON the host encoders take).  Names
+    are synthesised where the batch carries no string tables: actor ids that sort
+    in rank order, object UUIDs, map keys ``k<reg>``, string values ``s<id>``."""
+    doc = b.docs[d]
+    c0, n = int(doc["change_off"]), int(doc["n_changes"])
+    o0, m = int(doc["op_off"]), int(doc["n_ops"])
+    d0 = int(doc["dep_off"])
+    A = int(doc["n_actors"])
+    actors = b.doc_actors[d] if b.doc_actors else [f"actor{r:03d}" for r in range(A)]
+    objs = b.doc_objs[d] if b.doc_objs else [ROOT_ID] + [f"{i:08x}-0000-4000-8000-{d:012x}" for i in range(1, int(doc["n_objs"]))]
+    ops = b.ops[o0: o0 + m]
+    chs = b.changes[c0: c0 + n]
+    regkey: Dict[int, str] = {}
+    if b.doc_regs:
+        for g, (_, k) in enumerate(b.doc_regs[d]):
+            regkey[g] = k
+    else:
+        for ch in chs:                                   # element registers: actor:elem of their ins
+            s = int(ch["op_first"]) - o0
+            for op in ops[s: s + int(ch["n_ops"])]:
+                if op["action"] == INS:
+                    regkey.setdefault(int(op["reg"]), f"{actors[int(ch['actor'])]}:{int(op['elem'])}")
+
+    def key_of(reg: int) -> str:
+        return regkey.get(reg, f"k{reg}")
+
+    def val(op) -> Any:
+        vt, v = int(op["vtag"]), int(op["value"])
+        if vt == V_NULL:
+            return None
+        if vt in (V_FALSE, V_TRUE):
+            return vt == V_TRUE
+        if vt == V_INT:
+            return v - (1 << 64) if v >= (1 << 63) else v
+        if vt == V_FLOAT:
+            return float(np.array([v], "<u8").view("<f8")[0])
+        if vt == V_STR:
+            return b.strings[v] if b.strings else f"s{v}"
+        return objs[v]
+
+    out = []
+    for ch in chs:
+        deps = {actors[int(x["actor"])]: int(x["seq"])
+                for x in b.deps[int(ch["dep_off"]): int(ch["dep_off"]) + int(ch["n_deps"])]}
+        s = int(ch["op_first"]) - o0
+        jops = []
+        for op in ops[s: s + int(ch["n_ops"])]:
+            a = int(op["action"])
+            j: Dict[str, Any] = {"action": ACTION_NAMES[a], "obj": objs[int(op["obj"])]}
+            if a == INS:
+                p = int(op["parent"])
+                j["key"] = "_head" if p == HEAD else key_of(p)
+                j["elem"] = int(op["elem"])
+            elif a in (SET, DEL, LINK, INC):
+                j["key"] = key_of(int(op["reg"]))
+                if a == LINK:
+                    j["value"] = objs[int(op["value"])]
+                elif a != DEL:
+                    j["value"] = val(op)
+                if op["datatype"]:
+                    j["datatype"] = {DT_COUNTER: "counter", DT_TIMESTAMP: "timestamp"}[int(op["datatype"])]
+            jops.append(j)
+        out.append({"actor": actors[int(ch["actor"])], "seq": int(ch["seq"]), "deps": deps, "ops": jops})
+    return out

@@ -12,6 +12,7 @@
 #include <new>
 #include "../../include/hypermerge_amd.h"
 #include "merge_kernels.h"
+#include "engine_internal.h"
 
 struct hm_engine {
     int device = 0;
@@ -58,7 +59,7 @@ Caps launch_caps(const hm_batch *b) {
     return c;
 }
 
-int launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, hipStream_t s) {
+int launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, hipStream_t s, const uint32_t *doc_slot = nullptr) {
     Caps c = launch_caps(b);
     SmallParams p;
     p.docs = b->docs; p.changes = b->changes; p.deps = b->deps; p.ops = b->ops; p.min_clock = b->min_clock;
@@ -67,6 +68,7 @@ int launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, hipStream
     p.n_docs = b->n_docs; p.a_stride = b->a_stride; p.cap_regs = 0; p.cap_objs = 0; p.cap_deps = 0;
     p.counters = c.counters ? 1u : 0u;
     p.general_only = (e->flags & HM_CFG_GENERAL_ONLY) ? 1u : 0u;
+    p.doc_slot = doc_slot;
     if (b->n_docs == 0) { e->n_last = 0; return HM_OK; }
     // scratch: [counters 256 B: large-kernel chunk cursor, pool bump pointer][large-kernel pool]
     const size_t pool_bytes = hm_large_scratch_bound(b);
@@ -104,6 +106,14 @@ int check_batch(hm_engine *e, const hm_batch *b) {
 }
 
 }  // namespace
+
+// ---- internal interface for store.cpp (engine_internal.h) ----
+int hm_engine_launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, const uint32_t *doc_slot) {
+    return launch_merge(e, b, o, e->stream, doc_slot);
+}
+hipStream_t hm_engine_stream(hm_engine *e) { return e->stream; }
+int hm_engine_device(hm_engine *e) { return e->device; }
+int hm_engine_fail(hm_engine *e, int status, const char *msg) { return fail(e, status, msg); }
 
 extern "C" {
 

@@ -1,0 +1,11 @@
+// engine_internal.h — what store.cpp needs from the engine (not part of the C-ABI)
+#pragma once
+#include <hip/hip_runtime.h>
+#include "../../include/hypermerge_amd.h"
+
+// launch the merge kernels on the engine stream; doc_slot maps launch rows to the rows of
+// the per-document outputs (NULL = identity)
+int hm_engine_launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, const uint32_t *doc_slot);
+hipStream_t hm_engine_stream(hm_engine *e);
+int hm_engine_device(hm_engine *e);
+int hm_engine_fail(hm_engine *e, int status, const char *msg);

@@ -21,7 +21,12 @@ struct SmallParams {
     uint32_t counters;               // the carve has the counter sums (HM_DOC_HAS_COUNTERS)
     uint32_t *large_cursor;          // merge_large_kernel's chunk cursor (zeroed before the launch)
     uint32_t general_only;           // HM_CFG_GENERAL_ONLY: defer every document
+    const uint32_t *doc_slot;        // optional: launch row d -> row of the per-document outputs
+                                     // (res_docs, clocks, heads, min_clock); NULL = identity
 };
+#ifdef __HIPCC__
+__device__ __forceinline__ uint32_t hm_slot(const SmallParams &p, uint32_t d) { return p.doc_slot ? p.doc_slot[d] : d; }
+#endif
 
 // internal: the small kernel hands a document to merge_large_kernel (never returned to callers)
 #define HM_DEFERRED 0x7FFFFFFF

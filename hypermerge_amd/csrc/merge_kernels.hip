@@ -901,7 +901,8 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
     const uint32_t lane = threadIdx.x;
     const uint32_t S = p.a_stride;
     const uint32_t n = doc.n_changes, A = doc.n_actors, R = doc.n_regs;
-    hm_doc_result *dres = p.res_docs + d;
+    const uint32_t ds = hm_slot(p, d);      // row of the per-document outputs
+    hm_doc_result *dres = p.res_docs + ds;
     if (oc == OUT_ERROR) {
         // an Automerge throw aborted this document's Backend.applyChanges
         const u64 ek = *L.errkey;
@@ -957,11 +958,11 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
     uint32_t bc = 0, mc = 0;
     if (lane < S) {
         const bool ar = lane < A;
-        p.res_clock[(size_t)d * S + lane] = ar ? (uint32_t)__popcll(L.chain[lane]) : 0u;
-        p.res_heads[(size_t)d * S + lane] = ar ? L.headv[lane] : 0u;
+        p.res_clock[(size_t)ds * S + lane] = ar ? (uint32_t)__popcll(L.chain[lane]) : 0u;
+        p.res_heads[(size_t)ds * S + lane] = ar ? L.headv[lane] : 0u;
         bc = ar ? L.bclock[lane] : 0u;
-        p.res_back_clock[(size_t)d * S + lane] = bc;              // DocBackend.clock (queued included)
-        if (p.min_clock) mc = p.min_clock[(size_t)d * S + lane];
+        p.res_back_clock[(size_t)ds * S + lane] = bc;              // DocBackend.clock (queued included)
+        if (p.min_clock) mc = p.min_clock[(size_t)ds * S + lane];
     }
     const bool aGTE = __ballot(lane < S && bc < mc) == 0;
     const bool bGTE = __ballot(lane < S && mc < bc) == 0;

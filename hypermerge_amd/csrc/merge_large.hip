@@ -605,7 +605,7 @@ __global__ __launch_bounds__(LWG) void merge_large_kernel(SmallParams p, uint8_t
         bsync();
         const size_t c0 = (size_t)chunk_id * LWG;
         if (c0 >= p.n_docs) break;
-        if (c0 + tid < p.n_docs && p.res_docs[c0 + tid].status == HM_DEFERRED)
+        if (c0 + tid < p.n_docs && p.res_docs[hm_slot(p, (uint32_t)(c0 + tid))].status == HM_DEFERRED)
             chunk_docs[atomicAdd(&chunk_n, 1u)] = (uint32_t)(c0 + tid);
         bsync();
         const uint32_t cn = chunk_n;
@@ -613,6 +613,7 @@ __global__ __launch_bounds__(LWG) void merge_large_kernel(SmallParams p, uint8_t
         const uint32_t d = chunk_docs[ci];
         bsync();
         const hm_doc_row doc = p.docs[d];
+        const uint32_t ds = hm_slot(p, d);
         int32_t H = 0;
         const Outcome oc = merge_doc_large(p, sh, doc, d, pool, pool_bytes, pool_used, H);
         bsync();
@@ -637,7 +638,7 @@ __global__ __launch_bounds__(LWG) void merge_large_kernel(SmallParams p, uint8_t
             bool ag = true, bg = true;
             for (uint32_t a = 0; a < S; a++) {
                 const uint32_t bc = a < doc.n_actors ? sh.bclock[a] : 0u;
-                const uint32_t mc = p.min_clock ? p.min_clock[(size_t)d * S + a] : 0u;
+                const uint32_t mc = p.min_clock ? p.min_clock[(size_t)ds * S + a] : 0u;
                 if (bc < mc) ag = false;
                 if (mc < bc) bg = false;
             }
@@ -645,11 +646,11 @@ __global__ __launch_bounds__(LWG) void merge_large_kernel(SmallParams p, uint8_t
         }
         if (tid < S) {
             const bool ok = oc == LOK, ar = tid < doc.n_actors;
-            p.res_clock[(size_t)d * S + tid] = ok && ar ? sh.clock[tid] : 0u;
-            p.res_heads[(size_t)d * S + tid] = ok && ar ? sh.headv[tid] : 0u;
-            p.res_back_clock[(size_t)d * S + tid] = ok && ar ? sh.bclock[tid] : 0u;
+            p.res_clock[(size_t)ds * S + tid] = ok && ar ? sh.clock[tid] : 0u;
+            p.res_heads[(size_t)ds * S + tid] = ok && ar ? sh.headv[tid] : 0u;
+            p.res_back_clock[(size_t)ds * S + tid] = ok && ar ? sh.bclock[tid] : 0u;
         }
-        if (tid == 0) p.res_docs[d] = r;
+        if (tid == 0) p.res_docs[ds] = r;
         bsync();
         }
         bsync();

@@ -21,7 +21,9 @@ LIB = os.environ.get("HMGPU_LIB") or os.path.join(_HERE, "_lib", "libhmgpu.so")
 EXPORTS = ("hm_abi_version", "hm_status_message", "hm_engine_create", "hm_engine_destroy",
            "hm_engine_last_error", "hm_merge_host", "hm_scratch_bytes", "hm_merge_device",
            "hm_last_kernel_ms", "hm_clock_cmp_device", "hm_clock_union_device",
-           "hm_clock_intersection_device")
+           "hm_clock_intersection_device", "hm_store_create", "hm_store_destroy", "hm_doc_open",
+           "hm_batch_submit", "hm_batch_wait", "hm_doc_info", "hm_doc_read", "hm_doc_log",
+           "hm_doc_history_prefix", "hm_doc_set_min_clock", "hm_store_clock_update", "hm_sync_ranges_device")
 
 _lib = None
 
@@ -58,6 +60,18 @@ def lib():
         L.hm_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
         for f in ("hm_clock_cmp_device", "hm_clock_union_device", "hm_clock_intersection_device"):
             getattr(L, f).argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 3 + [ctypes.c_uint32] * 2 + [ctypes.c_void_p]
+        vp, u32 = ctypes.c_void_p, ctypes.c_uint32
+        sig = {
+            "hm_store_create": [vp, vp, vp], "hm_store_destroy": [vp], "hm_doc_open": [vp, vp],
+            "hm_batch_submit": [vp, vp, vp, vp, vp], "hm_batch_wait": [vp, ctypes.c_uint64, vp, vp, vp, vp],
+            "hm_doc_info": [vp, u32, vp], "hm_doc_read": [vp, u32] + [vp] * 7, "hm_doc_log": [vp, u32, vp, vp, vp],
+            "hm_doc_history_prefix": [vp, u32, u32, vp], "hm_doc_set_min_clock": [vp, u32, vp],
+            "hm_store_clock_update": [vp, u32, vp, vp, vp, vp],
+            "hm_sync_ranges_device": [vp, vp, vp, vp, vp, vp, u32, vp],
+        }
+        for f, a in sig.items():
+            getattr(L, f).argtypes = a
+        L.hm_store_destroy.restype = None
         _lib = L
     return _lib
 

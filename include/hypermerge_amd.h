@@ -235,6 +235,105 @@ int hm_clock_union_device(hm_engine *e, const uint32_t *a, const uint32_t *b, ui
 int hm_clock_intersection_device(hm_engine *e, const uint32_t *a, const uint32_t *b, uint32_t *c,
                                  uint32_t n_docs, uint32_t a_stride, void *stream);
 
+/* ------------------------------------------------------------------ */
+/* Resident document store: the per-document Automerge BackendState    */
+/* (`DocBackend.back`, src/DocBackend.ts:50) kept on the device.       */
+/* ------------------------------------------------------------------ */
+/*
+ * Every open document owns device segments holding its change log (the
+ * change/dep/op rows of every change handed to applyChanges so far, in
+ * arrival order) and its merged state (history, allDeps, registers,
+ * survivors, clocks).  `Backend.applyChanges(back, changes)` is a left fold of
+ * addChange over `changes`, so applyChanges(applyChanges(s, A), B) is
+ * applyChanges(s, A ++ B): a submit appends each document's new rows to its
+ * log and re-merges the log with the batch kernels.  A document whose merge
+ * throws is rolled back to its previous log, exactly as a throwing
+ * applyChanges leaves `DocBackend.back` (and `DocBackend.clock`) unchanged
+ * (src/DocBackend.ts:170-184).
+ *
+ *   replaces: src/DocBackend.ts:144-167 init(changes)  (hm_doc_open + submit)
+ *             src/DocBackend.ts:115-117,169-185 applyRemoteChanges
+ *             src/DocBackend.ts:90-113 testMinimumClockSatisfied / updateMinimumClock
+ *             src/DocBackend.ts:135-142 updateClock (hm_batch_wait back_clock)
+ *             src/RepoBackend.ts:572-576 history.slice(0, n) (hm_doc_history_prefix)
+ *             src/ClockStore.ts:78-91 update (hm_store_clock_update)
+ *             src/RepoBackend.ts:506-531 syncChanges contiguity (hm_sync_ranges_device)
+ */
+typedef struct hm_store hm_store;
+
+typedef struct {
+    uint32_t a_stride;      /* per-actor row width of every document (1..32) */
+    uint32_t reserved;
+} hm_store_config;
+
+int  hm_store_create(hm_engine *e, const hm_store_config *cfg, hm_store **out);
+void hm_store_destroy(hm_store *s);
+
+/* A new, empty document (Backend.init()).  Handles are dense from 0. */
+int hm_doc_open(hm_store *s, uint32_t *out_doc);
+
+/* Append new changes to documents and re-merge them.  `b` is a batch in the
+ * hm_batch layout whose rows are only the NEW changes (offsets local to `b`);
+ * for each row i, docs[i].n_actors / n_regs / n_objs are document totals
+ * after the append and doc_handles[i] names the document (each at most once
+ * per batch).  actor_remap (optional, [n_docs * a_stride]) gives, for each row,
+ * the new rank of every previously used actor rank (identity rows allowed;
+ * NULL = no document's ranks moved) — ranks are actor-id string order, so a
+ * new actor can shift the ranks of the document's existing rows.
+ * Asynchronous: results are collected by hm_batch_wait.  One batch in flight. */
+int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
+                    const uint8_t *actor_remap, uint64_t *out_batch_id);
+
+/* Wait for a submitted batch; per batch row: the merge result of the
+ * document's whole log, and (each optional) its opSet.clock, DocBackend.clock
+ * and opSet.deps rows ([n_docs * a_stride]).  Documents whose merge threw are
+ * reported with their error status and rolled back before this returns. */
+int hm_batch_wait(hm_store *s, uint64_t batch_id, hm_doc_result *out_docs,
+                  uint32_t *out_clock, uint32_t *out_back_clock, uint32_t *out_heads);
+
+/* Sizes of a document's log and merged state. */
+typedef struct {
+    uint32_t n_changes, n_deps, n_ops, n_regs, n_objs, n_actors;
+    uint32_t hist_len, n_queued, n_surv;
+    int32_t  status;
+} hm_doc_info_t;
+int hm_doc_info(hm_store *s, uint32_t doc, hm_doc_info_t *out);
+
+/* Read a document's merged state (any pointer may be NULL):
+ * hist [n_changes], all_deps [n_changes*a_stride], regs [n_regs],
+ * surv [n_ops] (first n_surv valid), clock/back_clock/heads [a_stride]. */
+int hm_doc_read(hm_store *s, uint32_t doc, int32_t *hist, uint32_t *all_deps, hm_reg_result *regs,
+                hm_surv_result *surv, uint32_t *clock, uint32_t *back_clock, uint32_t *heads);
+
+/* The log rows of a document (debug / materialize): changes [n_changes]
+ * with dep_off/op_first local to the document, deps [n_deps], ops [n_ops]. */
+int hm_doc_log(hm_store *s, uint32_t doc, hm_change_row *changes, hm_dep_row *deps, hm_op_row *ops);
+
+/* history.slice(0, n): log indices of the first n applied changes, in history
+ * order (src/RepoBackend.ts:572-576).  Returns the count written (<= n). */
+int hm_doc_history_prefix(hm_store *s, uint32_t doc, uint32_t n, uint32_t *out_log_index);
+
+/* minimumClock row of a document (rank-indexed, 0 = absent); used for the
+ * min_cmp of the next merges (Clock.cmp(DocBackend.clock, minimumClock)). */
+int hm_doc_set_min_clock(hm_store *s, uint32_t doc, const uint32_t *clock);
+
+/* ClockStore.update(repoId=self, docId, doc.clock) for n documents
+ * (src/ClockStore.ts:78-91, called at src/RepoBackend.ts:343-345): the stored
+ * row becomes max(stored, DocBackend.clock) per entry.  out_written[i] = 1 if any
+ * stored entry changed (the rows SQLite must persist); out_differs[i] = 1 if
+ * !Clock.equal(input, stored) (ClockStore pushes updateQ).  out_stored
+ * (optional, [n*a_stride]) receives the stored rows. */
+int hm_store_clock_update(hm_store *s, uint32_t n, const uint32_t *docs, uint8_t *out_written,
+                          uint8_t *out_differs, uint32_t *out_stored);
+
+/* syncChanges contiguity (src/RepoBackend.ts:513-522) over many (doc, actor)
+ * pairs on the device: for pair i, walk seq indices j = lo[i] .. hi[i]-1 while
+ * bit j of the actor feed's present bitmap (words from present + word_off[i])
+ * is set; out_end[i] = first missing index (or hi[i]).  Device pointers. */
+int hm_sync_ranges_device(hm_engine *e, const uint64_t *present, const uint64_t *word_off,
+                          const uint32_t *lo, const uint32_t *hi, uint32_t *out_end, uint32_t n,
+                          void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,163 @@
+"""Resident document store (hm_store_* / hm_batch_submit / hm_batch_wait) vs the
+CPU restatement: documents receive their changes over several applyChanges calls
+(DocBackend.init, then applyRemoteChanges, src/DocBackend.ts:144-185); after every
+call the device state of each document must be bit-exact with the oracle's cold
+merge of that document's whole log, and its canonical rendering must equal the
+rendering of one cold applyChanges over the concatenated changes."""
+import numpy as np
+import pytest
+
+from hypermerge_amd import synth
+from hypermerge_amd import clock as C
+from hypermerge_amd.columnar import decode_doc, encode
+from hypermerge_amd.render import canonical_json
+from hypermerge_amd.store import DocStore
+import oracle.oracle as O
+
+from kat_cases import ch, s, d, ins, mk, link
+
+pytestmark = pytest.mark.gpu
+
+
+def assert_doc_matches_oracle(store, h):
+    b, g = store.read(h)
+    o = O.merge(b)
+    S = b.a_stride
+    assert int(g.docs["status"][0]) == int(o.docs["status"][0])
+    for f in ("hist_len", "n_queued", "n_surv"):
+        assert int(g.docs[f][0]) == int(o.docs[f][0]), f
+    for f in ("clock", "back_clock", "heads", "hist", "all_deps", "regs"):
+        np.testing.assert_array_equal(getattr(g, f), getattr(o, f), err_msg=f)
+    n = int(o.docs["n_surv"][0])
+    np.testing.assert_array_equal(g.surv[:n], o.surv[:n])
+    return b, g
+
+
+def split(changes, k, rng):
+    cuts = sorted(rng.integers(0, len(changes) + 1, size=k - 1)) if k > 1 else []
+    parts, prev = [], 0
+    for c in list(cuts) + [len(changes)]:
+        parts.append(changes[prev:c])
+        prev = c
+    return parts
+
+
+@pytest.mark.parametrize("name,n,rounds,extra", [
+    ("C4", 600, 4, {}),
+    ("C2", 400, 3, {}),
+    ("C5", 400, 5, {}),                                   # nested maps + lists, blocked + duplicate changes
+    ("C2", 300, 6, {"arrival": 2, "shuffle_pct": 30}),    # changes that wait in the queue across calls
+    ("C3", 40, 3, {"changes_per_actor": 40}),             # text documents (RGA)
+])
+def test_incremental_parity(engine, name, n, rounds, extra):
+    b = synth.generate(synth.config(name, n_docs=n, **extra))
+    docs = [decode_doc(b, i) for i in range(b.n_docs)]
+    rng = np.random.default_rng(7)
+    store = DocStore(engine, a_stride=8)
+    hs = [store.open() for _ in docs]
+    parts = [split(c, rounds, rng) for c in docs]
+    for rd in range(rounds):
+        items = [(h, parts[i][rd]) for i, h in enumerate(hs) if rd == 0 or parts[i][rd]]
+        res = store.apply(items)
+        assert (res.docs["status"] == 0).all(), res.docs["status"]
+        # the per-call results (RemotePatchMsg.history, DocBackend.clock) agree with the device state
+        for j in rng.choice(len(items), size=min(25, len(items)), replace=False):
+            h = items[j][0]
+            bb, g = assert_doc_matches_oracle(store, h)
+            assert int(res.docs["hist_len"][j]) == int(g.docs["hist_len"][0])
+            np.testing.assert_array_equal(res.back_clock[j], g.back_clock)
+    # final state: every document, and the rendering equals one cold applyChanges of all changes
+    cold = encode(docs, 8)
+    co = O.merge(cold)
+    for i, h in enumerate(hs):
+        bb, g = assert_doc_matches_oracle(store, h) if i % 7 == 0 else store.read(h)
+        assert canonical_json(bb, g, 0) == canonical_json(cold, co, i), i
+
+
+def test_new_actor_reranks_existing_rows(engine):
+    """An actor whose id sorts before the document's existing actors arrives later:
+    every earlier row is re-ranked on the device (actor order = string order)."""
+    R = "00000000-0000-0000-0000-000000000000"
+    store = DocStore(engine, a_stride=8)
+    h = store.open()
+    first = [ch("mmmm", 1, {}, s("x", 1)), ch("zzzz", 1, {}, s("x", 2)), ch("mmmm", 2, {"zzzz": 1}, s("y", 3))]
+    later = [ch("aaaa", 1, {}, s("x", 9)), ch("bbbb", 1, {"mmmm": 2}, s("y", 4))]
+    r1 = store.apply([(h, first)])
+    assert r1.docs["status"][0] == 0
+    r2 = store.apply([(h, later)])
+    assert r2.docs["status"][0] == 0
+    bb, g = assert_doc_matches_oracle(store, h)
+    cold = encode([first + later], 8)
+    assert canonical_json(bb, g, 0) == canonical_json(cold, O.merge(cold), 0)
+    assert store.enc[h].actors == ["aaaa", "bbbb", "mmmm", "zzzz"]
+    c, dp, op = store.log(h)
+    assert list(c["actor"]) == [2, 3, 2, 0, 1]
+
+
+def test_throwing_apply_rolls_back(engine):
+    """A mismatched duplicate throws 'Inconsistent reuse of sequence number': the
+    document keeps its previous state (DocBackend.back is not reassigned) and later
+    calls merge on top of that state."""
+    store = DocStore(engine, a_stride=8)
+    h, h2 = store.open(), store.open()
+    ok = [ch("aaaa", 1, {}, s("x", 1)), ch("bbbb", 1, {}, s("x", 2))]
+    r = store.apply([(h, ok), (h2, ok)])
+    assert (r.docs["status"] == 0).all()
+    before = canonical_json(*store.read(h), 0)
+    bad = [ch("cccc", 1, {}, s("z", 5)), ch("aaaa", 1, {}, s("x", 99))]       # seq 1 reused with new content
+    r = store.apply([(h, bad), (h2, [ch("cccc", 1, {}, s("w", 1))])])
+    assert r.docs["status"][0] == 1 and r.docs["status"][1] == 0
+    assert canonical_json(*store.read(h), 0) == before
+    assert store.info(h)["n_changes"] == 2 and store.enc[h].actors == ["aaaa", "bbbb"]
+    r = store.apply([(h, [ch("cccc", 1, {"aaaa": 1}, s("x", 3))])])
+    assert r.docs["status"][0] == 0
+    bb, g = assert_doc_matches_oracle(store, h)
+    cold = encode([ok + [ch("cccc", 1, {"aaaa": 1}, s("x", 3))]], 8)
+    assert canonical_json(bb, g, 0) == canonical_json(cold, O.merge(cold), 0)
+
+
+def test_arena_compaction_keeps_state(engine):
+    """Enough documents and growth to overflow the initial arenas several times."""
+    b = synth.generate(synth.config("C4", n_docs=3000))
+    docs = [decode_doc(b, i) for i in range(b.n_docs)]
+    store = DocStore(engine, a_stride=8)
+    hs = [store.open() for _ in docs]
+    for rd in range(4):
+        r = store.apply([(h, docs[i][rd * 16:(rd + 1) * 16]) for i, h in enumerate(hs)])
+        assert (r.docs["status"] == 0).all()
+    cold = encode(docs, 8)
+    co = O.merge(cold)
+    for i in range(0, len(hs), 97):
+        bb, g = assert_doc_matches_oracle(store, hs[i])
+        assert canonical_json(bb, g, 0) == canonical_json(cold, co, i)
+
+
+def test_min_clock_and_clock_store(engine):
+    """minimumClock comparison (DocBackend.testMinimumClockSatisfied) and the batched
+    ClockStore.update(self, doc, doc.clock) flags against src/Clock.ts semantics."""
+    store = DocStore(engine, a_stride=8)
+    hs = [store.open() for _ in range(3)]
+    peers = {hs[0]: {"aaaa": 2, "bbbb": 1}, hs[1]: {"aaaa": 1}, hs[2]: {"aaaa": 5, "cccc": 1}}
+    first = {hs[0]: [ch("aaaa", 1, {}, s("x", 1))],
+             hs[1]: [ch("aaaa", 1, {}, s("x", 1)), ch("aaaa", 2, {}, s("x", 2))],
+             hs[2]: [ch("aaaa", 1, {}, s("x", 1))]}
+    r = store.apply([(h, first[h]) for h in hs], extra_actors={h: list(peers[h]) for h in hs})
+    for h in hs:
+        store.set_min_clock(h, peers[h])
+    # the min_cmp of the first merge saw empty minimum clocks; merge again with no new changes
+    r = store.apply([(h, []) for h in hs])
+    for j, h in enumerate(hs):
+        bc = {a: int(v) for a, v in zip(store.enc[h].actors, r.back_clock[j]) if v}
+        exp = {"EQ": 0, "GT": 1, "LT": 2, "CONCUR": 3}[C.cmp(bc, peers[h])]
+        assert int(r.docs["min_cmp"][j]) == exp, (h, bc, peers[h])
+    # ClockStore: first update writes every row; a repeat writes nothing and differs nowhere
+    w, df, st = store.clock_update(hs)
+    assert w.all() and not df.any()
+    w, df, st = store.clock_update(hs)
+    assert not w.any() and not df.any()
+    # a queued change still advances DocBackend.clock (src/DocBackend.ts:135-142)
+    r = store.apply([(hs[0], [ch("aaaa", 3, {}, s("y", 1))])])       # needs aaaa:2 -> queued
+    assert int(r.docs["n_queued"][0]) == 1
+    w, df, st = store.clock_update([hs[0]])
+    assert w[0] and not df[0]
+    assert int(st[0][store.enc[hs[0]].actors.index("aaaa")]) == 3
