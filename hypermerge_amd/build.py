@@ -54,9 +54,25 @@ def build_synth(force: bool = False) -> str:
     return out
 
 
+def build_node(force: bool = False) -> str:
+    """N-API addon (hypermerge_amd/js/hmgpu_node.c) over libhmgpu.so; skipped without Node headers."""
+    out = os.path.join(LIBDIR, "hmgpu.node")
+    src = os.path.join(HERE, "js", "hmgpu_node.c")
+    if not os.path.exists("/usr/include/node/node_api.h"):
+        return ""
+    if force or not os.path.exists(out) or any(
+            os.path.getmtime(f) > os.path.getmtime(out)
+            for f in (src, os.path.join(LIBDIR, "libhmgpu.so"), os.path.join(CSRC, "../../include/hypermerge_amd.h"))):
+        _run(["gcc", "-O2", "-Wall", "-shared", "-fPIC", "-I/usr/include/node",
+              "-I" + os.path.join(HERE, "..", "include"), "-o", out, src, "-L" + LIBDIR, "-lhmgpu",
+              "-Wl,-rpath,$ORIGIN"])
+    return out
+
+
 def build_all(force: bool = False) -> None:
     build_gpu(force)
     build_synth(force)
+    build_node(force)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,401 @@
+'use strict'
+// GpuDocBackend.js — the Node host side of the MI355X merge engine, a drop-in for the
+// reference's remote-change path:
+//
+//   Backend      Automerge's functional API as DocBackend/RepoBackend use it
+//                (Backend.init, Backend.applyChanges(state, changes) -> [state, patch],
+//                state.getIn(['opSet','history']).size / .slice(0, n).toArray();
+//                src/DocBackend.ts:79,148,157,172,175, src/RepoBackend.ts:572-576).
+//   DocBackend   the reference class (src/DocBackend.ts:46-213): same constructor, fields
+//                (id, actorId, clock, back, changes, ready) and methods (init, initActor,
+//                applyRemoteChanges, applyLocalChange, updateMinimumClock), same
+//                ReadyMsg / ActorIdMsg / RemotePatchMsg / LocalPatchMsg messages.
+//   GpuEngine    owns the device store (N-API addon -> include/hypermerge_amd.h) and runs
+//                every document's applyChanges calls as batched GPU submits: per-document
+//                FIFO job queues, one submit per round over all documents with work.
+//                mode 'sync' flushes inside the caller's stack (the reference's Queue
+//                semantics: a push runs the merge synchronously); mode 'batched' flushes
+//                once per event-loop turn (setImmediate), merging every document that
+//                received changes during the turn in one launch.
+//   ClockStore   the reference's clock table semantics (src/ClockStore.ts:24-112) kept in
+//                host memory, with updateDocs(): ClockStore.update(repo, doc, doc.clock)
+//                for many documents from one GPU upsert-max (hm_store_clock_update).
+//
+// A document's applyChanges that throws (e.g. 'Inconsistent reuse of sequence number')
+// is rolled back on the device and rethrown here, like the reference's throw out of
+// Backend.applyChanges leaves DocBackend.back unchanged.
+
+const path = require('path')
+const addon = require(path.join(__dirname, '..', '_lib', 'hmgpu.node'))
+const C = require('./columnar')
+const Clock = require('./clocks')
+const Channel = require('./channel')
+
+const ERR_TEXT = {
+  1: 'Inconsistent reuse of sequence number',
+  2: 'Modification of unknown object',
+  3: 'Duplicate creation of object',
+  4: 'Duplicate list element ID',
+  5: 'Missing index entry for list element',
+  16: 'Document outside the engine envelope',
+}
+
+class History {
+  constructor(state) { this.state = state; this.size = state.histLen }
+  slice(a, b) {
+    const st = this.state
+    const lo = a || 0
+    const hi = b === undefined ? this.size : Math.min(b, this.size)
+    const idx = addon.historyPrefix(st.engine.store, st.handle, Math.max(hi, 0))
+    const out = []
+    for (let i = lo; i < idx.length / 4; i++) out.push(st.log[idx.readUInt32LE(4 * i)])
+    return { toArray: () => out, size: out.length }
+  }
+}
+
+// The per-document BackendState: a handle into the device store plus the host-side
+// interner and the change objects of the log (for history slices).  States are linear:
+// applyChanges advances the document in place and returns the same state object.
+class GpuBackendState {
+  constructor(engine) {
+    this.engine = engine
+    this.handle = addon.openDoc(engine.store)
+    this.enc = new C.DocEncoder(engine.pool)
+    this.log = []
+    this.histLen = 0
+    this.nQueued = 0
+    this.clock = {}
+    this.deps = {}
+  }
+
+  getIn(p) {
+    if (p.length === 2 && p[0] === 'opSet' && p[1] === 'history') return new History(this)
+    if (p.length === 2 && p[0] === 'opSet' && p[1] === 'clock') return Object.assign({}, this.clock)
+    if (p.length === 2 && p[0] === 'opSet' && p[1] === 'deps') return Object.assign({}, this.deps)
+    throw new Error(`GpuBackendState.getIn: unsupported path ${JSON.stringify(p)}`)
+  }
+}
+
+class GpuEngine {
+  constructor(opts) {
+    const o = opts || {}
+    this.aStride = o.aStride || 8
+    this.mode = o.mode || 'batched'
+    this.store = addon.createStore(o.device || 0, this.aStride)
+    this.pool = new C.StringPool()
+    this.queues = new Map()          // state -> FIFO of jobs
+    this.flushing = false
+    this.scheduled = false
+    this.onError = o.onError || null
+    this.submits = 0
+  }
+
+  init() { return new GpuBackendState(this) }
+
+  // job: {changes|null, extraActors, done(result|null), fail(err)}
+  enqueue(state, job) {
+    let q = this.queues.get(state)
+    if (!q) { q = []; this.queues.set(state, q) }
+    q.push(job)
+    if (this.mode === 'sync') this.flush()
+    else if (!this.scheduled && !this.flushing) {
+      this.scheduled = true
+      setImmediate(() => { this.scheduled = false; this.flush() })
+    }
+  }
+
+  flush() {
+    if (this.flushing) return
+    this.flushing = true
+    try {
+      for (;;) {
+        // run leading callbacks, collect each document's head GPU job
+        const round = []
+        for (const [state, q] of Array.from(this.queues)) {
+          while (q.length && q[0].changes === null) q.shift().done(null)
+          if (q.length) round.push([state, q.shift()])
+          else this.queues.delete(state)
+        }
+        if (!round.length) {
+          if (this.queues.size === 0) break
+          continue
+        }
+        this.runRound(round)
+      }
+    } finally {
+      this.flushing = false
+    }
+  }
+
+  runRound(round) {
+    const appends = [], snaps = [], handles = new Uint32Array(round.length)
+    round.forEach(([state, job], i) => {
+      snaps.push(state.enc.snapshot())
+      const a = state.enc.encode(job.changes, job.extraActors)
+      if (a.nActors > this.aStride) {
+        state.enc.restore(snaps[i])
+        throw new Error(`document has ${a.nActors} actors > engine aStride ${this.aStride}`)
+      }
+      appends.push(a)
+      handles[i] = state.handle
+    })
+    const b = C.buildBatch(appends, this.aStride)
+    const id = addon.submit(this.store, b.docs, b.changes, b.deps, b.ops, handles, b.remap)
+    const r = addon.wait(this.store, id, round.length)
+    this.submits++
+    const S = this.aStride
+    const errors = []
+    round.forEach(([state, job], i) => {
+      const res = C.readDocResult(r.docs, i)
+      if (res.status !== 0) {
+        state.enc.restore(snaps[i])
+        errors.push([job, this.errorFor(state, job.changes, res)])
+        return
+      }
+      const base = state.log.length
+      state.log.push(...job.changes)
+      const prevHist = state.histLen
+      state.histLen = res.histLen
+      state.nQueued = res.nQueued
+      state.clock = Clock.fromRow(r.clock, i * S * 4, state.enc.actors)
+      state.deps = Clock.fromRow(r.heads, i * S * 4, state.enc.actors)
+      const backClock = Clock.fromRow(r.backClock, i * S * 4, state.enc.actors)
+      job.done({ res, base, prevHist, backClock, minCmp: Clock.CMP_CODES[res.minCmp] })
+    })
+    for (const [job, err] of errors) {
+      if (job.fail) job.fail(err)
+      else if (this.onError) this.onError(err)
+      else throw err
+    }
+  }
+
+  errorFor(state, changes, res) {
+    const text = ERR_TEXT[res.status] || `engine status ${res.status}`
+    const all = state.log.concat(changes)
+    const c = res.errChange < all.length ? all[res.errChange] : null
+    let detail = ''
+    if (c && res.status === 1) detail = ` ${c.seq} by ${c.actor}`
+    else if (c && res.errOp !== C.NONE && c.ops && c.ops[res.errOp]) {
+      const op = c.ops[res.errOp]
+      detail = res.status === 4 ? ` ${c.actor}:${op.elem}` : res.status === 5 ? ` ${op.key}` : ` ${op.obj}`
+    }
+    const e = new Error(text + detail)
+    e.status = res.status
+    return e
+  }
+
+  // Synchronous single-document applyChanges (Backend.applyChanges)
+  applyChanges(state, changes) {
+    let out = null, err = null
+    const prevMode = this.mode
+    this.mode = 'sync'
+    try {
+      this.enqueue(state, { changes, done: (r) => { out = r }, fail: (e) => { err = e } })
+    } finally {
+      this.mode = prevMode
+    }
+    if (err) throw err
+    return out
+  }
+}
+
+function makePatch(state) {
+  // clock / deps are applied-only (queued changes excluded); diffs are not emitted yet
+  return { clock: Object.assign({}, state.clock), deps: Object.assign({}, state.deps), canUndo: false, canRedo: false, diffs: [] }
+}
+
+function makeBackend(engine) {
+  return {
+    init: () => engine.init(),
+    applyChanges: (state, changes) => {
+      engine.applyChanges(state, changes)
+      return [state, makePatch(state)]
+    },
+    getPatch: (state) => makePatch(state),
+  }
+}
+
+class DocBackend {
+  constructor(documentId, notify, back, engine) {
+    this.id = documentId
+    this.actorId = undefined
+    this.clock = {}
+    this.back = undefined
+    this.changes = new Map()
+    this.ready = new Channel('doc:back:readyQ')
+    this.notify = notify
+    this.minimumClock = undefined
+    this.minimumClockSatisfied = false
+    this.localChangeQ = new Channel('doc:back:localChangeQ')
+    this.remoteChangesQ = new Channel('doc:back:remoteChangesQ')
+    this.engine = engine || (back && back.engine) || DocBackend.defaultEngine()
+    if (back) {
+      this.back = back
+      this.actorId = documentId                           // rootActorId(documentId)
+      this.ready.subscribe((f) => f())
+      this.minimumClockSatisfied = true
+      this.subscribeToRemoteChanges()
+      this.subscribeToLocalChanges()
+      this.notify({ type: 'ReadyMsg', id: this.id, minimumClockSatisfied: this.minimumClockSatisfied,
+        actorId: this.actorId, history: this.back.histLen })
+    }
+  }
+
+  static defaultEngine() {
+    if (!DocBackend._engine) DocBackend._engine = new GpuEngine({})
+    return DocBackend._engine
+  }
+
+  testMinimumClockSatisfied() {
+    if (this.minimumClock) {
+      const t = Clock.cmp(this.clock, this.minimumClock)
+      this.minimumClockSatisfied = t === 'GT' || t === 'EQ'
+    }
+  }
+
+  updateMinimumClock(clock) {
+    if (this.minimumClockSatisfied) return
+    this.minimumClock = Clock.union(clock, this.minimumClock || {})
+    this.testMinimumClockSatisfied()
+  }
+
+  applyRemoteChanges(changes) { this.remoteChangesQ.push(changes) }
+
+  applyLocalChange(change) { this.localChangeQ.push(change) }
+
+  initActor(actorId) {
+    if (this.back) {
+      this.actorId = this.actorId || actorId
+      this.notify({ type: 'ActorIdMsg', id: this.id, actorId: this.actorId })
+    }
+  }
+
+  updateClock(changes) {
+    changes.forEach((change) => {
+      const old = this.clock[change.actor] || 0
+      this.clock[change.actor] = Math.max(old, change.seq)
+    })
+    if (!this.minimumClockSatisfied) this.testMinimumClockSatisfied()
+  }
+
+  init(changes, actorId) {
+    const state = this.engine.init()
+    this.engine.enqueue(state, { changes, done: () => {
+      this.actorId = this.actorId || actorId
+      this.back = state
+      this.updateClock(changes)
+      this.minimumClockSatisfied = changes.length > 0
+      const patch = makePatch(state)
+      this.ready.subscribe((f) => f())
+      this.subscribeToLocalChanges()
+      this.subscribeToRemoteChanges()
+      // ReadyMsg after the buffered remote changes drained above (per-document FIFO)
+      this.engine.enqueue(state, { changes: null, done: () => {
+        this.notify({ type: 'ReadyMsg', id: this.id, minimumClockSatisfied: this.minimumClockSatisfied,
+          actorId: this.actorId, patch, history: this.back.histLen })
+      } })
+    } })
+  }
+
+  subscribeToRemoteChanges() {
+    this.remoteChangesQ.subscribe((changes) => {
+      this.engine.enqueue(this.back, { changes, done: () => {
+        this.updateClock(changes)
+        this.notify({ type: 'RemotePatchMsg', id: this.id, minimumClockSatisfied: this.minimumClockSatisfied,
+          patch: makePatch(this.back), history: this.back.histLen })
+      } })
+    })
+  }
+
+  subscribeToLocalChanges() {
+    this.localChangeQ.subscribe((change) => {
+      // Backend.applyLocalChange: the change must extend its actor's sequence
+      const cur = this.back.clock[change.actor] || 0
+      if (change.seq <= cur) throw new Error(`Change request has already been applied: ${change.actor}:${change.seq}`)
+      this.engine.enqueue(this.back, { changes: [change], done: () => {
+        this.updateClock([change])
+        const patch = Object.assign(makePatch(this.back), { actor: change.actor, seq: change.seq })
+        this.notify({ type: 'LocalPatchMsg', id: this.id, actorId: this.actorId,
+          minimumClockSatisfied: this.minimumClockSatisfied, change, patch, history: this.back.histLen })
+      } })
+    })
+  }
+}
+
+// ClockStore with the reference's semantics (src/ClockStore.ts:24-112, SQL upsert-max per
+// entry, zero entries stored and returned, updateQ pushed when the input differs from the
+// stored clock), in host memory (better-sqlite3 is not part of this engine).
+class ClockStore {
+  constructor(engine) {
+    this.engine = engine || null
+    this.rows = new Map()            // repoId \0 docId -> Map(actorId -> seq)
+    this.updateQ = new Channel('clockstore:updateQ')
+  }
+
+  key(repoId, docId) { return repoId + '\u0000' + docId }
+
+  get(repoId, docId) {
+    const m = this.rows.get(this.key(repoId, docId))
+    const c = {}
+    if (m) Array.from(m.keys()).sort(byteOrder).forEach((a) => { c[a] = m.get(a) })
+    return c
+  }
+
+  getMultiple(repoId, docIds) {
+    return docIds.reduce((acc, d) => { acc[d] = this.get(repoId, d); return acc }, {})
+  }
+
+  update(repoId, docId, clock) {
+    const k = this.key(repoId, docId)
+    let m = this.rows.get(k)
+    if (!m) { m = new Map(); this.rows.set(k, m) }
+    for (const [a, s] of Object.entries(clock)) {
+      if (!m.has(a) || s > m.get(a)) m.set(a, s)
+    }
+    const stored = this.get(repoId, docId)
+    const d = [repoId, docId, stored]
+    if (!Clock.equal(clock, stored)) this.updateQ.push(d)
+    return d
+  }
+
+  set(repoId, docId, clock) {
+    this.rows.delete(this.key(repoId, docId))
+    return this.update(repoId, docId, clock)
+  }
+
+  getAllDocumentIds(repoId) {
+    const out = []
+    for (const k of this.rows.keys()) { const [r, d] = k.split('\u0000'); if (r === repoId) out.push(d) }
+    return out
+  }
+
+  getAllRepoIds() { return Array.from(new Set(Array.from(this.rows.keys()).map((k) => k.split('\u0000')[0]))) }
+
+  // ClockStore.update(repoId, doc.id, doc.clock) for many GPU documents at once
+  // (src/RepoBackend.ts:343-345): the device upsert-max decides which rows change
+  // (written) and which inputs differ from the stored clock (updateQ).
+  updateDocs(repoId, docs) {
+    if (!docs.length) return []
+    const handles = Uint32Array.from(docs.map((d) => d.back.handle))
+    const r = addon.clockUpdate(this.engine.store, handles)
+    const S = this.engine.aStride
+    return docs.map((doc, i) => {
+      const actors = doc.back.enc.actors
+      const k = this.key(repoId, doc.id)
+      if (r.written[i]) {
+        const stored = Clock.fromRow(r.stored, i * S * 4, actors)
+        let m = this.rows.get(k)
+        if (!m) { m = new Map(); this.rows.set(k, m) }
+        for (const [a, s] of Object.entries(stored)) if (!m.has(a) || s > m.get(a)) m.set(a, s)
+      }
+      const d = [repoId, doc.id, this.get(repoId, doc.id)]
+      if (r.differs[i]) this.updateQ.push(d)
+      return d
+    })
+  }
+}
+
+// SQLite's BINARY collation (memcmp of UTF-8) orders the Clocks primary key
+function byteOrder(a, b) { return Buffer.compare(Buffer.from(a, 'utf8'), Buffer.from(b, 'utf8')) }
+
+module.exports = { GpuEngine, GpuBackendState, DocBackend, ClockStore, makeBackend, addon }

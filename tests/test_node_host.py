@@ -1,0 +1,68 @@
+"""Node host pieces that need no GPU: the JS encoder (hypermerge_amd/js/columnar.js)
+must produce the same rows as the Python encoder for the same change sequence (both
+feed the same C-ABI), the JS clock helpers must answer like src/Clock.ts (golden
+vectors from dist/Clock.js), and the channel must deliver like src/Queue.ts."""
+import json
+import math
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from hypermerge_amd import synth
+from hypermerge_amd.columnar import decode_doc
+from hypermerge_amd.store import DocEncoder, StringPool
+from kat_cases import CASES
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NODE = shutil.which("node")
+pytestmark = pytest.mark.skipif(NODE is None, reason="node not installed")
+
+
+def run_node(payload):
+    p = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "encode_rows.js")], input=json.dumps(payload),
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    return json.loads(p.stdout)
+
+
+def test_js_encoder_rows_equal_python_encoder():
+    b = synth.generate(synth.config("C5", n_docs=40))
+    t = synth.generate(synth.config("C3", n_docs=5, changes_per_actor=30))
+    docs = [decode_doc(b, i) for i in range(b.n_docs)] + [decode_doc(t, i) for i in range(t.n_docs)]
+    docs += [c[1] for c in CASES]
+    rng = np.random.default_rng(5)
+    chunked = []
+    for chs in docs:
+        cuts = sorted(rng.integers(0, len(chs) + 1, size=2))
+        chunked.append([chs[:cuts[0]], chs[cuts[0]:cuts[1]], chs[cuts[1]:]])
+    got = run_node({"docs": chunked})
+    pool = StringPool()
+    for chunks, js in zip(chunked, got["docs"]):
+        e = DocEncoder(pool, keep_log=False)
+        for ch, j in zip(chunks, js):
+            a = e.encode(ch)
+            cc = a.changes.copy()
+            assert cc.tobytes().hex() == j["changes"]
+            assert a.deps.tobytes().hex() == j["deps"]
+            assert a.ops.tobytes().hex() == j["ops"]
+            assert (a.n_actors, a.n_regs, a.n_objs, a.flags) == (j["nActors"], j["nRegs"], j["nObjs"], j["flags"])
+            assert (None if a.remap is None else list(a.remap)) == j["remap"]
+            assert e.actors == j["actors"]
+    assert pool.strings == got["strings"]
+
+
+def test_js_clock_helpers_match_reference_vectors():
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "clock_vectors.json")))
+    cases = [c for c in gold["cases"] if "Infinity" not in json.dumps(c)]
+    got = run_node({"docs": [], "clocks": [[c["a"], c["b"]] for c in cases]})
+    for c, (cmp, uni, eq) in zip(cases, got["clock"]):
+        assert cmp == c["cmp"] and eq == c["equal"]
+        assert uni == c["union"]
+
+
+def test_js_channel_delivery_order():
+    got = run_node({"docs": []})
+    assert got["channel"] == [[1, 2, 3, "once4"], 1]
