@@ -143,6 +143,27 @@ def main() -> int:
     else:
         applied_all, wall_max = float(applied), wall
 
+    # ClockStore feed across the node (off the merge's critical path, timed separately):
+    # every rank's changed DocBackend.clock rows gathered over RCCL (hypermerge_amd/exchange.py)
+    xchg = None
+    if ws > 1:
+        from hypermerge_amd import exchange as X
+        keys = torch.from_numpy((batch.docs["reserved"][:, 0].astype(np.int64)
+                                 | (batch.docs["reserved"][:, 1].astype(np.int64) << 32))).to(dev)
+        newc = r_bclock.view(nd, S)
+        zero = torch.zeros_like(newc)
+        times = []
+        for it in range(4):
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            t = time.perf_counter()
+            rows = X.changed_rows(keys, newc, zero)
+            allrows = X.gather_clock_rows(rows)
+            torch.cuda.synchronize(dev)
+            times.append(time.perf_counter() - t)
+        xchg = {"clock_rows_gathered": int(allrows.shape[0]), "ms": 1000.0 * float(np.median(times[1:])),
+                "collective": "all_gather (RCCL)"}
+
     value = applied_all * args.steps / wall_max
     ms_per_step = wall_max * 1000.0 / args.steps
     # roofline of the dominant kernel (merge_small_kernel): algorithmic bytes per launch
@@ -185,6 +206,7 @@ def main() -> int:
             "cpu_baseline": cpu,
             "parity_sample_ok": parity, "unsupported_docs": unsupported, "error_docs": errors,
             "gen_s": round(gen_s, 2), "event_ms_per_step": ev_ms / args.steps,
+            "clock_exchange": xchg,
         }
         print(json.dumps(line), flush=True)
     if ws > 1:

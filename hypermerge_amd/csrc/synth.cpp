@@ -482,10 +482,14 @@ void *hm_synth_generate(const hm_synth_config *cfg) {
     size_t nc = 0, nd = 0, no = 0;
     for (auto &p : parts) for (auto &d : p) { nc += d.ch.size(); nd += d.dp.size(); no += d.op.size(); }
     o->ch.reserve(nc); o->dp.reserve(nd); o->op.reserve(no); o->docs.reserve(gidx.size());
+    size_t k = 0;                        // docs come out in gidx order
     for (auto &p : parts)
         for (auto &d : p) {
             hm_doc_row row;
             memset(&row, 0, sizeof(row));
+            // the document's global index in the doc-id stream (its key across shards)
+            row.reserved[0] = (uint32_t)gidx[k]; row.reserved[1] = (uint32_t)(gidx[k] >> 32);
+            k++;
             row.change_off = (uint32_t)o->ch.size(); row.n_changes = (uint32_t)d.ch.size();
             row.dep_off = (uint32_t)o->dp.size(); row.n_deps = (uint32_t)d.dp.size();
             row.op_off = (uint32_t)o->op.size(); row.n_ops = (uint32_t)d.op.size();

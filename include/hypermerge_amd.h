@@ -97,7 +97,7 @@ typedef struct {
     uint32_t n_objs;      /* interned object ids, 0 = ROOT '00000000-0000-0000-0000-000000000000' */
     uint16_t n_actors;    /* actor ranks 0..n_actors-1 (rank = order of the actor id strings) */
     uint16_t flags;       /* HM_DOC_* bits set by the encoder */
-    uint32_t reserved[2];
+    uint32_t reserved[2]; /* not read by the engine (the synthetic feeds keep the doc's global index here) */
 } hm_doc_row;
 #define HM_DOC_HAS_LISTS 1u     /* the doc creates a list/text object (launch sizing hint only) */
 #define HM_DOC_HAS_COUNTERS 2u  /* the doc has counter sets or incs (launch sizing hint only) */

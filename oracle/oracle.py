@@ -49,3 +49,12 @@ def merge(batch, results=None, threads: int = 1, doc_range: Optional[tuple] = No
             list(ex.map(lambda s: L.oracle_merge(ctypes.byref(cb), ctypes.byref(cr), s, min(hi, s + step)),
                         range(lo, hi, step)))
     return results
+
+
+def sync_end(present, lo: int, hi: int) -> int:
+    """RepoBackend.syncChanges' walk (src/RepoBackend.ts:517-519):
+    for (i = min; i < max && actor.changes.hasOwnProperty(i); i++) — returns the final i."""
+    i = lo
+    while i < hi and i < len(present) and present[i]:
+        i += 1
+    return i

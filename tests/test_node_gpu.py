@@ -54,6 +54,7 @@ def test_batched_feed_matches_oracle():
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr
     got = json.loads(p.stdout)
+    assert got["clockMismatch"] == 0 and got["gpuPush"] == got["hostPush"]
     assert got["submits"] <= 4 * 2          # one submit per round (init round + remote rounds), not per document
     cold = encode(docs, 8)
     co = O.merge(cold)

@@ -66,3 +66,15 @@ def test_js_clock_helpers_match_reference_vectors():
 def test_js_channel_delivery_order():
     got = run_node({"docs": []})
     assert got["channel"] == [[1, 2, 3, "once4"], 1]
+
+
+def test_js_clockstore_matches_reference_sql():
+    """tests/golden/clockstore_vectors.json: the reference's ClockStore SQL executed in
+    sqlite3 (tools/golden/gen_clockstore_vectors.py), incl. tests/ClockStore.test.ts."""
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "clockstore_vectors.json")))
+    p = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "run_clockstore.js")], capture_output=True, text=True,
+                       timeout=120)
+    assert p.returncode == 0, p.stderr
+    got = json.loads(p.stdout)
+    for name, c in gold["cases"].items():
+        assert got[name] == c["results"], name

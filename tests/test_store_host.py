@@ -73,3 +73,13 @@ def test_remap_when_a_smaller_actor_arrives():
     e.encode([ch("0000", 1, {}, s("q", 1))])
     e.restore(snap)
     assert e.actors == ["aaaa", "mmmm", "zzzz"] and len(e.log_changes) == 4
+
+
+def test_feed_bitmaps_pack_lsb_first():
+    from hypermerge_amd.sync import pack_feeds
+    p = np.zeros(70, bool)
+    p[[0, 3, 63, 64, 69]] = True
+    w, off = pack_feeds([p, np.ones(3, bool)])
+    assert list(off) == [0, 3]
+    assert int(w[0]) == (1 | 8 | (1 << 63)) and int(w[1]) == (1 | (1 << 5)) and int(w[2]) == 0
+    assert int(w[3]) == 7
