@@ -83,10 +83,11 @@ int launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, hipStream
     p.large_cursor = (uint32_t *)pb;
     unsigned long long *pool_used = (unsigned long long *)(pb + 8);
     HIPCHK(e, hipMemsetAsync(pb, 0, 16, s));
-    // persistent grid: enough resident 1-wave workgroups to fill every CU
-    size_t lds = hm_small_lds_bytes(c.opl, c.cls, c.lists, c.counters);
-    uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>(32, (160 * 1024) / std::max<size_t>(lds, 1)));
-    uint32_t grid = std::min<uint32_t>(b->n_docs, (uint32_t)e->num_cus * per_cu * 2);
+    // persistent grid: exactly the resident 1-wave workgroups (VGPR/LDS occupancy of the
+    // instantiation), so every wave starts at once and the documents split evenly — a
+    // larger grid would leave a partial second round of waves as a tail
+    const uint32_t per_cu = hm_small_occupancy(c.opl, c.cls, c.lists, c.counters);
+    uint32_t grid = std::min<uint32_t>(b->n_docs, (uint32_t)e->num_cus * per_cu);
     HIPCHK(e, hipEventRecord(e->ev[0], s));
     hipError_t r = hm_launch_small(p, c.opl, c.cls, c.lists, grid, s);
     if (r != hipSuccess) return hip_fail(e, r, "merge_small_kernel launch");

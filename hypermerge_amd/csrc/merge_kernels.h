@@ -37,6 +37,7 @@ hipError_t hm_launch_large(const SmallParams &p, void *pool, size_t pool_bytes, 
 // small-kernel size class (LDS carve) for a batch's per-document maxima
 uint32_t hm_small_class(uint32_t max_regs, uint32_t max_objs, uint32_t max_deps);
 size_t hm_small_lds_bytes(uint32_t opl, uint32_t cls, bool lists, bool counters);
+uint32_t hm_small_occupancy(uint32_t opl, uint32_t cls, bool lists, bool counters);
 hipError_t hm_launch_small(const SmallParams &p, uint32_t opl, uint32_t cls, bool lists, uint32_t grid, hipStream_t s);
 // which: 0 cmp (out uint8_t*), 1 union, 2 intersection (out uint32_t*)
 hipError_t hm_launch_clock(int which, const uint32_t *a, const uint32_t *b, void *out, uint32_t n_docs,

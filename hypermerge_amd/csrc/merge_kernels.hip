@@ -37,9 +37,13 @@
 #include "merge_kernels.h"
 
 #ifndef HM_ABLATE
-#define HM_ABLATE 0     // dev-only timing builds: 1 skip ancestor push, 2 stop after K1, 4 stop after K2 survivors,
+#define HM_ABLATE 0     // dev-only timing builds: 2 stop after K1, 4 stop after K2 survivors,
                         // 8 stop right after staging
 #endif
+#ifndef HM_STAMPS
+#define HM_STAMPS 0     // diagnostic builds only: per-phase s_memtime shares (tools/stamps.py); never timed
+#endif
+#define HM_NSTAMP 12
 #ifndef HM_WAVES_PER_EU
 #define HM_WAVES_PER_EU 4   // register-allocator target: LDS already caps C4-class launches at ~4.25 waves/SIMD
 #endif
@@ -89,20 +93,21 @@ __device__ __forceinline__ u64 err_key(uint32_t h, uint32_t op_plus1, uint32_t a
 }
 
 struct SmallLds {
-    LDS u64 *anc, *chain, *segor, *errkey, *cov, *opval;
+    LDS u64 *anc, *chain, *segor, *errkey, *cov;
     LDS int64_t *survsum;           // counter launches only
     LDS uint2 *cw0, *cw1, *cw2;     // staged change rows (three 8-byte words, conflict-free)
     LDS uint32_t *first, *base, *bclock, *headv, *objslot, *segcnt, *survcnt, *regoff, *regobj, *insmin;
-    LDS uint32_t *flags, *deps, *segoff, *segfill, *seglist, *survp;
+    LDS uint32_t *flags, *deps, *seglist, *survp, *survent;
     LDS uint32_t *opmeta;           // action | datatype << 8 | vtag << 16
     LDS uint32_t *opro;             // reg | obj << 16 (clamped to 0xFFFF: >= any carve)
     LDS uint32_t *opelem;           // ins element counter (list launches)
     LDS int32_t *hist_of;
-    LDS uint16_t *survtmp, *survop, *opbase, *oppar;
+    LDS uint16_t *survop, *opbase, *oppar;
     LDS uint8_t *h2a, *chactor, *opchg, *objtype;
     // K3 (RGA lists); carved only for launches with list documents
     LDS uint32_t *nins, *pcount, *poff, *pfill, *nodekey, *tour0, *tour1, *listbase;
     LDS uint16_t *nodeop, *nodepi, *regnode, *plist, *fc, *ns, *listid;
+    LDS u64 *stamps;                // HM_STAMPS builds: [HM_NSTAMP] cycle sums + last stamp
 };
 #define PAR_HEAD 0xFFFFu             // oppar of an insert after '_head'
 
@@ -116,23 +121,22 @@ template <> struct SizeClass<1> { static constexpr uint32_t NR = 256, NO = 64, N
 // resident waves per CU, so nothing is carved that the launch's documents cannot use.
 // The kernel instantiates it with compile-time sizes (a size class), so every LDS address
 // folds into a ds_* immediate offset instead of occupying an SGPR.
-// Aliases: seglist/survp live in `first` (dead after K1b), survtmp in `deps` (dead after K1b).
+// Aliases: seglist/survp live in `first` (dead after K1b), survent in `deps` (dead after K1b).
 template <typename L_t, typename P>
 __host__ __device__ inline size_t small_carve(P base, uint32_t NOp, uint32_t NR, uint32_t NO, uint32_t ND,
                                               bool lists, bool counters, L_t *L) {
     size_t o = 0;
 #define TAKE(f, T, cnt) do { L->f = (decltype(L->f))(base + o); o = (o + (size_t)(cnt) * sizeof(T) + 15) & ~(size_t)15; } while (0)
     TAKE(anc, u64, 64);          TAKE(chain, u64, NA_MAX);     TAKE(segor, u64, NR);
-    TAKE(errkey, u64, 1);        TAKE(cov, u64, 1);            TAKE(opval, u64, NOp);
+    TAKE(errkey, u64, 1);        TAKE(cov, u64, 1);
     TAKE(cw0, uint2, 64);        TAKE(cw1, uint2, 64);         TAKE(cw2, uint2, 64);
     TAKE(first, uint32_t, NA_MAX * 64 > 2 * NOp ? NA_MAX * 64 : 2 * NOp);
     L->seglist = L->first; L->survp = L->first + NOp;
     TAKE(base, uint32_t, NA_MAX * 3);
     TAKE(objslot, uint32_t, NO); TAKE(segcnt, uint32_t, NR);   TAKE(survcnt, uint32_t, NR);
     TAKE(regoff, uint32_t, NR);  TAKE(regobj, uint32_t, NR);   TAKE(insmin, uint32_t, NR);
-    TAKE(flags, uint32_t, 1);    TAKE(deps, uint32_t, ND > NOp / 2 ? ND : NOp / 2);
-    L->survtmp = (decltype(L->survtmp))L->deps;
-    TAKE(segoff, uint32_t, NR);  TAKE(segfill, uint32_t, NR);
+    TAKE(flags, uint32_t, 1);    TAKE(deps, uint32_t, ND > NOp ? ND : NOp);
+    L->survent = L->deps;
     TAKE(opmeta, uint32_t, NOp); TAKE(opro, uint32_t, NOp);
     TAKE(hist_of, int32_t, 64);
     TAKE(survop, uint16_t, NOp); TAKE(opbase, uint16_t, 64);   TAKE(oppar, uint16_t, NOp);
@@ -148,6 +152,7 @@ __host__ __device__ inline size_t small_carve(P base, uint32_t NOp, uint32_t NR,
         TAKE(plist, uint16_t, NOp);   TAKE(fc, uint16_t, NP);      TAKE(ns, uint16_t, NOp);
         TAKE(listid, uint16_t, NO);
     }
+    TAKE(stamps, u64, HM_STAMPS ? HM_NSTAMP + 1 : 0);
     TAKE(survsum, int64_t, counters ? NOp : 0);       // last: the rest of the carve ignores `counters`
 #undef TAKE
     L->bclock = L->base + NA_MAX;
@@ -160,6 +165,20 @@ template <typename T> __device__ __forceinline__ T lds_or(LDS T *p, typename Id<
 template <typename T> __device__ __forceinline__ T lds_min(LDS T *p, typename Id<T>::type v) { return __atomic_fetch_min(p, v, __ATOMIC_RELAXED); }
 template <typename T> __device__ __forceinline__ T lds_max(LDS T *p, typename Id<T>::type v) { return __atomic_fetch_max(p, v, __ATOMIC_RELAXED); }
 template <typename T> __device__ __forceinline__ T lds_add(LDS T *p, typename Id<T>::type v) { return __atomic_fetch_add(p, v, __ATOMIC_RELAXED); }
+
+#if HM_STAMPS
+__device__ unsigned long long hm_stamp_acc[HM_NSTAMP];
+__device__ __forceinline__ u64 stamp_now() {
+    u64 t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define STAMP(L_, i) do { const u64 t_ = stamp_now(); if (threadIdx.x == 0) { (L_).stamps[i] += t_ - (L_).stamps[HM_NSTAMP]; (L_).stamps[HM_NSTAMP] = t_; } } while (0)
+#else
+#define STAMP(L_, i) do { } while (0)
+#endif
 
 enum : uint32_t { FL_UNSUPPORTED = 1u };
 enum Outcome { OUT_OK = 0, OUT_ERROR = 1, OUT_UNSUPPORTED = 2 };
@@ -401,6 +420,11 @@ __device__ __forceinline__ Rows load_rows(const SmallParams &p, const hm_doc_row
     if (lane + WAVE < doc.n_deps) r.d1 = *reinterpret_cast<const uint2 *>(dp + lane + WAVE);
     return r;
 }
+// an op's 8-byte value, re-read from its row (L2-resident: the row was read moments ago);
+// only survivors and counter ops need it, so it is not staged in LDS
+__device__ __forceinline__ u64 op_value(const SmallParams &p, const hm_doc_row &doc, uint32_t k) {
+    return *reinterpret_cast<const u64 *>(&p.ops[doc.op_off + k].value);
+}
 // dep row -> actor << 24 | seq (all ones: outside the envelope)
 __device__ __forceinline__ uint32_t pack_dep(uint2 w) {
     const uint32_t a = w.x & 0xFFFF;
@@ -414,7 +438,6 @@ __device__ __forceinline__ void stage_op(const SmallLds &L, uint32_t k, uint32_t
     L.opro[k] = reg | (obj << 16);
     L.oppar[k] = (uint16_t)(a.z == HM_HEAD ? PAR_HEAD : (a.z < 0xFFFEu ? a.z : 0xFFFEu));
     L.opmeta[k] = b.x & 0xFFFFFFu;
-    L.opval[k] = ((u64)b.w << 32) | b.z;
     if (LISTS) L.opelem[k] = a.w;
 }
 template <int OPL, bool LISTS>
@@ -453,6 +476,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
 
     // ---------------- the staged rows (lane = arrival index) ----------------
     if (HM_ABLATE & 8) return OUT_UNSUPPORTED;
+    STAMP(L, 0);
     const bool act = lane < n;
     const hm_change_row c = act ? change_of(L.cw0[lane], L.cw1[lane], L.cw2[lane])
                                 : change_of(make_uint2(0, 0), make_uint2(0, 0), make_uint2(0, 0));
@@ -491,6 +515,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     wave_sync();
     if (*L.flags & FL_UNSUPPORTED) return OUT_UNSUPPORTED;
 
+    STAMP(L, 1);
     const uint32_t first_me = act ? L.first[actor * 64 + slot] : lane;
     const bool dup = act && first_me != lane;
     const uint32_t cid_first = shfl32(c.content_id, (int)(first_me & 63));
@@ -528,6 +553,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     wave_sync();
     if (*L.flags & FL_UNSUPPORTED) return OUT_UNSUPPORTED;
 
+    STAMP(L, 2);
     int32_t hist = -1;
     uint32_t H = 0;
     if (__ballot(act && !ok) == 0) {
@@ -601,6 +627,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         }
     }
 
+    STAMP(L, 3);
     // ---------------- K1b: ancestor sets in history order ----------------
     if (act) L.hist_of[lane] = hist;
     if (act && hist >= 0) L.h2a[hist] = (uint8_t)lane;
@@ -630,14 +657,16 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     // Positions below 32 only have low-word ancestors.
     uint32_t alo = hv && lane < 32 ? 1u << lane : 0u, ahi = hv && lane >= 32 ? 1u << (lane - 32) : 0u;
     {
-        const uint32_t Hs = (HM_ABLATE & 1) ? 0u : (uint32_t)__builtin_amdgcn_readfirstlane((int)H);
+        const uint32_t Hs = (uint32_t)__builtin_amdgcn_readfirstlane((int)H);
         const uint32_t Dlo = (uint32_t)D, Dhi = (uint32_t)(D >> 32);
         const uint32_t H1 = Hs < 32 ? Hs : 32;
 #define PUSH_LO(k) alo |= (uint32_t)__builtin_amdgcn_readlane((int)alo, (int)(k)) & (uint32_t)__builtin_amdgcn_sbfe((int)Dlo, (k), 1)
 #define PUSH_HI(k) do { const uint32_t m_ = (uint32_t)__builtin_amdgcn_sbfe((int)Dhi, (k) - 32, 1);          \
                         alo |= (uint32_t)__builtin_amdgcn_readlane((int)alo, (int)(k)) & m_;              \
                         ahi |= (uint32_t)__builtin_amdgcn_readlane((int)ahi, (int)(k)) & m_; } while (0)
-        uint32_t k = 0;                                   // wave-uniform: manual 4x unroll
+        uint32_t k = 0;
+        // wave-uniform: manual 4x unroll.  (A blocked variant — 4 positions per readlane round
+        // trip, finished on the scalar unit — measured slower: this phase is issue-bound.)
         for (; k + 4 <= H1; k += 4) { PUSH_LO(k); PUSH_LO(k + 1); PUSH_LO(k + 2); PUSH_LO(k + 3); }
         for (; k < H1; k++) PUSH_LO(k);
         for (k = 32; k + 2 <= Hs; k += 2) { PUSH_HI(k); PUSH_HI(k + 1); }
@@ -648,6 +677,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     const u64 anc = hv ? ((((u64)ahi << 32) | alo) & ~(1ull << lane)) : 0ull;   // strict ancestors
     if (hv) L.anc[lane] = anc;
     wave_sync();
+    STAMP(L, 4);
     const u64 covered = *L.cov;
     // transitiveDeps folds deps.set(actor, seq-1) in key order: acc = max(acc, FC(d)); acc[a_d] = s_d.
     // The `.set` can LOWER acc[a_d] when an earlier entry already knows a later change of a_d;
@@ -677,6 +707,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     }
     wave_sync();
 
+    STAMP(L, 5);
     if (HM_ABLATE & 2) return OUT_UNSUPPORTED;
     // ---------------- K2: ops (lane + 64*t) ----------------
     uint32_t oreg[OPL], oobj[OPL], opar[OPL], oact[OPL], okey[OPL], oarr[OPL], oelem[OPL];
@@ -716,6 +747,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
             }
         }
     }
+    STAMP(L, 6);
     if (__ballot(malformed)) return OUT_UNSUPPORTED;
     // counter sums need the carve's survsum table (launches flagged HM_DOC_HAS_COUNTERS)
     if (!p.counters && __ballot(counter_ops)) lds_or(L.flags, FL_UNSUPPORTED);
@@ -768,6 +800,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     if (*L.errkey != ~0ull) return OUT_ERROR;                    // the first throw wins
     if (*L.flags & FL_UNSUPPORTED) return OUT_UNSUPPORTED;
 
+    STAMP(L, 7);
     if (HM_ABLATE & 4) return OUT_UNSUPPORTED;
     // survivor offsets: exclusive scan over register ids
     uint32_t total = 0;
@@ -779,9 +812,13 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         total += tot;
     }
     wave_sync();
+    // survivor slots hold op | actor << 16: one LDS word per slot for the rank scans
+    uint32_t my_act[OPL];
 #pragma unroll
-    for (int t = 0; t < OPL; t++)
-        if (surv[t]) { sslot[t] += L.regoff[oreg[t]]; L.survtmp[sslot[t]] = (uint16_t)(lane + WAVE * t); }
+    for (int t = 0; t < OPL; t++) {
+        my_act[t] = surv[t] ? (uint32_t)L.chactor[oarr[t]] : 0u;
+        if (surv[t]) { sslot[t] += L.regoff[oreg[t]]; L.survent[sslot[t]] = (lane + WAVE * t) | (my_act[t] << 16); }
+    }
     wave_sync();
     // rank: actor rank descending ...
     uint32_t rank[OPL];
@@ -791,55 +828,48 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         rank[t] = 0; tie[t] = false;
         if (!surv[t]) continue;
         const uint32_t k = lane + WAVE * t, reg = oreg[t];
-        const uint32_t my_a = L.chactor[oarr[t]];
         const uint32_t b0 = L.regoff[reg], cnt = L.survcnt[reg];
         for (uint32_t q = 0; q < cnt; q++) {
-            const uint32_t k2 = L.survtmp[b0 + q];
-            if (k2 == k) continue;
-            const uint32_t a2 = L.chactor[L.opchg[k2]];
-            if (a2 > my_a) rank[t]++;
-            else if (a2 == my_a) tie[t] = true;
+            const uint32_t e = L.survent[b0 + q];
+            if ((e & 0xFFFFu) == k) continue;
+            rank[t] += (e >> 16) > my_act[t] ? 1u : 0u;
+            tie[t] |= (e >> 16) == my_act[t];
         }
     }
     bool anytie = false;
 #pragma unroll
     for (int t = 0; t < OPL; t++) anytie |= tie[t];
     if (__ballot(anytie)) {
-        // ... equal actors (ops of one change): p = assigns applied on the register before
-        // the op; per-register assign lists (CSR) give p in O(register length)
-        uint32_t tot2 = 0;
-        for (uint32_t r0 = 0; r0 < R; r0 += WAVE) {
-            const uint32_t r = r0 + lane;
-            uint32_t tt;
-            const uint32_t ex = wave_excl_scan(r < R ? L.segcnt[r] : 0u, &tt);
-            if (r < R) { L.segoff[r] = tot2 + ex; L.segfill[r] = 0; }
-            tot2 += tt;
-        }
-        wave_sync();
-#pragma unroll
-        for (int t = 0; t < OPL; t++)
-            if (oh[t] >= 0 && oact[t] >= HM_SET && oact[t] <= HM_INC && oreg[t] < R)
-                L.seglist[L.segoff[oreg[t]] + lds_add(&L.segfill[oreg[t]], 1u)] = okey[t];
-        wave_sync();
+        // ... equal actors (ops of one change on one register): p = assigns applied on the
+        // register before the op.  Tie ops are few per document: broadcast each one and count
+        // the wave's applied assigns on its register with a smaller (history, op) key.
 #pragma unroll
         for (int t = 0; t < OPL; t++) {
-            if (!tie[t]) continue;
-            const uint32_t s0 = L.segoff[oreg[t]], sc = L.segcnt[oreg[t]];
-            uint32_t pc = 0;
-            for (uint32_t q = 0; q < sc; q++) pc += L.seglist[s0 + q] < okey[t] ? 1u : 0u;
-            L.survp[sslot[t]] = tie_order(pc);
+            u64 tm = __ballot(tie[t]);
+            while (tm) {
+                const int j = (int)__builtin_ctzll(tm);
+                tm &= tm - 1;
+                const uint32_t rj = (uint32_t)__builtin_amdgcn_readlane((int)oreg[t], j);
+                const uint32_t kj = (uint32_t)__builtin_amdgcn_readlane((int)okey[t], j);
+                uint32_t pc = 0;
+#pragma unroll
+                for (int t2 = 0; t2 < OPL; t2++)
+                    pc += (uint32_t)__popcll(__ballot(oh[t2] >= 0 && oact[t2] >= HM_SET && oact[t2] <= HM_INC &&
+                                                      oreg[t2] == rj && okey[t2] < kj));
+                if ((int)lane == j) L.survp[sslot[t]] = tie_order(pc);
+            }
         }
         wave_sync();
 #pragma unroll
         for (int t = 0; t < OPL; t++) {
             if (!tie[t]) continue;
             const uint32_t k = lane + WAVE * t, reg = oreg[t];
-            const uint32_t my_a = L.chactor[oarr[t]], my_t = L.survp[sslot[t]];
+            const uint32_t my_t = L.survp[sslot[t]];
             const bool odd_n = L.segcnt[reg] & 1;      // the group is reversed after an odd count
             const uint32_t b0 = L.regoff[reg], cnt = L.survcnt[reg];
             for (uint32_t q = 0; q < cnt; q++) {
-                const uint32_t k2 = L.survtmp[b0 + q];
-                if (k2 == k || L.chactor[L.opchg[k2]] != my_a) continue;
+                const uint32_t e = L.survent[b0 + q];
+                if ((e & 0xFFFFu) == k || (e >> 16) != my_act[t]) continue;
                 const uint32_t t2 = L.survp[b0 + q];
                 if (odd_n ? (t2 > my_t) : (t2 < my_t)) rank[t]++;
             }
@@ -853,6 +883,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         if (p.counters) L.survsum[pos] = 0;
     }
     wave_sync();
+    STAMP(L, 8);
     if constexpr (LISTS) {
         if (doc_lists) rga_order<OPL>(L, R, O, oreg, oobj, opar, oact, oelem, oarr, oh);
     }
@@ -869,7 +900,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
             const uint32_t reg = oreg[t], b0 = L.regoff[reg], cnt = L.survcnt[reg];
             const u64 an = L.anc[oh[t]];
             const uint32_t my_vtag = (L.opmeta[k] >> 16) & 0xFF;
-            const int64_t v = (int64_t)L.opval[k];
+            const int64_t v = (int64_t)op_value(p, doc, k);
             for (uint32_t q = 0; q < cnt; q++) {
                 const uint32_t k2 = L.survop[b0 + q];
                 const uint32_t m2 = L.opmeta[k2], vt2 = (m2 >> 16) & 0xFF;
@@ -883,7 +914,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         for (uint32_t q = lane; q < total; q += WAVE) {
             const uint32_t k = L.survop[q], mt = L.opmeta[k];
             if ((mt & 0xFF) == HM_SET && ((mt >> 8) & 0xFF) == HM_DT_COUNTER && ((mt >> 16) & 0xFF) == HM_V_INT) {
-                const int64_t b = (int64_t)L.opval[k];
+                const int64_t b = (int64_t)op_value(p, doc, k);
                 outside |= (u64)(b < 0 ? -b : b) >= (1ull << 52);
             }
         }
@@ -929,7 +960,7 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
     for (uint32_t q = lane; q < st.total; q += WAVE) {
         const uint32_t k = L.survop[q], mt = L.opmeta[k];
         hm_surv_result sr;
-        sr.op = k; sr.vtag = (mt >> 16) & 0xFF; sr.value = L.opval[k];
+        sr.op = k; sr.vtag = (mt >> 16) & 0xFF; sr.value = op_value(p, doc, k);
         if (p.counters && (mt & 0xFF) == HM_SET && ((mt >> 8) & 0xFF) == HM_DT_COUNTER && sr.vtag == HM_V_INT)
             sr.value = (u64)((int64_t)sr.value + L.survsum[q]);
         p.res_surv[doc.op_off + q] = sr;
@@ -988,6 +1019,9 @@ void merge_small_kernel(SmallParams p) {
     p.cap_regs = C::NR; p.cap_objs = C::NO; p.cap_deps = C::ND;
     uint32_t d = blockIdx.x;
     if (d >= p.n_docs) return;
+#if HM_STAMPS
+    if (threadIdx.x == 0) { for (int i = 0; i < HM_NSTAMP; i++) L.stamps[i] = 0; L.stamps[HM_NSTAMP] = stamp_now(); }
+#endif
     hm_doc_row doc = p.docs[d];
     stage_rows<OPL, LISTS>(p, L, doc, load_rows<OPL>(p, doc));
     wave_sync();
@@ -1005,14 +1039,21 @@ void merge_small_kernel(SmallParams p) {
         const Outcome oc = in_env ? merge_doc_small<OPL, LISTS>(p, L, doc, st) : OUT_UNSUPPORTED;
         Rows next;
         if (more) next = load_rows<OPL>(p, docn);
+        STAMP(L, 9);
         write_outputs<LISTS>(p, L, d, doc, oc, st);
         wave_sync();
+        STAMP(L, 10);
         if (!more) break;
         stage_rows<OPL, LISTS>(p, L, docn, next);
         wave_sync();
+        STAMP(L, 11);
         d = dn;
         doc = docn;
     }
+#if HM_STAMPS
+    if (threadIdx.x == 0)
+        for (int i = 0; i < HM_NSTAMP; i++) atomicAdd(&hm_stamp_acc[i], (unsigned long long)L.stamps[i]);
+#endif
 }
 
 // ---------------- Clock algebra over dense rows (src/Clock.ts) ----------------
@@ -1043,6 +1084,18 @@ __global__ void clock_intersection_kernel(const uint32_t *a, const uint32_t *b, 
 }  // namespace hm
 
 // ---------------- host-side launchers ----------------
+#if HM_STAMPS
+extern "C" int hm_debug_stamps(unsigned long long *out, int n, int reset) {
+    if (n > HM_NSTAMP) n = HM_NSTAMP;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hm::hm_stamp_acc), n * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[HM_NSTAMP] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(hm::hm_stamp_acc), z, sizeof z) != hipSuccess) return -1;
+    }
+    return n;
+}
+#endif
 uint32_t hm_small_class(uint32_t max_regs, uint32_t max_objs, uint32_t max_deps) {
     typedef hm::SizeClass<0> S;
     return (max_regs <= S::NR && max_objs <= S::NO && max_deps <= S::ND) ? 0u : 1u;
@@ -1054,6 +1107,19 @@ size_t hm_small_lds_bytes(uint32_t opl, uint32_t cls, bool lists, bool counters)
                                       hm::SizeClass<0>::ND, lists, counters, &L)
                     : hm::small_carve((uintptr_t)0, 64 * opl, hm::SizeClass<1>::NR, hm::SizeClass<1>::NO,
                                       hm::SizeClass<1>::ND, lists, counters, &L);
+}
+
+// resident 1-wave workgroups per CU for the instantiation a launch will use (VGPRs and LDS)
+uint32_t hm_small_occupancy(uint32_t opl, uint32_t cls, bool lists, bool counters) {
+    const size_t lds = hm_small_lds_bytes(opl, cls, lists, counters);
+    int n = 0;
+#define HM_OCC(O_, L_, C_) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, hm::merge_small_kernel<O_, L_, C_>, WAVE, lds)
+#define HM_OCC_OPL(L_, C_) switch (opl) { case 1: HM_OCC(1, L_, C_); break; case 2: HM_OCC(2, L_, C_); break; default: HM_OCC(4, L_, C_); }
+    if (cls == 0) { if (lists) { HM_OCC_OPL(true, 0) } else { HM_OCC_OPL(false, 0) } }
+    else          { if (lists) { HM_OCC_OPL(true, 1) } else { HM_OCC_OPL(false, 1) } }
+#undef HM_OCC_OPL
+#undef HM_OCC
+    return n > 0 ? (uint32_t)n : 1u;
 }
 
 hipError_t hm_launch_small(const SmallParams &p, uint32_t opl, uint32_t cls, bool lists, uint32_t grid, hipStream_t s) {

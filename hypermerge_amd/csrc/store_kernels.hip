@@ -143,7 +143,8 @@ __global__ void sync_ranges_kernel(const uint64_t *present, const uint64_t *word
         if (run < 64u - (j & 63)) { j += run; break; }     // a hole inside this word
         j += 64u - (j & 63);
     }
-    out_end[i] = j < h ? j : h;
+    // for (i = min; i < max && present(i); i++): i stays at min when min >= max
+    out_end[i] = lo[i] >= h ? lo[i] : (j < h ? j : h);
 }
 
 }  // namespace hms
