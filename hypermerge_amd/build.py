@@ -36,7 +36,10 @@ def build_gpu(force: bool = False) -> str:
         from concurrent.futures import ThreadPoolExecutor
         objdir = os.path.join(LIBDIR, "obj")
         os.makedirs(objdir, exist_ok=True)
-        flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall"]
+        # uniform-address LDS atomics (wave ORs/mins into one word) are reduced with DPP row ops;
+        # the default iterative strategy walks the active lanes on the scalar unit (~7 SALU each)
+        flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+                 "-mllvm", "-amdgpu-atomic-optimizer-strategy=DPP"]
         objs = [os.path.join(objdir, s + ".o") for s in GPU_SRCS]
         with ThreadPoolExecutor(min(8, len(GPU_SRCS))) as ex:
             list(ex.map(lambda so: _run([HIPCC] + flags + ["-c", "-o", so[1], os.path.join(CSRC, so[0])]),

@@ -37,7 +37,8 @@
 #include "merge_kernels.h"
 
 #ifndef HM_ABLATE
-#define HM_ABLATE 0     // dev-only timing builds: 2 stop after K1, 4 stop after K2 survivors,
+#define HM_ABLATE 0     // dev-only builds: stop (defer the doc) after a phase — 16 validate, 32 deps, 64 push,
+                        // 2 K1b, 128 K2 scan, 4 K2 survivors, 256 rank;
                         // 8 stop right after staging
 #endif
 #ifndef HM_STAMPS
@@ -516,6 +517,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     if (*L.flags & FL_UNSUPPORTED) return OUT_UNSUPPORTED;
 
     STAMP(L, 1);
+    if (HM_ABLATE & 16) return OUT_UNSUPPORTED;
     const uint32_t first_me = act ? L.first[actor * 64 + slot] : lane;
     const bool dup = act && first_me != lane;
     const uint32_t cid_first = shfl32(c.content_id, (int)(first_me & 63));
@@ -554,13 +556,16 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     if (*L.flags & FL_UNSUPPORTED) return OUT_UNSUPPORTED;
 
     STAMP(L, 2);
+    if (HM_ABLATE & 32) return OUT_UNSUPPORTED;
     int32_t hist = -1;
     uint32_t H = 0;
+    bool identity = false;                // history == arrival order (no queueing, no duplicates)
     if (__ballot(act && !ok) == 0) {
         // every change was ready on arrival: history = arrival order minus duplicates
         const u64 appl = __ballot(act && !dup);
         if (act) hist = dup ? -2 : (int32_t)__popcll(appl & ((1ull << lane) - 1));
         H = (uint32_t)__popcll(appl);
+        identity = __ballot(dup) == 0;
     } else {
         // ---- exact emulation of addChange / applyQueuedOps (wave-uniform control) ----
         for (uint32_t i = lane; i < NA_MAX * 64; i += WAVE) L.first[i] = 0xFFFFFFFFu;   // -> applied lane
@@ -639,7 +644,10 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     const uint32_t hseq = shfl32(seq, (int)ai);
     const uint32_t hpred = shfl32(pred_arr, (int)ai);
     u64 D = 0, Dnp = 0;                                   // direct deps (history space); without own pred
-    if (hv) {
+    if (identity) {                                       // history position == arrival index
+        D = hv ? dm_arr : 0ull;
+        Dnp = hv && hpred != 0xFFu ? D & ~(1ull << hpred) : D;
+    } else if (hv) {
         u64 x = dm_arr;
         while (x) {
             const uint32_t j = (uint32_t)__builtin_ctzll(x);
@@ -664,13 +672,22 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
 #define PUSH_HI(k) do { const uint32_t m_ = (uint32_t)__builtin_amdgcn_sbfe((int)Dhi, (k) - 32, 1);          \
                         alo |= (uint32_t)__builtin_amdgcn_readlane((int)alo, (int)(k)) & m_;              \
                         ahi |= (uint32_t)__builtin_amdgcn_readlane((int)ahi, (int)(k)) & m_; } while (0)
-        uint32_t k = 0;
-        // wave-uniform: manual 4x unroll.  (A blocked variant — 4 positions per readlane round
-        // trip, finished on the scalar unit — measured slower: this phase is issue-bound.)
-        for (; k + 4 <= H1; k += 4) { PUSH_LO(k); PUSH_LO(k + 1); PUSH_LO(k + 2); PUSH_LO(k + 3); }
-        for (; k < H1; k++) PUSH_LO(k);
-        for (k = 32; k + 2 <= Hs; k += 2) { PUSH_HI(k); PUSH_HI(k + 1); }
-        for (; k < Hs; k++) PUSH_HI(k);
+        // Fully unrolled with immediate lane indices (no scalar index arithmetic per step), one
+        // wave-uniform check per group of 8.  Steps at positions >= H are no-ops: those lanes
+        // hold no ancestors and no lane depends on them.  (A blocked variant — 4 positions per
+        // readlane round trip, finished on the scalar unit — measured slower.)
+#pragma unroll
+        for (int g = 0; g < 32; g += 8) {
+            if ((uint32_t)g >= H1) break;
+            PUSH_LO(g); PUSH_LO(g + 1); PUSH_LO(g + 2); PUSH_LO(g + 3);
+            PUSH_LO(g + 4); PUSH_LO(g + 5); PUSH_LO(g + 6); PUSH_LO(g + 7);
+        }
+#pragma unroll
+        for (int g = 32; g < 64; g += 8) {
+            if ((uint32_t)g >= Hs) break;
+            PUSH_HI(g); PUSH_HI(g + 1); PUSH_HI(g + 2); PUSH_HI(g + 3);
+            PUSH_HI(g + 4); PUSH_HI(g + 5); PUSH_HI(g + 6); PUSH_HI(g + 7);
+        }
 #undef PUSH_LO
 #undef PUSH_HI
     }
@@ -678,6 +695,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     if (hv) L.anc[lane] = anc;
     wave_sync();
     STAMP(L, 4);
+    if (HM_ABLATE & 64) return OUT_UNSUPPORTED;
     const u64 covered = *L.cov;
     // transitiveDeps folds deps.set(actor, seq-1) in key order: acc = max(acc, FC(d)); acc[a_d] = s_d.
     // The `.set` can LOWER acc[a_d] when an earlier entry already knows a later change of a_d;
@@ -748,6 +766,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         }
     }
     STAMP(L, 6);
+    if (HM_ABLATE & 128) return OUT_UNSUPPORTED;
     if (__ballot(malformed)) return OUT_UNSUPPORTED;
     // counter sums need the carve's survsum table (launches flagged HM_DOC_HAS_COUNTERS)
     if (!p.counters && __ballot(counter_ops)) lds_or(L.flags, FL_UNSUPPORTED);
@@ -884,6 +903,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     }
     wave_sync();
     STAMP(L, 8);
+    if (HM_ABLATE & 256) return OUT_UNSUPPORTED;
     if constexpr (LISTS) {
         if (doc_lists) rga_order<OPL>(L, R, O, oreg, oobj, opar, oact, oelem, oarr, oh);
     }
