@@ -45,6 +45,9 @@
 #define HM_STAMPS 0     // diagnostic builds only: per-phase s_memtime shares (tools/stamps.py); never timed
 #endif
 #define HM_NSTAMP 12
+#ifndef HM_PREFETCH_EARLY
+#define HM_PREFETCH_EARLY 0 // 1: the next document's rows are loaded before this document's merge
+#endif
 #ifndef HM_WAVES_PER_EU
 #define HM_WAVES_PER_EU 4   // register-allocator target: LDS already caps C4-class launches at ~4.25 waves/SIMD
 #endif
@@ -75,18 +78,46 @@ __device__ __forceinline__ u64 wave_or64(u64 v) {
     for (int o = 1; o < WAVE; o <<= 1) v |= shfl64(v, (int)(threadIdx.x ^ o));
     return v;
 }
-// exclusive prefix sum across the wave; *total = sum over all lanes
+// DPP lane moves (gfx9 encodings): lanes without a source read 0
+#define DPP_ROW_SHR(n) (0x110 + (n))
+#define DPP_WAVE_SHR1 0x138
+#define DPP_ROW_BCAST15 0x142
+#define DPP_ROW_BCAST31 0x143
+// exclusive prefix sum across the wave; *total = sum over all lanes.  Row-local shifts and
+// the gfx9 row broadcasts (VALU only: no LDS round trip as a bpermute ladder would need).
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t *total) {
-    const uint32_t lane = threadIdx.x;
     uint32_t x = v;
-    for (int o = 1; o < WAVE; o <<= 1) {
-        const uint32_t y = shfl32(x, (int)(lane >= (uint32_t)o ? lane - o : lane));
-        if (lane >= (uint32_t)o) x += y;
-    }
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_SHR(1), 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_SHR(2), 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_SHR(4), 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_SHR(8), 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_BCAST15, 0xA, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_BCAST31, 0xC, 0xF, false);
     *total = (uint32_t)__builtin_amdgcn_readlane((int)x, WAVE - 1);
     return x - v;
 }
-__device__ __forceinline__ void wave_sync() { __syncthreads(); }   // 1-wave workgroup: cheap
+// wave-wide max of a value (inclusive max-scan, last lane)
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+    uint32_t x = v, y;
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_SHR(1), 0xF, 0xF, false); x = x > y ? x : y;
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_SHR(2), 0xF, 0xF, false); x = x > y ? x : y;
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_SHR(4), 0xF, 0xF, false); x = x > y ? x : y;
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_SHR(8), 0xF, 0xF, false); x = x > y ? x : y;
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_BCAST15, 0xA, 0xF, false); x = x > y ? x : y;
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_BCAST31, 0xC, 0xF, false); x = x > y ? x : y;
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, WAVE - 1);
+}
+// value of the previous lane (lane 0 reads 0)
+__device__ __forceinline__ uint32_t prev_lane(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_WAVE_SHR1, 0xF, 0xF, false);
+}
+// One-wave workgroups: a wave's LDS instructions execute in issue order, so an exchange
+// through LDS between lanes needs only a compiler ordering point — no s_waitcnt, no barrier
+// (__syncthreads' workgroup fence would drain lgkmcnt at every exchange).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
 
 // error key: (history position, op index + 1, arrival index, code); the first throw is the min
 __device__ __forceinline__ u64 err_key(uint32_t h, uint32_t op_plus1, uint32_t arr, uint32_t code) {
@@ -96,9 +127,8 @@ __device__ __forceinline__ u64 err_key(uint32_t h, uint32_t op_plus1, uint32_t a
 struct SmallLds {
     LDS u64 *anc, *chain, *segor, *errkey, *cov;
     LDS int64_t *survsum;           // counter launches only
-    LDS uint2 *cw0, *cw1, *cw2;     // staged change rows (three 8-byte words, conflict-free)
     LDS uint32_t *first, *base, *bclock, *headv, *objslot, *segcnt, *survcnt, *regoff, *regobj, *insmin;
-    LDS uint32_t *flags, *deps, *seglist, *survp, *survent;
+    LDS uint32_t *flags, *deps, *depinfo, *seglist, *survp, *survent;
     LDS uint32_t *opmeta;           // action | datatype << 8 | vtag << 16
     LDS uint32_t *opro;             // reg | obj << 16 (clamped to 0xFFFF: >= any carve)
     LDS uint32_t *opelem;           // ins element counter (list launches)
@@ -130,13 +160,13 @@ __host__ __device__ inline size_t small_carve(P base, uint32_t NOp, uint32_t NR,
 #define TAKE(f, T, cnt) do { L->f = (decltype(L->f))(base + o); o = (o + (size_t)(cnt) * sizeof(T) + 15) & ~(size_t)15; } while (0)
     TAKE(anc, u64, 64);          TAKE(chain, u64, NA_MAX);     TAKE(segor, u64, NR);
     TAKE(errkey, u64, 1);        TAKE(cov, u64, 1);
-    TAKE(cw0, uint2, 64);        TAKE(cw1, uint2, 64);         TAKE(cw2, uint2, 64);
     TAKE(first, uint32_t, NA_MAX * 64 > 2 * NOp ? NA_MAX * 64 : 2 * NOp);
     L->seglist = L->first; L->survp = L->first + NOp;
     TAKE(base, uint32_t, NA_MAX * 3);
     TAKE(objslot, uint32_t, NO); TAKE(segcnt, uint32_t, NR);   TAKE(survcnt, uint32_t, NR);
     TAKE(regoff, uint32_t, NR);  TAKE(regobj, uint32_t, NR);   TAKE(insmin, uint32_t, NR);
-    TAKE(flags, uint32_t, 1);    TAKE(deps, uint32_t, ND > NOp ? ND : NOp);
+    TAKE(flags, uint32_t, 2);    TAKE(deps, uint32_t, ND > NOp ? ND : NOp);   // flags[1]: max n_deps
+    TAKE(depinfo, uint32_t, ND);
     L->survent = L->deps;
     TAKE(opmeta, uint32_t, NOp); TAKE(opro, uint32_t, NOp);
     TAKE(hist_of, int32_t, 64);
@@ -444,7 +474,6 @@ __device__ __forceinline__ void stage_op(const SmallLds &L, uint32_t k, uint32_t
 template <int OPL, bool LISTS>
 __device__ __forceinline__ void stage_rows(const SmallParams &p, const SmallLds &L, const hm_doc_row &doc, const Rows &r) {
     const uint32_t lane = threadIdx.x, m = doc.n_ops;
-    if (lane < doc.n_changes) { L.cw0[lane] = r.c0; L.cw1[lane] = r.c1; L.cw2[lane] = r.c2; }
     stage_op<LISTS>(L, lane, m, r.a0, r.b0);
     if (OPL > 1) stage_op<LISTS>(L, lane + WAVE, m, r.a1, r.b1);
     if (OPL > 2) { stage_op<LISTS>(L, lane + 2 * WAVE, m, r.a2, r.b2); stage_op<LISTS>(L, lane + 3 * WAVE, m, r.a3, r.b3); }
@@ -470,7 +499,7 @@ struct DocState {
 // Merge one document with the whole wave (no global stores).  Every return is wave-uniform.
 template <int OPL, bool LISTS>
 __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const SmallLds &L, const hm_doc_row &doc,
-                                                   DocState &st) {
+                                                   const uint2 w0, const uint2 w1, const uint2 w2, DocState &st) {
     const uint32_t lane = threadIdx.x;
     const uint32_t n = doc.n_changes, A = doc.n_actors, m = doc.n_ops, R = doc.n_regs, O = doc.n_objs;
     st.hist = -1; st.H = 0; st.total = 0; st.doc_lists = false;
@@ -479,11 +508,10 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     if (HM_ABLATE & 8) return OUT_UNSUPPORTED;
     STAMP(L, 0);
     const bool act = lane < n;
-    const hm_change_row c = act ? change_of(L.cw0[lane], L.cw1[lane], L.cw2[lane])
-                                : change_of(make_uint2(0, 0), make_uint2(0, 0), make_uint2(0, 0));
+    const hm_change_row c = change_of(w0, w1, w2);      // zero rows for lanes >= n (load_rows)
     for (uint32_t i = lane; i < NA_MAX * 64; i += WAVE) L.first[i] = 0xFFFFFFFFu;
     if (lane < NA_MAX) { L.base[lane] = 0xFFFFFFFFu; L.bclock[lane] = 0; L.headv[lane] = 0; L.chain[lane] = 0; }
-    if (lane == 0) { *L.errkey = ~0ull; *L.flags = 0; *L.cov = 0; }
+    if (lane == 0) { *L.errkey = ~0ull; L.flags[0] = 0; L.flags[1] = 0; *L.cov = 0; }
     const uint32_t dep_lo = doc.dep_off, ndep = doc.n_deps;
     wave_sync();
     const uint32_t actor = c.actor, seq = c.seq;
@@ -491,33 +519,52 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     // layout contract (include/hypermerge_amd.h): op and dep rows are grouped by change in
     // arrival order without gaps; anything else leaves the envelope
     const uint32_t op_end = c.op_first + c.n_ops, dep_end = c.dep_off + c.n_deps;
-    const uint32_t prev_op = shfl32(op_end, lane ? (int)lane - 1 : 0), prev_dep = shfl32(dep_end, lane ? (int)lane - 1 : 0);
-    if ((n == 0 && (m || ndep)) ||
-        (act && (c.op_first != (lane ? prev_op : doc.op_off) || c.dep_off != (lane ? prev_dep : dep_lo) ||
-                 (lane == n - 1 && (op_end != doc.op_off + m || dep_end != dep_lo + ndep)))))
-        lds_or(L.flags, FL_UNSUPPORTED);
-    if (act) {
-        if (actor >= A || seq == 0 || c.dep_off < dep_lo || my_dep0 + c.n_deps > ndep) lds_or(L.flags, FL_UNSUPPORTED);
-        else { lds_min(&L.base[actor], seq); lds_max(&L.bclock[actor], seq); }
-        L.chactor[lane] = (uint8_t)actor;
-        L.opbase[lane] = (uint16_t)(c.op_first - doc.op_off);
-        if (c.op_first < doc.op_off || c.op_first - doc.op_off + c.n_ops > m) lds_or(L.flags, FL_UNSUPPORTED);
-    }
+    const uint32_t prev_op = prev_lane(op_end), prev_dep = prev_lane(dep_end);
+    bool bad = (n == 0 && (m || ndep)) ||
+               (act && (c.op_first != (lane ? prev_op : doc.op_off) || c.dep_off != (lane ? prev_dep : dep_lo) ||
+                        (lane == n - 1 && (op_end != doc.op_off + m || dep_end != dep_lo + ndep))));
+    // predicated (no per-lane branches): neutral operands for lanes that must not update
+    const bool rowok = act && !(actor >= A || seq == 0 || c.dep_off < dep_lo || my_dep0 + c.n_deps > ndep);
+    bad |= act && !rowok;
+    bad |= act && (c.op_first < doc.op_off || c.op_first - doc.op_off + c.n_ops > m);
+    const uint32_t a8 = actor & (NA_MAX - 1);
+    lds_min(&L.base[a8], rowok ? seq : 0xFFFFFFFFu);
+    lds_max(&L.bclock[a8], rowok ? seq : 0u);
+    L.chactor[lane] = (uint8_t)actor;
+    L.opbase[lane] = (uint16_t)(c.op_first - doc.op_off);
+    if (__ballot(bad)) return OUT_UNSUPPORTED;
     wave_sync();
-    if (*L.flags & FL_UNSUPPORTED) return OUT_UNSUPPORTED;
-    const uint32_t mybase = act ? L.base[actor] : 0;
+    const uint32_t mybase = act ? L.base[a8] : 0;
     const uint32_t slot = seq - mybase;
-    if (act) {
-        if (slot >= 64) lds_or(L.flags, FL_UNSUPPORTED);
-        else lds_min(&L.first[actor * 64 + slot], lane);
+    if (__ballot(act && slot >= 64)) return OUT_UNSUPPORTED;
+    lds_min(&L.first[a8 * 64 + (slot & 63)], act ? lane : 0xFFFFFFFFu);
+    {
         const uint32_t o0 = c.op_first - doc.op_off;       // ops -> arrival index of their change
-        for (uint32_t j = 0; j < c.n_ops; j++) L.opchg[o0 + j] = (uint8_t)lane;
+        if (act) for (uint32_t j = 0; j < c.n_ops; j++) L.opchg[o0 + j] = (uint8_t)lane;
     }
     wave_sync();
-    if (*L.flags & FL_UNSUPPORTED) return OUT_UNSUPPORTED;
 
     STAMP(L, 1);
     if (HM_ABLATE & 16) return OUT_UNSUPPORTED;
+    // Every dep row at once: its lookups (the actor's base seq, then the first-arrival table)
+    // are done per row here, so the per-change loop below reads one LDS word per dep.
+    //   depinfo = first-arrival lane (bits 0-6, 0x7F none) | (s - base + 1) << 8 (0x7F outside
+    //             the batch's window of that actor, 0 for seq 0) | actor << 16
+    {
+        bool bad_dep = false;
+        for (uint32_t i = lane; i < ndep; i += WAVE) {
+            const uint32_t pk = L.deps[i];
+            const uint32_t a = pk >> 24, s = pk & 0xFFFFFF;
+            bad_dep |= pk == 0xFFFFFFFFu || a >= A;
+            const uint32_t ad = a & (NA_MAX - 1);
+            const uint32_t b = L.base[ad];
+            const bool inwin = b != 0xFFFFFFFFu && s >= b && s - b < 64;
+            const uint32_t f = L.first[ad * 64 + ((s - b) & 63)];
+            const uint32_t rel = s == 0 ? 0u : (inwin ? s - b + 1 : 0x7Fu);
+            L.depinfo[i] = (inwin && f < 64 ? f : 0x7Fu) | (rel << 8) | (ad << 16);
+        }
+        if (__ballot(bad_dep)) return OUT_UNSUPPORTED;
+    }
     const uint32_t first_me = act ? L.first[actor * 64 + slot] : lane;
     const bool dup = act && first_me != lane;
     const uint32_t cid_first = shfl32(c.content_id, (int)(first_me & 63));
@@ -528,32 +575,39 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     uint32_t pred_arr = 0xFFu;
     bool ok = true;                      // ready on arrival
     bool own_row = false;                // the deps map lists the change's own actor
-    if (act) {
-        for (uint32_t j = 0; j < c.n_deps; j++) {
-            const uint32_t pk = L.deps[my_dep0 + j];
-            const uint32_t a = pk >> 24, s = pk & 0xFFFFFF;
-            if (pk == 0xFFFFFFFFu || a >= A) { lds_or(L.flags, FL_UNSUPPORTED); continue; }
-            if (a == actor) own_row = true;
-            if (a == actor || s == 0) continue;                // deps.set(actor, seq-1) overrides
-            const uint32_t b = L.base[a];
-            if (b == 0xFFFFFFFFu || s < b || s - b >= 64) { need_set(need_lo, need_hi, a, 0x7F); ok = false; continue; }
-            need_set(need_lo, need_hi, a, s - b + 1);
-            const uint32_t f = L.first[a * 64 + (s - b)];
-            if (f >= lane) ok = false; else dmask |= 1ull << f;
-        }
-        const uint32_t ps = seq - 1;
-        if (ps != 0) {
-            if (ps < mybase) { need_set(need_lo, need_hi, actor, 0x7F); ok = false; }
-            else {
-                need_set(need_lo, need_hi, actor, ps - mybase + 1);
-                const uint32_t f = L.first[actor * 64 + (ps - mybase)];
-                if (f >= lane) ok = false; else { dmask |= 1ull << f; pred_arr = f; }
+    wave_sync();
+    {
+        // predicated over the wave's longest deps map, 4 deps per round (reads in flight together)
+        const uint32_t maxd = wave_max(act ? (uint32_t)c.n_deps : 0u);
+        for (uint32_t j0 = 0; j0 < maxd; j0 += 4) {
+            uint32_t inf[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const bool live = act && j0 + u < c.n_deps;
+                inf[u] = L.depinfo[live ? my_dep0 + j0 + u : 0u];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const bool live = act && j0 + u < c.n_deps;
+                const uint32_t a = (inf[u] >> 16) & (NA_MAX - 1), rel = (inf[u] >> 8) & 0x7F, f = inf[u] & 0x7F;
+                own_row |= live && a == actor;
+                const bool use = live && a != actor && rel != 0;                // deps.set(actor, seq-1) overrides
+                need_set(need_lo, need_hi, a, use ? rel : 0u);
+                ok = ok && !(use && (rel == 0x7F || f >= lane));
+                dmask |= (use && rel != 0x7F && f < lane) ? (1ull << f) : 0ull;
             }
         }
-        if (dup && cid_first != c.content_id) ok = false;      // mismatched duplicate: exact path
+        const uint32_t ps = seq - 1;
+        const bool hp = act && ps != 0, inb = ps >= mybase;
+        need_set(need_lo, need_hi, a8, hp ? (inb ? ps - mybase + 1 : 0x7Fu) : 0u);
+        const uint32_t f = L.first[a8 * 64 + ((ps - mybase) & 63)];
+        ok = ok && !(hp && (!inb || f >= lane));
+        const bool pv = hp && inb && f < lane;
+        dmask |= pv ? (1ull << (f & 63)) : 0ull;
+        pred_arr = pv ? f : pred_arr;
+        ok = ok && !(dup && cid_first != c.content_id);                  // mismatched duplicate: exact path
     }
     wave_sync();
-    if (*L.flags & FL_UNSUPPORTED) return OUT_UNSUPPORTED;
 
     STAMP(L, 2);
     if (HM_ABLATE & 32) return OUT_UNSUPPORTED;
@@ -638,11 +692,14 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     if (act && hist >= 0) L.h2a[hist] = (uint8_t)lane;
     wave_sync();
     const bool hv = lane < H;
-    const uint32_t ai = hv ? L.h2a[lane] : 0;            // arrival index at history position `lane`
-    const u64 dm_arr = shfl64(dmask, (int)ai);
-    const uint32_t hactor = shfl32(actor, (int)ai);
-    const uint32_t hseq = shfl32(seq, (int)ai);
-    const uint32_t hpred = shfl32(pred_arr, (int)ai);
+    // arrival index at history position `lane` (identity history: the same lane, no gathers)
+    uint32_t ai = lane, hactor = actor, hseq = seq, hpred = pred_arr;
+    u64 dm_arr = dmask;
+    if (!identity) {
+        ai = hv ? L.h2a[lane] : 0;
+        dm_arr = shfl64(dmask, (int)ai);
+        hactor = shfl32(actor, (int)ai); hseq = shfl32(seq, (int)ai); hpred = shfl32(pred_arr, (int)ai);
+    }
     u64 D = 0, Dnp = 0;                                   // direct deps (history space); without own pred
     if (identity) {                                       // history position == arrival index
         D = hv ? dm_arr : 0ull;
@@ -711,8 +768,10 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
             if (L.anc[i2] & Dnp) suspect = true;
         }
     }
-    const uint32_t h_own_row = shfl32(own_row ? 1u : 0u, (int)ai);     // all lanes: bpermute sources
-    const uint32_t h_dep0 = shfl32(my_dep0, (int)ai), h_nd = shfl32(c.n_deps, (int)ai);
+    uint32_t h_own_row = own_row ? 1u : 0u, h_dep0 = my_dep0, h_nd = c.n_deps;
+    if (!identity) {                                                     // all lanes: bpermute sources
+        h_own_row = shfl32(h_own_row, (int)ai); h_dep0 = shfl32(my_dep0, (int)ai); h_nd = shfl32(c.n_deps, (int)ai);
+    }
     suspect |= hv && h_own_row != 0;
     if (suspect) {
         const FoldView fv = {L.anc, L.chain, L.first, L.base, L.deps, L.hist_of};
@@ -738,7 +797,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         if (k < m) {
             const uint32_t meta = L.opmeta[k], ro = L.opro[k], pr = L.oppar[k];
             const uint32_t ch = L.opchg[k];
-            oarr[t] = ch; oh[t] = L.hist_of[ch];
+            oarr[t] = ch; oh[t] = identity ? (int32_t)ch : L.hist_of[ch];
             oreg[t] = ro & 0xFFFFu; oobj[t] = ro >> 16; oact[t] = meta & 0xFF;
             opar[t] = pr == PAR_HEAD ? HM_HEAD : pr;
             if (LISTS) {
@@ -783,36 +842,35 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     uint32_t sslot[OPL];
     bool surv[OPL];
     bool has_list = false;
+    u64 errk = ~0ull;                    // this lane's earliest throw (one wave-wide min below)
 #pragma unroll
     for (int t = 0; t < OPL; t++) {
-        surv[t] = false; sslot[t] = 0;
-        if (oh[t] < 0 || oact[t] < HM_INS || oact[t] > HM_INC || oreg[t] >= R) continue;
-        const uint32_t os = oobj[t] < O ? L.objslot[oobj[t]] : 0xFFFFFFFFu;
-        if (os == 0xFFFFFFFFu || os > okey[t]) {       // 'Modification of unknown object'
-            lds_min(L.errkey, err_key((uint32_t)oh[t], (okey[t] & 0xFFFF) + 1, oarr[t], HM_ERR_UNKNOWN_OBJECT));
-            continue;
-        }
-        const uint32_t ot = L.objtype[oobj[t]];
+        // predicated: every lane reads (clamped) and decides with selects, no per-op branches
+        const bool asg = oh[t] >= 0 && oact[t] >= HM_INS && oact[t] <= HM_INC && oreg[t] < R;
+        const uint32_t oi = oobj[t] < O ? oobj[t] : 0u, ri = oreg[t] < R ? oreg[t] : 0u;
+        const uint32_t pi = opar[t] < R ? opar[t] : 0u;
+        const uint32_t os = oobj[t] < O ? L.objslot[oi] : 0xFFFFFFFFu;
+        const uint32_t ot = L.objtype[oi], im = L.insmin[ri], ip = L.insmin[pi];
+        const u64 so = L.segor[ri];
+        const uint32_t h = oh[t] < 0 ? 0u : (uint32_t)oh[t], kk = (okey[t] & 0xFFFF) + 1;
+        const bool unknown = asg && (os == 0xFFFFFFFFu || os > okey[t]);    // 'Modification of unknown object'
+        const bool known = asg && !unknown;
         const bool is_list = ot == HM_MAKE_LIST || ot == HM_MAKE_TEXT;
-        if (oact[t] == HM_INS) {
-            has_list = true;
-            if (L.insmin[oreg[t]] != okey[t] + 1)     // 'Duplicate list element ID'
-                lds_min(L.errkey, err_key((uint32_t)oh[t], (okey[t] & 0xFFFF) + 1, oarr[t], HM_ERR_DUPLICATE_ELEM));
-            // engine envelope, ordered like a throw: insert after an element not yet inserted
-            if (opar[t] != HM_HEAD && !(L.insmin[opar[t]] <= okey[t]))
-                lds_min(L.errkey, err_key((uint32_t)oh[t], (okey[t] & 0xFFFF) + 1, oarr[t], HM_ERR_UNSUPPORTED));
-            continue;
-        }
-        has_list |= is_list;
-        if (oact[t] == HM_SET || oact[t] == HM_LINK) {
-            if (is_list && !(L.insmin[oreg[t]] <= okey[t]))   // 'Missing index entry for list element'
-                lds_min(L.errkey, err_key((uint32_t)oh[t], (okey[t] & 0xFFFF) + 1, oarr[t], HM_ERR_MISSING_ELEM));
-            if (!((L.segor[oreg[t]] >> oh[t]) & 1)) {
-                surv[t] = true;
-                sslot[t] = lds_add(&L.survcnt[oreg[t]], 1u);
-            }
-        }
+        const bool ins = known && oact[t] == HM_INS;
+        const bool sl = known && (oact[t] == HM_SET || oact[t] == HM_LINK);
+        has_list |= ins || (known && is_list);
+        u64 ek = unknown ? err_key(h, kk, oarr[t], HM_ERR_UNKNOWN_OBJECT) : ~0ull;
+        const u64 e1 = ins && im != okey[t] + 1 ? err_key(h, kk, oarr[t], HM_ERR_DUPLICATE_ELEM) : ~0ull;
+        // engine envelope, ordered like a throw: insert after an element not yet inserted
+        const u64 e2 = ins && opar[t] != HM_HEAD && !(ip <= okey[t]) ? err_key(h, kk, oarr[t], HM_ERR_UNSUPPORTED) : ~0ull;
+        // 'Missing index entry for list element'
+        const u64 e3 = sl && is_list && !(im <= okey[t]) ? err_key(h, kk, oarr[t], HM_ERR_MISSING_ELEM) : ~0ull;
+        ek = ek < e1 ? ek : e1; ek = ek < e2 ? ek : e2; ek = ek < e3 ? ek : e3;
+        errk = errk < ek ? errk : ek;
+        surv[t] = sl && !((so >> h) & 1);
+        sslot[t] = lds_add(&L.survcnt[ri], surv[t] ? 1u : 0u);
     }
+    lds_min(L.errkey, errk);
     const bool doc_lists = __ballot(has_list) != 0;
     if (!LISTS && doc_lists) lds_or(L.flags, FL_UNSUPPORTED);   // launched without the K3 carve
     wave_sync();
@@ -832,38 +890,62 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     }
     wave_sync();
     // survivor slots hold op | actor << 16: one LDS word per slot for the rank scans
-    uint32_t my_act[OPL];
+    uint32_t my_act[OPL], rb0[OPL], rcnt[OPL];
 #pragma unroll
     for (int t = 0; t < OPL; t++) {
+        const uint32_t ri = surv[t] ? oreg[t] : 0u;
         my_act[t] = surv[t] ? (uint32_t)L.chactor[oarr[t]] : 0u;
-        if (surv[t]) { sslot[t] += L.regoff[oreg[t]]; L.survent[sslot[t]] = (lane + WAVE * t) | (my_act[t] << 16); }
+        rb0[t] = L.regoff[ri];
+        rcnt[t] = surv[t] ? L.survcnt[ri] : 0u;
+        if (surv[t]) { sslot[t] += rb0[t]; L.survent[sslot[t]] = (lane + WAVE * t) | (my_act[t] << 16); }
     }
     wave_sync();
-    // rank: actor rank descending ...
+    // rank: actor rank descending ...  (every slot of this lane scanned in the same rounds,
+    // 4 entries per slot per round: registers rarely hold more than 4 survivors)
     uint32_t rank[OPL];
     bool tie[OPL];
+    constexpr int RG = OPL < 2 ? OPL : 2;      // op slots scanned together (register budget)
 #pragma unroll
-    for (int t = 0; t < OPL; t++) {
-        rank[t] = 0; tie[t] = false;
-        if (!surv[t]) continue;
-        const uint32_t k = lane + WAVE * t, reg = oreg[t];
-        const uint32_t b0 = L.regoff[reg], cnt = L.survcnt[reg];
-        for (uint32_t q = 0; q < cnt; q++) {
-            const uint32_t e = L.survent[b0 + q];
-            if ((e & 0xFFFFu) == k) continue;
-            rank[t] += (e >> 16) > my_act[t] ? 1u : 0u;
-            tie[t] |= (e >> 16) == my_act[t];
+    for (int t = 0; t < OPL; t++) { rank[t] = 0; tie[t] = false; }
+#pragma unroll
+    for (int g = 0; g < OPL; g += RG) {
+        uint32_t cmax = 0;
+#pragma unroll
+        for (int t = g; t < g + RG; t++) cmax = cmax > rcnt[t] ? cmax : rcnt[t];
+        for (uint32_t q0 = 0; q0 < cmax; q0 += 4) {
+            uint32_t e[RG][4];
+#pragma unroll
+            for (int t = g; t < g + RG; t++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const uint32_t q = q0 + i < rcnt[t] ? q0 + i : (rcnt[t] ? rcnt[t] - 1 : 0u);
+                    e[t - g][i] = L.survent[rb0[t] + q];
+                }
+#pragma unroll
+            for (int t = g; t < g + RG; t++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const bool v = q0 + i < rcnt[t] && (e[t - g][i] & 0xFFFFu) != lane + WAVE * t;
+                    rank[t] += v && (e[t - g][i] >> 16) > my_act[t] ? 1u : 0u;
+                    tie[t] |= v && (e[t - g][i] >> 16) == my_act[t];
+                }
         }
     }
     bool anytie = false;
 #pragma unroll
     for (int t = 0; t < OPL; t++) anytie |= tie[t];
     if (__ballot(anytie)) {
-        // ... equal actors (ops of one change on one register): p = assigns applied on the
-        // register before the op.  Tie ops are few per document: broadcast each one and count
-        // the wave's applied assigns on its register with a smaller (history, op) key.
+        // ... equal actors = ops of one change on one register (two changes of one actor are
+        // causally ordered, so only one change's ops survive together).  p = assigns applied on
+        // the register before the op: broadcast each tie op and count the wave's applied assigns
+        // on its register with a smaller (history, op) key; then broadcast each tie op's order to
+        // the other members of its group.  Registers and ballots only, no LDS round trips.
+        uint32_t myt[OPL];
+        bool oddn[OPL];
 #pragma unroll
         for (int t = 0; t < OPL; t++) {
+            myt[t] = 0;
+            oddn[t] = tie[t] && (L.segcnt[tie[t] ? oreg[t] : 0u] & 1);   // the group is reversed after an odd count
             u64 tm = __ballot(tie[t]);
             while (tm) {
                 const int j = (int)__builtin_ctzll(tm);
@@ -875,29 +957,30 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
                 for (int t2 = 0; t2 < OPL; t2++)
                     pc += (uint32_t)__popcll(__ballot(oh[t2] >= 0 && oact[t2] >= HM_SET && oact[t2] <= HM_INC &&
                                                       oreg[t2] == rj && okey[t2] < kj));
-                if ((int)lane == j) L.survp[sslot[t]] = tie_order(pc);
+                if ((int)lane == j) myt[t] = tie_order(pc);
             }
         }
-        wave_sync();
 #pragma unroll
         for (int t = 0; t < OPL; t++) {
-            if (!tie[t]) continue;
-            const uint32_t k = lane + WAVE * t, reg = oreg[t];
-            const uint32_t my_t = L.survp[sslot[t]];
-            const bool odd_n = L.segcnt[reg] & 1;      // the group is reversed after an odd count
-            const uint32_t b0 = L.regoff[reg], cnt = L.survcnt[reg];
-            for (uint32_t q = 0; q < cnt; q++) {
-                const uint32_t e = L.survent[b0 + q];
-                if ((e & 0xFFFFu) == k || (e >> 16) != my_act[t]) continue;
-                const uint32_t t2 = L.survp[b0 + q];
-                if (odd_n ? (t2 > my_t) : (t2 < my_t)) rank[t]++;
+            u64 tm = __ballot(tie[t]);
+            while (tm) {
+                const int j = (int)__builtin_ctzll(tm);
+                tm &= tm - 1;
+                const uint32_t rj = (uint32_t)__builtin_amdgcn_readlane((int)oreg[t], j);
+                const uint32_t aj = (uint32_t)__builtin_amdgcn_readlane((int)my_act[t], j);
+                const uint32_t tj = (uint32_t)__builtin_amdgcn_readlane((int)myt[t], j);
+#pragma unroll
+                for (int t2 = 0; t2 < OPL; t2++) {
+                    const bool peer = tie[t2] && oreg[t2] == rj && my_act[t2] == aj && !(t2 == t && (int)lane == j);
+                    rank[t2] += (peer && (oddn[t2] ? (tj > myt[t2]) : (tj < myt[t2]))) ? 1u : 0u;
+                }
             }
         }
     }
 #pragma unroll
     for (int t = 0; t < OPL; t++) {
         if (!surv[t]) continue;
-        const uint32_t pos = L.regoff[oreg[t]] + rank[t];
+        const uint32_t pos = rb0[t] + rank[t];
         L.survop[pos] = (uint16_t)(lane + WAVE * t);
         if (p.counters) L.survsum[pos] = 0;
     }
@@ -946,7 +1029,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
 }
 
 // Output phase of one document (all reads from LDS; coalesced stores).
-template <bool LISTS>
+template <int OPL, bool LISTS>
 __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallLds &L, uint32_t d,
                                               const hm_doc_row &doc, Outcome oc, const DocState &st) {
     const uint32_t lane = threadIdx.x;
@@ -977,13 +1060,18 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
         }
         return;
     }
-    for (uint32_t q = lane; q < st.total; q += WAVE) {
-        const uint32_t k = L.survop[q], mt = L.opmeta[k];
-        hm_surv_result sr;
-        sr.op = k; sr.vtag = (mt >> 16) & 0xFF; sr.value = op_value(p, doc, k);
-        if (p.counters && (mt & 0xFF) == HM_SET && ((mt >> 8) & 0xFF) == HM_DT_COUNTER && sr.vtag == HM_V_INT)
-            sr.value = (u64)((int64_t)sr.value + L.survsum[q]);
-        p.res_surv[doc.op_off + q] = sr;
+    // survivors' values are re-read from their op rows (L2-resident): issue those loads and
+    // the minimumClock row first, store them last
+    uint32_t mc = 0;
+    if (p.min_clock && lane < S) mc = p.min_clock[(size_t)ds * S + lane];
+    constexpr int SV = OPL < 2 ? OPL : 2;      // survivor slots whose loads go first (register budget)
+    uint32_t sop[SV], smt[SV];
+    u64 sval[SV];
+#pragma unroll
+    for (int t = 0; t < SV; t++) {
+        const uint32_t q = lane + WAVE * t;
+        sop[t] = 0; smt[t] = 0; sval[t] = 0;
+        if (q < st.total) { sop[t] = L.survop[q]; smt[t] = L.opmeta[sop[t]]; sval[t] = op_value(p, doc, sop[t]); }
     }
     for (uint32_t r = lane; r < R; r += WAVE) {
         hm_reg_result rr;
@@ -1006,14 +1094,13 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
             for (uint32_t a = 0; a < S; a++) row[a] = a < NA_MAX ? (uint32_t)__popcll(an & L.chain[a]) : 0u;
         }
     }
-    uint32_t bc = 0, mc = 0;
+    uint32_t bc = 0;
     if (lane < S) {
         const bool ar = lane < A;
         p.res_clock[(size_t)ds * S + lane] = ar ? (uint32_t)__popcll(L.chain[lane]) : 0u;
         p.res_heads[(size_t)ds * S + lane] = ar ? L.headv[lane] : 0u;
         bc = ar ? L.bclock[lane] : 0u;
         p.res_back_clock[(size_t)ds * S + lane] = bc;              // DocBackend.clock (queued included)
-        if (p.min_clock) mc = p.min_clock[(size_t)ds * S + lane];
     }
     const bool aGTE = __ballot(lane < S && bc < mc) == 0;
     const bool bGTE = __ballot(lane < S && mc < bc) == 0;
@@ -1026,6 +1113,21 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
         r.hist_len = st.H; r.n_queued = (uint32_t)__popcll(q); r.n_surv = st.total;
         r.min_cmp = p.min_clock ? ((aGTE && bGTE) ? 0u : (aGTE ? 1u : (bGTE ? 2u : 3u))) : 0u;
         *dres = r;
+    }
+#pragma unroll
+    for (int t = 0; t < OPL; t++) {
+        const uint32_t q = lane + WAVE * t;
+        if (q >= st.total) continue;
+        uint32_t k, mt;
+        u64 v;
+        if (t < SV) { k = sop[t < SV ? t : 0]; mt = smt[t < SV ? t : 0]; v = sval[t < SV ? t : 0]; }
+        else { k = L.survop[q]; mt = L.opmeta[k]; v = op_value(p, doc, k); }
+        hm_surv_result sr;
+        sr.op = k; sr.vtag = (mt >> 16) & 0xFF; sr.value = v;
+        const uint32_t smt_t = mt;
+        if (p.counters && (smt_t & 0xFF) == HM_SET && ((smt_t >> 8) & 0xFF) == HM_DT_COUNTER && sr.vtag == HM_V_INT)
+            sr.value = (u64)((int64_t)sr.value + L.survsum[q]);
+        p.res_surv[doc.op_off + q] = sr;
     }
 }
 
@@ -1043,32 +1145,46 @@ void merge_small_kernel(SmallParams p) {
     if (threadIdx.x == 0) { for (int i = 0; i < HM_NSTAMP; i++) L.stamps[i] = 0; L.stamps[HM_NSTAMP] = stamp_now(); }
 #endif
     hm_doc_row doc = p.docs[d];
-    stage_rows<OPL, LISTS>(p, L, doc, load_rows<OPL>(p, doc));
+    hm_doc_row docn = {};                    // the next document's row, read one iteration ahead
+    if (d + gridDim.x < p.n_docs) docn = p.docs[d + gridDim.x];
+    uint2 w0, w1, w2;                        // this document's change row (lane = arrival index)
+    {
+        const Rows r = load_rows<OPL>(p, doc);
+        stage_rows<OPL, LISTS>(p, L, doc, r);
+        w0 = r.c0; w1 = r.c1; w2 = r.c2;
+    }
     wave_sync();
     for (;;) {
         // software pipeline over this wave's documents: the next document's rows are
         // loaded before this document's stores and staged to LDS after them
         const uint32_t dn = d + gridDim.x;
         const bool more = dn < p.n_docs;
-        hm_doc_row docn = {};
-        if (more) docn = p.docs[dn];
+        hm_doc_row docnn = {};
+        if (dn + gridDim.x < p.n_docs) docnn = p.docs[dn + gridDim.x];
+        Rows next;
+#if HM_PREFETCH_EARLY
+        if (more) next = load_rows<OPL>(p, docn);
+#endif
         const bool in_env = doc.n_changes <= 64 && doc.n_actors <= NA_MAX && doc.n_ops <= WAVE * OPL &&
                             doc.n_regs <= p.cap_regs && doc.n_objs <= p.cap_objs && doc.n_objs >= 1 &&
                             doc.n_deps <= p.cap_deps && !p.general_only;
         DocState st;
-        const Outcome oc = in_env ? merge_doc_small<OPL, LISTS>(p, L, doc, st) : OUT_UNSUPPORTED;
-        Rows next;
+        const Outcome oc = in_env ? merge_doc_small<OPL, LISTS>(p, L, doc, w0, w1, w2, st) : OUT_UNSUPPORTED;
+#if !HM_PREFETCH_EARLY
         if (more) next = load_rows<OPL>(p, docn);
+#endif
         STAMP(L, 9);
-        write_outputs<LISTS>(p, L, d, doc, oc, st);
+        write_outputs<OPL, LISTS>(p, L, d, doc, oc, st);
         wave_sync();
         STAMP(L, 10);
         if (!more) break;
         stage_rows<OPL, LISTS>(p, L, docn, next);
+        w0 = next.c0; w1 = next.c1; w2 = next.c2;
         wave_sync();
         STAMP(L, 11);
         d = dn;
         doc = docn;
+        docn = docnn;
     }
 #if HM_STAMPS
     if (threadIdx.x == 0)

@@ -5,9 +5,9 @@ set -o pipefail
 R=$PWD
 mkdir -p gpurun_out/phase
 export TMPDIR=/tmp
-for so in $R/hypermerge_amd/_lib/ablate/lib_a*.so; do
+for so in ${@:-$R/hypermerge_amd/_lib/ablate/lib_a*.so}; do
   t=$(basename $so .so)
-  ( cd /tmp && HMGPU_LIB=$so timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY --output-format csv -d $R/gpurun_out/phase/$t -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu > $R/gpurun_out/phase/$t.log 2>&1 ) || { echo "fail $t"; exit 1; }
+  ( cd /tmp && HMGPU_LIB=$so timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD --output-format csv -d $R/gpurun_out/phase/$t -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu > $R/gpurun_out/phase/$t.log 2>&1 ) || { echo "fail $t"; exit 1; }
   python3 - $R/gpurun_out/phase/$t <<'PY'
 import csv, glob, sys
 from collections import defaultdict
