@@ -70,9 +70,11 @@ int launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, hipStream
     p.general_only = (e->flags & HM_CFG_GENERAL_ONLY) ? 1u : 0u;
     p.doc_slot = doc_slot;
     if (b->n_docs == 0) { e->n_last = 0; return HM_OK; }
-    // scratch: [counters 256 B: large-kernel chunk cursor, pool bump pointer][large-kernel pool]
+    // scratch: [counters 256 B: large-kernel cursor, pool bump pointer, deferred count]
+    //          [deferred document list, n_docs u32][large-kernel pool]
     const size_t pool_bytes = hm_large_scratch_bound(b);
-    const size_t need = 256 + pool_bytes;
+    const size_t list_bytes = ((size_t)b->n_docs * 4 + 255) & ~(size_t)255;
+    const size_t need = 256 + list_bytes + pool_bytes;
     if (need > e->pool_size) {
         if (e->pool) { HIPCHK(e, hipStreamSynchronize(s)); HIPCHK(e, hipFree(e->pool)); }
         e->pool = nullptr; e->pool_size = 0;
@@ -82,7 +84,9 @@ int launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, hipStream
     char *pb = (char *)e->pool;
     p.large_cursor = (uint32_t *)pb;
     unsigned long long *pool_used = (unsigned long long *)(pb + 8);
-    HIPCHK(e, hipMemsetAsync(pb, 0, 16, s));
+    p.n_deferred = (uint32_t *)(pb + 16);
+    p.deferred = (uint32_t *)(pb + 256);
+    HIPCHK(e, hipMemsetAsync(pb, 0, 32, s));
     // persistent grid: exactly the resident 1-wave workgroups (VGPR/LDS occupancy of the
     // instantiation), so every wave starts at once and the documents split evenly — a
     // larger grid would leave a partial second round of waves as a tail
@@ -93,7 +97,7 @@ int launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, hipStream
     if (r != hipSuccess) return hip_fail(e, r, "merge_small_kernel launch");
     HIPCHK(e, hipEventRecord(e->ev[1], s));
     HIPCHK(e, hipEventRecord(e->ev[2], s));
-    r = hm_launch_large(p, pb + 256, pool_bytes, pool_used, (uint32_t)e->num_cus * 4, s);
+    r = hm_launch_large(p, pb + 256 + list_bytes, pool_bytes, pool_used, (uint32_t)e->num_cus * 4, s);
     if (r != hipSuccess) return hip_fail(e, r, "merge_large_kernel launch");
     HIPCHK(e, hipEventRecord(e->ev[3], s));
     e->n_last = 2;

@@ -19,7 +19,9 @@ struct SmallParams {
     uint32_t cap_regs, cap_objs;     // LDS carve of this launch (set by the kernel's size class)
     uint32_t cap_deps;               // dep rows per document the carve holds
     uint32_t counters;               // the carve has the counter sums (HM_DOC_HAS_COUNTERS)
-    uint32_t *large_cursor;          // merge_large_kernel's chunk cursor (zeroed before the launch)
+    uint32_t *large_cursor;          // merge_large_kernel's document cursor (zeroed before the launch)
+    uint32_t *n_deferred;            // documents merge_small_kernel handed over (zeroed before the launch)
+    uint32_t *deferred;              // [n_docs] their launch rows, in hand-over order
     uint32_t general_only;           // HM_CFG_GENERAL_ONLY: defer every document
     const uint32_t *doc_slot;        // optional: launch row d -> row of the per-document outputs
                                      // (res_docs, clocks, heads, min_clock); NULL = identity

@@ -1057,6 +1057,7 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
             hm_doc_result r = {};
             r.status = HM_DEFERRED; r.err_change = HM_NONE; r.err_op = HM_NONE;
             *dres = r;
+            p.deferred[atomicAdd(p.n_deferred, 1u)] = d;     // merge_large_kernel's work list
         }
         return;
     }

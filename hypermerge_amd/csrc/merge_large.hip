@@ -595,23 +595,18 @@ __global__ __launch_bounds__(LWG) void merge_large_kernel(SmallParams p, uint8_t
     __shared__ Shared sh;
     const uint32_t tid = threadIdx.x;
     const uint32_t S = p.a_stride;
-    // Deferred documents carry status HM_DEFERRED (written by merge_small_kernel).  Workgroups
-    // claim chunks of LWG result rows from a cursor, compact the deferred ones in LDS and
-    // merge them: one atomic per chunk instead of one per document.
-    __shared__ uint32_t chunk_docs[LWG];
-    __shared__ uint32_t chunk_id, chunk_n;
+    // Deferred documents are listed by merge_small_kernel (p.deferred, p.n_deferred).  Each
+    // workgroup claims one document at a time: deferred documents are the long ones, so
+    // per-document claiming balances the grid (one atomic per document is noise beside a
+    // long document's merge), and an empty list costs one read per workgroup.
+    __shared__ uint32_t claim;
+    const uint32_t nd = *p.n_deferred;
     for (;;) {
-        if (tid == 0) { chunk_id = atomicAdd(p.large_cursor, 1u); chunk_n = 0; }
+        if (tid == 0) claim = atomicAdd(p.large_cursor, 1u);
         bsync();
-        const size_t c0 = (size_t)chunk_id * LWG;
-        if (c0 >= p.n_docs) break;
-        if (c0 + tid < p.n_docs && p.res_docs[hm_slot(p, (uint32_t)(c0 + tid))].status == HM_DEFERRED)
-            chunk_docs[atomicAdd(&chunk_n, 1u)] = (uint32_t)(c0 + tid);
-        bsync();
-        const uint32_t cn = chunk_n;
-        for (uint32_t ci = 0; ci < cn; ci++) {
-        const uint32_t d = chunk_docs[ci];
-        bsync();
+        const uint32_t ci = claim;
+        if (ci >= nd) break;
+        const uint32_t d = p.deferred[ci];
         const hm_doc_row doc = p.docs[d];
         const uint32_t ds = hm_slot(p, d);
         int32_t H = 0;
@@ -651,8 +646,6 @@ __global__ __launch_bounds__(LWG) void merge_large_kernel(SmallParams p, uint8_t
             p.res_back_clock[(size_t)ds * S + tid] = ok && ar ? sh.bclock[tid] : 0u;
         }
         if (tid == 0) p.res_docs[ds] = r;
-        bsync();
-        }
         bsync();
     }
 }
