@@ -48,6 +48,10 @@
 #ifndef HM_PREFETCH_EARLY
 #define HM_PREFETCH_EARLY 0 // 1: the next document's rows are loaded before this document's merge
 #endif
+#ifndef HM_WAVES_PER_EU_OPL4
+#define HM_WAVES_PER_EU_OPL4 3  // 256 ops per document: the op arrays need a larger register budget (measured:
+                                // C2 0.87 -> 0.65 ms at 3 waves/SIMD; list launches (C5) best at 2: 3.99 -> 3.25 ms)
+#endif
 #ifndef HM_WAVES_PER_EU
 #define HM_WAVES_PER_EU 4   // register-allocator target: LDS already caps C4-class launches at ~4.25 waves/SIMD
 #endif
@@ -1133,7 +1137,7 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
 }
 
 template <int OPL, bool LISTS, int CLS>
-__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(HM_WAVES_PER_EU)))
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(OPL >= 4 ? (LISTS ? HM_WAVES_PER_EU_OPL4 - 1 : HM_WAVES_PER_EU_OPL4) : HM_WAVES_PER_EU)))
 void merge_small_kernel(SmallParams p) {
     extern __shared__ __align__(16) uint8_t lds_raw[];
     typedef SizeClass<CLS> C;

@@ -5,7 +5,8 @@ R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for so in sys.argv[1:]:
     env = dict(os.environ, HMGPU_LIB=os.path.abspath(so))
     out = subprocess.run([sys.executable, os.path.join(R, "bench.py"), "--steps", "5", "--warmup", "2", "--no-cpu",
-                          "--docs", os.environ.get("ABL_DOCS", "1000000")], env=env, capture_output=True, text=True,
+                          "--docs", os.environ.get("ABL_DOCS", "1000000"),
+                          "--config", os.environ.get("ABL_CONFIG", "C4"), "--no-traffic", "--no-e2e"], env=env, capture_output=True, text=True,
                          timeout=600)
     line = [l for l in out.stdout.splitlines() if l.startswith("{")]
     print(os.path.basename(so), json.loads(line[-1])["roofline"]["kernel_ms"] if line else out.stderr[-800:], flush=True)
