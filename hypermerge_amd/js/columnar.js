@@ -160,6 +160,27 @@ class DocEncoder {
   }
 }
 
+// Block.unpack (src/Block.ts:18-29): a hypercore block is raw JSON (header '{"', blocks
+// written before compression was added) or 'BR' + brotli(JSON).  iltorb (the reference's native
+// brotli) is not part of this engine; Node's zlib brotli decodes the same stream format.
+// JsonBuffer.parse is JSON.parse(buffer.toString()) (src/JsonBuffer.ts:1-4).
+const zlib = require('zlib')
+function unpackBlock(data) {
+  const buf = Buffer.isBuffer(data) ? data : Buffer.from(data.buffer, data.byteOffset, data.byteLength)
+  const header = buf.slice(0, 2).toString()
+  switch (header) {
+    case '{"':
+      return JSON.parse(buf.toString())
+    case 'BR':
+      return JSON.parse(zlib.brotliDecompressSync(buf.slice(2)).toString())
+    default:
+      throw new Error(`fail to unpack blocks - head is '${header}'`)
+  }
+}
+
+// Actor.parseBlock over downloaded blocks (src/Actor.ts:120-141): one Change per block
+function unpackBlocks(blocks) { return blocks.map(unpackBlock) }
+
 // Concatenate per-document appends into one hm_batch (rows' offsets rebased).
 function buildBatch(appends, aStride) {
   const n = appends.length
@@ -208,5 +229,5 @@ function readDocResult(buf, i) {
 module.exports = {
   ROOT_ID, ACTIONS, DATATYPES, V, HEAD, NONE, DOC_HAS_LISTS, DOC_HAS_COUNTERS,
   DOC_ROW, CHANGE_ROW, DEP_ROW, OP_ROW, DOC_RESULT, REG_RESULT, SURV_RESULT,
-  StringPool, DocEncoder, buildBatch, readDocResult, canonical,
+  StringPool, DocEncoder, buildBatch, readDocResult, canonical, unpackBlock, unpackBlocks,
 }

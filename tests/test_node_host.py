@@ -78,3 +78,17 @@ def test_js_clockstore_matches_reference_sql():
     got = json.loads(p.stdout)
     for name, c in gold["cases"].items():
         assert got[name] == c["results"], name
+
+
+def test_block_unpack_raw_and_brotli():
+    """Block.unpack (src/Block.ts:18-29): raw '{"' JSON blocks and 'BR' + brotli blocks decode to
+    the same Change objects and the same columnar rows; an unknown header throws the
+    reference's message."""
+    b = synth.generate(synth.config("C5", n_docs=3))
+    changes = [c for i in range(b.n_docs) for c in decode_doc(b, i)][:200]
+    p = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "run_blocks.js")], input=json.dumps({"changes": changes}),
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    got = json.loads(p.stdout)
+    assert got["same"] and got["rowsSame"] and got["n"] == len(changes)
+    assert got["err"] == "fail to unpack blocks - head is 'xx'"
