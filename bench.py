@@ -31,6 +31,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+ARRIVAL = {0: "generation", 1: "actor-major (loadDocument)", 2: "shuffled"}
 WORKLOAD_KIND = {"C1": "map sets, 2 alternating actors", "C2": "map LWW sets + counters",
                  "C3": "text RGA inserts/deletes", "C4": "map LWW sets",
                  "C5": "nested maps/lists, conflicts, deletes, causally blocked + duplicate changes"}
@@ -55,6 +56,9 @@ def main() -> int:
     ap.add_argument("--check-docs", type=int, default=20_000, help="docs checked against the oracle")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host->device->host (PCIe-inclusive) leg")
+    ap.add_argument("--arrival", type=int, default=None,
+                    help="override the config's arrival order (0 generation, 1 actor-major as RepoBackend.loadDocument "
+                         "concatenates, 2 shuffled)")
     args = ap.parse_args()
 
     ws, rank, local = _dist()
@@ -71,7 +75,8 @@ def main() -> int:
     from hypermerge_amd.engine import Engine
 
     t0 = time.time()
-    cfg = synth.config(args.config, n_docs=args.docs, shard=rank, n_shards=ws)
+    over = {} if args.arrival is None else {"arrival": args.arrival}
+    cfg = synth.config(args.config, n_docs=args.docs, shard=rank, n_shards=ws, **over)
     batch = synth.generate(cfg, threads=min(16, os.cpu_count() or 1))
     gen_s = time.time() - t0
 
@@ -223,7 +228,8 @@ def main() -> int:
             "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "u32", "data": "synthetic (seeded gossip feeds, hypermerge_amd/csrc/synth.cpp)",
             "config": {"workload": f"{args.config}: {nd} docs/GPU x {batch.docs['n_actors'].max()} actors x "
-                                   f"{nc / max(nd, 1):.0f} changes/doc, {WORKLOAD_KIND.get(args.config, '')}", "docs_per_gpu": nd,
+                                   f"{nc / max(nd, 1):.0f} changes/doc, {WORKLOAD_KIND.get(args.config, '')}"
+                                   + ("" if args.arrival is None else f", arrival order {ARRIVAL[args.arrival]}"), "docs_per_gpu": nd,
                        "changes_per_gpu": nc, "ops_per_gpu": no, "parallelism": f"doc-shard{ws}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": traffic["bytes"] if traffic else None,

@@ -45,6 +45,9 @@
 #define HM_STAMPS 0     // diagnostic builds only: per-phase s_memtime shares (tools/stamps.py); never timed
 #endif
 #define HM_NSTAMP 12
+#ifndef HM_DOCROW_AHEAD
+#define HM_DOCROW_AHEAD 0   // 1: the next document's row is read one iteration earlier (more live SGPRs)
+#endif
 #ifndef HM_PREFETCH_EARLY
 #define HM_PREFETCH_EARLY 0 // 1: the next document's rows are loaded before this document's merge
 #endif
@@ -1150,8 +1153,10 @@ void merge_small_kernel(SmallParams p) {
     if (threadIdx.x == 0) { for (int i = 0; i < HM_NSTAMP; i++) L.stamps[i] = 0; L.stamps[HM_NSTAMP] = stamp_now(); }
 #endif
     hm_doc_row doc = p.docs[d];
+#if HM_DOCROW_AHEAD
     hm_doc_row docn = {};                    // the next document's row, read one iteration ahead
     if (d + gridDim.x < p.n_docs) docn = p.docs[d + gridDim.x];
+#endif
     uint2 w0, w1, w2;                        // this document's change row (lane = arrival index)
     {
         const Rows r = load_rows<OPL>(p, doc);
@@ -1164,8 +1169,13 @@ void merge_small_kernel(SmallParams p) {
         // loaded before this document's stores and staged to LDS after them
         const uint32_t dn = d + gridDim.x;
         const bool more = dn < p.n_docs;
+#if HM_DOCROW_AHEAD
         hm_doc_row docnn = {};
         if (dn + gridDim.x < p.n_docs) docnn = p.docs[dn + gridDim.x];
+#else
+        hm_doc_row docn = {};
+        if (more) docn = p.docs[dn];
+#endif
         Rows next;
 #if HM_PREFETCH_EARLY
         if (more) next = load_rows<OPL>(p, docn);
@@ -1189,7 +1199,9 @@ void merge_small_kernel(SmallParams p) {
         STAMP(L, 11);
         d = dn;
         doc = docn;
+#if HM_DOCROW_AHEAD
         docn = docnn;
+#endif
     }
 #if HM_STAMPS
     if (threadIdx.x == 0)

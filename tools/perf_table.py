@@ -10,7 +10,8 @@ import sys
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # config, docs per GPU, CPU sample docs, parity-check docs, timed steps
 RUNS = [("C1", 1, 1, 1, 3), ("C2", 100_000, 20_000, 5_000, 10), ("C3", 10_000, 100, 100, 3),
-        ("C4", 1_000_000, 200_000, 20_000, 20), ("C5", 100_000, 20_000, 5_000, 10)]
+        ("C4", 1_000_000, 200_000, 20_000, 20), ("C5", 100_000, 20_000, 5_000, 10),
+        ("C4am", 1_000_000, 100_000, 10_000, 10)]      # C4 in loadDocument's actor-major order
 
 
 def main() -> int:
@@ -19,8 +20,9 @@ def main() -> int:
     for cfg, docs, cpu_docs, check, steps in RUNS:
         if only and cfg not in only:
             continue
-        cmd = [sys.executable, os.path.join(R, "bench.py"), "--config", cfg, "--docs", str(docs), "--steps", str(steps),
-               "--warmup", "2", "--cpu-sample-docs", str(cpu_docs), "--check-docs", str(check), "--no-traffic"]
+        extra = ["--arrival", "1"] if cfg.endswith("am") else []
+        cmd = [sys.executable, os.path.join(R, "bench.py"), "--config", cfg[:2], "--docs", str(docs), "--steps", str(steps),
+               "--warmup", "2", "--cpu-sample-docs", str(cpu_docs), "--check-docs", str(check), "--no-traffic"] + extra
         p = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
         lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
         if p.returncode or not lines:
