@@ -62,6 +62,8 @@ class GpuBackendState {
     this.handle = addon.openDoc(engine.store)
     this.enc = new C.DocEncoder(engine.pool)
     this.log = []
+    this.opActor = []                // doc-local op index -> [op, actor] (the log's ops in order)
+    this.view = null                 // materialized view of the last patch (diff base)
     this.histLen = 0
     this.nQueued = 0
     this.clock = {}
@@ -88,6 +90,7 @@ class GpuEngine {
     this.scheduled = false
     this.onError = o.onError || null
     this.submits = 0
+    this.patches = o.patches !== false  // emit patch diffs (one device read per patch)
   }
 
   init() { return new GpuBackendState(this) }
@@ -154,6 +157,7 @@ class GpuEngine {
       }
       const base = state.log.length
       state.log.push(...job.changes)
+      for (const c of job.changes) for (const op of c.ops || []) state.opActor.push([op, c.actor])
       const prevHist = state.histLen
       state.histLen = res.histLen
       state.nQueued = res.nQueued
@@ -199,9 +203,113 @@ class GpuEngine {
   }
 }
 
+// ---------------- patches (Automerge makePatch, consumed by Frontend.applyPatch) ----------------
+// clock / deps are applied-only (queued changes excluded).  `diffs` turn the frontend's copy of
+// the document from the state of the previous patch into the current one, in the Automerge 0.12
+// diff vocabulary (SURVEY.md Appendix A.4): {action:'create', obj, type},
+// {action:'set'|'remove', type:'map'|'table', obj, key, value, link?, datatype?, conflicts?},
+// {action:'insert'|'set'|'remove', type:'list'|'text', obj, index, elemId?, value, ...}.
+// They are derived from the GPU's merged registers (one diff per changed register / element,
+// removals before insertions), not replayed op by op: the document a frontend builds from them
+// equals the merged state, but the diff sequence is not Automerge's per-op sequence (parity of
+// that sequence is unpinned: Automerge 0.12 is not available here).
+const TYPE_OF = { 0: 'map', 1: 'table', 2: 'list', 3: 'text' }
+const DT_NAME = { 1: 'counter', 2: 'timestamp' }
+const TWO32 = 4294967296
+
+function opValue(state, vtag, lo, hi) {
+  switch (vtag) {
+    case C.V.NULL: return { value: null }
+    case C.V.FALSE: return { value: false }
+    case C.V.TRUE: return { value: true }
+    case C.V.INT: return { value: hi >= 0x80000000 ? (hi - TWO32) * TWO32 + lo : hi * TWO32 + lo }
+    case C.V.FLOAT: { const b = Buffer.alloc(8); b.writeUInt32LE(lo, 0); b.writeUInt32LE(hi, 4); return { value: b.readDoubleLE(0) } }
+    case C.V.STR: return { value: state.engine.pool.strings[lo] }
+    case C.V.OBJ: return { value: state.enc.objList[lo], link: true }
+    default: throw new Error(`unknown value tag ${vtag}`)
+  }
+}
+
+// the merged document as {objUuid -> {type, keys: Map(key -> entry) | elems: [[elemId, entry]]}}
+function materialize(state) {
+  const r = addon.read(state.engine.store, state.handle)
+  const objType = new Map([[0, 0]])
+  for (const [op] of state.opActor) {
+    const a = C.ACTIONS[op.action]
+    if (a <= C.ACTIONS.makeText) { const o = state.enc.objs.get(op.obj); if (!objType.has(o)) objType.set(o, a) }
+  }
+  const view = new Map()
+  const nRegs = r.regs.length / C.REG_RESULT
+  for (let g = 0; g < nRegs; g++) {
+    const b = g * C.REG_RESULT
+    const n = r.regs.readUInt32LE(b), off = r.regs.readUInt32LE(b + 4), li = r.regs.readInt32LE(b + 8), o = r.regs.readUInt32LE(b + 12)
+    if (!n || o === C.NONE) continue
+    const t = objType.has(o) ? objType.get(o) : 0
+    const list = t === 2 || t === 3
+    if (list && li < 0) continue
+    const surv = []
+    for (let q = 0; q < n; q++) {
+      const sb = (off + q) * C.SURV_RESULT
+      const k = r.surv.readUInt32LE(sb), vt = r.surv.readUInt32LE(sb + 4)
+      const [op, actor] = state.opActor[k]
+      const v = opValue(state, vt, r.surv.readUInt32LE(sb + 8), r.surv.readUInt32LE(sb + 12))
+      if (op.datatype) v.datatype = op.datatype
+      surv.push([actor, v])
+    }
+    const entry = Object.assign({}, surv[0][1])
+    if (surv.length > 1) entry.conflicts = surv.slice(1).map(([actor, v]) => Object.assign({ actor }, v))
+    const uuid = state.enc.objList[o]
+    let ov = view.get(uuid)
+    if (!ov) { ov = { type: TYPE_OF[t], keys: new Map(), elems: [] }; view.set(uuid, ov) }
+    const key = state.enc.regList[g][1]
+    if (list) ov.elems[li] = [key, entry]
+    else ov.keys.set(key, entry)
+  }
+  // objects created but still empty (a linked empty map/list)
+  for (const [o, t] of objType) {
+    const uuid = state.enc.objList[o]
+    if (!view.has(uuid)) view.set(uuid, { type: TYPE_OF[t], keys: new Map(), elems: [] })
+  }
+  return view
+}
+
+function diffViews(prev, next) {
+  const diffs = []
+  const sig = (e) => JSON.stringify(e)
+  for (const [uuid, ov] of next) if (uuid !== C.ROOT_ID && !prev.has(uuid)) diffs.push({ action: 'create', obj: uuid, type: ov.type })
+  for (const [uuid, ov] of next) {
+    const po = prev.get(uuid) || { keys: new Map(), elems: [] }
+    if (ov.type === 'list' || ov.type === 'text') {
+      const keep = new Set(ov.elems.map(([id]) => id))
+      const was = new Map(po.elems.map(([id, e], i) => [id, [i, e]]))
+      for (let i = po.elems.length - 1; i >= 0; i--)
+        if (!keep.has(po.elems[i][0])) diffs.push({ action: 'remove', type: ov.type, obj: uuid, index: i })
+      ov.elems.forEach(([id, e], i) => {
+        if (!was.has(id)) diffs.push(Object.assign({ action: 'insert', type: ov.type, obj: uuid, index: i, elemId: id }, e))
+      })
+      ov.elems.forEach(([id, e], i) => {
+        if (was.has(id) && sig(was.get(id)[1]) !== sig(e)) diffs.push(Object.assign({ action: 'set', type: ov.type, obj: uuid, index: i }, e))
+      })
+    } else {
+      const keys = Array.from(new Set([...po.keys.keys(), ...ov.keys.keys()])).sort()
+      for (const k of keys) {
+        const a = po.keys.get(k), b = ov.keys.get(k)
+        if (b === undefined) diffs.push({ action: 'remove', type: ov.type, obj: uuid, key: k })
+        else if (a === undefined || sig(a) !== sig(b)) diffs.push(Object.assign({ action: 'set', type: ov.type, obj: uuid, key: k }, b))
+      }
+    }
+  }
+  return diffs
+}
+
 function makePatch(state) {
-  // clock / deps are applied-only (queued changes excluded); diffs are not emitted yet
-  return { clock: Object.assign({}, state.clock), deps: Object.assign({}, state.deps), canUndo: false, canRedo: false, diffs: [] }
+  let diffs = []
+  if (state.engine.patches) {
+    const view = materialize(state)
+    diffs = diffViews(state.view || new Map(), view)
+    state.view = view
+  }
+  return { clock: Object.assign({}, state.clock), deps: Object.assign({}, state.deps), canUndo: false, canRedo: false, diffs }
 }
 
 function makeBackend(engine) {

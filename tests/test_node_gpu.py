@@ -66,3 +66,34 @@ def test_batched_feed_matches_oracle():
         assert g["clock"] == s["clock"] and g["deps"] == s["deps"], i
         assert g["backendClock"] == s["backend_clock"], i
         assert g["types"][-1] in ("RemotePatchMsg", "ReadyMsg")
+
+
+@pytest.mark.parametrize("name,n", [("C5", 200), ("C3", 12), ("C2", 100)])
+def test_patch_diffs_rebuild_the_merged_document(name, n):
+    """Applying every patch's diffs in order (a restatement of Frontend.applyPatch's effect,
+    src/DocFrontend.ts:162-179) rebuilds exactly the canonical merged document of the oracle's
+    cold merge of the same changes — maps, conflicts, counters, links, lists and text."""
+    import numpy as np
+    from hypermerge_amd import synth
+    from hypermerge_amd.columnar import decode_doc, encode
+    from hypermerge_amd.render import doc_summary
+    import oracle.oracle as O
+    over = {"changes_per_actor": 40} if name == "C3" else {}
+    b = synth.generate(synth.config(name, n_docs=n, **over))
+    docs = [decode_doc(b, i) for i in range(b.n_docs)]
+    rng = np.random.default_rng(23)
+    chunked = []
+    for chs in docs:
+        cuts = sorted(rng.integers(1, len(chs) + 1, size=3))
+        chunked.append([chs[:cuts[0]], chs[cuts[0]:cuts[1]], chs[cuts[1]:cuts[2]], chs[cuts[2]:]])
+    p = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "run_patches.js")], input=json.dumps({"docs": chunked}),
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr
+    got = json.loads(p.stdout)["docs"]
+    cold = encode(docs, 8)
+    co = O.merge(cold)
+    for i, g in enumerate(got):
+        s = doc_summary(cold, co, i)
+        assert s["status"] == "OK"
+        assert g["state"] == json.loads(json.dumps(s["state"])), i
+        assert g["nDiffs"] > 0 and g["nonEmpty"] > 0
