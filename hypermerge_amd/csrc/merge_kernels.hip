@@ -233,6 +233,15 @@ __device__ __forceinline__ void need_set(uint32_t &lo, uint32_t &hi, uint32_t a,
 }
 
 
+// the (actor, seq) table: NA_MAX x 64 words of all ones, two 16-byte stores per lane
+__device__ __forceinline__ void clear_first(LDS uint32_t *first) {
+    static_assert(NA_MAX * 64 == 2 * WAVE * 4, "first-table size");
+    LDS uint4 *f4 = (LDS uint4 *)first;
+    const uint4 ones = make_uint4(~0u, ~0u, ~0u, ~0u);
+    f4[threadIdx.x] = ones;
+    f4[threadIdx.x + WAVE] = ones;
+}
+
 // tie order key of an assign at position p on its register: odd p first (p descending),
 // then even p ascending ("append, then reverse" after every assign)
 __device__ __forceinline__ uint32_t tie_order(uint32_t pc) { return (pc & 1) ? (0x10000u - pc) : (0x20000u + pc); }
@@ -516,7 +525,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     STAMP(L, 0);
     const bool act = lane < n;
     const hm_change_row c = change_of(w0, w1, w2);      // zero rows for lanes >= n (load_rows)
-    for (uint32_t i = lane; i < NA_MAX * 64; i += WAVE) L.first[i] = 0xFFFFFFFFu;
+    clear_first(L.first);
     if (lane < NA_MAX) { L.base[lane] = 0xFFFFFFFFu; L.bclock[lane] = 0; L.headv[lane] = 0; L.chain[lane] = 0; }
     if (lane == 0) { *L.errkey = ~0ull; L.flags[0] = 0; L.flags[1] = 0; *L.cov = 0; }
     const uint32_t dep_lo = doc.dep_off, ndep = doc.n_deps;
@@ -629,7 +638,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         identity = __ballot(dup) == 0;
     } else {
         // ---- exact emulation of addChange / applyQueuedOps (wave-uniform control) ----
-        for (uint32_t i = lane; i < NA_MAX * 64; i += WAVE) L.first[i] = 0xFFFFFFFFu;   // -> applied lane
+        clear_first(L.first);                                                           // -> applied lane
         wave_sync();
         uint32_t crel_lo = 0, crel_hi = 0;      // relative applied clock per actor (bytes)
         u64 queued = 0;

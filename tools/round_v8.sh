@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out
 [ -n "$SKIP_TESTS" ] || timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
 [ -n "$SKIP_TESTS" ] || tail -1 gpurun_out/gpu_tests.log
-for c in "C4 1000000" "C5 100000" "C4 1000000 1"; do
+for c in ${CFGS:-"C4 1000000" "C5 100000" "C4 1000000 1"}; do
   set -- $c
   for so in hypermerge_amd/_lib/ablate/lib_*.so; do
     a=""; [ -n "$3" ] && a="--arrival $3"
