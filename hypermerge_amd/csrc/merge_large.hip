@@ -38,7 +38,7 @@ __device__ __forceinline__ u64 err_key(uint32_t h, uint32_t op_plus1, uint32_t a
 struct Shared {
     uint32_t base[LA_MAX], maxs[LA_MAX], tabo[LA_MAX + 1], clock[LA_MAX], bclock[LA_MAX], headv[LA_MAX];
     uint32_t maxad[LA_MAX];
-    uint32_t flags, all_ok, H, nins, nl, total, lists;
+    uint32_t flags, all_ok, H, nins, nl, total, lists, grew;
     u64 errkey;
     uint32_t scan[LWG / 64 + 1];
     u64 scratch_base;
@@ -84,6 +84,7 @@ struct Scratch {
     int32_t *hist;
     u64 *opkey, *insmin, *objslot, *seglist, *nodekey, *survabs;
     int64_t *survsum;
+    uint32_t *vc;                   // [n * A] closure rows (L2 pointer jumping, second buffer)
 };
 
 __host__ __device__ inline size_t large_carve(uintptr_t base, uint32_t n, uint32_t m, uint32_t R, uint32_t O,
@@ -92,7 +93,7 @@ __host__ __device__ inline size_t large_carve(uintptr_t base, uint32_t n, uint32
     const uint32_t NP = R + O, NE = 2 * (m + O);
 #define TK(f, T_, cnt) do { S->f = (T_ *)(base + o); o = (o + (size_t)(cnt) * sizeof(T_) + 15) & ~(size_t)15; } while (0)
     TK(opkey, u64, m); TK(insmin, u64, R); TK(objslot, u64, O); TK(seglist, u64, m); TK(nodekey, u64, m);
-    TK(survabs, u64, m); TK(survsum, int64_t, m);
+    TK(survabs, u64, m); TK(survsum, int64_t, m); TK(vc, uint32_t, (size_t)n * A);
     TK(tab, uint32_t, T); TK(h2a, uint32_t, n); TK(hist, int32_t, n); TK(opchg, uint32_t, m);
     TK(segmax, uint32_t, (size_t)R * A); TK(segcnt, uint32_t, R); TK(survcnt, uint32_t, R);
     TK(regoff, uint32_t, R); TK(regobj, uint32_t, R); TK(segoff, uint32_t, R); TK(segfill, uint32_t, R);
@@ -274,8 +275,94 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, const hm_do
     const uint32_t H = sh.H;
     H_out = (int32_t)H;
 
-    // ---- L2: allDeps by the literal fold, history order, lanes = actors (wave 0) ----
-    if (wave == 0) {
+    // ---- L2: allDeps ----
+    // (a) the transitive closure by pointer jumping over the actor chains, every change at once:
+    //     v(i) <- max(v(i), v(latest change of actor a known to v(i))) for every actor a, from
+    //     v(i) = the change's own deps (deps.set(actor, seq-1)); an actor's changes are a chain, so
+    //     the fixpoint is the closure (log-depth rounds instead of a history-length serial walk).
+    // (b) every change folds its deps literally (key order, `.set` may lower an entry) over the
+    //     closure rows of its deps; if that equals its closure everywhere, the closure is allDeps.
+    //     Otherwise (a listed dep dominated by another: never for heads-based deps) the literal
+    //     fold runs serially in history order below.
+    uint32_t *cur = p.res_all_deps + (size_t)doc.change_off * S, *nxt = X.vc;   // row stride S / A
+    for (uint32_t i = tid; i < n; i += LWG) {
+        uint32_t *row = cur + (size_t)i * S;
+        for (uint32_t a = 0; a < S; a++) row[a] = 0;
+        if (X.hist[i] < 0) continue;
+        const hm_change_row c = CH[i];
+        for (uint32_t j = 0; j < c.n_deps; j++) {
+            const hm_dep_row dp = p.deps[c.dep_off + j];
+            const uint32_t sq = dp.actor == c.actor ? c.seq - 1 : dp.seq;
+            if (row[dp.actor] < sq) row[dp.actor] = sq;
+        }
+        if (row[c.actor] < c.seq - 1) row[c.actor] = c.seq - 1;
+    }
+    bsync();
+    for (;;) {                                  // monotone and bounded: terminates (rounds ~ log depth)
+        if (tid == 0) sh.grew = 0;
+        bsync();
+        bool grew = false;
+        for (uint32_t i = tid; i < n; i += LWG) {
+            const uint32_t *row = cur + (size_t)i * S;
+            uint32_t *out = nxt + (size_t)i * A;
+            for (uint32_t a = 0; a < A; a++) out[a] = row[a];
+            if (X.hist[i] < 0) continue;
+            for (uint32_t a = 0; a < A; a++) {
+                const uint32_t sq = row[a];
+                if (!sq) continue;
+                const uint32_t sl = slot_of(a, sq), ti = sl == 0xFFFFFFFFu ? 0xFFFFFFFFu : X.tab[sl];
+                if (ti >= n) continue;                           // not applied: cannot occur for deps of applied changes
+                const uint32_t *r2 = cur + (size_t)ti * S;       // the applied change (a, sq)
+                for (uint32_t b = 0; b < A; b++) {
+                    const uint32_t v = b == a ? sq : r2[b];
+                    if (out[b] < v) { out[b] = v; grew = true; }
+                }
+            }
+        }
+        if (grew) sh.grew = 1;
+        bsync();
+        for (uint32_t i = tid; i < n; i += LWG)
+            for (uint32_t a = 0; a < A; a++) cur[(size_t)i * S + a] = nxt[(size_t)i * A + a];
+        bsync();
+        if (!sh.grew) break;
+    }
+    if (tid == 0) sh.all_ok = 1;
+    bsync();
+    for (uint32_t i = tid; i < n; i += LWG) {
+        if (X.hist[i] < 0) continue;
+        const hm_change_row c = CH[i];
+        const uint32_t *row = cur + (size_t)i * S;
+        uint32_t *acc = nxt + (size_t)i * A;
+        for (uint32_t a = 0; a < A; a++) acc[a] = 0;
+        auto fold = [&](uint32_t a, uint32_t sq) {
+            if (sq == 0) return;
+            const uint32_t sl = slot_of(a, sq), ti = sl == 0xFFFFFFFFu ? 0xFFFFFFFFu : X.tab[sl];
+            if (ti >= n) { acc[a] = 0xFFFFFFFFu; return; }       // (cannot occur) forces the serial path
+            const uint32_t *r2 = cur + (size_t)ti * S;
+            for (uint32_t b = 0; b < A; b++) if (acc[b] < r2[b]) acc[b] = r2[b];
+            acc[a] = sq;
+        };
+        bool own = false;
+        for (uint32_t j = 0; j < c.n_deps; j++) {
+            const hm_dep_row dp = p.deps[c.dep_off + j];
+            if (dp.actor == c.actor) { own = true; fold(c.actor, c.seq - 1); }
+            else fold(dp.actor, dp.seq);
+        }
+        if (!own) fold(c.actor, c.seq - 1);
+        bool same = true;
+        for (uint32_t a = 0; a < A; a++) same = same && acc[a] == row[a];
+        if (!same) sh.all_ok = 0;
+    }
+    bsync();
+    const bool closure_ok = sh.all_ok != 0;
+    if (closure_ok) {
+        for (uint32_t h = tid; h < H; h += LWG) {
+            const uint32_t *row = cur + (size_t)X.h2a[h] * S;
+            for (uint32_t a = 0; a < A; a++) atomicMax(&sh.maxad[a], row[a]);
+        }
+    }
+    // literal fold, history order, lanes = actors (wave 0)
+    if (!closure_ok && wave == 0) {
         for (uint32_t h = 0; h < H; h++) {
             const uint32_t ci = X.h2a[h];
             const hm_change_row c = CH[ci];

@@ -31,13 +31,14 @@ def main() -> int:
         d = json.loads(lines[-1])
         rows.append(d)
         print("<!-- " + json.dumps(d) + " -->", flush=True)
-    print("| config | workload | merged changes/s (kernel, both kernels) | ms/step | merge_small_kernel % HBM roofline "
+    print("| config | workload | merged changes/s (kernel, both kernels) | ms/step | % HBM roofline (algorithmic bytes / step) "
           "| end-to-end changes/s (PCIe incl.) | CPU 1 thread | CPU N threads | parity sample | unsupported docs |")
     print("|---|---|---|---|---|---|---|---|---|---|")
     for d in rows:
         c, e, m = d.get("cpu_baseline") or {}, d.get("end_to_end") or {}, d.get("cpu_parallel") or {}
         print(f"| {d['config']['workload'].split(':')[0]} | {d['config']['workload'].split(': ', 1)[1]} | {d['value']:.3e} "
-              f"| {d['ms_per_step']:.3f} | {100 * d['roofline']['frac']:.1f} % | {e.get('value', float('nan')):.3e} "
+              f"| {d['ms_per_step']:.3f} | {100 * d['roofline']['alg_bytes'] / (d['ms_per_step'] * 1e-3) / 8e12:.1f} % "
+              f"| {e.get('value', float('nan')):.3e} "
               f"| {c.get('value', float('nan')):.3e} | {m.get('value', float('nan')):.3e} ({m.get('cores', '?')} threads) "
               f"| {d['parity_sample_ok']} | {d['unsupported_docs']} |")
     return 0
