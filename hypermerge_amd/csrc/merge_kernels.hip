@@ -636,6 +636,94 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         if (act) hist = dup ? -2 : (int32_t)__popcll(appl & ((1ull << lane) - 1));
         H = (uint32_t)__popcll(appl);
         identity = __ballot(dup) == 0;
+    } else if (__ballot(dup && cid_first != c.content_id) == 0) {
+        // ---- addChange / applyQueuedOps, a pass at a time (no mismatched duplicates, so every
+        // dep is met by its first arrival and a duplicate is ready with its original) ----
+        // The queue is arrival order.  After an arrival, pass 1 can only apply it (the queue was
+        // at a fixpoint); each further pass applies, in queue order, every queued change whose
+        // deps were met before the pass or by an earlier change of the same pass: that set is a
+        // fixpoint of one ballot per dependency level.  Duplicates are removed as no-ops.
+        // A duplicate copy stands for its (actor, seq) if it is the first copy applied (its
+        // original may still wait in the queue): applied-ness is tracked per key = the first
+        // arrival's lane.  Documents without duplicates skip the per-copy loops.
+        // every dep's first-arrival lane (dall) and whether the batch can satisfy them all
+        u64 dall = 0;
+        bool never = false;
+        uint32_t pred_any = 0xFFu;
+        {
+            const uint32_t maxd = wave_max(act ? (uint32_t)c.n_deps : 0u);
+            for (uint32_t j = 0; j < maxd; j++) {
+                const bool live = act && j < c.n_deps;
+                const uint32_t inf = L.depinfo[live ? my_dep0 + j : 0u];
+                const uint32_t a = (inf >> 16) & (NA_MAX - 1), rel = (inf >> 8) & 0x7F, f = inf & 0x7F;
+                const bool use = live && a != actor && rel != 0;
+                never |= use && (rel == 0x7F || f == 0x7F);
+                dall |= (use && rel != 0x7F && f != 0x7F) ? (1ull << f) : 0ull;
+            }
+            const uint32_t ps = seq - 1;
+            const bool hp = act && ps != 0, inb = ps >= mybase;
+            const uint32_t f = L.first[a8 * 64 + ((ps - mybase) & 63)];
+            never |= hp && (!inb || f >= 64);
+            dall |= (hp && inb && f < 64) ? (1ull << f) : 0ull;
+            pred_any = (hp && inb && f < 64) ? f : 0xFFu;
+        }
+        const u64 dupm = __ballot(dup), nodupm = __ballot(act && !dup);
+        const u64 below = (1ull << lane) - 1;
+        const uint32_t key = first_me & 63;
+        u64 applied = 0, queue = 0;                       // applied keys; queued lanes
+        bool copy_applied = false;                        // a duplicate copy stands for its key
+        for (uint32_t i = 0; i < n; i++) {
+            queue |= 1ull << i;
+            u64 P = __ballot(lane == i && !never && (dall & ~applied) == 0);
+            while (P) {
+                // which lanes of the pass apply a change (the rest are duplicate no-ops)
+                u64 ap = P & nodupm & ~applied, keys = ap;
+                for (u64 dm = P & dupm; dm; dm &= dm - 1) {
+                    const uint32_t d = (uint32_t)__builtin_ctzll(dm);
+                    const uint32_t kd = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)d);
+                    if (!((applied | keys) >> kd & 1)) {
+                        ap |= 1ull << d; keys |= 1ull << kd; copy_applied = true;
+                        if (lane == d) L.first[a8 * 64 + (slot & 63)] = lane;   // (actor, seq) -> applied lane
+                    }
+                }
+                if ((P >> lane) & 1) hist = ((ap >> lane) & 1) ? (int32_t)(H + (uint32_t)__popcll(ap & below)) : -2;
+                H += (uint32_t)__popcll(ap);
+                applied |= keys;
+                queue &= ~P;
+                // the next pass: queued changes whose deps are met before it or by an earlier
+                // change of the same pass
+                u64 np = 0;
+                for (;;) {
+                    u64 kb = np & nodupm & below;                 // keys met earlier in the pass
+                    for (u64 dm = np & dupm; dm; dm &= dm - 1) {
+                        const uint32_t d = (uint32_t)__builtin_ctzll(dm);
+                        const uint32_t kd = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)d);
+                        kb |= d < lane ? (1ull << kd) : 0ull;
+                    }
+                    const u64 nx = __ballot(((queue >> lane) & 1) && !never && ((dall & ~applied) & ~kb) == 0);
+                    if (nx == np) break;
+                    np = nx;
+                }
+                P = np;
+            }
+        }
+        // direct deps of the applied changes: their first arrivals, or the applied copies
+        const bool ap = act && hist >= 0;
+        dmask = ap ? dall : 0ull;
+        pred_arr = ap ? pred_any : 0xFFu;
+        if (copy_applied) {
+            wave_sync();
+            dmask = 0; pred_arr = 0xFFu;
+            if (ap) {
+                for (uint32_t j = 0; j < c.n_deps; j++) {
+                    const uint32_t pk = L.deps[my_dep0 + j];
+                    const uint32_t a = pk >> 24, s = pk & 0xFFFFFF;
+                    if (a == actor || s == 0) continue;
+                    dmask |= 1ull << L.first[a * 64 + (s - L.base[a])];
+                }
+                if (seq - 1 != 0) { pred_arr = L.first[actor * 64 + (seq - 1 - mybase)]; dmask |= 1ull << pred_arr; }
+            }
+        }
     } else {
         // ---- exact emulation of addChange / applyQueuedOps (wave-uniform control) ----
         clear_first(L.first);                                                           // -> applied lane
