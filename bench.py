@@ -266,7 +266,7 @@ def _pmc_traffic(args):
         d = tempfile.mkdtemp(prefix="hm_pmc_", dir="/tmp")
         cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "run", "--",
                sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1", "--no-cpu",
-               "--no-traffic", "--docs", str(args.docs), "--config", args.config]
+               "--no-traffic", "--no-e2e", "--docs", str(args.docs), "--config", args.config] + ([] if args.arrival is None else ["--arrival", str(args.arrival)])
         pr = subprocess.Popen(cmd, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), stdout=subprocess.DEVNULL,
                               stderr=subprocess.DEVNULL, start_new_session=True)
         try:

@@ -321,10 +321,11 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, const hm_do
         }
         if (grew) sh.grew = 1;
         bsync();
-        for (uint32_t i = tid; i < n; i += LWG)
+        const bool any = sh.grew != 0;          // read by every thread before the barrier below,
+        for (uint32_t i = tid; i < n; i += LWG) // so thread 0's reset of the next round cannot race it
             for (uint32_t a = 0; a < A; a++) cur[(size_t)i * S + a] = nxt[(size_t)i * A + a];
         bsync();
-        if (!sh.grew) break;
+        if (!any) break;
     }
     if (tid == 0) sh.all_ok = 1;
     bsync();
