@@ -53,6 +53,8 @@ def assert_same(b, g, o, allow_unsupported=False):
     ("C4", 2000, {"actors": 3, "changes_per_actor": 20}),
     ("C5", 4000, {}),                                      # nested maps + lists, blocked + duplicate changes
     ("C5", 2000, {"arrival": 1, "dup_pct": 0}),
+    ("C4", 4000, {"arrival": 2, "shuffle_pct": 30, "dup_pct": 6}),   # duplicate copies applied before their originals
+    ("C5", 4000, {"dup_pct": 12}),
 ])
 def test_synthetic_parity(engine, name, n, extra):
     b = synth.generate(synth.config(name, n_docs=n, **extra))

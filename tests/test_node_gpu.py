@@ -97,3 +97,15 @@ def test_patch_diffs_rebuild_the_merged_document(name, n):
         assert s["status"] == "OK"
         assert g["state"] == json.loads(json.dumps(s["state"])), i
         assert g["nDiffs"] > 0 and g["nonEmpty"] > 0
+
+
+def test_materialize_history_prefix():
+    """MaterializeMsg (src/RepoBackend.ts:570-579): history.slice(0, n) replayed through
+    Backend.applyChanges(Backend.init(), ...) — the reference's tests/repo.test.ts:129-164
+    expects foo == 'bar1' for the first 2 entries of foo = bar0, bar1, bar2, bar3."""
+    p = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "run_materialize.js")], capture_output=True, text=True,
+                       timeout=120)
+    assert p.returncode == 0, p.stderr
+    got = json.loads(p.stdout)
+    assert got["materialized"] == {"1": "bar0", "2": "bar1", "3": "bar2", "4": "bar3"}
+    assert got["history"] == 4 and got["types"] == ["ReadyMsg", "LocalPatchMsg", "LocalPatchMsg", "LocalPatchMsg"]
