@@ -92,9 +92,11 @@ def test_known_answers_general_kernel(engine_general, name, changes, expect):
 
 
 def test_full_size_c4_properties(engine):
-    """BASELINE size (1M docs): size-independent properties, no oracle run."""
+    """BASELINE size (1M docs): bit-exact against the oracle on every document (16 threads),
+    plus size-independent properties."""
     b = synth.generate(synth.config("C4", n_docs=1_000_000))
     g = engine.merge(b)
+    assert_same(b, g, O.merge(b, threads=16))
     assert (g.docs["status"] == 0).all()
     assert int(g.docs["hist_len"].sum()) == len(b.changes)          # every change applied once
     S = b.a_stride
@@ -138,3 +140,25 @@ def test_envelope_precedence_on_gpu(engine, engine_general, general, name, chang
     got = doc_summary(b, g, 0)
     for k, v in expect.items():
         assert got.get(k) == v, (name, k, got)
+
+
+@pytest.mark.parametrize("general", [False, True], ids=["small", "general"])
+def test_literal_transitive_deps_fold_on_gpu(engine, engine_general, general):
+    """A listed dep dominated by another listed dep LOWERS allDeps in Automerge's literal
+    transitiveDeps fold (tests/test_oracle_kat.py); the GPU must reproduce it: the small
+    kernel hands the document over, the general kernel's closure check falls back to the
+    serial literal fold."""
+    A, B, C = "aaaa", "bbbb", "cccc"
+    from hypermerge_amd.columnar import ROOT_ID as R
+    changes = [
+        {"actor": A, "seq": 1, "deps": {}, "ops": []},
+        {"actor": A, "seq": 2, "deps": {}, "ops": [{"action": "set", "obj": R, "key": "k", "value": "a2"}]},
+        {"actor": B, "seq": 1, "deps": {A: 2}, "ops": []},
+        {"actor": C, "seq": 1, "deps": {B: 1, A: 1}, "ops": [{"action": "set", "obj": R, "key": "k", "value": "c1"}]},
+    ]
+    b = encode([changes, changes[:3]])
+    g = (engine_general if general else engine).merge(b)
+    o = O.merge(b)
+    assert_same(b, g, o)
+    assert list(g.all_deps[3 * b.a_stride: 3 * b.a_stride + 3]) == [1, 1, 0]
+    assert canonical_json(b, g, 0) == canonical_json(b, o, 0)
