@@ -22,11 +22,48 @@
 
 #define LWG 256
 #define LA_MAX 32
+// LDS arena per workgroup (u32 words): 36 KB keeps 4 workgroups per CU (the VGPR-bound
+// occupancy at 128 VGPRs).  Documents whose L2 closure rows (2·n·A + T words) or L4 Euler
+// tour (E words, 16-bit links) fit run those phases out of LDS instead of the pool.
+#define LARENA 9216
+// Explicit address spaces: LDS pointers -> ds_*, pool pointers -> global_* (a generic pointer
+// would compile to flat_* ops, which count against lgkmcnt too, so every LDS wait would also
+// wait for the outstanding pool loads, stores and atomics).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define LDS __attribute__((address_space(3)))
+#define GLB __attribute__((address_space(1)))
+#else
+#define LDS
+#define GLB
+#endif
 typedef unsigned long long u64;
+
+#ifndef HM_STAMPS
+#define HM_STAMPS 0     // diagnostic builds only: per-phase s_memtime shares (tools/lstamps.py); never timed
+#endif
+#define HML_NSTAMP 16
+// registers with at most this many assigns test survivors against the assign list directly;
+// longer lists build per-actor maxima with atomics (SEG_SHORT assign lists cost one LDS row
+// read each, where every assign's A atomicMax on shared L2 lines cost ~27 % of C3's kernel)
+#define SEG_SHORT 8
 
 namespace hml {
 
 __device__ __forceinline__ void bsync() { __syncthreads(); }
+#if HM_STAMPS
+__device__ unsigned long long hml_stamp_acc[HML_NSTAMP];
+__shared__ unsigned long long hml_st[HML_NSTAMP + 1];
+__device__ __forceinline__ u64 lstamp_now() {
+    u64 t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define LSTAMP(i) do { bsync(); const u64 t_ = lstamp_now(); if (threadIdx.x == 0) { hml_st[i] += t_ - hml_st[HML_NSTAMP]; hml_st[HML_NSTAMP] = t_; } } while (0)
+#else
+#define LSTAMP(i) do { } while (0)
+#endif
 // order one lane's global writes before the wave's next reads (wave-uniform sections)
 __device__ __forceinline__ void wfence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
 
@@ -38,13 +75,18 @@ __device__ __forceinline__ u64 err_key(uint32_t h, uint32_t op_plus1, uint32_t a
 struct Shared {
     uint32_t base[LA_MAX], maxs[LA_MAX], tabo[LA_MAX + 1], clock[LA_MAX], bclock[LA_MAX], headv[LA_MAX];
     uint32_t maxad[LA_MAX];
-    uint32_t flags, all_ok, H, nins, nl, total, lists, grew;
+    uint32_t flags, all_ok, H, nins, nl, total, lists, grew, nmake;
     u64 errkey;
     uint32_t scan[LWG / 64 + 1];
     u64 scratch_base;
 };
 
 enum : uint32_t { LF_UNSUPPORTED = 1u, LF_NOPOOL = 2u };
+
+// device-scope relaxed atomics on pool (global) pointers
+template <typename T> __device__ __forceinline__ T g_add(GLB T *p, T v) { return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <typename T> __device__ __forceinline__ T g_min(GLB T *p, T v) { return __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <typename T> __device__ __forceinline__ T g_max(GLB T *p, T v) { return __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
 // exclusive scan of v over the block; returns the prefix, *total = block sum
 __device__ __forceinline__ uint32_t block_excl_scan(Shared &sh, uint32_t v, uint32_t *total) {
@@ -78,26 +120,26 @@ __device__ void scan_array(Shared &sh, uint32_t *arr, uint32_t N, uint32_t *tota
 }
 
 struct Scratch {
-    uint32_t *tab, *h2a, *opchg, *segmax, *segcnt, *survcnt, *regoff, *regobj, *segoff, *segfill;
-    uint32_t *survtmp, *survop, *survp, *objtype, *listid, *nodeop, *nodepi, *regnode, *pcount, *poff;
-    uint32_t *pfill, *plist, *fc, *ns, *tour0, *tour1, *tval0, *tval1, *listbase, *pos, *vis;
-    int32_t *hist;
-    u64 *opkey, *insmin, *objslot, *seglist, *nodekey, *survabs;
-    int64_t *survsum;
-    uint32_t *vc;                   // [n * A] closure rows (L2 pointer jumping, second buffer)
+    GLB uint32_t *tab, *h2a, *opchg, *segmax, *segcnt, *survcnt, *regoff, *regobj, *segoff, *segfill;
+    GLB uint32_t *survtmp, *segk, *survop, *survp, *objtype, *listid, *nodeop, *nodepi, *regnode, *pcount, *poff;
+    GLB uint32_t *pfill, *plist, *fc, *ns, *tour0, *tour1, *tval0, *tval1, *listbase, *pos, *vis;
+    GLB int32_t *hist;
+    GLB u64 *opkey, *insmin, *objslot, *seglist, *nodekey, *survabs;
+    GLB int64_t *survsum;
+    GLB uint32_t *vc;                   // [n * A] closure rows (L2 pointer jumping, second buffer)
 };
 
 __host__ __device__ inline size_t large_carve(uintptr_t base, uint32_t n, uint32_t m, uint32_t R, uint32_t O,
                                               uint32_t A, uint32_t T, Scratch *S) {
     size_t o = 0;
     const uint32_t NP = R + O, NE = 2 * (m + O);
-#define TK(f, T_, cnt) do { S->f = (T_ *)(base + o); o = (o + (size_t)(cnt) * sizeof(T_) + 15) & ~(size_t)15; } while (0)
+#define TK(f, T_, cnt) do { S->f = (GLB T_ *)(base + o); o = (o + (size_t)(cnt) * sizeof(T_) + 15) & ~(size_t)15; } while (0)
     TK(opkey, u64, m); TK(insmin, u64, R); TK(objslot, u64, O); TK(seglist, u64, m); TK(nodekey, u64, m);
     TK(survabs, u64, m); TK(survsum, int64_t, m); TK(vc, uint32_t, (size_t)n * A);
     TK(tab, uint32_t, T); TK(h2a, uint32_t, n); TK(hist, int32_t, n); TK(opchg, uint32_t, m);
     TK(segmax, uint32_t, (size_t)R * A); TK(segcnt, uint32_t, R); TK(survcnt, uint32_t, R);
     TK(regoff, uint32_t, R); TK(regobj, uint32_t, R); TK(segoff, uint32_t, R); TK(segfill, uint32_t, R);
-    TK(survtmp, uint32_t, m); TK(survop, uint32_t, m); TK(survp, uint32_t, m); TK(objtype, uint32_t, O);
+    TK(survtmp, uint32_t, m); TK(segk, uint32_t, m); TK(survop, uint32_t, m); TK(survp, uint32_t, m); TK(objtype, uint32_t, O);
     TK(listid, uint32_t, O); TK(nodeop, uint32_t, m); TK(nodepi, uint32_t, m); TK(regnode, uint32_t, R);
     TK(pcount, uint32_t, NP); TK(poff, uint32_t, NP); TK(pfill, uint32_t, NP); TK(plist, uint32_t, m);
     TK(fc, uint32_t, NP); TK(ns, uint32_t, m); TK(tour0, uint32_t, NE); TK(tour1, uint32_t, NE);
@@ -114,7 +156,7 @@ __device__ __forceinline__ uint32_t *ad_row(const SmallParams &p, const hm_doc_r
     return p.res_all_deps + ((size_t)doc.change_off + ci) * p.a_stride;
 }
 
-__device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, const hm_doc_row &doc, uint32_t d,
+__device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_t *ar, const hm_doc_row &doc, uint32_t d,
                                    uint8_t *pool, u64 pool_bytes, u64 *pool_used, int32_t &H_out) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t n = doc.n_changes, A = doc.n_actors, m = doc.n_ops, R = doc.n_regs, O = doc.n_objs;
@@ -166,12 +208,13 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, const hm_do
         if (a >= A || s < sh.base[a] || s > sh.maxs[a] || sh.maxs[a] == 0) return 0xFFFFFFFFu;
         return sh.tabo[a] + (s - sh.base[a]);
     };
-    for (uint32_t i = tid; i < n; i += LWG) { const hm_change_row c = CH[i]; atomicMin(&X.tab[slot_of(c.actor, c.seq)], i); }
+    for (uint32_t i = tid; i < n; i += LWG) { const hm_change_row c = CH[i]; g_min(&X.tab[slot_of(c.actor, c.seq)], i); }
     for (uint32_t i = tid; i < n; i += LWG) {
         const hm_change_row c = CH[i];
         for (uint32_t j = 0; j < c.n_ops; j++) X.opchg[c.op_first - doc.op_off + j] = i;
     }
     bsync();
+    LSTAMP(0);
     // ---- L1 fast path: every dependency arrived earlier ----
     uint32_t ndup_local = 0;
     for (uint32_t i = tid; i < n; i += LWG) {
@@ -273,6 +316,7 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, const hm_do
     }
     bsync();
     const uint32_t H = sh.H;
+    LSTAMP(1);
     H_out = (int32_t)H;
 
     // ---- L2: allDeps ----
@@ -285,76 +329,159 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, const hm_do
     //     Otherwise (a listed dep dominated by another: never for heads-based deps) the literal
     //     fold runs serially in history order below.
     uint32_t *cur = p.res_all_deps + (size_t)doc.change_off * S, *nxt = X.vc;   // row stride S / A
-    for (uint32_t i = tid; i < n; i += LWG) {
-        uint32_t *row = cur + (size_t)i * S;
-        for (uint32_t a = 0; a < S; a++) row[a] = 0;
-        if (X.hist[i] < 0) continue;
-        const hm_change_row c = CH[i];
-        for (uint32_t j = 0; j < c.n_deps; j++) {
-            const hm_dep_row dp = p.deps[c.dep_off + j];
-            const uint32_t sq = dp.actor == c.actor ? c.seq - 1 : dp.seq;
-            if (row[dp.actor] < sq) row[dp.actor] = sq;
-        }
-        if (row[c.actor] < c.seq - 1) row[c.actor] = c.seq - 1;
-    }
-    bsync();
-    for (;;) {                                  // monotone and bounded: terminates (rounds ~ log depth)
-        if (tid == 0) sh.grew = 0;
-        bsync();
-        bool grew = false;
+    if (2 * n * A + T <= LARENA) {
+        // the same rounds and check with the first-arrival table and both row buffers in LDS
+        LDS uint32_t *lt = ar, *lc = ar + T, *ln = ar + T + n * A;        // row stride A
+        for (uint32_t i = tid; i < T; i += LWG) lt[i] = X.tab[i];
         for (uint32_t i = tid; i < n; i += LWG) {
-            const uint32_t *row = cur + (size_t)i * S;
-            uint32_t *out = nxt + (size_t)i * A;
-            for (uint32_t a = 0; a < A; a++) out[a] = row[a];
+            LDS uint32_t *row = lc + i * A;
+            for (uint32_t a = 0; a < A; a++) row[a] = 0;
             if (X.hist[i] < 0) continue;
-            for (uint32_t a = 0; a < A; a++) {
-                const uint32_t sq = row[a];
-                if (!sq) continue;
-                const uint32_t sl = slot_of(a, sq), ti = sl == 0xFFFFFFFFu ? 0xFFFFFFFFu : X.tab[sl];
-                if (ti >= n) continue;                           // not applied: cannot occur for deps of applied changes
-                const uint32_t *r2 = cur + (size_t)ti * S;       // the applied change (a, sq)
-                for (uint32_t b = 0; b < A; b++) {
-                    const uint32_t v = b == a ? sq : r2[b];
-                    if (out[b] < v) { out[b] = v; grew = true; }
+            const hm_change_row c = CH[i];
+            for (uint32_t j = 0; j < c.n_deps; j++) {
+                const hm_dep_row dp = p.deps[c.dep_off + j];
+                const uint32_t sq = dp.actor == c.actor ? c.seq - 1 : dp.seq;
+                if (row[dp.actor] < sq) row[dp.actor] = sq;
+            }
+            if (row[c.actor] < c.seq - 1) row[c.actor] = c.seq - 1;
+        }
+        bsync();
+        auto lslot = [&](uint32_t a, uint32_t sq) -> uint32_t {      // applied change (a, sq) or >= n
+            if (sq < sh.base[a] || sq > sh.maxs[a] || sh.maxs[a] == 0) return 0xFFFFFFFFu;
+            return lt[sh.tabo[a] + (sq - sh.base[a])];
+        };
+        for (;;) {
+            if (tid == 0) sh.grew = 0;
+            bsync();
+            bool grew = false;
+            for (uint32_t i = tid; i < n; i += LWG) {
+                const LDS uint32_t *row = lc + i * A;
+                LDS uint32_t *out = ln + i * A;
+                for (uint32_t a = 0; a < A; a++) out[a] = row[a];
+                if (X.hist[i] < 0) continue;
+                for (uint32_t a = 0; a < A; a++) {
+                    const uint32_t sq = row[a];
+                    if (!sq) continue;
+                    const uint32_t ti = lslot(a, sq);
+                    if (ti >= n) continue;
+                    const LDS uint32_t *r2 = lc + ti * A;
+                    for (uint32_t b = 0; b < A; b++) {
+                        const uint32_t v = b == a ? sq : r2[b];
+                        if (out[b] < v) { out[b] = v; grew = true; }
+                    }
                 }
             }
+            if (grew) sh.grew = 1;
+            bsync();
+            const bool any = sh.grew != 0;
+            LDS uint32_t *t = lc; lc = ln; ln = t;          // every row of the new buffer was written
+            bsync();
+            if (!any) break;
         }
-        if (grew) sh.grew = 1;
+        LSTAMP(2);
+        if (tid == 0) sh.all_ok = 1;
         bsync();
-        const bool any = sh.grew != 0;          // read by every thread before the barrier below,
-        for (uint32_t i = tid; i < n; i += LWG) // so thread 0's reset of the next round cannot race it
-            for (uint32_t a = 0; a < A; a++) cur[(size_t)i * S + a] = nxt[(size_t)i * A + a];
-        bsync();
-        if (!any) break;
-    }
-    if (tid == 0) sh.all_ok = 1;
-    bsync();
-    for (uint32_t i = tid; i < n; i += LWG) {
-        if (X.hist[i] < 0) continue;
-        const hm_change_row c = CH[i];
-        const uint32_t *row = cur + (size_t)i * S;
-        uint32_t *acc = nxt + (size_t)i * A;
-        for (uint32_t a = 0; a < A; a++) acc[a] = 0;
-        auto fold = [&](uint32_t a, uint32_t sq) {
-            if (sq == 0) return;
-            const uint32_t sl = slot_of(a, sq), ti = sl == 0xFFFFFFFFu ? 0xFFFFFFFFu : X.tab[sl];
-            if (ti >= n) { acc[a] = 0xFFFFFFFFu; return; }       // (cannot occur) forces the serial path
-            const uint32_t *r2 = cur + (size_t)ti * S;
-            for (uint32_t b = 0; b < A; b++) if (acc[b] < r2[b]) acc[b] = r2[b];
-            acc[a] = sq;
-        };
-        bool own = false;
-        for (uint32_t j = 0; j < c.n_deps; j++) {
-            const hm_dep_row dp = p.deps[c.dep_off + j];
-            if (dp.actor == c.actor) { own = true; fold(c.actor, c.seq - 1); }
-            else fold(dp.actor, dp.seq);
+        for (uint32_t i = tid; i < n; i += LWG) {
+            uint32_t *grow_ = cur + (size_t)i * S;
+            const LDS uint32_t *row = lc + i * A;
+            for (uint32_t a = 0; a < S; a++) grow_[a] = a < A ? row[a] : 0u;
+            if (X.hist[i] < 0) continue;
+            const hm_change_row c = CH[i];
+            LDS uint32_t *acc = ln + i * A;
+            for (uint32_t a = 0; a < A; a++) acc[a] = 0;
+            auto fold = [&](uint32_t a, uint32_t sq) {
+                if (sq == 0) return;
+                const uint32_t ti = lslot(a, sq);
+                if (ti >= n) { acc[a] = 0xFFFFFFFFu; return; }
+                const LDS uint32_t *r2 = lc + ti * A;
+                for (uint32_t b = 0; b < A; b++) if (acc[b] < r2[b]) acc[b] = r2[b];
+                acc[a] = sq;
+            };
+            bool own = false;
+            for (uint32_t j = 0; j < c.n_deps; j++) {
+                const hm_dep_row dp = p.deps[c.dep_off + j];
+                if (dp.actor == c.actor) { own = true; fold(c.actor, c.seq - 1); }
+                else fold(dp.actor, dp.seq);
+            }
+            if (!own) fold(c.actor, c.seq - 1);
+            bool same = true;
+            for (uint32_t a = 0; a < A; a++) same = same && acc[a] == row[a];
+            if (!same) sh.all_ok = 0;
         }
-        if (!own) fold(c.actor, c.seq - 1);
-        bool same = true;
-        for (uint32_t a = 0; a < A; a++) same = same && acc[a] == row[a];
-        if (!same) sh.all_ok = 0;
+        bsync();
+    } else {
+        for (uint32_t i = tid; i < n; i += LWG) {
+            uint32_t *row = cur + (size_t)i * S;
+            for (uint32_t a = 0; a < S; a++) row[a] = 0;
+            if (X.hist[i] < 0) continue;
+            const hm_change_row c = CH[i];
+            for (uint32_t j = 0; j < c.n_deps; j++) {
+                const hm_dep_row dp = p.deps[c.dep_off + j];
+                const uint32_t sq = dp.actor == c.actor ? c.seq - 1 : dp.seq;
+                if (row[dp.actor] < sq) row[dp.actor] = sq;
+            }
+            if (row[c.actor] < c.seq - 1) row[c.actor] = c.seq - 1;
+        }
+        bsync();
+        for (;;) {                                  // monotone and bounded: terminates (rounds ~ log depth)
+            if (tid == 0) sh.grew = 0;
+            bsync();
+            bool grew = false;
+            for (uint32_t i = tid; i < n; i += LWG) {
+                const uint32_t *row = cur + (size_t)i * S;
+                uint32_t *out = nxt + (size_t)i * A;
+                for (uint32_t a = 0; a < A; a++) out[a] = row[a];
+                if (X.hist[i] < 0) continue;
+                for (uint32_t a = 0; a < A; a++) {
+                    const uint32_t sq = row[a];
+                    if (!sq) continue;
+                    const uint32_t sl = slot_of(a, sq), ti = sl == 0xFFFFFFFFu ? 0xFFFFFFFFu : X.tab[sl];
+                    if (ti >= n) continue;                           // not applied: cannot occur for deps of applied changes
+                    const uint32_t *r2 = cur + (size_t)ti * S;       // the applied change (a, sq)
+                    for (uint32_t b = 0; b < A; b++) {
+                        const uint32_t v = b == a ? sq : r2[b];
+                        if (out[b] < v) { out[b] = v; grew = true; }
+                    }
+                }
+            }
+            if (grew) sh.grew = 1;
+            bsync();
+            const bool any = sh.grew != 0;          // read by every thread before the barrier below,
+            for (uint32_t i = tid; i < n; i += LWG) // so thread 0's reset of the next round cannot race it
+                for (uint32_t a = 0; a < A; a++) cur[(size_t)i * S + a] = nxt[(size_t)i * A + a];
+            bsync();
+            if (!any) break;
+        }
+        LSTAMP(2);
+        if (tid == 0) sh.all_ok = 1;
+        bsync();
+        for (uint32_t i = tid; i < n; i += LWG) {
+            if (X.hist[i] < 0) continue;
+            const hm_change_row c = CH[i];
+            const uint32_t *row = cur + (size_t)i * S;
+            uint32_t *acc = nxt + (size_t)i * A;
+            for (uint32_t a = 0; a < A; a++) acc[a] = 0;
+            auto fold = [&](uint32_t a, uint32_t sq) {
+                if (sq == 0) return;
+                const uint32_t sl = slot_of(a, sq), ti = sl == 0xFFFFFFFFu ? 0xFFFFFFFFu : X.tab[sl];
+                if (ti >= n) { acc[a] = 0xFFFFFFFFu; return; }       // (cannot occur) forces the serial path
+                const uint32_t *r2 = cur + (size_t)ti * S;
+                for (uint32_t b = 0; b < A; b++) if (acc[b] < r2[b]) acc[b] = r2[b];
+                acc[a] = sq;
+            };
+            bool own = false;
+            for (uint32_t j = 0; j < c.n_deps; j++) {
+                const hm_dep_row dp = p.deps[c.dep_off + j];
+                if (dp.actor == c.actor) { own = true; fold(c.actor, c.seq - 1); }
+                else fold(dp.actor, dp.seq);
+            }
+            if (!own) fold(c.actor, c.seq - 1);
+            bool same = true;
+            for (uint32_t a = 0; a < A; a++) same = same && acc[a] == row[a];
+            if (!same) sh.all_ok = 0;
+        }
+        bsync();
     }
-    bsync();
     const bool closure_ok = sh.all_ok != 0;
     if (closure_ok) {
         for (uint32_t h = tid; h < H; h += LWG) {
@@ -391,6 +518,7 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, const hm_do
             if (X.hist[i] < 0) for (uint32_t a = 0; a < S; a++) ad_row(p, doc, i)[a] = 0;
     }
     bsync();
+    LSTAMP(3);
     // clock / heads: a head survives unless some applied change's allDeps reaches it
     for (uint32_t h = tid; h < H; h += LWG) {
         const hm_change_row c = CH[X.h2a[h]];
@@ -400,57 +528,101 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, const hm_do
     if (tid < A && sh.clock[tid] && sh.maxad[tid] < sh.clock[tid]) sh.headv[tid] = sh.clock[tid];
 
     // ---- L3: ops ----
+    // Per-change inputs of the op loops (history position, actor, seq, first op, allDeps row)
+    // and the op -> change map are staged in the LDS arena when they fit (L2 is done with it).
+    const bool l3 = n * (A + 4) + m <= LARENA;
+    LDS uint32_t *l_hist = ar, *l_act = ar + n, *l_seq = ar + 2 * n, *l_op0 = ar + 3 * n, *l_ad = ar + 4 * n,
+                 *l_opchg = ar + 4 * n + n * A;
     for (uint32_t i = tid; i < O; i += LWG) { X.objslot[i] = i == 0 ? 0ull : ~0ull; X.objtype[i] = i == 0 ? HM_MAKE_MAP : 0xFFu; }
     for (uint32_t i = tid; i < R; i += LWG) {
         X.segcnt[i] = 0; X.survcnt[i] = 0; X.insmin[i] = ~0ull; X.regobj[i] = HM_NONE; X.segfill[i] = 0;
         for (uint32_t a = 0; a < A; a++) X.segmax[(size_t)i * A + a] = 0;
     }
+    if (tid == 0) sh.nmake = 0;
+    if (l3) {
+        for (uint32_t i = tid; i < n; i += LWG) {
+            const hm_change_row c = CH[i];
+            const uint32_t o0 = c.op_first - doc.op_off;
+            l_hist[i] = (uint32_t)X.hist[i]; l_act[i] = c.actor; l_seq[i] = c.seq; l_op0[i] = o0;
+            const uint32_t *ad = ad_row(p, doc, i);
+            for (uint32_t a = 0; a < A; a++) l_ad[i * A + a] = ad[a];
+            for (uint32_t j = 0; j < c.n_ops; j++) l_opchg[o0 + j] = i;
+        }
+    }
     bsync();
+    LSTAMP(11);
+    auto opchg_of = [&](uint32_t k) -> uint32_t { return l3 ? l_opchg[k] : X.opchg[k]; };
+    auto hist_of = [&](uint32_t ci) -> int32_t { return l3 ? (int32_t)l_hist[ci] : X.hist[ci]; };
+    auto op0_of = [&](uint32_t ci) -> uint32_t { return l3 ? l_op0[ci] : CH[ci].op_first - doc.op_off; };
+    auto act_of = [&](uint32_t ci) -> uint32_t { return l3 ? l_act[ci] : CH[ci].actor; };
+    auto seq_of = [&](uint32_t ci) -> uint32_t { return l3 ? l_seq[ci] : CH[ci].seq; };
+    auto ad_of = [&](uint32_t ci, uint32_t a) -> uint32_t { return l3 ? l_ad[ci * A + a] : ad_row(p, doc, ci)[a]; };
     for (uint32_t k = tid; k < m; k += LWG) {
         const hm_op_row o = OP[k];
-        const uint32_t ci = X.opchg[k];
-        const int32_t h = X.hist[ci];
-        X.opkey[k] = h >= 0 ? (((u64)h << 32) | (k - (CH[ci].op_first - doc.op_off))) : ~0ull;
+        const uint32_t ci = opchg_of(k);
+        const int32_t h = hist_of(ci);
+        const u64 key = h >= 0 ? (((u64)h << 32) | (k - op0_of(ci))) : ~0ull;
+        X.opkey[k] = key;
         // malformed rows (any op, applied or not) put the whole document outside the envelope
         const bool bad = o.action <= HM_MAKE_TEXT ? o.obj >= O
                        : (o.action <= HM_INC ? (o.reg >= R || (o.action == HM_INS && o.parent != HM_HEAD && o.parent >= R)) : true);
         if (bad) { atomicOr(&sh.flags, LF_UNSUPPORTED); continue; }
         if (h < 0) continue;
-        const u64 key = X.opkey[k];
         if (o.action <= HM_MAKE_TEXT) {
-            atomicMin(&X.objslot[o.obj], key + 1);
+            g_min(&X.objslot[o.obj], key + 1);
+            X.survtmp[atomicAdd(&sh.nmake, 1u)] = k;              // make-op list (survtmp is free until L3 offsets)
         } else {
             if (o.obj >= O) continue;
             X.regobj[o.reg] = o.obj;
-            if (o.action == HM_INS) { atomicMin(&X.insmin[o.reg], key + 1); if (o.elem >= (1u << 24)) atomicOr(&sh.flags, LF_UNSUPPORTED); }
-            else {
-                atomicAdd(&X.segcnt[o.reg], 1u);
-                if (o.action != HM_INC) {
-                    const uint32_t *ad = ad_row(p, doc, ci);
-                    for (uint32_t a = 0; a < A; a++) atomicMax(&X.segmax[(size_t)o.reg * A + a], ad[a]);
-                }
-            }
+            if (o.action == HM_INS) { g_min(&X.insmin[o.reg], key + 1); if (o.elem >= (1u << 24)) atomicOr(&sh.flags, LF_UNSUPPORTED); }
+            else g_add(&X.segcnt[o.reg], 1u);
         }
     }
     bsync();
     if (sh.flags) return LUNSUP;
-    for (uint32_t k = tid; k < m; k += LWG) {
+    LSTAMP(12);
+    for (uint32_t q = tid; q < sh.nmake; q += LWG) {
+        const uint32_t k = X.survtmp[q];
         const hm_op_row o = OP[k];
         const u64 key = X.opkey[k];
-        if (key == ~0ull || o.action > HM_MAKE_TEXT || o.obj >= O) continue;
-        const uint32_t ci = X.opchg[k];
+        const uint32_t ci = opchg_of(k);
         if (X.objslot[o.obj] != key + 1)
             atomicMin(&sh.errkey, err_key((uint32_t)(key >> 32), (uint32_t)key + 1, ci, HM_ERR_DUPLICATE_OBJECT));
         else X.objtype[o.obj] = o.action;
     }
     bsync();
+    // per-register assign lists (set/del/link/inc; segk = op index | inc << 31), used by the
+    // survivor test and by the tie positions; per-actor maxima only for long lists
+    for (uint32_t i = tid; i < R; i += LWG) X.segoff[i] = X.segcnt[i];
+    bsync();
+    uint32_t tot2;
+    scan_array(sh, X.segoff, R, &tot2);
+    for (uint32_t k = tid; k < m; k += LWG) {
+        const hm_op_row o = OP[k];
+        if (o.action < HM_SET || o.action > HM_INC || o.reg >= R || o.obj >= O) continue;   // exactly the ops segcnt counted
+        const uint32_t ci = opchg_of(k);
+        const int32_t h = hist_of(ci);
+        if (h < 0) continue;
+        const uint32_t q = X.segoff[o.reg] + g_add(&X.segfill[o.reg], 1u);
+        X.seglist[q] = ((u64)h << 32) | (k - op0_of(ci));
+        X.segk[q] = k | (o.action == HM_INC ? 0x80000000u : 0u);
+        if (o.action != HM_INC && X.segcnt[o.reg] > SEG_SHORT)
+            for (uint32_t a = 0; a < A; a++) {
+                const uint32_t v = ad_of(ci, a);
+                if (v) g_max(&X.segmax[(size_t)o.reg * A + a], v);   // 0 is the initial value
+            }
+    }
+    bsync();
+    LSTAMP(13);
     bool any_list = false;
     for (uint32_t k = tid; k < m; k += LWG) {
         const hm_op_row o = OP[k];
-        const u64 key = X.opkey[k];
         X.survp[k] = 0xFFFFFFFFu;                             // survivor slot (or none)
-        if (key == ~0ull || o.action < HM_INS || o.action > HM_INC || o.reg >= R) continue;
-        const uint32_t ci = X.opchg[k];
+        if (o.action < HM_INS || o.action > HM_INC || o.reg >= R) continue;
+        const uint32_t ci = opchg_of(k);
+        const int32_t h = hist_of(ci);
+        if (h < 0) continue;
+        const u64 key = ((u64)h << 32) | (k - op0_of(ci));
         const u64 os = o.obj < O ? X.objslot[o.obj] : ~0ull;
         if (os == ~0ull || os > key) {
             atomicMin(&sh.errkey, err_key((uint32_t)(key >> 32), (uint32_t)key + 1, ci, HM_ERR_UNKNOWN_OBJECT));
@@ -471,8 +643,18 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, const hm_do
         if (o.action == HM_SET || o.action == HM_LINK) {
             if (is_list && !(X.insmin[o.reg] <= key))
                 atomicMin(&sh.errkey, err_key((uint32_t)(key >> 32), (uint32_t)key + 1, ci, HM_ERR_MISSING_ELEM));
-            const hm_change_row c = CH[ci];
-            if (X.segmax[(size_t)o.reg * A + c.actor] < c.seq) X.survp[k] = atomicAdd(&X.survcnt[o.reg], 1u);
+            // survivor: no set/del/link on the register has this op's change among its allDeps
+            const uint32_t ao = act_of(ci), so = seq_of(ci), cnt = X.segcnt[o.reg];
+            bool surv = true;
+            if (cnt > SEG_SHORT) surv = X.segmax[(size_t)o.reg * A + ao] < so;
+            else {
+                const uint32_t b0 = X.segoff[o.reg];
+                for (uint32_t q = 0; q < cnt; q++) {
+                    const uint32_t e = X.segk[b0 + q];
+                    if (!(e >> 31) && ad_of(opchg_of(e & 0x7FFFFFFFu), ao) >= so) surv = false;
+                }
+            }
+            if (surv) X.survp[k] = g_add(&X.survcnt[o.reg], 1u);
         }
     }
     if (any_list) sh.lists = 1;
@@ -480,6 +662,7 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, const hm_do
     const bool lists_flag = sh.lists != 0;
     if (sh.errkey != ~0ull) return LERR;
     if (sh.flags) return LUNSUP;
+    LSTAMP(4);
     // survivor offsets
     for (uint32_t i = tid; i < R; i += LWG) X.regoff[i] = X.survcnt[i];
     bsync();
@@ -488,22 +671,12 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, const hm_do
     if (tid == 0) sh.total = total;
     for (uint32_t k = tid; k < m; k += LWG)
         if (X.survp[k] != 0xFFFFFFFFu) X.survtmp[X.regoff[OP[k].reg] + X.survp[k]] = k;
-    // per-register assign lists (for tie positions)
-    for (uint32_t i = tid; i < R; i += LWG) X.segoff[i] = X.segcnt[i];
-    bsync();
-    uint32_t tot2;
-    scan_array(sh, X.segoff, R, &tot2);
-    for (uint32_t k = tid; k < m; k += LWG) {
-        const hm_op_row o = OP[k];
-        if (X.opkey[k] == ~0ull || o.action < HM_SET || o.action > HM_INC || o.reg >= R) continue;
-        X.seglist[X.segoff[o.reg] + atomicAdd(&X.segfill[o.reg], 1u)] = X.opkey[k];
-    }
     bsync();
     // ranks: actor descending; ties (one change) by the sortBy(actor).reverse() flip
     for (uint32_t k = tid; k < m; k += LWG) {
         if (X.survp[k] == 0xFFFFFFFFu) continue;
         const hm_op_row o = OP[k];
-        const uint32_t my_a = CH[X.opchg[k]].actor;
+        const uint32_t my_a = act_of(opchg_of(k));
         const uint32_t b0 = X.regoff[o.reg], cnt = X.survcnt[o.reg];
         const bool odd_n = X.segcnt[o.reg] & 1;
         auto tkey = [&](uint32_t kk) -> uint32_t {
@@ -517,7 +690,7 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, const hm_do
         for (uint32_t q = 0; q < cnt; q++) {
             const uint32_t k2 = X.survtmp[b0 + q];
             if (k2 == k) continue;
-            const uint32_t a2 = CH[X.opchg[k2]].actor;
+            const uint32_t a2 = act_of(opchg_of(k2));
             if (a2 > my_a) rank++;
             else if (a2 == my_a) {
                 if (!have_t) { my_t = tkey(k); have_t = true; }
@@ -530,27 +703,29 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, const hm_do
         X.survabs[b0 + rank] = 0;
     }
     bsync();
+    LSTAMP(5);
     // counters
     for (uint32_t k = tid; k < m; k += LWG) {
         const hm_op_row o = OP[k];
         if (X.opkey[k] == ~0ull || o.action != HM_INC || o.reg >= R) continue;
-        const uint32_t *adi = ad_row(p, doc, X.opchg[k]);
+        const uint32_t ci = opchg_of(k);
         const uint32_t b0 = X.regoff[o.reg], cnt = X.survcnt[o.reg];
         for (uint32_t q = 0; q < cnt; q++) {
             const uint32_t k2 = X.survop[b0 + q];
             const hm_op_row o2 = OP[k2];
             if (o2.action != HM_SET || o2.datatype != HM_DT_COUNTER || (o2.vtag != HM_V_INT && o2.vtag != HM_V_FLOAT)) continue;
-            const hm_change_row c2 = CH[X.opchg[k2]];
-            if (adi[c2.actor] < c2.seq) continue;                 // concurrent inc: no effect
+            const uint32_t c2 = opchg_of(k2);
+            if (ad_of(ci, act_of(c2)) < seq_of(c2)) continue;                 // concurrent inc: no effect
             if (o2.vtag != HM_V_INT || o.vtag != HM_V_INT) { atomicOr(&sh.flags, LF_UNSUPPORTED); continue; }
             const int64_t v = (int64_t)o.value;
-            atomicAdd((unsigned long long *)&X.survsum[b0 + q], (unsigned long long)v);
-            atomicAdd((unsigned long long *)&X.survabs[b0 + q], (unsigned long long)(v < 0 ? -v : v));
+            g_add((GLB u64 *)&X.survsum[b0 + q], (u64)v);
+            g_add(&X.survabs[b0 + q], (u64)(v < 0 ? -v : v));
         }
     }
     bsync();
     if (sh.flags) return LUNSUP;
 
+    LSTAMP(6);
     // ---- L4: RGA order ----
     if (lists_flag) {
         const uint32_t NP = R + O;
@@ -566,9 +741,9 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, const hm_do
             const uint32_t i = atomicAdd(&sh.nins, 1u);
             const uint32_t pi = o.parent == HM_HEAD ? R + o.obj : o.parent;
             X.nodeop[i] = k; X.nodepi[i] = pi;
-            X.nodekey[i] = ((u64)o.elem << 8) | CH[X.opchg[k]].actor;
+            X.nodekey[i] = ((u64)o.elem << 8) | act_of(opchg_of(k));
             X.regnode[o.reg] = i;
-            atomicAdd(&X.pcount[pi], 1u);
+            g_add(&X.pcount[pi], 1u);
         }
         bsync();
         const uint32_t N = sh.nins;
@@ -576,7 +751,7 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, const hm_do
         bsync();
         uint32_t tp;
         scan_array(sh, X.poff, NP, &tp);
-        for (uint32_t i = tid; i < N; i += LWG) { const uint32_t pi = X.nodepi[i]; X.plist[X.poff[pi] + atomicAdd(&X.pfill[pi], 1u)] = i; }
+        for (uint32_t i = tid; i < N; i += LWG) { const uint32_t pi = X.nodepi[i]; X.plist[X.poff[pi] + g_add(&X.pfill[pi], 1u)] = i; }
         bsync();
         for (uint32_t i = tid; i < N; i += LWG) {
             const uint32_t pi = X.nodepi[i];
@@ -592,35 +767,60 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, const hm_do
             if (firstc) X.fc[pi] = i;
         }
         bsync();
+        LSTAMP(7);
         const uint32_t E = 2 * (N + nl), END = 0xFFFFFFFFu;
-        // tour entries: (next, value) as two arrays packed into u64? keep next in tour0/tour1, values in pos/vis
+        // tour entries (next, value): two pool arrays, or one LDS word each (next << 16 | value,
+        // END = 0xFFFF) when the tour fits the arena and its indices fit 16 bits
+        const bool tour_lds = E <= LARENA && E < 0xFFFFu;
+        LDS uint32_t *tw = ar;
         uint32_t *nx0 = X.tour0, *nx1 = X.tour1;
         uint32_t *va0 = X.tval0, *va1 = X.tval1;
+        auto put = [&](uint32_t e, uint32_t nx, uint32_t va) {
+            if (tour_lds) tw[e] = ((nx == END ? 0xFFFFu : nx) << 16) | va;
+            else { nx0[e] = nx; va0[e] = va; }
+        };
         for (uint32_t i = tid; i < N; i += LWG) {
             const hm_op_row o = OP[X.nodeop[i]];
             const uint32_t hd = N + X.listid[o.obj];
             const uint32_t f = X.fc[o.reg];
             const uint32_t pi = X.nodepi[i];
-            nx0[2 * i] = f != 0xFFFFFFFFu ? 2 * f : 2 * i + 1;           va0[2 * i] = 1;
-            nx0[2 * i + 1] = X.ns[i] != 0xFFFFFFFFu ? 2 * X.ns[i] : (pi >= R ? 2 * hd + 1 : 2 * X.regnode[pi] + 1);
-            va0[2 * i + 1] = 0;
+            put(2 * i, f != 0xFFFFFFFFu ? 2 * f : 2 * i + 1, 1);
+            put(2 * i + 1, X.ns[i] != 0xFFFFFFFFu ? 2 * X.ns[i] : (pi >= R ? 2 * hd + 1 : 2 * X.regnode[pi] + 1), 0);
         }
         for (uint32_t o = tid; o < O; o += LWG) {
             if (!(X.objtype[o] == HM_MAKE_LIST || X.objtype[o] == HM_MAKE_TEXT)) continue;
             const uint32_t h = N + X.listid[o], f = X.fc[R + o];
-            nx0[2 * h] = f != 0xFFFFFFFFu ? 2 * f : 2 * h + 1; va0[2 * h] = 0;
-            nx0[2 * h + 1] = END; va0[2 * h + 1] = 0;
+            put(2 * h, f != 0xFFFFFFFFu ? 2 * f : 2 * h + 1, 0);
+            put(2 * h + 1, END, 0);
         }
         bsync();
         const uint32_t rounds = E ? 32 - __builtin_clz(E) : 0;
-        for (uint32_t rd = 0; rd < rounds; rd++) {
-            for (uint32_t e = tid; e < E; e += LWG) {
-                const uint32_t x = nx0[e];
-                if (x != END) { nx1[e] = nx0[x]; va1[e] = va0[e] + va0[x]; } else { nx1[e] = END; va1[e] = va0[e]; }
+        if (tour_lds) {
+            // in-place pointer jumping: a word is read and written whole, so every word keeps
+            // "value = sum of the values from this entry up to its link" at every moment, and a
+            // link at least 2^r entries ahead after round r (links only move forward)
+            for (uint32_t rd = 0; rd < rounds; rd++) {
+                for (uint32_t e = tid; e < E; e += LWG) {
+                    const uint32_t w = tw[e], x = w >> 16;
+                    if (x == 0xFFFFu) continue;
+                    const uint32_t w2 = tw[x];
+                    tw[e] = (w2 & 0xFFFF0000u) | ((w & 0xFFFFu) + (w2 & 0xFFFFu));
+                }
+                bsync();
             }
+            for (uint32_t e = tid; e < E; e += LWG) va0[e] = tw[e] & 0xFFFFu;
             bsync();
-            uint32_t *t = nx0; nx0 = nx1; nx1 = t; t = va0; va0 = va1; va1 = t;
+        } else {
+            for (uint32_t rd = 0; rd < rounds; rd++) {
+                for (uint32_t e = tid; e < E; e += LWG) {
+                    const uint32_t x = nx0[e];
+                    if (x != END) { nx1[e] = nx0[x]; va1[e] = va0[e] + va0[x]; } else { nx1[e] = END; va1[e] = va0[e]; }
+                }
+                bsync();
+                uint32_t *t = nx0; nx0 = nx1; nx1 = t; t = va0; va0 = va1; va1 = t;
+            }
         }
+        LSTAMP(8);
         for (uint32_t o = tid; o < O; o += LWG) {
             const bool isl = X.objtype[o] == HM_MAKE_LIST || X.objtype[o] == HM_MAKE_TEXT;
             if (isl) X.listbase[X.listid[o]] = va0[2 * (N + X.listid[o])];
@@ -654,6 +854,7 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, const hm_do
         bsync();
     }
 
+    LSTAMP(9);
     // ---- outputs ----
     for (uint32_t q = tid; q < total; q += LWG) {
         const uint32_t k = X.survop[q];
@@ -676,11 +877,14 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, const hm_do
     for (uint32_t i = tid; i < n; i += LWG) p.res_hist[doc.change_off + i] = X.hist[i];
     bsync();
     if (sh.flags) return LUNSUP;
+    LSTAMP(10);
     return LOK;
 }
 
-__global__ __launch_bounds__(LWG) void merge_large_kernel(SmallParams p, uint8_t *pool, u64 pool_bytes, u64 *pool_used) {
+__global__ __launch_bounds__(LWG) __attribute__((amdgpu_waves_per_eu(4))) void merge_large_kernel(SmallParams p, uint8_t *pool, u64 pool_bytes, u64 *pool_used) {
     __shared__ Shared sh;
+    __shared__ __align__(16) uint32_t arena_raw[LARENA];
+    LDS uint32_t *arena = (LDS uint32_t *)arena_raw;
     const uint32_t tid = threadIdx.x;
     const uint32_t S = p.a_stride;
     // Deferred documents are listed by merge_small_kernel (p.deferred, p.n_deferred).  Each
@@ -689,6 +893,9 @@ __global__ __launch_bounds__(LWG) void merge_large_kernel(SmallParams p, uint8_t
     // long document's merge), and an empty list costs one read per workgroup.
     __shared__ uint32_t claim;
     const uint32_t nd = *p.n_deferred;
+#if HM_STAMPS
+    if (tid <= HML_NSTAMP) hml_st[tid] = 0;
+#endif
     for (;;) {
         if (tid == 0) claim = atomicAdd(p.large_cursor, 1u);
         bsync();
@@ -698,7 +905,10 @@ __global__ __launch_bounds__(LWG) void merge_large_kernel(SmallParams p, uint8_t
         const hm_doc_row doc = p.docs[d];
         const uint32_t ds = hm_slot(p, d);
         int32_t H = 0;
-        const Outcome oc = merge_doc_large(p, sh, doc, d, pool, pool_bytes, pool_used, H);
+#if HM_STAMPS
+        { const u64 t0 = lstamp_now(); if (tid == 0) hml_st[HML_NSTAMP] = t0; }
+#endif
+        const Outcome oc = merge_doc_large(p, sh, arena, doc, d, pool, pool_bytes, pool_used, H);
         bsync();
         hm_doc_result r = {};
         r.err_change = HM_NONE; r.err_op = HM_NONE;
@@ -736,6 +946,9 @@ __global__ __launch_bounds__(LWG) void merge_large_kernel(SmallParams p, uint8_t
         if (tid == 0) p.res_docs[ds] = r;
         bsync();
     }
+#if HM_STAMPS
+    if (tid < HML_NSTAMP) atomicAdd(&hml_stamp_acc[tid], (unsigned long long)hml_st[tid]);
+#endif
 }
 
 }  // namespace hml
@@ -749,6 +962,19 @@ size_t hm_large_scratch_bound(const hm_batch *b) {
                                   4 * b->n_changes + 64 * b->n_docs, &s);
     return per + (size_t)b->n_docs * 48 * 16 + (1u << 20);
 }
+
+#if HM_STAMPS
+extern "C" int hm_debug_lstamps(unsigned long long *out, int n, int reset) {
+    if (n > HML_NSTAMP) n = HML_NSTAMP;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hml::hml_stamp_acc), n * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[HML_NSTAMP] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(hml::hml_stamp_acc), z, sizeof z) != hipSuccess) return -1;
+    }
+    return n;
+}
+#endif
 
 hipError_t hm_launch_large(const SmallParams &p, void *pool, size_t pool_bytes, unsigned long long *pool_used,
                            uint32_t grid, hipStream_t s) {
