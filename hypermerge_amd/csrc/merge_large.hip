@@ -329,7 +329,8 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
     //     Otherwise (a listed dep dominated by another: never for heads-based deps) the literal
     //     fold runs serially in history order below.
     uint32_t *cur = p.res_all_deps + (size_t)doc.change_off * S, *nxt = X.vc;   // row stride S / A
-    if (2 * n * A + T <= LARENA) {
+    const bool regrows = A <= 8;            // rows held in registers: one LDS buffer, updated in place
+    if ((regrows ? n * A : 2 * n * A) + T <= LARENA) {
         // the same rounds and check with the first-arrival table and both row buffers in LDS
         LDS uint32_t *lt = ar, *lc = ar + T, *ln = ar + T + n * A;        // row stride A
         for (uint32_t i = tid; i < T; i += LWG) lt[i] = X.tab[i];
@@ -350,33 +351,70 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
             if (sq < sh.base[a] || sq > sh.maxs[a] || sh.maxs[a] == 0) return 0xFFFFFFFFu;
             return lt[sh.tabo[a] + (sq - sh.base[a])];
         };
-        for (;;) {
-            if (tid == 0) sh.grew = 0;
-            bsync();
-            bool grew = false;
-            for (uint32_t i = tid; i < n; i += LWG) {
-                const LDS uint32_t *row = lc + i * A;
-                LDS uint32_t *out = ln + i * A;
-                for (uint32_t a = 0; a < A; a++) out[a] = row[a];
-                if (X.hist[i] < 0) continue;
-                for (uint32_t a = 0; a < A; a++) {
-                    const uint32_t sq = row[a];
-                    if (!sq) continue;
-                    const uint32_t ti = lslot(a, sq);
-                    if (ti >= n) continue;
-                    const LDS uint32_t *r2 = lc + ti * A;
-                    for (uint32_t b = 0; b < A; b++) {
-                        const uint32_t v = b == a ? sq : r2[b];
-                        if (out[b] < v) { out[b] = v; grew = true; }
+        if (regrows) {
+            // in place: every entry is a seq the closure contains, so reading a row another thread
+            // is growing mixes valid lower bounds, and a round in which no row grows is the fixpoint
+            for (;;) {
+                if (tid == 0) sh.grew = 0;
+                bsync();
+                bool grew = false;
+                for (uint32_t i = tid; i < n; i += LWG) {
+                    if (X.hist[i] < 0) continue;
+                    LDS uint32_t *row = lc + i * A;
+                    uint32_t v[8], v0[8];
+#pragma unroll
+                    for (uint32_t b = 0; b < 8; b++) v0[b] = v[b] = b < A ? row[b] : 0u;
+#pragma unroll
+                    for (uint32_t a = 0; a < 8; a++) {
+                        if (a >= A) break;
+                        const uint32_t sq = v[a];
+                        if (!sq) continue;
+                        const uint32_t ti = lslot(a, sq);
+                        if (ti >= n) continue;
+                        const LDS uint32_t *r2 = lc + ti * A;
+#pragma unroll
+                        for (uint32_t b = 0; b < 8; b++)
+                            if (b < A && b != a) { const uint32_t x = r2[b]; v[b] = v[b] > x ? v[b] : x; }
+                    }
+#pragma unroll
+                    for (uint32_t b = 0; b < 8; b++)
+                        if (b < A && v[b] != v0[b]) { row[b] = v[b]; grew = true; }
+                }
+                if (grew) sh.grew = 1;
+                bsync();
+                const bool any = sh.grew != 0;
+                bsync();
+                if (!any) break;
+            }
+        } else {
+            for (;;) {
+                if (tid == 0) sh.grew = 0;
+                bsync();
+                bool grew = false;
+                for (uint32_t i = tid; i < n; i += LWG) {
+                    const LDS uint32_t *row = lc + i * A;
+                    LDS uint32_t *out = ln + i * A;
+                    for (uint32_t a = 0; a < A; a++) out[a] = row[a];
+                    if (X.hist[i] < 0) continue;
+                    for (uint32_t a = 0; a < A; a++) {
+                        const uint32_t sq = row[a];
+                        if (!sq) continue;
+                        const uint32_t ti = lslot(a, sq);
+                        if (ti >= n) continue;
+                        const LDS uint32_t *r2 = lc + ti * A;
+                        for (uint32_t b = 0; b < A; b++) {
+                            const uint32_t v = b == a ? sq : r2[b];
+                            if (out[b] < v) { out[b] = v; grew = true; }
+                        }
                     }
                 }
+                if (grew) sh.grew = 1;
+                bsync();
+                const bool any = sh.grew != 0;
+                LDS uint32_t *t = lc; lc = ln; ln = t;          // every row of the new buffer was written
+                bsync();
+                if (!any) break;
             }
-            if (grew) sh.grew = 1;
-            bsync();
-            const bool any = sh.grew != 0;
-            LDS uint32_t *t = lc; lc = ln; ln = t;          // every row of the new buffer was written
-            bsync();
-            if (!any) break;
         }
         LSTAMP(2);
         if (tid == 0) sh.all_ok = 1;
@@ -387,25 +425,49 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
             for (uint32_t a = 0; a < S; a++) grow_[a] = a < A ? row[a] : 0u;
             if (X.hist[i] < 0) continue;
             const hm_change_row c = CH[i];
-            LDS uint32_t *acc = ln + i * A;
-            for (uint32_t a = 0; a < A; a++) acc[a] = 0;
-            auto fold = [&](uint32_t a, uint32_t sq) {
-                if (sq == 0) return;
-                const uint32_t ti = lslot(a, sq);
-                if (ti >= n) { acc[a] = 0xFFFFFFFFu; return; }
-                const LDS uint32_t *r2 = lc + ti * A;
-                for (uint32_t b = 0; b < A; b++) if (acc[b] < r2[b]) acc[b] = r2[b];
-                acc[a] = sq;
-            };
-            bool own = false;
-            for (uint32_t j = 0; j < c.n_deps; j++) {
-                const hm_dep_row dp = p.deps[c.dep_off + j];
-                if (dp.actor == c.actor) { own = true; fold(c.actor, c.seq - 1); }
-                else fold(dp.actor, dp.seq);
-            }
-            if (!own) fold(c.actor, c.seq - 1);
             bool same = true;
-            for (uint32_t a = 0; a < A; a++) same = same && acc[a] == row[a];
+            if (regrows) {
+                uint32_t acc[8];
+#pragma unroll
+                for (uint32_t b = 0; b < 8; b++) acc[b] = 0;
+                auto fold = [&](uint32_t a, uint32_t sq) {
+                    if (sq == 0) return;
+                    const uint32_t ti = lslot(a, sq);
+                    if (ti >= n) { same = false; return; }
+                    const LDS uint32_t *r2 = lc + ti * A;
+#pragma unroll
+                    for (uint32_t b = 0; b < 8; b++)
+                        if (b < A) { const uint32_t x = r2[b]; acc[b] = b == a ? sq : (acc[b] > x ? acc[b] : x); }
+                };
+                bool own = false;
+                for (uint32_t j = 0; j < c.n_deps; j++) {
+                    const hm_dep_row dp = p.deps[c.dep_off + j];
+                    if (dp.actor == c.actor) { own = true; fold(c.actor, c.seq - 1); }
+                    else fold(dp.actor, dp.seq);
+                }
+                if (!own) fold(c.actor, c.seq - 1);
+#pragma unroll
+                for (uint32_t b = 0; b < 8; b++) if (b < A) same = same && acc[b] == row[b];
+            } else {
+                LDS uint32_t *acc = ln + i * A;
+                for (uint32_t a = 0; a < A; a++) acc[a] = 0;
+                auto fold = [&](uint32_t a, uint32_t sq) {
+                    if (sq == 0) return;
+                    const uint32_t ti = lslot(a, sq);
+                    if (ti >= n) { acc[a] = 0xFFFFFFFFu; return; }
+                    const LDS uint32_t *r2 = lc + ti * A;
+                    for (uint32_t b = 0; b < A; b++) if (acc[b] < r2[b]) acc[b] = r2[b];
+                    acc[a] = sq;
+                };
+                bool own = false;
+                for (uint32_t j = 0; j < c.n_deps; j++) {
+                    const hm_dep_row dp = p.deps[c.dep_off + j];
+                    if (dp.actor == c.actor) { own = true; fold(c.actor, c.seq - 1); }
+                    else fold(dp.actor, dp.seq);
+                }
+                if (!own) fold(c.actor, c.seq - 1);
+                for (uint32_t a = 0; a < A; a++) same = same && acc[a] == row[a];
+            }
             if (!same) sh.all_ok = 0;
         }
         bsync();
