@@ -797,12 +797,14 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
         bsync();
         uint32_t nl;
         scan_array(sh, X.listid, O, &nl);          // exclusive prefix -> compact list id (valid for list objects)
+        // per node: its register and compact list id (survtmp / segk are free after the ranks)
+        // per node i: its register in survtmp[i], its compact list id in segk[i] (both free after the ranks)
         for (uint32_t k = tid; k < m; k += LWG) {
             const hm_op_row o = OP[k];
-            if (X.opkey[k] == ~0ull || o.action != HM_INS) continue;
+            if (o.action != HM_INS || hist_of(opchg_of(k)) < 0) continue;
             const uint32_t i = atomicAdd(&sh.nins, 1u);
             const uint32_t pi = o.parent == HM_HEAD ? R + o.obj : o.parent;
-            X.nodeop[i] = k; X.nodepi[i] = pi;
+            X.nodeop[i] = k; X.nodepi[i] = pi; X.survtmp[i] = o.reg; X.segk[i] = X.listid[o.obj];
             X.nodekey[i] = ((u64)o.elem << 8) | act_of(opchg_of(k));
             X.regnode[o.reg] = i;
             g_add(&X.pcount[pi], 1u);
@@ -813,13 +815,18 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
         bsync();
         uint32_t tp;
         scan_array(sh, X.poff, NP, &tp);
-        for (uint32_t i = tid; i < N; i += LWG) { const uint32_t pi = X.nodepi[i]; X.plist[X.poff[pi] + g_add(&X.pfill[pi], 1u)] = i; }
-        bsync();
+        // sibling lists (an only child needs none: no next sibling, first child of its parent)
         for (uint32_t i = tid; i < N; i += LWG) {
             const uint32_t pi = X.nodepi[i];
+            if (X.pcount[pi] > 1) X.plist[X.poff[pi] + g_add(&X.pfill[pi], 1u)] = i;
+        }
+        bsync();
+        for (uint32_t i = tid; i < N; i += LWG) {
+            const uint32_t pi = X.nodepi[i], np = X.pcount[pi];
+            if (np == 1) { X.ns[i] = 0xFFFFFFFFu; X.fc[pi] = i; continue; }
             const u64 key = X.nodekey[i];
             uint32_t best = 0xFFFFFFFFu; u64 bkey = 0; bool firstc = true;
-            for (uint32_t q = 0; q < X.pcount[pi]; q++) {
+            for (uint32_t q = 0; q < np; q++) {
                 const uint32_t j = X.plist[X.poff[pi] + q];
                 const u64 kj = X.nodekey[j];
                 if (kj > key) firstc = false;
@@ -842,9 +849,8 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
             else { nx0[e] = nx; va0[e] = va; }
         };
         for (uint32_t i = tid; i < N; i += LWG) {
-            const hm_op_row o = OP[X.nodeop[i]];
-            const uint32_t hd = N + X.listid[o.obj];
-            const uint32_t f = X.fc[o.reg];
+            const uint32_t hd = N + X.segk[i];
+            const uint32_t f = X.fc[X.survtmp[i]];
             const uint32_t pi = X.nodepi[i];
             put(2 * i, f != 0xFFFFFFFFu ? 2 * f : 2 * i + 1, 1);
             put(2 * i + 1, X.ns[i] != 0xFFFFFFFFu ? 2 * X.ns[i] : (pi >= R ? 2 * hd + 1 : 2 * X.regnode[pi] + 1), 0);
@@ -870,8 +876,6 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
                 }
                 bsync();
             }
-            for (uint32_t e = tid; e < E; e += LWG) va0[e] = tw[e] & 0xFFFFu;
-            bsync();
         } else {
             for (uint32_t rd = 0; rd < rounds; rd++) {
                 for (uint32_t e = tid; e < E; e += LWG) {
@@ -883,21 +887,22 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
             }
         }
         LSTAMP(8);
+        // tour sums (entries from here to the end of the list): LDS words or the pool array
+        auto tsum = [&](uint32_t e) -> uint32_t { return tour_lds ? (tw[e] & 0xFFFFu) : va0[e]; };
         for (uint32_t o = tid; o < O; o += LWG) {
             const bool isl = X.objtype[o] == HM_MAKE_LIST || X.objtype[o] == HM_MAKE_TEXT;
-            if (isl) X.listbase[X.listid[o]] = va0[2 * (N + X.listid[o])];
+            if (isl) X.listbase[X.listid[o]] = tsum(2 * (N + X.listid[o]));
         }
         bsync();
         uint32_t tl;
         scan_array(sh, X.listbase, nl, &tl);
         for (uint32_t i = tid; i < N; i += LWG) {
-            const hm_op_row o = OP[X.nodeop[i]];
-            const uint32_t l = X.listid[o.obj];
-            const uint32_t total_l = va0[2 * (N + l)];
-            const uint32_t ps = X.listbase[l] + total_l - va0[2 * i];
+            const uint32_t l = X.segk[i], rg = X.survtmp[i];
+            const uint32_t total_l = tsum(2 * (N + l));
+            const uint32_t ps = X.listbase[l] + total_l - tsum(2 * i);
             X.pos[i] = ps;
-            X.vis[ps] = X.survcnt[o.reg] > 0 ? 1u : 0u;
-            X.insmin[o.reg] = 0xFFFFFFFFull;                     // -> list index or -1
+            X.vis[ps] = X.survcnt[rg] > 0 ? 1u : 0u;
+            X.insmin[rg] = 0xFFFFFFFFull;                        // -> list index or -1
         }
         bsync();
         // exclusive scan of visibility over pre-order positions, kept in survp (free now)
@@ -906,12 +911,8 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
         uint32_t tv;
         scan_array(sh, X.survp, N, &tv);
         for (uint32_t i = tid; i < N; i += LWG) {
-            const hm_op_row o = OP[X.nodeop[i]];
             const uint32_t ps = X.pos[i];
-            if (X.vis[ps]) {
-                const uint32_t l = X.listid[o.obj];
-                X.insmin[o.reg] = X.survp[ps] - X.survp[X.listbase[l]];
-            }
+            if (X.vis[ps]) X.insmin[X.survtmp[i]] = X.survp[ps] - X.survp[X.listbase[X.segk[i]]];
         }
         bsync();
     }
