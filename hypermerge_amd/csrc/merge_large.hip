@@ -79,6 +79,7 @@ struct Shared {
     u64 errkey;
     uint32_t scan[LWG / 64 + 1];
     u64 scratch_base;
+    u64 ws_base, ws_size;           // this workgroup's scratch, reused by its next documents
 };
 
 enum : uint32_t { LF_UNSUPPORTED = 1u, LF_NOPOOL = 2u };
@@ -104,18 +105,18 @@ __device__ __forceinline__ uint32_t block_excl_scan(Shared &sh, uint32_t v, uint
     *total = tot;
     return off + x - v;
 }
-// exclusive scan of arr[0..N) in place (chunks of LWG)
+// exclusive scan of arr[0..N) in place: each thread owns a contiguous run of ceil(N / LWG)
+// entries (its loads are independent, so they overlap), one block scan of the run sums
 __device__ void scan_array(Shared &sh, uint32_t *arr, uint32_t N, uint32_t *total) {
-    uint32_t carry = 0;
-    for (uint32_t c0 = 0; c0 < N; c0 += LWG) {
-        const uint32_t i = c0 + threadIdx.x;
-        const uint32_t v = i < N ? arr[i] : 0;
-        uint32_t t;
-        const uint32_t ex = block_excl_scan(sh, v, &t);
-        if (i < N) arr[i] = carry + ex;
-        carry += t;
-    }
-    *total = carry;
+    const uint32_t per = (N + LWG - 1) / LWG;
+    const uint32_t b0 = threadIdx.x * per < N ? threadIdx.x * per : N;
+    const uint32_t b1 = b0 + per < N ? b0 + per : N;
+    uint32_t sum = 0;
+    for (uint32_t i = b0; i < b1; i++) sum += arr[i];
+    uint32_t tot;
+    uint32_t ex = block_excl_scan(sh, sum, &tot);
+    for (uint32_t i = b0; i < b1; i++) { const uint32_t v = arr[i]; arr[i] = ex; ex += v; }
+    *total = tot;
     bsync();
 }
 
@@ -193,9 +194,15 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
         // scratch for this document
         Scratch tmp;
         const size_t need = large_carve(0, n, m, R, O, A, t, &tmp);
-        const u64 at = atomicAdd(pool_used, (u64)need);
-        if (at + need > pool_bytes) sh.flags |= LF_NOPOOL;
-        sh.scratch_base = (u64)(uintptr_t)(pool + at);
+        // reuse the workgroup's previous scratch when it is big enough: its lines are still in
+        // L2 / MALL, where fresh pool memory per document cost HBM write-backs and misses
+        if (need <= sh.ws_size) sh.scratch_base = sh.ws_base;
+        else {
+            const u64 at = atomicAdd(pool_used, (u64)need);
+            if (at + need > pool_bytes) sh.flags |= LF_NOPOOL;
+            else { sh.ws_base = (u64)(uintptr_t)(pool + at); sh.ws_size = need; }
+            sh.scratch_base = (u64)(uintptr_t)(pool + at);
+        }
     }
     bsync();
     if (sh.flags) return LUNSUP;
@@ -956,6 +963,7 @@ __global__ __launch_bounds__(LWG) __attribute__((amdgpu_waves_per_eu(4))) void m
     // long document's merge), and an empty list costs one read per workgroup.
     __shared__ uint32_t claim;
     const uint32_t nd = *p.n_deferred;
+    if (tid == 0) { sh.ws_base = 0; sh.ws_size = 0; }
 #if HM_STAMPS
     if (tid <= HML_NSTAMP) hml_st[tid] = 0;
 #endif
