@@ -184,7 +184,7 @@ def main() -> int:
     # spot parity against the oracle on a sample (checker only; not timed)
     parity = None
     cpu = cpu_mt = None
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and ws == 1 and not args.no_cpu:          # CPU legs: rank 0 at N=1 only
         import oracle.oracle as O
         from hypermerge_amd.columnar import Batch
         k = min(args.check_docs, nd)
@@ -210,7 +210,7 @@ def main() -> int:
     # end to end: host tables -> device -> merge -> host results (hm_merge_host, PCIe included);
     # reported beside the kernel rate, never as `value`
     e2e = None
-    if rank == 0 and not args.no_e2e:
+    if rank == 0 and ws == 1 and not args.no_e2e:
         eng.merge(_subbatch(batch, min(nd, 1000)))          # allocate staging once
         t = time.perf_counter()
         ge = eng.merge(batch)
