@@ -672,7 +672,65 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         const uint32_t key = first_me & 63;
         u64 applied = 0, queue = 0;                       // applied keys; queued lanes
         bool copy_applied = false;                        // a duplicate copy stands for its key
-        for (uint32_t i = 0; i < n; i++) {
+        bool solved = false;
+        if (dupm == 0) {
+            // No duplicates: every change's place in history in parallel.  The arrival whose
+            // processing applies change c is t(c) = max(arrival(c), t(deps)) = the latest arrival
+            // among c and its ancestors (never for a change that cannot apply).  Within that
+            // processing the arrival itself applies in pass 1 (it is last in the queue); a queued
+            // change applies in the first pass whose scan reaches it after all its deps:
+            // pass(c) = max(2, pass(d) + [d after c in the queue]) over its deps applied by the
+            // same arrival.  History = applied changes ordered by (t, pass, arrival).  The result
+            // is checked (every dep ordered before its dependent; a dependency cycle fails the
+            // check) and the pass loop below runs otherwise.
+            LDS uint32_t *tx = (LDS uint32_t *)L.hist_of;           // free until K1b
+            const uint32_t INF = 0xFFu;
+            uint32_t t = (!act || never) ? INF : lane;
+            for (uint32_t it = 0; it <= n; it++) {
+                tx[lane] = t;
+                wave_sync();
+                uint32_t nt = t;
+                if (act && t != INF)
+                    for (u64 m = dall; m; m &= m - 1) { const uint32_t x = tx[__builtin_ctzll(m)]; nt = nt > x ? nt : x; }
+                wave_sync();
+                const bool grew = nt != t;
+                t = nt;
+                if (__ballot(grew) == 0) break;
+            }
+            uint32_t ps = t == lane ? 1u : 2u;
+            bool conv = false;
+            for (uint32_t it = 0; it <= n + 1; it++) {
+                tx[lane] = (t << 8) | ps;
+                wave_sync();
+                uint32_t np = ps;
+                if (act && t != INF && t != lane)
+                    for (u64 m = dall; m; m &= m - 1) {
+                        const uint32_t d = (uint32_t)__builtin_ctzll(m), w = tx[d];
+                        if ((w >> 8) == t) { const uint32_t v = (w & 0xFFu) + (d > lane ? 1u : 0u); np = np > v ? np : v; }
+                    }
+                wave_sync();
+                const bool grew = np != ps;
+                ps = np > 0xFEu ? 0xFEu : np;
+                if (__ballot(grew) == 0) { conv = true; break; }
+            }
+            const bool apl = act && t != INF;
+            const uint32_t hk = apl ? ((t << 16) | (ps << 8) | lane) : 0xFFFFFFFFu;
+            // check: every dep of an applied change is applied before it
+            tx[lane] = hk;
+            wave_sync();
+            bool bad = false;
+            if (apl)
+                for (u64 m = dall; m; m &= m - 1) bad |= tx[__builtin_ctzll(m)] >= hk;
+            wave_sync();
+            if (conv && __ballot(bad) == 0) {
+                uint32_t rank = 0;
+                for (uint32_t j = 0; j < n; j++) rank += (uint32_t)__builtin_amdgcn_readlane((int)hk, (int)j) < hk ? 1u : 0u;
+                hist = apl ? (int32_t)rank : -1;
+                H = (uint32_t)__popcll(__ballot(apl));
+                solved = true;
+            }
+        }
+        for (uint32_t i = 0; i < n && !solved; i++) {
             queue |= 1ull << i;
             u64 P = __ballot(lane == i && !never && (dall & ~applied) == 0);
             while (P) {
