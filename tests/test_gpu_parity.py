@@ -166,3 +166,44 @@ def test_literal_transitive_deps_fold_on_gpu(engine, engine_general, general):
     assert_same(b, g, o)
     assert list(g.all_deps[3 * b.a_stride: 3 * b.a_stride + 3]) == [1, 1, 0]
     assert canonical_json(b, g, 0) == canonical_json(b, o, 0)
+
+
+def _qc(actor, seq, deps, key=None):
+    from hypermerge_amd.columnar import ROOT_ID as R
+    ops = [] if key is None else [{"action": "set", "obj": R, "key": key, "value": f"{actor}{seq}"}]
+    return {"actor": actor, "seq": seq, "deps": deps, "ops": ops}
+
+
+QUEUE_ORDERS = [
+    # a chain arriving newest first: each later pass applies one more link (history A1..A5)
+    ("reversed_chain", [_qc("aaaa", s, {}, "k") for s in (5, 4, 3, 2, 1)]),
+    # a queued change ahead of its dep in the queue waits one pass longer than the dep
+    ("queued_behind_dep", [_qc("bbbb", 2, {"aaaa": 1}, "x"), _qc("aaaa", 2, {}, "x"), _qc("bbbb", 1, {}, "y"),
+                           _qc("aaaa", 1, {}, "y")]),
+    # a dependency cycle never becomes ready (both stay queued); the rest still applies
+    ("dep_cycle", [_qc("aaaa", 1, {"bbbb": 1}, "k"), _qc("bbbb", 1, {"aaaa": 1}, "k"), _qc("cccc", 1, {}, "k"),
+                   _qc("cccc", 2, {}, "j")]),
+    # a change depending on a cycle member is stuck too
+    ("behind_cycle", [_qc("cccc", 1, {"aaaa": 1}, "k"), _qc("aaaa", 1, {"bbbb": 1}, "k"),
+                      _qc("bbbb", 1, {"aaaa": 1}, "k"), _qc("dddd", 1, {}, "k")]),
+    # several arrivals, each unblocking a different queued subset, interleaved actors
+    ("interleaved_unblocks", [_qc("aaaa", 3, {"bbbb": 2}, "k"), _qc("bbbb", 2, {"cccc": 1}, "k"),
+                              _qc("cccc", 2, {"aaaa": 2}, "j"), _qc("aaaa", 2, {}, "j"), _qc("bbbb", 1, {}, "i"),
+                              _qc("cccc", 1, {"bbbb": 1}, "k"), _qc("aaaa", 1, {}, "k")]),
+    # a dep that never arrives blocks its dependents for good
+    ("missing_dep", [_qc("aaaa", 1, {"zzzz": 3}, "k"), _qc("aaaa", 2, {}, "k"), _qc("bbbb", 1, {}, "k")]),
+]
+
+
+@pytest.mark.parametrize("general", [False, True], ids=["small", "general"])
+@pytest.mark.parametrize("name,changes", QUEUE_ORDERS, ids=[c[0] for c in QUEUE_ORDERS])
+def test_queue_orders_on_gpu(engine, engine_general, general, name, changes):
+    """Causal-queue pass order (Automerge applyQueuedOps) for hand-built arrival orders:
+    history position of every change, queued changes and the merged registers equal the
+    oracle's on both kernels (the small kernel's parallel (arrival, pass) history included)."""
+    b = encode([changes])
+    g = (engine_general if general else engine).merge(b)
+    o = O.merge(b)
+    assert g.docs["status"][0] != 16
+    assert_same(b, g, o)
+    assert canonical_json(b, g, 0) == canonical_json(b, o, 0)

@@ -9,7 +9,8 @@ NAMES = ["pre-merge", "validate+first-table", "deps/readiness", "history", "ance
          "K2 op scan", "objects+survivors", "offsets+rank+ties", "lists/counters", "outputs(+next loads)", "stage next"]
 cfg = sys.argv[1] if len(sys.argv) > 1 else "C4"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000
-b = synth.generate(synth.config(cfg, n_docs=n))
+over = {"arrival": int(sys.argv[3])} if len(sys.argv) > 3 else {}
+b = synth.generate(synth.config(cfg, n_docs=n, **over))
 e = Engine(0)
 L = lib()
 L.hm_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
