@@ -673,51 +673,76 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         u64 applied = 0, queue = 0;                       // applied keys; queued lanes
         bool copy_applied = false;                        // a duplicate copy stands for its key
         bool solved = false;
-        if (dupm == 0) {
-            // No duplicates: every change's place in history in parallel.  The arrival whose
-            // processing applies change c is t(c) = max(arrival(c), t(deps)) = the latest arrival
-            // among c and its ancestors (never for a change that cannot apply).  Within that
-            // processing the arrival itself applies in pass 1 (it is last in the queue); a queued
-            // change applies in the first pass whose scan reaches it after all its deps:
-            // pass(c) = max(2, pass(d) + [d after c in the queue]) over its deps applied by the
-            // same arrival.  History = applied changes ordered by (t, pass, arrival).  The result
-            // is checked (every dep ordered before its dependent; a dependency cycle fails the
+        {
+            // Every change's place in history in parallel, per (actor, seq) key (its first
+            // arrival's lane; copies of a key have equal content, hence equal deps).  The arrival
+            // whose processing applies key K is t(K) = max(first arrival of K, t(deps)) = the
+            // latest first arrival among K and its ancestors (never for a key that cannot apply).
+            // Within that processing the arrival itself applies in pass 1 (it is last in the
+            // queue); otherwise the queued copy c of K (arrived before t(K)) can apply in pass
+            // p(c) = max(2, pass(D) + [D's applied copy after c in the queue]) over the deps D
+            // applied by the same arrival, and the copy that applies is the first one a pass
+            // reaches: (pass, pos)(K) = min over copies of (p(c), c).  The other copies are
+            // duplicate no-ops.  History = applied copies ordered by (t, pass, pos).  The result is
+            // checked (every dep ordered before its dependent; a dependency cycle fails the
             // check) and the pass loop below runs otherwise.
             LDS uint32_t *tx = (LDS uint32_t *)L.hist_of;           // free until K1b
+            LDS uint32_t *tm = (LDS uint32_t *)L.anc;               // (free until K1b) copy minima
             const uint32_t INF = 0xFFu;
-            uint32_t t = (!act || never) ? INF : lane;
+            const bool has_dup = dupm != 0;
+            const bool kl = act && !dup;                            // this lane is its key's first arrival
+            uint32_t t = (!kl || never) ? INF : lane;
             for (uint32_t it = 0; it <= n; it++) {
                 tx[lane] = t;
                 wave_sync();
                 uint32_t nt = t;
-                if (act && t != INF)
+                if (kl && t != INF)
                     for (u64 m = dall; m; m &= m - 1) { const uint32_t x = tx[__builtin_ctzll(m)]; nt = nt > x ? nt : x; }
                 wave_sync();
                 const bool grew = nt != t;
                 t = nt;
                 if (__ballot(grew) == 0) break;
             }
-            uint32_t ps = t == lane ? 1u : 2u;
+            // every copy learns its key's t; key word = t << 16 | pass << 8 | pos
+            tx[lane] = t;
+            wave_sync();
+            const uint32_t tk = act ? tx[key] : INF;
+            wave_sync();
+            uint32_t w = (!kl || t == INF) ? 0xFFFFFFFFu : ((t << 16) | ((t == lane ? 1u : 2u) << 8) | lane);
             bool conv = false;
             for (uint32_t it = 0; it <= n + 1; it++) {
-                tx[lane] = (t << 8) | ps;
+                tx[lane] = w;                                       // meaningful on key lanes
+                if (has_dup) tm[lane] = 0xFFFFFFFFu;
                 wave_sync();
-                uint32_t np = ps;
-                if (act && t != INF && t != lane)
+                uint32_t cand = 0xFFFFFFFFu;
+                if (act && tk != INF && tk != key && lane < tk) {   // a queued copy of a queued key
+                    uint32_t pc = 2;
                     for (u64 m = dall; m; m &= m - 1) {
-                        const uint32_t d = (uint32_t)__builtin_ctzll(m), w = tx[d];
-                        if ((w >> 8) == t) { const uint32_t v = (w & 0xFFu) + (d > lane ? 1u : 0u); np = np > v ? np : v; }
+                        const uint32_t wd = tx[__builtin_ctzll(m)];
+                        if ((wd >> 16) == tk) {
+                            const uint32_t v = ((wd >> 8) & 0xFFu) + ((wd & 0xFFu) > lane ? 1u : 0u);
+                            pc = pc > v ? pc : v;
+                        }
                     }
+                    cand = (tk << 16) | ((pc > 0xFEu ? 0xFEu : pc) << 8) | lane;
+                }
                 wave_sync();
-                const bool grew = np != ps;
-                ps = np > 0xFEu ? 0xFEu : np;
+                uint32_t nw = w;
+                if (has_dup) {
+                    if (cand != 0xFFFFFFFFu) lds_min(&tm[key], cand);
+                    wave_sync();
+                    if (kl && t != INF && t != lane) nw = tm[lane];
+                } else if (kl && t != INF && t != lane) nw = cand;
+                const bool grew = nw != w;
+                w = nw;
                 if (__ballot(grew) == 0) { conv = true; break; }
             }
-            const bool apl = act && t != INF;
-            const uint32_t hk = apl ? ((t << 16) | (ps << 8) | lane) : 0xFFFFFFFFu;
-            // check: every dep of an applied change is applied before it
-            tx[lane] = hk;
+            tx[lane] = w;
             wave_sync();
+            const uint32_t wk = act && tk != INF ? tx[key] : 0xFFFFFFFFu;
+            const bool apl = wk != 0xFFFFFFFFu && (wk & 0xFFu) == lane;
+            const uint32_t hk = apl ? wk : 0xFFFFFFFFu;
+            // check: every dep of an applied copy is applied before it
             bool bad = false;
             if (apl)
                 for (u64 m = dall; m; m &= m - 1) bad |= tx[__builtin_ctzll(m)] >= hk;
@@ -725,8 +750,10 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
             if (conv && __ballot(bad) == 0) {
                 uint32_t rank = 0;
                 for (uint32_t j = 0; j < n; j++) rank += (uint32_t)__builtin_amdgcn_readlane((int)hk, (int)j) < hk ? 1u : 0u;
-                hist = apl ? (int32_t)rank : -1;
+                hist = apl ? (int32_t)rank : (act && tk != INF ? -2 : -1);
                 H = (uint32_t)__popcll(__ballot(apl));
+                if (apl && dup) L.first[a8 * 64 + (slot & 63)] = lane;   // (actor, seq) -> applied copy
+                copy_applied = __ballot(apl && dup) != 0;
                 solved = true;
             }
         }

@@ -55,6 +55,9 @@ def assert_same(b, g, o, allow_unsupported=False):
     ("C5", 2000, {"arrival": 1, "dup_pct": 0}),
     ("C4", 4000, {"arrival": 2, "shuffle_pct": 30, "dup_pct": 6}),   # duplicate copies applied before their originals
     ("C5", 4000, {"dup_pct": 12}),
+    ("C5", 3000, {"dup_pct": 30, "shuffle_pct": 40}),       # many copies, heavy reordering
+    ("C4", 3000, {"arrival": 1, "dup_pct": 10}),            # actor-major with duplicate copies
+    ("C2", 3000, {"arrival": 2, "shuffle_pct": 50, "dup_pct": 15}),
 ])
 def test_synthetic_parity(engine, name, n, extra):
     b = synth.generate(synth.config(name, n_docs=n, **extra))
@@ -192,6 +195,16 @@ QUEUE_ORDERS = [
                               _qc("cccc", 1, {"bbbb": 1}, "k"), _qc("aaaa", 1, {}, "k")]),
     # a dep that never arrives blocks its dependents for good
     ("missing_dep", [_qc("aaaa", 1, {"zzzz": 3}, "k"), _qc("aaaa", 2, {}, "k"), _qc("bbbb", 1, {}, "k")]),
+    # duplicate copies: the queued first copy applies, the later copy is a no-op
+    ("dup_after_apply", [_qc("aaaa", 2, {}, "k"), _qc("aaaa", 1, {}, "j"), _qc("aaaa", 2, {}, "k")]),
+    # the second copy applies (its dep is applied earlier in the same pass), the first is a no-op
+    ("dup_second_copy_applies", [_qc("bbbb", 1, {"aaaa": 2}, "k"), _qc("aaaa", 2, {}, "k"),
+                                 _qc("bbbb", 1, {"aaaa": 2}, "k"), _qc("aaaa", 1, {}, "j")]),
+    # copies of a key stuck behind a missing dep stay queued
+    ("dup_never", [_qc("aaaa", 1, {"zzzz": 1}, "k"), _qc("bbbb", 1, {}, "k"), _qc("aaaa", 1, {"zzzz": 1}, "k")]),
+    # a dependent of a key applied through its second copy
+    ("dup_dependent", [_qc("bbbb", 1, {"aaaa": 2}, "k"), _qc("aaaa", 2, {}, "k"), _qc("bbbb", 1, {"aaaa": 2}, "k"),
+                       _qc("cccc", 1, {"bbbb": 1}, "j"), _qc("aaaa", 1, {}, "j"), _qc("bbbb", 2, {}, "i")]),
 ]
 
 
