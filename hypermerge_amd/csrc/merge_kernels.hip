@@ -1185,6 +1185,11 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     // values go to merge_large_kernel, which tracks sum|inc| exactly).
     if (p.counters && __ballot(counter_ops)) {
         bool outside = false;
+        // every inc's value load issued before the first is used (they are L2 round trips)
+        int64_t incv[OPL];
+#pragma unroll
+        for (int t = 0; t < OPL; t++)
+            incv[t] = (oh[t] >= 0 && oact[t] == HM_INC) ? (int64_t)op_value(p, doc, lane + WAVE * t) : 0;
 #pragma unroll
         for (int t = 0; t < OPL; t++) {
             if (oh[t] < 0 || oact[t] != HM_INC) continue;
@@ -1192,7 +1197,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
             const uint32_t reg = oreg[t], b0 = L.regoff[reg], cnt = L.survcnt[reg];
             const u64 an = L.anc[oh[t]];
             const uint32_t my_vtag = (L.opmeta[k] >> 16) & 0xFF;
-            const int64_t v = (int64_t)op_value(p, doc, k);
+            const int64_t v = incv[t];
             for (uint32_t q = 0; q < cnt; q++) {
                 const uint32_t k2 = L.survop[b0 + q];
                 const uint32_t m2 = L.opmeta[k2], vt2 = (m2 >> 16) & 0xFF;
