@@ -1186,10 +1186,20 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     if (p.counters && __ballot(counter_ops)) {
         bool outside = false;
         // every inc's value load issued before the first is used (they are L2 round trips)
+        // and the base values of surviving integer counter sets (the 2^52 envelope check)
         int64_t incv[OPL];
+        u64 basev[OPL];
 #pragma unroll
-        for (int t = 0; t < OPL; t++)
+        for (int t = 0; t < OPL; t++) {
             incv[t] = (oh[t] >= 0 && oact[t] == HM_INC) ? (int64_t)op_value(p, doc, lane + WAVE * t) : 0;
+            const uint32_t q = lane + WAVE * t;
+            basev[t] = 0;
+            if (q < total) {
+                const uint32_t k = L.survop[q], mt = L.opmeta[k];
+                if ((mt & 0xFF) == HM_SET && ((mt >> 8) & 0xFF) == HM_DT_COUNTER && ((mt >> 16) & 0xFF) == HM_V_INT)
+                    basev[t] = op_value(p, doc, k);
+            }
+        }
 #pragma unroll
         for (int t = 0; t < OPL; t++) {
             if (oh[t] < 0 || oact[t] != HM_INC) continue;
@@ -1208,12 +1218,10 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
                 lds_add((LDS u64 *)&L.survsum[b0 + q], (unsigned long long)v);
             }
         }
-        for (uint32_t q = lane; q < total; q += WAVE) {
-            const uint32_t k = L.survop[q], mt = L.opmeta[k];
-            if ((mt & 0xFF) == HM_SET && ((mt >> 8) & 0xFF) == HM_DT_COUNTER && ((mt >> 16) & 0xFF) == HM_V_INT) {
-                const int64_t b = (int64_t)op_value(p, doc, k);
-                outside |= (u64)(b < 0 ? -b : b) >= (1ull << 52);
-            }
+#pragma unroll
+        for (int t = 0; t < OPL; t++) {                   // (total <= WAVE * OPL)
+            const int64_t b = (int64_t)basev[t];
+            outside |= (u64)(b < 0 ? -b : b) >= (1ull << 52);
         }
         if (__ballot(outside)) return OUT_UNSUPPORTED;
         wave_sync();
