@@ -216,7 +216,25 @@ def main() -> int:
         ge = eng.merge(batch)
         dt = time.perf_counter() - t
         e2e = {"value": float(ge.docs["hist_len"].astype(np.int64).sum()) / dt, "unit": "changes/s",
-               "ms": dt * 1e3, "path": "hm_merge_host (H2D + both kernels + D2H, pageable host buffers)"}
+               "ms": dt * 1e3, "path": "hm_merge_host (H2D + both kernels + D2H, pageable host buffers, "
+                                       "fresh result arrays)",
+               "same_as_device_path": bool(np.array_equal(ge.docs, docs_res))}
+        # the same call on page-locked host tables and result arrays the caller keeps between
+        # batches (a long-running RepoBackend reuses its buffers): DMA at PCIe rate, no first-touch
+        # page faults inside the timed region
+        pb, pr, keep = _pinned_batch(batch, ge)
+        eng.merge(pb, pr)                                    # warm: same sizes, staging reused
+        t = time.perf_counter()
+        eng.merge(pb, pr)
+        dt = time.perf_counter() - t
+        ok = bool(np.array_equal(pr.docs, ge.docs) and np.array_equal(pr.surv, ge.surv))
+        e2e["pinned"] = {"value": float(pr.docs["hist_len"].astype(np.int64).sum()) / dt, "unit": "changes/s",
+                         "ms": dt * 1e3, "h2d_bytes": int(sum(a.nbytes for a in (pb.docs, pb.changes, pb.deps, pb.ops))),
+                         "d2h_bytes": int(sum(a.nbytes for a in (pr.docs, pr.clock, pr.back_clock, pr.heads, pr.hist,
+                                                                 pr.all_deps, pr.regs, pr.surv))),
+                         "same_results": ok,
+                         "path": "hm_merge_host, page-locked (torch pin_memory) host tables and reused result arrays"}
+        del pb, pr, keep
     traffic = None
     if rank == 0 and ws == 1 and not args.no_traffic:
         traffic = _pmc_traffic(args)
@@ -301,6 +319,27 @@ def _subbatch(b, k):
     ch = b.changes[:nc].copy()
     nd = int(ch["dep_off"][-1] + ch["n_deps"][-1]) if nc else 0
     return Batch(docs, ch, b.deps[:nd].copy(), b.ops[:no].copy(), b.a_stride)
+
+
+def _pinned_batch(b, like):
+    """Copies of batch `b` and of results `like` in page-locked host memory (torch pin_memory
+    buffers, returned in `keep` so they outlive the numpy views)."""
+    import dataclasses
+    import torch
+    keep = []
+
+    def pin(a, copy=True):
+        t = torch.zeros(max(a.nbytes, 1), dtype=torch.uint8, pin_memory=True)
+        keep.append(t)
+        v = t.numpy()[:a.nbytes].view(a.dtype).reshape(a.shape)
+        if copy:
+            v[...] = a
+        return v
+
+    pb = dataclasses.replace(b, docs=pin(b.docs), changes=pin(b.changes), deps=pin(b.deps), ops=pin(b.ops),
+                             min_clock=None if b.min_clock is None else pin(b.min_clock))
+    pr = dataclasses.replace(like, **{f.name: pin(getattr(like, f.name), False) for f in dataclasses.fields(like)})
+    return pb, pr, keep
 
 
 def _same(b, g, o) -> bool:

@@ -27,6 +27,7 @@ struct hm_engine {
     size_t dbuf_size = 0;
     void *pool = nullptr;        // merge_large_kernel cursor + scratch pool
     size_t pool_size = 0;
+    hipStream_t h2d = nullptr, d2h = nullptr;   // copy streams of the chunked hm_merge_host pipeline
 };
 
 namespace {
@@ -104,6 +105,22 @@ int launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, hipStream
     return HM_OK;
 }
 
+// hm_merge_host splits a batch into document ranges when its tables are laid out in document
+// order (each doc's changes, deps, ops and registers directly follow the previous doc's, as
+// every encoder here writes them); other layouts, and small batches, go in one piece.
+uint32_t host_chunks(const hm_batch *b) {
+    const uint32_t per = 1u << 17;                 // >= 128k documents per chunk
+    if (b->n_docs < 2 * per || !b->docs || !b->changes || !b->ops) return 1;
+    uint64_t c = 0, p = 0, o = 0, r = 0;
+    for (uint32_t i = 0; i < b->n_docs; i++) {
+        const hm_doc_row &d = b->docs[i];
+        if (d.change_off != c || d.dep_off != p || d.op_off != o || d.reg_off != r) return 1;
+        c += d.n_changes; p += d.n_deps; o += d.n_ops; r += d.n_regs;
+    }
+    if (c != b->n_changes || p != b->n_deps || o != b->n_ops) return 1;
+    return std::min<uint32_t>(8, b->n_docs / per);
+}
+
 int check_batch(hm_engine *e, const hm_batch *b) {
     if (!b || b->a_stride == 0 || b->a_stride > 64) return fail(e, HM_ERR_INVALID, "a_stride must be in [1,64]");
     if (b->n_docs && !b->docs) return fail(e, HM_ERR_INVALID, "docs table missing");
@@ -167,6 +184,8 @@ void hm_engine_destroy(hm_engine *e) {
     if (e->pool) (void)hipFree(e->pool);
     for (auto &ev : e->ev) if (ev) (void)hipEventDestroy(ev);
     if (e->stream) (void)hipStreamDestroy(e->stream);
+    if (e->h2d) (void)hipStreamDestroy(e->h2d);
+    if (e->d2h) (void)hipStreamDestroy(e->d2h);
     delete e;
 }
 
@@ -225,9 +244,6 @@ int hm_merge_host(hm_engine *e, const hm_batch *hb, const hm_results *ho) {
         char *base = (char *)e->dbuf;
         auto P = [&](int i) { return (void *)(base + off[i]); };
         hipStream_t s = e->stream;
-        const void *src[5] = {hb->docs, hb->changes, hb->deps, hb->ops, hb->min_clock};
-        for (int i = 0; i < 5; i++)
-            if (sz[i]) HIPCHK(e, hipMemcpyAsync(P(i), src[i], sz[i], hipMemcpyHostToDevice, s));
         b.docs = (const hm_doc_row *)P(0); b.changes = (const hm_change_row *)P(1);
         b.deps = (const hm_dep_row *)P(2); b.ops = (const hm_op_row *)P(3);
         b.min_clock = hb->min_clock ? (const uint32_t *)P(4) : nullptr;
@@ -235,15 +251,85 @@ int hm_merge_host(hm_engine *e, const hm_batch *hb, const hm_results *ho) {
         d.docs = (hm_doc_result *)P(5); d.clock = (uint32_t *)P(6); d.back_clock = (uint32_t *)P(7);
         d.heads = (uint32_t *)P(8); d.hist = (int32_t *)P(9); d.all_deps = (uint32_t *)P(10);
         d.regs = (hm_reg_result *)P(11); d.surv = (hm_surv_result *)P(12);
-        // the survivor table is only defined on [0, n_surv) per doc: zero it for stable host views
-        if (sz[12]) HIPCHK(e, hipMemsetAsync(P(12), 0, sz[12], s));
-        st = launch_merge(e, &b, &d, s);
-        if (st) return st;
+        const void *src[5] = {hb->docs, hb->changes, hb->deps, hb->ops, hb->min_clock};
         void *dst[8] = {ho->docs, ho->clock, ho->back_clock, ho->heads, ho->hist, ho->all_deps, ho->regs, ho->surv};
-        for (int i = 0; i < 8; i++)
-            if (sz[5 + i] && dst[i]) HIPCHK(e, hipMemcpyAsync(dst[i], P(5 + i), sz[5 + i], hipMemcpyDeviceToHost, s));
-        HIPCHK(e, hipStreamSynchronize(s));
-        return HM_OK;
+        const uint32_t nchunk = host_chunks(hb);
+        if (nchunk <= 1) {
+            for (int i = 0; i < 5; i++)
+                if (sz[i]) HIPCHK(e, hipMemcpyAsync(P(i), src[i], sz[i], hipMemcpyHostToDevice, s));
+            // the survivor table is only defined on [0, n_surv) per doc: zero it for stable host views
+            if (sz[12]) HIPCHK(e, hipMemsetAsync(P(12), 0, sz[12], s));
+            st = launch_merge(e, &b, &d, s);
+            if (st) return st;
+            for (int i = 0; i < 8; i++)
+                if (sz[5 + i] && dst[i]) HIPCHK(e, hipMemcpyAsync(dst[i], P(5 + i), sz[5 + i], hipMemcpyDeviceToHost, s));
+            HIPCHK(e, hipStreamSynchronize(s));
+            return HM_OK;
+        }
+        // Chunked pipeline over document ranges (documents laid out in order, host_chunks):
+        // chunk k's upload (h2d stream) overlaps chunk k-1's merge (engine stream) and chunk
+        // k-2's download (d2h stream), so both PCIe directions run at once.  Each chunk is a
+        // sub-batch whose doc-indexed pointers start at its first document; row offsets inside
+        // the doc rows stay absolute into the full-size device tables.
+        if (!e->h2d) HIPCHK(e, hipStreamCreateWithFlags(&e->h2d, hipStreamNonBlocking));
+        if (!e->d2h) HIPCHK(e, hipStreamCreateWithFlags(&e->d2h, hipStreamNonBlocking));
+        std::vector<hipEvent_t> evs(2 * nchunk, nullptr);
+        int rc = HM_OK;
+        auto cleanup = [&]() {
+            (void)hipStreamSynchronize(e->h2d); (void)hipStreamSynchronize(s); (void)hipStreamSynchronize(e->d2h);
+            for (auto ev : evs) if (ev) (void)hipEventDestroy(ev);
+        };
+        for (auto &ev : evs)
+            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) { cleanup(); return fail(e, HM_ERR_DEVICE, "hipEventCreate"); }
+        const hm_doc_row *hd = hb->docs;
+        const uint32_t nd = b.n_docs;
+        auto H2D = [&](void *dp, const void *hp, size_t bytes) {
+            return bytes ? hipMemcpyAsync(dp, hp, bytes, hipMemcpyHostToDevice, e->h2d) : hipSuccess; };
+        auto D2H = [&](void *hp, const void *dp, size_t bytes) {
+            return (bytes && hp) ? hipMemcpyAsync(hp, dp, bytes, hipMemcpyDeviceToHost, e->d2h) : hipSuccess; };
+#define HM_CK(x) do { hipError_t _r = (x); if (_r != hipSuccess) { rc = hip_fail(e, _r, #x); goto done; } } while (0)
+        for (uint32_t k = 0; k < nchunk; k++) {
+            const uint32_t d0 = (uint32_t)((uint64_t)nd * k / nchunk), d1 = (uint32_t)((uint64_t)nd * (k + 1) / nchunk);
+            const uint32_t l = d1 - 1;
+            const size_t c0 = hd[d0].change_off, c1 = (size_t)hd[l].change_off + hd[l].n_changes;
+            const size_t p0 = hd[d0].dep_off, p1 = (size_t)hd[l].dep_off + hd[l].n_deps;
+            const size_t o0 = hd[d0].op_off, o1 = (size_t)hd[l].op_off + hd[l].n_ops;
+            const size_t r0 = hd[d0].reg_off, r1 = (size_t)hd[l].reg_off + hd[l].n_regs;
+            char *dc = (char *)P(1), *dp = (char *)P(2), *dop = (char *)P(3);
+            HM_CK(H2D((char *)P(0) + d0 * sizeof(hm_doc_row), hd + d0, (size_t)(d1 - d0) * sizeof(hm_doc_row)));
+            HM_CK(H2D(dc + c0 * sizeof(hm_change_row), hb->changes + c0, (c1 - c0) * sizeof(hm_change_row)));
+            HM_CK(H2D(dp + p0 * sizeof(hm_dep_row), hb->deps + p0, (p1 - p0) * sizeof(hm_dep_row)));
+            HM_CK(H2D(dop + o0 * sizeof(hm_op_row), hb->ops + o0, (o1 - o0) * sizeof(hm_op_row)));
+            if (hb->min_clock) HM_CK(H2D((char *)P(4) + d0 * S * 4, hb->min_clock + d0 * S, (d1 - d0) * S * 4));
+            HM_CK(hipEventRecord(evs[2 * k], e->h2d));
+            HM_CK(hipStreamWaitEvent(s, evs[2 * k], 0));
+            HM_CK(hipMemsetAsync((char *)P(12) + o0 * sizeof(hm_surv_result), 0, (o1 - o0) * sizeof(hm_surv_result), s));
+            {
+                hm_batch cb = b;
+                cb.n_docs = d1 - d0;
+                cb.docs = b.docs + d0;
+                cb.min_clock = b.min_clock ? b.min_clock + d0 * S : nullptr;
+                hm_results co = d;
+                co.docs = d.docs + d0; co.clock = d.clock + d0 * S; co.back_clock = d.back_clock + d0 * S;
+                co.heads = d.heads + d0 * S;
+                rc = launch_merge(e, &cb, &co, s);
+                if (rc) goto done;
+            }
+            HM_CK(hipEventRecord(evs[2 * k + 1], s));
+            HM_CK(hipStreamWaitEvent(e->d2h, evs[2 * k + 1], 0));
+            HM_CK(D2H(ho->docs + d0, d.docs + d0, (size_t)(d1 - d0) * sizeof(hm_doc_result)));
+            HM_CK(D2H(ho->clock ? ho->clock + d0 * S : nullptr, d.clock + d0 * S, (d1 - d0) * S * 4));
+            HM_CK(D2H(ho->back_clock ? ho->back_clock + d0 * S : nullptr, d.back_clock + d0 * S, (d1 - d0) * S * 4));
+            HM_CK(D2H(ho->heads ? ho->heads + d0 * S : nullptr, d.heads + d0 * S, (d1 - d0) * S * 4));
+            HM_CK(D2H(ho->hist ? ho->hist + c0 : nullptr, d.hist + c0, (c1 - c0) * 4));
+            HM_CK(D2H(ho->all_deps ? ho->all_deps + c0 * S : nullptr, d.all_deps + c0 * S, (c1 - c0) * S * 4));
+            HM_CK(D2H(ho->regs ? ho->regs + r0 : nullptr, d.regs + r0, (r1 - r0) * sizeof(hm_reg_result)));
+            HM_CK(D2H(ho->surv ? ho->surv + o0 : nullptr, d.surv + o0, (o1 - o0) * sizeof(hm_surv_result)));
+        }
+#undef HM_CK
+    done:
+        cleanup();
+        return rc;
     } catch (...) {
         return fail(e, HM_ERR_DEVICE, "exception in hm_merge_host");
     }

@@ -2,6 +2,7 @@
 (called through the C-ABI).  Documents the engine reports as UNSUPPORTED are
 outside its current envelope (counted, and required to be zero for the
 configs in scope)."""
+import dataclasses
 import numpy as np
 import pytest
 
@@ -220,3 +221,25 @@ def test_queue_orders_on_gpu(engine, engine_general, general, name, changes):
     assert g.docs["status"][0] != 16
     assert_same(b, g, o)
     assert canonical_json(b, g, 0) == canonical_json(b, o, 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,n,extra", [
+    ("C5", 300_000, {}),                                   # mixed documents, some on the general kernel
+    ("C2", 270_000, {"arrival": 2, "shuffle_pct": 25, "dup_pct": 5}),
+])
+def test_chunked_host_pipeline(engine, name, n, extra):
+    """hm_merge_host splits batches of >= 256k in-order documents into document ranges whose
+    uploads, merges and downloads overlap on three streams (engine.cpp host_chunks): every
+    chunk boundary must give the same results as the oracle, and as the same batch merged in
+    one piece (a batch whose doc rows are not in table order is never chunked)."""
+    b = synth.generate(synth.config(name, n_docs=n, **extra))
+    g = engine.merge(b)
+    assert_same(b, g, O.merge(b, threads=16))
+    # the same tables with the last two doc rows swapped: not in table order -> one piece
+    sw = dataclasses.replace(b, docs=b.docs.copy())
+    sw.docs[[-1, -2]] = sw.docs[[-2, -1]]
+    g1 = engine.merge(sw)
+    for f in ("hist", "all_deps", "regs", "surv"):
+        assert np.array_equal(getattr(g, f), getattr(g1, f)), f
+    assert np.array_equal(g.docs[:-2], g1.docs[:-2]) and np.array_equal(g.docs[-2:], g1.docs[-2:][::-1])
