@@ -207,7 +207,11 @@ void hm_engine_destroy(hm_engine *e);
 const char *hm_engine_last_error(const hm_engine *e);
 
 /* Host batch -> device -> merge -> host results (synchronous).  All host
- * buffers are owned by the caller; the engine stages copies. */
+ * buffers are owned by the caller; the engine stages copies.  A batch of
+ * >= 256k documents whose tables are in document order is processed in up to
+ * 8 document ranges with upload, merge and download overlapped on three
+ * streams; page-locked caller buffers (hipHostMalloc / torch pin_memory) let
+ * those copies run at PCIe DMA rate.  Results are identical either way. */
 int hm_merge_host(hm_engine *e, const hm_batch *batch, const hm_results *out);
 
 /* Device-resident merge: every pointer in `batch` and `out` is a device
