@@ -6,6 +6,7 @@
 // library cannot run, calls fail with HM_ERR_DEVICE.
 #include <hip/hip_runtime.h>
 #include <cstring>
+#include <cstdlib>
 #include <string>
 #include <vector>
 #include <algorithm>
@@ -69,6 +70,10 @@ int launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, hipStream
     p.n_docs = b->n_docs; p.a_stride = b->a_stride; p.cap_regs = 0; p.cap_objs = 0; p.cap_deps = 0;
     p.counters = c.counters ? 1u : 0u;
     p.general_only = (e->flags & HM_CFG_GENERAL_ONLY) ? 1u : 0u;
+    {
+        static const int remap = [] { const char *v = getenv("HM_XCD_REMAP"); return v ? atoi(v) : 1; }();
+        p.xcd_remap = remap ? 1u : 0u;
+    }
     p.doc_slot = doc_slot;
     if (b->n_docs == 0) { e->n_last = 0; return HM_OK; }
     // scratch: [counters 256 B: large-kernel cursor, pool bump pointer, deferred count]

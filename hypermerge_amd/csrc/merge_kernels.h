@@ -23,6 +23,7 @@ struct SmallParams {
     uint32_t *n_deferred;            // documents merge_small_kernel handed over (zeroed before the launch)
     uint32_t *deferred;              // [n_docs] their launch rows, in hand-over order
     uint32_t general_only;           // HM_CFG_GENERAL_ONLY: defer every document
+    uint32_t xcd_remap;              // 1: neighbouring documents go to workgroups on one XCD
     const uint32_t *doc_slot;        // optional: launch row d -> row of the per-document outputs
                                      // (res_docs, clocks, heads, min_clock); NULL = identity
 };

@@ -1342,7 +1342,11 @@ void merge_small_kernel(SmallParams p) {
     SmallLds L;
     small_carve((LDS uint8_t *)lds_raw, WAVE * OPL, C::NR, C::NO, C::ND, LISTS, true, &L);
     p.cap_regs = C::NR; p.cap_objs = C::NO; p.cap_deps = C::ND;
+    // workgroups are dealt round-robin over the 8 XCDs (speed only, MI355X_MICROARCH.md): give
+    // the workgroups of one XCD consecutive documents, so the 128 B lines a document boundary
+    // splits in every table are read and written through one L2 instead of two
     uint32_t d = blockIdx.x;
+    if (p.xcd_remap && (gridDim.x & 7) == 0) d = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
     if (d >= p.n_docs) return;
 #if HM_STAMPS
     if (threadIdx.x == 0) { for (int i = 0; i < HM_NSTAMP; i++) L.stamps[i] = 0; L.stamps[HM_NSTAMP] = stamp_now(); }
