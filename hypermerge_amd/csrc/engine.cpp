@@ -114,7 +114,7 @@ int launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, hipStream
 // order (each doc's changes, deps, ops and registers directly follow the previous doc's, as
 // every encoder here writes them); other layouts, and small batches, go in one piece.
 uint32_t host_chunks(const hm_batch *b) {
-    const uint32_t per = 1u << 17;                 // >= 128k documents per chunk
+    const uint32_t per = 1u << 16;                 // >= 64k documents per chunk
     if (b->n_docs < 2 * per || !b->docs || !b->changes || !b->ops) return 1;
     uint64_t c = 0, p = 0, o = 0, r = 0;
     for (uint32_t i = 0; i < b->n_docs; i++) {
@@ -123,7 +123,7 @@ uint32_t host_chunks(const hm_batch *b) {
         c += d.n_changes; p += d.n_deps; o += d.n_ops; r += d.n_regs;
     }
     if (c != b->n_changes || p != b->n_deps || o != b->n_ops) return 1;
-    return std::min<uint32_t>(8, b->n_docs / per);
+    return std::min<uint32_t>(16, b->n_docs / per);
 }
 
 int check_batch(hm_engine *e, const hm_batch *b) {

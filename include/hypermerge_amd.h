@@ -208,8 +208,8 @@ const char *hm_engine_last_error(const hm_engine *e);
 
 /* Host batch -> device -> merge -> host results (synchronous).  All host
  * buffers are owned by the caller; the engine stages copies.  A batch of
- * >= 256k documents whose tables are in document order is processed in up to
- * 8 document ranges with upload, merge and download overlapped on three
+ * >= 128k documents whose tables are in document order is processed in up to
+ * 16 document ranges with upload, merge and download overlapped on three
  * streams; page-locked caller buffers (hipHostMalloc / torch pin_memory) let
  * those copies run at PCIe DMA rate.  Results are identical either way. */
 int hm_merge_host(hm_engine *e, const hm_batch *batch, const hm_results *out);

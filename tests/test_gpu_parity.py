@@ -229,7 +229,7 @@ def test_queue_orders_on_gpu(engine, engine_general, general, name, changes):
     ("C2", 270_000, {"arrival": 2, "shuffle_pct": 25, "dup_pct": 5}),
 ])
 def test_chunked_host_pipeline(engine, name, n, extra):
-    """hm_merge_host splits batches of >= 256k in-order documents into document ranges whose
+    """hm_merge_host splits batches of >= 128k in-order documents into document ranges whose
     uploads, merges and downloads overlap on three streams (engine.cpp host_chunks): every
     chunk boundary must give the same results as the oracle, and as the same batch merged in
     one piece (a batch whose doc rows are not in table order is never chunked)."""
