@@ -56,6 +56,7 @@ def main() -> int:
     ap.add_argument("--check-docs", type=int, default=20_000, help="docs checked against the oracle")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host->device->host (PCIe-inclusive) leg")
+    ap.add_argument("--no-orders", action="store_true", help="skip the C4 actor-major (loadDocument order) leg")
     ap.add_argument("--arrival", type=int, default=None,
                     help="override the config's arrival order (0 generation, 1 actor-major as RepoBackend.loadDocument "
                          "concatenates, 2 shuffled)")
@@ -71,7 +72,6 @@ def main() -> int:
     torch.cuda.set_device(dev)
 
     from hypermerge_amd import synth
-    from hypermerge_amd.columnar import CBatch, CResults, Results
     from hypermerge_amd.engine import Engine
 
     t0 = time.time()
@@ -81,39 +81,11 @@ def main() -> int:
     gen_s = time.time() - t0
 
     eng = Engine(local)
-
-    def to_dev(a: np.ndarray) -> torch.Tensor:
-        t = torch.from_numpy(a.view(np.uint8).reshape(-1)).to(dev)
-        return t
-
-    S = batch.a_stride
-    nd, nc, no = batch.n_docs, len(batch.changes), len(batch.ops)
-    nr = int(batch.docs["n_regs"].sum())
-    d_docs, d_ch, d_dp, d_op = (to_dev(x) for x in (batch.docs, batch.changes, batch.deps, batch.ops))
-    u8 = dict(dtype=torch.uint8, device=dev)
-    r_docs = torch.zeros(nd * 32, **u8)   # hm_doc_result rows
-    r_clock = torch.zeros(nd * S, dtype=torch.int32, device=dev)
-    r_bclock = torch.zeros(nd * S, dtype=torch.int32, device=dev)
-    r_heads = torch.zeros(nd * S, dtype=torch.int32, device=dev)
-    r_hist = torch.zeros(nc, dtype=torch.int32, device=dev)
-    r_ad = torch.zeros(nc * S, dtype=torch.int32, device=dev)
-    r_regs = torch.zeros(nr * 16, **u8)
-    r_surv = torch.zeros(no * 16, **u8)
-    hc = batch.c_struct()
-    cb = CBatch(hc.n_docs, hc.n_changes, hc.n_deps, hc.n_ops, hc.n_regs, hc.a_stride,
-                hc.max_changes, hc.max_ops, hc.max_regs, hc.max_objs, hc.doc_flags, hc.max_deps,
-                d_docs.data_ptr(), d_ch.data_ptr(), d_dp.data_ptr(), d_op.data_ptr(), None)
-    cr = CResults(r_docs.data_ptr(), r_clock.data_ptr(), r_bclock.data_ptr(), r_heads.data_ptr(),
-                  r_hist.data_ptr(), r_ad.data_ptr(), r_regs.data_ptr(), r_surv.data_ptr())
     stream = torch.cuda.Stream(dev)          # a real stream: the C-ABI treats handle 0 as "engine stream"
     torch.cuda.set_stream(stream)
-    sptr = stream.cuda_stream
-
-    def step():
-        eng.merge_device(cb, cr, sptr)
-
+    run = _Resident(eng, batch, dev, stream)
     for _ in range(args.warmup):
-        step()
+        run.step()
     torch.cuda.synchronize(dev)
     if ws > 1:
         dist.barrier()
@@ -122,7 +94,7 @@ def main() -> int:
     t_start = time.perf_counter()
     ev0.record(stream)
     for _ in range(args.steps):
-        step()
+        run.step()
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     if ws > 1:
@@ -130,16 +102,10 @@ def main() -> int:
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t_start
     ev_ms = ev0.elapsed_time(ev1)
-    # per-launch kernel duration: HIP events on the launch stream, one extra timed launch
-    klist = []
-    for _ in range(max(3, min(args.steps, 10))):
-        step()
-        klist.append(eng.last_kernel_ms()[0])
-    kern_ms = float(np.mean(klist))
-
-    # pull results back once for counting + spot parity
-    from hypermerge_amd.columnar import DOC_RESULT_DT
-    docs_res = r_docs.cpu().numpy().view(DOC_RESULT_DT)
+    # per-launch kernel durations (both kernels): HIP events on the launch stream, extra launches
+    kern = run.kernel_roofline(max(3, min(args.steps, 10)))
+    nd, nc, no, S = batch.n_docs, len(batch.changes), len(batch.ops), batch.a_stride
+    docs_res = run.docs_res
     applied = int(docs_res["hist_len"].astype(np.int64).sum())
     unsupported = int((docs_res["status"] == 16).sum())
     errors = int(((docs_res["status"] != 0) & (docs_res["status"] != 16)).sum())
@@ -154,32 +120,14 @@ def main() -> int:
         applied_all, wall_max = float(applied), wall
 
     # ClockStore feed across the node (off the merge's critical path, timed separately):
-    # every rank's changed DocBackend.clock rows gathered over RCCL (hypermerge_amd/exchange.py)
+    # every rank's changed DocBackend.clock rows, keyed by (docId hash, actorId hash), gathered
+    # over RCCL through the C-ABI (hm_clock_allgather), plus the replica min-clock
     xchg = None
     if ws > 1:
-        from hypermerge_amd import exchange as X
-        keys = torch.from_numpy((batch.docs["reserved"][:, 0].astype(np.int64)
-                                 | (batch.docs["reserved"][:, 1].astype(np.int64) << 32))).to(dev)
-        newc = r_bclock.view(nd, S)
-        zero = torch.zeros_like(newc)
-        times = []
-        for it in range(4):
-            torch.cuda.synchronize(dev)
-            dist.barrier()
-            t = time.perf_counter()
-            rows = X.changed_rows(keys, newc, zero)
-            allrows = X.gather_clock_rows(rows)
-            torch.cuda.synchronize(dev)
-            times.append(time.perf_counter() - t)
-        xchg = {"clock_rows_gathered": int(allrows.shape[0]), "ms": 1000.0 * float(np.median(times[1:])),
-                "collective": "all_gather (RCCL)"}
+        xchg = _clock_exchange(eng, batch, run, dev, rank, ws, cfg)
 
     value = applied_all * args.steps / wall_max
     ms_per_step = wall_max * 1000.0 / args.steps
-    # roofline of the dominant kernel (merge_small_kernel): algorithmic bytes per launch
-    full = Results(docs_res, None, None, None, None, None, None, None)
-    alg_bytes = batch.algorithmic_bytes(full)
-    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
 
     # spot parity against the oracle on a sample (checker only; not timed)
     parity = None
@@ -235,9 +183,35 @@ def main() -> int:
                          "same_results": ok,
                          "path": "hm_merge_host, page-locked (torch pin_memory) host tables and reused result arrays"}
         del pb, pr, keep
+    # the same workload in RepoBackend.loadDocument's arrival order (actor-major concatenation,
+    # src/RepoBackend.ts:242-248): changes whose deps come later in the array wait in the queue
+    orders = None
+    if rank == 0 and ws == 1 and args.arrival is None and args.config == "C4" and not args.no_orders:
+        del run
+        torch.cuda.empty_cache()
+        cfg_am = synth.config(args.config, n_docs=args.docs, shard=rank, n_shards=ws, arrival=1)
+        b_am = synth.generate(cfg_am, threads=min(16, os.cpu_count() or 1))
+        r_am = _Resident(eng, b_am, dev, stream)
+        for _ in range(2):
+            r_am.step()
+        torch.cuda.synchronize(dev)
+        k_am = max(3, args.steps // 2)
+        t = time.perf_counter()
+        for _ in range(k_am):
+            r_am.step()
+        torch.cuda.synchronize(dev)
+        dt = (time.perf_counter() - t) / k_am
+        kr = r_am.kernel_roofline(3)
+        ap = int(r_am.docs_res["hist_len"].astype(np.int64).sum())
+        orders = {"actor_major": {"value": ap / dt, "unit": "changes/s", "ms_per_step": dt * 1e3,
+                                  "roofline_frac": kr["frac"], "kernel": kr["kernel"],
+                                  "unsupported_docs": int((r_am.docs_res["status"] == 16).sum()),
+                                  "order": "RepoBackend.loadDocument (actor-major, src/RepoBackend.ts:242-248)"},
+                  "generation": {"value": value, "order": "generation (every change ready on arrival)"}}
+        del r_am, b_am
     traffic = None
     if rank == 0 and ws == 1 and not args.no_traffic:
-        traffic = _pmc_traffic(args)
+        traffic = _pmc_traffic(args, kern["kernel"])
 
     if rank == 0:
         line = {
@@ -249,11 +223,12 @@ def main() -> int:
                                    f"{nc / max(nd, 1):.0f} changes/doc, {WORKLOAD_KIND.get(args.config, '')}"
                                    + ("" if args.arrival is None else f", arrival order {ARRIVAL[args.arrival]}"), "docs_per_gpu": nd,
                        "changes_per_gpu": nc, "ops_per_gpu": no, "parallelism": f"doc-shard{ws}"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": achieved / PEAK_HBM_GBS, "traffic": traffic["bytes"] if traffic else None,
-                         "kernel": "merge_small_kernel", "kernel_ms": kern_ms, "alg_bytes": alg_bytes,
-                         "traffic_detail": traffic},
-            "cpu_baseline": cpu, "cpu_parallel": cpu_mt, "end_to_end": e2e,
+            "roofline": {"bound": "hbm", "achieved": kern["achieved"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": kern["frac"], "traffic": traffic["bytes"] if traffic else None,
+                         "kernel": kern["kernel"], "kernel_ms": kern["kernel_ms"], "alg_bytes": kern["alg_bytes"],
+                         "kernels": kern["kernels"], "traffic_detail": traffic},
+            "cpu_baseline": cpu, "cpu_parallel": cpu_mt, "end_to_end": e2e, "arrival_orders": orders,
+            "host": _host_info(),
             "parity_sample_ok": parity, "unsupported_docs": unsupported, "error_docs": errors,
             "gen_s": round(gen_s, 2), "event_ms_per_step": ev_ms / args.steps,
             "clock_exchange": xchg,
@@ -264,8 +239,138 @@ def main() -> int:
     return 0
 
 
-def _pmc_traffic(args):
-    """HBM bytes per launch of merge_small_kernel, from two rocprofv3 PMC passes over a short
+def _clock_exchange(eng, batch, run, dev, rank, ws, cfg):
+    """The ClockStore feed across the node, through the C-ABI over RCCL (exchange.hip): every
+    rank's DocBackend.clock rows -> repo-global records (hm_clock_records_device) -> every
+    rank's records on every rank (hm_clock_count_allgather + hm_clock_allgather) -> the
+    min-clock over the gathered key universe (hm_clock_min_allreduce).  Under docId sharding
+    every (doc, actor) record is unique, so the universe is the gathered list itself (the
+    host-side alignment of replicated documents is exchange.align, tested over gloo).
+    Timed separately from the merge (off its critical path)."""
+    import torch
+    import torch.distributed as dist
+    from hypermerge_amd import exchange as X
+    from hypermerge_amd import synth
+    idt = torch.zeros(128, dtype=torch.uint8, device=dev)
+    if rank == 0:
+        idt.copy_(torch.tensor(list(X.RcclTransport.unique_id(eng)), dtype=torch.uint8, device=dev))
+    dist.broadcast(idt, 0)
+    tr = X.RcclTransport(eng, ws, rank, bytes(idt.cpu().numpy().tolist()))
+    dk, ak = synth.keys(cfg, batch)
+    d_dk = torch.from_numpy(dk.view(np.int64)).to(dev)
+    d_ak = torch.from_numpy(ak.view(np.int64)).to(dev)
+    times, ok = [], True
+    for it in range(4):
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t = time.perf_counter()
+        recs = tr.records_device(d_dk, d_ak, run.r_bclock)
+        allr, counts = tr.gather_device(recs)
+        total = sum(counts)
+        off = sum(counts[:rank])
+        seq = torch.full((total,), -1, dtype=torch.int32, device=dev)       # HM_CLOCK_NOT_HELD
+        own = recs.view(torch.int32).view(-1, 6)[:, 4]
+        seq[off:off + own.numel()] = own
+        tr.min_allreduce_device(seq)
+        torch.cuda.synchronize(dev)
+        times.append(time.perf_counter() - t)
+        if it == 0:      # single holder per document: the min-clock is every document's own clock
+            ok = bool(torch.equal(seq, allr.view(torch.int32).view(-1, 6)[:, 4]))
+    tr.close()
+    return {"records_gathered": int(total), "record_bytes": 24, "ms": 1000.0 * float(np.median(times[1:])),
+            "min_clock_ok": ok, "collectives": "hm_clock_count_allgather + hm_clock_allgather (grouped "
+            "ncclBroadcast, exact counts) + hm_clock_min_allreduce (ncclAllReduce MIN), RCCL via the C-ABI"}
+
+
+class _Resident:
+    """A batch resident in HBM with its result tensors: one step = one hm_merge_device launch
+    pair (merge_small_kernel + merge_large_kernel) over every document, on ``stream``."""
+
+    def __init__(self, eng, batch, dev, stream):
+        import torch
+        from hypermerge_amd.columnar import CBatch, CResults
+        self.eng, self.batch, self.stream = eng, batch, stream
+        S = batch.a_stride
+        nd, nc, no = batch.n_docs, len(batch.changes), len(batch.ops)
+        nr = int(batch.docs["n_regs"].sum())
+
+        def to_dev(a):
+            return torch.from_numpy(a.view(np.uint8).reshape(-1)).to(dev)
+        u8 = dict(dtype=torch.uint8, device=dev)
+        self.t = [to_dev(x) for x in (batch.docs, batch.changes, batch.deps, batch.ops)]
+        self.r_docs = torch.zeros(nd * 32, **u8)
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.r_clock, self.r_bclock, self.r_heads = (torch.zeros(nd * S, **i32) for _ in range(3))
+        self.r_hist = torch.zeros(nc, **i32)
+        self.r_ad = torch.zeros(nc * S, **i32)
+        self.r_regs = torch.zeros(nr * 16, **u8)
+        self.r_surv = torch.zeros(no * 16, **u8)
+        hc = batch.c_struct()
+        d_docs, d_ch, d_dp, d_op = self.t
+        self.cb = CBatch(hc.n_docs, hc.n_changes, hc.n_deps, hc.n_ops, hc.n_regs, hc.a_stride,
+                         hc.max_changes, hc.max_ops, hc.max_regs, hc.max_objs, hc.doc_flags, hc.max_deps,
+                         d_docs.data_ptr(), d_ch.data_ptr(), d_dp.data_ptr(), d_op.data_ptr(), None)
+        self.cr = CResults(self.r_docs.data_ptr(), self.r_clock.data_ptr(), self.r_bclock.data_ptr(),
+                           self.r_heads.data_ptr(), self.r_hist.data_ptr(), self.r_ad.data_ptr(),
+                           self.r_regs.data_ptr(), self.r_surv.data_ptr())
+        self._docs_res = None
+
+    def step(self):
+        self.eng.merge_device(self.cb, self.cr, self.stream.cuda_stream)
+
+    @property
+    def docs_res(self):
+        from hypermerge_amd.columnar import DOC_RESULT_DT
+        if self._docs_res is None:
+            self._docs_res = self.r_docs.cpu().numpy().view(DOC_RESULT_DT)
+        return self._docs_res
+
+    def kernel_roofline(self, launches):
+        """Both kernels' average launch durations (HIP events on the launch stream), each
+        kernel's algorithmic bytes (the documents it merged: merge_large_kernel takes the ones
+        merge_small_kernel handed over, hm_last_deferred), and the roofline of the kernel that
+        dominates the step."""
+        from hypermerge_amd.columnar import DOC_RESULT_DT, REG_RESULT_DT, Results
+        ms = []
+        for _ in range(launches):
+            self.step()
+            ms.append(self.eng.last_kernel_ms())
+        ms = np.mean(np.array(ms, dtype=np.float64), axis=0)
+        deferred = self.eng.last_deferred(self.batch.n_docs)
+        self._docs_res = None
+        res = Results(self.docs_res, None, None, None, None, None,
+                      self.r_regs.cpu().numpy().view(REG_RESULT_DT), None)
+        per_doc = self.batch.doc_algorithmic_bytes(res)
+        large_b = int(per_doc[deferred].sum()) if len(deferred) else 0
+        small_b = int(per_doc.sum()) - large_b
+        ks = [{"kernel": "merge_small_kernel", "ms": float(ms[0]), "alg_bytes": small_b,
+               "docs": int(self.batch.n_docs - len(deferred))},
+              {"kernel": "merge_large_kernel", "ms": float(ms[1]), "alg_bytes": large_b, "docs": int(len(deferred))}]
+        for k in ks:
+            k["frac"] = k["alg_bytes"] / (k["ms"] * 1e-3) / (PEAK_HBM_GBS * 1e9) if k["ms"] > 0 else 0.0
+        dom = max(ks, key=lambda k: k["ms"])
+        achieved = dom["alg_bytes"] / (dom["ms"] * 1e-3) / 1e9
+        assert achieved / PEAK_HBM_GBS <= 1.0, f"roofline fraction above 1: {ks}"
+        return {"kernel": dom["kernel"], "kernel_ms": dom["ms"], "alg_bytes": dom["alg_bytes"],
+                "achieved": achieved, "frac": achieved / PEAK_HBM_GBS, "kernels": ks}
+
+
+def _host_info():
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "cpu_model": model,
+            "cpu_share_used": min(16, os.cpu_count() or 1)}
+
+
+def _pmc_traffic(args, kernel="merge_small_kernel"):
+    """HBM bytes per launch of the dominant kernel, from two rocprofv3 PMC passes over a short
     run of this same workload (separate passes: FETCH_SIZE and WRITE_SIZE do not fit one pass's
     TCC counters).  Corrected as /opt/skills/guides/MI355X_MICROARCH.md §HBM prescribes: on gfx950
     FETCH_SIZE (KiB) counts half the bytes of wide streaming reads, WRITE_SIZE counts them exactly.
@@ -284,7 +389,7 @@ def _pmc_traffic(args):
         d = tempfile.mkdtemp(prefix="hm_pmc_", dir="/tmp")
         cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "run", "--",
                sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1", "--no-cpu",
-               "--no-traffic", "--no-e2e", "--docs", str(args.docs), "--config", args.config] + ([] if args.arrival is None else ["--arrival", str(args.arrival)])
+               "--no-traffic", "--no-e2e", "--no-orders", "--docs", str(args.docs), "--config", args.config] + ([] if args.arrival is None else ["--arrival", str(args.arrival)])
         pr = subprocess.Popen(cmd, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), stdout=subprocess.DEVNULL,
                               stderr=subprocess.DEVNULL, start_new_session=True)
         try:
@@ -298,7 +403,7 @@ def _pmc_traffic(args):
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             with open(f) as fh:
                 for row in csv.DictReader(fh):
-                    if "merge_small_kernel" in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
+                    if kernel in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
                         got.append(float(row["Counter_Value"]))
         shutil.rmtree(d, ignore_errors=True)
         if not got:

@@ -13,7 +13,7 @@ CSRC = os.path.join(HERE, "csrc")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("HM_OFFLOAD_ARCH", "gfx950")
 
-GPU_SRCS = ["merge_kernels.hip", "merge_large.hip", "store_kernels.hip", "engine.cpp", "store.cpp"]
+GPU_SRCS = ["merge_kernels.hip", "merge_large.hip", "store_kernels.hip", "exchange.hip", "engine.cpp", "store.cpp"]
 GPU_DEPS = GPU_SRCS + ["merge_kernels.h", "store_kernels.h", "engine_internal.h", "../../include/hypermerge_amd.h"]
 
 
@@ -44,7 +44,7 @@ def build_gpu(force: bool = False) -> str:
         with ThreadPoolExecutor(min(8, len(GPU_SRCS))) as ex:
             list(ex.map(lambda so: _run([HIPCC] + flags + ["-c", "-o", so[1], os.path.join(CSRC, so[0])]),
                         zip(GPU_SRCS, objs)))
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs)
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs + ["-ldl"])
     return out
 
 

@@ -146,16 +146,25 @@ class Batch:
                       self.docs.ctypes.data, self.changes.ctypes.data, self.deps.ctypes.data,
                       self.ops.ctypes.data, mc)
 
-    def algorithmic_bytes(self, results: Optional["Results"] = None) -> int:
-        """B = Σ_changes(24 + 8·nDeps + 4·A) + Σ_ops 32 + Σ_docs 8·A
-        + Σ_segments 16 + Σ_conflicts 16 (A = the batch's per-actor row stride)."""
+    def doc_algorithmic_bytes(self, results: Optional["Results"] = None) -> np.ndarray:
+        """Per document, SURVEY.md §8(d): Σ_changes(24 + 8·nDeps + 4·A) + Σ_ops 32 + 8·A
+        + Σ_segments 16 + Σ_conflicts 16 (A = the batch's per-actor row stride; a segment is
+        a register, its winner or element order written once; conflicts = survivors beyond
+        each register's winner, so they need ``results.regs``)."""
         A = self.a_stride
-        b = len(self.changes) * (24 + 4 * A) + 8 * len(self.deps) + 32 * len(self.ops)
-        b += len(self.docs) * 8 * A + 16 * int(self.docs["n_regs"].sum())
-        if results is not None:
-            b += 16 * int(results.docs["n_surv"].sum())
-        return int(b)
+        d = self.docs
+        b = (d["n_changes"].astype(np.int64) * (24 + 4 * A) + 8 * d["n_deps"].astype(np.int64)
+             + 32 * d["n_ops"].astype(np.int64) + 8 * A + 16 * d["n_regs"].astype(np.int64))
+        if results is not None and results.regs is not None and len(d):
+            live = np.concatenate([[0], np.cumsum(results.regs["n_surv"] > 0, dtype=np.int64)])
+            lo = d["reg_off"].astype(np.int64)
+            hi = lo + d["n_regs"].astype(np.int64)
+            winners = live[hi] - live[lo]
+            b += 16 * (results.docs["n_surv"].astype(np.int64) - winners)
+        return b
 
+    def algorithmic_bytes(self, results: Optional["Results"] = None) -> int:
+        return int(self.doc_algorithmic_bytes(results).sum())
 
 @dataclass
 class Results:

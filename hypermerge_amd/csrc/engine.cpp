@@ -29,6 +29,7 @@ struct hm_engine {
     void *pool = nullptr;        // merge_large_kernel cursor + scratch pool
     size_t pool_size = 0;
     hipStream_t h2d = nullptr, d2h = nullptr;   // copy streams of the chunked hm_merge_host pipeline
+    const char *last_scratch = nullptr;         // scratch of the last launch (hm_last_deferred)
 };
 
 namespace {
@@ -61,7 +62,13 @@ Caps launch_caps(const hm_batch *b) {
     return c;
 }
 
-int launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, hipStream_t s, const uint32_t *doc_slot = nullptr) {
+// The launch's scratch: [counters 256 B: large-kernel cursor, pool bump pointer, deferred
+// count][deferred document list, n_docs u32][large-kernel pool].  `scratch` = caller memory of
+// hm_launch_scratch_bytes(b) bytes, or NULL for the engine's own pool (calls on the engine pool
+// must be serialised: one stream at a time, which the engine enforces by synchronising the
+// device before the pool is resized).
+int launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, hipStream_t s, const uint32_t *doc_slot,
+                 const hm_extents *ext, void *scratch) {
     Caps c = launch_caps(b);
     SmallParams p;
     p.docs = b->docs; p.changes = b->changes; p.deps = b->deps; p.ops = b->ops; p.min_clock = b->min_clock;
@@ -75,19 +82,22 @@ int launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, hipStream
         p.xcd_remap = remap ? 1u : 0u;
     }
     p.doc_slot = doc_slot;
+    p.lim_changes = ext ? ext->n_changes : b->n_changes; p.lim_deps = ext ? ext->n_deps : b->n_deps;
+    p.lim_ops = ext ? ext->n_ops : b->n_ops; p.lim_regs = ext ? ext->n_regs : b->n_regs;
     if (b->n_docs == 0) { e->n_last = 0; return HM_OK; }
-    // scratch: [counters 256 B: large-kernel cursor, pool bump pointer, deferred count]
-    //          [deferred document list, n_docs u32][large-kernel pool]
-    const size_t pool_bytes = hm_large_scratch_bound(b);
     const size_t list_bytes = ((size_t)b->n_docs * 4 + 255) & ~(size_t)255;
-    const size_t need = 256 + list_bytes + pool_bytes;
-    if (need > e->pool_size) {
-        if (e->pool) { HIPCHK(e, hipStreamSynchronize(s)); HIPCHK(e, hipFree(e->pool)); }
-        e->pool = nullptr; e->pool_size = 0;
-        if (hipMalloc(&e->pool, need) != hipSuccess) return fail(e, HM_ERR_NOMEM, "hipMalloc scratch pool");
-        e->pool_size = need;
+    const size_t need = hm_launch_scratch_bytes(b);
+    const size_t pool_bytes = need - 256 - list_bytes;
+    char *pb = (char *)scratch;
+    if (!pb) {
+        if (need > e->pool_size) {
+            if (e->pool) { HIPCHK(e, hipDeviceSynchronize()); HIPCHK(e, hipFree(e->pool)); }
+            e->pool = nullptr; e->pool_size = 0;
+            if (hipMalloc(&e->pool, need) != hipSuccess) return fail(e, HM_ERR_NOMEM, "hipMalloc scratch pool");
+            e->pool_size = need;
+        }
+        pb = (char *)e->pool;
     }
-    char *pb = (char *)e->pool;
     p.large_cursor = (uint32_t *)pb;
     unsigned long long *pool_used = (unsigned long long *)(pb + 8);
     p.n_deferred = (uint32_t *)(pb + 16);
@@ -107,8 +117,18 @@ int launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, hipStream
     if (r != hipSuccess) return hip_fail(e, r, "merge_large_kernel launch");
     HIPCHK(e, hipEventRecord(e->ev[3], s));
     e->n_last = 2;
+    e->last_scratch = pb;
     return HM_OK;
 }
+
+}  // namespace
+
+size_t hm_launch_scratch_bytes(const hm_batch *b) {
+    const size_t list_bytes = ((size_t)b->n_docs * 4 + 255) & ~(size_t)255;
+    return 256 + list_bytes + hm_large_scratch_bound(b);
+}
+
+namespace {
 
 // hm_merge_host splits a batch into document ranges when its tables are laid out in document
 // order (each doc's changes, deps, ops and registers directly follow the previous doc's, as
@@ -129,14 +149,17 @@ uint32_t host_chunks(const hm_batch *b) {
 int check_batch(hm_engine *e, const hm_batch *b) {
     if (!b || b->a_stride == 0 || b->a_stride > 64) return fail(e, HM_ERR_INVALID, "a_stride must be in [1,64]");
     if (b->n_docs && !b->docs) return fail(e, HM_ERR_INVALID, "docs table missing");
+    if ((b->n_changes && !b->changes) || (b->n_deps && !b->deps) || (b->n_ops && !b->ops))
+        return fail(e, HM_ERR_INVALID, "row table missing");
     return HM_OK;
 }
 
 }  // namespace
 
 // ---- internal interface for store.cpp (engine_internal.h) ----
-int hm_engine_launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, const uint32_t *doc_slot) {
-    return launch_merge(e, b, o, e->stream, doc_slot);
+int hm_engine_launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, const uint32_t *doc_slot,
+                           const hm_extents *ext) {
+    return launch_merge(e, b, o, e->stream, doc_slot, ext, nullptr);
 }
 hipStream_t hm_engine_stream(hm_engine *e) { return e->stream; }
 int hm_engine_device(hm_engine *e) { return e->device; }
@@ -196,10 +219,9 @@ void hm_engine_destroy(hm_engine *e) {
 
 const char *hm_engine_last_error(const hm_engine *e) { return e ? e->err.c_str() : "no engine"; }
 
-size_t hm_scratch_bytes(const hm_batch *) { return 0; }
+size_t hm_scratch_bytes(const hm_batch *b) { return b ? hm_launch_scratch_bytes(b) : 0; }
 
 int hm_merge_device(hm_engine *e, const hm_batch *b, const hm_results *o, void *scratch, void *stream) {
-    (void)scratch;
     try {
         if (!e || !o) return HM_ERR_INVALID;
         int st = check_batch(e, b);
@@ -207,7 +229,7 @@ int hm_merge_device(hm_engine *e, const hm_batch *b, const hm_results *o, void *
         if (b->n_docs && (!b->max_changes && !b->max_ops && !b->max_regs && !b->max_objs))
             return fail(e, HM_ERR_INVALID, "device batches must carry max_* launch hints");
         HIPCHK(e, hipSetDevice(e->device));
-        return launch_merge(e, b, o, stream ? (hipStream_t)stream : e->stream);
+        return launch_merge(e, b, o, stream ? (hipStream_t)stream : e->stream, nullptr, nullptr, scratch);
     } catch (...) {
         return fail(e, HM_ERR_DEVICE, "exception in hm_merge_device");
     }
@@ -264,7 +286,7 @@ int hm_merge_host(hm_engine *e, const hm_batch *hb, const hm_results *ho) {
                 if (sz[i]) HIPCHK(e, hipMemcpyAsync(P(i), src[i], sz[i], hipMemcpyHostToDevice, s));
             // the survivor table is only defined on [0, n_surv) per doc: zero it for stable host views
             if (sz[12]) HIPCHK(e, hipMemsetAsync(P(12), 0, sz[12], s));
-            st = launch_merge(e, &b, &d, s);
+            st = launch_merge(e, &b, &d, s, nullptr, nullptr, nullptr);
             if (st) return st;
             for (int i = 0; i < 8; i++)
                 if (sz[5 + i] && dst[i]) HIPCHK(e, hipMemcpyAsync(dst[i], P(5 + i), sz[5 + i], hipMemcpyDeviceToHost, s));
@@ -317,12 +339,12 @@ int hm_merge_host(hm_engine *e, const hm_batch *hb, const hm_results *ho) {
                 hm_results co = d;
                 co.docs = d.docs + d0; co.clock = d.clock + d0 * S; co.back_clock = d.back_clock + d0 * S;
                 co.heads = d.heads + d0 * S;
-                rc = launch_merge(e, &cb, &co, s);
+                rc = launch_merge(e, &cb, &co, s, nullptr, nullptr, nullptr);
                 if (rc) goto done;
             }
             HM_CK(hipEventRecord(evs[2 * k + 1], s));
             HM_CK(hipStreamWaitEvent(e->d2h, evs[2 * k + 1], 0));
-            HM_CK(D2H(ho->docs + d0, d.docs + d0, (size_t)(d1 - d0) * sizeof(hm_doc_result)));
+            HM_CK(D2H(ho->docs ? ho->docs + d0 : nullptr, d.docs + d0, (size_t)(d1 - d0) * sizeof(hm_doc_result)));
             HM_CK(D2H(ho->clock ? ho->clock + d0 * S : nullptr, d.clock + d0 * S, (d1 - d0) * S * 4));
             HM_CK(D2H(ho->back_clock ? ho->back_clock + d0 * S : nullptr, d.back_clock + d0 * S, (d1 - d0) * S * 4));
             HM_CK(D2H(ho->heads ? ho->heads + d0 * S : nullptr, d.heads + d0 * S, (d1 - d0) * S * 4));
@@ -348,6 +370,18 @@ int hm_last_kernel_ms(hm_engine *e, float *ms, int max_kernels) {
         if (hipEventElapsedTime(&ms[i], e->ev[2 * i], e->ev[2 * i + 1]) != hipSuccess) return 0;
     }
     return n;
+}
+
+int hm_last_deferred(hm_engine *e, uint32_t *out_docs, uint32_t cap) {
+    if (!e) return -HM_ERR_INVALID;
+    if (!e->last_scratch || e->n_last < 2) return 0;
+    if (hipEventSynchronize(e->ev[3]) != hipSuccess) return -HM_ERR_DEVICE;
+    uint32_t n = 0;
+    if (hipMemcpy(&n, e->last_scratch + 16, 4, hipMemcpyDeviceToHost) != hipSuccess) return -HM_ERR_DEVICE;
+    const uint32_t k = std::min(n, cap);
+    if (k && out_docs && hipMemcpy(out_docs, e->last_scratch + 256, (size_t)k * 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return -HM_ERR_DEVICE;
+    return (int)n;
 }
 
 int hm_clock_cmp_device(hm_engine *e, const uint32_t *a, const uint32_t *b, uint8_t *out, uint32_t n_docs,

@@ -26,13 +26,27 @@ struct SmallParams {
     uint32_t xcd_remap;              // 1: neighbouring documents go to workgroups on one XCD
     const uint32_t *doc_slot;        // optional: launch row d -> row of the per-document outputs
                                      // (res_docs, clocks, heads, min_clock); NULL = identity
+    // extents of the row tables: a document row whose ranges leave them (or whose n_actors
+    // exceeds a_stride) is reported HM_ERR_INVALID and never read through
+    uint32_t lim_changes, lim_deps, lim_ops, lim_regs;
 };
+#ifdef __HIPCC__
+__device__ __forceinline__ bool hm_doc_row_ok(const SmallParams &p, const hm_doc_row &d) {
+    return (unsigned long long)d.change_off + d.n_changes <= p.lim_changes &&
+           (unsigned long long)d.dep_off + d.n_deps <= p.lim_deps &&
+           (unsigned long long)d.op_off + d.n_ops <= p.lim_ops &&
+           (unsigned long long)d.reg_off + d.n_regs <= p.lim_regs && d.n_actors <= p.a_stride;
+}
+#endif
 #ifdef __HIPCC__
 __device__ __forceinline__ uint32_t hm_slot(const SmallParams &p, uint32_t d) { return p.doc_slot ? p.doc_slot[d] : d; }
 #endif
 
 // internal: the small kernel hands a document to merge_large_kernel (never returned to callers)
 #define HM_DEFERRED 0x7FFFFFFF
+
+// bytes of device scratch a launch over `b` uses: [256 B counters][deferred list][large-kernel pool]
+size_t hm_launch_scratch_bytes(const hm_batch *b);
 
 size_t hm_large_scratch_bound(const hm_batch *b);
 hipError_t hm_launch_large(const SmallParams &p, void *pool, size_t pool_bytes, unsigned long long *pool_used,

@@ -45,9 +45,6 @@
 #define HM_STAMPS 0     // diagnostic builds only: per-phase s_memtime shares (tools/stamps.py); never timed
 #endif
 #define HM_NSTAMP 12
-#ifndef HM_DOCROW_AHEAD
-#define HM_DOCROW_AHEAD 0   // 1: the next document's row is read one iteration earlier (more live SGPRs)
-#endif
 #ifndef HM_PREFETCH_EARLY
 #define HM_PREFETCH_EARLY 0 // 1: the next document's rows are loaded before this document's merge
 #endif
@@ -219,7 +216,7 @@ __device__ __forceinline__ u64 stamp_now() {
 #endif
 
 enum : uint32_t { FL_UNSUPPORTED = 1u };
-enum Outcome { OUT_OK = 0, OUT_ERROR = 1, OUT_UNSUPPORTED = 2 };
+enum Outcome { OUT_OK = 0, OUT_ERROR = 1, OUT_UNSUPPORTED = 2, OUT_INVALID = 3 };
 
 // raise byte a of the 8-byte packed requirement (lo: actors 0-3, hi: 4-7) to at least v;
 // selects only (a data-dependent reference would push lo/hi to scratch)
@@ -443,6 +440,13 @@ struct Rows {
     uint4 a0, b0, a1, b1, a2, b2, a3, b3;    // op rows lane + 64 t (first / second 16 B)
     uint2 d0, d1;                            // dep rows lane, lane + 64
 };
+// a document row; one whose ranges leave the tables reads as an empty row (ok = false)
+__device__ __forceinline__ hm_doc_row read_doc(const SmallParams &p, uint32_t d, bool &ok) {
+    hm_doc_row r = p.docs[d];
+    ok = hm_doc_row_ok(p, r);
+    if (!ok) r = hm_doc_row{};
+    return r;
+}
 __device__ __forceinline__ void load_op(const SmallParams &p, const hm_doc_row &doc, uint32_t k, uint4 &a, uint4 &b) {
     a = make_uint4(0, 0, 0, 0); b = a;
     if (k < doc.n_ops) {
@@ -1253,6 +1257,19 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
         }
         return;
     }
+    if (oc == OUT_INVALID) {
+        // malformed row (ranges outside the batch tables): nothing of it is read or written
+        if (lane == 0) {
+            hm_doc_result r = {};
+            r.status = HM_ERR_INVALID; r.err_change = HM_NONE; r.err_op = HM_NONE;
+            *dres = r;
+        }
+        if (lane < S) {
+            p.res_clock[(size_t)ds * S + lane] = 0u; p.res_heads[(size_t)ds * S + lane] = 0u;
+            p.res_back_clock[(size_t)ds * S + lane] = 0u;
+        }
+        return;
+    }
     if (oc == OUT_UNSUPPORTED) {
         // outside this kernel's envelope: merge_large_kernel finds the status and takes the document
         if (lane == 0) {
@@ -1351,11 +1368,8 @@ void merge_small_kernel(SmallParams p) {
 #if HM_STAMPS
     if (threadIdx.x == 0) { for (int i = 0; i < HM_NSTAMP; i++) L.stamps[i] = 0; L.stamps[HM_NSTAMP] = stamp_now(); }
 #endif
-    hm_doc_row doc = p.docs[d];
-#if HM_DOCROW_AHEAD
-    hm_doc_row docn = {};                    // the next document's row, read one iteration ahead
-    if (d + gridDim.x < p.n_docs) docn = p.docs[d + gridDim.x];
-#endif
+    bool dok;
+    hm_doc_row doc = read_doc(p, d, dok);
     uint2 w0, w1, w2;                        // this document's change row (lane = arrival index)
     {
         const Rows r = load_rows<OPL>(p, doc);
@@ -1368,13 +1382,9 @@ void merge_small_kernel(SmallParams p) {
         // loaded before this document's stores and staged to LDS after them
         const uint32_t dn = d + gridDim.x;
         const bool more = dn < p.n_docs;
-#if HM_DOCROW_AHEAD
-        hm_doc_row docnn = {};
-        if (dn + gridDim.x < p.n_docs) docnn = p.docs[dn + gridDim.x];
-#else
+        bool dokn = true;
         hm_doc_row docn = {};
-        if (more) docn = p.docs[dn];
-#endif
+        if (more) docn = read_doc(p, dn, dokn);
         Rows next;
 #if HM_PREFETCH_EARLY
         if (more) next = load_rows<OPL>(p, docn);
@@ -1383,7 +1393,7 @@ void merge_small_kernel(SmallParams p) {
                             doc.n_regs <= p.cap_regs && doc.n_objs <= p.cap_objs && doc.n_objs >= 1 &&
                             doc.n_deps <= p.cap_deps && !p.general_only;
         DocState st;
-        const Outcome oc = in_env ? merge_doc_small<OPL, LISTS>(p, L, doc, w0, w1, w2, st) : OUT_UNSUPPORTED;
+        const Outcome oc = !dok ? OUT_INVALID : in_env ? merge_doc_small<OPL, LISTS>(p, L, doc, w0, w1, w2, st) : OUT_UNSUPPORTED;
 #if !HM_PREFETCH_EARLY
         if (more) next = load_rows<OPL>(p, docn);
 #endif
@@ -1398,9 +1408,7 @@ void merge_small_kernel(SmallParams p) {
         STAMP(L, 11);
         d = dn;
         doc = docn;
-#if HM_DOCROW_AHEAD
-        docn = docnn;
-#endif
+        dok = dokn;
     }
 #if HM_STAMPS
     if (threadIdx.x == 0)

@@ -189,7 +189,8 @@ int launch_store_merge(hm_store *s, const std::vector<uint32_t> &handles, uint8_
     o.docs = s->res_docs; o.clock = s->clock; o.back_clock = s->back_clock; o.heads = s->heads;
     o.hist = s->hist; o.all_deps = s->all_deps; o.regs = s->regs; o.surv = s->surv;
     // the launch's host copies must outlive the async H2D copies: synchronise here
-    int rc = hm_engine_launch_merge(s->e, &b, &o, dev_handles);
+    const hm_extents ext = {(uint32_t)s->cap_c, (uint32_t)s->cap_d, (uint32_t)s->cap_o, (uint32_t)s->cap_r};
+    int rc = hm_engine_launch_merge(s->e, &b, &o, dev_handles, &ext);
     SCHK(s, hipStreamSynchronize(st));
     return rc;
 }
@@ -333,6 +334,24 @@ int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
                 return hm_engine_fail(s->e, HM_ERR_INVALID, "document rows outside the batch tables");
             if (r.n_actors > S || r.n_actors < m.n_actors || r.n_regs < m.n_r || r.n_objs < m.n_objs || r.n_objs == 0)
                 return hm_engine_fail(s->e, HM_ERR_INVALID, "document totals must cover the existing log (and n_actors <= a_stride)");
+            // every change row must lie inside its document's slice of the batch tables
+            for (uint32_t c = r.change_off; c < r.change_off + r.n_changes; c++) {
+                const hm_change_row &cr = b->changes[c];
+                if ((uint64_t)cr.dep_off < r.dep_off || (uint64_t)cr.dep_off + cr.n_deps > (uint64_t)r.dep_off + r.n_deps ||
+                    (uint64_t)cr.op_first < r.op_off || (uint64_t)cr.op_first + cr.n_ops > (uint64_t)r.op_off + r.n_ops)
+                    return hm_engine_fail(s->e, HM_ERR_INVALID, "change rows outside their document's deps/ops");
+            }
+            // the actor re-rank of the existing rows: a permutation into the new ranks.  Checked
+            // here, before any document meta or arena pointer moves (a failure leaves the store as it was)
+            if (actor_remap) {
+                const uint8_t *mp = actor_remap + (size_t)i * S;
+                uint64_t used = 0;
+                for (uint32_t a = 0; a < m.n_actors; a++) {
+                    if (mp[a] >= r.n_actors || ((used >> mp[a]) & 1))
+                        return hm_engine_fail(s->e, HM_ERR_INVALID, "actor remap is not a permutation into the new ranks");
+                    used |= 1ull << mp[a];
+                }
+            }
         }
         // plan segments: grow into fresh segments, compact the arenas when full
         size_t need_c = 0, need_d = 0, need_o = 0, need_r = 0;
@@ -379,8 +398,7 @@ int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
                     std::vector<uint8_t> inv(S, 0xFF), row(S, 0xFF);
                     for (uint32_t a = 0; a < S; a++) {
                         if (a < m.n_actors) {
-                            if (mp[a] >= r.n_actors) return hm_engine_fail(s->e, HM_ERR_INVALID, "actor remap out of range");
-                            row[a] = mp[a]; inv[mp[a]] = (uint8_t)a;
+                            row[a] = mp[a]; inv[mp[a]] = (uint8_t)a;     // validated above
                         } else row[a] = 0xFF;
                     }
                     D.remap_row = n_remap++;

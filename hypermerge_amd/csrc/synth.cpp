@@ -527,4 +527,18 @@ void hm_synth_free(void *h) { delete (Output *)h; }
 
 uint64_t hm_synth_fnv1a64_docid(uint64_t seed, uint64_t g) { return fnv1a64(doc_id(seed, g)); }
 
+// Repo-global record keys of a synthetic shard (the clock exchange, exchange.hip): per document
+// FNV-1a64 of its base58 doc id, per (document, actor rank < n_actors) FNV-1a64 of the actor's
+// synthetic id "<docId>/<rank>" (0 past n_actors).
+void hm_synth_keys(uint64_t seed, const hm_doc_row *docs, uint32_t n, uint32_t S, uint64_t *doc_keys,
+                   uint64_t *actor_keys) {
+    for (uint32_t d = 0; d < n; d++) {
+        const uint64_t g = (uint64_t)docs[d].reserved[0] | ((uint64_t)docs[d].reserved[1] << 32);
+        const std::string id = doc_id(seed, g);
+        doc_keys[d] = fnv1a64(id);
+        for (uint32_t a = 0; a < S; a++)
+            actor_keys[(size_t)d * S + a] = a < docs[d].n_actors ? fnv1a64(id + "/" + std::to_string(a)) : 0;
+    }
+}
+
 }  // extern "C"

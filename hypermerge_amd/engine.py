@@ -20,10 +20,14 @@ LIB = os.environ.get("HMGPU_LIB") or os.path.join(_HERE, "_lib", "libhmgpu.so")
 # every symbol include/hypermerge_amd.h declares
 EXPORTS = ("hm_abi_version", "hm_status_message", "hm_engine_create", "hm_engine_destroy",
            "hm_engine_last_error", "hm_merge_host", "hm_scratch_bytes", "hm_merge_device",
-           "hm_last_kernel_ms", "hm_clock_cmp_device", "hm_clock_union_device",
+           "hm_last_kernel_ms", "hm_last_deferred", "hm_clock_cmp_device", "hm_clock_union_device",
            "hm_clock_intersection_device", "hm_store_create", "hm_store_destroy", "hm_doc_open",
            "hm_batch_submit", "hm_batch_wait", "hm_doc_info", "hm_doc_read", "hm_doc_log",
-           "hm_doc_history_prefix", "hm_doc_set_min_clock", "hm_store_clock_update", "hm_sync_ranges_device")
+           "hm_doc_history_prefix", "hm_doc_set_min_clock", "hm_store_clock_update", "hm_sync_ranges_device",
+           "hm_comm_unique_id", "hm_comm_create", "hm_comm_destroy", "hm_comm_group_start", "hm_comm_group_end",
+           "hm_clock_records_scratch_bytes", "hm_clock_records_device", "hm_clock_count_allgather",
+           "hm_clock_allgather", "hm_clock_min_allreduce", "hm_comm_create_local", "hm_clock_exchange_host",
+           "hm_clock_min_host")
 
 _lib = None
 
@@ -58,6 +62,7 @@ def lib():
         L.hm_scratch_bytes.argtypes = [ctypes.POINTER(CBatch)]
         L.hm_scratch_bytes.restype = ctypes.c_size_t
         L.hm_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
+        L.hm_last_deferred.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
         for f in ("hm_clock_cmp_device", "hm_clock_union_device", "hm_clock_intersection_device"):
             getattr(L, f).argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 3 + [ctypes.c_uint32] * 2 + [ctypes.c_void_p]
         vp, u32 = ctypes.c_void_p, ctypes.c_uint32
@@ -68,10 +73,21 @@ def lib():
             "hm_doc_history_prefix": [vp, u32, u32, vp], "hm_doc_set_min_clock": [vp, u32, vp],
             "hm_store_clock_update": [vp, u32, vp, vp, vp, vp],
             "hm_sync_ranges_device": [vp, vp, vp, vp, vp, vp, u32, vp],
+            "hm_comm_unique_id": [vp], "hm_comm_create": [vp, ctypes.c_int, ctypes.c_int, vp, vp],
+            "hm_comm_destroy": [vp], "hm_comm_group_start": [], "hm_comm_group_end": [],
+            "hm_clock_records_scratch_bytes": [u32, u32],
+            "hm_clock_records_device": [vp, vp, vp, vp, vp, u32, u32, vp, vp, vp, vp],
+            "hm_clock_count_allgather": [vp, ctypes.c_uint64, vp, vp],
+            "hm_clock_allgather": [vp, vp, vp, vp, vp], "hm_clock_min_allreduce": [vp, vp, ctypes.c_uint64, vp],
+            "hm_comm_create_local": [vp, ctypes.c_int, vp],
+            "hm_clock_exchange_host": [vp, ctypes.c_int, vp, vp, vp, ctypes.c_uint64, vp],
+            "hm_clock_min_host": [vp, ctypes.c_int, vp, ctypes.c_uint64],
         }
         for f, a in sig.items():
             getattr(L, f).argtypes = a
         L.hm_store_destroy.restype = None
+        L.hm_comm_destroy.restype = None
+        L.hm_clock_records_scratch_bytes.restype = ctypes.c_size_t
         _lib = L
     return _lib
 
@@ -127,6 +143,14 @@ class Engine:
         buf = (ctypes.c_float * 4)()
         n = self._L.hm_last_kernel_ms(self._h, buf, 4)
         return [float(buf[i]) for i in range(n)]
+
+    def last_deferred(self, n_docs: int) -> np.ndarray:
+        """Launch rows the last launch handed to the general kernel (hand-over order)."""
+        out = np.zeros(max(n_docs, 1), np.uint32)
+        n = self._L.hm_last_deferred(self._h, out.ctypes.data, len(out))
+        if n < 0:
+            self._check(-n, "hm_last_deferred")
+        return out[:min(n, len(out))].copy()
 
     def clock_op(self, which: str, a_ptr: int, b_ptr: int, out_ptr: int, n_docs: int, a_stride: int,
                  stream: int = 0) -> None:

@@ -38,6 +38,7 @@ typedef struct {
     hm_engine *engine;
     hm_store *store;
     uint32_t a_stride;
+    uint32_t pending_n;   /* documents of the batch in flight (sizes Wait's buffers) */
 } Store;
 
 static void store_finalize(napi_env env, void *data, void *hint) {
@@ -159,19 +160,21 @@ static napi_value Submit(napi_env env, napi_callback_info info) {
     uint64_t id = 0;
     int st = hm_batch_submit(s->store, &b, (const uint32_t *)p[4], (const uint8_t *)p[5], &id);
     if (st) return throw_status(env, s->engine, st, "hm_batch_submit");
+    s->pending_n = b.n_docs;
     napi_value out;
     CHECK_NAPI(napi_create_double(env, (double)id, &out));
     return out;
 }
 
-/* wait(store, id, nDocs) -> {docs, clock, backClock, heads} (Buffers) */
+/* wait(store, id[, nDocs]) -> {docs, clock, backClock, heads} (Buffers).  The buffers are
+ * sized from the submitted batch's document count, never from the caller's nDocs. */
 static napi_value Wait(napi_env env, napi_callback_info info) {
-    napi_value argv[3];
-    if (!get_args(env, info, 3, argv)) return NULL;
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return NULL;
     Store *s = get_store(env, argv[0]);
     if (!s) return NULL;
     double idd; napi_get_value_double(env, argv[1], &idd);
-    const uint32_t n = get_u32(env, argv[2]), S = s->a_stride;
+    const uint32_t n = s->pending_n, S = s->a_stride;
     size_t rb = (size_t)n * sizeof(hm_doc_result), cb = (size_t)n * S * 4;
     uint8_t *buf = (uint8_t *)malloc(rb + 3 * cb + 16);
     int st = hm_batch_wait(s->store, (uint64_t)idd, (hm_doc_result *)buf, (uint32_t *)(buf + rb),

@@ -82,6 +82,8 @@ def lib():
         _lib.hm_synth_free.argtypes = [ctypes.c_void_p]
         _lib.hm_synth_fnv1a64_docid.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
         _lib.hm_synth_fnv1a64_docid.restype = ctypes.c_uint64
+        _lib.hm_synth_keys.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                       ctypes.c_void_p, ctypes.c_void_p]
     return _lib
 
 
@@ -103,6 +105,16 @@ def generate(cfg: SynthConfig, threads: Optional[int] = None) -> Batch:
     finally:
         L.hm_synth_free(h)
     return Batch(docs, ch, dp, op, S)
+
+
+def keys(cfg: SynthConfig, b: Batch):
+    """(doc_keys u64[n], actor_keys u64[n*S]): FNV-1a64 of each document's base58 id and of
+    its actors' synthetic ids — the repo-global keys of the clock exchange."""
+    n, S = b.n_docs, b.a_stride
+    dk = np.zeros(n, np.uint64)
+    ak = np.zeros(n * S, np.uint64)
+    lib().hm_synth_keys(cfg.seed, b.docs.ctypes.data, n, S, dk.ctypes.data, ak.ctypes.data)
+    return dk, ak
 
 
 def config(name: str, **overrides) -> SynthConfig:

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define HM_ABI_VERSION 2u
+#define HM_ABI_VERSION 3u
 
 /* ------------------------------------------------------------------ */
 /* Status codes                                                        */
@@ -225,6 +225,11 @@ int hm_merge_device(hm_engine *e, const hm_batch *batch, const hm_results *out,
 /* Per-kernel launch timing of the last hm_merge_* call on `stream`,
  * measured with HIP events on that stream (ms).  Returns number filled. */
 int hm_last_kernel_ms(hm_engine *e, float *ms, int max_kernels);
+/* Documents the last hm_merge_* launch routed to the general (workgroup) kernel: waits
+ * for that launch, copies up to `cap` of their launch-row indices (in hand-over order)
+ * and returns their count (negative hm_status on failure).  Diagnostics / roofline
+ * attribution: the two kernels' algorithmic bytes are split by it. */
+int hm_last_deferred(hm_engine *e, uint32_t *out_docs, uint32_t cap);
 
 /* ------------------------------------------------------------------ */
 /* Clock algebra (src/Clock.ts) over dense per-doc rows (a_stride wide) */
@@ -337,6 +342,74 @@ int hm_store_clock_update(hm_store *s, uint32_t n, const uint32_t *docs, uint8_t
 int hm_sync_ranges_device(hm_engine *e, const uint64_t *present, const uint64_t *word_off,
                           const uint32_t *lo, const uint32_t *hi, uint32_t *out_end, uint32_t n,
                           void *stream);
+
+/* ------------------------------------------------------------------ */
+/* Clock exchange across the node's GPUs (RCCL over xGMI)              */
+/* ------------------------------------------------------------------ */
+/*
+ * Documents shard by FNV-1a64(docId) % G; each GPU (engine) owns its documents' state and the
+ * merge never communicates.  What crosses GPUs is the ClockStore feed: per-document clock
+ * entries as repo-global records, the analogue of the `clocks` a CursorMessage carries
+ * ({docId, clock: {actorId: seq}}, src/PeerMsg.ts:12-16, assembled from ClockStore at
+ * src/RepoBackend.ts:374-392 and applied at :397-418).  Actor ranks are per-document and
+ * encoder-local, so records name documents and actors by 64-bit keys (FNV-1a64 of the docId /
+ * actorId strings; 0 = no actor); the host keeps the key -> string tables.
+ *
+ *   replaces: src/RepoBackend.ts:374-392 onDiscovery clocks = ClockStore.get per doc
+ *             src/RepoBackend.ts:402,412-418 ClockStore.update(sender, doc, clock) + minimumClock
+ *             src/Clock.ts:103-113 intersection (the min-clock across replicas)
+ *
+ * One process per GPU: rank 0 makes a unique id (hm_comm_unique_id), the host distributes it
+ * (any channel), every rank calls hm_comm_create.  One thread driving several GPUs: create
+ * (and later issue each collective on) every communicator between hm_comm_group_start/_end.
+ */
+#define HM_COMM_ID_BYTES 128
+#define HM_CLOCK_NOT_HELD 0xFFFFFFFFu   /* min-allreduce identity: "this rank does not hold the doc" */
+
+typedef struct {          /* 24 B */
+    uint64_t doc_key;     /* FNV-1a64(docId) */
+    uint64_t actor_key;   /* FNV-1a64(actorId) */
+    uint32_t seq;         /* the clock entry (DocBackend.clock / ClockStore row) */
+    uint32_t flags;       /* 0 (reserved) */
+} hm_clock_rec;
+
+typedef struct hm_comm hm_comm;
+int  hm_comm_unique_id(uint8_t *out /* HM_COMM_ID_BYTES */);
+int  hm_comm_create(hm_engine *e, int world, int rank, const uint8_t *unique_id, hm_comm **out);
+void hm_comm_destroy(hm_comm *c);
+int  hm_comm_group_start(void);
+int  hm_comm_group_end(void);
+
+/* Dense per-document clock rows (device: doc_keys[n_docs], actor_keys / clock / base
+ * [n_docs*a_stride], base optional) -> records of every entry with actor_key != 0 and
+ * clock > base (base NULL: > 0), document-major, rank order within a document.
+ * *out_count (device u32) receives the count; `scratch` = hm_clock_records_scratch_bytes. */
+size_t hm_clock_records_scratch_bytes(uint32_t n_docs, uint32_t a_stride);
+int hm_clock_records_device(hm_engine *e, const uint64_t *doc_keys, const uint64_t *actor_keys,
+                            const uint32_t *clock, const uint32_t *base, uint32_t n_docs, uint32_t a_stride,
+                            hm_clock_rec *out, uint32_t *out_count, void *scratch, void *stream);
+
+/* d_counts[world] (device u64) <- every rank's record count (all-gather; returns after it). */
+int hm_clock_count_allgather(hm_comm *c, uint64_t n_local, uint64_t *d_counts, void *stream);
+/* d_out <- every rank's records back to back in rank order; counts (host, [world]) from
+ * hm_clock_count_allgather; d_out holds sum(counts) records.  Enqueued on `stream`. */
+int hm_clock_allgather(hm_comm *c, const hm_clock_rec *d_recs, const uint64_t *counts, hm_clock_rec *d_out,
+                       void *stream);
+/* In place, elementwise MIN over every rank of rank-aligned seq rows (row = a (doc, actor) key
+ * of the gathered key universe): a rank that holds the document contributes its entry (0 =
+ * absent), one that does not HM_CLOCK_NOT_HELD.  After it, 0 and HM_CLOCK_NOT_HELD are absent
+ * entries and the rest is Clock.intersection over the replicas holding the document. */
+int hm_clock_min_allreduce(hm_comm *c, uint32_t *d_seq, uint64_t n, void *stream);
+
+/* One process driving n GPUs (the Node host's GpuEngine, one engine per device): an n-rank
+ * communicator over the engines, and host-buffer forms of the two collectives (staged
+ * through each device; every engine's records / seq row is one rank's contribution).
+ * hm_clock_exchange_host: out <- all records in rank order (*out_total of them, <= out_cap).
+ * hm_clock_min_host: every seq[i] row (len entries) <- the MIN over the n rows. */
+int hm_comm_create_local(hm_engine *const *engines, int n, hm_comm **out);
+int hm_clock_exchange_host(hm_comm *const *comms, int n, const hm_clock_rec *const *recs, const uint64_t *n_recs,
+                           hm_clock_rec *out, uint64_t out_cap, uint64_t *out_total);
+int hm_clock_min_host(hm_comm *const *comms, int n, uint32_t *const *seq, uint64_t len);
 
 #ifdef __cplusplus
 }

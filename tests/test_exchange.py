@@ -1,25 +1,32 @@
-"""Sharding and the cross-rank clock exchange (hypermerge_amd/exchange.py) with
-world_size 2 over gloo on CPU (the GPU box runs the same code over RCCL).
+"""Sharding and the cross-rank clock exchange (hypermerge_amd/exchange.py; C-ABI
+hm_clock_* in include/hypermerge_amd.h) with world_size 2 over gloo on CPU — the GPU box
+runs the same protocol over RCCL (tests/test_exchange_gpu.py runs the C-ABI itself).
 
 * shards: FNV-1a64(docId) % world partitions the global doc-id stream (disjoint,
   complete), and each shard merges independently (no data-path collective);
-* gather_clock_rows: every rank ends with the union of all ranks' changed clock rows;
-* min_clock / union_clock: element-wise MIN / MAX all-reduce == Clock.intersection /
-  Clock.union (src/Clock.ts:87-113) of the ranks' clocks.
+* the ranks own *different* documents with *different* actor tables (2..11 actors per
+  document, actors shared between documents as a merge/fork shares them); every rank's host
+  rebuilds, from the gathered records, exactly the {docId: {actorId: seq}} clocks a
+  CursorMessage carries for every document of the node (src/RepoBackend.ts:374-392,
+  src/PeerMsg.ts:12-16): the DocBackend.clock of each document (src/DocBackend.ts:135-142);
+* the min-clock over replicas (documents held by both ranks at different progress, plus
+  documents held by one rank only) equals Clock.intersection (src/Clock.ts:103-113) of the
+  holders' clocks.
 """
 import os
+import random
 import socket
 
 import numpy as np
-import pytest
-import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from hypermerge_amd import synth
 from hypermerge_amd import clock as C
+from hypermerge_amd import columnar as col
 
 N_DOCS = 400
+B58 = "123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstuvwxyz"
 
 
 def _free_port():
@@ -30,36 +37,94 @@ def _free_port():
     return p
 
 
-def _keys(b):
-    return b.docs["reserved"][:, 0].astype(np.int64) | (b.docs["reserved"][:, 1].astype(np.int64) << 32)
+def _b58(rng):
+    """A base58 id of 32 random bytes, as hypermerge mints doc and actor ids."""
+    n = int.from_bytes(bytes(rng.getrandbits(8) for _ in range(32)), "big")
+    s = ""
+    while n:
+        n, r = divmod(n, 58)
+        s = B58[r] + s
+    return s
+
+
+def _world_docs(seed=7, n=48):
+    """Documents with ids, actor tables and change feeds (identical on every rank)."""
+    rng = random.Random(seed)
+    pool = [_b58(rng) for _ in range(40)]                   # actors, some shared across documents
+    docs = []
+    for _ in range(n):
+        doc = _b58(rng)
+        actors = rng.sample(pool, rng.randint(2, 11))
+        seqs = {a: 0 for a in actors}
+        changes = []
+        for i in range(rng.randint(3, 30)):
+            a = rng.choice(actors)
+            seqs[a] += 1
+            deps = {b: s for b, s in seqs.items() if b != a and s and rng.random() < 0.5}
+            changes.append({"actor": a, "seq": seqs[a], "deps": deps,
+                            "ops": [{"action": "set", "obj": col.ROOT_ID, "key": f"k{i % 5}", "value": i}]})
+        docs.append((doc, changes))
+    return docs
+
+
+def _doc_clock(changes):
+    """DocBackend.updateClock (src/DocBackend.ts:135-142): clock[actor] = max(clock[actor] || 0, seq)."""
+    c = {}
+    for ch in changes:
+        c[ch["actor"]] = max(c.get(ch["actor"], 0), ch["seq"])
+    return c
+
+
+def _engine_rows(owned, keys, X):
+    """The dense rows the engine keeps for `owned` documents: encoded columnar batch, the
+    CPU restatement's DocBackend.clock (back_clock) per document, actor keys per rank."""
+    import oracle.oracle as O
+    if not owned:
+        return np.zeros(0, X.CLOCK_REC_DT)
+    b = col.encode([ch for _, ch in owned], a_stride=16)
+    r = O.merge(b)
+    S = b.a_stride
+    dk = np.array([keys.key(d) for d, _ in owned], np.uint64)
+    ak = np.zeros(len(owned) * S, np.uint64)
+    for i, actors in enumerate(b.doc_actors):
+        for rank_, a in enumerate(actors):
+            ak[i * S + rank_] = keys.key(a)
+    return X.records_host(dk, ak, r.back_clock.astype(np.uint32))
 
 
 def _worker(rank, ws, port, out):
-    import oracle.oracle as O
     from hypermerge_amd import exchange as X
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     try:
+        # synthetic shards (bench.py's C4 stream): disjoint, keyed by FNV-1a64 of the doc id
         b = synth.generate(synth.config("C4", n_docs=N_DOCS, shard=rank, n_shards=ws), threads=2)
-        r = O.merge(b)
-        S = b.a_stride
-        keys = torch.from_numpy(_keys(b))
-        newc = torch.from_numpy(r.back_clock.view(np.int32).reshape(-1, S).copy())
-        rows = X.changed_rows(keys, newc, torch.zeros_like(newc))
-        allrows = X.gather_clock_rows(rows)
-        # replicas: every rank holds the same 50 documents at a different progress
-        rep = synth.generate(synth.config("C4", n_docs=50), threads=2)
-        k = 10 + 20 * rank
-        sub = rep.changes.copy()
-        prog = np.zeros((50, S), np.int64)
-        for d in range(50):
-            c0 = int(rep.docs["change_off"][d])
-            for c in sub[c0: c0 + min(k, int(rep.docs["n_changes"][d]))]:
-                prog[d, c["actor"]] = max(prog[d, c["actor"]], int(c["seq"]))
-        mn = X.min_clock(torch.from_numpy(prog.copy()))
-        mx = X.union_clock(torch.from_numpy(prog.copy()))
-        out[rank] = {"keys": _keys(b).tolist(), "rows": allrows.numpy().tolist(), "prog": prog.tolist(),
-                     "min": mn.numpy().tolist(), "max": mx.numpy().tolist(), "n_changes": int(r.docs["hist_len"].sum())}
+        gkeys = (b.docs["reserved"][:, 0].astype(np.int64) | (b.docs["reserved"][:, 1].astype(np.int64) << 32))
+
+        world = _world_docs()
+        keys = X.KeyTable()
+        tr = X.TorchTransport()
+        ex = X.ClockExchange(tr, keys)
+        owned = [(d, ch) for d, ch in world if X.shard_of(d, ws) == rank]
+        own = _engine_rows(owned, keys, X)
+        tr.exchange_keys(keys)                    # host id tables (the swarm's feed ids)
+        gathered = ex.gather(own)
+        clocks = ex.clocks(gathered)
+
+        # replicas: the first 20 documents on both ranks at a different progress, the next 8
+        # on one rank only
+        rep = []
+        for i, (d, ch) in enumerate(world[:28]):
+            if i < 20:
+                rep.append((d, ch[: max(1, len(ch) * (rank + 1) // 3)]))
+            elif i % 2 == rank:
+                rep.append((d, ch))
+        rown = _engine_rows(rep, keys, X)
+        tr.exchange_keys(keys)
+        rall = ex.gather(rown)
+        mc = ex.min_clock(rall, rown)
+        out[rank] = {"keys": gkeys.tolist(), "owned": [d for d, _ in owned], "clocks": clocks, "min": mc,
+                     "rep": {d: _doc_clock(ch) for d, ch in rep}, "n_recs": len(gathered)}
     finally:
         dist.destroy_process_group()
 
@@ -71,20 +136,63 @@ def test_two_rank_sharding_and_clock_exchange():
         out = m.dict()
         mp.spawn(_worker, args=(ws, port, out), nprocs=ws, join=True)
         out = dict(out)
+    # synthetic sharding: disjoint, complete, every key hashes to its shard
     k0, k1 = set(out[0]["keys"]), set(out[1]["keys"])
     assert len(k0) == N_DOCS and len(k1) == N_DOCS and not (k0 & k1)
-    for r in (0, 1):                                   # every key hashes to its shard
+    for r in (0, 1):
         for g in list(out[r]["keys"])[:50]:
             assert synth.lib().hm_synth_fnv1a64_docid(synth.CONFIGS["C4"].seed, g) % ws == r
-    # gathered rows: identical on both ranks, = union of per-rank rows, one per (doc, actor) entry
-    assert out[0]["rows"] == out[1]["rows"]
-    keys_in_rows = {row[0] for row in out[0]["rows"]}
-    assert keys_in_rows == k0 | k1
-    # min/max all-reduce == Clock.intersection / Clock.union of the two ranks' rows
-    p0, p1 = np.array(out[0]["prog"]), np.array(out[1]["prog"])
-    for d in range(len(p0)):
-        a = {str(i): int(v) for i, v in enumerate(p0[d]) if v}
-        b = {str(i): int(v) for i, v in enumerate(p1[d]) if v}
-        inter, uni = C.intersection(a, b), C.union(a, b)
-        assert out[0]["min"][d] == [inter.get(str(i), 0) for i in range(len(p0[d]))]
-        assert out[1]["max"][d] == [uni.get(str(i), 0) for i in range(len(p0[d]))]
+
+    world = _world_docs()
+    o0, o1 = set(out[0]["owned"]), set(out[1]["owned"])
+    assert o0 and o1 and not (o0 & o1) and o0 | o1 == {d for d, _ in world}
+    # the ranks' actor tables differ (documents of different actor sets on each rank)
+    acts = [{a for d, ch in world if d in o for a in _doc_clock(ch)} for o in (o0, o1)]
+    assert acts[0] != acts[1]
+    # every rank rebuilds the CursorMessage clocks of every document of the node, exactly
+    expect = {d: _doc_clock(ch) for d, ch in world}
+    for r in (0, 1):
+        assert out[r]["clocks"] == expect
+        assert out[r]["n_recs"] == sum(len(c) for c in expect.values())
+    # min-clock = Clock.intersection over the ranks holding each document
+    held = [out[0]["rep"], out[1]["rep"]]
+    for d in set(held[0]) | set(held[1]):
+        cs = [h[d] for h in held if d in h]
+        want = cs[0]
+        for c in cs[1:]:
+            want = C.intersection(want, c)
+        for r in (0, 1):
+            assert out[r]["min"][d] == want, (d, r)
+
+
+def test_alignment_and_records_host():
+    from hypermerge_amd import exchange as X
+    keys = X.KeyTable()
+    dk, ak, ck = X.dense_rows([("docA", {"b": 3, "a": 1}), ("docB", {"c": 2})], 4, keys)
+    recs = X.records_host(dk, ak, ck)
+    assert [(keys[int(r["doc_key"])], keys[int(r["actor_key"])], int(r["seq"])) for r in recs] == \
+        [("docA", "a", 1), ("docA", "b", 3), ("docB", "c", 2)]
+    # delta records against a stored row: only entries that grew
+    base = ck.copy()
+    base[0] = 1
+    base[1] = 2
+    base[4] = 0
+    d = X.records_host(dk, ak, ck, base)
+    assert [(keys[int(r["actor_key"])], int(r["seq"])) for r in d] == [("b", 3), ("c", 2)]
+    other = X.records_host(*X.dense_rows([("docA", {"a": 5, "d": 1})], 4, keys))
+    allr = np.concatenate([recs, other])
+    pairs, mine = X.align(allr, recs)
+    named = [(keys[int(p[0])], keys[int(p[1])]) for p in pairs]
+    assert named == sorted(named, key=lambda x: (X.fnv1a64(x[0]), X.fnv1a64(x[1])))
+    got = {n: int(v) for n, v in zip(named, mine)}
+    assert got[("docA", "a")] == 1 and got[("docA", "b")] == 3 and got[("docA", "d")] == 0
+    assert got[("docB", "c")] == 2
+    pairs2, mine2 = X.align(allr, other)
+    got2 = {(keys[int(p[0])], keys[int(p[1])]): int(v) for p, v in zip(pairs2, mine2)}
+    assert got2[("docB", "c")] == X.NOT_HELD and got2[("docA", "b")] == 0 and got2[("docA", "a")] == 5
+    # the MIN over the two contributions is Clock.intersection over the holders (docB: one)
+    m = np.minimum(mine, mine2)
+    inter = {(d, a): int(v) for (d, a), v in zip(named, m) if v not in (0, X.NOT_HELD)}
+    assert inter == {("docA", "a"): 1, ("docB", "c"): 2}
+    assert C.intersection({"a": 1, "b": 3}, {"a": 5, "d": 1}) == {"a": 1}
+    assert X.fnv1a64("") == 0xCBF29CE484222325 and X.fnv1a64("a") == 0xAF63DC4C8601EC8C

@@ -243,3 +243,29 @@ def test_chunked_host_pipeline(engine, name, n, extra):
     for f in ("hist", "all_deps", "regs", "surv"):
         assert np.array_equal(getattr(g, f), getattr(g1, f)), f
     assert np.array_equal(g.docs[:-2], g1.docs[:-2]) and np.array_equal(g.docs[-2:], g1.docs[-2:][::-1])
+
+
+def test_malformed_doc_rows_are_invalid_per_document(engine):
+    """A document row whose ranges leave the batch tables (or whose n_actors exceeds the
+    stride) is reported HM_ERR_INVALID for that document only, and never read through; the
+    other documents merge exactly as the oracle does."""
+    b = synth.generate(synth.config("C4", n_docs=64))
+    o = O.merge(b)
+    bad = b.docs.copy()
+    bad[3]["op_off"] = len(b.ops) - 1                    # op range runs past the op table
+    bad[9]["n_actors"] = b.a_stride + 1
+    bad[20]["reg_off"] = 1 << 30
+    bad[41]["change_off"] = len(b.changes)               # change range past the table
+    import dataclasses
+    bb = dataclasses.replace(b, docs=bad)
+    g = engine.merge(bb)
+    badset = {3, 9, 20, 41}
+    for d in range(b.n_docs):
+        if d in badset:
+            assert int(g.docs["status"][d]) == 32, d
+        else:
+            assert int(g.docs["status"][d]) == int(o.docs["status"][d])
+            assert int(g.docs["hist_len"][d]) == int(o.docs["hist_len"][d])
+    S = b.a_stride
+    keep = np.repeat([d not in badset for d in range(b.n_docs)], S)
+    np.testing.assert_array_equal(g.back_clock[keep], o.back_clock[keep])

@@ -161,3 +161,36 @@ def test_min_clock_and_clock_store(engine):
     w, df, st = store.clock_update([hs[0]])
     assert w[0] and not df[0]
     assert int(st[0][store.enc[hs[0]].actors.index("aaaa")]) == 3
+
+
+def test_bad_remap_leaves_store_unchanged(engine):
+    """hm_batch_submit validates every actor re-rank row before it moves any document meta or
+    arena pointer: a rejected batch leaves every document (earlier rows included) readable
+    and unchanged."""
+    import ctypes
+    from hypermerge_amd.columnar import CBatch, DOC_DT, CHANGE_DT, DEP_DT, OP_DT
+    from hypermerge_amd.engine import EngineError
+    store = DocStore(engine, a_stride=8)
+    hs = [store.open() for _ in range(2)]
+    store.apply([(hs[0], [ch("bbbb", 1, {}, s("x", 1))]), (hs[1], [ch("cccc", 1, {}, s("y", 2))])])
+    before = [store.read(h) for h in hs]
+    # rows for both documents; the second row's remap sends the existing rank 0 out of range
+    docs = np.zeros(2, DOC_DT)
+    docs["n_regs"], docs["n_objs"], docs["n_actors"] = 1, 1, 1
+    remap = np.tile(np.arange(8, dtype=np.uint8), (2, 1))
+    remap[1, 0] = 5
+    hs_arr = np.array(hs, np.uint32)
+    cb = CBatch(2, 0, 0, 0, 2, 8, 0, 0, 0, 0, 0, 0, docs.ctypes.data, None, None, None, None)
+    bid = ctypes.c_uint64()
+    st = store._L.hm_batch_submit(store._h, ctypes.byref(cb), hs_arr.ctypes.data, remap.ctypes.data, ctypes.byref(bid))
+    assert st == 32                                      # HM_ERR_INVALID, nothing in flight
+    after = [store.read(h) for h in hs]
+    for (b0, g0), (b1, g1) in zip(before, after):
+        for f in ("docs", "clock", "back_clock", "heads", "hist", "all_deps", "regs"):
+            np.testing.assert_array_equal(getattr(g0, f), getattr(g1, f), err_msg=f)
+        np.testing.assert_array_equal(b0.changes, b1.changes)
+    for h in hs:
+        assert_doc_matches_oracle(store, h)
+    # and the store still takes work
+    store.apply([(hs[0], [ch("bbbb", 2, {}, s("x", 3))])])
+    assert_doc_matches_oracle(store, hs[0])
