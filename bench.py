@@ -132,14 +132,15 @@ def main() -> int:
     # spot parity against the oracle on a sample (checker only; not timed)
     parity = None
     cpu = cpu_mt = None
-    if rank == 0 and ws == 1 and not args.no_cpu:          # CPU legs: rank 0 at N=1 only
+    if rank == 0 and ws == 1 and args.check_docs > 0:      # checker only: rank 0 at N=1
         import oracle.oracle as O
-        from hypermerge_amd.columnar import Batch
         k = min(args.check_docs, nd)
         sub = _subbatch(batch, k)
         g = eng.merge(sub)
         o = O.merge(sub, threads=min(16, os.cpu_count() or 1))
         parity = bool(_same(sub, g, o))
+    if rank == 0 and ws == 1 and not args.no_cpu:          # CPU legs: rank 0 at N=1 only
+        import oracle.oracle as O
         ns = min(args.cpu_sample_docs, nd)
         cs = _subbatch(batch, ns)
         t = time.perf_counter()

@@ -111,6 +111,10 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
     y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_BCAST31, 0xC, 0xF, false); x = x > y ? x : y;
     return (uint32_t)__builtin_amdgcn_readlane((int)x, WAVE - 1);
 }
+// sum of the 8 bytes of a 64-bit word (v_sad_u8 against 0)
+__device__ __forceinline__ uint32_t bytesum64(u64 x) {
+    return __builtin_amdgcn_sad_u8((uint32_t)x, 0u, __builtin_amdgcn_sad_u8((uint32_t)(x >> 32), 0u, 0u));
+}
 // value of the previous lane (lane 0 reads 0)
 __device__ __forceinline__ uint32_t prev_lane(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_WAVE_SHR1, 0xF, 0xF, false);
@@ -130,15 +134,18 @@ __device__ __forceinline__ u64 err_key(uint32_t h, uint32_t op_plus1, uint32_t a
 
 struct SmallLds {
     LDS u64 *anc, *chain, *segor, *errkey, *cov;
+    LDS u64 *opval;                 // op values (staged with the rows: survivors and counters read them)
+    LDS u64 *survpk;                // per register: survivor count per actor rank, one byte each
     LDS int64_t *survsum;           // counter launches only
     LDS uint32_t *first, *base, *bclock, *headv, *objslot, *segcnt, *survcnt, *regoff, *regobj, *insmin;
-    LDS uint32_t *flags, *deps, *depinfo, *seglist, *survp, *survent;
+    LDS uint32_t *flags, *deps, *depinfo, *seglist, *survp;
     LDS uint32_t *opmeta;           // action | datatype << 8 | vtag << 16
     LDS uint32_t *opro;             // reg | obj << 16 (clamped to 0xFFFF: >= any carve)
     LDS uint32_t *opelem;           // ins element counter (list launches)
     LDS int32_t *hist_of;
     LDS uint16_t *survop, *opbase, *oppar;
-    LDS uint8_t *h2a, *chactor, *opchg, *objtype;
+    LDS uint8_t *h2a, *chactor, *objtype;
+    LDS uint16_t *opchg;            // op -> arrival index of its change | actor rank << 8
     // K3 (RGA lists); carved only for launches with list documents
     LDS uint32_t *nins, *pcount, *poff, *pfill, *nodekey, *tour0, *tour1, *listbase;
     LDS uint16_t *nodeop, *nodepi, *regnode, *plist, *fc, *ns, *listid;
@@ -156,13 +163,14 @@ template <> struct SizeClass<1> { static constexpr uint32_t NR = 256, NO = 64, N
 // resident waves per CU, so nothing is carved that the launch's documents cannot use.
 // The kernel instantiates it with compile-time sizes (a size class), so every LDS address
 // folds into a ds_* immediate offset instead of occupying an SGPR.
-// Aliases: seglist/survp live in `first` (dead after K1b), survent in `deps` (dead after K1b).
+// Aliases: seglist/survp live in `first` (dead after K1b).
 template <typename L_t, typename P>
 __host__ __device__ inline size_t small_carve(P base, uint32_t NOp, uint32_t NR, uint32_t NO, uint32_t ND,
                                               bool lists, bool counters, L_t *L) {
     size_t o = 0;
 #define TAKE(f, T, cnt) do { L->f = (decltype(L->f))(base + o); o = (o + (size_t)(cnt) * sizeof(T) + 15) & ~(size_t)15; } while (0)
     TAKE(anc, u64, 64);          TAKE(chain, u64, NA_MAX);     TAKE(segor, u64, NR);
+    TAKE(opval, u64, NOp);       TAKE(survpk, u64, NR);
     TAKE(errkey, u64, 1);        TAKE(cov, u64, 1);
     TAKE(first, uint32_t, NA_MAX * 64 > 2 * NOp ? NA_MAX * 64 : 2 * NOp);
     L->seglist = L->first; L->survp = L->first + NOp;
@@ -171,11 +179,10 @@ __host__ __device__ inline size_t small_carve(P base, uint32_t NOp, uint32_t NR,
     TAKE(regoff, uint32_t, NR);  TAKE(regobj, uint32_t, NR);   TAKE(insmin, uint32_t, NR);
     TAKE(flags, uint32_t, 2);    TAKE(deps, uint32_t, ND > NOp ? ND : NOp);   // flags[1]: max n_deps
     TAKE(depinfo, uint32_t, ND);
-    L->survent = L->deps;
     TAKE(opmeta, uint32_t, NOp); TAKE(opro, uint32_t, NOp);
     TAKE(hist_of, int32_t, 64);
     TAKE(survop, uint16_t, NOp); TAKE(opbase, uint16_t, 64);   TAKE(oppar, uint16_t, NOp);
-    TAKE(h2a, uint8_t, 64);      TAKE(chactor, uint8_t, 64);   TAKE(opchg, uint8_t, NOp);
+    TAKE(h2a, uint8_t, 64);      TAKE(chactor, uint8_t, 64);   TAKE(opchg, uint16_t, NOp);
     TAKE(objtype, uint8_t, NO);
     if (lists) {
         const uint32_t NP = NR + NO, NE = 2 * (NOp + NO);
@@ -440,12 +447,13 @@ struct Rows {
     uint4 a0, b0, a1, b1, a2, b2, a3, b3;    // op rows lane + 64 t (first / second 16 B)
     uint2 d0, d1;                            // dep rows lane, lane + 64
 };
-// a document row; one whose ranges leave the tables reads as an empty row (ok = false)
-__device__ __forceinline__ hm_doc_row read_doc(const SmallParams &p, uint32_t d, bool &ok) {
-    hm_doc_row r = p.docs[d];
-    ok = hm_doc_row_ok(p, r);
+// a document row is validated where its rows are first loaded (not where it is read: the
+// next document's row is read a whole merge ahead); one whose ranges leave the tables
+// becomes an empty row (ok = false)
+__device__ __forceinline__ bool check_doc(const SmallParams &p, hm_doc_row &r) {
+    const bool ok = hm_doc_row_ok(p, r);
     if (!ok) r = hm_doc_row{};
-    return r;
+    return ok;
 }
 __device__ __forceinline__ void load_op(const SmallParams &p, const hm_doc_row &doc, uint32_t k, uint4 &a, uint4 &b) {
     a = make_uint4(0, 0, 0, 0); b = a;
@@ -471,11 +479,9 @@ __device__ __forceinline__ Rows load_rows(const SmallParams &p, const hm_doc_row
     if (lane + WAVE < doc.n_deps) r.d1 = *reinterpret_cast<const uint2 *>(dp + lane + WAVE);
     return r;
 }
-// an op's 8-byte value, re-read from its row (L2-resident: the row was read moments ago);
-// only survivors and counter ops need it, so it is not staged in LDS
-__device__ __forceinline__ u64 op_value(const SmallParams &p, const hm_doc_row &doc, uint32_t k) {
-    return *reinterpret_cast<const u64 *>(&p.ops[doc.op_off + k].value);
-}
+// an op's 8-byte value, staged in LDS with its row (an L2 re-read would put a global-load
+// round trip on the output phase's critical path)
+__device__ __forceinline__ u64 op_value(const SmallLds &L, uint32_t k) { return L.opval[k]; }
 // dep row -> actor << 24 | seq (all ones: outside the envelope)
 __device__ __forceinline__ uint32_t pack_dep(uint2 w) {
     const uint32_t a = w.x & 0xFFFF;
@@ -489,6 +495,7 @@ __device__ __forceinline__ void stage_op(const SmallLds &L, uint32_t k, uint32_t
     L.opro[k] = reg | (obj << 16);
     L.oppar[k] = (uint16_t)(a.z == HM_HEAD ? PAR_HEAD : (a.z < 0xFFFEu ? a.z : 0xFFFEu));
     L.opmeta[k] = b.x & 0xFFFFFFu;
+    L.opval[k] = ((u64)b.w << 32) | b.z;
     if (LISTS) L.opelem[k] = a.w;
 }
 template <int OPL, bool LISTS>
@@ -560,7 +567,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     lds_min(&L.first[a8 * 64 + (slot & 63)], act ? lane : 0xFFFFFFFFu);
     {
         const uint32_t o0 = c.op_first - doc.op_off;       // ops -> arrival index of their change
-        if (act) for (uint32_t j = 0; j < c.n_ops; j++) L.opchg[o0 + j] = (uint8_t)lane;
+        if (act) for (uint32_t j = 0; j < c.n_ops; j++) L.opchg[o0 + j] = (uint16_t)(lane | (a8 << 8));
     }
     wave_sync();
 
@@ -973,24 +980,24 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     if (hv && !((covered >> lane) & 1)) L.headv[hactor] = hseq;     // opSet.deps
     for (uint32_t i = lane; i < O; i += WAVE) { L.objslot[i] = i == 0 ? 0u : 0xFFFFFFFFu; L.objtype[i] = i == 0 ? HM_MAKE_MAP : 0xFF; }
     for (uint32_t i = lane; i < R; i += WAVE) {
-        L.segor[i] = 0; L.segcnt[i] = 0; L.survcnt[i] = 0; L.insmin[i] = 0xFFFFFFFFu; L.regobj[i] = HM_NONE;
+        L.segor[i] = 0; L.segcnt[i] = 0; L.survpk[i] = 0; L.insmin[i] = 0xFFFFFFFFu; L.regobj[i] = HM_NONE;
     }
     wave_sync();
 
     STAMP(L, 5);
     if (HM_ABLATE & 2) return OUT_UNSUPPORTED;
     // ---------------- K2: ops (lane + 64*t) ----------------
-    uint32_t oreg[OPL], oobj[OPL], opar[OPL], oact[OPL], okey[OPL], oarr[OPL], oelem[OPL];
+    uint32_t oreg[OPL], oobj[OPL], opar[OPL], oact[OPL], okey[OPL], oarr[OPL], oelem[OPL], oactor[OPL];
     int32_t oh[OPL];
     bool counter_ops = false, malformed = false;
 #pragma unroll
     for (int t = 0; t < OPL; t++) {
         const uint32_t k = lane + WAVE * t;
-        oh[t] = -1; okey[t] = 0; oarr[t] = 0; oreg[t] = 0; oobj[t] = 0; opar[t] = 0; oact[t] = 0xFF; oelem[t] = 0;
+        oh[t] = -1; okey[t] = 0; oarr[t] = 0; oreg[t] = 0; oobj[t] = 0; opar[t] = 0; oact[t] = 0xFF; oelem[t] = 0; oactor[t] = 0;
         if (k < m) {
             const uint32_t meta = L.opmeta[k], ro = L.opro[k], pr = L.oppar[k];
-            const uint32_t ch = L.opchg[k];
-            oarr[t] = ch; oh[t] = identity ? (int32_t)ch : L.hist_of[ch];
+            const uint32_t cw = L.opchg[k], ch = cw & 0xFFu;
+            oarr[t] = ch; oactor[t] = cw >> 8; oh[t] = identity ? (int32_t)ch : L.hist_of[ch];
             oreg[t] = ro & 0xFFFFu; oobj[t] = ro >> 16; oact[t] = meta & 0xFF;
             opar[t] = pr == PAR_HEAD ? HM_HEAD : pr;
             if (LISTS) {
@@ -1032,7 +1039,6 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
             else L.objtype[oobj[t]] = (uint8_t)oact[t];
         }
     wave_sync();
-    uint32_t sslot[OPL];
     bool surv[OPL];
     bool has_list = false;
     u64 errk = ~0ull;                    // this lane's earliest throw (one wave-wide min below)
@@ -1061,7 +1067,8 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         ek = ek < e1 ? ek : e1; ek = ek < e2 ? ek : e2; ek = ek < e3 ? ek : e3;
         errk = errk < ek ? errk : ek;
         surv[t] = sl && !((so >> h) & 1);
-        sslot[t] = lds_add(&L.survcnt[ri], surv[t] ? 1u : 0u);
+        // survivors counted per (register, actor rank): the rank below needs no survivor list
+        if (surv[t]) lds_add(&L.survpk[ri], 1ull << (8 * oactor[t]));
     }
     lds_min(L.errkey, errk);
     const bool doc_lists = __ballot(has_list) != 0;
@@ -1072,57 +1079,30 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
 
     STAMP(L, 7);
     if (HM_ABLATE & 4) return OUT_UNSUPPORTED;
-    // survivor offsets: exclusive scan over register ids
+    // survivor offsets: exclusive scan over register ids (a register's count = its byte sum)
     uint32_t total = 0;
     for (uint32_t r0 = 0; r0 < R; r0 += WAVE) {
         const uint32_t r = r0 + lane;
         uint32_t tot;
-        const uint32_t ex = wave_excl_scan(r < R ? L.survcnt[r] : 0u, &tot);
-        if (r < R) L.regoff[r] = total + ex;
+        const uint32_t cnt = r < R ? bytesum64(L.survpk[r]) : 0u;
+        const uint32_t ex = wave_excl_scan(cnt, &tot);
+        if (r < R) { L.regoff[r] = total + ex; L.survcnt[r] = cnt; }
         total += tot;
     }
     wave_sync();
-    // survivor slots hold op | actor << 16: one LDS word per slot for the rank scans
-    uint32_t my_act[OPL], rb0[OPL], rcnt[OPL];
+    // rank: actor rank descending = the survivors of higher actors on the register (bytes above
+    // this actor's); equal actors (ties) are ordered below
+    uint32_t my_act[OPL], rb0[OPL], rank[OPL];
+    bool tie[OPL];
 #pragma unroll
     for (int t = 0; t < OPL; t++) {
         const uint32_t ri = surv[t] ? oreg[t] : 0u;
-        my_act[t] = surv[t] ? (uint32_t)L.chactor[oarr[t]] : 0u;
+        my_act[t] = surv[t] ? oactor[t] : 0u;
         rb0[t] = L.regoff[ri];
-        rcnt[t] = surv[t] ? L.survcnt[ri] : 0u;
-        if (surv[t]) { sslot[t] += rb0[t]; L.survent[sslot[t]] = (lane + WAVE * t) | (my_act[t] << 16); }
-    }
-    wave_sync();
-    // rank: actor rank descending ...  (every slot of this lane scanned in the same rounds,
-    // 4 entries per slot per round: registers rarely hold more than 4 survivors)
-    uint32_t rank[OPL];
-    bool tie[OPL];
-    constexpr int RG = OPL < 2 ? OPL : 2;      // op slots scanned together (register budget)
-#pragma unroll
-    for (int t = 0; t < OPL; t++) { rank[t] = 0; tie[t] = false; }
-#pragma unroll
-    for (int g = 0; g < OPL; g += RG) {
-        uint32_t cmax = 0;
-#pragma unroll
-        for (int t = g; t < g + RG; t++) cmax = cmax > rcnt[t] ? cmax : rcnt[t];
-        for (uint32_t q0 = 0; q0 < cmax; q0 += 4) {
-            uint32_t e[RG][4];
-#pragma unroll
-            for (int t = g; t < g + RG; t++)
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const uint32_t q = q0 + i < rcnt[t] ? q0 + i : (rcnt[t] ? rcnt[t] - 1 : 0u);
-                    e[t - g][i] = L.survent[rb0[t] + q];
-                }
-#pragma unroll
-            for (int t = g; t < g + RG; t++)
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const bool v = q0 + i < rcnt[t] && (e[t - g][i] & 0xFFFFu) != lane + WAVE * t;
-                    rank[t] += v && (e[t - g][i] >> 16) > my_act[t] ? 1u : 0u;
-                    tie[t] |= v && (e[t - g][i] >> 16) == my_act[t];
-                }
-        }
+        const u64 pk = L.survpk[ri];
+        const uint32_t sh = 8 * (my_act[t] + 1);
+        rank[t] = surv[t] ? bytesum64(sh >= 64 ? 0ull : pk >> sh) : 0u;
+        tie[t] = surv[t] && ((pk >> (8 * my_act[t])) & 0xFF) > 1;
     }
     bool anytie = false;
 #pragma unroll
@@ -1195,13 +1175,13 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         u64 basev[OPL];
 #pragma unroll
         for (int t = 0; t < OPL; t++) {
-            incv[t] = (oh[t] >= 0 && oact[t] == HM_INC) ? (int64_t)op_value(p, doc, lane + WAVE * t) : 0;
+            incv[t] = (oh[t] >= 0 && oact[t] == HM_INC) ? (int64_t)op_value(L, lane + WAVE * t) : 0;
             const uint32_t q = lane + WAVE * t;
             basev[t] = 0;
             if (q < total) {
                 const uint32_t k = L.survop[q], mt = L.opmeta[k];
                 if ((mt & 0xFF) == HM_SET && ((mt >> 8) & 0xFF) == HM_DT_COUNTER && ((mt >> 16) & 0xFF) == HM_V_INT)
-                    basev[t] = op_value(p, doc, k);
+                    basev[t] = op_value(L, k);
             }
         }
 #pragma unroll
@@ -1216,7 +1196,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
                 const uint32_t k2 = L.survop[b0 + q];
                 const uint32_t m2 = L.opmeta[k2], vt2 = (m2 >> 16) & 0xFF;
                 if ((m2 & 0xFF) != HM_SET || ((m2 >> 8) & 0xFF) != HM_DT_COUNTER || (vt2 != HM_V_INT && vt2 != HM_V_FLOAT)) continue;
-                if (!((an >> L.hist_of[L.opchg[k2]]) & 1)) continue;
+                if (!((an >> L.hist_of[L.opchg[k2] & 0xFFu]) & 1)) continue;
                 // f64 counters need the ordered sum
                 if (vt2 != HM_V_INT || my_vtag != HM_V_INT || (u64)(v < 0 ? -v : v) >= (1ull << 44)) { outside = true; continue; }
                 lds_add((LDS u64 *)&L.survsum[b0 + q], (unsigned long long)v);
@@ -1276,23 +1256,14 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
             hm_doc_result r = {};
             r.status = HM_DEFERRED; r.err_change = HM_NONE; r.err_op = HM_NONE;
             *dres = r;
+#if !HM_ABLATE
             p.deferred[atomicAdd(p.n_deferred, 1u)] = d;     // merge_large_kernel's work list
+#endif
         }
         return;
     }
-    // survivors' values are re-read from their op rows (L2-resident): issue those loads and
-    // the minimumClock row first, store them last
     uint32_t mc = 0;
     if (p.min_clock && lane < S) mc = p.min_clock[(size_t)ds * S + lane];
-    constexpr int SV = OPL < 2 ? OPL : 2;      // survivor slots whose loads go first (register budget)
-    uint32_t sop[SV], smt[SV];
-    u64 sval[SV];
-#pragma unroll
-    for (int t = 0; t < SV; t++) {
-        const uint32_t q = lane + WAVE * t;
-        sop[t] = 0; smt[t] = 0; sval[t] = 0;
-        if (q < st.total) { sop[t] = L.survop[q]; smt[t] = L.opmeta[sop[t]]; sval[t] = op_value(p, doc, sop[t]); }
-    }
     for (uint32_t r = lane; r < R; r += WAVE) {
         hm_reg_result rr;
         rr.n_surv = L.survcnt[r]; rr.surv_off = L.regoff[r]; rr.obj = L.regobj[r];
@@ -1338,10 +1309,8 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
     for (int t = 0; t < OPL; t++) {
         const uint32_t q = lane + WAVE * t;
         if (q >= st.total) continue;
-        uint32_t k, mt;
-        u64 v;
-        if (t < SV) { k = sop[t < SV ? t : 0]; mt = smt[t < SV ? t : 0]; v = sval[t < SV ? t : 0]; }
-        else { k = L.survop[q]; mt = L.opmeta[k]; v = op_value(p, doc, k); }
+        const uint32_t k = L.survop[q], mt = L.opmeta[k];
+        const u64 v = op_value(L, k);
         hm_surv_result sr;
         sr.op = k; sr.vtag = (mt >> 16) & 0xFF; sr.value = v;
         const uint32_t smt_t = mt;
@@ -1368,8 +1337,8 @@ void merge_small_kernel(SmallParams p) {
 #if HM_STAMPS
     if (threadIdx.x == 0) { for (int i = 0; i < HM_NSTAMP; i++) L.stamps[i] = 0; L.stamps[HM_NSTAMP] = stamp_now(); }
 #endif
-    bool dok;
-    hm_doc_row doc = read_doc(p, d, dok);
+    hm_doc_row doc = p.docs[d];
+    bool dok = check_doc(p, doc);
     uint2 w0, w1, w2;                        // this document's change row (lane = arrival index)
     {
         const Rows r = load_rows<OPL>(p, doc);
@@ -1384,18 +1353,18 @@ void merge_small_kernel(SmallParams p) {
         const bool more = dn < p.n_docs;
         bool dokn = true;
         hm_doc_row docn = {};
-        if (more) docn = read_doc(p, dn, dokn);
+        if (more) docn = p.docs[dn];
         Rows next;
 #if HM_PREFETCH_EARLY
-        if (more) next = load_rows<OPL>(p, docn);
+        if (more) { dokn = check_doc(p, docn); next = load_rows<OPL>(p, docn); }
 #endif
-        const bool in_env = doc.n_changes <= 64 && doc.n_actors <= NA_MAX && doc.n_ops <= WAVE * OPL &&
+        const bool in_env = doc.n_changes <= 64 && doc.n_actors <= NA_MAX && doc.n_ops <= WAVE * OPL && doc.n_ops < 256 &&
                             doc.n_regs <= p.cap_regs && doc.n_objs <= p.cap_objs && doc.n_objs >= 1 &&
                             doc.n_deps <= p.cap_deps && !p.general_only;
         DocState st;
         const Outcome oc = !dok ? OUT_INVALID : in_env ? merge_doc_small<OPL, LISTS>(p, L, doc, w0, w1, w2, st) : OUT_UNSUPPORTED;
 #if !HM_PREFETCH_EARLY
-        if (more) next = load_rows<OPL>(p, docn);
+        if (more) { dokn = check_doc(p, docn); next = load_rows<OPL>(p, docn); }
 #endif
         STAMP(L, 9);
         write_outputs<OPL, LISTS>(p, L, d, doc, oc, st);

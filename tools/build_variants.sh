@@ -1,11 +1,14 @@
 #!/bin/bash
 # Build A/B variants of libhmgpu.so for tools/ablate.py: tools/build_variants.sh name:"-DFLAG=1 ..." ...
 #   -> hypermerge_amd/_lib/ablate/lib_<name>.so   (dev tool; the product build is hypermerge_amd/build.py)
-cd "$(dirname "$0")/../hypermerge_amd/_lib" && mkdir -p ablate && cd ablate
+# CSRC=<dir> builds from another source tree (e.g. a `git worktree` of an older commit).
+R="$(cd "$(dirname "$0")/.." && pwd)"
+SRC="${CSRC:-$R/hypermerge_amd/csrc}"
+mkdir -p "$R/hypermerge_amd/_lib/ablate" && cd "$R/hypermerge_amd/_lib/ablate"
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -mllvm -amdgpu-atomic-optimizer-strategy=DPP $flags -o lib_$name.so \
-    ../../csrc/merge_kernels.hip ../../csrc/merge_large.hip ../../csrc/store_kernels.hip ../../csrc/engine.cpp ../../csrc/store.cpp &
+    $SRC/merge_kernels.hip $SRC/merge_large.hip $SRC/store_kernels.hip $SRC/exchange.hip $SRC/engine.cpp $SRC/store.cpp -ldl &
 done
 wait
 ls
