@@ -523,6 +523,40 @@ struct DocState {
     bool doc_lists;
 };
 
+// Per-op checks of K2 against the document's objects / elements: the first throw kind of the
+// op (0 none; ordered as the reference checks them: unknown object, then duplicate or
+// missing list element, the engine's insert-after-unknown envelope), whether a set/link
+// survives, and whether it touches a list.  Reads only LDS (K2's tables), so the rare
+// error-key pass can recompute it instead of keeping it live.
+struct OpCheck { uint32_t err; bool surv, has_list; };
+__device__ __forceinline__ OpCheck op_check(const SmallLds &L, int32_t ohv, uint32_t act, uint32_t obj, uint32_t reg,
+                                            uint32_t par, uint32_t okey, uint32_t R, uint32_t O) {
+    const bool asg = ohv >= 0 && act >= HM_INS && act <= HM_INC && reg < R;
+    const uint32_t oi = obj < O ? obj : 0u, ri = reg < R ? reg : 0u;
+    const uint32_t pi = par < R ? par : 0u;
+    const uint32_t os = obj < O ? L.objslot[oi] : 0xFFFFFFFFu;
+    const uint32_t ot = L.objtype[oi], im = L.insmin[ri], ip = L.insmin[pi];
+    const u64 so = L.segor[ri];
+    const uint32_t h = ohv < 0 ? 0u : (uint32_t)ohv;
+    const bool unknown = asg && (os == 0xFFFFFFFFu || os > okey);     // 'Modification of unknown object'
+    const bool known = asg && !unknown;
+    const bool is_list = ot == HM_MAKE_LIST || ot == HM_MAKE_TEXT;
+    const bool ins = known && act == HM_INS;
+    const bool sl = known && (act == HM_SET || act == HM_LINK);
+    OpCheck r;
+    r.has_list = ins || (known && is_list);
+    r.surv = sl && !((so >> h) & 1);
+    // (history, op) keys are shared by an op's checks, so the earliest code of one op wins:
+    // unknown object < duplicate element < missing element < the insert-after envelope
+    uint32_t e = 0;
+    if (ins && par != HM_HEAD && !(ip <= okey)) e = HM_ERR_UNSUPPORTED;      // insert after an element not yet inserted
+    if (sl && is_list && !(im <= okey)) e = HM_ERR_MISSING_ELEM;            // 'Missing index entry for list element'
+    if (ins && im != okey + 1) e = HM_ERR_DUPLICATE_ELEM;                   // 'Duplicate list element ID'
+    if (unknown) e = HM_ERR_UNKNOWN_OBJECT;
+    r.err = e;
+    return r;
+}
+
 // Merge one document with the whole wave (no global stores).  Every return is wave-uniform.
 template <int OPL, bool LISTS>
 __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const SmallLds &L, const hm_doc_row &doc,
@@ -595,38 +629,33 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     const uint32_t first_me = act ? L.first[actor * 64 + slot] : lane;
     const bool dup = act && first_me != lane;
     const uint32_t cid_first = shfl32(c.content_id, (int)(first_me & 63));
-    // per-actor clock requirement relative to the batch's first seq of that actor,
-    // packed as bytes (0x7F = never satisfiable in this batch)
-    uint32_t need_lo = 0, need_hi = 0;
     u64 dmask = 0;                       // direct deps in arrival-index space (fast path)
     uint32_t pred_arr = 0xFFu;
     bool ok = true;                      // ready on arrival
     bool own_row = false;                // the deps map lists the change's own actor
     wave_sync();
     {
-        // predicated over the wave's longest deps map, 4 deps per round (reads in flight together)
+        // predicated over the wave's longest deps map, 2 deps per round (reads in flight together)
         const uint32_t maxd = wave_max(act ? (uint32_t)c.n_deps : 0u);
-        for (uint32_t j0 = 0; j0 < maxd; j0 += 4) {
-            uint32_t inf[4];
+        for (uint32_t j0 = 0; j0 < maxd; j0 += 2) {
+            uint32_t inf[2];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < 2; u++) {
                 const bool live = act && j0 + u < c.n_deps;
                 inf[u] = L.depinfo[live ? my_dep0 + j0 + u : 0u];
             }
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < 2; u++) {
                 const bool live = act && j0 + u < c.n_deps;
                 const uint32_t a = (inf[u] >> 16) & (NA_MAX - 1), rel = (inf[u] >> 8) & 0x7F, f = inf[u] & 0x7F;
                 own_row |= live && a == actor;
                 const bool use = live && a != actor && rel != 0;                // deps.set(actor, seq-1) overrides
-                need_set(need_lo, need_hi, a, use ? rel : 0u);
                 ok = ok && !(use && (rel == 0x7F || f >= lane));
                 dmask |= (use && rel != 0x7F && f < lane) ? (1ull << f) : 0ull;
             }
         }
         const uint32_t ps = seq - 1;
         const bool hp = act && ps != 0, inb = ps >= mybase;
-        need_set(need_lo, need_hi, a8, hp ? (inb ? ps - mybase + 1 : 0x7Fu) : 0u);
         const uint32_t f = L.first[a8 * 64 + ((ps - mybase) & 63)];
         ok = ok && !(hp && (!inb || f >= lane));
         const bool pv = hp && inb && f < lane;
@@ -822,6 +851,18 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         }
     } else {
         // ---- exact emulation of addChange / applyQueuedOps (wave-uniform control) ----
+        // per-actor clock requirement relative to the batch's first seq of that actor, packed
+        // as bytes (0x7F = never satisfiable in this batch)
+        uint32_t need_lo = 0, need_hi = 0;
+        if (act) {
+            for (uint32_t j = 0; j < c.n_deps; j++) {
+                const uint32_t inf = L.depinfo[my_dep0 + j];
+                const uint32_t a = (inf >> 16) & (NA_MAX - 1), rel = (inf >> 8) & 0x7F;
+                need_set(need_lo, need_hi, a, (a != actor && rel != 0) ? rel : 0u);   // deps.set(actor, seq-1) overrides
+            }
+            const uint32_t ps = seq - 1;
+            need_set(need_lo, need_hi, a8, ps != 0 ? (ps >= mybase ? ps - mybase + 1 : 0x7Fu) : 0u);
+        }
         clear_first(L.first);                                                           // -> applied lane
         wave_sync();
         uint32_t crel_lo = 0, crel_hi = 0;      // relative applied clock per actor (bytes)
@@ -887,6 +928,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     }
 
     STAMP(L, 3);
+    if (HM_ABLATE & 512) return OUT_UNSUPPORTED;
     // ---------------- K1b: ancestor sets in history order ----------------
     if (act) L.hist_of[lane] = hist;
     if (act && hist >= 0) L.h2a[hist] = (uint8_t)lane;
@@ -921,6 +963,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     // Per step: v_readlane of lane k, bit k of D as an all-ones mask (v_bfe_i32), v_and_or.
     // Positions below 32 only have low-word ancestors.
     uint32_t alo = hv && lane < 32 ? 1u << lane : 0u, ahi = hv && lane >= 32 ? 1u << (lane - 32) : 0u;
+    if (HM_ABLATE & 1024) return OUT_UNSUPPORTED;
     {
         const uint32_t Hs = (uint32_t)__builtin_amdgcn_readfirstlane((int)H);
         const uint32_t Dlo = (uint32_t)D, Dhi = (uint32_t)(D >> 32);
@@ -973,6 +1016,9 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         h_own_row = shfl32(h_own_row, (int)ai); h_dep0 = shfl32(my_dep0, (int)ai); h_nd = shfl32(c.n_deps, (int)ai);
     }
     suspect |= hv && h_own_row != 0;
+#ifdef HM_DEV_NOFOLD
+    suspect = false;                    // dev-only timing build: skips the literal-fold check
+#endif
     if (suspect) {
         const FoldView fv = {L.anc, L.chain, L.first, L.base, L.deps, L.hist_of};
         if (fold_differs(fv, h_dep0, h_nd, hactor, hseq)) lds_or(L.flags, FL_UNSUPPORTED);
@@ -1040,37 +1086,29 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         }
     wave_sync();
     bool surv[OPL];
-    bool has_list = false;
-    u64 errk = ~0ull;                    // this lane's earliest throw (one wave-wide min below)
+    bool has_list = false, anyerr = false;
 #pragma unroll
     for (int t = 0; t < OPL; t++) {
         // predicated: every lane reads (clamped) and decides with selects, no per-op branches
-        const bool asg = oh[t] >= 0 && oact[t] >= HM_INS && oact[t] <= HM_INC && oreg[t] < R;
-        const uint32_t oi = oobj[t] < O ? oobj[t] : 0u, ri = oreg[t] < R ? oreg[t] : 0u;
-        const uint32_t pi = opar[t] < R ? opar[t] : 0u;
-        const uint32_t os = oobj[t] < O ? L.objslot[oi] : 0xFFFFFFFFu;
-        const uint32_t ot = L.objtype[oi], im = L.insmin[ri], ip = L.insmin[pi];
-        const u64 so = L.segor[ri];
-        const uint32_t h = oh[t] < 0 ? 0u : (uint32_t)oh[t], kk = (okey[t] & 0xFFFF) + 1;
-        const bool unknown = asg && (os == 0xFFFFFFFFu || os > okey[t]);    // 'Modification of unknown object'
-        const bool known = asg && !unknown;
-        const bool is_list = ot == HM_MAKE_LIST || ot == HM_MAKE_TEXT;
-        const bool ins = known && oact[t] == HM_INS;
-        const bool sl = known && (oact[t] == HM_SET || oact[t] == HM_LINK);
-        has_list |= ins || (known && is_list);
-        u64 ek = unknown ? err_key(h, kk, oarr[t], HM_ERR_UNKNOWN_OBJECT) : ~0ull;
-        const u64 e1 = ins && im != okey[t] + 1 ? err_key(h, kk, oarr[t], HM_ERR_DUPLICATE_ELEM) : ~0ull;
-        // engine envelope, ordered like a throw: insert after an element not yet inserted
-        const u64 e2 = ins && opar[t] != HM_HEAD && !(ip <= okey[t]) ? err_key(h, kk, oarr[t], HM_ERR_UNSUPPORTED) : ~0ull;
-        // 'Missing index entry for list element'
-        const u64 e3 = sl && is_list && !(im <= okey[t]) ? err_key(h, kk, oarr[t], HM_ERR_MISSING_ELEM) : ~0ull;
-        ek = ek < e1 ? ek : e1; ek = ek < e2 ? ek : e2; ek = ek < e3 ? ek : e3;
-        errk = errk < ek ? errk : ek;
-        surv[t] = sl && !((so >> h) & 1);
+        const OpCheck ck = op_check(L, oh[t], oact[t], oobj[t], oreg[t], opar[t], okey[t], R, O);
+        has_list |= ck.has_list;
+        anyerr |= ck.err != 0;
+        surv[t] = ck.surv;
         // survivors counted per (register, actor rank): the rank below needs no survivor list
-        if (surv[t]) lds_add(&L.survpk[ri], 1ull << (8 * oactor[t]));
+        if (surv[t]) lds_add(&L.survpk[oreg[t]], 1ull << (8 * oactor[t]));
     }
-    lds_min(L.errkey, errk);
+    if (__ballot(anyerr)) {
+        // a throw: its key (history position, op, arrival) orders it against the others
+        u64 errk = ~0ull;                // this lane's earliest throw (one wave-wide min below)
+#pragma unroll
+        for (int t = 0; t < OPL; t++) {
+            const OpCheck ck = op_check(L, oh[t], oact[t], oobj[t], oreg[t], opar[t], okey[t], R, O);
+            const uint32_t h = oh[t] < 0 ? 0u : (uint32_t)oh[t], kk = (okey[t] & 0xFFFF) + 1;
+            const u64 ek = ck.err ? err_key(h, kk, oarr[t], ck.err) : ~0ull;
+            errk = errk < ek ? errk : ek;
+        }
+        lds_min(L.errkey, errk);
+    }
     const bool doc_lists = __ballot(has_list) != 0;
     if (!LISTS && doc_lists) lds_or(L.flags, FL_UNSUPPORTED);   // launched without the K3 carve
     wave_sync();

@@ -1,21 +1,16 @@
 #!/bin/bash
-# Per-phase instruction counts: one PMC pass per ablation build (hypermerge_amd/_lib/ablate/lib_aNNN.so),
-# merge_small_kernel only.  Differences between consecutive stop points = the phase's counts.
+# Per-phase instruction counts of merge_small_kernel from ablation builds (tools/build_variants.sh
+# s008:-DHM_ABLATE=8 ...): one rocprofv3 PMC pass per library.  Usage: tools/phase_pmc.sh <tag> lib...
 set -o pipefail
+TAG=$1; shift
 R=$PWD
-mkdir -p gpurun_out/phase
+OUT=$R/gpurun_out/$TAG
+mkdir -p $OUT
 export TMPDIR=/tmp
-for so in ${@:-$R/hypermerge_amd/_lib/ablate/lib_a*.so}; do
-  t=$(basename $so .so)
-  ( cd /tmp && HMGPU_LIB=$so timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD --output-format csv -d $R/gpurun_out/phase/$t -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu > $R/gpurun_out/phase/$t.log 2>&1 ) || { echo "fail $t"; exit 1; }
-  python3 - $R/gpurun_out/phase/$t <<'PY'
-import csv, glob, sys
-from collections import defaultdict
-acc = defaultdict(list)
-for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
-    for row in csv.DictReader(open(f)):
-        if "merge_small_kernel" in row["Kernel_Name"]:
-            acc[row["Counter_Name"]].append(float(row["Counter_Value"]))
-print(sys.argv[1].split("/")[-1], " ".join(f"{k}={sum(v)/len(v)/1e6:.1f}" for k, v in sorted(acc.items())), "(per launch /1e6 ~ per doc)")
-PY
+cd /tmp
+for so in "$@"; do
+  n=$(basename $so .so)
+  HMGPU_LIB=$R/$so timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH SQ_IFETCH --output-format csv -d $OUT/$n -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu --no-traffic --no-e2e --no-orders --check-docs 0 > $OUT/$n.log 2>&1 || exit 1
+  python3 $R/tools/pmc_summary.py $OUT/$n > $OUT/$n.json
+  python3 -c "import json;d=json.load(open('$OUT/$n.json'));print('$n', ' '.join(f'{k}={v/1e6:.1f}' for k,v in sorted(d.items())))"
 done

@@ -5,7 +5,7 @@ from collections import defaultdict
 d = sys.argv[1]
 K = sys.argv[2] if len(sys.argv) > 2 else "merge_small_kernel"
 out = {}
-for f in glob.glob(os.path.join(d, "pmc*", "**", "*counter_collection.csv"), recursive=True):
+for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
     acc = defaultdict(list)
     for row in csv.DictReader(open(f)):
         if K not in row.get("Kernel_Name", ""):
