@@ -21,7 +21,7 @@
 #include "merge_kernels.h"
 
 #define LWG 256
-#define LA_MAX 32
+#define LA_MAX 64
 // LDS arena per workgroup (u32 words): 36 KB keeps 4 workgroups per CU (the VGPR-bound
 // occupancy at 128 VGPRs).  Documents whose L2 closure rows (2·n·A + T words) or L4 Euler
 // tour (E words, 16-bit links) fit run those phases out of LDS instead of the pool.
@@ -46,6 +46,7 @@ typedef unsigned long long u64;
 // longer lists build per-actor maxima with atomics (SEG_SHORT assign lists cost one LDS row
 // read each, where every assign's A atomicMax on shared L2 lines cost ~27 % of C3's kernel)
 #define SEG_SHORT 8
+#define ORDERED (1ull << 63)     // survabs flag: a counter survivor whose incs are summed in application order
 
 namespace hml {
 
@@ -86,6 +87,7 @@ enum : uint32_t { LF_UNSUPPORTED = 1u, LF_NOPOOL = 2u };
 
 // device-scope relaxed atomics on pool (global) pointers
 template <typename T> __device__ __forceinline__ T g_add(GLB T *p, T v) { return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <typename T> __device__ __forceinline__ T g_or(GLB T *p, T v) { return __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 template <typename T> __device__ __forceinline__ T g_min(GLB T *p, T v) { return __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 template <typename T> __device__ __forceinline__ T g_max(GLB T *p, T v) { return __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
@@ -785,11 +787,57 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
             if (o2.action != HM_SET || o2.datatype != HM_DT_COUNTER || (o2.vtag != HM_V_INT && o2.vtag != HM_V_FLOAT)) continue;
             const uint32_t c2 = opchg_of(k2);
             if (ad_of(ci, act_of(c2)) < seq_of(c2)) continue;                 // concurrent inc: no effect
-            if (o2.vtag != HM_V_INT || o.vtag != HM_V_INT) { atomicOr(&sh.flags, LF_UNSUPPORTED); continue; }
+            // a non-integral base or inc: JS adds doubles, whose sum depends on the order the incs
+            // are applied in -> the survivor is folded sequentially below (ORDERED)
+            if (o2.vtag != HM_V_INT || o.vtag != HM_V_INT) { g_or(&X.survabs[b0 + q], ORDERED); continue; }
             const int64_t v = (int64_t)o.value;
             g_add((GLB u64 *)&X.survsum[b0 + q], (u64)v);
             g_add(&X.survabs[b0 + q], (u64)(v < 0 ? -v : v));
         }
+    }
+    bsync();
+    // ORDERED survivors (Automerge 0.12 applyAssign): fold the incs of
+    // the register that causally follow the counter set, in application order (history
+    // position, op index) — one thread per survivor, the next inc found by a min-scan of the
+    // register's assign list (seglist keys).  Integer + integer adds stay int64 until the first
+    // non-integral operand; from there on the value is an IEEE double, as the JS sum is.
+    for (uint32_t q = tid; q < total; q += LWG) {
+        if (!(X.survabs[q] & ORDERED)) continue;
+        const uint32_t k2 = X.survop[q];
+        const hm_op_row o2 = OP[k2];
+        const uint32_t c2 = opchg_of(k2), a2 = act_of(c2), s2 = seq_of(c2), reg = o2.reg;
+        const uint32_t b0 = X.segoff[reg], cnt = X.segcnt[reg];
+        bool is_int = o2.vtag == HM_V_INT;
+        u64 acc = o2.value;
+        u64 prev = 0;
+        bool first = true;
+        for (;;) {
+            u64 best = ~0ull;
+            uint32_t bk = 0;
+            for (uint32_t e = 0; e < cnt; e++) {
+                const uint32_t sk = X.segk[b0 + e];
+                if (!(sk & 0x80000000u)) continue;                             // incs only
+                const u64 key = X.seglist[b0 + e];
+                if ((!first && key <= prev) || key >= best) continue;
+                const uint32_t ki = sk & 0x7FFFFFFFu;
+                if (ad_of(opchg_of(ki), a2) < s2) continue;                    // concurrent inc: no effect
+                best = key; bk = ki;
+            }
+            if (best == ~0ull) break;
+            const hm_op_row oi = OP[bk];
+            if (is_int && oi.vtag == HM_V_INT) {
+                acc = (u64)((int64_t)acc + (int64_t)oi.value);
+            } else {
+                const double x = is_int ? (double)(int64_t)acc : __longlong_as_double((long long)acc);
+                const double y = oi.vtag == HM_V_INT ? (double)(int64_t)oi.value : __longlong_as_double((long long)oi.value);
+                acc = (u64)__double_as_longlong(x + y);
+                is_int = false;
+            }
+            prev = best;
+            first = false;
+        }
+        X.survsum[q] = (int64_t)acc;                                            // the folded value's bits
+        if (is_int) atomicOr(&sh.flags, LF_UNSUPPORTED);                       // (a float operand was seen: unreachable)
     }
     bsync();
     if (sh.flags) return LUNSUP;
@@ -930,7 +978,9 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
         const uint32_t k = X.survop[q];
         const hm_op_row o = OP[k];
         hm_surv_result sr; sr.op = k; sr.vtag = o.vtag; sr.value = o.value;
-        if (o.action == HM_SET && o.datatype == HM_DT_COUNTER && o.vtag == HM_V_INT) {
+        if (X.survabs[q] & ORDERED) {
+            sr.vtag = HM_V_FLOAT; sr.value = (u64)X.survsum[q];
+        } else if (o.action == HM_SET && o.datatype == HM_DT_COUNTER && o.vtag == HM_V_INT) {
             const int64_t b = (int64_t)o.value;
             if (X.survabs[q] + (u64)(b < 0 ? -b : b) > (1ull << 53)) atomicOr(&sh.flags, LF_UNSUPPORTED);
             sr.value = (u64)(b + X.survsum[q]);

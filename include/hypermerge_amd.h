@@ -271,7 +271,7 @@ int hm_clock_intersection_device(hm_engine *e, const uint32_t *a, const uint32_t
 typedef struct hm_store hm_store;
 
 typedef struct {
-    uint32_t a_stride;      /* per-actor row width of every document (1..32) */
+    uint32_t a_stride;      /* per-actor row width of every document (1..64) */
     uint32_t reserved;
 } hm_store_config;
 

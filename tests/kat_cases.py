@@ -69,6 +69,31 @@ CASES = [
     ("counter_concurrent_sets", [ch(A, 1, {}, s("n", 1, datatype="counter")), ch(B, 1, {}, s("n", 100, datatype="counter")),
                                  ch(Cc, 1, {A: 1, B: 1}, inc("n", 7))],
      {"state": {"map": [["n", {"value": 107, "datatype": "counter", "conflicts": [[A, 8]]}]]}}),
+    # non-integral counters: JS adds doubles, in the order the incs are applied
+    # (0.1 + 0.2) + 0.3 = 0.6000000000000001, not 0.1 + (0.2 + 0.3) = 0.6
+    ("counter_float_order", [ch(A, 1, {}, s("n", 0.1, datatype="counter")), ch(B, 1, {A: 1}, inc("n", 0.2)),
+                             ch(A, 2, {B: 1}, inc("n", 0.3))],
+     {"state": {"map": [["n", {"value": (0.1 + 0.2) + 0.3, "datatype": "counter"}]]}}),
+    # history order, not arrival order: B1 waits for A2, so 0.3 is applied before 0.2
+    ("counter_float_history_order", [ch(B, 1, {A: 2}, inc("n", 0.2)), ch(A, 1, {}, s("n", 0.1, datatype="counter")),
+                                     ch(A, 2, {A: 1}, inc("n", 0.3))],
+     {"state": {"map": [["n", {"value": (0.1 + 0.3) + 0.2, "datatype": "counter"}]]},
+      "history": [[A, 1], [A, 2], [B, 1]]}),
+    # integer adds stay exact until the first non-integral operand
+    ("counter_int_then_float", [ch(A, 1, {}, s("n", 1, datatype="counter")), ch(A, 2, {}, inc("n", 2)),
+                                ch(B, 1, {A: 2}, inc("n", 0.5))],
+     {"state": {"map": [["n", {"value": 3.5, "datatype": "counter"}]]}}),
+    # a concurrent non-integral inc does not touch the counter
+    ("counter_float_concurrent", [ch(A, 1, {}, s("n", 2.5, datatype="counter")), ch(B, 1, {}, inc("n", 0.25)),
+                                  ch(A, 2, {A: 1}, inc("n", 1))],
+     {"state": {"map": [["n", {"value": 3.5, "datatype": "counter"}]]}}),
+    # 40 actors setting one key concurrently: winner = highest actor string, 39 conflicts in
+    # actor-descending order (wide documents: no actor limit in the reference)
+    ("forty_actors_concurrent", [ch(f"w{i:02d}", 1, {}, s("x", i)) for i in range(40)],
+     {"state": {"map": [["x", {"value": 39, "conflicts": [[f"w{i:02d}", i] for i in range(38, -1, -1)]}]]}}),
+    # ... and a 40-actor causal chain: each actor overwrites the previous one's value
+    ("forty_actors_chain", [ch(f"w{i:02d}", 1, ({f"w{i - 1:02d}": 1} if i else {}), s("x", i)) for i in range(40)],
+     {"state": {"map": [["x", {"value": 39}]]}, "deps": {"w39": 1}}),
     # ties: one change setting a key twice -> "append, then reverse" after every assign
     ("tie_two_sets", [ch(A, 1, {}, s("x", "first"), s("x", "second"))],
      {"state": {"map": [["x", {"value": "second", "conflicts": [[A, "first"]]}]]}}),

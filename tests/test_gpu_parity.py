@@ -269,3 +269,51 @@ def test_malformed_doc_rows_are_invalid_per_document(engine):
     S = b.a_stride
     keep = np.repeat([d not in badset for d in range(b.n_docs)], S)
     np.testing.assert_array_equal(g.back_clock[keep], o.back_clock[keep])
+
+
+def _float_counter_docs(n_docs, seed, n_actors=4, wide=False):
+    """Random documents of counters with integral and non-integral incs, concurrent and
+    causal, delivered shuffled (queued changes); `wide`: 9-40 actors per document."""
+    import random
+    from hypermerge_amd.columnar import ROOT_ID as R
+    rng = random.Random(seed)
+    docs = []
+    for _ in range(n_docs):
+        na = rng.randint(9, 40) if wide else n_actors
+        actors = [f"act{rng.randrange(10 ** 6):06d}{i}" for i in range(na)]
+        seqs = {a: 0 for a in actors}
+        heard = {a: {} for a in actors}
+        chs = []
+        for i in range(rng.randint(4, 48)):
+            a = rng.choice(actors)
+            seqs[a] += 1
+            ops = []
+            for _ in range(rng.randint(1, 3)):
+                key = f"c{rng.randrange(3)}"
+                if rng.random() < 0.25:
+                    v = rng.choice([rng.randint(-5, 5), rng.randint(-50, 50) / 10, rng.random()])
+                    ops.append({"action": "set", "obj": R, "key": key, "value": v, "datatype": "counter"})
+                else:
+                    v = rng.choice([rng.randint(-9, 9), rng.randint(-90, 90) / 8, rng.random() * 3])
+                    ops.append({"action": "inc", "obj": R, "key": key, "value": v})
+            deps = {b: s for b, s in heard[a].items() if b != a}
+            chs.append({"actor": a, "seq": seqs[a], "deps": deps, "ops": ops})
+            for b in actors:                                   # gossip: some actors hear of it
+                if b == a or rng.random() < 0.5:
+                    heard[b][a] = seqs[a]
+        if rng.random() < 0.5:
+            rng.shuffle(chs)
+        docs.append(chs)
+    return docs
+
+
+@pytest.mark.parametrize("wide", [False, True], ids=["4actors", "wide"])
+def test_float_counters_random(engine, engine_general, wide):
+    """Non-integral counter sums in application order, on both kernels (the small kernel
+    hands such documents to the general one), bit-exact with the oracle; wide documents
+    (up to 40 actors) too."""
+    b = encode(_float_counter_docs(300, 17 + wide, wide=wide))
+    o = O.merge(b)
+    assert (o.docs["status"] == 0).sum() > 250
+    assert_same(b, engine.merge(b), o)
+    assert_same(b, engine_general.merge(b), o)
