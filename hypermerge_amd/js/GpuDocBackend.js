@@ -46,20 +46,39 @@ class History {
     const st = this.state
     const lo = a || 0
     const hi = b === undefined ? this.size : Math.min(b, this.size)
-    const idx = addon.historyPrefix(st.engine.store, st.handle, Math.max(hi, 0))
+    const idx = addon.historyPrefix(st.store, st.handle, Math.max(hi, 0))
     const out = []
     for (let i = lo; i < idx.length / 4; i++) out.push(st.log[idx.readUInt32LE(4 * i)])
     return { toArray: () => out, size: out.length }
   }
 }
 
-// The per-document BackendState: a handle into the device store plus the host-side
-// interner and the change objects of the log (for history slices).  States are linear:
-// applyChanges advances the document in place and returns the same state object.
+// FNV-1a 64 over the UTF-8 bytes of an id string: the shard key (and the clock exchange's
+// record key) of hypermerge_amd/exchange.py and include/hypermerge_amd.h.
+const FNV_OFFSET = 0xcbf29ce484222325n, FNV_PRIME = 0x100000001b3n, M64 = (1n << 64n) - 1n
+function fnv1a64(s) {
+  let h = FNV_OFFSET
+  for (const b of Buffer.from(s, 'utf8')) h = ((h ^ BigInt(b)) * FNV_PRIME) & M64
+  return h
+}
+
+// Row widths of the stores a document can live in: a document starts in the narrowest that
+// holds its actors and moves to a wider one when a new actor outgrows it (its whole log is
+// re-merged there, once).
+const STRIDES = [8, 16, 32, 64]
+
+// The per-document BackendState: a handle into one device store (its shard's, at its stride)
+// plus the host-side interner and the change objects of the log (for history slices and
+// re-striding).  States are linear: applyChanges advances the document in place and returns
+// the same state object.
 class GpuBackendState {
-  constructor(engine) {
+  constructor(engine, docId) {
     this.engine = engine
-    this.handle = addon.openDoc(engine.store)
+    this.docId = docId
+    this.shard = docId === undefined ? 0 : engine.shardOf(docId)
+    this.stride = engine.minStride
+    this.store = engine.storeFor(this.shard, this.stride)
+    this.handle = addon.openDoc(this.store)
     this.enc = new C.DocEncoder(engine.pool)
     this.log = []
     this.opActor = []                // doc-local op index -> [op, actor] (the log's ops in order)
@@ -68,6 +87,7 @@ class GpuBackendState {
     this.nQueued = 0
     this.clock = {}
     this.deps = {}
+    this.backClock = {}              // DocBackend.clock as the engine computed it (queued included)
   }
 
   getIn(p) {
@@ -79,21 +99,37 @@ class GpuBackendState {
 }
 
 class GpuEngine {
+  // opts: devices (HIP ordinals; documents shard over them by FNV-1a64(docId) % devices.length),
+  // aStride (narrowest store stride), mode 'sync' | 'batched', onError, patches
   constructor(opts) {
     const o = opts || {}
-    this.aStride = o.aStride || 8
+    this.devices = o.devices || [o.device || 0]
+    this.minStride = o.aStride || 8
+    this.aStride = this.minStride
     this.mode = o.mode || 'batched'
-    this.store = addon.createStore(o.device || 0, this.aStride)
+    this.shards = this.devices.map((d) => ({ device: d, stores: new Map() }))
+    this.store = this.storeFor(0, this.minStride)
     this.pool = new C.StringPool()
     this.queues = new Map()          // state -> FIFO of jobs
     this.flushing = false
     this.scheduled = false
     this.onError = o.onError || null
     this.submits = 0
+    this.restrides = 0
     this.patches = o.patches !== false  // emit patch diffs (one device read per patch)
+    this.comm = null
   }
 
-  init() { return new GpuBackendState(this) }
+  shardOf(docId) { return Number(fnv1a64(docId) % BigInt(this.shards.length)) }
+
+  storeFor(shard, stride) {
+    const sh = this.shards[shard]
+    let st = sh.stores.get(stride)
+    if (!st) { st = addon.createStore(sh.device, stride); sh.stores.set(stride, st) }
+    return st
+  }
+
+  init(docId) { return new GpuBackendState(this, docId) }
 
   // job: {changes|null, extraActors, done(result|null), fail(err)}
   enqueue(state, job) {
@@ -130,42 +166,67 @@ class GpuEngine {
     }
   }
 
+  // One applyChanges per document of the round: the documents of each store (device shard x
+  // stride) go to that store as one batch; every store's batch is submitted before any is
+  // waited for, so the devices merge at once.
   runRound(round) {
-    const appends = [], snaps = [], handles = new Uint32Array(round.length)
-    round.forEach(([state, job], i) => {
-      snaps.push(state.enc.snapshot())
-      const a = state.enc.encode(job.changes, job.extraActors)
-      if (a.nActors > this.aStride) {
-        state.enc.restore(snaps[i])
-        throw new Error(`document has ${a.nActors} actors > engine aStride ${this.aStride}`)
-      }
-      appends.push(a)
-      handles[i] = state.handle
-    })
-    const b = C.buildBatch(appends, this.aStride)
-    const id = addon.submit(this.store, b.docs, b.changes, b.deps, b.ops, handles, b.remap)
-    const r = addon.wait(this.store, id, round.length)
-    this.submits++
-    const S = this.aStride
+    const groups = new Map()         // store -> [{state, job, snap, append, moved}]
     const errors = []
-    round.forEach(([state, job], i) => {
-      const res = C.readDocResult(r.docs, i)
-      if (res.status !== 0) {
-        state.enc.restore(snaps[i])
-        errors.push([job, this.errorFor(state, job.changes, res)])
-        return
+    for (const [state, job] of round) {
+      const snap = state.enc.snapshot()
+      let a = state.enc.encode(job.changes, job.extraActors)
+      let moved = null
+      if (a.nActors > state.stride) {
+        // a new actor outgrew the document's store: re-merge its whole log in a wider one
+        state.enc.restore(snap)
+        const stride = STRIDES.find((x) => x >= a.nActors)
+        if (stride === undefined) {
+          errors.push([job, new Error(`document has ${a.nActors} actors > ${STRIDES[STRIDES.length - 1]}`)])
+          continue
+        }
+        const enc = new C.DocEncoder(this.pool)
+        const store = this.storeFor(state.shard, stride)
+        a = enc.encode(state.log.concat(job.changes), job.extraActors)
+        moved = { enc, store, stride, handle: addon.openDoc(store) }
       }
-      const base = state.log.length
-      state.log.push(...job.changes)
-      for (const c of job.changes) for (const op of c.ops || []) state.opActor.push([op, c.actor])
-      const prevHist = state.histLen
-      state.histLen = res.histLen
-      state.nQueued = res.nQueued
-      state.clock = Clock.fromRow(r.clock, i * S * 4, state.enc.actors)
-      state.deps = Clock.fromRow(r.heads, i * S * 4, state.enc.actors)
-      const backClock = Clock.fromRow(r.backClock, i * S * 4, state.enc.actors)
-      job.done({ res, base, prevHist, backClock, minCmp: Clock.CMP_CODES[res.minCmp] })
-    })
+      const store = moved ? moved.store : state.store
+      if (!groups.has(store)) groups.set(store, [])
+      groups.get(store).push({ state, job, snap, append: a, moved })
+    }
+    const pending = []
+    for (const [store, items] of groups) {
+      const stride = items[0].moved ? items[0].moved.stride : items[0].state.stride
+      const b = C.buildBatch(items.map((it) => it.append), stride)
+      const handles = Uint32Array.from(items.map((it) => (it.moved ? it.moved.handle : it.state.handle)))
+      pending.push([store, stride, items, addon.submit(store, b.docs, b.changes, b.deps, b.ops, handles, b.remap)])
+    }
+    for (const [store, S, items, id] of pending) {
+      const r = addon.wait(store, id)
+      this.submits++
+      items.forEach(({ state, job, snap, moved }, i) => {
+        const res = C.readDocResult(r.docs, i)
+        if (res.status !== 0) {
+          if (!moved) state.enc.restore(snap)
+          errors.push([job, this.errorFor(state, job.changes, res)])
+          return
+        }
+        if (moved) {
+          Object.assign(state, { enc: moved.enc, store: moved.store, stride: moved.stride, handle: moved.handle })
+          this.restrides++
+        }
+        const base = state.log.length
+        state.log.push(...job.changes)
+        for (const c of job.changes) for (const op of c.ops || []) state.opActor.push([op, c.actor])
+        const prevHist = state.histLen
+        state.histLen = res.histLen
+        state.nQueued = res.nQueued
+        state.clock = Clock.fromRow(r.clock, i * S * 4, state.enc.actors)
+        state.deps = Clock.fromRow(r.heads, i * S * 4, state.enc.actors)
+        const backClock = Clock.fromRow(r.backClock, i * S * 4, state.enc.actors)
+        state.backClock = backClock
+        job.done({ res, base, prevHist, backClock, minCmp: Clock.CMP_CODES[res.minCmp] })
+      })
+    }
     for (const [job, err] of errors) {
       if (job.fail) job.fail(err)
       else if (this.onError) this.onError(err)
@@ -201,6 +262,44 @@ class GpuEngine {
     if (err) throw err
     return out
   }
+
+  // ---- the node-wide ClockStore feed (CursorMessage clocks, src/RepoBackend.ts:374-392) ----
+  // Every shard's documents' DocBackend.clock entries as repo-global records
+  // (FNV-1a64(docId), FNV-1a64(actorId), seq) gathered across the devices over RCCL
+  // (hm_comm_create_local + hm_clock_exchange_host) when they are distinct GPUs, and
+  // turned back into {docId: {actorId: seq}} with the host's id tables.
+  exchangeClocks(states) {
+    const perShard = this.shards.map(() => [])
+    const ids = new Map()
+    for (const st of states) {
+      const dk = fnv1a64(st.docId)
+      ids.set(dk, st.docId)
+      for (const [a, s] of Object.entries(st.backClock)) {
+        const ak = fnv1a64(a)
+        ids.set(ak, a)
+        perShard[st.shard].push([dk, ak, s])
+      }
+    }
+    const bufs = perShard.map((rows) => {
+      const b = Buffer.alloc(rows.length * 24)
+      rows.forEach(([dk, ak, s], i) => { b.writeBigUInt64LE(dk, 24 * i); b.writeBigUInt64LE(ak, 24 * i + 8); b.writeUInt32LE(s, 24 * i + 16) })
+      return b
+    })
+    let all
+    const distinct = new Set(this.devices).size === this.devices.length
+    if (distinct) {
+      if (!this.comm) this.comm = addon.commCreateLocal(this.shards.map((sh) => this.storeFor(this.shards.indexOf(sh), this.minStride)))
+      all = addon.clockExchange(this.comm, bufs)
+    } else all = Buffer.concat(bufs)           // shards sharing one device: the host holds them all
+    const out = {}
+    for (let i = 0; i < all.length / 24; i++) {
+      const doc = ids.get(all.readBigUInt64LE(24 * i)), actor = ids.get(all.readBigUInt64LE(24 * i + 8))
+      const c = out[doc] || (out[doc] = {})
+      const s = all.readUInt32LE(24 * i + 16)
+      if (!(actor in c) || s > c[actor]) c[actor] = s
+    }
+    return out
+  }
 }
 
 // ---------------- patches (Automerge makePatch, consumed by Frontend.applyPatch) ----------------
@@ -232,7 +331,7 @@ function opValue(state, vtag, lo, hi) {
 
 // the merged document as {objUuid -> {type, keys: Map(key -> entry) | elems: [[elemId, entry]]}}
 function materialize(state) {
-  const r = addon.read(state.engine.store, state.handle)
+  const r = addon.read(state.store, state.handle)
   const objType = new Map([[0, 0]])
   for (const [op] of state.opActor) {
     const a = C.ACTIONS[op.action]
@@ -314,7 +413,7 @@ function makePatch(state) {
 
 function makeBackend(engine) {
   return {
-    init: () => engine.init(),
+    init: (docId) => engine.init(docId),
     applyChanges: (state, changes) => {
       engine.applyChanges(state, changes)
       return [state, makePatch(state)]
@@ -387,7 +486,7 @@ class DocBackend {
   }
 
   init(changes, actorId) {
-    const state = this.engine.init()
+    const state = this.engine.init(this.id)
     this.engine.enqueue(state, { changes, done: () => {
       this.actorId = this.actorId || actorId
       this.back = state
@@ -484,26 +583,38 @@ class ClockStore {
   // (written) and which inputs differ from the stored clock (updateQ).
   updateDocs(repoId, docs) {
     if (!docs.length) return []
-    const handles = Uint32Array.from(docs.map((d) => d.back.handle))
-    const r = addon.clockUpdate(this.engine.store, handles)
-    const S = this.engine.aStride
-    return docs.map((doc, i) => {
-      const actors = doc.back.enc.actors
-      const k = this.key(repoId, doc.id)
-      if (r.written[i]) {
-        const stored = Clock.fromRow(r.stored, i * S * 4, actors)
-        let m = this.rows.get(k)
-        if (!m) { m = new Map(); this.rows.set(k, m) }
-        for (const [a, s] of Object.entries(stored)) if (!m.has(a) || s > m.get(a)) m.set(a, s)
-      }
-      const d = [repoId, doc.id, this.get(repoId, doc.id)]
-      if (r.differs[i]) this.updateQ.push(d)
-      return d
+    // one device upsert-max per store holding some of the documents
+    const byStore = new Map()
+    docs.forEach((doc, i) => {
+      const st = doc.back.store
+      if (!byStore.has(st)) byStore.set(st, [])
+      byStore.get(st).push(i)
     })
+    const out = new Array(docs.length)
+    for (const [store, idx] of byStore) {
+      const handles = Uint32Array.from(idx.map((i) => docs[i].back.handle))
+      const r = addon.clockUpdate(store, handles)
+      const S = docs[idx[0]].back.stride
+      idx.forEach((i, j) => {
+        const doc = docs[i]
+        const actors = doc.back.enc.actors
+        const k = this.key(repoId, doc.id)
+        if (r.written[j]) {
+          const stored = Clock.fromRow(r.stored, j * S * 4, actors)
+          let m = this.rows.get(k)
+          if (!m) { m = new Map(); this.rows.set(k, m) }
+          for (const [a, s] of Object.entries(stored)) if (!m.has(a) || s > m.get(a)) m.set(a, s)
+        }
+        const d = [repoId, doc.id, this.get(repoId, doc.id)]
+        if (r.differs[j]) this.updateQ.push(d)
+        out[i] = d
+      })
+    }
+    return out
   }
 }
 
 // SQLite's BINARY collation (memcmp of UTF-8) orders the Clocks primary key
 function byteOrder(a, b) { return Buffer.compare(Buffer.from(a, 'utf8'), Buffer.from(b, 'utf8')) }
 
-module.exports = { GpuEngine, GpuBackendState, DocBackend, ClockStore, makeBackend, addon }
+module.exports = { GpuEngine, GpuBackendState, DocBackend, ClockStore, makeBackend, materialize, fnv1a64, addon }

@@ -289,6 +289,93 @@ static napi_value ClockUpdate(napi_env env, napi_callback_info info) {
     return o;
 }
 
+/* ---- clock exchange across the devices of one process (include/hypermerge_amd.h) ---- */
+typedef struct { int n; hm_comm *comms[64]; } Comms;
+
+static void comms_finalize(napi_env env, void *data, void *hint) {
+    (void)env; (void)hint;
+    Comms *c = (Comms *)data;
+    for (int i = 0; i < c->n; i++) hm_comm_destroy(c->comms[i]);
+    free(c);
+}
+
+/* commCreateLocal([store per device]) -> comm: one rank per store's engine (distinct GPUs) */
+static napi_value CommCreateLocal(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return NULL;
+    uint32_t n = 0;
+    if (napi_get_array_length(env, argv[0], &n) != napi_ok || n < 1 || n > 64) {
+        napi_throw_range_error(env, NULL, "expected 1..64 stores");
+        return NULL;
+    }
+    hm_engine *engines[64];
+    for (uint32_t i = 0; i < n; i++) {
+        napi_value v;
+        CHECK_NAPI(napi_get_element(env, argv[0], i, &v));
+        Store *s = get_store(env, v);
+        if (!s) return NULL;
+        engines[i] = s->engine;
+    }
+    Comms *c = (Comms *)calloc(1, sizeof(Comms));
+    c->n = (int)n;
+    int st = hm_comm_create_local(engines, (int)n, c->comms);
+    if (st) { free(c); return throw_status(env, engines[0], st, "hm_comm_create_local"); }
+    napi_value out;
+    CHECK_NAPI(napi_create_external(env, c, comms_finalize, NULL, &out));
+    return out;
+}
+
+static Comms *get_comms(napi_env env, napi_value v) {
+    void *p = NULL;
+    if (napi_get_value_external(env, v, &p) != napi_ok || !p) { napi_throw_type_error(env, NULL, "expected a comm handle"); return NULL; }
+    return (Comms *)p;
+}
+
+/* clockExchange(comm, [Buffer of 24 B hm_clock_rec per rank]) -> Buffer: every rank's
+ * records in rank order (hm_clock_exchange_host: RCCL over the devices) */
+static napi_value ClockExchange(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return NULL;
+    Comms *c = get_comms(env, argv[0]);
+    if (!c) return NULL;
+    const hm_clock_rec *recs[64];
+    uint64_t n[64], total = 0;
+    for (int i = 0; i < c->n; i++) {
+        napi_value v; void *p; size_t len;
+        CHECK_NAPI(napi_get_element(env, argv[1], (uint32_t)i, &v));
+        if (!get_bytes(env, v, &p, &len)) return NULL;
+        recs[i] = (const hm_clock_rec *)p; n[i] = len / sizeof(hm_clock_rec); total += n[i];
+    }
+    hm_clock_rec *out = (hm_clock_rec *)malloc((total + 1) * sizeof(hm_clock_rec));
+    uint64_t got = 0;
+    int st = hm_clock_exchange_host(c->comms, c->n, recs, n, out, total, &got);
+    if (st) { free(out); return throw_status(env, NULL, st, "hm_clock_exchange_host"); }
+    napi_value r = buf_copy(env, out, got * sizeof(hm_clock_rec));
+    free(out);
+    return r;
+}
+
+/* clockMin(comm, [Uint32Array per rank, equal lengths]): every row <- the MIN over the rows
+ * (hm_clock_min_host) */
+static napi_value ClockMin(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return NULL;
+    Comms *c = get_comms(env, argv[0]);
+    if (!c) return NULL;
+    uint32_t *rows[64];
+    size_t len0 = 0;
+    for (int i = 0; i < c->n; i++) {
+        napi_value v; void *p; size_t len;
+        CHECK_NAPI(napi_get_element(env, argv[1], (uint32_t)i, &v));
+        if (!get_bytes(env, v, &p, &len)) return NULL;
+        if (i && len != len0) { napi_throw_range_error(env, NULL, "rows differ in length"); return NULL; }
+        rows[i] = (uint32_t *)p; len0 = len;
+    }
+    int st = hm_clock_min_host(c->comms, c->n, rows, len0 / 4);
+    if (st) return throw_status(env, NULL, st, "hm_clock_min_host");
+    return NULL;
+}
+
 static napi_value StatusMessage(napi_env env, napi_callback_info info) {
     napi_value argv[1];
     if (!get_args(env, info, 1, argv)) return NULL;
@@ -304,6 +391,7 @@ static napi_value Init(napi_env env, napi_value exports) {
         {"createStore", CreateStore}, {"openDoc", OpenDoc}, {"submit", Submit}, {"wait", Wait},
         {"info", Info}, {"read", Read}, {"historyPrefix", HistoryPrefix}, {"setMinClock", SetMinClock},
         {"clockUpdate", ClockUpdate}, {"statusMessage", StatusMessage},
+        {"commCreateLocal", CommCreateLocal}, {"clockExchange", ClockExchange}, {"clockMin", ClockMin},
     };
     for (size_t i = 0; i < sizeof fns / sizeof fns[0]; i++) {
         napi_value f;

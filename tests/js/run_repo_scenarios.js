@@ -1,0 +1,128 @@
+'use strict'
+// Replays tests/golden/repo_scenarios.json (the reference tests' document-level expectations:
+// tests/repo.test.ts merge / fork, tests/multiple-repos.test.ts) through the GPU drop-in
+// DocBackend (hypermerge_amd/js/GpuDocBackend.js, mode 'sync' = the reference Queue's
+// synchronous delivery).  The RepoBackend host logic around it is the same restatement as
+// tests/repo_harness.py (CursorStore upsert-max, ClockStore, loadDocument, syncChanges,
+// CursorMessage handling); renders follow DocFrontend: minimumClockSatisfied && diffs.length.
+// Prints {scenario: {"repo/doc": [renders...]}} as one JSON line.
+const path = require('path')
+const fs = require('fs')
+const G = require(path.join(__dirname, '..', '..', 'hypermerge_amd', 'js', 'GpuDocBackend.js'))
+const Clock = require(path.join(__dirname, '..', '..', 'hypermerge_amd', 'js', 'clocks.js'))
+
+const gold = JSON.parse(fs.readFileSync(path.join(__dirname, '..', 'golden', 'repo_scenarios.json'), 'utf8'))
+const INF = gold.INF
+const ROOT = '00000000-0000-0000-0000-000000000000'
+const engine = new G.GpuEngine({ mode: 'sync', aStride: 8 })
+
+function plain(view, uuid) {
+  const ov = view.get(uuid)
+  if (!ov) return {}
+  const val = (e) => (e.link ? plain(view, e.value) : e.value)
+  if (ov.type === 'list' || ov.type === 'text') return ov.elems.filter(Boolean).map(([, e]) => val(e))
+  const o = {}
+  for (const [k, e] of ov.keys) o[k] = val(e)
+  return o
+}
+const render = (doc) => plain(G.materialize(doc.back), ROOT)
+
+function runScenario(steps) {
+  const repos = new Map()
+  const clocks = new Map()                      // `${repo}\0${doc}` -> {actor: seq}  (ClockStore)
+  const clockKey = (r, d) => r + '\u0000' + d
+  const clocksUpdate = (r, d, c) => {
+    const cur = clocks.get(clockKey(r, d)) || {}
+    for (const [a, s] of Object.entries(c)) if (!(a in cur) || s > cur[a]) cur[a] = s
+    clocks.set(clockKey(r, d), cur)
+  }
+  const clocksGet = (r, d) => Object.assign({}, clocks.get(clockKey(r, d)) || {})
+  const repo = (id) => {
+    if (!repos.has(id)) repos.set(id, { id, docs: new Map(), feeds: new Map(), cursors: new Map(), watched: new Map() })
+    return repos.get(id)
+  }
+  const cursorUpdate = (R, doc, clock) => {
+    const cur = R.cursors.get(doc) || {}
+    for (const [a, s0] of Object.entries(clock)) { const s = Math.min(s0, INF); if (!(a in cur) || s > cur[a]) cur[a] = s }
+    R.cursors.set(doc, cur)
+  }
+  const notifier = (R) => (m) => {
+    const d = R.docs.get(m.id)
+    if (m.type === 'LocalPatchMsg') { const f = R.feeds.get(m.change.actor) || []; f.push(m.change); R.feeds.set(m.change.actor, f) }
+    if ((m.type === 'RemotePatchMsg' || m.type === 'LocalPatchMsg') && m.minimumClockSatisfied) clocksUpdate(R.id, m.id, d.clock)
+    if (R.watched.has(m.id) && m.patch && m.type !== 'ReadyMsg' && m.minimumClockSatisfied && m.patch.diffs.length > 0)
+      R.watched.get(m.id).push(render(d))
+  }
+  const syncChanges = (R, actor) => {
+    const feed = R.feeds.get(actor) || []
+    for (const [docId, cur] of R.cursors) {
+      const d = R.docs.get(docId)
+      if (!(actor in cur) || !d) continue
+      d.ready.push(() => {
+        const max = cur[actor], min = d.changes.get(actor) || 0
+        const out = []
+        let i = min
+        for (; i < max && i < feed.length; i++) out.push(feed[i])
+        d.changes.set(actor, i)
+        if (out.length) d.applyRemoteChanges(out)
+      })
+    }
+  }
+  for (const st of steps) {
+    const [op] = st
+    if (op === 'create') {
+      const R = repo(st[1])
+      const d = new G.DocBackend(st[2], notifier(R), engine.init(st[2]), engine)
+      R.docs.set(st[2], d)
+      cursorUpdate(R, st[2], { [st[2]]: INF })
+      for (const c of st[3]) d.applyLocalChange(c)
+    } else if (op === 'open') {
+      const R = repo(st[1])
+      const d = new G.DocBackend(st[2], notifier(R), undefined, engine)
+      R.docs.set(st[2], d)
+      cursorUpdate(R, st[2], { [st[2]]: INF })
+      const changes = []
+      for (const a of Object.keys(R.cursors.get(st[2]))) {
+        const sl = (R.feeds.get(a) || []).slice(0, R.cursors.get(st[2])[a])
+        d.changes.set(a, sl.length)
+        changes.push(...sl)
+      }
+      cursorUpdate(R, st[2], { [st[3]]: INF })
+      d.init(changes, st[3])
+    } else if (op === 'watch') {
+      const R = repo(st[1]), d = R.docs.get(st[2])
+      R.watched.set(st[2], [])
+      if (d.back && d.minimumClockSatisfied) R.watched.get(st[2]).push(render(d))
+    } else if (op === 'merge') {
+      const R = repo(st[1])
+      cursorUpdate(R, st[2], st[3])
+      for (const a of Object.keys(st[3])) syncChanges(R, a)
+    } else if (op === 'change') {
+      repo(st[1]).docs.get(st[2]).applyLocalChange(st[3])
+    } else if (op === 'cursor_message') {
+      const S = repo(st[1]), R = repo(st[2]), doc = st[3]
+      clocksUpdate(S.id, doc, clocksGet(S.id, doc))
+      cursorUpdate(R, doc, S.cursors.get(doc) || {})
+      const d = R.docs.get(doc)
+      if (d) d.updateMinimumClock(clocksGet(S.id, doc))
+      for (const a of Object.keys(S.cursors.get(doc) || {})) if (R.feeds.has(a)) syncChanges(R, a)
+    } else if (op === 'download') {
+      const S = repo(st[1]), R = repo(st[2])
+      R.feeds.set(st[3], (S.feeds.get(st[3]) || []).slice())
+      syncChanges(R, st[3])
+    } else if (op === 'expect_cursor') {
+      const want = {}
+      for (const [a, v] of Object.entries(st[3])) want[a] = v === 'INF' ? INF : v
+      const got = repo(st[1]).cursors.get(st[2]) || {}
+      if (!Clock.equal(got, want) || Object.keys(got).length !== Object.keys(want).length)
+        throw new Error(`cursor ${JSON.stringify(st)}: ${JSON.stringify(got)}`)
+    } else throw new Error(op)
+  }
+  const out = {}
+  for (const R of repos.values()) for (const [d, v] of R.watched) out[`${R.id}/${d}`] = v
+  return out
+}
+
+const result = {}
+for (const [name, sc] of Object.entries(gold.scenarios)) result[name] = runScenario(sc.steps)
+process.stdout.write(JSON.stringify(result) + '\n')

@@ -109,3 +109,63 @@ def test_materialize_history_prefix():
     got = json.loads(p.stdout)
     assert got["materialized"] == {"1": "bar0", "2": "bar1", "3": "bar2", "4": "bar3"}
     assert got["history"] == 4 and got["types"] == ["ReadyMsg", "LocalPatchMsg", "LocalPatchMsg", "LocalPatchMsg"]
+
+
+def test_repo_scenarios_on_gpu():
+    """The reference tests' document-level expectations (tests/golden/repo_scenarios.json:
+    repo.test.ts merge / fork, multiple-repos.test.ts share and three-way minimumClock gate)
+    replayed through the GPU drop-in DocBackend: every watched document renders exactly the
+    documents the reference tests expect."""
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "repo_scenarios.json")))
+    p = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "run_repo_scenarios.js")],
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    got = json.loads(p.stdout.strip().splitlines()[-1])
+    for name, sc in gold["scenarios"].items():
+        for key, want in sc["renders"].items():
+            assert got[name][key] == want, (name, key, got[name][key])
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0]], ids=["two-shards-one-device", "rccl-one-rank"])
+def test_sharded_engine_restride_and_clock_exchange(devices):
+    """GpuEngine with device shards (FNV-1a64(docId) % G routing) and stride classes: wide
+    documents (9-40 actors) move to wider stores as actors arrive; every document's state
+    equals the oracle's, and exchangeClocks returns every document's {actorId: seq} clock
+    (RCCL over the devices when they are distinct GPUs)."""
+    import random
+    import oracle.oracle as O
+    from hypermerge_amd.columnar import encode
+    from hypermerge_amd.render import doc_state
+    from repo_harness import plain
+    from test_gpu_parity import _float_counter_docs
+    rng = random.Random(5)
+    docs = {}
+    for i, chs in enumerate(_float_counter_docs(40, 99, wide=True) + _float_counter_docs(40, 98)):
+        # causal delivery in 1-4 batches (queued changes would stay queued across batches too)
+        cuts = sorted(rng.sample(range(1, len(chs)), min(3, len(chs) - 1))) if len(chs) > 1 else []
+        parts, prev = [], 0
+        for c in cuts + [len(chs)]:
+            parts.append(chs[prev:c])
+            prev = c
+        docs[f"doc{i:03d}-{rng.randrange(10 ** 9)}"] = parts
+    p = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "run_sharding.js"), json.dumps(devices)],
+                       input=json.dumps(docs), capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    got = json.loads(p.stdout.strip().splitlines()[-1])
+    assert got["restrides"] > 0
+    shards = set()
+    for d, parts in docs.items():
+        log = [c for part in parts for c in part]
+        b = encode([log])
+        o = O.merge(b)
+        g = got["docs"][d]
+        assert g["shard"] == g["expectShard"]
+        shards.add(g["shard"])
+        assert g["stride"] >= len(b.doc_actors[0])
+        assert g["view"] == plain(doc_state(b, o, 0)), d
+        clock = {}
+        for c in log:
+            clock[c["actor"]] = max(clock.get(c["actor"], 0), c["seq"])
+        assert g["clock"] == clock
+        assert got["exchanged"][d] == clock
+    assert shards == set(range(len(devices)))

@@ -51,11 +51,12 @@ def test_incremental_log_equals_cold_encoding(name):
 def test_known_answers_split_in_two_calls(name, changes, expect):
     """applyChanges(applyChanges(init, A), B) == applyChanges(init, A ++ B) on the oracle
     over the incremental log, for every known-answer case and every split point."""
-    cold = encode([changes], 8)
+    S = max(8, len({c["actor"] for c in changes} | {a for c in changes for a in c["deps"]}))
+    cold = encode([changes], S)
     want = canonical_json(cold, O.merge(cold), 0)
     for cut in range(len(changes) + 1):
         e, _ = incremental_log(changes, [cut])
-        lb = e.log_batch(8)
+        lb = e.log_batch(S)
         assert canonical_json(lb, O.merge(lb), 0) == want, (name, cut)
 
 

@@ -6,11 +6,11 @@
 // minimumClockSatisfied snapshots.  Output: tests/golden/docbackend_traces.json.
 //
 // DocBackend's dependencies that are absent here are stubbed in a temp dir on NODE_PATH:
-//   automerge         — a minimal Backend whose applyChanges implements the causal queue
-//                       (Appendix A.1: duplicates dropped, passes until no progress) so
-//                       opSet.history.size is meaningful; everything DocBackend itself does
-//                       (queues, clock quirk, minimum clock, message order) is the
-//                       reference's own code;
+//   automerge         — a Backend whose applyChanges asks the CPU restatement (oracle/) for
+//                       the merged history size and applied clock of the changes handed so
+//                       far, so opSet.history.size follows the restated queue rules;
+//                       everything DocBackend itself does (queues, clock quirk, minimum
+//                       clock, message order) is the reference's own code;
 //   bs58, hypercore-crypto — never called on this path (imported by Keys.js).
 // Usage: node tools/golden/gen_docbackend_traces.js > tests/golden/docbackend_traces.json
 const fs = require('fs')
@@ -23,33 +23,23 @@ const stub = (name, src) => {
   fs.mkdirSync(path.join(tmp, name), { recursive: true })
   fs.writeFileSync(path.join(tmp, name, 'index.js'), src)
 }
+// the queue rules (history sizes, applied clock) come from the CPU restatement of Automerge
+// (oracle/oracle.c via tools/golden/oracle_history.py): every applyChanges re-merges the
+// changes handed so far (applyChanges is a left fold of addChange)
+const ORACLE = path.join(__dirname, 'oracle_history.py')
 stub('automerge', `
-function ready(clock, c) {
-  const need = Object.assign({}, c.deps || {}); need[c.actor] = c.seq - 1
-  return Object.keys(need).every((a) => (clock[a] || 0) >= need[a])
-}
+const { execFileSync } = require('child_process')
 function applyChanges(state, changes) {
-  const s = { clock: Object.assign({}, state.clock), queue: state.queue.slice(), history: state.history }
-  for (const c of changes) {
-    s.queue.push(c)
-    for (;;) {
-      let progress = false
-      const keep = []
-      for (const q of s.queue) {
-        if ((s.clock[q.actor] || 0) >= q.seq) { progress = true; continue }       // duplicate: no-op
-        if (ready(s.clock, q)) { s.clock[q.actor] = q.seq; s.history++; progress = true } else keep.push(q)
-      }
-      s.queue = keep
-      if (!progress) break
-    }
-  }
-  const st = mk(s)
-  return [st, { clock: Object.assign({}, s.clock), deps: {}, diffs: changes.length ? [{}] : [] }]
+  const log = state.log.concat(changes)
+  const r = JSON.parse(execFileSync('python3', [${JSON.stringify(ORACLE)}], { input: JSON.stringify(log) }).toString())
+  if (r.status !== 0) throw new Error('oracle status ' + r.status)
+  const st = mk({ log, history: r.history, clock: r.clock })
+  return [st, { clock: Object.assign({}, r.clock), deps: {}, diffs: changes.length ? [{}] : [] }]
 }
 function mk(s) {
   return Object.assign(s, { getIn: (p) => ({ size: s.history }) })
 }
-module.exports = { Backend: { init: () => mk({ clock: {}, queue: [], history: 0 }), applyChanges } }
+module.exports = { Backend: { init: () => mk({ log: [], history: 0, clock: {} }), applyChanges } }
 `)
 stub('bs58', 'module.exports = { encode: (b) => b.toString("hex"), decode: (s) => Buffer.from(s, "hex") }')
 stub('hypercore-crypto', 'module.exports = { keyPair: () => ({}), discoveryKey: (b) => b }')
