@@ -57,6 +57,10 @@ def main() -> int:
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host->device->host (PCIe-inclusive) leg")
     ap.add_argument("--no-orders", action="store_true", help="skip the C4 actor-major (loadDocument order) leg")
+    ap.add_argument("--block-docs", type=int, default=50_000,
+                    help="documents in the raw-blocks leg (JSON blocks -> native decoder -> merge)")
+    ap.add_argument("--no-incremental", action="store_true",
+                    help="skip the resident-store leg (1-2 new changes per resident document per round)")
     ap.add_argument("--arrival", type=int, default=None,
                     help="override the config's arrival order (0 generation, 1 actor-major as RepoBackend.loadDocument "
                          "concatenates, 2 shuffled)")
@@ -184,6 +188,16 @@ def main() -> int:
                          "same_results": ok,
                          "path": "hm_merge_host, page-locked (torch pin_memory) host tables and reused result arrays"}
         del pb, pr, keep
+    # from raw hypercore blocks: JSON blocks (as Block.pack writes them) -> the native
+    # multi-threaded decoder (hm_decode_blocks) -> hm_merge_host; reported beside `value`
+    from_blocks = None
+    if rank == 0 and ws == 1 and not args.no_e2e and args.config in ("C1", "C2", "C4") and args.block_docs > 0:
+        from_blocks = _from_blocks(eng, batch, cfg, args)
+    # applyRemoteChanges on resident documents: every document of the shard resident in the
+    # store, then rounds in which each receives its next 1-2 changes (DocBackend.ts:169-185)
+    incremental = None
+    if rank == 0 and ws == 1 and not args.no_incremental and args.config == "C4" and args.arrival is None:
+        incremental = _incremental(eng, batch, args)
     # the same workload in RepoBackend.loadDocument's arrival order (actor-major concatenation,
     # src/RepoBackend.ts:242-248): changes whose deps come later in the array wait in the queue
     orders = None
@@ -228,7 +242,9 @@ def main() -> int:
                          "frac": kern["frac"], "traffic": traffic["bytes"] if traffic else None,
                          "kernel": kern["kernel"], "kernel_ms": kern["kernel_ms"], "alg_bytes": kern["alg_bytes"],
                          "kernels": kern["kernels"], "traffic_detail": traffic},
-            "cpu_baseline": cpu, "cpu_parallel": cpu_mt, "end_to_end": e2e, "arrival_orders": orders,
+            "cpu_baseline": cpu, "cpu_parallel": cpu_mt, "end_to_end": e2e, "from_blocks": from_blocks,
+            "resident_incremental": incremental,
+            "arrival_orders": orders,
             "host": _host_info(),
             "parity_sample_ok": parity, "unsupported_docs": unsupported, "error_docs": errors,
             "gen_s": round(gen_s, 2), "event_ms_per_step": ev_ms / args.steps,
@@ -238,6 +254,93 @@ def main() -> int:
     if ws > 1:
         dist.destroy_process_group()
     return 0
+
+
+def _from_blocks(eng, batch, cfg, args):
+    """Raw blocks -> merged documents on a sample of this rank's shard: the changes rendered as
+    the JSON blocks Block.pack writes (src/Block.ts:6-16), decoded by hm_decode_blocks over the
+    host's threads (Block.unpack + JSON.parse + the row encoder), merged by hm_merge_host."""
+    from hypermerge_amd import synth
+    from hypermerge_amd.decode import decode_packed
+    k = min(args.block_docs, batch.n_docs)
+    sub = _subbatch(batch, k)
+    data, bo, db = synth.blocks(cfg, sub)
+    nth = min(16, os.cpu_count() or 1)
+    decode_packed(data, bo, db[:min(k, 100) + 1].copy(), a_stride=sub.a_stride, threads=nth, tables=False)
+    t0 = time.perf_counter()
+    d, st = decode_packed(data, bo, db, a_stride=sub.a_stride, threads=nth, tables=False)
+    t1 = time.perf_counter()
+    r = eng.merge(d)
+    t2 = time.perf_counter()
+    want = eng.merge(sub)
+    ok = bool((st == 0).all() and np.array_equal(r.docs, want.docs) and np.array_equal(r.clock, want.clock))
+    applied = float(r.docs["hist_len"].astype(np.int64).sum())
+    nb = int(len(bo) - 1)
+    return {"value": applied / (t2 - t0), "unit": "changes/s", "ms": (t2 - t0) * 1e3,
+            "decode": {"value": nb / (t1 - t0), "unit": "blocks/s", "MB_per_s": data.nbytes / (t1 - t0) / 1e6,
+                       "threads": nth, "ms": (t1 - t0) * 1e3},
+            "merge_ms": (t2 - t1) * 1e3, "blocks": nb, "bytes": int(data.nbytes), "docs": k,
+            "same_as_generated_rows": ok,
+            "path": "JSON blocks -> hm_decode_blocks (native, multi-threaded) -> hm_merge_host (PCIe included)"}
+
+
+def _incremental(eng, batch, args, tail=4):
+    """The north-star event on resident state: every document of the shard is resident in a
+    hm_store with all but its last `tail` changes; then rounds in which each document receives
+    its next 1-2 changes (hm_batch_submit + hm_batch_wait, H2D of the new rows and D2H of the
+    per-document results included).  The same rounds run on a second store with the
+    incremental path off (whole-log re-merge) for the comparison and an equality check."""
+    from hypermerge_amd.store import RowStore, slice_changes
+    n = batch.n_docs
+    nch = batch.docs["n_changes"].astype(np.int64)
+    start = np.maximum(nch - tail, 0)
+    rng = np.random.default_rng(5)
+    stores = []
+    for inc in (True, False):
+        st = RowStore(eng, a_stride=batch.a_stride)
+        st.set_incremental(inc)
+        h0 = st.open_n(n)
+        st.submit_batch(slice_changes(batch, np.zeros(n, np.int64), start), np.arange(h0, h0 + n))
+        st.wait()
+        stores.append((st, h0))
+    from hypermerge_amd.store import BatchResult
+    from hypermerge_amd.columnar import DOC_RESULT_DT
+    S = batch.a_stride
+    # result arrays kept between rounds, as a long-running RepoBackend keeps its buffers
+    outs = [BatchResult(np.zeros(n, DOC_RESULT_DT), np.zeros((n, S), np.uint32), np.zeros((n, S), np.uint32),
+                        np.zeros((n, S), np.uint32)) for _ in stores]
+    pos = start.copy()
+    rounds = []
+    same = True
+    while (pos < nch).any():
+        k = rng.integers(1, 3, n)
+        hi = np.minimum(pos + k, nch)
+        sel = np.nonzero(hi > pos)[0]
+        sub = slice_changes(batch, pos, hi, sel)
+        r = {"docs": int(len(sel)), "changes": int(len(sub.changes))}
+        res = []
+        for (st, h0), tag, keep in zip(stores, ("incremental", "remerge"), outs):
+            hs = (sel + h0).astype(np.uint32)
+            t = time.perf_counter()
+            st.submit_batch(sub, hs)
+            out = st.wait(keep)
+            dt = time.perf_counter() - t
+            res.append(out)
+            r[tag] = {"ms": dt * 1e3, "changes_per_s": len(sub.changes) / dt, "routing": st.last_routing()}
+        same &= bool(np.array_equal(res[0].docs, res[1].docs) and np.array_equal(res[0].clock, res[1].clock)
+                     and np.array_equal(res[0].heads, res[1].heads))
+        rounds.append(r)
+        pos = np.maximum(pos, hi)
+    tot_c = sum(r["changes"] for r in rounds)
+    t_inc = sum(r["incremental"]["ms"] for r in rounds) / 1e3
+    t_rem = sum(r["remerge"]["ms"] for r in rounds) / 1e3
+    for st, _ in stores:
+        st.close()
+    return {"value": tot_c / t_inc, "unit": "changes/s", "resident_docs": n,
+            "us_per_round": t_inc * 1e6 / len(rounds), "remerge_value": tot_c / t_rem,
+            "speedup_vs_remerge": t_rem / t_inc, "same_as_remerge": same, "rounds": rounds,
+            "path": "RowStore (hm_store): hm_batch_submit + hm_batch_wait per round, new rows H2D and "
+                    "per-document results D2H included; incremental = inc_apply_kernel"}
 
 
 def _clock_exchange(eng, batch, run, dev, rank, ws, cfg):

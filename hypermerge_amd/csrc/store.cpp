@@ -14,11 +14,16 @@
 // A document's segments have power-of-two capacities; an append that overflows one
 // moves the document to a fresh segment at the arena's end (append_kernel copies and
 // rebases the old rows once).  When an arena is full every document is compacted into
-// a new, larger arena and re-merged.  A submit appends the new rows and re-merges each
-// document's whole log with the batch merge kernels (applyChanges is a left fold of
-// addChange, so the state after A then B is the state after A ++ B).
+// a new, larger arena and re-merged.  A submit appends the new rows; a document whose new
+// changes apply in arrival order on its resident state (nothing queued, map ops) is
+// advanced in place by inc_apply_kernel, touching only the registers the new ops hit;
+// any other document re-merges its whole log with the batch merge kernels (applyChanges
+// is a left fold of addChange, so the state after A then B is the state after A ++ B).
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -74,9 +79,12 @@ struct hm_store {
     uint64_t next_id = 1, pending_id = 0;
     std::vector<uint32_t> p_handles;              // batch rows -> handles
     std::vector<DocMeta> p_old;                   // metas before the append (rollback)
-    std::vector<std::vector<uint8_t>> p_inverse;  // inverse remap per batch row (empty = none)
-    std::vector<uint8_t> p_out;                   // gathered results (host)
+    std::vector<int32_t> p_inv_row;               // batch row -> offset of its inverse remap in p_inv (-1 = none)
+    std::vector<uint8_t> p_inv;                   // inverse remap rows [S]
     uint8_t *p_gather_dev = nullptr;
+    // incremental applyRemoteChanges (inc_apply_kernel) and the last submit's routing
+    bool incremental = true;
+    uint32_t st_inc = 0, st_cold = 0, st_bail = 0;
 };
 
 namespace {
@@ -132,6 +140,22 @@ int ensure_handles(hm_store *s, size_t need) {
     return HM_OK;
 }
 
+// HM_STORE_PROFILE=1: per-phase wall times of hm_batch_submit / hm_batch_wait on stderr (the
+// stream is synchronised at each mark, so device work is attributed to its phase)
+struct PhaseTimer {
+    bool on;
+    hipStream_t st;
+    std::chrono::steady_clock::time_point t;
+    explicit PhaseTimer(hipStream_t s) : on(getenv("HM_STORE_PROFILE") != nullptr), st(s), t(std::chrono::steady_clock::now()) {}
+    void mark(const char *what) {
+        if (!on) return;
+        (void)hipStreamSynchronize(st);
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[hm_store] %-18s %9.3f ms\n", what, std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+    }
+};
+
 struct Plan {
     std::vector<AppendDesc> descs;      // documents touched by the append kernel
     std::vector<uint32_t> merge;        // handles to re-merge (batch rows first)
@@ -139,9 +163,10 @@ struct Plan {
 
 // Staged batch layout on the device: [changes][deps][ops][descs][remap][launch docs][handles]
 struct StageLayout {
-    size_t o_ch, o_dp, o_op, o_desc, o_remap, o_docs, o_hand, o_gather, total;
+    size_t o_ch, o_dp, o_op, o_desc, o_remap, o_docs, o_hand, o_gather, o_bail, total;
 };
-StageLayout layout(size_t nc, size_t nd, size_t no, size_t ndesc, size_t nremap, size_t nmerge, size_t ngather, uint32_t S) {
+StageLayout layout(size_t nc, size_t nd, size_t no, size_t ndesc, size_t nremap, size_t nmerge, size_t ngather, uint32_t S,
+                   size_t ninc = 0) {
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     StageLayout L;
     size_t o = 0;
@@ -153,6 +178,7 @@ StageLayout layout(size_t nc, size_t nd, size_t no, size_t ndesc, size_t nremap,
     L.o_docs = o; o += al(nmerge * sizeof(hm_doc_row) + 1);
     L.o_hand = o; o += al(nmerge * 4 + 1);
     L.o_gather = o; o += al(ngather * (sizeof(hm_doc_result) + 3 * 4 * (size_t)S) + 1);
+    L.o_bail = o; o += al(ninc + 1);
     L.total = o;
     return L;
 }
@@ -312,6 +338,25 @@ int hm_doc_open(hm_store *s, uint32_t *out_doc) {
     }
 }
 
+int hm_doc_open_n(hm_store *s, uint32_t n, uint32_t *out_first) {
+    if (!s || !out_first) return HM_ERR_INVALID;
+    try {
+        if (s->pending) return hm_engine_fail(s->e, HM_ERR_INVALID, "hm_doc_open_n while a batch is in flight");
+        const uint32_t h0 = (uint32_t)s->docs.size();
+        int r = ensure_handles(s, (size_t)h0 + n);
+        if (r) return r;
+        DocMeta m;
+        m.last.err_change = HM_NONE; m.last.err_op = HM_NONE;
+        s->docs.resize((size_t)h0 + n, m);
+        std::vector<hm_doc_result> rows(n, m.last);
+        if (n) SCHK(s, hipMemcpy(s->res_docs + h0, rows.data(), (size_t)n * sizeof(hm_doc_result), hipMemcpyHostToDevice));
+        *out_first = h0;
+        return HM_OK;
+    } catch (...) {
+        return HM_ERR_NOMEM;
+    }
+}
+
 int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles, const uint8_t *actor_remap,
                     uint64_t *out_batch_id) {
     if (!s || !b || (b->n_docs && (!doc_handles || !b->docs))) return HM_ERR_INVALID;
@@ -321,6 +366,7 @@ int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
         if (b->a_stride != S) return hm_engine_fail(s->e, HM_ERR_INVALID, "batch a_stride must equal the store's");
         SCHK(s, hipSetDevice(hm_engine_device(s->e)));
         hipStream_t st = hm_engine_stream(s->e);
+        PhaseTimer T(st);
         // validate rows
         std::vector<uint8_t> seen(s->docs.size(), 0);
         for (uint32_t i = 0; i < n; i++) {
@@ -353,6 +399,7 @@ int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
                 }
             }
         }
+        T.mark("validate");
         // plan segments: grow into fresh segments, compact the arenas when full
         size_t need_c = 0, need_d = 0, need_o = 0, need_r = 0;
         for (uint32_t i = 0; i < n; i++) {
@@ -367,16 +414,22 @@ int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
             int r = compact(s, need_c, need_d, need_o, need_r);
             if (r) return r;
         }
-        s->p_old.assign(n, DocMeta());
-        s->p_inverse.assign(n, std::vector<uint8_t>());
+        s->p_old.resize(n);
+        s->p_inv_row.assign(n, -1);
+        s->p_inv.clear();
         s->p_handles.assign(doc_handles, doc_handles + n);
         std::vector<AppendDesc> descs(n);
         uint32_t n_remap = 0;
         std::vector<uint8_t> remap_rows;
+        // route: a document whose resident state is clean (last merge ok, nothing queued, no
+        // re-rank) and whose new rows fit the incremental tiles is applied by inc_apply_kernel;
+        // the rest re-merge their whole log (DocBackend.applyRemoteChanges either way)
+        std::vector<uint32_t> cold;
+        uint32_t n_inc = 0, mx_new_c = 0, mx_tgt = 0, mx_stage = 0, mx_regs = 0, mx_surv = 0, mx_slots = 0;
         for (uint32_t i = 0; i < n; i++) {
             const uint32_t h = doc_handles[i];
             DocMeta &m = s->docs[h];
-            s->p_old[i] = m;
+            const DocMeta &o = (s->p_old[i] = m);
             const hm_doc_row &r = b->docs[i];
             AppendDesc &D = descs[i];
             D = AppendDesc{};
@@ -384,33 +437,48 @@ int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
             D.src_c = m.c.off; D.n_old_c = m.n_c; D.new_c = r.change_off; D.n_new_c = r.n_changes;
             D.src_d = m.d.off; D.n_old_d = m.n_d; D.new_d = r.dep_off; D.n_new_d = r.n_deps;
             D.src_o = m.o.off; D.n_old_o = m.n_o; D.new_o = r.op_off; D.n_new_o = r.n_ops;
+            D.src_r = m.r.off; D.n_old_r = m.n_r;
             if (m.n_c + r.n_changes > m.c.cap) seg_alloc(s->used_c, s->cap_c, m.n_c + r.n_changes, m.c);
             if (m.n_d + r.n_deps > m.d.cap) seg_alloc(s->used_d, s->cap_d, m.n_d + r.n_deps, m.d);
             if (m.n_o + r.n_ops > m.o.cap) seg_alloc(s->used_o, s->cap_o, m.n_o + r.n_ops, m.o);
             if (r.n_regs > m.r.cap) seg_alloc(s->used_r, s->cap_r, r.n_regs, m.r);
-            D.dst_c = m.c.off; D.dst_d = m.d.off; D.dst_o = m.o.off;
+            D.dst_c = m.c.off; D.dst_d = m.d.off; D.dst_o = m.o.off; D.dst_r = m.r.off;
             D.remap_row = 0xFFFFFFFFu;
+            bool reranked = false;
             if (actor_remap) {
                 const uint8_t *mp = actor_remap + (size_t)i * S;
                 bool ident = true;
-                for (uint32_t a = 0; a < S; a++) if (a < m.n_actors && mp[a] != a) ident = false;
+                for (uint32_t a = 0; a < m.n_actors; a++) if (mp[a] != a) ident = false;
                 if (!ident) {
-                    std::vector<uint8_t> inv(S, 0xFF), row(S, 0xFF);
-                    for (uint32_t a = 0; a < S; a++) {
-                        if (a < m.n_actors) {
-                            row[a] = mp[a]; inv[mp[a]] = (uint8_t)a;     // validated above
-                        } else row[a] = 0xFF;
-                    }
+                    reranked = true;
+                    const size_t at = remap_rows.size();
+                    remap_rows.resize(at + S, 0xFF);
+                    s->p_inv_row[i] = (int32_t)s->p_inv.size();
+                    s->p_inv.resize(s->p_inv.size() + S, 0xFF);
+                    uint8_t *inv = s->p_inv.data() + s->p_inv_row[i];
+                    for (uint32_t a = 0; a < m.n_actors; a++) { remap_rows[at + a] = mp[a]; inv[mp[a]] = (uint8_t)a; }   // validated above
                     D.remap_row = n_remap++;
-                    remap_rows.insert(remap_rows.end(), row.begin(), row.end());
-                    s->p_inverse[i] = inv;
                 }
             }
             m.n_c += r.n_changes; m.n_d += r.n_deps; m.n_o += r.n_ops;
             m.n_r = r.n_regs; m.n_objs = r.n_objs; m.n_actors = r.n_actors; m.flags |= r.flags;
+            D.n_r = m.n_r; D.n_actors = (uint16_t)m.n_actors; D.n_objs = m.n_objs;
+            const uint32_t tgt = r.n_deps + r.n_changes;            // fold steps: deps + own predecessor
+            const bool inc = s->incremental && o.last.status == HM_OK && o.last.n_queued == 0 && !reranked &&
+                             r.n_changes > 0 && r.n_changes <= HM_INC_MAX_NEW_C && r.n_ops <= HM_INC_MAX_NEW_O &&
+                             tgt <= HM_INC_MAX_TGT && m.n_r <= HM_INC_MAX_REGS && o.last.n_surv <= HM_INC_MAX_SURV &&
+                             o.n_r <= m.n_r && m.n_actors <= S && !((o.flags | r.flags) & HM_DOC_HAS_LISTS);
+            if (!inc) { cold.push_back(h); continue; }
+            D.inc = 1;
+            n_inc++;
+            mx_new_c = std::max(mx_new_c, r.n_changes); mx_tgt = std::max(mx_tgt, tgt);
+            mx_stage = std::max(mx_stage, std::min<uint32_t>(o.n_c, HM_INC_MAX_STAGE));
+            mx_regs = std::max(mx_regs, m.n_r); mx_surv = std::max(mx_surv, o.last.n_surv);
+            mx_slots = std::max(mx_slots, std::min<uint32_t>(r.n_ops, HM_INC_SLOTS));
         }
+        T.mark("plan+route");
         // stage and launch: append, merge, gather
-        const StageLayout L = layout(b->n_changes, b->n_deps, b->n_ops, n, remap_rows.size(), n, n, S);
+        const StageLayout L = layout(b->n_changes, b->n_deps, b->n_ops, n, remap_rows.size(), n, n, S, n_inc ? n : 0);
         int rc = ensure_stage(s, L.total);
         if (rc) return rc;
         uint8_t *sp = s->stage.p;
@@ -423,12 +491,36 @@ int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
         SCHK(s, hm_launch_append((const AppendDesc *)(sp + L.o_desc), n, ar, ar, (const hm_change_row *)(sp + L.o_ch),
                                  (const hm_dep_row *)(sp + L.o_dp), (const hm_op_row *)(sp + L.o_op),
                                  remap_rows.empty() ? nullptr : sp + L.o_remap, S, st));
-        rc = launch_store_merge(s, s->p_handles, sp + L.o_docs, (uint32_t *)(sp + L.o_hand));
+        T.mark("stage+append");
+        if (n_inc) {
+            const IncDims M = hm_inc_dims(S, mx_new_c, mx_tgt, mx_stage, mx_regs, mx_surv, mx_slots);
+            IncArenas A = {s->changes, s->deps, s->ops, s->hist, s->all_deps, s->regs, s->surv,
+                           s->res_docs, s->clock, s->back_clock, s->heads, s->min_clock};
+            SCHK(s, hm_launch_inc_apply((const AppendDesc *)(sp + L.o_desc), n, A, M, sp + L.o_bail, st));
+        }
+        T.mark("incremental");
+        rc = launch_store_merge(s, cold, sp + L.o_docs, (uint32_t *)(sp + L.o_hand));
         if (rc) return rc;
+        T.mark("remerge");
+        s->st_inc = n_inc; s->st_cold = (uint32_t)cold.size(); s->st_bail = 0;
+        if (n_inc) {
+            // documents the incremental kernel handed back re-merge their whole log
+            std::vector<uint8_t> bail(n);
+            SCHK(s, hipMemcpyAsync(bail.data(), sp + L.o_bail, n, hipMemcpyDeviceToHost, st));
+            SCHK(s, hipStreamSynchronize(st));
+            std::vector<uint32_t> again;
+            for (uint32_t i = 0; i < n; i++) if (descs[i].inc && bail[i]) again.push_back(descs[i].handle);
+            s->st_bail = (uint32_t)again.size(); s->st_inc -= s->st_bail;
+            rc = launch_store_merge(s, again, sp + L.o_docs, (uint32_t *)(sp + L.o_hand));
+            if (rc) return rc;
+        }
+        T.mark("handed back");
+        // the merges above used the handle region for their own document lists
+        if (n) SCHK(s, hipMemcpyAsync(sp + L.o_hand, s->p_handles.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
         SCHK(s, hm_launch_gather((const uint32_t *)(sp + L.o_hand), n, S, s->res_docs, s->clock, s->back_clock, s->heads,
                                  sp + L.o_gather, st));
-        s->p_out.resize((size_t)n * (sizeof(hm_doc_result) + 12 * (size_t)S));
-        if (n) SCHK(s, hipMemcpyAsync(s->p_out.data(), sp + L.o_gather, s->p_out.size(), hipMemcpyDeviceToHost, st));
+        s->p_gather_dev = sp + L.o_gather;
+        T.mark("gather+d2h");
         s->pending = true;
         s->pending_id = s->next_id++;
         if (out_batch_id) *out_batch_id = s->pending_id;
@@ -444,15 +536,26 @@ int hm_batch_wait(hm_store *s, uint64_t batch_id, hm_doc_result *out_docs, uint3
     try {
         if (!s->pending || batch_id != s->pending_id) return hm_engine_fail(s->e, HM_ERR_INVALID, "no such batch in flight");
         hipStream_t st = hm_engine_stream(s->e);
+        PhaseTimer T(st);
         SCHK(s, hipStreamSynchronize(st));
+        T.mark("wait sync");
         s->pending = false;
         const uint32_t n = (uint32_t)s->p_handles.size(), S = s->S;
-        const hm_doc_result *res = (const hm_doc_result *)s->p_out.data();
-        const uint32_t *rows = (const uint32_t *)(s->p_out.data() + (size_t)n * sizeof(hm_doc_result));
-        if (out_docs) memcpy(out_docs, res, (size_t)n * sizeof(hm_doc_result));
-        if (out_clock) memcpy(out_clock, rows, (size_t)n * S * 4);
-        if (out_back_clock) memcpy(out_back_clock, rows + (size_t)n * S, (size_t)n * S * 4);
-        if (out_heads) memcpy(out_heads, rows + (size_t)2 * n * S, (size_t)n * S * 4);
+        // results straight from the gathered device rows into the caller's arrays
+        std::vector<hm_doc_result> tmp;
+        hm_doc_result *res = out_docs;
+        if (!res) { tmp.resize(n); res = tmp.data(); }
+        if (n) {
+            const uint8_t *g = s->p_gather_dev;
+            const size_t rb = (size_t)n * S * 4;
+            SCHK(s, hipMemcpyAsync(res, g, (size_t)n * sizeof(hm_doc_result), hipMemcpyDeviceToHost, st));
+            g += (size_t)n * sizeof(hm_doc_result);
+            if (out_clock) SCHK(s, hipMemcpyAsync(out_clock, g, rb, hipMemcpyDeviceToHost, st));
+            if (out_back_clock) SCHK(s, hipMemcpyAsync(out_back_clock, g + rb, rb, hipMemcpyDeviceToHost, st));
+            if (out_heads) SCHK(s, hipMemcpyAsync(out_heads, g + 2 * rb, rb, hipMemcpyDeviceToHost, st));
+            SCHK(s, hipStreamSynchronize(st));
+        }
+        T.mark("wait copy-out");
         // roll back documents whose merge threw (or left the envelope): the log returns to
         // its previous length (rows stay where they are), ranks are re-ranked back, and the
         // previous state is re-merged
@@ -471,9 +574,10 @@ int hm_batch_wait(hm_store *s, uint64_t batch_id, hm_doc_result *out_docs, uint3
             D.src_d = D.dst_d = m.d.off; D.n_old_d = o.n_d;
             D.src_o = D.dst_o = m.o.off; D.n_old_o = o.n_o;
             D.remap_row = 0xFFFFFFFFu;
-            if (!s->p_inverse[i].empty()) {
+            if (s->p_inv_row[i] >= 0) {
                 D.remap_row = n_remap++;
-                remap_rows.insert(remap_rows.end(), s->p_inverse[i].begin(), s->p_inverse[i].end());
+                const uint8_t *inv = s->p_inv.data() + s->p_inv_row[i];
+                remap_rows.insert(remap_rows.end(), inv, inv + S);
             }
             m.n_c = o.n_c; m.n_d = o.n_d; m.n_o = o.n_o; m.n_r = o.n_r; m.n_objs = o.n_objs;
             m.n_actors = o.n_actors; m.flags = o.flags;
@@ -497,6 +601,19 @@ int hm_batch_wait(hm_store *s, uint64_t batch_id, hm_doc_result *out_docs, uint3
     } catch (...) {
         return hm_engine_fail(s->e, HM_ERR_NOMEM, "exception in hm_batch_wait");
     }
+}
+
+int hm_store_set_incremental(hm_store *s, int on) {
+    if (!s) return HM_ERR_INVALID;
+    if (s->pending) return hm_engine_fail(s->e, HM_ERR_INVALID, "batch in flight");
+    s->incremental = on != 0;
+    return HM_OK;
+}
+
+int hm_store_last_routing(const hm_store *s, uint32_t *out3) {
+    if (!s || !out3) return HM_ERR_INVALID;
+    out3[0] = s->st_inc; out3[1] = s->st_cold; out3[2] = s->st_bail;
+    return HM_OK;
 }
 
 int hm_doc_info(hm_store *s, uint32_t doc, hm_doc_info_t *out) {

@@ -6,6 +6,8 @@
 //                       the rank-indexed per-document rows (minimumClock, stored clock),
 //                       and appends the new change/dep/op rows with their offsets rebased
 //                       from batch-local to arena positions.
+//  inc_apply_kernel     incremental applyRemoteChanges: new changes applied on the resident
+//                       state of documents whose submit is causally ready (see below).
 //  gather_kernel        per-document result rows of a batch (by handle) into one
 //                       contiguous buffer, so hm_batch_wait is a single D2H copy.
 //  clock_update_kernel  ClockStore.update (src/ClockStore.ts:78-91) over many documents:
@@ -74,13 +76,13 @@ __global__ __launch_bounds__(SWG) void append_kernel(const AppendDesc *descs, ui
         if (rm && t == 0) {
             uint32_t *rows[2] = {dst.min_clock + (size_t)D.handle * S, dst.stored_clock + (size_t)D.handle * S};
             for (int w = 0; w < 2; w++) {
-                uint32_t tmp[32];
-                for (uint32_t a = 0; a < S && a < 32; a++) tmp[a] = 0;
-                for (uint32_t a = 0; a < S && a < 32; a++) {
+                uint32_t tmp[64];
+                for (uint32_t a = 0; a < S && a < 64; a++) tmp[a] = 0;
+                for (uint32_t a = 0; a < S && a < 64; a++) {
                     const uint32_t na = mp[a];
-                    if (na < S && na < 32) tmp[na] = rows[w][a];
+                    if (na < S && na < 64) tmp[na] = rows[w][a];
                 }
-                for (uint32_t a = 0; a < S && a < 32; a++) rows[w][a] = tmp[a];
+                for (uint32_t a = 0; a < S && a < 64; a++) rows[w][a] = tmp[a];
             }
         }
         __syncthreads();
@@ -147,6 +149,356 @@ __global__ void sync_ranges_kernel(const uint64_t *present, const uint64_t *word
     out_end[i] = lo[i] >= h ? lo[i] : (j < h ? j : h);
 }
 
+// ---------------- incremental applyRemoteChanges ----------------
+// inc_apply_kernel: one wave per document whose new changes all apply in arrival order on
+// the resident state (Automerge's applyQueuedOps applies them in its first pass when each is
+// causally ready after the previous ones; DocBackend.ts:169-185 -> Backend.applyChanges).
+// For each new change: causallyReady against the resident opSet.clock, allDeps by the
+// transitiveDeps fold over the resident allDeps rows (each old fold source found by
+// (actor, seq) in one scan of the log), history position, heads and clock.  For each new map
+// op (set / del / link): the register's survivors filtered to the concurrent ones, the op
+// pushed, sortBy(actor).reverse() — only the registers the new ops hit are recomputed; the
+// rest of the register table is repacked as it was.  Anything outside that (a duplicate or
+// not-yet-ready change, inc / counter / list / object-creation ops, an unknown object, tiles
+// too small) sets bail[i] before any merged state is written, and the host re-merges that
+// document's whole log with the batch kernels.  The loads that depend only on the
+// descriptor (new rows, clock / heads, the old log's (actor, seq) keys, the register table,
+// the survivors) are issued together; the remaining dependent steps are one scan of the log
+// and one gather of allDeps rows.
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint32_t lane_bcast(uint32_t x, uint32_t l) { return __builtin_amdgcn_readlane(x, l); }
+__device__ __forceinline__ uint64_t wave_ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ uint64_t key_of(const hm_change_row *r) {
+    const uint2 w = *reinterpret_cast<const uint2 *>(r);          // actor | n_deps << 16, seq
+    return ((uint64_t)(w.x & 0xFFFFu) << 32) | w.y;
+}
+
+// was object `o` created as a map/table by an op of the old log?
+__device__ bool inc_obj_is_map(const AppendDesc &D, const IncArenas &A, uint32_t o, uint32_t lane) {
+    for (uint32_t base = 0; base < D.n_old_o; base += 64) {
+        const uint32_t i = base + lane;
+        bool m = false;
+        uint32_t act = 0;
+        if (i < D.n_old_o) {
+            const hm_op_row &r = A.ops[D.dst_o + i];
+            act = r.action;
+            m = act <= HM_MAKE_TEXT && r.obj == o;
+        }
+        const uint64_t b = wave_ballot(m);
+        if (b) {
+            const uint32_t first = lane_bcast(act, (uint32_t)__builtin_ctzll(b));
+            return first == HM_MAKE_MAP || first == HM_MAKE_TABLE;
+        }
+    }
+    return false;
+}
+
+__device__ bool inc_doc(const AppendDesc &D, const IncArenas &A, const IncDims &M, uint32_t lane, uint8_t *lds) {
+    const uint32_t S = M.S, h = D.handle, NA = D.n_actors, nnc = D.n_new_c, nno = D.n_new_o;
+    uint32_t *nc = reinterpret_cast<uint32_t *>(lds + M.o_nc);          // per new change: 8 words
+    uint32_t *dep = reinterpret_cast<uint32_t *>(lds + M.o_dep);        // new deps: actor, seq
+    uint64_t *tkey = reinterpret_cast<uint64_t *>(lds + M.o_tkey);      // fold steps: (actor, seq)
+    int32_t *tsrc = reinterpret_cast<int32_t *>(lds + M.o_tsrc);        // new change index, or -1 (old)
+    uint32_t *tidx = reinterpret_cast<uint32_t *>(tsrc + M.tgt), *tcnt = tidx + M.tgt;
+    uint32_t *tad = reinterpret_cast<uint32_t *>(lds + M.o_tad);        // allDeps rows of old sources
+    uint32_t *adn = reinterpret_cast<uint32_t *>(lds + M.o_adn);        // allDeps rows of the new changes
+    uint64_t *skey = reinterpret_cast<uint64_t *>(lds + M.o_skey);      // staged old log: (actor, seq)
+    uint32_t *sof = reinterpret_cast<uint32_t *>(lds + M.o_sof);        //                 first op
+    uint32_t *r_cnt = reinterpret_cast<uint32_t *>(lds + M.o_reg), *r_off = r_cnt + M.regs, *r_obj = r_off + M.regs;
+    uint8_t *r_slot = reinterpret_cast<uint8_t *>(r_obj + M.regs);
+    hm_surv_result *sold = reinterpret_cast<hm_surv_result *>(lds + M.o_sold);
+    hm_surv_result *wl = reinterpret_cast<hm_surv_result *>(lds + M.o_wl);
+    uint32_t *wls = reinterpret_cast<uint32_t *>(lds + M.o_wls), *scnt = reinterpret_cast<uint32_t *>(lds + M.o_scnt);
+    uint8_t *wla = lds + M.o_wla;
+
+    const uint32_t hist_len = uni(A.res_docs[h].hist_len), n_old_surv = uni(A.res_docs[h].n_surv);
+    if (NA > S || nnc == 0 || nnc > M.new_c || nno > 64 || D.n_r > M.regs || n_old_surv > M.surv || D.n_old_r > D.n_r)
+        return false;
+    const bool staged = D.n_old_c <= M.stage;
+
+    // ---- loads that depend only on the descriptor ----
+    uint32_t clk = 0, hd = 0, mc = 0;
+    if (lane < S) {
+        clk = A.clock[(size_t)h * S + lane];
+        hd = A.heads[(size_t)h * S + lane];
+        mc = A.min_clock ? A.min_clock[(size_t)h * S + lane] : 0u;
+    }
+    uint32_t ca = 0, cq = 0, cnd = 0, cdo = 0, cno = 0, coo = 0;
+    if (lane < nnc) {
+        const hm_change_row c = A.changes[D.dst_c + D.n_old_c + lane];
+        ca = c.actor; cq = c.seq; cnd = c.n_deps; cdo = c.dep_off - D.dst_d; cno = c.n_ops; coo = c.op_first - D.dst_o;
+    }
+    uint32_t o_act = 0, o_dt = 0, o_obj = 0, o_reg = 0, o_vt = 0, o_vlo = 0, o_vhi = 0;
+    if (lane < nno) {
+        const hm_op_row op = A.ops[D.dst_o + D.n_old_o + lane];
+        o_act = op.action; o_dt = op.datatype; o_obj = op.obj; o_reg = op.reg; o_vt = op.vtag;
+        o_vlo = (uint32_t)op.value; o_vhi = (uint32_t)(op.value >> 32);
+    }
+    if (staged)
+        for (uint32_t i = lane; i < D.n_old_c; i += 64) {
+            const hm_change_row *r = A.changes + D.dst_c + i;
+            skey[i] = key_of(r);
+            sof[i] = r->op_first - D.dst_o;
+        }
+    for (uint32_t g = lane; g < D.n_r; g += 64) {
+        uint32_t c = 0, o = 0, ob = HM_NONE;
+        if (g < D.n_old_r) {
+            const hm_reg_result r = A.regs[D.src_r + g];
+            c = r.n_surv; o = r.surv_off; ob = r.obj;
+        }
+        r_cnt[g] = c; r_off[g] = o; r_obj[g] = ob; r_slot[g] = 0xFF;
+    }
+    for (uint32_t i = lane; i < n_old_surv; i += 64) sold[i] = A.surv[D.src_o + i];
+
+    // ---- the new rows: layout (grouped by change, in order, after the old rows) and values ----
+    uint32_t sd = lane < nnc ? cnd : 0u, so = lane < nnc ? cno : 0u;
+    for (uint32_t d = 1; d < 8; d <<= 1) {
+        const uint32_t yd = __shfl_up(sd, d, 64), yo = __shfl_up(so, d, 64);
+        if (lane >= d) { sd += yd; so += yo; }
+    }
+    const uint32_t xd = sd - (lane < nnc ? cnd : 0u), xo = so - (lane < nnc ? cno : 0u);
+    const uint32_t total_d = lane_bcast(sd, nnc - 1), total_o = lane_bcast(so, nnc - 1);
+    const bool bad_c = lane < nnc && (ca >= NA || cq == 0 || cdo != D.n_old_d + xd || coo != D.n_old_o + xo);
+    const bool bad_o = lane < nno && ((o_act != HM_SET && o_act != HM_DEL && o_act != HM_LINK) || o_dt == HM_DT_COUNTER ||
+                                      o_obj >= D.n_objs || o_reg >= D.n_r ||
+                                      (o_vt == HM_V_INT && ((int64_t)(((uint64_t)o_vhi << 32) | o_vlo) > 9007199254740992ll ||
+                                                            (int64_t)(((uint64_t)o_vhi << 32) | o_vlo) < -9007199254740992ll)));
+    if (wave_ballot(bad_c || bad_o) || total_o != nno || total_d != D.n_new_d || total_d + nnc > M.tgt) return false;
+    if (lane < nnc) {
+        uint32_t *w = nc + lane * 8;
+        w[0] = ca; w[1] = cq; w[2] = cnd; w[3] = xd; w[4] = cno; w[5] = xo;
+    }
+    for (uint32_t t = lane; t < total_d; t += 64) {
+        const hm_dep_row d = A.deps[D.dst_d + D.n_old_d + t];
+        dep[2 * t] = d.actor; dep[2 * t + 1] = d.seq;
+    }
+    __syncthreads();
+
+    // ---- causallyReady in arrival order; the transitiveDeps fold steps (A.1) ----
+    uint32_t ck = clk, nt = 0;
+    for (uint32_t j = 0; j < nnc; j++) {
+        const uint32_t a = uni(nc[j * 8]), q = uni(nc[j * 8 + 1]), nd = uni(nc[j * 8 + 2]), d0 = uni(nc[j * 8 + 3]);
+        if (lane_bcast(ck, a) + 1u != q) return false;          // a duplicate, or not ready: queue semantics
+        const uint32_t t0 = nt;
+        bool own = false;
+        for (uint32_t t = 0; t <= nd; t++) {
+            uint32_t da, dq;
+            if (t < nd) {
+                da = uni(dep[2 * (d0 + t)]); dq = uni(dep[2 * (d0 + t) + 1]);
+                if (da >= NA) return false;
+                if (da == a) { dq = q - 1; own = true; }
+            } else {
+                if (own) break;
+                da = a; dq = q - 1;
+            }
+            if (lane_bcast(ck, da) < dq) return false;
+            if (dq == 0) continue;
+            int src = -1;
+            for (uint32_t k = 0; k < j; k++)
+                if (uni(nc[k * 8]) == da && uni(nc[k * 8 + 1]) == dq) src = (int)k;
+            if (lane == 0) { tkey[nt] = ((uint64_t)da << 32) | dq; tsrc[nt] = src; tcnt[nt] = 0; tidx[nt] = 0; }
+            nt++;
+        }
+        if (lane == 0) { nc[j * 8 + 6] = t0; nc[j * 8 + 7] = nt - t0; }
+        if (lane == a) ck = q;
+    }
+    __syncthreads();
+
+    // ---- old fold sources: exactly one applied row of the log per (actor, seq) ----
+    bool any_old = false;
+    for (uint32_t t = 0; t < nt; t++) any_old |= tsrc[t] < 0;
+    if (any_old) {
+        for (uint32_t base = 0; base < D.n_old_c; base += 64) {
+            const uint32_t i = base + lane;
+            uint64_t key = ~0ull;
+            if (i < D.n_old_c) key = staged ? skey[i] : key_of(A.changes + D.dst_c + i);
+            for (uint32_t t = 0; t < nt; t++) {
+                if (tsrc[t] >= 0) continue;
+                const uint64_t m = wave_ballot(key == tkey[t]);
+                if (m && lane == 0) { tcnt[t] += (uint32_t)__builtin_popcountll(m); tidx[t] = base + (uint32_t)__builtin_ctzll(m); }
+            }
+        }
+        __syncthreads();
+        for (uint32_t t = 0; t < nt; t++)
+            if (tsrc[t] < 0 && uni(tcnt[t]) != 1u) return false;       // duplicates in the log: re-merge
+        for (uint32_t w = lane; w < nt * S; w += 64) {
+            const uint32_t t = w / S, x = w - t * S;
+            tad[w] = tsrc[t] < 0 ? A.all_deps[(size_t)(D.src_c + tidx[t]) * S + x] : 0u;
+        }
+        __syncthreads();
+    }
+
+    // ---- per new change: allDeps, heads, clock (applyChange) ----
+    for (uint32_t j = 0; j < nnc; j++) {
+        const uint32_t a = uni(nc[j * 8]), q = uni(nc[j * 8 + 1]), t0 = uni(nc[j * 8 + 6]), tn = uni(nc[j * 8 + 7]);
+        uint32_t adv = 0;
+        for (uint32_t t = t0; t < t0 + tn; t++) {
+            const uint64_t key = tkey[t];
+            const uint32_t da = uni((uint32_t)(key >> 32)), dq = uni((uint32_t)key);
+            const int src = (int)uni((uint32_t)tsrc[t]);
+            const uint32_t row = lane < S ? (src >= 0 ? adn[src * S + lane] : tad[t * S + lane]) : 0u;
+            if (lane < NA && row > adv) adv = row;
+            if (lane == da) adv = dq;
+        }
+        if (lane >= NA) adv = 0;
+        if (lane < S) adn[j * S + lane] = adv;
+        if (hd && hd <= adv) hd = 0;
+        if (lane == a) { hd = q; clk = q; }
+        __syncthreads();
+    }
+
+    // ---- objects other than the root must be maps created by the old log ----
+    {
+        uint64_t om = wave_ballot(lane < nno && o_obj != 0);
+        uint32_t checked = 0;
+        while (om) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(om);
+            om &= om - 1;
+            const uint32_t o = lane_bcast(o_obj, l);
+            if (o == checked) continue;
+            if (!inc_obj_is_map(D, A, o, lane)) return false;
+            checked = o;
+        }
+    }
+
+    // ---- the new ops in order (applyAssign, A.2) on the registers they hit ----
+    uint32_t nslots = 0, j = 0, jend = uni(nc[4]);
+    for (uint32_t k = 0; k < nno; k++) {
+        while (k >= jend) { j++; jend += uni(nc[j * 8 + 4]); }
+        const uint32_t a = uni(nc[j * 8]), q = uni(nc[j * 8 + 1]);
+        const uint32_t act = lane_bcast(o_act, k), obj = lane_bcast(o_obj, k), g = lane_bcast(o_reg, k);
+        const uint32_t vtag = lane_bcast(o_vt, k);
+        const uint64_t val = ((uint64_t)lane_bcast(o_vhi, k) << 32) | lane_bcast(o_vlo, k);
+        uint32_t slot = uni(r_slot[g]);
+        if (slot == 0xFF) {
+            if (nslots == M.slots) return false;
+            slot = nslots++;
+            const uint32_t c0 = uni(r_cnt[g]), o0 = uni(r_off[g]);
+            if (c0 > HM_INC_SLOT_CAP || o0 + c0 > n_old_surv) return false;
+            if (lane < c0) {
+                const hm_surv_result x = sold[o0 + lane];
+                // the old change owning op x.op: the last change whose first op is <= x.op
+                uint32_t lo = 0, hi = D.n_old_c;
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    const uint32_t f = staged ? sof[mid] : A.changes[D.dst_c + mid].op_first - D.dst_o;
+                    if (f <= x.op) lo = mid; else hi = mid;
+                }
+                const uint64_t kk = staged ? skey[lo] : key_of(A.changes + D.dst_c + lo);
+                wl[slot * HM_INC_SLOT_CAP + lane] = x;
+                wla[slot * HM_INC_SLOT_CAP + lane] = (uint8_t)(kk >> 32);
+                wls[slot * HM_INC_SLOT_CAP + lane] = (uint32_t)kk;
+            }
+            if (lane == 0) { scnt[slot] = c0; r_slot[g] = (uint8_t)slot; }
+            __syncthreads();
+        }
+        const uint32_t base = slot * HM_INC_SLOT_CAP, cnt = uni(scnt[slot]);
+        // survivors concurrent with the new op stay (isConcurrent reduces to
+        // allDeps(new)[x.actor] < x.seq: no resident change can depend on the new one)
+        hm_surv_result x = {};
+        uint32_t xa = 0, xs = 0;
+        bool keep = false;
+        if (lane < cnt) {
+            x = wl[base + lane]; xa = wla[base + lane]; xs = wls[base + lane];
+            keep = adn[j * S + xa] < xs;
+        }
+        const uint64_t km = wave_ballot(keep);
+        const uint32_t nk = (uint32_t)__builtin_popcountll(km), pos = lanes_below(km);
+        const bool push = act != HM_DEL;
+        const uint32_t ncnt = nk + (push ? 1u : 0u);
+        if (ncnt > HM_INC_SLOT_CAP) return false;
+        __syncthreads();
+        if (keep) { wl[base + pos] = x; wla[base + pos] = (uint8_t)xa; wls[base + pos] = xs; }
+        if (push && lane == 0) {
+            hm_surv_result y;
+            y.op = D.n_old_o + k; y.vtag = vtag; y.value = val;
+            wl[base + nk] = y; wla[base + nk] = (uint8_t)a; wls[base + nk] = q;
+        }
+        __syncthreads();
+        // sortBy(actor) (stable) then reverse
+        if (lane < ncnt) { x = wl[base + lane]; xa = wla[base + lane]; xs = wls[base + lane]; }
+        uint32_t rank = 0;
+        for (uint32_t e = 0; e < ncnt; e++) {
+            const uint32_t ea = wla[base + e];
+            rank += (ea < xa || (ea == xa && e < lane)) ? 1u : 0u;
+        }
+        __syncthreads();
+        if (lane < ncnt) {
+            const uint32_t d = ncnt - 1 - rank;
+            wl[base + d] = x; wla[base + d] = (uint8_t)xa; wls[base + d] = xs;
+        }
+        if (lane == 0) { scnt[slot] = ncnt; r_obj[g] = obj; }
+        __syncthreads();
+    }
+
+    // ---- write back: registers (repacked in register order), survivors ----
+    const bool same_o = D.src_o == D.dst_o, same_r = D.src_r == D.dst_r;
+    uint32_t carry = 0;
+    for (uint32_t g0 = 0; g0 < D.n_r; g0 += 64) {
+        const uint32_t g = g0 + lane;
+        const bool valid = g < D.n_r;
+        const uint32_t slot = valid ? r_slot[g] : 0xFFu;
+        const uint32_t cnt = !valid ? 0u : (slot != 0xFF ? scnt[slot] : r_cnt[g]);
+        uint32_t incl = cnt;
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += y;
+        }
+        const uint32_t off = carry + incl - cnt;
+        carry += lane_bcast(incl, 63);
+        if (valid) {
+            const bool unchanged = slot == 0xFF && g < D.n_old_r && off == r_off[g];
+            if (!(unchanged && same_r)) {
+                hm_reg_result r;
+                r.n_surv = cnt; r.surv_off = off; r.list_index = -1; r.obj = r_obj[g];
+                A.regs[D.dst_r + g] = r;
+            }
+            if (!(unchanged && same_o))
+                for (uint32_t i = 0; i < cnt; i++)
+                    A.surv[D.dst_o + off + i] = slot != 0xFF ? wl[slot * HM_INC_SLOT_CAP + i] : sold[r_off[g] + i];
+        }
+    }
+
+    // ---- history, allDeps, clocks, the document's result row ----
+    if (D.src_c != D.dst_c) {
+        for (uint32_t i = lane; i < D.n_old_c; i += 64) A.hist[D.dst_c + i] = A.hist[D.src_c + i];
+        for (size_t w = lane; w < (size_t)D.n_old_c * S; w += 64)
+            A.all_deps[(size_t)D.dst_c * S + w] = A.all_deps[(size_t)D.src_c * S + w];
+    }
+    if (lane < nnc) A.hist[D.dst_c + D.n_old_c + lane] = (int32_t)(hist_len + lane);
+    for (uint32_t w = lane; w < nnc * S; w += 64) A.all_deps[(size_t)(D.dst_c + D.n_old_c) * S + w] = adn[w];
+    if (lane < S) {
+        A.clock[(size_t)h * S + lane] = clk;
+        A.back_clock[(size_t)h * S + lane] = clk;                 // queue empty: every handed change applied
+        A.heads[(size_t)h * S + lane] = hd;
+    }
+    const bool ag = wave_ballot(lane < S && clk < mc) == 0, bg = wave_ballot(lane < S && mc < clk) == 0;
+    if (lane == 0) {
+        hm_doc_result r = {};
+        r.status = HM_OK; r.err_change = HM_NONE; r.err_op = HM_NONE;
+        r.hist_len = hist_len + nnc; r.n_queued = 0; r.n_surv = carry;
+        r.min_cmp = (ag && bg) ? 0u : (ag ? 1u : (bg ? 2u : 3u));
+        A.res_docs[h] = r;
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(64, 8) void inc_apply_kernel(const AppendDesc *descs, uint32_t n, IncArenas A, IncDims M,
+                                                       uint8_t *bail) {
+    extern __shared__ __align__(16) uint8_t inc_lds[];
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t di = blockIdx.x; di < n; di += gridDim.x) {
+        if (!descs[di].inc) continue;
+        const AppendDesc D = descs[di];
+        const bool ok = inc_doc(D, A, M, lane, inc_lds);
+        if (lane == 0) bail[di] = ok ? 0 : 1;
+        __syncthreads();
+    }
+}
+
 }  // namespace hms
 
 hipError_t hm_launch_append(const AppendDesc *descs, uint32_t n_desc, const StoreArenas &src, const StoreArenas &dst,
@@ -156,6 +508,46 @@ hipError_t hm_launch_append(const AppendDesc *descs, uint32_t n_desc, const Stor
     const uint32_t grid = n_desc < 65535u ? n_desc : 65535u;
     hipLaunchKernelGGL(hms::append_kernel, dim3(grid), dim3(SWG), 0, s, descs, n_desc, src, dst, st_changes, st_deps,
                        st_ops, remap, S);
+    return hipGetLastError();
+}
+
+IncDims hm_inc_dims(uint32_t S, uint32_t new_c, uint32_t tgt, uint32_t stage, uint32_t regs, uint32_t surv,
+                    uint32_t slots) {
+    IncDims M = {};
+    M.S = S; M.new_c = new_c ? new_c : 1; M.tgt = tgt ? tgt : 1; M.stage = stage; M.regs = regs ? regs : 1;
+    M.surv = surv ? surv : 1; M.slots = slots ? slots : 1;
+    uint32_t o = 0;
+    auto take = [&](size_t bytes) { const uint32_t r = o; o += (uint32_t)((bytes + 15) & ~(size_t)15); return r; };
+    M.o_nc = take((size_t)M.new_c * 32);
+    M.o_dep = take((size_t)M.tgt * 8);
+    M.o_tkey = take((size_t)M.tgt * 8);
+    M.o_tsrc = take((size_t)M.tgt * 12);
+    M.o_tad = take((size_t)M.tgt * S * 4);
+    M.o_adn = take((size_t)M.new_c * S * 4);
+    M.o_skey = take((size_t)M.stage * 8);
+    M.o_sof = take((size_t)M.stage * 4);
+    M.o_reg = take((size_t)M.regs * 13);
+    M.o_sold = take((size_t)M.surv * 16);
+    M.o_wl = take((size_t)M.slots * HM_INC_SLOT_CAP * 16);
+    M.o_wls = take((size_t)M.slots * HM_INC_SLOT_CAP * 4);
+    M.o_wla = take((size_t)M.slots * HM_INC_SLOT_CAP);
+    M.o_scnt = take((size_t)M.slots * 4);
+    M.bytes = o;
+    return M;
+}
+
+hipError_t hm_launch_inc_apply(const AppendDesc *descs, uint32_t n, const IncArenas &A, const IncDims &M,
+                               uint8_t *bail, hipStream_t s) {
+    if (!n) return hipSuccess;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&hms::inc_apply_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    const uint32_t grid = n < (1u << 20) ? n : (1u << 20);
+    hipLaunchKernelGGL(hms::inc_apply_kernel, dim3(grid), dim3(64), M.bytes, s, descs, n, A, M, bail);
     return hipGetLastError();
 }
 

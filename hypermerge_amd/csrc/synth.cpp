@@ -527,6 +527,65 @@ void hm_synth_free(void *h) { delete (Output *)h; }
 
 uint64_t hm_synth_fnv1a64_docid(uint64_t seed, uint64_t g) { return fnv1a64(doc_id(seed, g)); }
 
+// Hypercore blocks of a synthetic batch, as Actor.writeChange / Block.pack store changes
+// (src/Actor.ts:73-80, src/Block.ts:6-16), uncompressed JSON form: one block per change, the
+// documents' changes in their arrival order.  Actor ids are "<docId>.<rank>" (their string
+// order is the rank order), map keys "k<register>", object ids ROOT or "o<id>-<docId>".
+// Sizes first (blocks == NULL): returns the total bytes; then fills data / block_off
+// [n_changes + 1] / doc_block [n_docs + 1].
+uint64_t hm_synth_blocks(uint64_t seed, const hm_doc_row *docs, uint32_t n_docs, const hm_change_row *ch,
+                         const hm_dep_row *dp, const hm_op_row *op, char *data, uint64_t *block_off,
+                         uint32_t *doc_block) {
+    static const char *names[] = {"makeMap", "makeTable", "makeList", "makeText", "ins", "set", "del", "link", "inc"};
+    const char *ROOT = "00000000-0000-0000-0000-000000000000";
+    uint64_t total = 0;
+    uint32_t nb = 0;
+    std::string js;
+    for (uint32_t d = 0; d < n_docs; d++) {
+        const hm_doc_row &D = docs[d];
+        const uint64_t g = (uint64_t)D.reserved[0] | ((uint64_t)D.reserved[1] << 32);
+        const std::string id = doc_id(seed, g);
+        auto actor = [&](uint32_t r) { char b[8]; snprintf(b, sizeof b, ".%02u", r); return id + b; };
+        auto objn = [&](uint32_t o) { return o == 0 ? std::string(ROOT) : "o" + std::to_string(o) + "-" + id; };
+        if (doc_block) doc_block[d] = nb;
+        for (uint32_t c = D.change_off; c < D.change_off + D.n_changes; c++) {
+            const hm_change_row &C = ch[c];
+            js = "{\"actor\":\"" + actor(C.actor) + "\",\"seq\":" + std::to_string(C.seq) + ",\"deps\":{";
+            for (uint32_t k = 0; k < C.n_deps; k++) {
+                const hm_dep_row &P = dp[C.dep_off + k];
+                js += (k ? ",\"" : "\"") + actor(P.actor) + "\":" + std::to_string(P.seq);
+            }
+            js += "},\"ops\":[";
+            for (uint32_t k = 0; k < C.n_ops; k++) {
+                const hm_op_row &O = op[C.op_first + k];
+                js += k ? ",{" : "{";
+                js += "\"action\":\"" + std::string(names[O.action < 9 ? O.action : 5]) + "\",\"obj\":\"" + objn(O.obj) + "\"";
+                if (O.action >= 5) {
+                    js += ",\"key\":\"k" + std::to_string(O.reg) + "\"";
+                    if (O.action == 7) js += ",\"value\":\"" + objn((uint32_t)O.value) + "\"";
+                    else if (O.action != 6) {
+                        if (O.vtag == HM_V_INT) js += ",\"value\":" + std::to_string((long long)O.value);
+                        else if (O.vtag == HM_V_TRUE) js += ",\"value\":true";
+                        else if (O.vtag == HM_V_FALSE) js += ",\"value\":false";
+                        else if (O.vtag == HM_V_STR) js += ",\"value\":\"s" + std::to_string((long long)O.value) + "\"";
+                        else js += ",\"value\":null";
+                    }
+                    if (O.datatype == HM_DT_COUNTER) js += ",\"datatype\":\"counter\"";
+                }
+                js += "}";
+            }
+            js += "]}";
+            if (block_off) block_off[nb] = total;
+            if (data) memcpy(data + total, js.data(), js.size());
+            total += js.size();
+            nb++;
+        }
+    }
+    if (block_off) block_off[nb] = total;
+    if (doc_block) doc_block[n_docs] = nb;
+    return total;
+}
+
 // Repo-global record keys of a synthetic shard (the clock exchange, exchange.hip): per document
 // FNV-1a64 of its base58 doc id, per (document, actor rank < n_actors) FNV-1a64 of the actor's
 // synthetic id "<docId>/<rank>" (0 past n_actors).

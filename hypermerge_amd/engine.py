@@ -27,7 +27,9 @@ EXPORTS = ("hm_abi_version", "hm_status_message", "hm_engine_create", "hm_engine
            "hm_comm_unique_id", "hm_comm_create", "hm_comm_destroy", "hm_comm_group_start", "hm_comm_group_end",
            "hm_clock_records_scratch_bytes", "hm_clock_records_device", "hm_clock_count_allgather",
            "hm_clock_allgather", "hm_clock_min_allreduce", "hm_comm_create_local", "hm_clock_exchange_host",
-           "hm_clock_min_host")
+           "hm_clock_min_host", "hm_decode_blocks", "hm_decoded_batch", "hm_decoded_status", "hm_decoded_n_strings",
+           "hm_decoded_string", "hm_decoded_actor", "hm_decoded_obj", "hm_decoded_reg", "hm_decoded_free",
+           "hm_store_set_incremental", "hm_store_last_routing", "hm_doc_open_n")
 
 _lib = None
 
@@ -82,11 +84,24 @@ def lib():
             "hm_comm_create_local": [vp, ctypes.c_int, vp],
             "hm_clock_exchange_host": [vp, ctypes.c_int, vp, vp, vp, ctypes.c_uint64, vp],
             "hm_clock_min_host": [vp, ctypes.c_int, vp, ctypes.c_uint64],
+            "hm_decode_blocks": [vp, vp, vp, u32, u32, ctypes.c_int, vp], "hm_decoded_batch": [vp, vp],
+            "hm_decoded_status": [vp], "hm_decoded_n_strings": [vp], "hm_decoded_string": [vp, u32, vp],
+            "hm_decoded_actor": [vp, u32, u32, vp], "hm_decoded_free": [vp],
+            "hm_decoded_obj": [vp, u32, u32, vp], "hm_decoded_reg": [vp, u32, u32, vp, vp],
+            "hm_store_set_incremental": [vp, ctypes.c_int], "hm_store_last_routing": [vp, vp],
+            "hm_doc_open_n": [vp, u32, vp],
         }
         for f, a in sig.items():
             getattr(L, f).argtypes = a
         L.hm_store_destroy.restype = None
         L.hm_comm_destroy.restype = None
+        L.hm_decoded_status.restype = ctypes.POINTER(ctypes.c_int32)
+        L.hm_decoded_n_strings.restype = ctypes.c_uint32
+        L.hm_decoded_string.restype = ctypes.c_void_p
+        L.hm_decoded_actor.restype = ctypes.c_void_p
+        L.hm_decoded_obj.restype = ctypes.c_void_p
+        L.hm_decoded_reg.restype = ctypes.c_void_p
+        L.hm_decoded_free.restype = None
         L.hm_clock_records_scratch_bytes.restype = ctypes.c_size_t
         _lib = L
     return _lib

@@ -225,6 +225,17 @@ class DocStore:
     def _check(self, st: int, what: str) -> None:
         self.engine._check(st, what)
 
+    def set_incremental(self, on: bool) -> None:
+        """Incremental applyRemoteChanges on the resident state (default on); off = every submit
+        re-merges each touched document's whole log.  Results are identical."""
+        self._check(self._L.hm_store_set_incremental(self._h, int(bool(on))), "hm_store_set_incremental")
+
+    def last_routing(self) -> Dict[str, int]:
+        """How the last submit's documents were merged: incremental / re-merged / handed back."""
+        out = np.zeros(3, np.uint32)
+        self._check(self._L.hm_store_last_routing(self._h, _p(out)), "hm_store_last_routing")
+        return {"incremental": int(out[0]), "remerged": int(out[1]), "handed_back": int(out[2])}
+
     def open(self) -> int:
         h = ctypes.c_uint32()
         self._check(self._L.hm_doc_open(self._h, ctypes.byref(h)), "hm_doc_open")
@@ -358,3 +369,76 @@ class DocStore:
         self._check(self._L.hm_store_clock_update(self._h, n, _p(hs), _p(w), _p(df), _p(st)),
                     "hm_store_clock_update")
         return w[:n].astype(bool), df[:n].astype(bool), st[:n]
+
+
+def slice_changes(b: Batch, lo: np.ndarray, hi: np.ndarray, docs: Optional[np.ndarray] = None) -> Batch:
+    """For each document d of `docs` (default: all), its changes lo[d] .. hi[d]-1 (document-local
+    arrival indices) with their dep and op rows, as a batch with batch-local offsets.  Document
+    totals (n_actors / n_regs / n_objs / flags) are kept: the rows' ids are the batch's own."""
+    idx = np.arange(b.n_docs) if docs is None else np.asarray(docs, np.int64)
+    drow = b.docs[idx].copy()
+    lo = np.asarray(lo, np.int64)[idx]
+    cnt = np.asarray(hi, np.int64)[idx] - lo
+    cnt = np.maximum(cnt, 0)
+    tot = int(cnt.sum())
+    excl = np.zeros(len(idx) + 1, np.int64)
+    np.cumsum(cnt, out=excl[1:])
+    ci = np.repeat(drow["change_off"].astype(np.int64) + lo - excl[:-1], cnt) + np.arange(tot)
+    ch = b.changes[ci].copy()
+
+    def rows(first, n, table):
+        n = n.astype(np.int64)
+        off = np.zeros(len(n) + 1, np.int64)
+        np.cumsum(n, out=off[1:])
+        ri = np.repeat(first.astype(np.int64) - off[:-1], n) + np.arange(int(off[-1]))
+        return table[ri].copy(), off
+    dp, doff = rows(ch["dep_off"], ch["n_deps"], b.deps)
+    op, ooff = rows(ch["op_first"], ch["n_ops"], b.ops)
+    ch["dep_off"] = doff[:-1]
+    ch["op_first"] = ooff[:-1]
+    drow["change_off"] = excl[:-1]
+    drow["n_changes"] = cnt
+    drow["dep_off"] = doff[excl[:-1]]
+    drow["n_deps"] = doff[excl[1:]] - doff[excl[:-1]]
+    drow["op_off"] = ooff[excl[:-1]]
+    drow["n_ops"] = ooff[excl[1:]] - ooff[excl[:-1]]
+    drow["reg_off"] = 0
+    return Batch(drow, ch, dp, op, b.a_stride)
+
+
+class RowStore(DocStore):
+    """Resident documents fed with prebuilt columnar rows (no per-document host encoder): actor
+    ranks, register and object ids in the rows are the caller's, stable across submits (e.g. a
+    synthetic feed, or rows from hm_decode_blocks over a repo-wide interner)."""
+
+    def open_n(self, n: int) -> int:
+        first = ctypes.c_uint32()
+        self._check(self._L.hm_doc_open_n(self._h, n, ctypes.byref(first)), "hm_doc_open_n")
+        return first.value
+
+    def submit_batch(self, b: Batch, handles: np.ndarray) -> int:
+        hs = np.ascontiguousarray(handles, np.uint32)
+        keep = (b, hs)
+        # the store reads the tables and per-document totals only (no launch-size hints)
+        cb = CBatch(b.n_docs, len(b.changes), len(b.deps), len(b.ops), 0, b.a_stride, 0, 0, 0, 0, 0, 0,
+                    b.docs.ctypes.data, b.changes.ctypes.data, b.deps.ctypes.data, b.ops.ctypes.data, None)
+        bid = ctypes.c_uint64()
+        self._check(self._L.hm_batch_submit(self._h, ctypes.byref(cb), _p(hs), None, ctypes.byref(bid)),
+                    "hm_batch_submit")
+        self._pending = (bid.value, list(range(len(hs))), None, keep)
+        return bid.value
+
+    def wait(self, out: Optional[BatchResult] = None) -> BatchResult:
+        """Results of the submitted batch; `out` (arrays of at least the batch's size, e.g. kept
+        between rounds by a long-running host) is filled instead of fresh arrays."""
+        bid, handles, _, _ = self._pending
+        self._pending = None
+        n, S = len(handles), self.S
+        if out is not None and len(out.docs) >= n:
+            r = BatchResult(out.docs[:n], out.clock[:n], out.back_clock[:n], out.heads[:n])
+        else:
+            r = BatchResult(np.zeros(n, DOC_RESULT_DT), np.zeros((n, S), np.uint32), np.zeros((n, S), np.uint32),
+                            np.zeros((n, S), np.uint32))
+        self._check(self._L.hm_batch_wait(self._h, ctypes.c_uint64(bid), _p(r.docs), _p(r.clock),
+                                          _p(r.back_clock), _p(r.heads)), "hm_batch_wait")
+        return r

@@ -82,6 +82,8 @@ def lib():
         _lib.hm_synth_free.argtypes = [ctypes.c_void_p]
         _lib.hm_synth_fnv1a64_docid.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
         _lib.hm_synth_fnv1a64_docid.restype = ctypes.c_uint64
+        _lib.hm_synth_blocks.argtypes = [ctypes.c_uint64] + [ctypes.c_void_p, ctypes.c_uint32] + [ctypes.c_void_p] * 6
+        _lib.hm_synth_blocks.restype = ctypes.c_uint64
         _lib.hm_synth_keys.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                        ctypes.c_void_p, ctypes.c_void_p]
     return _lib
@@ -115,6 +117,20 @@ def keys(cfg: SynthConfig, b: Batch):
     ak = np.zeros(n * S, np.uint64)
     lib().hm_synth_keys(cfg.seed, b.docs.ctypes.data, n, S, dk.ctypes.data, ak.ctypes.data)
     return dk, ak
+
+
+def blocks(cfg: SynthConfig, b: Batch):
+    """The batch's changes as raw-JSON hypercore blocks (one per change, arrival order):
+    (data u8, block_off u64[n_changes+1], doc_block u32[n_docs+1]) for hm_decode_blocks.
+    Map documents only (flat or nested maps; list ops are not rendered)."""
+    L = lib()
+    args = (cfg.seed, b.docs.ctypes.data, b.n_docs, b.changes.ctypes.data, b.deps.ctypes.data, b.ops.ctypes.data)
+    total = L.hm_synth_blocks(*args, None, None, None)
+    data = np.zeros(max(total, 1), np.uint8)
+    block_off = np.zeros(len(b.changes) + 1, np.uint64)
+    doc_block = np.zeros(b.n_docs + 1, np.uint32)
+    L.hm_synth_blocks(*args, data.ctypes.data, block_off.ctypes.data, doc_block.ctypes.data)
+    return data, block_off, doc_block
 
 
 def config(name: str, **overrides) -> SynthConfig:

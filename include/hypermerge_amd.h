@@ -255,7 +255,8 @@ int hm_clock_intersection_device(hm_engine *e, const uint32_t *a, const uint32_t
  * survivors, clocks).  `Backend.applyChanges(back, changes)` is a left fold of
  * addChange over `changes`, so applyChanges(applyChanges(s, A), B) is
  * applyChanges(s, A ++ B): a submit appends each document's new rows to its
- * log and re-merges the log with the batch kernels.  A document whose merge
+ * log and either applies them on the resident state (hm_store_set_incremental)
+ * or re-merges the log with the batch kernels.  A document whose merge
  * throws is rolled back to its previous log, exactly as a throwing
  * applyChanges leaves `DocBackend.back` (and `DocBackend.clock`) unchanged
  * (src/DocBackend.ts:170-184).
@@ -281,6 +282,9 @@ void hm_store_destroy(hm_store *s);
 /* A new, empty document (Backend.init()).  Handles are dense from 0. */
 int hm_doc_open(hm_store *s, uint32_t *out_doc);
 
+/* n new, empty documents with consecutive handles starting at *out_first. */
+int hm_doc_open_n(hm_store *s, uint32_t n, uint32_t *out_first);
+
 /* Append new changes to documents and re-merge them.  `b` is a batch in the
  * hm_batch layout whose rows are only the NEW changes (offsets local to `b`);
  * for each row i, docs[i].n_actors / n_regs / n_objs are document totals
@@ -299,6 +303,16 @@ int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
  * reported with their error status and rolled back before this returns. */
 int hm_batch_wait(hm_store *s, uint64_t batch_id, hm_doc_result *out_docs,
                   uint32_t *out_clock, uint32_t *out_back_clock, uint32_t *out_heads);
+
+/* Incremental applyRemoteChanges (on by default): a document whose new changes are each
+ * causally ready in arrival order on its resident state (nothing queued, no actor re-rank,
+ * map set/del/link ops, small submits) is advanced in place — history, allDeps, heads and
+ * clock appended, only the registers its new ops hit recomputed — instead of re-merging
+ * its whole log.  Results are identical either way; off = always re-merge. */
+int hm_store_set_incremental(hm_store *s, int on);
+/* Routing of the last submit: out3 = {incremental, re-merged, incremental handed back to
+ * the re-merge}. */
+int hm_store_last_routing(const hm_store *s, uint32_t *out3);
 
 /* Sizes of a document's log and merged state. */
 typedef struct {
@@ -342,6 +356,34 @@ int hm_store_clock_update(hm_store *s, uint32_t n, const uint32_t *docs, uint8_t
 int hm_sync_ranges_device(hm_engine *e, const uint64_t *present, const uint64_t *word_off,
                           const uint32_t *lo, const uint32_t *hi, uint32_t *out_end, uint32_t n,
                           void *stream);
+
+/* ------------------------------------------------------------------ */
+/* Blocks -> columnar rows (host, multi-threaded)                      */
+/* ------------------------------------------------------------------ */
+/*
+ * The host front of the path: hypercore blocks -> Change objects -> the rows above.
+ *   replaces: src/Block.ts:18-29 Block.unpack ('{"' raw JSON | 'BR' + brotli(JSON), else throw)
+ *             src/JsonBuffer.ts:1-4 JsonBuffer.parse, src/Actor.ts:137-141 Actor.parseBlock
+ *             + the host encoder (hypermerge_amd/js/columnar.js), row for row.
+ * Blocks of all documents lie back to back in `data`: block i is data[block_off[i] ..
+ * block_off[i+1]); document d's blocks (one Change each, in arrival order) are blocks
+ * doc_block[d] .. doc_block[d+1]-1.  Documents decode on `threads` threads; the rows do not
+ * depend on the thread count.  A document with an undecodable block (the reference's
+ * Block.unpack / JSON.parse throw) is reported HM_ERR_INVALID in hm_decoded_status with no
+ * rows.  a_stride 0 = the batch's widest document.  Brotli uses the system libbrotlidec.
+ */
+typedef struct hm_decoded hm_decoded;
+int hm_decode_blocks(const uint8_t *data, const uint64_t *block_off, const uint32_t *doc_block, uint32_t n_docs,
+                     uint32_t a_stride, int threads, hm_decoded **out);
+/* The decoded tables as a host hm_batch (pointers valid until hm_decoded_free). */
+int hm_decoded_batch(const hm_decoded *d, hm_batch *out);
+const int32_t *hm_decoded_status(const hm_decoded *d);            /* [n_docs] HM_OK / HM_ERR_INVALID */
+uint32_t hm_decoded_n_strings(const hm_decoded *d);               /* the string pool (keys, string values) */
+const char *hm_decoded_string(const hm_decoded *d, uint32_t i, size_t *len);
+const char *hm_decoded_actor(const hm_decoded *d, uint32_t doc, uint32_t rank, size_t *len);
+const char *hm_decoded_obj(const hm_decoded *d, uint32_t doc, uint32_t obj, size_t *len);       /* object uuid */
+const char *hm_decoded_reg(const hm_decoded *d, uint32_t doc, uint32_t reg, uint32_t *obj, size_t *len); /* key | elemId */
+void hm_decoded_free(hm_decoded *d);
 
 /* ------------------------------------------------------------------ */
 /* Clock exchange across the node's GPUs (RCCL over xGMI)              */

@@ -84,3 +84,33 @@ def test_feed_bitmaps_pack_lsb_first():
     assert list(off) == [0, 3]
     assert int(w[0]) == (1 | 8 | (1 << 63)) and int(w[1]) == (1 | (1 << 5)) and int(w[2]) == 0
     assert int(w[3]) == 7
+
+
+def test_slice_changes_rebuilds_each_document_range():
+    """store.slice_changes (the bench's / RowStore's row feed): the slices of a batch at any cut
+    points concatenate back to each document's rows."""
+    from hypermerge_amd.store import slice_changes
+    b = synth.generate(synth.config("C5", n_docs=50), threads=2)
+    rng = np.random.default_rng(1)
+    n = b.docs["n_changes"].astype(np.int64)
+    cut = (rng.random(b.n_docs) * (n + 1)).astype(np.int64)
+    sel = np.arange(0, b.n_docs, 2)
+    p1 = slice_changes(b, np.zeros(b.n_docs, np.int64), cut, sel)
+    p2 = slice_changes(b, cut, n, sel)
+    def rows(bt, j):
+        doc = bt.docs[j]
+        c = bt.changes[int(doc["change_off"]): int(doc["change_off"]) + int(doc["n_changes"])]
+        dp = bt.deps[int(doc["dep_off"]): int(doc["dep_off"]) + int(doc["n_deps"])]
+        op = bt.ops[int(doc["op_off"]): int(doc["op_off"]) + int(doc["n_ops"])]
+        # every change's deps / ops are its own, in order
+        assert (c["dep_off"][1:] == c["dep_off"][:-1] + c["n_deps"][:-1]).all() if len(c) else True
+        assert (c["op_first"][1:] == c["op_first"][:-1] + c["n_ops"][:-1]).all() if len(c) else True
+        cf = np.stack([c[f].astype(np.int64) for f in ("actor", "n_deps", "seq", "n_ops", "content_id")], 1)
+        return cf, dp, op
+    for j, d in enumerate(sel):
+        w = rows(b, int(d))
+        a, bb = rows(p1, j), rows(p2, j)
+        for x, y1, y2 in zip(w, a, bb):
+            assert np.concatenate([y1, y2]).tobytes() == x.tobytes()
+        for f in ("n_actors", "n_regs", "n_objs"):
+            assert p1.docs[f][j] == b.docs[f][d] == p2.docs[f][j]
