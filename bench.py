@@ -61,6 +61,9 @@ def main() -> int:
                     help="documents in the raw-blocks leg (JSON blocks -> native decoder -> merge)")
     ap.add_argument("--no-incremental", action="store_true",
                     help="skip the resident-store leg (1-2 new changes per resident document per round)")
+    ap.add_argument("--no-node", action="store_true",
+                    help="skip the Node DocBackend leg (C2 sample: JS restatement vs the GPU drop-in)")
+    ap.add_argument("--node-docs", type=int, default=2000)
     ap.add_argument("--arrival", type=int, default=None,
                     help="override the config's arrival order (0 generation, 1 actor-major as RepoBackend.loadDocument "
                          "concatenates, 2 shuffled)")
@@ -198,6 +201,10 @@ def main() -> int:
     incremental = None
     if rank == 0 and ws == 1 and not args.no_incremental and args.config == "C4" and args.arrival is None:
         incremental = _incremental(eng, batch, args)
+    # the Node host path end to end through the DocBackend message API (C2 sample)
+    node = None
+    if rank == 0 and ws == 1 and not args.no_node:
+        node = _node_e2e(args)
     # the same workload in RepoBackend.loadDocument's arrival order (actor-major concatenation,
     # src/RepoBackend.ts:242-248): changes whose deps come later in the array wait in the queue
     orders = None
@@ -243,7 +250,7 @@ def main() -> int:
                          "kernel": kern["kernel"], "kernel_ms": kern["kernel_ms"], "alg_bytes": kern["alg_bytes"],
                          "kernels": kern["kernels"], "traffic_detail": traffic},
             "cpu_baseline": cpu, "cpu_parallel": cpu_mt, "end_to_end": e2e, "from_blocks": from_blocks,
-            "resident_incremental": incremental,
+            "resident_incremental": incremental, "node_docbackend": node,
             "arrival_orders": orders,
             "host": _host_info(),
             "parity_sample_ok": parity, "unsupported_docs": unsupported, "error_docs": errors,
@@ -282,6 +289,38 @@ def _from_blocks(eng, batch, cfg, args):
             "merge_ms": (t2 - t1) * 1e3, "blocks": nb, "bytes": int(data.nbytes), "docs": k,
             "same_as_generated_rows": ok,
             "path": "JSON blocks -> hm_decode_blocks (native, multi-threaded) -> hm_merge_host (PCIe included)"}
+
+
+def _node_e2e(args):
+    """C2 documents fed through the DocBackend message API on one Node thread (tools/bench_node.js):
+    init() with each document's first 16 changes, then one applyRemoteChanges round per further
+    16.  `cpu` is the JS restatement (oracle/js/backend.js, BASELINE.md's second baseline); `gpu`
+    is the drop-in (GpuDocBackend, batched mode, patch diffs on), one GPU submit per round."""
+    import shutil
+    import subprocess
+    import tempfile
+    node = shutil.which("node")
+    if node is None:
+        return {"skipped": "node not installed"}
+    from hypermerge_amd import synth
+    from hypermerge_amd.columnar import decode_doc
+    b = synth.generate(synth.config("C2", n_docs=args.node_docs), threads=min(16, os.cpu_count() or 1))
+    docs = [decode_doc(b, i) for i in range(b.n_docs)]
+    here = os.path.dirname(os.path.abspath(__file__))
+    with tempfile.TemporaryDirectory() as td:
+        fn = os.path.join(td, "c2.json")
+        with open(fn, "w") as f:
+            json.dump({"docs": [[d[k:k + 16] for k in range(0, len(d), 16)] for d in docs]}, f)
+        p = subprocess.run([node, os.path.join(here, "tools", "bench_node.js"), fn, "cpu,gpu,gpu_async"],
+                           capture_output=True, text=True, timeout=600)
+    if p.returncode != 0:
+        return {"error": p.stderr[-800:]}
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    out["same_clocks"] = out["cpu"]["digest"] == out["gpu"]["digest"] == out["gpu_async"]["digest"]
+    out["sample"] = (f"C2: {b.n_docs} docs x 4 actors x 64 changes, 4 rounds of 16 changes per document "
+                     f"(init + 3 applyRemoteChanges), one Node thread")
+    out["gpu_vs_js"] = out["gpu"]["changes_per_s"] / out["cpu"]["changes_per_s"]
+    return out
 
 
 def _incremental(eng, batch, args, tail=4):

@@ -68,7 +68,7 @@ def build_node(force: bool = False) -> str:
             for f in (src, os.path.join(LIBDIR, "libhmgpu.so"), os.path.join(CSRC, "../../include/hypermerge_amd.h"))):
         _run(["gcc", "-O2", "-Wall", "-shared", "-fPIC", "-I/usr/include/node",
               "-I" + os.path.join(HERE, "..", "include"), "-o", out, src, "-L" + LIBDIR, "-lhmgpu",
-              "-Wl,-rpath,$ORIGIN"])
+              "-Wl,-rpath,$ORIGIN", "-lpthread"])
     return out
 
 

@@ -327,10 +327,13 @@ int hm_doc_open(hm_store *s, uint32_t *out_doc) {
         if (r) return r;
         DocMeta m;
         m.last.err_change = HM_NONE; m.last.err_op = HM_NONE;
-        // the new document's merged state is Backend.init(): write its result row
+        // the new document's merged state is Backend.init(): its result row, written on the
+        // engine stream (ordered before any submit; the reads below synchronise the stream)
         const uint32_t h = (uint32_t)s->docs.size();
         s->docs.push_back(m);
-        SCHK(s, hipMemcpy(s->res_docs + h, &m.last, sizeof(hm_doc_result), hipMemcpyHostToDevice));
+        hipStream_t st = hm_engine_stream(s->e);
+        SCHK(s, hipMemsetAsync(s->res_docs + h, 0, sizeof(hm_doc_result), st));
+        SCHK(s, hipMemsetAsync(&s->res_docs[h].err_change, 0xFF, 2 * sizeof(uint32_t), st));
         *out_doc = h;
         return HM_OK;
     } catch (...) {
@@ -535,6 +538,7 @@ int hm_batch_wait(hm_store *s, uint64_t batch_id, hm_doc_result *out_docs, uint3
     if (!s) return HM_ERR_INVALID;
     try {
         if (!s->pending || batch_id != s->pending_id) return hm_engine_fail(s->e, HM_ERR_INVALID, "no such batch in flight");
+        SCHK(s, hipSetDevice(hm_engine_device(s->e)));        // the caller may be a host thread of its own
         hipStream_t st = hm_engine_stream(s->e);
         PhaseTimer T(st);
         SCHK(s, hipStreamSynchronize(st));
@@ -619,6 +623,7 @@ int hm_store_last_routing(const hm_store *s, uint32_t *out3) {
 int hm_doc_info(hm_store *s, uint32_t doc, hm_doc_info_t *out) {
     if (!s || !out || doc >= s->docs.size()) return HM_ERR_INVALID;
     if (s->pending) return hm_engine_fail(s->e, HM_ERR_INVALID, "batch in flight");
+    SCHK(s, hipStreamSynchronize(hm_engine_stream(s->e)));
     const DocMeta &m = s->docs[doc];
     hm_doc_result r;
     SCHK(s, hipMemcpy(&r, s->res_docs + doc, sizeof(r), hipMemcpyDeviceToHost));
@@ -632,6 +637,7 @@ int hm_doc_read(hm_store *s, uint32_t doc, int32_t *hist, uint32_t *all_deps, hm
                 hm_surv_result *surv, uint32_t *clock, uint32_t *back_clock, uint32_t *heads) {
     if (!s || doc >= s->docs.size()) return HM_ERR_INVALID;
     if (s->pending) return hm_engine_fail(s->e, HM_ERR_INVALID, "batch in flight");
+    SCHK(s, hipStreamSynchronize(hm_engine_stream(s->e)));
     const DocMeta &m = s->docs[doc];
     const uint32_t S = s->S;
     if (hist && m.n_c) SCHK(s, hipMemcpy(hist, s->hist + m.c.off, m.n_c * 4, hipMemcpyDeviceToHost));
@@ -655,6 +661,46 @@ int hm_doc_log(hm_store *s, uint32_t doc, hm_change_row *changes, hm_dep_row *de
     if (deps && m.n_d) SCHK(s, hipMemcpy(deps, s->deps + m.d.off, m.n_d * sizeof(hm_dep_row), hipMemcpyDeviceToHost));
     if (ops && m.n_o) SCHK(s, hipMemcpy(ops, s->ops + m.o.off, m.n_o * sizeof(hm_op_row), hipMemcpyDeviceToHost));
     return HM_OK;
+}
+
+int hm_store_read_regs(hm_store *s, uint32_t n, const uint32_t *doc_handles, const uint32_t *regs,
+                       hm_reg_result *out_regs, hm_surv_result *out_surv, uint32_t surv_cap, uint32_t *out_n_surv) {
+    if (!s || (n && (!doc_handles || !regs || !out_regs || (surv_cap && !out_surv)))) return HM_ERR_INVALID;
+    if (s->pending) return hm_engine_fail(s->e, HM_ERR_INVALID, "batch in flight");
+    try {
+        std::vector<uint32_t> req(2 * (size_t)n);
+        for (uint32_t i = 0; i < n; i++) {
+            if (doc_handles[i] >= s->docs.size()) return hm_engine_fail(s->e, HM_ERR_INVALID, "bad handle");
+            const DocMeta &m = s->docs[doc_handles[i]];
+            if (regs[i] >= m.n_r) return hm_engine_fail(s->e, HM_ERR_INVALID, "register outside its document");
+            req[i] = m.r.off + regs[i];
+            req[n + i] = m.o.off;
+        }
+        if (out_n_surv) *out_n_surv = 0;
+        if (!n) return HM_OK;
+        hipStream_t st = hm_engine_stream(s->e);
+        auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+        const size_t o_req = 0, o_cnt = al(8 * (size_t)n), o_regs = o_cnt + 256,
+                     o_surv = o_regs + al((size_t)n * sizeof(hm_reg_result)), total = o_surv + al((size_t)surv_cap * sizeof(hm_surv_result) + 1);
+        int rc = ensure_stage(s, total);
+        if (rc) return rc;
+        uint8_t *sp = s->stage.p;
+        SCHK(s, hipMemcpyAsync(sp + o_req, req.data(), req.size() * 4, hipMemcpyHostToDevice, st));
+        SCHK(s, hipMemsetAsync(sp + o_cnt, 0, 4, st));
+        SCHK(s, hm_launch_read_regs(n, (const uint32_t *)(sp + o_req), (const uint32_t *)(sp + o_req) + n, s->regs, s->surv,
+                                    (hm_reg_result *)(sp + o_regs), (hm_surv_result *)(sp + o_surv), surv_cap,
+                                    (uint32_t *)(sp + o_cnt), st));
+        uint32_t total_surv = 0;
+        SCHK(s, hipMemcpyAsync(&total_surv, sp + o_cnt, 4, hipMemcpyDeviceToHost, st));
+        SCHK(s, hipMemcpyAsync(out_regs, sp + o_regs, (size_t)n * sizeof(hm_reg_result), hipMemcpyDeviceToHost, st));
+        SCHK(s, hipStreamSynchronize(st));
+        if (out_n_surv) *out_n_surv = total_surv;
+        if (total_surv > surv_cap) return hm_engine_fail(s->e, HM_ERR_NOMEM, "surv_cap below the survivors of the registers");
+        if (total_surv) SCHK(s, hipMemcpy(out_surv, sp + o_surv, (size_t)total_surv * sizeof(hm_surv_result), hipMemcpyDeviceToHost));
+        return HM_OK;
+    } catch (...) {
+        return hm_engine_fail(s->e, HM_ERR_NOMEM, "exception in hm_store_read_regs");
+    }
 }
 
 int hm_doc_history_prefix(hm_store *s, uint32_t doc, uint32_t n, uint32_t *out) {

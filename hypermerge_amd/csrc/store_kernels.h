@@ -63,6 +63,9 @@ hipError_t hm_launch_inc_apply(const AppendDesc *descs, uint32_t n, const IncAre
 hipError_t hm_launch_append(const AppendDesc *descs, uint32_t n_desc, const StoreArenas &src, const StoreArenas &dst,
                             const hm_change_row *st_changes, const hm_dep_row *st_deps, const hm_op_row *st_ops,
                             const uint8_t *remap, uint32_t S, hipStream_t s);
+hipError_t hm_launch_read_regs(uint32_t n, const uint32_t *abs_reg, const uint32_t *surv_base, const hm_reg_result *regs,
+                               const hm_surv_result *surv, hm_reg_result *out_regs, hm_surv_result *out_surv, uint32_t cap,
+                               uint32_t *counter, hipStream_t s);
 hipError_t hm_launch_gather(const uint32_t *handles, uint32_t n, uint32_t S, const hm_doc_result *res_docs,
                             const uint32_t *clock, const uint32_t *back_clock, const uint32_t *heads, uint8_t *out,
                             hipStream_t s);

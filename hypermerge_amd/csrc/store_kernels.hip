@@ -499,6 +499,22 @@ __global__ __launch_bounds__(64, 8) void inc_apply_kernel(const AppendDesc *desc
     }
 }
 
+// Rows of chosen registers (incremental patches): request i reads register abs_reg[i] and its
+// survivors (doc op-segment base surv_base[i] + surv_off) into out_surv at an offset taken
+// from a bump counter; its row's surv_off is rewritten to that offset.
+__global__ void read_regs_kernel(uint32_t n, const uint32_t *abs_reg, const uint32_t *surv_base, const hm_reg_result *regs,
+                                 const hm_surv_result *surv, hm_reg_result *out_regs, hm_surv_result *out_surv,
+                                 uint32_t cap, uint32_t *counter) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    hm_reg_result r = regs[abs_reg[i]];
+    const uint32_t off = atomicAdd(counter, r.n_surv);
+    if (off + r.n_surv <= cap)
+        for (uint32_t k = 0; k < r.n_surv; k++) out_surv[off + k] = surv[surv_base[i] + r.surv_off + k];
+    r.surv_off = off;
+    out_regs[i] = r;
+}
+
 }  // namespace hms
 
 hipError_t hm_launch_append(const AppendDesc *descs, uint32_t n_desc, const StoreArenas &src, const StoreArenas &dst,
@@ -548,6 +564,15 @@ hipError_t hm_launch_inc_apply(const AppendDesc *descs, uint32_t n, const IncAre
     }
     const uint32_t grid = n < (1u << 20) ? n : (1u << 20);
     hipLaunchKernelGGL(hms::inc_apply_kernel, dim3(grid), dim3(64), M.bytes, s, descs, n, A, M, bail);
+    return hipGetLastError();
+}
+
+hipError_t hm_launch_read_regs(uint32_t n, const uint32_t *abs_reg, const uint32_t *surv_base, const hm_reg_result *regs,
+                               const hm_surv_result *surv, hm_reg_result *out_regs, hm_surv_result *out_surv, uint32_t cap,
+                               uint32_t *counter, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(hms::read_regs_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, abs_reg, surv_base, regs, surv,
+                       out_regs, out_surv, cap, counter);
     return hipGetLastError();
 }
 

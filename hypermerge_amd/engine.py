@@ -29,7 +29,7 @@ EXPORTS = ("hm_abi_version", "hm_status_message", "hm_engine_create", "hm_engine
            "hm_clock_allgather", "hm_clock_min_allreduce", "hm_comm_create_local", "hm_clock_exchange_host",
            "hm_clock_min_host", "hm_decode_blocks", "hm_decoded_batch", "hm_decoded_status", "hm_decoded_n_strings",
            "hm_decoded_string", "hm_decoded_actor", "hm_decoded_obj", "hm_decoded_reg", "hm_decoded_free",
-           "hm_store_set_incremental", "hm_store_last_routing", "hm_doc_open_n")
+           "hm_store_set_incremental", "hm_store_last_routing", "hm_doc_open_n", "hm_store_read_regs")
 
 _lib = None
 
@@ -89,7 +89,7 @@ def lib():
             "hm_decoded_actor": [vp, u32, u32, vp], "hm_decoded_free": [vp],
             "hm_decoded_obj": [vp, u32, u32, vp], "hm_decoded_reg": [vp, u32, u32, vp, vp],
             "hm_store_set_incremental": [vp, ctypes.c_int], "hm_store_last_routing": [vp, vp],
-            "hm_doc_open_n": [vp, u32, vp],
+            "hm_doc_open_n": [vp, u32, vp], "hm_store_read_regs": [vp, u32, vp, vp, vp, vp, u32, vp],
         }
         for f, a in sig.items():
             getattr(L, f).argtypes = a

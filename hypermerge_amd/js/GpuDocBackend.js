@@ -16,7 +16,14 @@
 //                mode 'sync' flushes inside the caller's stack (the reference's Queue
 //                semantics: a push runs the merge synchronously); mode 'batched' flushes
 //                once per event-loop turn (setImmediate), merging every document that
-//                received changes during the turn in one launch.
+//                received changes during the turn in one launch; mode 'async' does the
+//                same but waits for the device on the store's host thread (waitAsync,
+//                completion through a napi_threadsafe_function), so the event loop never
+//                blocks on the GPU.
+//                Patches are incremental: after a round in which a document's new changes
+//                all applied, only the registers its new ops hit are read back
+//                (hm_store_read_regs, one call per store and round) and diffed against the
+//                document's previous view; otherwise the whole document is re-read.
 //   ClockStore   the reference's clock table semantics (src/ClockStore.ts:24-112) kept in
 //                host memory, with updateDocs(): ClockStore.update(repo, doc, doc.clock)
 //                for many documents from one GPU upsert-max (hm_store_clock_update).
@@ -83,6 +90,11 @@ class GpuBackendState {
     this.log = []
     this.opActor = []                // doc-local op index -> [op, actor] (the log's ops in order)
     this.view = null                 // materialized view of the last patch (diff base)
+    this.objType = new Map([[0, 0]]) // obj id -> make action (ROOT = map), kept per round
+    this.newObjs = []                // objects the last round created
+    this.roundSeq = 0                // rounds applied ...
+    this.patchedSeq = 0              // ... and the round the view reflects
+    this.pendingRegs = null          // registers the last round's ops hit, read back (incremental patch)
     this.histLen = 0
     this.nQueued = 0
     this.clock = {}
@@ -143,22 +155,27 @@ class GpuEngine {
     }
   }
 
+  // leading callbacks run; each document's head GPU job forms the round
+  collectRound() {
+    for (;;) {
+      const round = []
+      for (const [state, q] of Array.from(this.queues)) {
+        while (q.length && q[0].changes === null) q.shift().done(null)
+        if (q.length) round.push([state, q.shift()])
+        else this.queues.delete(state)
+      }
+      if (round.length || this.queues.size === 0) return round
+    }
+  }
+
   flush() {
+    if (this.mode === 'async') return this.flushAsync()
     if (this.flushing) return
     this.flushing = true
     try {
       for (;;) {
-        // run leading callbacks, collect each document's head GPU job
-        const round = []
-        for (const [state, q] of Array.from(this.queues)) {
-          while (q.length && q[0].changes === null) q.shift().done(null)
-          if (q.length) round.push([state, q.shift()])
-          else this.queues.delete(state)
-        }
-        if (!round.length) {
-          if (this.queues.size === 0) break
-          continue
-        }
+        const round = this.collectRound()
+        if (!round.length) break
         this.runRound(round)
       }
     } finally {
@@ -166,10 +183,63 @@ class GpuEngine {
     }
   }
 
+  flushAsync() {
+    if (this.flushing) return
+    this.flushing = true
+    let round
+    try {
+      round = this.collectRound()
+    } catch (e) {
+      this.flushing = false
+      throw e
+    }
+    if (!round.length) { this.flushing = false; return }
+    this.runRoundAsync(round, () => { this.flushing = false; this.flushAsync() })
+  }
+
+  // resolves when every queued job has run
+  idle() {
+    return new Promise((resolve) => {
+      const check = () => (this.queues.size || this.flushing || this.scheduled ? setImmediate(check) : resolve())
+      check()
+    })
+  }
+
   // One applyChanges per document of the round: the documents of each store (device shard x
   // stride) go to that store as one batch; every store's batch is submitted before any is
   // waited for, so the devices merge at once.
   runRound(round) {
+    const { pending, errors } = this.submitRound(round)
+    for (const p of pending) this.finishStore(p, addon.wait(p.store, p.id), errors)
+    this.raise(errors)
+  }
+
+  runRoundAsync(round, done) {
+    let sub
+    try {
+      sub = this.submitRound(round)
+    } catch (e) {
+      done()
+      throw e
+    }
+    const { pending, errors } = sub
+    let left = pending.length
+    const finish = () => { try { this.raise(errors) } finally { done() } }
+    if (!left) { finish(); return }
+    for (const p of pending) {
+      addon.waitAsync(p.store, p.id, (err, r) => {
+        try {
+          if (err) {
+            p.items.forEach(({ state, job, snap, moved }) => { if (!moved) state.enc.restore(snap); errors.push([job, err]) })
+          } else this.finishStore(p, r, errors)
+        } finally {
+          if (--left === 0) finish()
+        }
+      })
+    }
+  }
+
+  submitRound(round) {
     const groups = new Map()         // store -> [{state, job, snap, append, moved}]
     const errors = []
     for (const [state, job] of round) {
@@ -198,35 +268,95 @@ class GpuEngine {
       const stride = items[0].moved ? items[0].moved.stride : items[0].state.stride
       const b = C.buildBatch(items.map((it) => it.append), stride)
       const handles = Uint32Array.from(items.map((it) => (it.moved ? it.moved.handle : it.state.handle)))
-      pending.push([store, stride, items, addon.submit(store, b.docs, b.changes, b.deps, b.ops, handles, b.remap)])
+      pending.push({ store, stride, items, id: addon.submit(store, b.docs, b.changes, b.deps, b.ops, handles, b.remap) })
     }
-    for (const [store, S, items, id] of pending) {
-      const r = addon.wait(store, id)
-      this.submits++
-      items.forEach(({ state, job, snap, moved }, i) => {
-        const res = C.readDocResult(r.docs, i)
-        if (res.status !== 0) {
-          if (!moved) state.enc.restore(snap)
-          errors.push([job, this.errorFor(state, job.changes, res)])
-          return
+    return { pending, errors }
+  }
+
+  finishStore({ store, stride: S, items }, r, errors) {
+    this.submits++
+    const ok = []
+    items.forEach((it, i) => {
+      const { state, job, snap, moved, append } = it
+      const res = C.readDocResult(r.docs, i)
+      if (res.status !== 0) {
+        if (!moved) state.enc.restore(snap)
+        errors.push([job, this.errorFor(state, job.changes, res)])
+        return
+      }
+      if (moved) {
+        Object.assign(state, { enc: moved.enc, store: moved.store, stride: moved.stride, handle: moved.handle })
+        state.objType = null           // ids re-encoded: rebuilt from the log at the next patch
+        this.restrides++
+      }
+      const base = state.log.length
+      state.log.push(...job.changes)
+      for (const c of job.changes) for (const op of c.ops || []) state.opActor.push([op, c.actor])
+      // objects this round created (make ops, first creation wins)
+      state.newObjs = []
+      if (state.objType && !moved) {
+        for (let k = 0; k < append.ops.length / C.OP_ROW; k++) {
+          const act = append.ops[k * C.OP_ROW + 16]
+          if (act > C.ACTIONS.makeText) continue
+          const o = append.ops.readUInt32LE(k * C.OP_ROW)
+          if (!state.objType.has(o)) { state.objType.set(o, act); state.newObjs.push(o) }
         }
-        if (moved) {
-          Object.assign(state, { enc: moved.enc, store: moved.store, stride: moved.stride, handle: moved.handle })
-          this.restrides++
-        }
-        const base = state.log.length
-        state.log.push(...job.changes)
-        for (const c of job.changes) for (const op of c.ops || []) state.opActor.push([op, c.actor])
-        const prevHist = state.histLen
-        state.histLen = res.histLen
-        state.nQueued = res.nQueued
-        state.clock = Clock.fromRow(r.clock, i * S * 4, state.enc.actors)
-        state.deps = Clock.fromRow(r.heads, i * S * 4, state.enc.actors)
-        const backClock = Clock.fromRow(r.backClock, i * S * 4, state.enc.actors)
-        state.backClock = backClock
-        job.done({ res, base, prevHist, backClock, minCmp: Clock.CMP_CODES[res.minCmp] })
-      })
+      }
+      const prevHist = state.histLen, prevQueued = state.nQueued, prevSeq = state.roundSeq
+      state.roundSeq++
+      state.histLen = res.histLen
+      state.nQueued = res.nQueued
+      state.clock = Clock.fromRow(r.clock, i * S * 4, state.enc.actors)
+      state.deps = Clock.fromRow(r.heads, i * S * 4, state.enc.actors)
+      const backClock = Clock.fromRow(r.backClock, i * S * 4, state.enc.actors)
+      state.backClock = backClock
+      // incremental patch: the view is current up to the previous round (a fresh document's
+      // view is the empty root map) and every new change applied
+      if (state.view === null && prevSeq === 0 && state.patchedSeq === 0)
+        state.view = new Map([[C.ROOT_ID, { type: 'map', keys: new Map(), elems: [] }]])
+      const simple = !moved && state.view !== null && state.objType !== null && state.patchedSeq === prevSeq &&
+        prevQueued === 0 && res.nQueued === 0 && res.histLen - prevHist === job.changes.length
+      ok.push({ state, job, res, append, simple, payload: { res, base, prevHist, backClock, minCmp: Clock.CMP_CODES[res.minCmp] } })
+    })
+    if (this.patches) this.prefetchRegs(store, ok)
+    for (const e of ok) e.job.done(e.payload)
+  }
+
+  // one read of the registers the round's new ops hit, for every simple document of the store
+  prefetchRegs(store, ok) {
+    const docs = [], regs = [], owners = []
+    let cap = 0
+    for (const e of ok) {
+      const st = e.state
+      st.pendingRegs = null
+      if (!e.simple) continue
+      st.pendingRegs = []
+      const seen = new Set()
+      for (let k = 0; k < e.append.ops.length / C.OP_ROW; k++) {
+        const act = e.append.ops[k * C.OP_ROW + 16]
+        if (act < C.ACTIONS.set) continue                   // make / ins: no visible value of their own
+        const g = e.append.ops.readUInt32LE(k * C.OP_ROW + 4)
+        if (g === C.NONE || seen.has(g)) continue
+        seen.add(g)
+        docs.push(st.handle); regs.push(g); owners.push(st)
+      }
+      cap += e.res.nSurv
     }
+    if (!regs.length) return
+    const rr = addon.readRegs(store, Uint32Array.from(docs), Uint32Array.from(regs), cap)
+    for (let q = 0; q < regs.length; q++) {
+      const b = q * C.REG_RESULT
+      const n = rr.regs.readUInt32LE(b), off = rr.regs.readUInt32LE(b + 4)
+      const surv = []
+      for (let x = 0; x < n; x++) {
+        const sb = (off + x) * C.SURV_RESULT
+        surv.push([rr.surv.readUInt32LE(sb), rr.surv.readUInt32LE(sb + 4), rr.surv.readUInt32LE(sb + 8), rr.surv.readUInt32LE(sb + 12)])
+      }
+      owners[q].pendingRegs.push({ g: regs[q], n, li: rr.regs.readInt32LE(b + 8), o: rr.regs.readUInt32LE(b + 12), surv })
+    }
+  }
+
+  raise(errors) {
     for (const [job, err] of errors) {
       if (job.fail) job.fail(err)
       else if (this.onError) this.onError(err)
@@ -251,6 +381,7 @@ class GpuEngine {
 
   // Synchronous single-document applyChanges (Backend.applyChanges)
   applyChanges(state, changes) {
+    if (this.mode === 'async' && this.flushing) throw new Error('GpuEngine.applyChanges while an async round is in flight')
     let out = null, err = null
     const prevMode = this.mode
     this.mode = 'sync'
@@ -329,14 +460,34 @@ function opValue(state, vtag, lo, hi) {
   }
 }
 
-// the merged document as {objUuid -> {type, keys: Map(key -> entry) | elems: [[elemId, entry]]}}
-function materialize(state) {
-  const r = addon.read(state.store, state.handle)
+function objTypes(state) {
+  if (state.objType) return state.objType
   const objType = new Map([[0, 0]])
   for (const [op] of state.opActor) {
     const a = C.ACTIONS[op.action]
     if (a <= C.ACTIONS.makeText) { const o = state.enc.objs.get(op.obj); if (!objType.has(o)) objType.set(o, a) }
   }
+  state.objType = objType
+  return objType
+}
+
+// a register's survivors [[op, vtag, lo, hi]] -> a diff value with conflicts
+function entryOf(state, surv) {
+  const vals = surv.map(([k, vt, lo, hi]) => {
+    const [op, actor] = state.opActor[k]
+    const v = opValue(state, vt, lo, hi)
+    if (op.datatype) v.datatype = op.datatype
+    return [actor, v]
+  })
+  const entry = Object.assign({}, vals[0][1])
+  if (vals.length > 1) entry.conflicts = vals.slice(1).map(([actor, v]) => Object.assign({ actor }, v))
+  return entry
+}
+
+// the merged document as {objUuid -> {type, keys: Map(key -> entry) | elems: [[elemId, entry]]}}
+function materialize(state) {
+  const r = addon.read(state.store, state.handle)
+  const objType = objTypes(state)
   const view = new Map()
   const nRegs = r.regs.length / C.REG_RESULT
   for (let g = 0; g < nRegs; g++) {
@@ -349,14 +500,9 @@ function materialize(state) {
     const surv = []
     for (let q = 0; q < n; q++) {
       const sb = (off + q) * C.SURV_RESULT
-      const k = r.surv.readUInt32LE(sb), vt = r.surv.readUInt32LE(sb + 4)
-      const [op, actor] = state.opActor[k]
-      const v = opValue(state, vt, r.surv.readUInt32LE(sb + 8), r.surv.readUInt32LE(sb + 12))
-      if (op.datatype) v.datatype = op.datatype
-      surv.push([actor, v])
+      surv.push([r.surv.readUInt32LE(sb), r.surv.readUInt32LE(sb + 4), r.surv.readUInt32LE(sb + 8), r.surv.readUInt32LE(sb + 12)])
     }
-    const entry = Object.assign({}, surv[0][1])
-    if (surv.length > 1) entry.conflicts = surv.slice(1).map(([actor, v]) => Object.assign({ actor }, v))
+    const entry = entryOf(state, surv)
     const uuid = state.enc.objList[o]
     let ov = view.get(uuid)
     if (!ov) { ov = { type: TYPE_OF[t], keys: new Map(), elems: [] }; view.set(uuid, ov) }
@@ -370,6 +516,64 @@ function materialize(state) {
     if (!view.has(uuid)) view.set(uuid, { type: TYPE_OF[t], keys: new Map(), elems: [] })
   }
   return view
+}
+
+// the previous view advanced by the registers the round's ops hit (state.pendingRegs): the
+// same diffs diffViews would give for them — objects created, list removals (descending
+// index), insertions (ascending final index), then value changes
+function applyRegs(state) {
+  const view = state.view, diffs = [], sig = (e) => JSON.stringify(e)
+  for (const o of state.newObjs) {
+    const uuid = state.enc.objList[o]
+    if (view.has(uuid)) continue
+    const t = TYPE_OF[state.objType.get(o)]
+    view.set(uuid, { type: t, keys: new Map(), elems: [] })
+    if (uuid !== C.ROOT_ID) diffs.push({ action: 'create', obj: uuid, type: t })
+  }
+  const lists = new Map()
+  for (const r of state.pendingRegs) {
+    if (r.o === C.NONE) continue
+    const t = state.objType.has(r.o) ? state.objType.get(r.o) : 0
+    const list = t === 2 || t === 3
+    const uuid = state.enc.objList[r.o]
+    let ov = view.get(uuid)
+    if (!ov) { ov = { type: TYPE_OF[t], keys: new Map(), elems: [] }; view.set(uuid, ov) }
+    const key = state.enc.regList[r.g][1]
+    const entry = r.n ? entryOf(state, r.surv) : null
+    if (!list) {
+      const old = ov.keys.get(key)
+      if (!entry) {
+        if (old !== undefined) { ov.keys.delete(key); diffs.push({ action: 'remove', type: ov.type, obj: uuid, key }) }
+      } else if (old === undefined || sig(old) !== sig(entry)) {
+        ov.keys.set(key, entry)
+        diffs.push(Object.assign({ action: 'set', type: ov.type, obj: uuid, key }, entry))
+      }
+      continue
+    }
+    let L = lists.get(uuid)
+    if (!L) { L = { ov, rem: [], ins: [], set: [] }; lists.set(uuid, L) }
+    const visible = r.n > 0 && r.li >= 0
+    const oldIdx = ov.elems.findIndex((e) => e[0] === key)
+    if (oldIdx >= 0 && !visible) L.rem.push(oldIdx)
+    else if (oldIdx < 0 && visible) L.ins.push([r.li, key, entry])
+    else if (visible && sig(ov.elems[oldIdx][1]) !== sig(entry)) L.set.push([key, entry])
+  }
+  for (const [uuid, L] of lists) {
+    L.rem.sort((a, b) => b - a).forEach((i) => {
+      L.ov.elems.splice(i, 1)
+      diffs.push({ action: 'remove', type: L.ov.type, obj: uuid, index: i })
+    })
+    L.ins.sort((a, b) => a[0] - b[0]).forEach(([i, key, e]) => {
+      L.ov.elems.splice(i, 0, [key, e])
+      diffs.push(Object.assign({ action: 'insert', type: L.ov.type, obj: uuid, index: i, elemId: key }, e))
+    })
+    L.set.forEach(([key, e]) => {
+      const i = L.ov.elems.findIndex((x) => x[0] === key)
+      L.ov.elems[i] = [key, e]
+      diffs.push(Object.assign({ action: 'set', type: L.ov.type, obj: uuid, index: i }, e))
+    })
+  }
+  return diffs
 }
 
 function diffViews(prev, next) {
@@ -403,10 +607,17 @@ function diffViews(prev, next) {
 
 function makePatch(state) {
   let diffs = []
-  if (state.engine.patches) {
-    const view = materialize(state)
-    diffs = diffViews(state.view || new Map(), view)
-    state.view = view
+  if (state.engine.patches && state.patchedSeq !== state.roundSeq) {
+    if (state.view && state.pendingRegs && state.objType) {
+      diffs = applyRegs(state)
+      state.incrementalPatches = (state.incrementalPatches || 0) + 1
+    } else {
+      const view = materialize(state)
+      diffs = diffViews(state.view || new Map(), view)
+      state.view = view
+    }
+    state.patchedSeq = state.roundSeq
+    state.pendingRegs = null
   }
   return { clock: Object.assign({}, state.clock), deps: Object.assign({}, state.deps), canUndo: false, canRedo: false, diffs }
 }

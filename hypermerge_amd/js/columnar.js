@@ -47,8 +47,10 @@ class DocEncoder {
     this.objList = [ROOT_ID]
     this.regs = new Map()            // `${obj}\u0000${key}` -> reg
     this.regList = []                // reg -> [obj, key]
-    this.content = new Map()
+    this.content = new Map()         // `${actor}\u0000${seq}` -> [[cid, canonical|null, change]]
+    this.nContent = 0
     this.flags = 0
+    this.journal = null              // content entries replaced since the last snapshot
   }
 
   obj(u) {
@@ -64,13 +66,49 @@ class DocEncoder {
     return i
   }
 
+  // O(1) snapshot: the tables only grow (actors are replaced, never edited), so a snapshot is
+  // their lengths plus a journal of the content entries an encode replaces
   snapshot() {
-    return [this.actors.slice(), new Map(this.objs), this.objList.slice(), new Map(this.regs), this.regList.slice(),
-      new Map(this.content), this.flags]
+    this.journal = []
+    return [this.actors, this.objList.length, this.regList.length, this.nContent, this.flags, this.journal]
   }
 
   restore(s) {
-    [this.actors, this.objs, this.objList, this.regs, this.regList, this.content, this.flags] = s
+    const [actors, nObj, nReg, nContent, flags, journal] = s
+    this.actors = actors
+    for (let i = nObj; i < this.objList.length; i++) this.objs.delete(this.objList[i])
+    this.objList.length = nObj
+    for (let i = nReg; i < this.regList.length; i++) this.regs.delete(this.regList[i][0] + '\u0000' + this.regList[i][1])
+    this.regList.length = nReg
+    for (let i = journal.length - 1; i >= 0; i--) {
+      const [k, prev] = journal[i]
+      if (prev === undefined) this.content.delete(k); else this.content.set(k, prev)
+    }
+    journal.length = 0
+    this.nContent = nContent
+    this.flags = flags
+  }
+
+  // content id (Immutable `equals` classes): equal content needs equal (actor, seq), so the
+  // canonical form is only built when an (actor, seq) repeats in the document
+  contentId(c) {
+    const k = c.actor + '\u0000' + c.seq
+    const ent = this.content.get(k)
+    if (ent === undefined) {
+      const cid = this.nContent++
+      if (this.journal) this.journal.push([k, undefined])
+      this.content.set(k, [[cid, null, c]])
+      return cid
+    }
+    const ck = canonical(c)
+    for (const e of ent) {
+      if (e[1] === null) e[1] = canonical(e[2])
+      if (e[1] === ck) return e[0]
+    }
+    const cid = this.nContent++
+    if (this.journal) this.journal.push([k, ent])
+    this.content.set(k, ent.concat([[cid, ck, c]]))
+    return cid
   }
 
   // -> { changes: Buffer, deps: Buffer, ops: Buffer, nActors, nRegs, nObjs, flags, remap: Uint8Array|null }
@@ -108,9 +146,7 @@ class DocEncoder {
         db.writeUInt32LE(deps[a] >>> 0, di * DEP_ROW + 4)
         di++
       }
-      const ck = canonical(c)
-      let cid = this.content.get(ck)
-      if (cid === undefined) { cid = this.content.size; this.content.set(ck, cid) }
+      const cid = this.contentId(c)
       const opFirst = oi
       for (const op of c.ops || []) {
         const act = ACTIONS[op.action]

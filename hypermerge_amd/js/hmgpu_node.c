@@ -6,12 +6,18 @@
  * (no C++ and no exceptions cross the ABI).  GpuDocBackend.js (same directory) is the
  * only caller; it mirrors the reference's DocBackend API (src/DocBackend.ts:46-213).
  *
+ * waitAsync: each store owns one host thread that runs hm_batch_wait for it; completion is
+ * delivered to JS on the main thread through a napi_threadsafe_function (SURVEY.md §8b:
+ * N-API calls only from the main thread, one engine host thread per GPU store), so the
+ * event loop never blocks on the device.
+ *
  * Build (hypermerge_amd/build.py):
  *   gcc -shared -fPIC -I/usr/include/node -Iinclude hmgpu_node.c -Lhypermerge_amd/_lib -lhmgpu
  *       -Wl,-rpath,'$ORIGIN' -o hypermerge_amd/_lib/hmgpu.node
  */
-#define NAPI_VERSION 3
+#define NAPI_VERSION 4
 #include <node_api.h>
+#include <pthread.h>
 #include <stdbool.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -34,16 +40,62 @@ static napi_value throw_status(napi_env env, hm_engine *e, int st, const char *w
     return NULL;
 }
 
+typedef struct Job {
+    struct Job *next;
+    uint64_t id;
+    uint32_t n, S;
+    int st;
+    char err[512];
+    uint8_t *buf;                 /* results: docs | clock | backClock | heads */
+    napi_threadsafe_function tsfn;
+} Job;
+
 typedef struct {
     hm_engine *engine;
     hm_store *store;
     uint32_t a_stride;
     uint32_t pending_n;   /* documents of the batch in flight (sizes Wait's buffers) */
+    /* the store's host thread (waitAsync) */
+    pthread_t thread;
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    Job *head, *tail;
+    int started, stop;
 } Store;
+
+static void *store_thread(void *arg) {
+    Store *s = (Store *)arg;
+    for (;;) {
+        pthread_mutex_lock(&s->mu);
+        while (!s->head && !s->stop) pthread_cond_wait(&s->cv, &s->mu);
+        if (!s->head) { pthread_mutex_unlock(&s->mu); return NULL; }
+        Job *j = s->head;
+        s->head = j->next;
+        if (!s->head) s->tail = NULL;
+        pthread_mutex_unlock(&s->mu);
+        const size_t rb = (size_t)j->n * sizeof(hm_doc_result), cb = (size_t)j->n * j->S * 4;
+        j->buf = (uint8_t *)malloc(rb + 3 * cb + 16);
+        j->st = j->buf ? hm_batch_wait(s->store, j->id, (hm_doc_result *)j->buf, (uint32_t *)(j->buf + rb),
+                                       (uint32_t *)(j->buf + rb + cb), (uint32_t *)(j->buf + rb + 2 * cb))
+                       : HM_ERR_NOMEM;
+        if (j->st) snprintf(j->err, sizeof j->err, "hm_batch_wait: %s — %s", hm_status_message(j->st), hm_engine_last_error(s->engine));
+        napi_call_threadsafe_function(j->tsfn, j, napi_tsfn_blocking);
+        napi_release_threadsafe_function(j->tsfn, napi_tsfn_release);
+    }
+}
 
 static void store_finalize(napi_env env, void *data, void *hint) {
     (void)env; (void)hint;
     Store *s = (Store *)data;
+    if (s->started) {
+        pthread_mutex_lock(&s->mu);
+        s->stop = 1;
+        pthread_cond_signal(&s->cv);
+        pthread_mutex_unlock(&s->mu);
+        pthread_join(s->thread, NULL);
+        pthread_mutex_destroy(&s->mu);
+        pthread_cond_destroy(&s->cv);
+    }
     if (s->store) hm_store_destroy(s->store);
     if (s->engine) hm_engine_destroy(s->engine);
     free(s);
@@ -187,6 +239,104 @@ static napi_value Wait(napi_env env, napi_callback_info info) {
     set(env, o, "backClock", buf_copy(env, buf + rb + cb, cb));
     set(env, o, "heads", buf_copy(env, buf + rb + 2 * cb, cb));
     free(buf);
+    return o;
+}
+
+static napi_value result_object(napi_env env, const uint8_t *buf, uint32_t n, uint32_t S) {
+    const size_t rb = (size_t)n * sizeof(hm_doc_result), cb = (size_t)n * S * 4;
+    napi_value o;
+    napi_create_object(env, &o);
+    set(env, o, "docs", buf_copy(env, buf, rb));
+    set(env, o, "clock", buf_copy(env, buf + rb, cb));
+    set(env, o, "backClock", buf_copy(env, buf + rb + cb, cb));
+    set(env, o, "heads", buf_copy(env, buf + rb + 2 * cb, cb));
+    return o;
+}
+
+/* main thread: callback(err, result) for a finished job */
+static void job_call_js(napi_env env, napi_value cb, void *context, void *data) {
+    (void)context;
+    Job *j = (Job *)data;
+    if (env && cb) {
+        napi_value argv[2], undef, ret;
+        napi_get_undefined(env, &undef);
+        if (j->st) {
+            napi_value msg;
+            napi_create_string_utf8(env, j->err, NAPI_AUTO_LENGTH, &msg);
+            napi_create_error(env, NULL, msg, &argv[0]);
+            argv[1] = undef;
+        } else {
+            napi_get_null(env, &argv[0]);
+            argv[1] = result_object(env, j->buf, j->n, j->S);
+        }
+        napi_call_function(env, undef, cb, 2, argv, &ret);
+    }
+    free(j->buf);
+    free(j);
+}
+
+/* waitAsync(store, id, callback(err, {docs, clock, backClock, heads})): hm_batch_wait on the
+ * store's host thread; no other call on the store until the callback runs */
+static napi_value WaitAsync(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return NULL;
+    Store *s = get_store(env, argv[0]);
+    if (!s) return NULL;
+    double idd;
+    napi_get_value_double(env, argv[1], &idd);
+    Job *j = (Job *)calloc(1, sizeof(Job));
+    if (!j) { napi_throw_error(env, NULL, "out of memory"); return NULL; }
+    j->id = (uint64_t)idd; j->n = s->pending_n; j->S = s->a_stride;
+    napi_value name;
+    napi_create_string_utf8(env, "hmgpu.waitAsync", NAPI_AUTO_LENGTH, &name);
+    if (napi_create_threadsafe_function(env, argv[2], NULL, name, 0, 1, NULL, NULL, NULL, job_call_js, &j->tsfn) != napi_ok) {
+        free(j);
+        napi_throw_error(env, NULL, "napi_create_threadsafe_function failed");
+        return NULL;
+    }
+    if (!s->started) {
+        pthread_mutex_init(&s->mu, NULL);
+        pthread_cond_init(&s->cv, NULL);
+        if (pthread_create(&s->thread, NULL, store_thread, s) != 0) {
+            napi_release_threadsafe_function(j->tsfn, napi_tsfn_abort);
+            free(j);
+            napi_throw_error(env, NULL, "pthread_create failed");
+            return NULL;
+        }
+        s->started = 1;
+    }
+    pthread_mutex_lock(&s->mu);
+    if (s->tail) s->tail->next = j; else s->head = j;
+    s->tail = j;
+    pthread_cond_signal(&s->cv);
+    pthread_mutex_unlock(&s->mu);
+    return NULL;
+}
+
+/* readRegs(store, docs Uint32Array, regs Uint32Array, survCap) -> {regs, surv} (Buffers): the
+ * rows of the chosen registers, surv_off rewritten to offsets into `surv` */
+static napi_value ReadRegs(napi_env env, napi_callback_info info) {
+    napi_value argv[4];
+    if (!get_args(env, info, 4, argv)) return NULL;
+    Store *s = get_store(env, argv[0]);
+    if (!s) return NULL;
+    void *pd, *pr; size_t nd, nr;
+    if (!get_bytes(env, argv[1], &pd, &nd) || !get_bytes(env, argv[2], &pr, &nr)) return NULL;
+    if (nd != nr) { napi_throw_range_error(env, NULL, "docs and regs differ in length"); return NULL; }
+    const uint32_t n = (uint32_t)(nd / 4), cap = get_u32(env, argv[3]);
+    hm_reg_result *rr = (hm_reg_result *)malloc((size_t)n * sizeof(hm_reg_result) + 16);
+    hm_surv_result *sv = (hm_surv_result *)malloc((size_t)cap * sizeof(hm_surv_result) + 16);
+    uint32_t got = 0;
+    int st = (rr && sv) ? hm_store_read_regs(s->store, n, (const uint32_t *)pd, (const uint32_t *)pr, rr, sv, cap, &got)
+                        : HM_ERR_NOMEM;
+    napi_value o = NULL;
+    if (!st) {
+        napi_create_object(env, &o);
+        set(env, o, "regs", buf_copy(env, rr, (size_t)n * sizeof(hm_reg_result)));
+        set(env, o, "surv", buf_copy(env, sv, (size_t)got * sizeof(hm_surv_result)));
+    }
+    free(rr); free(sv);
+    if (st) return throw_status(env, s->engine, st, "hm_store_read_regs");
     return o;
 }
 
@@ -392,6 +542,7 @@ static napi_value Init(napi_env env, napi_value exports) {
         {"info", Info}, {"read", Read}, {"historyPrefix", HistoryPrefix}, {"setMinClock", SetMinClock},
         {"clockUpdate", ClockUpdate}, {"statusMessage", StatusMessage},
         {"commCreateLocal", CommCreateLocal}, {"clockExchange", ClockExchange}, {"clockMin", ClockMin},
+        {"waitAsync", WaitAsync}, {"readRegs", ReadRegs},
     };
     for (size_t i = 0; i < sizeof fns / sizeof fns[0]; i++) {
         napi_value f;

@@ -297,7 +297,8 @@ int hm_doc_open_n(hm_store *s, uint32_t n, uint32_t *out_first);
 int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
                     const uint8_t *actor_remap, uint64_t *out_batch_id);
 
-/* Wait for a submitted batch; per batch row: the merge result of the
+/* Wait for a submitted batch (from any one host thread; the store is not otherwise
+ * thread-safe: no other call on it until the wait returns); per batch row: the merge result of the
  * document's whole log, and (each optional) its opSet.clock, DocBackend.clock
  * and opSet.deps rows ([n_docs * a_stride]).  Documents whose merge threw are
  * reported with their error status and rolled back before this returns. */
@@ -327,6 +328,15 @@ int hm_doc_info(hm_store *s, uint32_t doc, hm_doc_info_t *out);
  * surv [n_ops] (first n_surv valid), clock/back_clock/heads [a_stride]. */
 int hm_doc_read(hm_store *s, uint32_t doc, int32_t *hist, uint32_t *all_deps, hm_reg_result *regs,
                 hm_surv_result *surv, uint32_t *clock, uint32_t *back_clock, uint32_t *heads);
+
+/* Chosen registers of resident documents (incremental patches: only the registers a submit's
+ * ops hit are read).  Request i = (doc_handles[i], regs[i]); out_regs[i] is that register's row
+ * with surv_off rewritten to an offset into out_surv, where its n_surv survivors are copied
+ * (request order of the survivor blocks is unspecified).  surv_cap = rows of out_surv; the
+ * survivors of a document's registers never exceed its hm_doc_result.n_surv.  *out_n_surv =
+ * rows needed; HM_ERR_NOMEM (nothing copied to out_surv) when that exceeds surv_cap. */
+int hm_store_read_regs(hm_store *s, uint32_t n, const uint32_t *doc_handles, const uint32_t *regs,
+                       hm_reg_result *out_regs, hm_surv_result *out_surv, uint32_t surv_cap, uint32_t *out_n_surv);
 
 /* The log rows of a document (debug / materialize): changes [n_changes]
  * with dep_off/op_first local to the document, deps [n_deps], ops [n_ops]. */

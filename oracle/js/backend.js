@@ -1,0 +1,266 @@
+'use strict'
+// oracle/js/backend.js — TEST / BASELINE INFRASTRUCTURE ONLY.  A from-scratch JavaScript
+// restatement of the Automerge 0.12 backend the reference drives (Backend.init /
+// Backend.applyChanges, called at src/DocBackend.ts:148,172), over plain JS Maps, plus a
+// DocBackend restatement (src/DocBackend.ts:46-213) that calls it synchronously the way the
+// reference's Queue does (push runs the subscriber, src/Queue.ts:38-57).  It is the
+// "JS restatement" CPU baseline of BASELINE.md (baseline 2): one Node thread, the same
+// DocBackend message API as the GPU drop-in.  Nothing in hypermerge_amd/ loads it.
+//
+// Rules (SURVEY.md Appendix A, the same restatement oracle/oracle.c follows; parity with
+// Automerge itself is unpinned — Automerge 0.12 is not vendored in the reference):
+//   A.1 addChange -> queue; applyQueuedOps passes until no change applies; causallyReady;
+//       duplicate (actor, seq) must have equal content; allDeps = transitiveDeps fold in deps
+//       key order then {actor: seq-1} whose set overrides the max; deps heads; clock; history.
+//   A.2 applyAssign: survivors = the concurrent prior ops, push set/link, stable
+//       sortBy(actor) then reverse after every assign; inc adds to causally prior counter sets.
+//   A.3 applyInsert / updateListElement / getPrevious / insertionsAfter (lamport order desc).
+// Actor order is JS string order, as Immutable's sortBy compares actor ids.
+
+const ROOT = '00000000-0000-0000-0000-000000000000'
+
+function canon(v) {
+  if (v === null || typeof v !== 'object') return JSON.stringify(v === 0 ? 0 : v)
+  if (Array.isArray(v)) return '[' + v.map(canon).join(',') + ']'
+  return '{' + Object.keys(v).sort().map((k) => JSON.stringify(k) + ':' + canon(v[k])).join(',') + '}'
+}
+
+class OpSet {
+  constructor() {
+    this.clock = new Map()        // actor -> seq (applied)
+    this.deps = new Map()         // heads
+    this.states = new Map()       // actor -> [{change, allDeps: Map, text}]
+    this.history = []
+    this.queue = []
+    this.objs = new Map([[ROOT, { type: 'map', keys: new Map(), following: new Map(), insertion: new Map(), elemIds: [] }]])
+  }
+}
+
+function allDepsOf(s, actor, seq) { return s.states.get(actor)[seq - 1].allDeps }
+
+function causallyReady(s, c) {
+  const deps = Object.assign({}, c.deps || {})
+  deps[c.actor] = c.seq - 1
+  for (const a of Object.keys(deps)) if ((s.clock.get(a) || 0) < deps[a]) return false
+  return true
+}
+
+// isConcurrent(opSet, op1, op2)
+function isConcurrent(s, o1, o2) {
+  const c1 = allDepsOf(s, o1.actor, o1.seq), c2 = allDepsOf(s, o2.actor, o2.seq)
+  return (c1.get(o2.actor) || 0) < o2.seq && (c2.get(o1.actor) || 0) < o1.seq
+}
+
+function transitiveDeps(s, baseDeps) {
+  let deps = new Map()
+  for (const a of Object.keys(baseDeps)) {
+    const q = baseDeps[a]
+    if (q <= 0) continue
+    const t = allDepsOf(s, a, q)
+    for (const [x, v] of t) if (v > (deps.get(x) || 0)) deps.set(x, v)
+    deps.set(a, q)
+  }
+  return deps
+}
+
+function lamportGreater(s, a, b) {             // element ops: (elem, actor) descending
+  if (a.elem !== b.elem) return a.elem > b.elem
+  return a.actor > b.actor
+}
+
+function insertionsAfter(obj, parent) {
+  const kids = (obj.following.get(parent) || []).slice()
+  kids.sort((x, y) => (lamportGreater(null, x, y) ? -1 : lamportGreater(null, y, x) ? 1 : 0))
+  return kids.map((op) => `${op.actor}:${op.elem}`)
+}
+
+function getPrevious(obj, elemId) {
+  const ins = obj.insertion.get(elemId)
+  if (!ins) throw new Error(`Missing index entry for list element ${elemId}`)
+  const parent = ins.key
+  const kids = insertionsAfter(obj, parent)
+  if (kids[0] === elemId) return parent === '_head' ? null : parent
+  let prev = null
+  for (const k of kids) { if (k === elemId) break; prev = k }
+  for (;;) {
+    const more = insertionsAfter(obj, prev)
+    if (!more.length) return prev
+    prev = more[more.length - 1]
+  }
+}
+
+function updateListElement(s, obj, elemId, diffs, objId) {
+  const ops = obj.keys.get(elemId) || []
+  let index = obj.elemIds.indexOf(elemId)
+  if (index >= 0) {
+    if (!ops.length) { obj.elemIds.splice(index, 1); diffs.push({ action: 'remove', type: obj.type, obj: objId, index }) }
+    else diffs.push({ action: 'set', type: obj.type, obj: objId, index, value: ops[0].value })
+    return
+  }
+  if (!ops.length) return
+  let prev = elemId
+  for (;;) {
+    index = -1
+    prev = getPrevious(obj, prev)
+    if (prev === null) break
+    index = obj.elemIds.indexOf(prev)
+    if (index >= 0) break
+  }
+  obj.elemIds.splice(index + 1, 0, elemId)
+  diffs.push({ action: 'insert', type: obj.type, obj: objId, index: index + 1, elemId, value: ops[0].value })
+}
+
+function applyAssign(s, op, diffs) {
+  const obj = s.objs.get(op.obj)
+  if (!obj) throw new Error(`Modification of unknown object ${op.obj}`)
+  const prior = obj.keys.get(op.key) || []
+  let remaining
+  if (op.action === 'inc') {
+    remaining = prior.map((o) => (o.action === 'set' && typeof o.value === 'number' && o.datatype === 'counter' &&
+      !isConcurrent(s, o, op)) ? Object.assign({}, o, { value: o.value + op.value }) : o)
+  } else {
+    remaining = prior.filter((o) => isConcurrent(s, o, op))
+  }
+  if (op.action === 'set' || op.action === 'link') remaining = remaining.concat([op])
+  // sortBy(op => op.actor).reverse(): stable ascending by actor, then reversed
+  remaining = remaining.map((o, i) => [o, i]).sort((x, y) => (x[0].actor < y[0].actor ? -1 : x[0].actor > y[0].actor ? 1 : x[1] - y[1]))
+    .map((x) => x[0]).reverse()
+  obj.keys.set(op.key, remaining)
+  if (obj.type === 'list' || obj.type === 'text') updateListElement(s, obj, op.key, diffs, op.obj)
+  else if (remaining.length) diffs.push({ action: 'set', type: obj.type, obj: op.obj, key: op.key, value: remaining[0].value })
+  else diffs.push({ action: 'remove', type: obj.type, obj: op.obj, key: op.key })
+}
+
+const MAKE = { makeMap: 'map', makeTable: 'table', makeList: 'list', makeText: 'text' }
+
+function applyChange(s, c, diffs) {
+  const prior = s.states.get(c.actor) || []
+  if (c.seq <= prior.length) {
+    if (prior[c.seq - 1].text !== canon(c)) throw new Error(`Inconsistent reuse of sequence number ${c.seq} by ${c.actor}`)
+    return
+  }
+  const base = Object.assign({}, c.deps || {})
+  base[c.actor] = c.seq - 1
+  const allDeps = transitiveDeps(s, base)
+  prior.push({ change: c, allDeps, text: canon(c) })
+  s.states.set(c.actor, prior)
+  for (const raw of c.ops || []) {
+    const op = Object.assign({ actor: c.actor, seq: c.seq }, raw)
+    if (MAKE[op.action]) {
+      if (s.objs.has(op.obj)) throw new Error(`Duplicate creation of object ${op.obj}`)
+      s.objs.set(op.obj, { type: MAKE[op.action], keys: new Map(), following: new Map(), insertion: new Map(), elemIds: [] })
+      diffs.push({ action: 'create', obj: op.obj, type: MAKE[op.action] })
+    } else if (op.action === 'ins') {
+      const obj = s.objs.get(op.obj)
+      if (!obj) throw new Error(`Modification of unknown object ${op.obj}`)
+      const elemId = `${op.actor}:${op.elem}`
+      if (obj.insertion.has(elemId)) throw new Error(`Duplicate list element ID ${elemId}`)
+      const f = obj.following.get(op.key) || []
+      f.push(op)
+      obj.following.set(op.key, f)
+      obj.insertion.set(elemId, op)
+    } else {
+      applyAssign(s, op, diffs)
+    }
+  }
+  for (const [a, q] of Array.from(s.deps)) if (q <= (allDeps.get(a) || 0)) s.deps.delete(a)
+  s.deps.set(c.actor, c.seq)
+  s.clock.set(c.actor, c.seq)
+  s.history.push(c)
+}
+
+function applyQueuedOps(s, diffs) {
+  for (;;) {
+    const next = []
+    let applied = false
+    for (const c of s.queue) {
+      if (causallyReady(s, c)) { applyChange(s, c, diffs); applied = true } else next.push(c)
+    }
+    s.queue = next
+    if (!applied) return
+  }
+}
+
+const Backend = {
+  init() { return new OpSet() },
+  // applyChanges(state, changes) -> [state, patch]; the state is advanced in place (the
+  // restatement's states are linear, like the GPU drop-in's)
+  applyChanges(s, changes) {
+    const diffs = []
+    for (const c of changes) { s.queue.push(c); applyQueuedOps(s, diffs) }
+    const clock = {}, deps = {}
+    for (const [a, q] of s.clock) clock[a] = q
+    for (const [a, q] of s.deps) deps[a] = q
+    return [s, { clock, deps, canUndo: false, canRedo: false, diffs }]
+  },
+}
+
+// DocBackend (src/DocBackend.ts:46-213) over the restatement, synchronous Queue semantics
+class Queue {
+  constructor() { this.buf = []; this.sub = null }
+  push(x) { if (this.sub) this.sub(x); else this.buf.push(x) }
+  subscribe(f) { this.sub = f; const b = this.buf; this.buf = []; b.forEach(f) }
+}
+
+class DocBackend {
+  constructor(documentId, notify, back) {
+    this.id = documentId
+    this.actorId = undefined
+    this.clock = {}
+    this.back = back
+    this.changes = new Map()
+    this.ready = new Queue()
+    this.notify = notify
+    this.minimumClock = undefined
+    this.minimumClockSatisfied = false
+    this.localChangeQ = new Queue()
+    this.remoteChangesQ = new Queue()
+    if (back) {
+      this.actorId = documentId
+      this.ready.subscribe((f) => f())
+      this.minimumClockSatisfied = true
+      this.subscribeToRemoteChanges()
+      this.notify({ type: 'ReadyMsg', id: this.id, minimumClockSatisfied: true, actorId: this.actorId, history: back.history.length })
+    }
+  }
+
+  applyRemoteChanges(changes) { this.remoteChangesQ.push(changes) }
+
+  updateClock(changes) {
+    for (const c of changes) this.clock[c.actor] = Math.max(this.clock[c.actor] || 0, c.seq)
+  }
+
+  init(changes, actorId) {
+    const [back, patch] = Backend.applyChanges(Backend.init(), changes)
+    this.actorId = this.actorId || actorId
+    this.back = back
+    this.updateClock(changes)
+    this.minimumClockSatisfied = changes.length > 0
+    this.ready.subscribe((f) => f())
+    this.subscribeToRemoteChanges()
+    this.notify({ type: 'ReadyMsg', id: this.id, minimumClockSatisfied: this.minimumClockSatisfied, actorId: this.actorId,
+      patch, history: back.history.length })
+  }
+
+  subscribeToRemoteChanges() {
+    this.remoteChangesQ.subscribe((changes) => {
+      const [back, patch] = Backend.applyChanges(this.back, changes)
+      this.back = back
+      this.updateClock(changes)
+      this.notify({ type: 'RemotePatchMsg', id: this.id, minimumClockSatisfied: this.minimumClockSatisfied, patch,
+        history: back.history.length })
+    })
+  }
+}
+
+// the merged document as plain JS (maps by key, lists in element order; conflicts dropped)
+function materialize(s, objId) {
+  const obj = s.objs.get(objId || ROOT)
+  const val = (ops) => (ops[0].action === 'link' ? materialize(s, ops[0].value) : ops[0].value)
+  if (obj.type === 'list' || obj.type === 'text') return obj.elemIds.map((e) => val(obj.keys.get(e)))
+  const out = {}
+  for (const [k, ops] of obj.keys) if (ops.length) out[k] = val(ops)
+  return out
+}
+
+module.exports = { Backend, DocBackend, materialize, ROOT }

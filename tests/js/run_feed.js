@@ -8,7 +8,7 @@ const path = require('path')
 const { GpuEngine, DocBackend, ClockStore } = require(path.join(__dirname, '..', '..', 'hypermerge_amd', 'js', 'GpuDocBackend.js'))
 
 const input = JSON.parse(require('fs').readFileSync(0, 'utf8'))
-const engine = new GpuEngine({ mode: 'batched', aStride: 8 })
+const engine = new GpuEngine({ mode: input.mode || 'batched', aStride: 8 })
 const tick = () => new Promise((r) => setImmediate(r))
 
 ;(async () => {
@@ -30,7 +30,8 @@ const tick = () => new Promise((r) => setImmediate(r))
       if (r === 0) x.d.init(x.chunks[0], 'local')
       else if (x.chunks[r].length) x.d.applyRemoteChanges(x.chunks[r])
     }
-    await tick(); await tick()
+    if (engine.mode === 'async') await engine.idle()
+    else { await tick(); await tick() }
     const sat = docs.filter((x) => x.d.back && x.d.minimumClockSatisfied).map((x) => x.d)
     const g = gpuStore.updateDocs('self', sat)
     sat.forEach((d, i) => {

@@ -41,7 +41,7 @@ function render(objects, uuid, depth) {
 }
 
 const input = JSON.parse(require('fs').readFileSync(0, 'utf8'))
-const engine = new GpuEngine({ mode: 'batched', aStride: 8 })
+const engine = new GpuEngine({ mode: input.mode || 'batched', aStride: 8 })
 const tick = () => new Promise((r) => setImmediate(r))
 ;(async () => {
   const docs = input.docs.map((chunks, i) => {
@@ -55,7 +55,8 @@ const tick = () => new Promise((r) => setImmediate(r))
       if (r === 0) x.d.init(x.chunks[0], 'local')
       else if (x.chunks[r].length) x.d.applyRemoteChanges(x.chunks[r])
     }
-    await tick(); await tick()
+    if (engine.mode === 'async') await engine.idle()
+    else { await tick(); await tick() }
   }
   const out = docs.map((x) => {
     const objects = new Map([[ROOT, { type: 'map', keys: new Map(), elems: [] }]])
@@ -63,7 +64,8 @@ const tick = () => new Promise((r) => setImmediate(r))
     const remote = x.msgs.filter((m) => m.type === 'RemotePatchMsg')
     let nDiffs = 0
     for (const m of ready.concat(remote)) { applyDiffs(objects, m.patch.diffs); nDiffs += m.patch.diffs.length }
-    return { state: render(objects, ROOT, 0), nDiffs, nonEmpty: x.msgs.filter((m) => m.patch && m.patch.diffs.length > 0).length }
+    return { state: render(objects, ROOT, 0), nDiffs, nonEmpty: x.msgs.filter((m) => m.patch && m.patch.diffs.length > 0).length,
+      incremental: x.d.back.incrementalPatches || 0 }
   })
   process.stdout.write(JSON.stringify({ docs: out }) + '\n')
 })().catch((e) => { console.error(e); process.exit(1) })

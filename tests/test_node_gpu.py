@@ -35,9 +35,11 @@ def test_docbackend_traces_match_reference(mode):
         assert _strip(got[name]) == _strip(sc["trace"]), name
 
 
-def test_batched_feed_matches_oracle():
-    """Many documents through GpuDocBackend (batched mode): init + 3 remote calls each;
-    history order, opSet clock/deps and DocBackend.clock equal the oracle's cold merge."""
+@pytest.mark.parametrize("mode", ["batched", "async"])
+def test_batched_feed_matches_oracle(mode):
+    """Many documents through GpuDocBackend (batched mode, and async mode: hm_batch_wait on the
+    store's host thread, completion through a napi_threadsafe_function): init + 3 remote calls
+    each; history order, opSet clock/deps and DocBackend.clock equal the oracle's cold merge."""
     import numpy as np
     from hypermerge_amd import synth
     from hypermerge_amd.columnar import decode_doc, encode
@@ -50,7 +52,7 @@ def test_batched_feed_matches_oracle():
     for chs in docs:
         cuts = sorted(rng.integers(1, len(chs) + 1, size=3))
         chunked.append([chs[:cuts[0]], chs[cuts[0]:cuts[1]], chs[cuts[1]:cuts[2]], chs[cuts[2]:]])
-    p = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "run_feed.js")], input=json.dumps({"docs": chunked}),
+    p = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "run_feed.js")], input=json.dumps({"docs": chunked, "mode": mode}),
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr
     got = json.loads(p.stdout)
@@ -68,8 +70,9 @@ def test_batched_feed_matches_oracle():
         assert g["types"][-1] in ("RemotePatchMsg", "ReadyMsg")
 
 
-@pytest.mark.parametrize("name,n", [("C5", 200), ("C3", 12), ("C2", 100)])
-def test_patch_diffs_rebuild_the_merged_document(name, n):
+@pytest.mark.parametrize("name,n,mode", [("C5", 200, "batched"), ("C3", 12, "batched"), ("C2", 100, "batched"),
+                                         ("C5", 200, "async"), ("C4", 300, "async")])
+def test_patch_diffs_rebuild_the_merged_document(name, n, mode):
     """Applying every patch's diffs in order (a restatement of Frontend.applyPatch's effect,
     src/DocFrontend.ts:162-179) rebuilds exactly the canonical merged document of the oracle's
     cold merge of the same changes — maps, conflicts, counters, links, lists and text."""
@@ -86,7 +89,8 @@ def test_patch_diffs_rebuild_the_merged_document(name, n):
     for chs in docs:
         cuts = sorted(rng.integers(1, len(chs) + 1, size=3))
         chunked.append([chs[:cuts[0]], chs[cuts[0]:cuts[1]], chs[cuts[1]:cuts[2]], chs[cuts[2]:]])
-    p = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "run_patches.js")], input=json.dumps({"docs": chunked}),
+    p = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "run_patches.js")],
+                       input=json.dumps({"docs": chunked, "mode": mode}),
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr
     got = json.loads(p.stdout)["docs"]
@@ -97,6 +101,8 @@ def test_patch_diffs_rebuild_the_merged_document(name, n):
         assert s["status"] == "OK"
         assert g["state"] == json.loads(json.dumps(s["state"])), i
         assert g["nDiffs"] > 0 and g["nonEmpty"] > 0
+    if name in ("C2", "C4", "C5"):                 # rounds whose changes all applied patch incrementally
+        assert sum(g["incremental"] for g in got) > 0
 
 
 def test_materialize_history_prefix():

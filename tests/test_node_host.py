@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 from hypermerge_amd import synth
-from hypermerge_amd.columnar import decode_doc
+from hypermerge_amd.columnar import ROOT_ID, decode_doc
 from hypermerge_amd.store import DocEncoder, StringPool
 from kat_cases import CASES
 
@@ -92,3 +92,36 @@ def test_block_unpack_raw_and_brotli():
     got = json.loads(p.stdout)
     assert got["same"] and got["rowsSame"] and got["n"] == len(changes)
     assert got["err"] == "fail to unpack blocks - head is 'xx'"
+
+
+def test_js_encoder_snapshot_restore():
+    """DocEncoder.snapshot/restore (the rollback of a throwing applyChanges): after restoring,
+    re-encoding the same changes gives the same rows, ids and content classes as the first time,
+    including a new actor that re-ranks, new objects/registers and a repeated (actor, seq)."""
+    script = r"""
+const C = require(process.argv[1] + '/hypermerge_amd/js/columnar.js')
+const R = '00000000-0000-0000-0000-000000000000'
+const ch = (actor, seq, deps, ops) => ({ actor, seq, deps, ops })
+const e = new C.DocEncoder(new C.StringPool())
+e.encode([ch('mm', 1, {}, [{ action: 'set', obj: R, key: 'x', value: 1 }])])
+const B = [ch('aa', 1, {}, [{ action: 'makeMap', obj: 'o1' }, { action: 'link', obj: R, key: 'm', value: 'o1' }]),
+           ch('mm', 1, {}, [{ action: 'set', obj: R, key: 'x', value: 2 }]),
+           ch('mm', 1, {}, [{ action: 'set', obj: R, key: 'x', value: 1 }])]
+const snap = e.snapshot()
+const first = e.encode(B)
+const t1 = JSON.stringify([e.actors, e.objList, e.regList, e.nContent])
+e.restore(snap)
+const t0 = JSON.stringify([e.actors, e.objList, e.regList, e.nContent])
+const again = e.encode(B)
+const t2 = JSON.stringify([e.actors, e.objList, e.regList, e.nContent])
+const hex = (a) => [a.changes, a.deps, a.ops].map((b) => b.toString('hex')).join('|')
+console.log(JSON.stringify({ same: hex(first) === hex(again), t0, t1, t2, remap: Array.from(first.remap || []),
+  cids: [0, 1, 2].map((i) => first.changes.readUInt32LE(i * 24 + 20)) }))
+"""
+    p = subprocess.run([NODE, "-e", script, ROOT], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stderr
+    got = json.loads(p.stdout)
+    assert got["same"] and got["t1"] == got["t2"]
+    assert json.loads(got["t0"]) == [["mm"], [ROOT_ID], [[0, "x"]], 1]
+    assert got["remap"] == [1]
+    assert got["cids"] == [1, 2, 0]          # aa:1 new, mm:1 with new content new, mm:1 as before = class 0
