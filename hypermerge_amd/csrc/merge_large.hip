@@ -38,6 +38,17 @@
 #endif
 typedef unsigned long long u64;
 
+#ifndef HM_PAR_HIST
+#define HM_PAR_HIST 1   // 0: queued documents always take the serial queue emulation (dev A/B builds)
+#endif
+#ifndef HM_PAR_HIST_INLINE
+#define HM_PAR_HIST_INLINE 1
+#endif
+#if HM_PAR_HIST_INLINE
+#define PH_ATTR
+#else
+#define PH_ATTR __noinline__
+#endif
 #ifndef HM_STAMPS
 #define HM_STAMPS 0     // diagnostic builds only: per-phase s_memtime shares (tools/lstamps.py); never timed
 #endif
@@ -76,7 +87,7 @@ __device__ __forceinline__ u64 err_key(uint32_t h, uint32_t op_plus1, uint32_t a
 struct Shared {
     uint32_t base[LA_MAX], maxs[LA_MAX], tabo[LA_MAX + 1], clock[LA_MAX], bclock[LA_MAX], headv[LA_MAX];
     uint32_t maxad[LA_MAX];
-    uint32_t flags, all_ok, H, nins, nl, total, lists, grew, nmake;
+    uint32_t flags, all_ok, H, nins, nl, total, lists, grew, nmake, nodup;
     u64 errkey;
     uint32_t scan[LWG / 64 + 1];
     u64 scratch_base;
@@ -130,6 +141,7 @@ struct Scratch {
     GLB u64 *opkey, *insmin, *objslot, *seglist, *nodekey, *survabs;
     GLB int64_t *survsum;
     GLB uint32_t *vc;                   // [n * A] closure rows (L2 pointer jumping, second buffer)
+    GLB uint32_t *hx;                   // parallel history (L1): [ht n][hp n][hnev n][hfill n][hmem n][hoff n+1][pm T]
 };
 
 __host__ __device__ inline size_t large_carve(uintptr_t base, uint32_t n, uint32_t m, uint32_t R, uint32_t O,
@@ -148,6 +160,7 @@ __host__ __device__ inline size_t large_carve(uintptr_t base, uint32_t n, uint32
     TK(fc, uint32_t, NP); TK(ns, uint32_t, m); TK(tour0, uint32_t, NE); TK(tour1, uint32_t, NE);
     TK(tval0, uint32_t, NE); TK(tval1, uint32_t, NE);
     TK(listbase, uint32_t, O + 1); TK(pos, uint32_t, m); TK(vis, uint32_t, m);
+    TK(hx, uint32_t, 6 * (size_t)n + 1 + T);
 #undef TK
     return o;
 }
@@ -157,6 +170,194 @@ enum Outcome { LOK = 0, LERR = 1, LUNSUP = 2 };
 // allDeps row of the applied change at arrival index ci (global, written in history order)
 __device__ __forceinline__ uint32_t *ad_row(const SmallParams &p, const hm_doc_row &doc, uint32_t ci) {
     return p.res_all_deps + ((size_t)doc.change_off + ci) * p.a_stride;
+}
+
+// exclusive max-scan of v over the block (identity 0): the max over lower-numbered threads
+__device__ __forceinline__ uint32_t block_excl_max(Shared &sh, uint32_t v) {
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane >= (uint32_t)o ? lane - o : lane) << 2), (int)x);
+        if (lane >= (uint32_t)o) x = x > y ? x : y;
+    }
+    const uint32_t ex = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane ? lane - 1 : 0) << 2), (int)x);
+    if (lane == 63) sh.scan[w] = x;
+    bsync();
+    uint32_t off = 0;
+    for (uint32_t i = 0; i < LWG / 64; i++) if (i < w) off = off > sh.scan[i] ? off : sh.scan[i];
+    bsync();
+    const uint32_t e = lane ? ex : 0u;
+    return off > e ? off : e;
+}
+
+// ---- L1 parallel: the exact queue-pass history without the serial emulation ----
+// (documents without duplicate changes; the rest take the serial emulation)
+// The arrival whose processing applies change K is t(K) = the latest arrival among K and its
+// ancestors (ancestors = per actor a chain prefix up to the closure clock C(K)[a], so
+// t(K) = max(arr(K), max_a PM_a[C(K)[a]]) with PM_a the prefix max of arrival index along
+// actor a's seqs; never for a missing ancestor or a dependency cycle).  K applies in pass 1
+// of that processing if t(K) = arr(K), else in pass max(2, pass(D) + [arr(D) > arr(K)]) over
+// its direct deps D applied in the same processing (a pass walks the queue, which is arrival
+// order, applying what is ready).  History = applied changes ordered by (t, pass, arr).
+// C(K) comes from pointer jumping over the actor chains (log-depth rounds).  Returns false
+// (block-uniform) when the serial emulation must run instead.
+__device__ PH_ATTR bool parallel_history(const SmallParams &p, Shared &sh, const hm_doc_row &doc, const Scratch &X,
+                                 uint32_t n, uint32_t A, uint32_t T) {
+    const uint32_t tid = threadIdx.x;
+    const hm_change_row *CH = p.changes + doc.change_off;
+    const uint32_t INF = 0xFFFFFFFFu;
+    GLB uint32_t *C = X.vc;                                   // [n * A] closure clocks (self excluded)
+    // this phase's arrays, from one base (fewer live pointers in the kernel)
+    struct { GLB uint32_t *ht, *hp, *hnev, *hfill, *hmem, *hoff, *pm, *tab, *h2a; GLB int32_t *hist; } Y;
+    Y.ht = X.hx; Y.hp = Y.ht + n; Y.hnev = Y.hp + n; Y.hfill = Y.hnev + n; Y.hmem = Y.hfill + n; Y.hoff = Y.hmem + n;
+    Y.pm = Y.hoff + n + 1; Y.tab = X.tab; Y.h2a = X.h2a; Y.hist = X.hist;
+    auto arrival = [&](uint32_t a, uint32_t s) -> uint32_t {  // first arrival of (a, s), or INF
+        if (a >= A || s < sh.base[a] || s > sh.maxs[a] || sh.maxs[a] == 0) return INF;
+        return Y.tab[sh.tabo[a] + (s - sh.base[a])];
+    };
+    if (tid == 0) sh.nodup = 1;
+    bsync();
+    for (uint32_t i = tid; i < n; i += LWG) {
+        const hm_change_row c = CH[i];
+        if (arrival(c.actor, c.seq) != i) sh.nodup = 0;        // a duplicate (actor, seq)
+        GLB uint32_t *row = C + (size_t)i * A;
+        for (uint32_t a = 0; a < A; a++) row[a] = 0;
+        uint32_t nev = c.seq > 1 && arrival(c.actor, c.seq - 1) == INF;
+        row[c.actor] = c.seq - 1;
+        for (uint32_t j = 0; j < c.n_deps; j++) {
+            const hm_dep_row dp = p.deps[c.dep_off + j];
+            if (dp.actor == c.actor || dp.seq == 0) continue;
+            if (arrival(dp.actor, dp.seq) == INF) nev = 1;
+            if (row[dp.actor] < dp.seq) row[dp.actor] = dp.seq;
+        }
+        Y.hnev[i] = nev;
+    }
+    bsync();
+    if (!sh.nodup) return false;
+    // closure by pointer jumping, in place (entries are valid lower bounds throughout)
+    for (uint32_t round = 0;; round++) {
+        if (round > 64) return false;
+        if (tid == 0) sh.grew = 0;
+        bsync();
+        bool grew = false;
+        for (uint32_t i = tid; i < n; i += LWG) {
+            GLB uint32_t *row = C + (size_t)i * A;
+            uint32_t nev = Y.hnev[i];
+            for (uint32_t a = 0; a < A; a++) {
+                const uint32_t s = row[a];
+                if (!s) continue;
+                const uint32_t j = arrival(a, s);
+                if (j >= n) { if (!nev) { nev = 1; grew = true; } continue; }
+                if (j == i) continue;
+                const GLB uint32_t *r2 = C + (size_t)j * A;
+                for (uint32_t b = 0; b < A; b++) { const uint32_t x = r2[b]; if (x > row[b]) { row[b] = x; grew = true; } }
+                if (Y.hnev[j] && !nev) { nev = 1; grew = true; }
+            }
+            Y.hnev[i] = nev;
+        }
+        if (grew) sh.grew = 1;
+        bsync();
+        const bool any = sh.grew != 0;
+        bsync();
+        if (!any) break;
+    }
+    // PM_a: prefix max of the first-arrival index along each actor's seqs; INF for a missing
+    // change and for one that can never apply (a missing ancestor, or on a dependency cycle),
+    // so every descendant of those gets t = INF too
+    for (uint32_t i = tid; i < T; i += LWG) Y.pm[i] = Y.tab[i];
+    bsync();
+    for (uint32_t i = tid; i < n; i += LWG) {
+        const hm_change_row c = CH[i];
+        if (Y.hnev[i] || C[(size_t)i * A + c.actor] >= c.seq) Y.pm[sh.tabo[c.actor] + (c.seq - sh.base[c.actor])] = INF;
+    }
+    bsync();
+    for (uint32_t a = 0; a < A; a++) {
+        const uint32_t lo = sh.tabo[a], hi = sh.tabo[a + 1];
+        if (hi == lo) continue;
+        const uint32_t N = hi - lo, per = (N + LWG - 1) / LWG;
+        const uint32_t b0 = lo + (tid * per < N ? tid * per : N), b1 = b0 + per < hi ? b0 + per : hi;
+        uint32_t run = sh.base[a] > 1 ? INF : 0u;              // seqs below the batch's first: missing
+        for (uint32_t i = b0; i < b1; i++) run = run > Y.pm[i] ? run : Y.pm[i];
+        uint32_t cur = block_excl_max(sh, run);
+        if (sh.base[a] > 1) cur = INF;
+        for (uint32_t i = b0; i < b1; i++) { cur = cur > Y.pm[i] ? cur : Y.pm[i]; Y.pm[i] = cur; }
+        bsync();
+    }
+    // t(K); pass 1 for K applied by its own arrival, else at least 2
+    for (uint32_t i = tid; i < n; i += LWG) {
+        const hm_change_row c = CH[i];
+        const GLB uint32_t *row = C + (size_t)i * A;
+        uint32_t t = (Y.hnev[i] || row[c.actor] >= c.seq) ? INF : i;    // missing ancestor / cycle
+        for (uint32_t a = 0; a < A && t != INF; a++) {
+            const uint32_t s = row[a];
+            if (!s) continue;
+            const uint32_t v = (s < sh.base[a] || s > sh.maxs[a]) ? INF : Y.pm[sh.tabo[a] + (s - sh.base[a])];
+            t = t > v ? t : v;
+        }
+        Y.ht[i] = t;
+        Y.hp[i] = t == INF ? 0u : (t == i ? 1u : 2u);
+    }
+    bsync();
+    for (uint32_t round = 0;; round++) {
+        if (round > 256) return false;
+        if (tid == 0) sh.grew = 0;
+        bsync();
+        bool grew = false;
+        for (uint32_t i = tid; i < n; i += LWG) {
+            const uint32_t t = Y.ht[i];
+            if (t == INF || t == i) continue;
+            const hm_change_row c = CH[i];
+            uint32_t ps = Y.hp[i];
+            auto dep = [&](uint32_t j) {
+                if (j < n && Y.ht[j] == t) { const uint32_t v = Y.hp[j] + (j > i ? 1u : 0u); ps = ps > v ? ps : v; }
+            };
+            for (uint32_t j = 0; j < c.n_deps; j++) {
+                const hm_dep_row dp = p.deps[c.dep_off + j];
+                if (dp.actor == c.actor || dp.seq == 0) continue;
+                dep(arrival(dp.actor, dp.seq));
+            }
+            if (c.seq > 1) dep(arrival(c.actor, c.seq - 1));
+            if (ps > Y.hp[i]) { Y.hp[i] = ps; grew = true; }
+        }
+        if (grew) sh.grew = 1;
+        bsync();
+        const bool any = sh.grew != 0;
+        bsync();
+        if (!any) break;
+    }
+    // history: bucket by t (counting sort), then (pass, arrival) within a bucket
+    for (uint32_t i = tid; i <= n; i += LWG) { Y.hoff[i] = 0; if (i < n) Y.hfill[i] = 0; }
+    bsync();
+    for (uint32_t i = tid; i < n; i += LWG) if (Y.ht[i] != INF) g_add(&Y.hoff[Y.ht[i]], 1u);
+    bsync();
+    uint32_t Hn;
+    scan_array(sh, Y.hoff, n + 1, &Hn);
+    for (uint32_t i = tid; i < n; i += LWG) {
+        const uint32_t t = Y.ht[i];
+        if (t == INF) continue;
+        const uint32_t at = g_add(&Y.hfill[t], 1u);
+        Y.hmem[Y.hoff[t] + at] = i;
+    }
+    if (tid == 0) sh.grew = 0;
+    bsync();
+    for (uint32_t i = tid; i < n; i += LWG) {
+        const uint32_t t = Y.ht[i];
+        if (t == INF) { Y.hist[i] = -1; continue; }
+        const uint32_t lo = Y.hoff[t], sz = Y.hoff[t + 1] - lo, ps = Y.hp[i];
+        if (sz > 2048) { sh.grew = 1; continue; }             // a huge batch of queued changes: serial path
+        uint32_t rank = 0;
+        for (uint32_t k = 0; k < sz; k++) {
+            const uint32_t o = Y.hmem[lo + k], po = Y.hp[o];
+            rank += (po < ps || (po == ps && o < i)) ? 1u : 0u;
+        }
+        Y.hist[i] = (int32_t)(lo + rank);
+        Y.h2a[lo + rank] = i;
+    }
+    bsync();
+    if (sh.grew) return false;
+    if (tid == 0) sh.H = Hn;
+    bsync();
+    return true;
 }
 
 __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_t *ar, const hm_doc_row &doc, uint32_t d,
@@ -243,7 +444,11 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
     }
     bsync();
     if (sh.flags) return LUNSUP;
-    if (sh.all_ok) {
+    // read before the barrier: parallel_history reuses sh.all_ok, and a wave still reading it
+    // here must not see that write (every thread takes the same branch)
+    const bool all_ready = sh.all_ok != 0;
+    bsync();
+    if (all_ready) {
         // history = arrival order minus duplicates (block scan of non-duplicate flags)
         uint32_t carry = 0;
         for (uint32_t c0 = 0; c0 < n; c0 += LWG) {
@@ -257,6 +462,8 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
         }
         if (tid == 0) sh.H = carry;
         (void)ndup_local;
+    } else if (HM_PAR_HIST && parallel_history(p, sh, doc, X, n, A, T)) {
+        // history from (t, pass, arrival) without the serial queue emulation
     } else if (wave == 0) {
         // ---- exact emulation of addChange / applyQueuedOps; wave 0, wave-uniform control ----
         // hist: -3 not arrived, -1 queued, -2 duplicate (no-op), >= 0 history position

@@ -75,6 +75,11 @@ def test_synthetic_parity(engine, name, n, extra):
     ("C3", 40, {"actors": 12}),                            # > 8 actors: closure rows double-buffered in LDS
     ("C3", 4, {"changes_per_actor": 6000}),                # tour and L3 inputs too big for LDS, closure in LDS
     ("C3", 2, {"changes_per_actor": 12000}),               # closure rows too big for LDS as well
+    # queued changes in long documents: the parallel (t, pass, arrival) history
+    ("C1", 1, {"arrival": 1}),                             # loadDocument actor-major: 5k arrivals unblock 1-2 each
+    ("C1", 1, {"arrival": 2, "shuffle_pct": 30}),
+    ("C3", 40, {"arrival": 1}),
+    ("C3", 40, {"arrival": 2, "shuffle_pct": 60, "dup_pct": 0}),
 ])
 def test_large_documents(engine, name, n, extra):
     b = synth.generate(synth.config(name, n_docs=n, **extra))
@@ -84,6 +89,8 @@ def test_large_documents(engine, name, n, extra):
 @pytest.mark.parametrize("name,n,extra", [
     ("C4", 3000, {}), ("C2", 3000, {}), ("C5", 2000, {}), ("C4", 1000, {"arrival": 1}),
     ("C2", 1000, {"arrival": 2, "shuffle_pct": 25, "dup_pct": 5}),
+    ("C2", 1000, {"arrival": 2, "shuffle_pct": 60, "dup_pct": 0}),
+    ("C5", 1000, {"arrival": 1, "dup_pct": 0}),
 ])
 def test_general_kernel_on_small_docs(engine_general, name, n, extra):
     """The general kernel alone must agree too (it is the path for long documents)."""

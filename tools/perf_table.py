@@ -11,7 +11,8 @@ R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # config, docs per GPU, CPU sample docs, parity-check docs, timed steps
 RUNS = [("C1", 1, 1, 1, 3), ("C2", 100_000, 20_000, 5_000, 10), ("C3", 10_000, 100, 100, 3),
         ("C4", 1_000_000, 200_000, 20_000, 20), ("C5", 100_000, 20_000, 5_000, 10),
-        ("C4am", 1_000_000, 100_000, 10_000, 10)]      # C4 in loadDocument's actor-major order
+        ("C4am", 1_000_000, 100_000, 10_000, 10),       # C4 in loadDocument's actor-major order
+        ("C1am", 1, 1, 1, 3)]                           # C1 in loadDocument's actor-major order
 
 
 def main() -> int:
@@ -23,6 +24,8 @@ def main() -> int:
         extra = ["--arrival", "1"] if cfg.endswith("am") else []
         cmd = [sys.executable, os.path.join(R, "bench.py"), "--config", cfg[:2], "--docs", str(docs), "--steps", str(steps),
                "--warmup", "2", "--cpu-sample-docs", str(cpu_docs), "--check-docs", str(check), "--no-traffic"] + extra
+        if cfg != "C2":
+            cmd.append("--no-node")                     # the Node leg runs its own C2 sample
         p = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
         lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
         if p.returncode or not lines:
