@@ -359,6 +359,41 @@ int hm_doc_set_min_clock(hm_store *s, uint32_t doc, const uint32_t *clock);
 int hm_store_clock_update(hm_store *s, uint32_t n, const uint32_t *docs, uint8_t *out_written,
                           uint8_t *out_differs, uint32_t *out_stored);
 
+/* ------------------------------------------------------------------ */
+/* CursorStore (src/CursorStore.ts:19-79) on the device                 */
+/* ------------------------------------------------------------------ */
+/* One repo's Cursors table (schema src/migrations/0001_initial_schema.sql:15-21): per
+ * document row (dense indices the caller assigns), up to max_actors_per_doc entries of
+ * (actor key, seq); actor key = FNV-1a64 of the actor id (as hm_clock_rec), seq stored
+ * boundedSeq-clamped to [0, INFINITY_SEQ = 2^53 - 1].  Entries keep insertion order.
+ * It gates syncChanges (src/RepoBackend.ts:506-531): docsWithActor picks the documents of
+ * a synced actor and entry bounds each one's range; every call here is a batch. */
+typedef struct hm_cursors hm_cursors;
+int  hm_cursors_create(hm_engine *e, uint32_t max_actors_per_doc, hm_cursors **out);
+void hm_cursors_destroy(hm_cursors *c);
+/* rows 0 .. n_rows-1 exist (new rows empty) */
+int  hm_cursors_reserve(hm_cursors *c, uint32_t n_rows);
+/* CursorStore.update(repoId, docId, cursor) for n_docs documents (src/CursorStore.ts:51-64):
+ * document d's entries are [entry_off[d], entry_off[d+1]) of actor_keys / seqs (distinct
+ * actors per document; seqs as JS numbers, Infinity allowed); each is an upsert-max
+ * (ON CONFLICT DO UPDATE ... WHERE excluded.seq > seq).  out_differs[d] (optional) = 1 if
+ * !Clock.equal(cursor, stored cursor after the update), i.e. updateQ is pushed.
+ * HM_ERR_INVALID if a row outgrows max_actors_per_doc. */
+int  hm_cursors_update(hm_cursors *c, uint32_t n_docs, const uint32_t *rows, const uint32_t *entry_off,
+                       const uint64_t *actor_keys, const double *seqs, uint8_t *out_differs);
+/* CursorStore.get for n rows: out_count[i] entries in out_actor/out_seq [i * max_actors_per_doc ...] */
+int  hm_cursors_get(hm_cursors *c, uint32_t n, const uint32_t *rows, uint32_t *out_count, uint64_t *out_actor,
+                    uint64_t *out_seq);
+/* CursorStore.entry (src/CursorStore.ts:68-70) for n (row, actor) pairs: stored seq or 0 */
+int  hm_cursors_entry(hm_cursors *c, uint32_t n, const uint32_t *rows, const uint64_t *actor_keys, uint64_t *out_seq);
+/* CursorStore.docsWithActor(repoId, actor, seq) (src/CursorStore.ts:73-75) for n_actors
+ * actors at once: every stored entry of one of the actors with seq >= boundedSeq(min_seqs[q])
+ * (min_seqs may be NULL = 0) -> (row, query index q, stored seq); order unspecified.
+ * *out_n = matches; HM_ERR_NOMEM (nothing copied) when that exceeds cap. */
+int  hm_cursors_docs_with_actors(hm_cursors *c, uint32_t n_actors, const uint64_t *actor_keys, const double *min_seqs,
+                                 uint32_t cap, uint32_t *out_row, uint32_t *out_actor, uint64_t *out_seq,
+                                 uint32_t *out_n);
+
 /* syncChanges contiguity (src/RepoBackend.ts:513-522) over many (doc, actor)
  * pairs on the device: for pair i, walk seq indices j = lo[i] .. hi[i]-1 while
  * bit j of the actor feed's present bitmap (words from present + word_off[i])
