@@ -27,6 +27,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 #include "../../include/hypermerge_amd.h"
 #include "engine_internal.h"
@@ -78,10 +79,16 @@ struct hm_store {
     bool pending = false;
     uint64_t next_id = 1, pending_id = 0;
     std::vector<uint32_t> p_handles;              // batch rows -> handles
-    std::vector<DocMeta> p_old;                   // metas before the append (rollback)
+    struct OldMeta { uint32_t n_c, n_d, n_o, n_r, n_objs; uint16_t n_actors, flags; };
+    std::vector<OldMeta> p_old;                   // log sizes before the append (rollback)
     std::vector<int32_t> p_inv_row;               // batch row -> offset of its inverse remap in p_inv (-1 = none)
     std::vector<uint8_t> p_inv;                   // inverse remap rows [S]
     uint8_t *p_gather_dev = nullptr;
+    // per-submit host scratch kept between submits (a 1M-document submit would otherwise
+    // allocate and first-touch ~130 MB every round)
+    std::vector<AppendDesc> descs;
+    std::vector<uint32_t> grow;
+    std::vector<uint8_t> bail;
     // incremental applyRemoteChanges (inc_apply_kernel) and the last submit's routing
     bool incremental = true;
     uint32_t st_inc = 0, st_cold = 0, st_bail = 0;
@@ -155,6 +162,20 @@ struct PhaseTimer {
         t = now;
     }
 };
+
+// f(lo, hi, t) over [0, n) split in contiguous ranges; host threads for big submits only
+// (the box's CPU share is 16 threads)
+template <typename F> uint32_t par_for(uint32_t n, F &&f) {
+    const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
+    const uint32_t T = n >= 65536 ? std::min<uint32_t>(16, hw) : 1;
+    if (T == 1) { f(0u, n, 0u); return 1; }
+    std::vector<std::thread> th;
+    th.reserve(T);
+    for (uint32_t t = 0; t < T; t++)
+        th.emplace_back([&f, n, t, T] { f((uint32_t)((uint64_t)n * t / T), (uint32_t)((uint64_t)n * (t + 1) / T), t); });
+    for (auto &x : th) x.join();
+    return T;
+}
 
 struct Plan {
     std::vector<AppendDesc> descs;      // documents touched by the append kernel
@@ -370,115 +391,173 @@ int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
         SCHK(s, hipSetDevice(hm_engine_device(s->e)));
         hipStream_t st = hm_engine_stream(s->e);
         PhaseTimer T(st);
-        // validate rows
+        // validate rows (threads over documents; the first error wins)
         std::vector<uint8_t> seen(s->docs.size(), 0);
-        for (uint32_t i = 0; i < n; i++) {
-            const uint32_t h = doc_handles[i];
-            if (h >= s->docs.size() || seen[h]) return hm_engine_fail(s->e, HM_ERR_INVALID, "bad or repeated document handle");
-            seen[h] = 1;
-            const hm_doc_row &r = b->docs[i];
-            const DocMeta &m = s->docs[h];
-            if ((uint64_t)r.change_off + r.n_changes > b->n_changes || (uint64_t)r.dep_off + r.n_deps > b->n_deps ||
-                (uint64_t)r.op_off + r.n_ops > b->n_ops)
-                return hm_engine_fail(s->e, HM_ERR_INVALID, "document rows outside the batch tables");
-            if (r.n_actors > S || r.n_actors < m.n_actors || r.n_regs < m.n_r || r.n_objs < m.n_objs || r.n_objs == 0)
-                return hm_engine_fail(s->e, HM_ERR_INVALID, "document totals must cover the existing log (and n_actors <= a_stride)");
-            // every change row must lie inside its document's slice of the batch tables
-            for (uint32_t c = r.change_off; c < r.change_off + r.n_changes; c++) {
-                const hm_change_row &cr = b->changes[c];
-                if ((uint64_t)cr.dep_off < r.dep_off || (uint64_t)cr.dep_off + cr.n_deps > (uint64_t)r.dep_off + r.n_deps ||
-                    (uint64_t)cr.op_first < r.op_off || (uint64_t)cr.op_first + cr.n_ops > (uint64_t)r.op_off + r.n_ops)
-                    return hm_engine_fail(s->e, HM_ERR_INVALID, "change rows outside their document's deps/ops");
-            }
-            // the actor re-rank of the existing rows: a permutation into the new ranks.  Checked
-            // here, before any document meta or arena pointer moves (a failure leaves the store as it was)
-            if (actor_remap) {
-                const uint8_t *mp = actor_remap + (size_t)i * S;
-                uint64_t used = 0;
-                for (uint32_t a = 0; a < m.n_actors; a++) {
-                    if (mp[a] >= r.n_actors || ((used >> mp[a]) & 1))
-                        return hm_engine_fail(s->e, HM_ERR_INVALID, "actor remap is not a permutation into the new ranks");
-                    used |= 1ull << mp[a];
+        const char *bad = nullptr;
+        auto fail_with = [&](const char *m) { const char *expect = nullptr; __atomic_compare_exchange_n(&bad, &expect, m, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED); };
+        par_for(n, [&](uint32_t lo, uint32_t hi, uint32_t) {
+            for (uint32_t i = lo; i < hi; i++) {
+                const uint32_t h = doc_handles[i];
+                if (h >= s->docs.size() || __atomic_exchange_n(&seen[h], (uint8_t)1, __ATOMIC_RELAXED)) {
+                    fail_with("bad or repeated document handle"); return;
+                }
+                const hm_doc_row &r = b->docs[i];
+                const DocMeta &m = s->docs[h];
+                if ((uint64_t)r.change_off + r.n_changes > b->n_changes || (uint64_t)r.dep_off + r.n_deps > b->n_deps ||
+                    (uint64_t)r.op_off + r.n_ops > b->n_ops) { fail_with("document rows outside the batch tables"); return; }
+                if (r.n_actors > S || r.n_actors < m.n_actors || r.n_regs < m.n_r || r.n_objs < m.n_objs || r.n_objs == 0) {
+                    fail_with("document totals must cover the existing log (and n_actors <= a_stride)"); return;
+                }
+                // every change row must lie inside its document's slice of the batch tables
+                for (uint32_t c = r.change_off; c < r.change_off + r.n_changes; c++) {
+                    const hm_change_row &cr = b->changes[c];
+                    if ((uint64_t)cr.dep_off < r.dep_off || (uint64_t)cr.dep_off + cr.n_deps > (uint64_t)r.dep_off + r.n_deps ||
+                        (uint64_t)cr.op_first < r.op_off || (uint64_t)cr.op_first + cr.n_ops > (uint64_t)r.op_off + r.n_ops) {
+                        fail_with("change rows outside their document's deps/ops"); return;
+                    }
+                }
+                // the actor re-rank of the existing rows: a permutation into the new ranks.  Checked
+                // here, before any document meta or arena pointer moves (a failure leaves the store as it was)
+                if (actor_remap) {
+                    const uint8_t *mp = actor_remap + (size_t)i * S;
+                    uint64_t used = 0;
+                    for (uint32_t a = 0; a < m.n_actors; a++) {
+                        if (mp[a] >= r.n_actors || ((used >> mp[a]) & 1)) {
+                            fail_with("actor remap is not a permutation into the new ranks"); return;
+                        }
+                        used |= 1ull << mp[a];
+                    }
                 }
             }
-        }
+        });
+        if (bad) return hm_engine_fail(s->e, HM_ERR_INVALID, bad);
         T.mark("validate");
-        // plan segments: grow into fresh segments, compact the arenas when full
-        size_t need_c = 0, need_d = 0, need_o = 0, need_r = 0;
-        for (uint32_t i = 0; i < n; i++) {
-            const DocMeta &m = s->docs[doc_handles[i]];
-            need_c += pow2ceil(std::max<uint32_t>(m.n_c + b->docs[i].n_changes, 16));
-            need_d += pow2ceil(std::max<uint32_t>(m.n_d + b->docs[i].n_deps, 16));
-            need_o += pow2ceil(std::max<uint32_t>(m.n_o + b->docs[i].n_ops, 16));
-            need_r += pow2ceil(std::max<uint32_t>(b->docs[i].n_regs, 16));
-        }
-        if (s->used_c + need_c > s->cap_c || s->used_d + need_d > s->cap_d || s->used_o + need_o > s->cap_o ||
-            s->used_r + need_r > s->cap_r) {
-            int r = compact(s, need_c, need_d, need_o, need_r);
-            if (r) return r;
+        // plan segments: a document outgrowing a segment moves to a fresh one at the arena's end;
+        // the arenas are compacted first when the worst case would not fit
+        {
+            std::vector<size_t> part(4 * 16, 0);
+            par_for(n, [&](uint32_t lo, uint32_t hi, uint32_t t) {
+                size_t c = 0, d = 0, o = 0, g = 0;
+                for (uint32_t i = lo; i < hi; i++) {
+                    const DocMeta &m = s->docs[doc_handles[i]];
+                    c += pow2ceil(std::max<uint32_t>(m.n_c + b->docs[i].n_changes, 16));
+                    d += pow2ceil(std::max<uint32_t>(m.n_d + b->docs[i].n_deps, 16));
+                    o += pow2ceil(std::max<uint32_t>(m.n_o + b->docs[i].n_ops, 16));
+                    g += pow2ceil(std::max<uint32_t>(b->docs[i].n_regs, 16));
+                }
+                part[4 * t] = c; part[4 * t + 1] = d; part[4 * t + 2] = o; part[4 * t + 3] = g;
+            });
+            size_t need_c = 0, need_d = 0, need_o = 0, need_r = 0;
+            for (uint32_t t = 0; t < 16; t++) { need_c += part[4 * t]; need_d += part[4 * t + 1]; need_o += part[4 * t + 2]; need_r += part[4 * t + 3]; }
+            if (s->used_c + need_c > s->cap_c || s->used_d + need_d > s->cap_d || s->used_o + need_o > s->cap_o ||
+                s->used_r + need_r > s->cap_r) {
+                int r = compact(s, need_c, need_d, need_o, need_r);
+                if (r) return r;
+            }
         }
         s->p_old.resize(n);
-        s->p_inv_row.assign(n, -1);
+        s->p_inv_row.resize(n);
         s->p_inv.clear();
         s->p_handles.assign(doc_handles, doc_handles + n);
-        std::vector<AppendDesc> descs(n);
+        s->descs.resize(n);
+        std::vector<AppendDesc> &descs = s->descs;
         uint32_t n_remap = 0;
         std::vector<uint8_t> remap_rows;
-        // route: a document whose resident state is clean (last merge ok, nothing queued, no
-        // re-rank) and whose new rows fit the incremental tiles is applied by inc_apply_kernel;
-        // the rest re-merge their whole log (DocBackend.applyRemoteChanges either way)
-        std::vector<uint32_t> cold;
-        uint32_t n_inc = 0, mx_new_c = 0, mx_tgt = 0, mx_stage = 0, mx_regs = 0, mx_surv = 0, mx_slots = 0;
-        for (uint32_t i = 0; i < n; i++) {
-            const uint32_t h = doc_handles[i];
-            DocMeta &m = s->docs[h];
-            const DocMeta &o = (s->p_old[i] = m);
-            const hm_doc_row &r = b->docs[i];
-            AppendDesc &D = descs[i];
-            D = AppendDesc{};
-            D.handle = h;
-            D.src_c = m.c.off; D.n_old_c = m.n_c; D.new_c = r.change_off; D.n_new_c = r.n_changes;
-            D.src_d = m.d.off; D.n_old_d = m.n_d; D.new_d = r.dep_off; D.n_new_d = r.n_deps;
-            D.src_o = m.o.off; D.n_old_o = m.n_o; D.new_o = r.op_off; D.n_new_o = r.n_ops;
-            D.src_r = m.r.off; D.n_old_r = m.n_r;
-            if (m.n_c + r.n_changes > m.c.cap) seg_alloc(s->used_c, s->cap_c, m.n_c + r.n_changes, m.c);
-            if (m.n_d + r.n_deps > m.d.cap) seg_alloc(s->used_d, s->cap_d, m.n_d + r.n_deps, m.d);
-            if (m.n_o + r.n_ops > m.o.cap) seg_alloc(s->used_o, s->cap_o, m.n_o + r.n_ops, m.o);
-            if (r.n_regs > m.r.cap) seg_alloc(s->used_r, s->cap_r, r.n_regs, m.r);
-            D.dst_c = m.c.off; D.dst_d = m.d.off; D.dst_o = m.o.off; D.dst_r = m.r.off;
-            D.remap_row = 0xFFFFFFFFu;
-            bool reranked = false;
-            if (actor_remap) {
+        // re-ranked documents (rare): their remap rows, in batch order
+        if (actor_remap) {
+            for (uint32_t i = 0; i < n; i++) {
+                const DocMeta &m = s->docs[doc_handles[i]];
                 const uint8_t *mp = actor_remap + (size_t)i * S;
                 bool ident = true;
                 for (uint32_t a = 0; a < m.n_actors; a++) if (mp[a] != a) ident = false;
-                if (!ident) {
-                    reranked = true;
-                    const size_t at = remap_rows.size();
-                    remap_rows.resize(at + S, 0xFF);
-                    s->p_inv_row[i] = (int32_t)s->p_inv.size();
-                    s->p_inv.resize(s->p_inv.size() + S, 0xFF);
-                    uint8_t *inv = s->p_inv.data() + s->p_inv_row[i];
-                    for (uint32_t a = 0; a < m.n_actors; a++) { remap_rows[at + a] = mp[a]; inv[mp[a]] = (uint8_t)a; }   // validated above
-                    D.remap_row = n_remap++;
-                }
+                s->p_inv_row[i] = -1;
+                if (ident) continue;
+                const size_t at = remap_rows.size();
+                remap_rows.resize(at + S, 0xFF);
+                s->p_inv_row[i] = (int32_t)s->p_inv.size();
+                s->p_inv.resize(s->p_inv.size() + S, 0xFF);
+                uint8_t *inv = s->p_inv.data() + s->p_inv_row[i];
+                for (uint32_t a = 0; a < m.n_actors; a++) { remap_rows[at + a] = mp[a]; inv[mp[a]] = (uint8_t)a; }   // validated above
+                descs[i].remap_row = n_remap++;
             }
-            m.n_c += r.n_changes; m.n_d += r.n_deps; m.n_o += r.n_ops;
-            m.n_r = r.n_regs; m.n_objs = r.n_objs; m.n_actors = r.n_actors; m.flags |= r.flags;
-            D.n_r = m.n_r; D.n_actors = (uint16_t)m.n_actors; D.n_objs = m.n_objs;
-            const uint32_t tgt = r.n_deps + r.n_changes;            // fold steps: deps + own predecessor
-            const bool inc = s->incremental && o.last.status == HM_OK && o.last.n_queued == 0 && !reranked &&
-                             r.n_changes > 0 && r.n_changes <= HM_INC_MAX_NEW_C && r.n_ops <= HM_INC_MAX_NEW_O &&
-                             tgt <= HM_INC_MAX_TGT && m.n_r <= HM_INC_MAX_REGS && o.last.n_surv <= HM_INC_MAX_SURV &&
-                             o.n_r <= m.n_r && m.n_actors <= S && !((o.flags | r.flags) & HM_DOC_HAS_LISTS);
-            if (!inc) { cold.push_back(h); continue; }
-            D.inc = 1;
-            n_inc++;
-            mx_new_c = std::max(mx_new_c, r.n_changes); mx_tgt = std::max(mx_tgt, tgt);
-            mx_stage = std::max(mx_stage, std::min<uint32_t>(o.n_c, HM_INC_MAX_STAGE));
-            mx_regs = std::max(mx_regs, m.n_r); mx_surv = std::max(mx_surv, o.last.n_surv);
-            mx_slots = std::max(mx_slots, std::min<uint32_t>(r.n_ops, HM_INC_SLOTS));
         }
+        // new segments: sizes per document (0 = fits), then arena offsets by a prefix over the
+        // batch (threads sum their ranges, one serial pass over the partial sums)
+        s->grow.resize(4 * (size_t)n);
+        std::vector<uint32_t> &grow = s->grow;
+        std::vector<size_t> base(4 * 17, 0);
+        const uint32_t TT = par_for(n, [&](uint32_t lo, uint32_t hi, uint32_t t) {
+            size_t acc[4] = {0, 0, 0, 0};
+            for (uint32_t i = lo; i < hi; i++) {
+                const DocMeta &m = s->docs[doc_handles[i]];
+                const hm_doc_row &r = b->docs[i];
+                uint32_t *g = &grow[4 * (size_t)i];
+                g[0] = g[1] = g[2] = g[3] = 0;
+                if (m.n_c + r.n_changes > m.c.cap) g[0] = pow2ceil(std::max<uint32_t>(m.n_c + r.n_changes, 16));
+                if (m.n_d + r.n_deps > m.d.cap) g[1] = pow2ceil(std::max<uint32_t>(m.n_d + r.n_deps, 16));
+                if (m.n_o + r.n_ops > m.o.cap) g[2] = pow2ceil(std::max<uint32_t>(m.n_o + r.n_ops, 16));
+                if (r.n_regs > m.r.cap) g[3] = pow2ceil(std::max<uint32_t>(r.n_regs, 16));
+                for (int k = 0; k < 4; k++) acc[k] += g[k];
+            }
+            for (int k = 0; k < 4; k++) base[4 * (t + 1) + k] = acc[k];
+        });
+        base[0] = s->used_c; base[1] = s->used_d; base[2] = s->used_o; base[3] = s->used_r;
+        for (uint32_t t = 1; t <= TT; t++) for (int k = 0; k < 4; k++) base[4 * t + k] += base[4 * (t - 1) + k];
+        s->used_c = base[4 * TT]; s->used_d = base[4 * TT + 1]; s->used_o = base[4 * TT + 2]; s->used_r = base[4 * TT + 3];
+        // route: a document whose resident state is clean (last merge ok, nothing queued, no
+        // re-rank) and whose new rows fit the incremental tiles is applied by inc_apply_kernel;
+        // the rest re-merge their whole log (DocBackend.applyRemoteChanges either way)
+        struct Part { std::vector<uint32_t> cold; uint32_t n_inc = 0, mx[6] = {0, 0, 0, 0, 0, 0}; };
+        std::vector<Part> parts(16);
+        par_for(n, [&](uint32_t lo, uint32_t hi, uint32_t t) {
+            size_t at[4] = {base[4 * t], base[4 * t + 1], base[4 * t + 2], base[4 * t + 3]};
+            Part &P = parts[t];
+            for (uint32_t i = lo; i < hi; i++) {
+                const uint32_t h = doc_handles[i];
+                DocMeta &m = s->docs[h];
+                const hm_store::OldMeta o = {m.n_c, m.n_d, m.n_o, m.n_r, m.n_objs, (uint16_t)m.n_actors, m.flags};
+                s->p_old[i] = o;
+                const hm_doc_result last = m.last;
+                const hm_doc_row &r = b->docs[i];
+                AppendDesc &D = descs[i];
+                const uint32_t remap_row = D.remap_row;
+                D = AppendDesc{};
+                D.handle = h;
+                D.src_c = m.c.off; D.n_old_c = m.n_c; D.new_c = r.change_off; D.n_new_c = r.n_changes;
+                D.src_d = m.d.off; D.n_old_d = m.n_d; D.new_d = r.dep_off; D.n_new_d = r.n_deps;
+                D.src_o = m.o.off; D.n_old_o = m.n_o; D.new_o = r.op_off; D.n_new_o = r.n_ops;
+                D.src_r = m.r.off; D.n_old_r = m.n_r;
+                const uint32_t *g = &grow[4 * (size_t)i];
+                Seg *segs[4] = {&m.c, &m.d, &m.o, &m.r};
+                for (int k = 0; k < 4; k++) if (g[k]) { segs[k]->off = (uint32_t)at[k]; segs[k]->cap = g[k]; at[k] += g[k]; }
+                D.dst_c = m.c.off; D.dst_d = m.d.off; D.dst_o = m.o.off; D.dst_r = m.r.off;
+                if (!actor_remap) s->p_inv_row[i] = -1;
+                D.remap_row = actor_remap && s->p_inv_row[i] >= 0 ? remap_row : 0xFFFFFFFFu;
+                const bool reranked = D.remap_row != 0xFFFFFFFFu;
+                m.n_c += r.n_changes; m.n_d += r.n_deps; m.n_o += r.n_ops;
+                m.n_r = r.n_regs; m.n_objs = r.n_objs; m.n_actors = r.n_actors; m.flags |= r.flags;
+                D.n_r = m.n_r; D.n_actors = (uint16_t)m.n_actors; D.n_objs = m.n_objs;
+                const uint32_t tgt = r.n_deps + r.n_changes;            // fold steps: deps + own predecessor
+                const bool inc = s->incremental && last.status == HM_OK && last.n_queued == 0 && !reranked &&
+                                 r.n_changes > 0 && r.n_changes <= HM_INC_MAX_NEW_C && r.n_ops <= HM_INC_MAX_NEW_O &&
+                                 tgt <= HM_INC_MAX_TGT && m.n_r <= HM_INC_MAX_REGS && last.n_surv <= HM_INC_MAX_SURV &&
+                                 o.n_r <= m.n_r && m.n_actors <= S && !((o.flags | r.flags) & HM_DOC_HAS_LISTS);
+                if (!inc) { P.cold.push_back(h); continue; }
+                D.inc = 1;
+                P.n_inc++;
+                const uint32_t v[6] = {r.n_changes, tgt, std::min<uint32_t>(o.n_c, HM_INC_MAX_STAGE), m.n_r, last.n_surv,
+                                       std::min<uint32_t>(r.n_ops, HM_INC_SLOTS)};
+                for (int k = 0; k < 6; k++) P.mx[k] = std::max(P.mx[k], v[k]);
+            }
+        });
+        std::vector<uint32_t> cold;
+        uint32_t n_inc = 0, mx[6] = {0, 0, 0, 0, 0, 0};
+        for (auto &P : parts) {
+            cold.insert(cold.end(), P.cold.begin(), P.cold.end());
+            n_inc += P.n_inc;
+            for (int k = 0; k < 6; k++) mx[k] = std::max(mx[k], P.mx[k]);
+        }
+        const uint32_t mx_new_c = mx[0], mx_tgt = mx[1], mx_stage = mx[2], mx_regs = mx[3], mx_surv = mx[4], mx_slots = mx[5];
         T.mark("plan+route");
         // stage and launch: append, merge, gather
         const StageLayout L = layout(b->n_changes, b->n_deps, b->n_ops, n, remap_rows.size(), n, n, S, n_inc ? n : 0);
@@ -508,7 +587,8 @@ int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
         s->st_inc = n_inc; s->st_cold = (uint32_t)cold.size(); s->st_bail = 0;
         if (n_inc) {
             // documents the incremental kernel handed back re-merge their whole log
-            std::vector<uint8_t> bail(n);
+            s->bail.resize(n);
+            std::vector<uint8_t> &bail = s->bail;
             SCHK(s, hipMemcpyAsync(bail.data(), sp + L.o_bail, n, hipMemcpyDeviceToHost, st));
             SCHK(s, hipStreamSynchronize(st));
             std::vector<uint32_t> again;
@@ -571,7 +651,7 @@ int hm_batch_wait(hm_store *s, uint64_t batch_id, hm_doc_result *out_docs, uint3
             const uint32_t h = s->p_handles[i];
             if (res[i].status == HM_OK) { s->docs[h].last = res[i]; continue; }
             DocMeta &m = s->docs[h];
-            const DocMeta &o = s->p_old[i];
+            const hm_store::OldMeta &o = s->p_old[i];
             AppendDesc D = {};
             D.handle = h;
             D.src_c = D.dst_c = m.c.off; D.n_old_c = o.n_c;
