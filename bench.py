@@ -515,7 +515,8 @@ def _host_info():
 def _pmc_traffic(args, kernel="merge_small_kernel"):
     """HBM bytes per launch of the dominant kernel, from two rocprofv3 PMC passes over a short
     run of this same workload (separate passes: FETCH_SIZE and WRITE_SIZE do not fit one pass's
-    TCC counters).  Corrected as /opt/skills/guides/MI355X_MICROARCH.md §HBM prescribes: on gfx950
+    TCC counters; the child runs full-workload launches only: no parity sample, no side legs,
+    whose smaller launches would dilute the per-launch average).  Corrected as /opt/skills/guides/MI355X_MICROARCH.md §HBM prescribes: on gfx950
     FETCH_SIZE (KiB) counts half the bytes of wide streaming reads, WRITE_SIZE counts them exactly.
     Each pass is a child process in its own session under a time limit; None if unavailable."""
     import csv
@@ -532,7 +533,8 @@ def _pmc_traffic(args, kernel="merge_small_kernel"):
         d = tempfile.mkdtemp(prefix="hm_pmc_", dir="/tmp")
         cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "run", "--",
                sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1", "--no-cpu",
-               "--no-traffic", "--no-e2e", "--no-orders", "--docs", str(args.docs), "--config", args.config] + ([] if args.arrival is None else ["--arrival", str(args.arrival)])
+               "--no-traffic", "--no-e2e", "--no-orders", "--no-incremental", "--no-node", "--check-docs", "0",
+               "--docs", str(args.docs), "--config", args.config] + ([] if args.arrival is None else ["--arrival", str(args.arrival)])
         pr = subprocess.Popen(cmd, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), stdout=subprocess.DEVNULL,
                               stderr=subprocess.DEVNULL, start_new_session=True)
         try:
