@@ -171,6 +171,21 @@ class RcclTransport:
         idb = (ctypes.c_uint8 * 128).from_buffer_copy(unique_id)
         engine._check(self.L.hm_comm_create(engine._h, world, rank, idb, ctypes.byref(self._h)), "hm_comm_create")
         self.d_counts = torch.zeros(world, dtype=torch.int64, device=self.device)
+        self._stream = torch.cuda.Stream(device=self.device)
+
+    def _enter(self, stream):
+        """The stream a call runs on.  A NULL stream means the engine's own (non-blocking)
+        stream in the C-ABI, so torch's default stream (handle 0) is never passed: without an
+        explicit stream the call runs on this transport's stream, ordered after the caller's
+        current stream and (``_leave``) before it."""
+        if stream is not None:
+            return stream
+        self._stream.wait_stream(self.torch.cuda.current_stream())
+        return self._stream.cuda_stream
+
+    def _leave(self, stream):
+        if stream is None:
+            self.torch.cuda.current_stream().wait_stream(self._stream)
 
     @staticmethod
     def unique_id(engine) -> bytes:
@@ -193,27 +208,31 @@ class RcclTransport:
         cnt = torch.zeros(1, dtype=torch.int32, device=self.device)
         scr = torch.empty(int(self.L.hm_clock_records_scratch_bytes(n, max(S, 1))) + 16, dtype=torch.uint8,
                           device=self.device)
-        st = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        st = self._enter(stream)
         self.eng._check(self.L.hm_clock_records_device(
             self.eng._h, doc_keys.data_ptr(), actor_keys.data_ptr(), clock.data_ptr(),
             base.data_ptr() if base is not None else None, n, max(S, 1), out.data_ptr(), cnt.data_ptr(),
             scr.data_ptr(), st), "hm_clock_records_device")
+        self._leave(stream)
+        if stream is not None:
+            torch.cuda.ExternalStream(stream).synchronize()
         k = int(cnt.item())
         return out[: k * 24]
 
     def gather_device(self, d_recs, stream=None):
         """Every rank's device records, back to back in rank order (device uint8 tensor)."""
         torch = self.torch
-        st = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        st = self._enter(stream)
         n_local = d_recs.numel() // 24
         self.eng._check(self.L.hm_clock_count_allgather(self._h, n_local, self.d_counts.data_ptr(), st),
-                        "hm_clock_count_allgather")
+                        "hm_clock_count_allgather")           # returns after the counts arrived
         counts = self.d_counts.cpu().numpy().astype(np.uint64)
         total = int(counts.sum())
         out = torch.empty(max(total, 1) * 24, dtype=torch.uint8, device=self.device)
         cbuf = (ctypes.c_uint64 * self.world)(*[int(c) for c in counts])
         self.eng._check(self.L.hm_clock_allgather(self._h, d_recs.data_ptr() if n_local else None, cbuf,
                                                   out.data_ptr(), st), "hm_clock_allgather")
+        self._leave(stream)
         return out[: total * 24], [int(c) for c in counts]
 
     def gather(self, recs: np.ndarray) -> Tuple[np.ndarray, List[int]]:
@@ -225,9 +244,10 @@ class RcclTransport:
         return out.cpu().numpy().view(CLOCK_REC_DT).copy(), counts
 
     def min_allreduce_device(self, d_seq, stream=None) -> None:
-        st = stream if stream is not None else self.torch.cuda.current_stream().cuda_stream
+        st = self._enter(stream)
         self.eng._check(self.L.hm_clock_min_allreduce(self._h, d_seq.data_ptr(), d_seq.numel(), st),
                         "hm_clock_min_allreduce")
+        self._leave(stream)
 
     def min_allreduce(self, seq: np.ndarray) -> np.ndarray:
         torch = self.torch
