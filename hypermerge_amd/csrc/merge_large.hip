@@ -20,12 +20,15 @@
 #include "../../include/hypermerge_amd.h"
 #include "merge_kernels.h"
 
-#define LWG 256
+#ifndef HML_WGS_PER_CU
+#define HML_WGS_PER_CU 4   // workgroups per CU: 16 waves per CU split into this many documents
+#endif
+#define LWG (1024 / HML_WGS_PER_CU)
 #define LA_MAX 64
 // LDS arena per workgroup (u32 words): 36 KB keeps 4 workgroups per CU (the VGPR-bound
 // occupancy at 128 VGPRs).  Documents whose L2 closure rows (2·n·A + T words) or L4 Euler
 // tour (E words, 16-bit links) fit run those phases out of LDS instead of the pool.
-#define LARENA 9216
+#define LARENA (36864 / HML_WGS_PER_CU)
 // Explicit address spaces: LDS pointers -> ds_*, pool pointers -> global_* (a generic pointer
 // would compile to flat_* ops, which count against lgkmcnt too, so every LDS wait would also
 // wait for the outstanding pool loads, stores and atomics).
@@ -87,7 +90,7 @@ __device__ __forceinline__ u64 err_key(uint32_t h, uint32_t op_plus1, uint32_t a
 struct Shared {
     uint32_t base[LA_MAX], maxs[LA_MAX], tabo[LA_MAX + 1], clock[LA_MAX], bclock[LA_MAX], headv[LA_MAX];
     uint32_t maxad[LA_MAX];
-    uint32_t flags, all_ok, H, nins, nl, total, lists, grew, nmake, nodup;
+    uint32_t flags, all_ok, H, nins, nl, total, lists, grew, nmake, nodup, ctrs, nsurv;
     u64 errkey;
     uint32_t scan[LWG / 64 + 1];
     u64 scratch_base;
@@ -135,10 +138,11 @@ __device__ void scan_array(Shared &sh, uint32_t *arr, uint32_t N, uint32_t *tota
 
 struct Scratch {
     GLB uint32_t *tab, *h2a, *opchg, *segmax, *segcnt, *survcnt, *regoff, *regobj, *segoff, *segfill;
-    GLB uint32_t *survtmp, *segk, *survop, *survp, *objtype, *listid, *nodeop, *nodepi, *regnode, *pcount, *poff;
+    GLB uint32_t *survtmp, *segk, *survop, *survp, *objtype, *listid, *nodepi, *regnode, *pcount, *poff;
     GLB uint32_t *pfill, *plist, *fc, *ns, *tour0, *tour1, *tval0, *tval1, *listbase, *pos, *vis;
     GLB int32_t *hist;
-    GLB u64 *opkey, *insmin, *objslot, *seglist, *nodekey, *survabs;
+    GLB uint32_t *insmin, *objslot, *seglist, *nodekey, *kbase, *survk;   // 32-bit op keys (L3)
+    GLB u64 *survabs;
     GLB int64_t *survsum;
     GLB uint32_t *vc;                   // [n * A] closure rows (L2 pointer jumping, second buffer)
     GLB uint32_t *hx;                   // parallel history (L1): [ht n][hp n][hnev n][hfill n][hmem n][hoff n+1][pm T]
@@ -149,13 +153,14 @@ __host__ __device__ inline size_t large_carve(uintptr_t base, uint32_t n, uint32
     size_t o = 0;
     const uint32_t NP = R + O, NE = 2 * (m + O);
 #define TK(f, T_, cnt) do { S->f = (GLB T_ *)(base + o); o = (o + (size_t)(cnt) * sizeof(T_) + 15) & ~(size_t)15; } while (0)
-    TK(opkey, u64, m); TK(insmin, u64, R); TK(objslot, u64, O); TK(seglist, u64, m); TK(nodekey, u64, m);
     TK(survabs, u64, m); TK(survsum, int64_t, m); TK(vc, uint32_t, (size_t)n * A);
+    TK(survk, uint32_t, m); TK(insmin, uint32_t, R); TK(objslot, uint32_t, O); TK(seglist, uint32_t, m);
+    TK(nodekey, uint32_t, m); TK(kbase, uint32_t, n);
     TK(tab, uint32_t, T); TK(h2a, uint32_t, n); TK(hist, int32_t, n); TK(opchg, uint32_t, m);
     TK(segmax, uint32_t, (size_t)R * A); TK(segcnt, uint32_t, R); TK(survcnt, uint32_t, R);
     TK(regoff, uint32_t, R); TK(regobj, uint32_t, R); TK(segoff, uint32_t, R); TK(segfill, uint32_t, R);
     TK(survtmp, uint32_t, m); TK(segk, uint32_t, m); TK(survop, uint32_t, m); TK(survp, uint32_t, m); TK(objtype, uint32_t, O);
-    TK(listid, uint32_t, O); TK(nodeop, uint32_t, m); TK(nodepi, uint32_t, m); TK(regnode, uint32_t, R);
+    TK(listid, uint32_t, O); TK(nodepi, uint32_t, m); TK(regnode, uint32_t, R);
     TK(pcount, uint32_t, NP); TK(poff, uint32_t, NP); TK(pfill, uint32_t, NP); TK(plist, uint32_t, m);
     TK(fc, uint32_t, NP); TK(ns, uint32_t, m); TK(tour0, uint32_t, NE); TK(tour1, uint32_t, NE);
     TK(tval0, uint32_t, NE); TK(tval1, uint32_t, NE);
@@ -166,6 +171,11 @@ __host__ __device__ inline size_t large_carve(uintptr_t base, uint32_t n, uint32
 }
 
 enum Outcome { LOK = 0, LERR = 1, LUNSUP = 2 };
+
+// L3 stages per-change inputs and a 16-bit op -> change map in the LDS arena (merge_doc_large)
+__device__ __forceinline__ bool l3_ok(uint32_t n, uint32_t m, uint32_t A) {
+    return n < 65536 && n * (A + 5) + (m + 1) / 2 <= LARENA;
+}
 
 // allDeps row of the applied change at arrival index ci (global, written in history order)
 __device__ __forceinline__ uint32_t *ad_row(const SmallParams &p, const hm_doc_row &doc, uint32_t ci) {
@@ -372,7 +382,7 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
     // ---- per-actor seq ranges -> first-arrival table size ----
     if (tid < LA_MAX) { sh.base[tid] = 0xFFFFFFFFu; sh.maxs[tid] = 0; sh.clock[tid] = 0; sh.bclock[tid] = 0;
                         sh.headv[tid] = 0; sh.maxad[tid] = 0; }
-    if (tid == 0) { sh.flags = 0; sh.errkey = ~0ull; sh.all_ok = 1; sh.H = 0; sh.nins = 0; sh.total = 0; sh.lists = 0; }
+    if (tid == 0) { sh.flags = 0; sh.errkey = ~0ull; sh.all_ok = 1; sh.H = 0; sh.nins = 0; sh.total = 0; sh.lists = 0; sh.ctrs = 0; }
     bsync();
     if (n == 0 && (m || doc.n_deps)) return LUNSUP;
     for (uint32_t i = tid; i < n; i += LWG) {
@@ -421,7 +431,7 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
     for (uint32_t i = tid; i < n; i += LWG) { const hm_change_row c = CH[i]; g_min(&X.tab[slot_of(c.actor, c.seq)], i); }
     for (uint32_t i = tid; i < n; i += LWG) {
         const hm_change_row c = CH[i];
-        for (uint32_t j = 0; j < c.n_ops; j++) X.opchg[c.op_first - doc.op_off + j] = i;
+        if (!l3_ok(n, m, A)) for (uint32_t j = 0; j < c.n_ops; j++) X.opchg[c.op_first - doc.op_off + j] = i;
     }
     bsync();
     LSTAMP(0);
@@ -806,51 +816,78 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
     if (tid < A && sh.clock[tid] && sh.maxad[tid] < sh.clock[tid]) sh.headv[tid] = sh.clock[tid];
 
     // ---- L3: ops ----
-    // Per-change inputs of the op loops (history position, actor, seq, first op, allDeps row)
-    // and the op -> change map are staged in the LDS arena when they fit (L2 is done with it).
-    const bool l3 = n * (A + 4) + m <= LARENA;
-    LDS uint32_t *l_hist = ar, *l_act = ar + n, *l_seq = ar + 2 * n, *l_op0 = ar + 3 * n, *l_ad = ar + 4 * n,
-                 *l_opchg = ar + 4 * n + n * A;
-    for (uint32_t i = tid; i < O; i += LWG) { X.objslot[i] = i == 0 ? 0ull : ~0ull; X.objtype[i] = i == 0 ? HM_MAKE_MAP : 0xFFu; }
+    // Op keys: an applied op's position in application order, i.e. (history position, op index)
+    // as one 32-bit number: kbase[change] = the ops of the changes before it in history.
+    for (uint32_t h = tid; h < H; h += LWG) X.survp[h] = CH[X.h2a[h]].n_ops;     // survp is free until L3 survivors
+    bsync();
+    uint32_t m_applied;
+    scan_array(sh, X.survp, H, &m_applied);
+    (void)m_applied;
+    // Per-change inputs of the op loops (history position, actor, seq, first op, key base,
+    // allDeps row) and the op -> change map (16 bit) are staged in the LDS arena when they fit
+    // (L2 is done with it); so is one compact word per op — register (20 b) | action (4 b) |
+    // object (8 b) — when the document's ids fit those widths, so the op loops below do not
+    // re-read 32-byte op rows from HBM (only INS parents / elems and survivor values are).
+    const uint32_t l3_words = n * (A + 5) + (m + 1) / 2;
+    const bool l3 = l3_ok(n, m, A);
+    const bool lop = l3 && R <= (1u << 20) && O < 255 && l3_words + m <= LARENA;
+    LDS uint32_t *l_hist = ar, *l_act = ar + n, *l_seq = ar + 2 * n, *l_op0 = ar + 3 * n, *l_kb = ar + 4 * n,
+                 *l_ad = ar + 5 * n, *l_op = ar + l3_words;
+    LDS uint16_t *l_opchg = (LDS uint16_t *)(ar + 5 * n + n * A);
+    for (uint32_t i = tid; i < O; i += LWG) { X.objslot[i] = i == 0 ? 0u : 0xFFFFFFFFu; X.objtype[i] = i == 0 ? HM_MAKE_MAP : 0xFFu; }
     for (uint32_t i = tid; i < R; i += LWG) {
-        X.segcnt[i] = 0; X.survcnt[i] = 0; X.insmin[i] = ~0ull; X.regobj[i] = HM_NONE; X.segfill[i] = 0;
-        for (uint32_t a = 0; a < A; a++) X.segmax[(size_t)i * A + a] = 0;
+        X.segcnt[i] = 0; X.survcnt[i] = 0; X.insmin[i] = 0xFFFFFFFFu; X.regobj[i] = HM_NONE; X.segfill[i] = 0;
     }
-    if (tid == 0) sh.nmake = 0;
-    if (l3) {
-        for (uint32_t i = tid; i < n; i += LWG) {
-            const hm_change_row c = CH[i];
+    if (tid == 0) { sh.nmake = 0; sh.nsurv = 0; }
+    for (uint32_t i = tid; i < n; i += LWG) {
+        const hm_change_row c = CH[i];
+        const int32_t hi = X.hist[i];
+        const uint32_t kb = hi >= 0 ? X.survp[hi] : 0xFFFFFFFFu;
+        if (l3) {
             const uint32_t o0 = c.op_first - doc.op_off;
-            l_hist[i] = (uint32_t)X.hist[i]; l_act[i] = c.actor; l_seq[i] = c.seq; l_op0[i] = o0;
+            l_hist[i] = (uint32_t)hi; l_act[i] = c.actor; l_seq[i] = c.seq; l_op0[i] = o0; l_kb[i] = kb;
             const uint32_t *ad = ad_row(p, doc, i);
             for (uint32_t a = 0; a < A; a++) l_ad[i * A + a] = ad[a];
-            for (uint32_t j = 0; j < c.n_ops; j++) l_opchg[o0 + j] = i;
+            for (uint32_t j = 0; j < c.n_ops; j++) l_opchg[o0 + j] = (uint16_t)i;
+        } else {
+            X.kbase[i] = kb;
         }
     }
     bsync();
     LSTAMP(11);
-    auto opchg_of = [&](uint32_t k) -> uint32_t { return l3 ? l_opchg[k] : X.opchg[k]; };
+    auto opchg_of = [&](uint32_t k) -> uint32_t { return l3 ? (uint32_t)l_opchg[k] : X.opchg[k]; };
     auto hist_of = [&](uint32_t ci) -> int32_t { return l3 ? (int32_t)l_hist[ci] : X.hist[ci]; };
     auto op0_of = [&](uint32_t ci) -> uint32_t { return l3 ? l_op0[ci] : CH[ci].op_first - doc.op_off; };
     auto act_of = [&](uint32_t ci) -> uint32_t { return l3 ? l_act[ci] : CH[ci].actor; };
     auto seq_of = [&](uint32_t ci) -> uint32_t { return l3 ? l_seq[ci] : CH[ci].seq; };
     auto ad_of = [&](uint32_t ci, uint32_t a) -> uint32_t { return l3 ? l_ad[ci * A + a] : ad_row(p, doc, ci)[a]; };
+    auto kb_of = [&](uint32_t ci) -> uint32_t { return l3 ? l_kb[ci] : X.kbase[ci]; };
+    // (register, action, object) of op k
+    struct OpC { uint32_t reg, action, obj; };
+    auto op_c = [&](uint32_t k) -> OpC {
+        if (lop) { const uint32_t w = l_op[k]; return OpC{w & 0xFFFFFu, (w >> 20) & 15u, w >> 24}; }
+        const hm_op_row &o = OP[k];
+        return OpC{o.reg, o.action, o.obj};
+    };
+    auto key_of = [&](uint32_t k, uint32_t ci) -> uint32_t { return kb_of(ci) + (k - op0_of(ci)); };   // applied ops
     for (uint32_t k = tid; k < m; k += LWG) {
         const hm_op_row o = OP[k];
         const uint32_t ci = opchg_of(k);
         const int32_t h = hist_of(ci);
-        const u64 key = h >= 0 ? (((u64)h << 32) | (k - op0_of(ci))) : ~0ull;
-        X.opkey[k] = key;
+        if (o.action == HM_INC || o.datatype == HM_DT_COUNTER) sh.ctrs = 1;
         // malformed rows (any op, applied or not) put the whole document outside the envelope
         const bool bad = o.action <= HM_MAKE_TEXT ? o.obj >= O
                        : (o.action <= HM_INC ? (o.reg >= R || (o.action == HM_INS && o.parent != HM_HEAD && o.parent >= R)) : true);
         if (bad) { atomicOr(&sh.flags, LF_UNSUPPORTED); continue; }
+        // (object 255: an unknown object id, >= O)
+        if (lop) l_op[k] = (o.action <= HM_MAKE_TEXT ? 0u : o.reg) | (o.action << 20) | ((o.obj < O ? o.obj : 255u) << 24);
         if (h < 0) continue;
+        const uint32_t key = key_of(k, ci);
         if (o.action <= HM_MAKE_TEXT) {
             g_min(&X.objslot[o.obj], key + 1);
             X.survtmp[atomicAdd(&sh.nmake, 1u)] = k;              // make-op list (survtmp is free until L3 offsets)
         } else {
-            if (o.obj >= O) continue;
+            if (o.obj >= O) continue;                              // an unknown object: the survivor pass throws
             X.regobj[o.reg] = o.obj;
             if (o.action == HM_INS) { g_min(&X.insmin[o.reg], key + 1); if (o.elem >= (1u << 24)) atomicOr(&sh.flags, LF_UNSUPPORTED); }
             else g_add(&X.segcnt[o.reg], 1u);
@@ -859,30 +896,33 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
     bsync();
     if (sh.flags) return LUNSUP;
     LSTAMP(12);
+    const bool ctrs = sh.ctrs != 0;
     for (uint32_t q = tid; q < sh.nmake; q += LWG) {
         const uint32_t k = X.survtmp[q];
-        const hm_op_row o = OP[k];
-        const u64 key = X.opkey[k];
+        const OpC o = op_c(k);
         const uint32_t ci = opchg_of(k);
-        if (X.objslot[o.obj] != key + 1)
-            atomicMin(&sh.errkey, err_key((uint32_t)(key >> 32), (uint32_t)key + 1, ci, HM_ERR_DUPLICATE_OBJECT));
+        if (X.objslot[o.obj] != key_of(k, ci) + 1)
+            atomicMin(&sh.errkey, err_key((uint32_t)hist_of(ci), k - op0_of(ci) + 1, ci, HM_ERR_DUPLICATE_OBJECT));
         else X.objtype[o.obj] = o.action;
     }
     bsync();
     // per-register assign lists (set/del/link/inc; segk = op index | inc << 31), used by the
     // survivor test and by the tie positions; per-actor maxima only for long lists
-    for (uint32_t i = tid; i < R; i += LWG) X.segoff[i] = X.segcnt[i];
+    for (uint32_t i = tid; i < R; i += LWG) {
+        const uint32_t c = X.segcnt[i];
+        X.segoff[i] = c;
+        if (c > SEG_SHORT) for (uint32_t a = 0; a < A; a++) X.segmax[(size_t)i * A + a] = 0;
+    }
     bsync();
     uint32_t tot2;
     scan_array(sh, X.segoff, R, &tot2);
     for (uint32_t k = tid; k < m; k += LWG) {
-        const hm_op_row o = OP[k];
-        if (o.action < HM_SET || o.action > HM_INC || o.reg >= R || o.obj >= O) continue;   // exactly the ops segcnt counted
+        const OpC o = op_c(k);
+        if (o.action < HM_SET || o.action > HM_INC || o.obj >= O) continue;   // exactly the ops segcnt counted
         const uint32_t ci = opchg_of(k);
-        const int32_t h = hist_of(ci);
-        if (h < 0) continue;
+        if (hist_of(ci) < 0) continue;
         const uint32_t q = X.segoff[o.reg] + g_add(&X.segfill[o.reg], 1u);
-        X.seglist[q] = ((u64)h << 32) | (k - op0_of(ci));
+        X.seglist[q] = key_of(k, ci);
         X.segk[q] = k | (o.action == HM_INC ? 0x80000000u : 0u);
         if (o.action != HM_INC && X.segcnt[o.reg] > SEG_SHORT)
             for (uint32_t a = 0; a < A; a++) {
@@ -892,35 +932,36 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
     }
     bsync();
     LSTAMP(13);
+    // survivors, listed as (op, slot in its register) pairs: survk / survp[0 .. nsurv)
     bool any_list = false;
     for (uint32_t k = tid; k < m; k += LWG) {
-        const hm_op_row o = OP[k];
-        X.survp[k] = 0xFFFFFFFFu;                             // survivor slot (or none)
-        if (o.action < HM_INS || o.action > HM_INC || o.reg >= R) continue;
+        const OpC o = op_c(k);
+        if (o.action < HM_INS || o.action > HM_INC) continue;
         const uint32_t ci = opchg_of(k);
         const int32_t h = hist_of(ci);
         if (h < 0) continue;
-        const u64 key = ((u64)h << 32) | (k - op0_of(ci));
-        const u64 os = o.obj < O ? X.objslot[o.obj] : ~0ull;
-        if (os == ~0ull || os > key) {
-            atomicMin(&sh.errkey, err_key((uint32_t)(key >> 32), (uint32_t)key + 1, ci, HM_ERR_UNKNOWN_OBJECT));
+        const uint32_t kx = k - op0_of(ci), key = kb_of(ci) + kx;
+        const uint32_t os = o.obj < O ? X.objslot[o.obj] : 0xFFFFFFFFu;
+        if (os == 0xFFFFFFFFu || os > key) {
+            atomicMin(&sh.errkey, err_key((uint32_t)h, kx + 1, ci, HM_ERR_UNKNOWN_OBJECT));
             continue;
         }
         const uint32_t ot = X.objtype[o.obj];
         const bool is_list = ot == HM_MAKE_LIST || ot == HM_MAKE_TEXT;
         if (o.action == HM_INS) {
             any_list = true;
+            const uint32_t parent = OP[k].parent;
             if (X.insmin[o.reg] != key + 1)
-                atomicMin(&sh.errkey, err_key((uint32_t)(key >> 32), (uint32_t)key + 1, ci, HM_ERR_DUPLICATE_ELEM));
+                atomicMin(&sh.errkey, err_key((uint32_t)h, kx + 1, ci, HM_ERR_DUPLICATE_ELEM));
             // engine envelope, ordered like a throw: insert after an element not yet inserted
-            if (o.parent != HM_HEAD && !(X.insmin[o.parent] <= key))
-                atomicMin(&sh.errkey, err_key((uint32_t)(key >> 32), (uint32_t)key + 1, ci, HM_ERR_UNSUPPORTED));
+            if (parent != HM_HEAD && !(X.insmin[parent] <= key))
+                atomicMin(&sh.errkey, err_key((uint32_t)h, kx + 1, ci, HM_ERR_UNSUPPORTED));
             continue;
         }
         any_list |= is_list;
         if (o.action == HM_SET || o.action == HM_LINK) {
             if (is_list && !(X.insmin[o.reg] <= key))
-                atomicMin(&sh.errkey, err_key((uint32_t)(key >> 32), (uint32_t)key + 1, ci, HM_ERR_MISSING_ELEM));
+                atomicMin(&sh.errkey, err_key((uint32_t)h, kx + 1, ci, HM_ERR_MISSING_ELEM));
             // survivor: no set/del/link on the register has this op's change among its allDeps
             const uint32_t ao = act_of(ci), so = seq_of(ci), cnt = X.segcnt[o.reg];
             bool surv = true;
@@ -932,12 +973,17 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
                     if (!(e >> 31) && ad_of(opchg_of(e & 0x7FFFFFFFu), ao) >= so) surv = false;
                 }
             }
-            if (surv) X.survp[k] = g_add(&X.survcnt[o.reg], 1u);
+            if (surv) {
+                const uint32_t slot = g_add(&X.survcnt[o.reg], 1u);
+                const uint32_t j = atomicAdd(&sh.nsurv, 1u);
+                X.survk[j] = k; X.survp[j] = slot;
+            }
         }
     }
     if (any_list) sh.lists = 1;
     bsync();
     const bool lists_flag = sh.lists != 0;
+    const uint32_t nsurv = sh.nsurv;
     if (sh.errkey != ~0ull) return LERR;
     if (sh.flags) return LUNSUP;
     LSTAMP(4);
@@ -947,45 +993,50 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
     uint32_t total;
     scan_array(sh, X.regoff, R, &total);
     if (tid == 0) sh.total = total;
-    for (uint32_t k = tid; k < m; k += LWG)
-        if (X.survp[k] != 0xFFFFFFFFu) X.survtmp[X.regoff[OP[k].reg] + X.survp[k]] = k;
+    for (uint32_t j = tid; j < nsurv; j += LWG) {
+        const uint32_t k = X.survk[j];
+        X.survtmp[X.regoff[op_c(k).reg] + X.survp[j]] = k;
+    }
     bsync();
     // ranks: actor descending; ties (one change) by the sortBy(actor).reverse() flip
-    for (uint32_t k = tid; k < m; k += LWG) {
-        if (X.survp[k] == 0xFFFFFFFFu) continue;
-        const hm_op_row o = OP[k];
+    for (uint32_t j = tid; j < nsurv; j += LWG) {
+        const uint32_t k = X.survk[j];
+        const uint32_t reg = op_c(k).reg;
         const uint32_t my_a = act_of(opchg_of(k));
-        const uint32_t b0 = X.regoff[o.reg], cnt = X.survcnt[o.reg];
-        const bool odd_n = X.segcnt[o.reg] & 1;
-        auto tkey = [&](uint32_t kk) -> uint32_t {
-            uint32_t pc = 0;
-            const u64 key = X.opkey[kk];
-            for (uint32_t q = 0; q < X.segcnt[o.reg]; q++) pc += X.seglist[X.segoff[o.reg] + q] < key ? 1u : 0u;
-            return (pc & 1) ? (0x80000000u - pc) : (0x80000000u + pc);
-        };
-        uint32_t rank = 0, my_t = 0;
-        bool have_t = false;
-        for (uint32_t q = 0; q < cnt; q++) {
-            const uint32_t k2 = X.survtmp[b0 + q];
-            if (k2 == k) continue;
-            const uint32_t a2 = act_of(opchg_of(k2));
-            if (a2 > my_a) rank++;
-            else if (a2 == my_a) {
-                if (!have_t) { my_t = tkey(k); have_t = true; }
-                const uint32_t t2 = tkey(k2);
-                if (odd_n ? (t2 > my_t) : (t2 < my_t)) rank++;
+        const uint32_t b0 = X.regoff[reg], cnt = X.survcnt[reg];
+        uint32_t rank = 0;
+        if (cnt > 1) {
+            const uint32_t nseg = X.segcnt[reg], sb = X.segoff[reg];
+            const bool odd_n = nseg & 1;
+            auto tkey = [&](uint32_t kk) -> uint32_t {
+                uint32_t pc = 0;
+                const uint32_t key = key_of(kk, opchg_of(kk));
+                for (uint32_t q = 0; q < nseg; q++) pc += X.seglist[sb + q] < key ? 1u : 0u;
+                return (pc & 1) ? (0x80000000u - pc) : (0x80000000u + pc);
+            };
+            uint32_t my_t = 0;
+            bool have_t = false;
+            for (uint32_t q = 0; q < cnt; q++) {
+                const uint32_t k2 = X.survtmp[b0 + q];
+                if (k2 == k) continue;
+                const uint32_t a2 = act_of(opchg_of(k2));
+                if (a2 > my_a) rank++;
+                else if (a2 == my_a) {
+                    if (!have_t) { my_t = tkey(k); have_t = true; }
+                    const uint32_t t2 = tkey(k2);
+                    if (odd_n ? (t2 > my_t) : (t2 < my_t)) rank++;
+                }
             }
         }
         X.survop[b0 + rank] = k;
-        X.survsum[b0 + rank] = 0;
-        X.survabs[b0 + rank] = 0;
+        if (ctrs) { X.survsum[b0 + rank] = 0; X.survabs[b0 + rank] = 0; }
     }
     bsync();
     LSTAMP(5);
     // counters
-    for (uint32_t k = tid; k < m; k += LWG) {
+    for (uint32_t k = tid; ctrs && k < m; k += LWG) {
         const hm_op_row o = OP[k];
-        if (X.opkey[k] == ~0ull || o.action != HM_INC || o.reg >= R) continue;
+        if (o.action != HM_INC || o.reg >= R || hist_of(opchg_of(k)) < 0) continue;
         const uint32_t ci = opchg_of(k);
         const uint32_t b0 = X.regoff[o.reg], cnt = X.survcnt[o.reg];
         for (uint32_t q = 0; q < cnt; q++) {
@@ -1008,7 +1059,7 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
     // position, op index) — one thread per survivor, the next inc found by a min-scan of the
     // register's assign list (seglist keys).  Integer + integer adds stay int64 until the first
     // non-integral operand; from there on the value is an IEEE double, as the JS sum is.
-    for (uint32_t q = tid; q < total; q += LWG) {
+    for (uint32_t q = tid; ctrs && q < total; q += LWG) {
         if (!(X.survabs[q] & ORDERED)) continue;
         const uint32_t k2 = X.survop[q];
         const hm_op_row o2 = OP[k2];
@@ -1016,21 +1067,21 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
         const uint32_t b0 = X.segoff[reg], cnt = X.segcnt[reg];
         bool is_int = o2.vtag == HM_V_INT;
         u64 acc = o2.value;
-        u64 prev = 0;
+        uint32_t prev = 0;
         bool first = true;
         for (;;) {
-            u64 best = ~0ull;
+            uint32_t best = 0xFFFFFFFFu;
             uint32_t bk = 0;
             for (uint32_t e = 0; e < cnt; e++) {
                 const uint32_t sk = X.segk[b0 + e];
                 if (!(sk & 0x80000000u)) continue;                             // incs only
-                const u64 key = X.seglist[b0 + e];
+                const uint32_t key = X.seglist[b0 + e];
                 if ((!first && key <= prev) || key >= best) continue;
                 const uint32_t ki = sk & 0x7FFFFFFFu;
                 if (ad_of(opchg_of(ki), a2) < s2) continue;                    // concurrent inc: no effect
                 best = key; bk = ki;
             }
-            if (best == ~0ull) break;
+            if (best == 0xFFFFFFFFu) break;
             const hm_op_row oi = OP[bk];
             if (is_int && oi.vtag == HM_V_INT) {
                 acc = (u64)((int64_t)acc + (int64_t)oi.value);
@@ -1062,13 +1113,16 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
         // per node: its register and compact list id (survtmp / segk are free after the ranks)
         // per node i: its register in survtmp[i], its compact list id in segk[i] (both free after the ranks)
         for (uint32_t k = tid; k < m; k += LWG) {
-            const hm_op_row o = OP[k];
-            if (o.action != HM_INS || hist_of(opchg_of(k)) < 0) continue;
+            const OpC c = op_c(k);
+            if (c.action != HM_INS) continue;
+            const uint32_t ci = opchg_of(k);
+            if (hist_of(ci) < 0) continue;
+            const uint32_t parent = OP[k].parent, elem = OP[k].elem;
             const uint32_t i = atomicAdd(&sh.nins, 1u);
-            const uint32_t pi = o.parent == HM_HEAD ? R + o.obj : o.parent;
-            X.nodeop[i] = k; X.nodepi[i] = pi; X.survtmp[i] = o.reg; X.segk[i] = X.listid[o.obj];
-            X.nodekey[i] = ((u64)o.elem << 8) | act_of(opchg_of(k));
-            X.regnode[o.reg] = i;
+            const uint32_t pi = parent == HM_HEAD ? R + c.obj : parent;
+            X.nodepi[i] = pi; X.survtmp[i] = c.reg; X.segk[i] = X.listid[c.obj];
+            X.nodekey[i] = (elem << 8) | act_of(ci);                        // elem < 2^24 (op scan)
+            X.regnode[c.reg] = i;
             g_add(&X.pcount[pi], 1u);
         }
         bsync();
@@ -1086,11 +1140,11 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
         for (uint32_t i = tid; i < N; i += LWG) {
             const uint32_t pi = X.nodepi[i], np = X.pcount[pi];
             if (np == 1) { X.ns[i] = 0xFFFFFFFFu; X.fc[pi] = i; continue; }
-            const u64 key = X.nodekey[i];
-            uint32_t best = 0xFFFFFFFFu; u64 bkey = 0; bool firstc = true;
+            const uint32_t key = X.nodekey[i];
+            uint32_t best = 0xFFFFFFFFu, bkey = 0; bool firstc = true;
             for (uint32_t q = 0; q < np; q++) {
                 const uint32_t j = X.plist[X.poff[pi] + q];
-                const u64 kj = X.nodekey[j];
+                const uint32_t kj = X.nodekey[j];
                 if (kj > key) firstc = false;
                 else if (kj < key && (best == 0xFFFFFFFFu || kj > bkey)) { best = j; bkey = kj; }
             }
@@ -1164,7 +1218,7 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
             const uint32_t ps = X.listbase[l] + total_l - tsum(2 * i);
             X.pos[i] = ps;
             X.vis[ps] = X.survcnt[rg] > 0 ? 1u : 0u;
-            X.insmin[rg] = 0xFFFFFFFFull;                        // -> list index or -1
+            X.insmin[rg] = 0xFFFFFFFFu;                          // -> list index or -1
         }
         bsync();
         // exclusive scan of visibility over pre-order positions, kept in survp (free now)
@@ -1185,11 +1239,12 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
         const uint32_t k = X.survop[q];
         const hm_op_row o = OP[k];
         hm_surv_result sr; sr.op = k; sr.vtag = o.vtag; sr.value = o.value;
-        if (X.survabs[q] & ORDERED) {
+        const u64 sabs = ctrs ? X.survabs[q] : 0ull;
+        if (sabs & ORDERED) {
             sr.vtag = HM_V_FLOAT; sr.value = (u64)X.survsum[q];
         } else if (o.action == HM_SET && o.datatype == HM_DT_COUNTER && o.vtag == HM_V_INT) {
             const int64_t b = (int64_t)o.value;
-            if (X.survabs[q] + (u64)(b < 0 ? -b : b) > (1ull << 53)) atomicOr(&sh.flags, LF_UNSUPPORTED);
+            if (sabs + (u64)(b < 0 ? -b : b) > (1ull << 53)) atomicOr(&sh.flags, LF_UNSUPPORTED);
             sr.value = (u64)(b + X.survsum[q]);
         }
         p.res_surv[doc.op_off + q] = sr;
@@ -1198,7 +1253,7 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
         hm_reg_result rr;
         rr.n_surv = X.survcnt[r]; rr.surv_off = X.regoff[r]; rr.obj = X.regobj[r];
         // list elements carry their visible index (or -1) in insmin after L4
-        rr.list_index = (lists_flag && X.regnode[r] != 0xFFFFFFFFu && X.insmin[r] != 0xFFFFFFFFull) ? (int32_t)X.insmin[r] : -1;
+        rr.list_index = (lists_flag && X.regnode[r] != 0xFFFFFFFFu && X.insmin[r] != 0xFFFFFFFFu) ? (int32_t)X.insmin[r] : -1;
         p.res_regs[doc.reg_off + r] = rr;
     }
     for (uint32_t i = tid; i < n; i += LWG) p.res_hist[doc.change_off + i] = X.hist[i];
@@ -1306,6 +1361,6 @@ extern "C" int hm_debug_lstamps(unsigned long long *out, int n, int reset) {
 
 hipError_t hm_launch_large(const SmallParams &p, void *pool, size_t pool_bytes, unsigned long long *pool_used,
                            uint32_t grid, hipStream_t s) {
-    hipLaunchKernelGGL(hml::merge_large_kernel, dim3(grid), dim3(LWG), 0, s, p, (uint8_t *)pool, (u64)pool_bytes, pool_used);
+    hipLaunchKernelGGL(hml::merge_large_kernel, dim3(grid / 4 * HML_WGS_PER_CU), dim3(LWG), 0, s, p, (uint8_t *)pool, (u64)pool_bytes, pool_used);
     return hipGetLastError();
 }
