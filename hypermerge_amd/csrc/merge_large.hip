@@ -90,6 +90,7 @@ __device__ __forceinline__ u64 err_key(uint32_t h, uint32_t op_plus1, uint32_t a
 struct Shared {
     uint32_t base[LA_MAX], maxs[LA_MAX], tabo[LA_MAX + 1], clock[LA_MAX], bclock[LA_MAX], headv[LA_MAX];
     uint32_t maxad[LA_MAX];
+    uint32_t oslot[LA_MAX], otype[LA_MAX];   // objslot / objtype of documents with <= LA_MAX objects
     uint32_t flags, all_ok, H, nins, nl, total, lists, grew, nmake, nodup, ctrs, nsurv;
     u64 errkey;
     uint32_t scan[LWG / 64 + 1];
@@ -138,8 +139,8 @@ __device__ void scan_array(Shared &sh, uint32_t *arr, uint32_t N, uint32_t *tota
 
 struct Scratch {
     GLB uint32_t *tab, *h2a, *opchg, *segmax, *segcnt, *survcnt, *regoff, *regobj, *segoff, *segfill;
-    GLB uint32_t *survtmp, *segk, *survop, *survp, *objtype, *listid, *nodepi, *regnode, *pcount, *poff;
-    GLB uint32_t *pfill, *plist, *fc, *ns, *tour0, *tour1, *tval0, *tval1, *listbase, *pos, *vis;
+    GLB uint32_t *survtmp, *segk, *survop, *survp, *objtype, *listid, *nodepi, *nreg, *nlist, *regnode, *pcount, *poff;
+    GLB uint32_t *pfill, *plist, *fc, *ns, *tour0, *tour1, *tval0, *tval1, *listbase, *vis;
     GLB int32_t *hist;
     GLB uint32_t *insmin, *objslot, *seglist, *nodekey, *kbase, *survk;   // 32-bit op keys (L3)
     GLB u64 *survabs;
@@ -160,11 +161,11 @@ __host__ __device__ inline size_t large_carve(uintptr_t base, uint32_t n, uint32
     TK(segmax, uint32_t, (size_t)R * A); TK(segcnt, uint32_t, R); TK(survcnt, uint32_t, R);
     TK(regoff, uint32_t, R); TK(regobj, uint32_t, R); TK(segoff, uint32_t, R); TK(segfill, uint32_t, R);
     TK(survtmp, uint32_t, m); TK(segk, uint32_t, m); TK(survop, uint32_t, m); TK(survp, uint32_t, m); TK(objtype, uint32_t, O);
-    TK(listid, uint32_t, O); TK(nodepi, uint32_t, m); TK(regnode, uint32_t, R);
+    TK(listid, uint32_t, O); TK(nodepi, uint32_t, m); TK(nreg, uint32_t, m); TK(nlist, uint32_t, m); TK(regnode, uint32_t, R);
     TK(pcount, uint32_t, NP); TK(poff, uint32_t, NP); TK(pfill, uint32_t, NP); TK(plist, uint32_t, m);
     TK(fc, uint32_t, NP); TK(ns, uint32_t, m); TK(tour0, uint32_t, NE); TK(tour1, uint32_t, NE);
     TK(tval0, uint32_t, NE); TK(tval1, uint32_t, NE);
-    TK(listbase, uint32_t, O + 1); TK(pos, uint32_t, m); TK(vis, uint32_t, m);
+    TK(listbase, uint32_t, O + 1); TK(vis, uint32_t, m);
     TK(hx, uint32_t, 6 * (size_t)n + 1 + T);
 #undef TK
     return o;
@@ -834,9 +835,22 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
     LDS uint32_t *l_hist = ar, *l_act = ar + n, *l_seq = ar + 2 * n, *l_op0 = ar + 3 * n, *l_kb = ar + 4 * n,
                  *l_ad = ar + 5 * n, *l_op = ar + l3_words;
     LDS uint16_t *l_opchg = (LDS uint16_t *)(ar + 5 * n + n * A);
-    for (uint32_t i = tid; i < O; i += LWG) { X.objslot[i] = i == 0 ? 0u : 0xFFFFFFFFu; X.objtype[i] = i == 0 ? HM_MAKE_MAP : 0xFFu; }
+    // object tables in LDS when they fit (text / list documents have a handful of objects)
+    const bool obj_lds = O <= LA_MAX;
+    auto oslot_get = [&](uint32_t o) -> uint32_t { return obj_lds ? sh.oslot[o] : X.objslot[o]; };
+    auto otype_get = [&](uint32_t o) -> uint32_t { return obj_lds ? sh.otype[o] : X.objtype[o]; };
+    for (uint32_t i = tid; i < O; i += LWG) {
+        const uint32_t sl = i == 0 ? 0u : 0xFFFFFFFFu, ty = i == 0 ? (uint32_t)HM_MAKE_MAP : 0xFFu;
+        if (obj_lds) { sh.oslot[i] = sl; sh.otype[i] = ty; } else { X.objslot[i] = sl; X.objtype[i] = ty; }
+    }
+    // RGA nodes are allocated by the op scan when the encoder's hint says the document has
+    // lists (HM_DOC_HAS_LISTS), otherwise by a pass of their own in L4 (either way exact)
+    const bool early = (doc.flags & HM_DOC_HAS_LISTS) != 0;
+    const uint32_t NP = R + O;
+    if (early) for (uint32_t i = tid; i < NP; i += LWG) { X.pcount[i] = 0; X.pfill[i] = 0; X.fc[i] = 0xFFFFFFFFu; }
     for (uint32_t i = tid; i < R; i += LWG) {
         X.segcnt[i] = 0; X.survcnt[i] = 0; X.insmin[i] = 0xFFFFFFFFu; X.regobj[i] = HM_NONE; X.segfill[i] = 0;
+        if (early) X.regnode[i] = 0xFFFFFFFFu;
     }
     if (tid == 0) { sh.nmake = 0; sh.nsurv = 0; }
     for (uint32_t i = tid; i < n; i += LWG) {
@@ -884,13 +898,23 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
         if (h < 0) continue;
         const uint32_t key = key_of(k, ci);
         if (o.action <= HM_MAKE_TEXT) {
-            g_min(&X.objslot[o.obj], key + 1);
+            if (obj_lds) atomicMin(&sh.oslot[o.obj], key + 1); else g_min(&X.objslot[o.obj], key + 1);
             X.survtmp[atomicAdd(&sh.nmake, 1u)] = k;              // make-op list (survtmp is free until L3 offsets)
         } else {
             if (o.obj >= O) continue;                              // an unknown object: the survivor pass throws
             X.regobj[o.reg] = o.obj;
-            if (o.action == HM_INS) { g_min(&X.insmin[o.reg], key + 1); if (o.elem >= (1u << 24)) atomicOr(&sh.flags, LF_UNSUPPORTED); }
-            else g_add(&X.segcnt[o.reg], 1u);
+            if (o.action == HM_INS) {
+                g_min(&X.insmin[o.reg], key + 1);
+                if (o.elem >= (1u << 24)) atomicOr(&sh.flags, LF_UNSUPPORTED);
+                if (early) {
+                    const uint32_t i = atomicAdd(&sh.nins, 1u);
+                    const uint32_t pi = o.parent == HM_HEAD ? R + o.obj : o.parent;
+                    X.nodepi[i] = pi; X.nreg[i] = o.reg; X.nlist[i] = o.obj;     // nlist: object -> list id in L4
+                    X.nodekey[i] = (o.elem << 8) | act_of(ci);
+                    X.regnode[o.reg] = i;
+                    g_add(&X.pcount[pi], 1u);
+                }
+            } else g_add(&X.segcnt[o.reg], 1u);
         }
     }
     bsync();
@@ -901,8 +925,9 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
         const uint32_t k = X.survtmp[q];
         const OpC o = op_c(k);
         const uint32_t ci = opchg_of(k);
-        if (X.objslot[o.obj] != key_of(k, ci) + 1)
+        if (oslot_get(o.obj) != key_of(k, ci) + 1)
             atomicMin(&sh.errkey, err_key((uint32_t)hist_of(ci), k - op0_of(ci) + 1, ci, HM_ERR_DUPLICATE_OBJECT));
+        else if (obj_lds) sh.otype[o.obj] = o.action;
         else X.objtype[o.obj] = o.action;
     }
     bsync();
@@ -941,12 +966,12 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
         const int32_t h = hist_of(ci);
         if (h < 0) continue;
         const uint32_t kx = k - op0_of(ci), key = kb_of(ci) + kx;
-        const uint32_t os = o.obj < O ? X.objslot[o.obj] : 0xFFFFFFFFu;
+        const uint32_t os = o.obj < O ? oslot_get(o.obj) : 0xFFFFFFFFu;
         if (os == 0xFFFFFFFFu || os > key) {
             atomicMin(&sh.errkey, err_key((uint32_t)h, kx + 1, ci, HM_ERR_UNKNOWN_OBJECT));
             continue;
         }
-        const uint32_t ot = X.objtype[o.obj];
+        const uint32_t ot = otype_get(o.obj);
         const bool is_list = ot == HM_MAKE_LIST || ot == HM_MAKE_TEXT;
         if (o.action == HM_INS) {
             any_list = true;
@@ -1103,29 +1128,31 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
     LSTAMP(6);
     // ---- L4: RGA order ----
     if (lists_flag) {
-        const uint32_t NP = R + O;
-        for (uint32_t i = tid; i < NP; i += LWG) { X.pcount[i] = 0; X.pfill[i] = 0; X.fc[i] = 0xFFFFFFFFu; }
-        for (uint32_t i = tid; i < R; i += LWG) X.regnode[i] = 0xFFFFFFFFu;
-        for (uint32_t i = tid; i < O; i += LWG) X.listid[i] = (X.objtype[i] == HM_MAKE_LIST || X.objtype[i] == HM_MAKE_TEXT) ? 1u : 0u;
+        if (!early) {
+            for (uint32_t i = tid; i < NP; i += LWG) { X.pcount[i] = 0; X.pfill[i] = 0; X.fc[i] = 0xFFFFFFFFu; }
+            for (uint32_t i = tid; i < R; i += LWG) X.regnode[i] = 0xFFFFFFFFu;
+        }
+        for (uint32_t i = tid; i < O; i += LWG) { const uint32_t t = otype_get(i); X.listid[i] = (t == HM_MAKE_LIST || t == HM_MAKE_TEXT) ? 1u : 0u; }
         bsync();
         uint32_t nl;
         scan_array(sh, X.listid, O, &nl);          // exclusive prefix -> compact list id (valid for list objects)
-        // per node: its register and compact list id (survtmp / segk are free after the ranks)
-        // per node i: its register in survtmp[i], its compact list id in segk[i] (both free after the ranks)
-        for (uint32_t k = tid; k < m; k += LWG) {
-            const OpC c = op_c(k);
-            if (c.action != HM_INS) continue;
-            const uint32_t ci = opchg_of(k);
-            if (hist_of(ci) < 0) continue;
-            const uint32_t parent = OP[k].parent, elem = OP[k].elem;
-            const uint32_t i = atomicAdd(&sh.nins, 1u);
-            const uint32_t pi = parent == HM_HEAD ? R + c.obj : parent;
-            X.nodepi[i] = pi; X.survtmp[i] = c.reg; X.segk[i] = X.listid[c.obj];
-            X.nodekey[i] = (elem << 8) | act_of(ci);                        // elem < 2^24 (op scan)
-            X.regnode[c.reg] = i;
-            g_add(&X.pcount[pi], 1u);
+        // per node i: its register nreg[i], its compact list id nlist[i], parent slot, sibling key
+        if (!early) {
+            for (uint32_t k = tid; k < m; k += LWG) {
+                const OpC c = op_c(k);
+                if (c.action != HM_INS) continue;
+                const uint32_t ci = opchg_of(k);
+                if (hist_of(ci) < 0) continue;
+                const uint32_t parent = OP[k].parent, elem = OP[k].elem;
+                const uint32_t i = atomicAdd(&sh.nins, 1u);
+                const uint32_t pi = parent == HM_HEAD ? R + c.obj : parent;
+                X.nodepi[i] = pi; X.nreg[i] = c.reg; X.nlist[i] = X.listid[c.obj];
+                X.nodekey[i] = (elem << 8) | act_of(ci);                    // elem < 2^24 (op scan)
+                X.regnode[c.reg] = i;
+                g_add(&X.pcount[pi], 1u);
+            }
+            bsync();
         }
-        bsync();
         const uint32_t N = sh.nins;
         for (uint32_t i = tid; i < NP; i += LWG) X.poff[i] = X.pcount[i];
         bsync();
@@ -1135,6 +1162,7 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
         for (uint32_t i = tid; i < N; i += LWG) {
             const uint32_t pi = X.nodepi[i];
             if (X.pcount[pi] > 1) X.plist[X.poff[pi] + g_add(&X.pfill[pi], 1u)] = i;
+            if (early) X.nlist[i] = X.listid[X.nlist[i]];
         }
         bsync();
         for (uint32_t i = tid; i < N; i += LWG) {
@@ -1165,14 +1193,15 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
             else { nx0[e] = nx; va0[e] = va; }
         };
         for (uint32_t i = tid; i < N; i += LWG) {
-            const uint32_t hd = N + X.segk[i];
-            const uint32_t f = X.fc[X.survtmp[i]];
+            const uint32_t hd = N + X.nlist[i];
+            const uint32_t f = X.fc[X.nreg[i]];
             const uint32_t pi = X.nodepi[i];
             put(2 * i, f != 0xFFFFFFFFu ? 2 * f : 2 * i + 1, 1);
             put(2 * i + 1, X.ns[i] != 0xFFFFFFFFu ? 2 * X.ns[i] : (pi >= R ? 2 * hd + 1 : 2 * X.regnode[pi] + 1), 0);
         }
         for (uint32_t o = tid; o < O; o += LWG) {
-            if (!(X.objtype[o] == HM_MAKE_LIST || X.objtype[o] == HM_MAKE_TEXT)) continue;
+            const uint32_t t = otype_get(o);
+            if (!(t == HM_MAKE_LIST || t == HM_MAKE_TEXT)) continue;
             const uint32_t h = N + X.listid[o], f = X.fc[R + o];
             put(2 * h, f != 0xFFFFFFFFu ? 2 * f : 2 * h + 1, 0);
             put(2 * h + 1, END, 0);
@@ -1206,29 +1235,23 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
         // tour sums (entries from here to the end of the list): LDS words or the pool array
         auto tsum = [&](uint32_t e) -> uint32_t { return tour_lds ? (tw[e] & 0xFFFFu) : va0[e]; };
         for (uint32_t o = tid; o < O; o += LWG) {
-            const bool isl = X.objtype[o] == HM_MAKE_LIST || X.objtype[o] == HM_MAKE_TEXT;
+            const uint32_t t = otype_get(o);
+            const bool isl = t == HM_MAKE_LIST || t == HM_MAKE_TEXT;
             if (isl) X.listbase[X.listid[o]] = tsum(2 * (N + X.listid[o]));
         }
         bsync();
         uint32_t tl;
         scan_array(sh, X.listbase, nl, &tl);
-        for (uint32_t i = tid; i < N; i += LWG) {
-            const uint32_t l = X.segk[i], rg = X.survtmp[i];
-            const uint32_t total_l = tsum(2 * (N + l));
-            const uint32_t ps = X.listbase[l] + total_l - tsum(2 * i);
-            X.pos[i] = ps;
-            X.vis[ps] = X.survcnt[rg] > 0 ? 1u : 0u;
-            X.insmin[rg] = 0xFFFFFFFFu;                          // -> list index or -1
-        }
-        bsync();
-        // exclusive scan of visibility over pre-order positions, kept in survp (free now)
-        for (uint32_t i = tid; i < N; i += LWG) X.survp[i] = X.vis[i];
+        // pre-order position of node i: its list's base + (entries of its list) - (entries from i on)
+        auto pos_of = [&](uint32_t i, uint32_t l) -> uint32_t { return X.listbase[l] + tsum(2 * (N + l)) - tsum(2 * i); };
+        for (uint32_t i = tid; i < N; i += LWG) X.vis[pos_of(i, X.nlist[i])] = X.survcnt[X.nreg[i]] > 0 ? 1u : 0u;
         bsync();
         uint32_t tv;
-        scan_array(sh, X.survp, N, &tv);
+        scan_array(sh, X.vis, N, &tv);             // exclusive scan of visibility over pre-order positions
         for (uint32_t i = tid; i < N; i += LWG) {
-            const uint32_t ps = X.pos[i];
-            if (X.vis[ps]) X.insmin[X.survtmp[i]] = X.survp[ps] - X.survp[X.listbase[X.segk[i]]];
+            const uint32_t l = X.nlist[i], rg = X.nreg[i];
+            // list elements carry their visible index (or -1) in insmin from here on
+            X.insmin[rg] = X.survcnt[rg] > 0 ? X.vis[pos_of(i, l)] - X.vis[X.listbase[l]] : 0xFFFFFFFFu;
         }
         bsync();
     }
@@ -1361,6 +1384,9 @@ extern "C" int hm_debug_lstamps(unsigned long long *out, int n, int reset) {
 
 hipError_t hm_launch_large(const SmallParams &p, void *pool, size_t pool_bytes, unsigned long long *pool_used,
                            uint32_t grid, hipStream_t s) {
-    hipLaunchKernelGGL(hml::merge_large_kernel, dim3(grid / 4 * HML_WGS_PER_CU), dim3(LWG), 0, s, p, (uint8_t *)pool, (u64)pool_bytes, pool_used);
+#ifndef HML_RESIDENT
+#define HML_RESIDENT HML_WGS_PER_CU    // workgroups launched per CU (dev A/B builds launch fewer)
+#endif
+    hipLaunchKernelGGL(hml::merge_large_kernel, dim3(grid / 4 * HML_RESIDENT), dim3(LWG), 0, s, p, (uint8_t *)pool, (u64)pool_bytes, pool_used);
     return hipGetLastError();
 }

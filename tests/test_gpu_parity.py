@@ -98,6 +98,17 @@ def test_general_kernel_on_small_docs(engine_general, name, n, extra):
     assert_same(b, engine_general.merge(b), O.merge(b, threads=8))
 
 
+@pytest.mark.parametrize("name,n,extra", [
+    ("C3", 60, {}), ("C3", 30, {"arrival": 2, "shuffle_pct": 20, "dup_pct": 3}), ("C5", 1000, {}),
+])
+def test_general_kernel_without_list_hint(engine_general, name, n, extra):
+    """HM_DOC_HAS_LISTS is a launch hint only: without it the general kernel allocates RGA nodes
+    in a pass of their own instead of in the op scan, with the same results."""
+    b = synth.generate(synth.config(name, n_docs=n, **extra))
+    b.docs["flags"] &= ~np.uint16(1)
+    assert_same(b, engine_general.merge(b), O.merge(b, threads=8))
+
+
 @pytest.mark.parametrize("name,changes,expect", CASES, ids=[c[0] for c in CASES])
 def test_known_answers_general_kernel(engine_general, name, changes, expect):
     b = encode([changes])
