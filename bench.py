@@ -345,9 +345,15 @@ def _incremental(eng, batch, args, tail=4):
     from hypermerge_amd.store import BatchResult
     from hypermerge_amd.columnar import DOC_RESULT_DT
     S = batch.a_stride
-    # result arrays kept between rounds, as a long-running RepoBackend keeps its buffers
-    outs = [BatchResult(np.zeros(n, DOC_RESULT_DT), np.zeros((n, S), np.uint32), np.zeros((n, S), np.uint32),
-                        np.zeros((n, S), np.uint32)) for _ in stores]
+    # result arrays kept between rounds, as a long-running RepoBackend keeps its buffers (page-locked,
+    # so the per-round D2H runs at DMA speed)
+    import torch
+
+    def pinned(shape, dt):
+        nb = int(np.prod(shape)) * np.dtype(dt).itemsize
+        return torch.zeros(max(nb, 1), dtype=torch.uint8, pin_memory=True).numpy()[:nb].view(dt).reshape(shape)
+    outs = [BatchResult(pinned((n,), DOC_RESULT_DT), pinned((n, S), np.uint32), pinned((n, S), np.uint32),
+                        pinned((n, S), np.uint32)) for _ in stores]
     pos = start.copy()
     rounds = []
     same = True

@@ -88,7 +88,6 @@ struct hm_store {
     // allocate and first-touch ~130 MB every round)
     std::vector<AppendDesc> descs;
     std::vector<uint32_t> grow;
-    std::vector<uint8_t> bail;
     // incremental applyRemoteChanges (inc_apply_kernel) and the last submit's routing
     bool incremental = true;
     uint32_t st_inc = 0, st_cold = 0, st_bail = 0;
@@ -199,7 +198,7 @@ StageLayout layout(size_t nc, size_t nd, size_t no, size_t ndesc, size_t nremap,
     L.o_docs = o; o += al(nmerge * sizeof(hm_doc_row) + 1);
     L.o_hand = o; o += al(nmerge * 4 + 1);
     L.o_gather = o; o += al(ngather * (sizeof(hm_doc_result) + 3 * 4 * (size_t)S) + 1);
-    L.o_bail = o; o += al(ninc + 1);
+    L.o_bail = o; o += al(4 * (ninc + 1));
     L.total = o;
     return L;
 }
@@ -455,6 +454,7 @@ int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
                 if (r) return r;
             }
         }
+        T.mark("plan: sizes");
         s->p_old.resize(n);
         s->p_inv_row.resize(n);
         s->p_inv.clear();
@@ -501,6 +501,7 @@ int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
             }
             for (int k = 0; k < 4; k++) base[4 * (t + 1) + k] = acc[k];
         });
+        T.mark("plan: grow");
         base[0] = s->used_c; base[1] = s->used_d; base[2] = s->used_o; base[3] = s->used_r;
         for (uint32_t t = 1; t <= TT; t++) for (int k = 0; k < 4; k++) base[4 * t + k] += base[4 * (t - 1) + k];
         s->used_c = base[4 * TT]; s->used_d = base[4 * TT + 1]; s->used_o = base[4 * TT + 2]; s->used_r = base[4 * TT + 3];
@@ -511,7 +512,7 @@ int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
         std::vector<Part> parts(16);
         par_for(n, [&](uint32_t lo, uint32_t hi, uint32_t t) {
             size_t at[4] = {base[4 * t], base[4 * t + 1], base[4 * t + 2], base[4 * t + 3]};
-            Part &P = parts[t];
+            Part P;                                                   // thread-local (no false sharing)
             for (uint32_t i = lo; i < hi; i++) {
                 const uint32_t h = doc_handles[i];
                 DocMeta &m = s->docs[h];
@@ -549,7 +550,9 @@ int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
                                        std::min<uint32_t>(r.n_ops, HM_INC_SLOTS)};
                 for (int k = 0; k < 6; k++) P.mx[k] = std::max(P.mx[k], v[k]);
             }
+            parts[t] = std::move(P);
         });
+        T.mark("plan: route");
         std::vector<uint32_t> cold;
         uint32_t n_inc = 0, mx[6] = {0, 0, 0, 0, 0, 0};
         for (auto &P : parts) {
@@ -568,6 +571,7 @@ int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
         if (b->n_deps) SCHK(s, hipMemcpyAsync(sp + L.o_dp, b->deps, b->n_deps * sizeof(hm_dep_row), hipMemcpyHostToDevice, st));
         if (b->n_ops) SCHK(s, hipMemcpyAsync(sp + L.o_op, b->ops, b->n_ops * sizeof(hm_op_row), hipMemcpyHostToDevice, st));
         if (n) SCHK(s, hipMemcpyAsync(sp + L.o_desc, descs.data(), n * sizeof(AppendDesc), hipMemcpyHostToDevice, st));
+        T.mark("stage: h2d");
         if (!remap_rows.empty()) SCHK(s, hipMemcpyAsync(sp + L.o_remap, remap_rows.data(), remap_rows.size(), hipMemcpyHostToDevice, st));
         StoreArenas ar = {s->changes, s->deps, s->ops, s->min_clock, s->stored};
         SCHK(s, hm_launch_append((const AppendDesc *)(sp + L.o_desc), n, ar, ar, (const hm_change_row *)(sp + L.o_ch),
@@ -578,7 +582,7 @@ int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
             const IncDims M = hm_inc_dims(S, mx_new_c, mx_tgt, mx_stage, mx_regs, mx_surv, mx_slots);
             IncArenas A = {s->changes, s->deps, s->ops, s->hist, s->all_deps, s->regs, s->surv,
                            s->res_docs, s->clock, s->back_clock, s->heads, s->min_clock};
-            SCHK(s, hm_launch_inc_apply((const AppendDesc *)(sp + L.o_desc), n, A, M, sp + L.o_bail, st));
+            SCHK(s, hm_launch_inc_apply((const AppendDesc *)(sp + L.o_desc), n, A, M, (uint32_t *)(sp + L.o_bail), st));
         }
         T.mark("incremental");
         rc = launch_store_merge(s, cold, sp + L.o_docs, (uint32_t *)(sp + L.o_hand));
@@ -587,12 +591,15 @@ int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
         s->st_inc = n_inc; s->st_cold = (uint32_t)cold.size(); s->st_bail = 0;
         if (n_inc) {
             // documents the incremental kernel handed back re-merge their whole log
-            s->bail.resize(n);
-            std::vector<uint8_t> &bail = s->bail;
-            SCHK(s, hipMemcpyAsync(bail.data(), sp + L.o_bail, n, hipMemcpyDeviceToHost, st));
+            uint32_t nb = 0;
+            SCHK(s, hipMemcpyAsync(&nb, sp + L.o_bail, 4, hipMemcpyDeviceToHost, st));
             SCHK(s, hipStreamSynchronize(st));
-            std::vector<uint32_t> again;
-            for (uint32_t i = 0; i < n; i++) if (descs[i].inc && bail[i]) again.push_back(descs[i].handle);
+            std::vector<uint32_t> again(nb);
+            if (nb) {
+                SCHK(s, hipMemcpyAsync(again.data(), sp + L.o_bail + 4, (size_t)nb * 4, hipMemcpyDeviceToHost, st));
+                SCHK(s, hipStreamSynchronize(st));
+                std::sort(again.begin(), again.end());
+            }
             s->st_bail = (uint32_t)again.size(); s->st_inc -= s->st_bail;
             rc = launch_store_merge(s, again, sp + L.o_docs, (uint32_t *)(sp + L.o_hand));
             if (rc) return rc;

@@ -59,7 +59,7 @@ IncDims hm_inc_dims(uint32_t S, uint32_t new_c, uint32_t tgt, uint32_t stage, ui
                     uint32_t slots);
 
 hipError_t hm_launch_inc_apply(const AppendDesc *descs, uint32_t n, const IncArenas &A, const IncDims &M,
-                               uint8_t *bail, hipStream_t s);
+                               uint32_t *bail, hipStream_t s);
 hipError_t hm_launch_append(const AppendDesc *descs, uint32_t n_desc, const StoreArenas &src, const StoreArenas &dst,
                             const hm_change_row *st_changes, const hm_dep_row *st_deps, const hm_op_row *st_ops,
                             const uint8_t *remap, uint32_t S, hipStream_t s);

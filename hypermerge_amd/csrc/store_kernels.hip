@@ -160,7 +160,7 @@ __global__ void sync_ranges_kernel(const uint64_t *present, const uint64_t *word
 // pushed, sortBy(actor).reverse() — only the registers the new ops hit are recomputed; the
 // rest of the register table is repacked as it was.  Anything outside that (a duplicate or
 // not-yet-ready change, inc / counter / list / object-creation ops, an unknown object, tiles
-// too small) sets bail[i] before any merged state is written, and the host re-merges that
+// too small) lists the document in bail before any merged state is written, and the host re-merges that
 // document's whole log with the batch kernels.  The loads that depend only on the
 // descriptor (new rows, clock / heads, the old log's (actor, seq) keys, the register table,
 // the survivors) are issued together; the remaining dependent steps are one scan of the log
@@ -486,15 +486,16 @@ __device__ bool inc_doc(const AppendDesc &D, const IncArenas &A, const IncDims &
     return true;
 }
 
+// bail[0] = count, bail[1 ..] = the handles handed back (any order)
 __global__ __launch_bounds__(64, 8) void inc_apply_kernel(const AppendDesc *descs, uint32_t n, IncArenas A, IncDims M,
-                                                       uint8_t *bail) {
+                                                       uint32_t *bail) {
     extern __shared__ __align__(16) uint8_t inc_lds[];
     const uint32_t lane = threadIdx.x;
     for (uint32_t di = blockIdx.x; di < n; di += gridDim.x) {
         if (!descs[di].inc) continue;
         const AppendDesc D = descs[di];
         const bool ok = inc_doc(D, A, M, lane, inc_lds);
-        if (lane == 0) bail[di] = ok ? 0 : 1;
+        if (lane == 0 && !ok) bail[1 + atomicAdd(&bail[0], 1u)] = D.handle;
         __syncthreads();
     }
 }
@@ -553,8 +554,10 @@ IncDims hm_inc_dims(uint32_t S, uint32_t new_c, uint32_t tgt, uint32_t stage, ui
 }
 
 hipError_t hm_launch_inc_apply(const AppendDesc *descs, uint32_t n, const IncArenas &A, const IncDims &M,
-                               uint8_t *bail, hipStream_t s) {
+                               uint32_t *bail, hipStream_t s) {
     if (!n) return hipSuccess;
+    hipError_t z = hipMemsetAsync(bail, 0, 4, s);
+    if (z != hipSuccess) return z;
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&hms::inc_apply_kernel),

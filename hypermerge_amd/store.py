@@ -425,15 +425,15 @@ class RowStore(DocStore):
         bid = ctypes.c_uint64()
         self._check(self._L.hm_batch_submit(self._h, ctypes.byref(cb), _p(hs), None, ctypes.byref(bid)),
                     "hm_batch_submit")
-        self._pending = (bid.value, list(range(len(hs))), None, keep)
+        self._pending = (bid.value, len(hs), None, keep)
         return bid.value
 
     def wait(self, out: Optional[BatchResult] = None) -> BatchResult:
         """Results of the submitted batch; `out` (arrays of at least the batch's size, e.g. kept
         between rounds by a long-running host) is filled instead of fresh arrays."""
-        bid, handles, _, _ = self._pending
+        bid, n, _, _ = self._pending
         self._pending = None
-        n, S = len(handles), self.S
+        S = self.S
         if out is not None and len(out.docs) >= n:
             r = BatchResult(out.docs[:n], out.clock[:n], out.back_clock[:n], out.heads[:n])
         else:
