@@ -22,6 +22,9 @@
 #include <cstdint>
 #include <cstring>
 #include <deque>
+#include <chrono>
+#include <cstdio>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <string>
@@ -783,11 +786,21 @@ bool decode_doc(const uint8_t *data, const uint64_t *block_off, uint32_t b0, uin
 
 }  // namespace
 
+// a table of POD rows written once by the decoder threads (no zero fill before they write it)
+template <typename T> struct Rows {
+    std::unique_ptr<T[]> p;
+    size_t n = 0;
+    void alloc(size_t k) { p.reset(k ? new T[k] : nullptr); n = k; }
+    T *data() { return p.get(); }
+    const T *data() const { return p.get(); }
+    size_t size() const { return n; }
+};
+
 struct hm_decoded {
     std::vector<hm_doc_row> docs;
-    std::vector<hm_change_row> ch;
-    std::vector<hm_dep_row> dp;
-    std::vector<hm_op_row> op;
+    Rows<hm_change_row> ch;
+    Rows<hm_dep_row> dp;
+    Rows<hm_op_row> op;
     std::vector<int32_t> status;
     std::vector<std::string> strings;
     std::vector<std::vector<std::string>> actors, objs;
@@ -802,6 +815,7 @@ int hm_decode_blocks(const uint8_t *data, const uint64_t *block_off, const uint3
     if (!out || (n_docs && (!block_off || !doc_block))) return HM_ERR_INVALID;
     *out = nullptr;
     try {
+        const auto t_start = std::chrono::steady_clock::now();
         std::vector<DocOut> docs(n_docs);
         const int T = std::max(1, std::min(threads, 256));
         auto work = [&](uint32_t lo, uint32_t hi) {
@@ -823,56 +837,92 @@ int hm_decode_blocks(const uint8_t *data, const uint64_t *block_off, const uint3
             }
             for (auto &x : th) x.join();
         }
+        const auto t_par = std::chrono::steady_clock::now();
         hm_decoded *D = new hm_decoded();
+        std::unique_ptr<hm_decoded> own(D);
+        // the batch's string pool, in document order (columnar.js StringPool over documents):
+        // the one serial step; every document's local string ids -> pool ids in `remap`
         Intern pool;
         pool.reset(1024);
-        size_t nc = 0, nd = 0, no = 0;
-        for (auto &x : docs) { nc += x.ch.size(); nd += x.dp.size(); no += x.op.size(); }
-        D->docs.resize(n_docs); D->ch.reserve(nc); D->dp.reserve(nd); D->op.reserve(no);
-        D->status.resize(n_docs); D->actors.resize(n_docs); D->objs.resize(n_docs); D->regs.resize(n_docs);
-        uint32_t reg_off = 0, maxa = 1;
-        std::vector<uint32_t> remap;
+        std::vector<uint64_t> roff(n_docs + 1, 0);
+        for (uint32_t d = 0; d < n_docs; d++) roff[d + 1] = roff[d] + docs[d].strings.size();
+        std::vector<uint32_t> remap(roff[n_docs]);
         for (uint32_t d = 0; d < n_docs; d++) {
             DocOut &x = docs[d];
-            // the batch's string pool, in document order (columnar.js StringPool over documents)
-            remap.resize(x.strings.size());
             for (size_t i = 0; i < x.strings.size(); i++) {
                 bool fresh;
                 const std::string &t = x.strings[i];
-                remap[i] = pool.get(SV{t.data(), (uint32_t)t.size()}, 0, fresh);
+                remap[roff[d] + i] = pool.get(SV{t.data(), (uint32_t)t.size()}, 0, fresh);
                 if (fresh) D->strings.push_back(t);
             }
+        }
+        // document rows and table offsets (prefix over documents), then the rows themselves are
+        // copied by the threads, each into its documents' ranges
+        D->docs.resize(n_docs);
+        D->status.resize(n_docs); D->actors.resize(n_docs); D->objs.resize(n_docs); D->regs.resize(n_docs);
+        uint64_t nc = 0, nd = 0, no = 0;
+        uint32_t reg_off = 0, maxa = 1;
+        for (uint32_t d = 0; d < n_docs; d++) {
+            const DocOut &x = docs[d];
             hm_doc_row &r = D->docs[d];
             r = hm_doc_row{};
-            r.change_off = (uint32_t)D->ch.size(); r.n_changes = (uint32_t)x.ch.size();
-            r.dep_off = (uint32_t)D->dp.size(); r.n_deps = (uint32_t)x.dp.size();
-            r.op_off = (uint32_t)D->op.size(); r.n_ops = (uint32_t)x.op.size();
+            r.change_off = (uint32_t)nc; r.n_changes = (uint32_t)x.ch.size();
+            r.dep_off = (uint32_t)nd; r.n_deps = (uint32_t)x.dp.size();
+            r.op_off = (uint32_t)no; r.n_ops = (uint32_t)x.op.size();
             r.reg_off = reg_off; r.n_regs = x.n_regs; r.n_objs = x.n_objs;
             r.n_actors = (uint16_t)x.actors.size(); r.flags = x.flags;
-            for (hm_change_row c : x.ch) { c.dep_off += r.dep_off; c.op_first += r.op_off; D->ch.push_back(c); }
-            D->dp.insert(D->dp.end(), x.dp.begin(), x.dp.end());
-            for (size_t i = 0; i < x.op.size(); i++) {
-                hm_op_row o = x.op[i];
-                if (x.op_str_key[i]) o.key = remap[o.key];
-                if (x.op_str_val[i]) o.value = remap[(size_t)o.value];
-                D->op.push_back(o);
-            }
+            nc += x.ch.size(); nd += x.dp.size(); no += x.op.size();
             reg_off += x.n_regs;
             D->status[d] = x.status;
-            D->actors[d] = std::move(x.actors);
-            D->objs[d] = std::move(x.objs);
-            D->regs[d] = std::move(x.regs);
             maxa = std::max<uint32_t>(maxa, r.n_actors);
             D->max_changes = std::max(D->max_changes, r.n_changes); D->max_ops = std::max(D->max_ops, r.n_ops);
             D->max_regs = std::max(D->max_regs, r.n_regs); D->max_objs = std::max(D->max_objs, r.n_objs);
             D->max_deps = std::max(D->max_deps, r.n_deps); D->doc_flags |= r.flags;
-            DocOut().ch.swap(x.ch);
+        }
+        D->ch.alloc(nc); D->dp.alloc(nd); D->op.alloc(no);
+        auto place = [&](uint32_t lo, uint32_t hi) {
+            for (uint32_t d = lo; d < hi; d++) {
+                DocOut &x = docs[d];
+                const hm_doc_row &r = D->docs[d];
+                hm_change_row *ch = D->ch.data() + r.change_off;
+                for (size_t i = 0; i < x.ch.size(); i++) {
+                    hm_change_row c = x.ch[i];
+                    c.dep_off += r.dep_off; c.op_first += r.op_off;
+                    ch[i] = c;
+                }
+                if (!x.dp.empty()) memcpy(D->dp.data() + r.dep_off, x.dp.data(), x.dp.size() * sizeof(hm_dep_row));
+                hm_op_row *op = D->op.data() + r.op_off;
+                const uint32_t *rm = remap.data() + roff[d];
+                for (size_t i = 0; i < x.op.size(); i++) {
+                    hm_op_row o = x.op[i];
+                    if (x.op_str_key[i]) o.key = rm[o.key];
+                    if (x.op_str_val[i]) o.value = rm[(size_t)o.value];
+                    op[i] = o;
+                }
+                D->actors[d] = std::move(x.actors);
+                D->objs[d] = std::move(x.objs);
+                D->regs[d] = std::move(x.regs);
+                DocOut().ch.swap(x.ch);
+            }
+        };
+        if (T == 1 || n_docs < 2) place(0, n_docs);
+        else {
+            std::vector<std::thread> th;
+            for (int t = 0; t < T; t++)
+                th.emplace_back(place, (uint32_t)((uint64_t)n_docs * t / T), (uint32_t)((uint64_t)n_docs * (t + 1) / T));
+            for (auto &x : th) x.join();
+        }
+        if (getenv("HM_DECODE_PROFILE")) {
+            const auto t_end = std::chrono::steady_clock::now();
+            fprintf(stderr, "[hm_decode] parallel %.3f ms  merge %.3f ms\n",
+                    std::chrono::duration<double, std::milli>(t_par - t_start).count(),
+                    std::chrono::duration<double, std::milli>(t_end - t_par).count());
         }
         D->a_stride = a_stride ? a_stride : maxa;
         if (D->a_stride < maxa)
             for (uint32_t d = 0; d < n_docs; d++)
                 if (D->docs[d].n_actors > D->a_stride) D->status[d] = HM_ERR_INVALID;   // the merge rejects the row too
-        *out = D;
+        *out = own.release();
         return HM_OK;
     } catch (...) {
         return HM_ERR_NOMEM;

@@ -36,38 +36,50 @@ def decode_packed(data: np.ndarray, block_off: np.ndarray, doc_block: np.ndarray
                             threads, ctypes.byref(h))
     if st:
         raise RuntimeError(f"hm_decode_blocks: {L.hm_status_message(st).decode()}")
-    try:
-        cb = CBatch()
-        L.hm_decoded_batch(h, ctypes.byref(cb))
+    owner = _Decoded(L, h)
+    cb = CBatch()
+    L.hm_decoded_batch(h, ctypes.byref(cb))
 
-        def take(ptr, n, dt):
-            if n == 0:
-                return np.zeros(0, dt)
-            buf = (ctypes.c_uint8 * (n * dt.itemsize)).from_address(ptr)
-            return np.frombuffer(buf, dt).copy()
-        docs = take(cb.docs, cb.n_docs, DOC_DT)
-        b = Batch(docs, take(cb.changes, cb.n_changes, CHANGE_DT), take(cb.deps, cb.n_deps, DEP_DT),
-                  take(cb.ops, cb.n_ops, OP_DT), int(cb.a_stride))
-        status = np.ctypeslib.as_array(L.hm_decoded_status(h), shape=(max(n_docs, 1),))[:n_docs].copy()
-        ln = ctypes.c_size_t()
+    def take(ptr, n, dt):
+        # the decoder's own row buffers, without a copy: they live until the last array over them
+        if n == 0:
+            return np.zeros(0, dt)
+        buf = (ctypes.c_uint8 * (n * dt.itemsize)).from_address(ptr)
+        buf._owner = owner
+        return np.frombuffer(buf, dt)
+    docs = take(cb.docs, cb.n_docs, DOC_DT)
+    b = Batch(docs, take(cb.changes, cb.n_changes, CHANGE_DT), take(cb.deps, cb.n_deps, DEP_DT),
+              take(cb.ops, cb.n_ops, OP_DT), int(cb.a_stride))
+    status = np.ctypeslib.as_array(L.hm_decoded_status(h), shape=(max(n_docs, 1),))[:n_docs].copy()
+    ln = ctypes.c_size_t()
 
-        def text(p):
-            if not p:
-                raise RuntimeError("hm_decoded_*: index out of range")
-            return ctypes.string_at(p, ln.value).decode("utf-8", "surrogatepass")
-        b.strings = [text(L.hm_decoded_string(h, i, ctypes.byref(ln))) for i in range(L.hm_decoded_n_strings(h))]
-        if not tables:
-            return b, status
-        b.doc_actors = [[text(L.hm_decoded_actor(h, d, r, ctypes.byref(ln))) for r in range(int(docs["n_actors"][d]))]
-                        for d in range(n_docs)]
-        b.doc_objs = [[text(L.hm_decoded_obj(h, d, o, ctypes.byref(ln))) for o in range(int(docs["n_objs"][d]))]
-                      for d in range(n_docs)]
-        ob = ctypes.c_uint32()
-        b.doc_regs = [[(lambda t: (int(ob.value), t))(text(L.hm_decoded_reg(h, d, g, ctypes.byref(ob), ctypes.byref(ln))))
-                       for g in range(int(docs["n_regs"][d]))] for d in range(n_docs)]
+    def text(p):
+        if not p:
+            raise RuntimeError("hm_decoded_*: index out of range")
+        return ctypes.string_at(p, ln.value).decode("utf-8", "surrogatepass")
+    b.strings = [text(L.hm_decoded_string(h, i, ctypes.byref(ln))) for i in range(L.hm_decoded_n_strings(h))]
+    if not tables:
         return b, status
-    finally:
-        L.hm_decoded_free(h)
+    b.doc_actors = [[text(L.hm_decoded_actor(h, d, r, ctypes.byref(ln))) for r in range(int(docs["n_actors"][d]))]
+                    for d in range(n_docs)]
+    b.doc_objs = [[text(L.hm_decoded_obj(h, d, o, ctypes.byref(ln))) for o in range(int(docs["n_objs"][d]))]
+                  for d in range(n_docs)]
+    ob = ctypes.c_uint32()
+    b.doc_regs = [[(lambda t: (int(ob.value), t))(text(L.hm_decoded_reg(h, d, g, ctypes.byref(ob), ctypes.byref(ln))))
+                   for g in range(int(docs["n_regs"][d]))] for d in range(n_docs)]
+    return b, status
+
+
+class _Decoded:
+    """Owns one hm_decoded (its row tables back the batch's arrays)."""
+
+    def __init__(self, L, h):
+        self.L, self.h = L, h
+
+    def __del__(self):
+        if self.h:
+            self.L.hm_decoded_free(self.h)
+            self.h = None
 
 
 def decode_blocks(docs: Sequence[Sequence[bytes]], a_stride: int = 0, threads: int = 16):
