@@ -198,6 +198,11 @@ int hm_engine_create(const hm_config *cfg, hm_engine **out) {
     if (hipSetDevice(e->device) != hipSuccess) { delete e; return HM_ERR_DEVICE; }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, e->device) == hipSuccess) e->num_cus = prop.multiProcessorCount;
+    {
+        size_t lim = 0, need = hm_large_stack_bytes();
+        if (hipDeviceGetLimit(&lim, hipLimitStackSize) == hipSuccess && need > lim &&
+            hipDeviceSetLimit(hipLimitStackSize, need) != hipSuccess) { delete e; return HM_ERR_DEVICE; }
+    }
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { delete e; return HM_ERR_DEVICE; }
     for (auto &ev : e->ev)
         if (hipEventCreate(&ev) != hipSuccess) { delete e; return HM_ERR_DEVICE; }

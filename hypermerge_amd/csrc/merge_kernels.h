@@ -49,6 +49,7 @@ __device__ __forceinline__ uint32_t hm_slot(const SmallParams &p, uint32_t d) { 
 size_t hm_launch_scratch_bytes(const hm_batch *b);
 
 size_t hm_large_scratch_bound(const hm_batch *b);
+size_t hm_large_stack_bytes();
 hipError_t hm_launch_large(const SmallParams &p, void *pool, size_t pool_bytes, unsigned long long *pool_used,
                            uint32_t grid, hipStream_t s);
 // small-kernel size class (LDS carve) for a batch's per-document maxima

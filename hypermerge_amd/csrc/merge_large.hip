@@ -21,14 +21,33 @@
 #include "merge_kernels.h"
 
 #ifndef HML_WGS_PER_CU
-#define HML_WGS_PER_CU 4   // workgroups per CU: 16 waves per CU split into this many documents
+#define HML_WGS_PER_CU 1   // workgroups per CU: 16 waves per CU split into this many documents
 #endif
 #define LWG (1024 / HML_WGS_PER_CU)
 #define LA_MAX 64
-// LDS arena per workgroup (u32 words): 36 KB keeps 4 workgroups per CU (the VGPR-bound
-// occupancy at 128 VGPRs).  Documents whose L2 closure rows (2·n·A + T words) or L4 Euler
-// tour (E words, 16-bit links) fit run those phases out of LDS instead of the pool.
+// LDS arena per workgroup (u32 words).  One 1024-thread workgroup per CU owns 150 KB: a
+// document's whole L3/L4 working set (op words, assign lists, register / node / parent tables,
+// Euler tour) is resident there (l34_res) instead of in the pool, whose per-document tables
+// (~300 KB for a C3 text document) cannot stay in an XCD's 4 MB L2 across its workgroups and
+// were re-fetched from HBM (7.4x the algorithmic bytes).  Documents whose L2 closure rows
+// (2·n·A + T words) or L4 Euler tour (E words, 16-bit links) fit run those phases out of LDS.
+#if HML_WGS_PER_CU == 1
+#define LARENA 38400
+#else
 #define LARENA (36864 / HML_WGS_PER_CU)
+#endif
+#ifndef HML_RES
+#define HML_RES 1       // 0: every document takes the pool L3/L4 (dev A/B builds)
+#endif
+#ifndef HML_STAGE
+#define HML_STAGE 1     // 0: L1/L2 read change / dep rows from HBM and keep the L1 table in the pool (dev A/B)
+#endif
+#ifndef HML_DOC_ATTR
+#define HML_DOC_ATTR __forceinline__
+#endif
+#ifndef HML_RES_ATTR
+#define HML_RES_ATTR __forceinline__
+#endif
 // Explicit address spaces: LDS pointers -> ds_*, pool pointers -> global_* (a generic pointer
 // would compile to flat_* ops, which count against lgkmcnt too, so every LDS wait would also
 // wait for the outstanding pool loads, stores and atomics).
@@ -44,14 +63,7 @@ typedef unsigned long long u64;
 #ifndef HM_PAR_HIST
 #define HM_PAR_HIST 1   // 0: queued documents always take the serial queue emulation (dev A/B builds)
 #endif
-#ifndef HM_PAR_HIST_INLINE
-#define HM_PAR_HIST_INLINE 1
-#endif
-#if HM_PAR_HIST_INLINE
-#define PH_ATTR
-#else
 #define PH_ATTR __noinline__
-#endif
 #ifndef HM_STAMPS
 #define HM_STAMPS 0     // diagnostic builds only: per-phase s_memtime shares (tools/lstamps.py); never timed
 #endif
@@ -91,7 +103,9 @@ struct Shared {
     uint32_t base[LA_MAX], maxs[LA_MAX], tabo[LA_MAX + 1], clock[LA_MAX], bclock[LA_MAX], headv[LA_MAX];
     uint32_t maxad[LA_MAX];
     uint32_t oslot[LA_MAX], otype[LA_MAX];   // objslot / objtype of documents with <= LA_MAX objects
+    uint32_t listid[LA_MAX], listbase[LA_MAX + 1];   // l34_res: compact list ids, list bases
     uint32_t flags, all_ok, H, nins, nl, total, lists, grew, nmake, nodup, ctrs, nsurv;
+    uint32_t gflag[3];
     u64 errkey;
     uint32_t scan[LWG / 64 + 1];
     u64 scratch_base;
@@ -124,7 +138,9 @@ __device__ __forceinline__ uint32_t block_excl_scan(Shared &sh, uint32_t v, uint
 }
 // exclusive scan of arr[0..N) in place: each thread owns a contiguous run of ceil(N / LWG)
 // entries (its loads are independent, so they overlap), one block scan of the run sums
-__device__ void scan_array(Shared &sh, uint32_t *arr, uint32_t N, uint32_t *total) {
+// (P: a pool pointer or an LDS pointer)
+template <typename P>
+__device__ uint32_t scan_array(Shared &sh, P arr, uint32_t N) {
     const uint32_t per = (N + LWG - 1) / LWG;
     const uint32_t b0 = threadIdx.x * per < N ? threadIdx.x * per : N;
     const uint32_t b1 = b0 + per < N ? b0 + per : N;
@@ -133,8 +149,8 @@ __device__ void scan_array(Shared &sh, uint32_t *arr, uint32_t N, uint32_t *tota
     uint32_t tot;
     uint32_t ex = block_excl_scan(sh, sum, &tot);
     for (uint32_t i = b0; i < b1; i++) { const uint32_t v = arr[i]; arr[i] = ex; ex += v; }
-    *total = tot;
     bsync();
+    return tot;
 }
 
 struct Scratch {
@@ -212,16 +228,17 @@ __device__ __forceinline__ uint32_t block_excl_max(Shared &sh, uint32_t v) {
 // order, applying what is ready).  History = applied changes ordered by (t, pass, arr).
 // C(K) comes from pointer jumping over the actor chains (log-depth rounds).  Returns false
 // (block-uniform) when the serial emulation must run instead.
-__device__ PH_ATTR bool parallel_history(const SmallParams &p, Shared &sh, const hm_doc_row &doc, const Scratch &X,
-                                 uint32_t n, uint32_t A, uint32_t T) {
+// (not inlined: it runs for queued documents only; every argument by value, so the caller's
+// parameter block and scratch table stay in registers instead of a stack copy)
+__device__ PH_ATTR bool parallel_history(const hm_change_row *CH, const hm_dep_row *deps, Shared &sh,
+                                         GLB uint32_t *C, GLB uint32_t *hx, GLB uint32_t *tab, GLB uint32_t *h2a,
+                                         GLB int32_t *hist, uint32_t n, uint32_t A, uint32_t T) {
     const uint32_t tid = threadIdx.x;
-    const hm_change_row *CH = p.changes + doc.change_off;
     const uint32_t INF = 0xFFFFFFFFu;
-    GLB uint32_t *C = X.vc;                                   // [n * A] closure clocks (self excluded)
-    // this phase's arrays, from one base (fewer live pointers in the kernel)
+    // C: [n * A] closure clocks (self excluded); this phase's arrays from one base (hx)
     struct { GLB uint32_t *ht, *hp, *hnev, *hfill, *hmem, *hoff, *pm, *tab, *h2a; GLB int32_t *hist; } Y;
-    Y.ht = X.hx; Y.hp = Y.ht + n; Y.hnev = Y.hp + n; Y.hfill = Y.hnev + n; Y.hmem = Y.hfill + n; Y.hoff = Y.hmem + n;
-    Y.pm = Y.hoff + n + 1; Y.tab = X.tab; Y.h2a = X.h2a; Y.hist = X.hist;
+    Y.ht = hx; Y.hp = Y.ht + n; Y.hnev = Y.hp + n; Y.hfill = Y.hnev + n; Y.hmem = Y.hfill + n; Y.hoff = Y.hmem + n;
+    Y.pm = Y.hoff + n + 1; Y.tab = tab; Y.h2a = h2a; Y.hist = hist;
     auto arrival = [&](uint32_t a, uint32_t s) -> uint32_t {  // first arrival of (a, s), or INF
         if (a >= A || s < sh.base[a] || s > sh.maxs[a] || sh.maxs[a] == 0) return INF;
         return Y.tab[sh.tabo[a] + (s - sh.base[a])];
@@ -236,7 +253,7 @@ __device__ PH_ATTR bool parallel_history(const SmallParams &p, Shared &sh, const
         uint32_t nev = c.seq > 1 && arrival(c.actor, c.seq - 1) == INF;
         row[c.actor] = c.seq - 1;
         for (uint32_t j = 0; j < c.n_deps; j++) {
-            const hm_dep_row dp = p.deps[c.dep_off + j];
+            const hm_dep_row dp = deps[c.dep_off + j];
             if (dp.actor == c.actor || dp.seq == 0) continue;
             if (arrival(dp.actor, dp.seq) == INF) nev = 1;
             if (row[dp.actor] < dp.seq) row[dp.actor] = dp.seq;
@@ -323,7 +340,7 @@ __device__ PH_ATTR bool parallel_history(const SmallParams &p, Shared &sh, const
                 if (j < n && Y.ht[j] == t) { const uint32_t v = Y.hp[j] + (j > i ? 1u : 0u); ps = ps > v ? ps : v; }
             };
             for (uint32_t j = 0; j < c.n_deps; j++) {
-                const hm_dep_row dp = p.deps[c.dep_off + j];
+                const hm_dep_row dp = deps[c.dep_off + j];
                 if (dp.actor == c.actor || dp.seq == 0) continue;
                 dep(arrival(dp.actor, dp.seq));
             }
@@ -342,7 +359,7 @@ __device__ PH_ATTR bool parallel_history(const SmallParams &p, Shared &sh, const
     for (uint32_t i = tid; i < n; i += LWG) if (Y.ht[i] != INF) g_add(&Y.hoff[Y.ht[i]], 1u);
     bsync();
     uint32_t Hn;
-    scan_array(sh, Y.hoff, n + 1, &Hn);
+    Hn = scan_array(sh, Y.hoff, n + 1);
     for (uint32_t i = tid; i < n; i += LWG) {
         const uint32_t t = Y.ht[i];
         if (t == INF) continue;
@@ -371,7 +388,354 @@ __device__ PH_ATTR bool parallel_history(const SmallParams &p, Shared &sh, const
     return true;
 }
 
-__device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_t *ar, const hm_doc_row &doc, uint32_t d,
+// ---- L3 + L4 with every table resident in the LDS arena (l34_res) ----
+// The same rules, in the same order of checks, as the pool L3/L4 in merge_doc_large; only the
+// storage differs: 16-bit op / node indices, u8 object ids, assign lists of op indices (keys
+// recomputed from the staged per-change key bases), survivors flagged in a bit set and ranked
+// within their register's assign list.  Envelope (checked before anything is written; outside
+// it the caller runs the pool L3/L4 from its start): A <= 8 (allDeps rows staged), O <= LA_MAX,
+// m < 2^16, R + O < 2^15 (16-bit tour links), no counter ops, assign lists <= RES_SEG_MAX per
+// register, and the layout below fits the arena.
+#define RES_SEG_MAX 64
+#define RES_FALLBACK 3
+__device__ HML_RES_ATTR int l34_res(const SmallParams &p, Shared &sh, LDS uint32_t *ar, const hm_doc_row &doc, const Scratch &X,
+                       uint32_t H) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t n = doc.n_changes, A = doc.n_actors, m = doc.n_ops, R = doc.n_regs, O = doc.n_objs;
+    const hm_change_row *CH = p.changes + doc.change_off;
+    const hm_op_row *OP = p.ops + doc.op_off;
+    const uint32_t NP = R + O;
+    const uint16_t N16 = 0xFFFFu;
+    // ---- layout (words); region S and the survivor list die after the ranks (L4 reuses them) ----
+    uint32_t off = 0;
+    auto w32 = [&](uint32_t cnt) -> LDS uint32_t * { LDS uint32_t *q = ar + off; off += cnt; return q; };
+    auto w16 = [&](uint32_t cnt) -> LDS uint16_t * { LDS uint16_t *q = (LDS uint16_t *)(ar + off); off += (cnt + 1) / 2; return q; };
+    auto w8 = [&](uint32_t cnt) -> LDS uint8_t * { LDS uint8_t *q = (LDS uint8_t *)(ar + off); off += (cnt + 3) / 4; return q; };
+    LDS uint32_t *c_tmp = w32(n), *c_hist = w32(n), *c_act = w32(n), *c_seq = w32(n), *c_op0 = w32(n), *c_kb = w32(n);
+    LDS uint32_t *c_ad = w32(n * A);
+    LDS uint32_t *o_w = w32(m);                 // reg (16) | action (4) << 16 | obj (7, 127 unknown) << 20
+    LDS uint16_t *o_chg = w16(m);               // op -> arrival index of its change
+    LDS uint16_t *a_k = w16(m);                 // assign lists (set/del/link/inc op indices), by register
+    LDS uint16_t *s_list = w16(m);              // make ops, then survivors
+    LDS uint32_t *s_bits = w32(m / 32 + 1);     // survivor flags by op index
+    const uint32_t dead_end = off;              // [0, dead_end) is free once the ranks are done
+    LDS uint32_t *r_ins = w32(R), *r_segcnt = w32(R), *r_seg = w32(R), *r_scnt = w32(R), *r_soff = w32(R);
+    LDS uint8_t *r_obj = w8(R);                 // 0xFF: HM_NONE
+    LDS uint16_t *r_node = w16(R);
+    LDS uint16_t *s_op = w16(m);                // survivors in output order
+    LDS uint16_t *n_pi = w16(R), *n_reg = w16(R), *n_ns = w16(R), *n_pl = w16(R);
+    LDS uint32_t *n_key = w32(R);
+    LDS uint8_t *n_list = w8(R);
+    LDS uint32_t *p_cnt = w32(NP), *p_off = w32(NP);
+    LDS uint16_t *p_fc = w16(NP);
+    const uint32_t tail = off;
+    if (A > 8 || O > LA_MAX || m >= 65536 || NP >= 32767 || n >= 65536 || tail > LARENA) return RES_FALLBACK;
+    auto dec_reg = [](uint32_t w) { return w & 0xFFFFu; };
+    auto dec_act = [](uint32_t w) { return (w >> 16) & 15u; };
+    auto dec_obj = [](uint32_t w) { return (w >> 20) & 127u; };
+    auto key_of = [&](uint32_t k, uint32_t ci) -> uint32_t { return c_kb[ci] + (k - c_op0[ci]); };
+
+    // ---- key bases: ops of the changes before each history position ----
+    for (uint32_t h = tid; h < H; h += LWG) c_tmp[h] = CH[X.h2a[h]].n_ops;
+    bsync();
+    uint32_t m_applied;
+    m_applied = scan_array(sh, c_tmp, H);
+    (void)m_applied;
+    // ---- staging: per-change inputs, op -> change, object / register / parent tables ----
+    for (uint32_t i = tid; i < n; i += LWG) {
+        const hm_change_row c = CH[i];
+        const int32_t hi = X.hist[i];
+        const uint32_t o0 = c.op_first - doc.op_off;
+        c_hist[i] = (uint32_t)hi; c_act[i] = c.actor; c_seq[i] = c.seq; c_op0[i] = o0;
+        c_kb[i] = hi >= 0 ? c_tmp[hi] : 0xFFFFFFFFu;
+        const uint32_t *ad = ad_row(p, doc, i);
+        for (uint32_t a = 0; a < A; a++) c_ad[i * A + a] = ad[a];
+        for (uint32_t j = 0; j < c.n_ops; j++) o_chg[o0 + j] = (uint16_t)i;
+    }
+    for (uint32_t i = tid; i < O; i += LWG) { sh.oslot[i] = i == 0 ? 0u : 0xFFFFFFFFu; sh.otype[i] = i == 0 ? (uint32_t)HM_MAKE_MAP : 0xFFu; }
+    for (uint32_t i = tid; i < R; i += LWG) {
+        r_ins[i] = 0xFFFFFFFFu; r_segcnt[i] = 0; r_scnt[i] = 0; r_obj[i] = 0xFFu; r_node[i] = N16;
+    }
+    for (uint32_t i = tid; i < NP; i += LWG) { p_cnt[i] = 0; p_fc[i] = N16; }
+    for (uint32_t i = tid; i <= m / 32; i += LWG) s_bits[i] = 0;
+    if (tid == 0) { sh.nmake = 0; sh.nsurv = 0; sh.nins = 0; sh.grew = 0; }
+    bsync();
+    LSTAMP(11);
+    // ---- op scan: rows read once from HBM, four per thread in flight ----
+    for (uint32_t k0 = 0; k0 < m; k0 += 4 * LWG) {
+        hm_op_row orow[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) { const uint32_t k = k0 + tid + u * LWG; if (k < m) orow[u] = OP[k]; }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t k = k0 + tid + u * LWG;
+            if (k >= m) continue;
+            const hm_op_row &o = orow[u];
+            const uint32_t ci = o_chg[k];
+            const int32_t h = (int32_t)c_hist[ci];
+            if (o.action == HM_INC || o.datatype == HM_DT_COUNTER) sh.ctrs = 1;
+            const bool bad = o.action <= HM_MAKE_TEXT ? o.obj >= O
+                           : (o.action <= HM_INC ? (o.reg >= R || (o.action == HM_INS && o.parent != HM_HEAD && o.parent >= R)) : true);
+            if (bad) { atomicOr(&sh.flags, LF_UNSUPPORTED); continue; }
+            o_w[k] = (o.action <= HM_MAKE_TEXT ? 0u : o.reg) | ((uint32_t)o.action << 16) | ((o.obj < O ? o.obj : 127u) << 20);
+            if (h < 0) continue;
+            const uint32_t key = key_of(k, ci);
+            if (o.action <= HM_MAKE_TEXT) {
+                atomicMin(&sh.oslot[o.obj], key + 1);
+                s_list[atomicAdd(&sh.nmake, 1u)] = (uint16_t)k;
+            } else {
+                if (o.obj >= O) continue;                          // an unknown object: the survivor pass throws
+                r_obj[o.reg] = (uint8_t)o.obj;
+                if (o.action == HM_INS) {
+                    atomicMin(&r_ins[o.reg], key + 1);
+                    if (o.elem >= (1u << 24)) atomicOr(&sh.flags, LF_UNSUPPORTED);
+                    const uint32_t i = atomicAdd(&sh.nins, 1u);
+                    if (i < R) {                                   // more inserts than registers: a duplicate throws
+                        const uint32_t pi = o.parent == HM_HEAD ? R + o.obj : o.parent;
+                        n_pi[i] = (uint16_t)pi; n_reg[i] = (uint16_t)o.reg; n_list[i] = (uint8_t)o.obj;
+                        n_key[i] = (o.elem << 8) | c_act[ci];
+                        r_node[o.reg] = (uint16_t)i;
+                        atomicAdd(&p_cnt[pi], 1u);
+                    }
+                } else if (atomicAdd(&r_segcnt[o.reg], 1u) >= RES_SEG_MAX) sh.grew = 1;   // a long assign list
+            }
+        }
+    }
+    bsync();
+    LSTAMP(12);
+    if (sh.flags) return LUNSUP;
+    {
+        // counters, long assign lists, or a tour that does not fit over the dead region: pool path
+        const uint32_t N = sh.nins < R ? sh.nins : R;
+        const bool out = sh.ctrs || sh.grew || 2 * (N + O) + N > dead_end;
+        bsync();
+        if (out) {
+            if (tid == 0) { sh.nins = 0; sh.ctrs = 0; }
+            bsync();
+            return RES_FALLBACK;
+        }
+    }
+    // ---- objects: the earliest make op creates, later ones throw ----
+    for (uint32_t q = tid; q < sh.nmake; q += LWG) {
+        const uint32_t k = s_list[q], w = o_w[k], ci = o_chg[k], obj = dec_obj(w);
+        if (sh.oslot[obj] != key_of(k, ci) + 1)
+            atomicMin(&sh.errkey, err_key(c_hist[ci], k - c_op0[ci] + 1, ci, HM_ERR_DUPLICATE_OBJECT));
+        else sh.otype[obj] = dec_act(w);
+    }
+    // ---- assign lists: r_seg = exclusive offsets, advanced to the segment ends by the fill ----
+    for (uint32_t i = tid; i < R; i += LWG) r_seg[i] = r_segcnt[i];
+    bsync();
+    uint32_t tot2;
+    tot2 = scan_array(sh, r_seg, R);
+    for (uint32_t k = tid; k < m; k += LWG) {
+        const uint32_t w = o_w[k], a = dec_act(w);
+        if (a < HM_SET || a > HM_INC || dec_obj(w) >= O) continue;     // exactly the ops r_segcnt counted
+        if ((int32_t)c_hist[o_chg[k]] < 0) continue;
+        a_k[atomicAdd(&r_seg[dec_reg(w)], 1u)] = (uint16_t)k;
+    }
+    bsync();
+    LSTAMP(13);
+    // ---- survivors and per-op checks ----
+    bool any_list = false;
+    for (uint32_t k = tid; k < m; k += LWG) {
+        const uint32_t w = o_w[k], a = dec_act(w), obj = dec_obj(w), reg = dec_reg(w);
+        if (a < HM_INS || a > HM_INC) continue;
+        const uint32_t ci = o_chg[k];
+        const int32_t h = (int32_t)c_hist[ci];
+        if (h < 0) continue;
+        const uint32_t kx = k - c_op0[ci], key = c_kb[ci] + kx;
+        const uint32_t os = obj < O ? sh.oslot[obj] : 0xFFFFFFFFu;
+        if (os == 0xFFFFFFFFu || os > key) {
+            atomicMin(&sh.errkey, err_key((uint32_t)h, kx + 1, ci, HM_ERR_UNKNOWN_OBJECT));
+            continue;
+        }
+        const uint32_t ot = sh.otype[obj];
+        const bool is_list = ot == HM_MAKE_LIST || ot == HM_MAKE_TEXT;
+        if (a == HM_INS) {
+            any_list = true;
+            const uint32_t parent = OP[k].parent;
+            if (r_ins[reg] != key + 1) atomicMin(&sh.errkey, err_key((uint32_t)h, kx + 1, ci, HM_ERR_DUPLICATE_ELEM));
+            if (parent != HM_HEAD && !(r_ins[parent] <= key))
+                atomicMin(&sh.errkey, err_key((uint32_t)h, kx + 1, ci, HM_ERR_UNSUPPORTED));
+            continue;
+        }
+        any_list |= is_list;
+        if (a == HM_SET || a == HM_LINK) {
+            if (is_list && !(r_ins[reg] <= key)) atomicMin(&sh.errkey, err_key((uint32_t)h, kx + 1, ci, HM_ERR_MISSING_ELEM));
+            // survivor: no set/del/link on the register has this op's change among its allDeps
+            const uint32_t ao = c_act[ci], so = c_seq[ci], cnt = r_segcnt[reg], e0 = r_seg[reg] - cnt;
+            bool surv = true;
+            for (uint32_t q = 0; q < cnt; q++) {
+                const uint32_t e = a_k[e0 + q];
+                if (dec_act(o_w[e]) != HM_INC && c_ad[o_chg[e] * A + ao] >= so) surv = false;
+            }
+            if (surv) {
+                atomicAdd(&r_scnt[reg], 1u);
+                atomicOr(&s_bits[k >> 5], 1u << (k & 31));
+                s_list[atomicAdd(&sh.nsurv, 1u)] = (uint16_t)k;
+            }
+        }
+    }
+    if (any_list) sh.lists = 1;
+    bsync();
+    const bool lists_flag = sh.lists != 0;
+    const uint32_t nsurv = sh.nsurv;
+    if (sh.errkey != ~0ull) return LERR;
+    if (sh.flags) return LUNSUP;
+    LSTAMP(4);
+    // ---- survivor offsets and ranks: actor descending; equal actors (one change) by the
+    //      sortBy(actor).reverse() flip, from the assigns applied on the register before each ----
+    for (uint32_t i = tid; i < R; i += LWG) r_soff[i] = r_scnt[i];
+    bsync();
+    uint32_t total;
+    total = scan_array(sh, r_soff, R);
+    for (uint32_t j = tid; j < nsurv; j += LWG) {
+        const uint32_t k = s_list[j], reg = dec_reg(o_w[k]), ck = o_chg[k], my_a = c_act[ck];
+        const uint32_t cnt = r_scnt[reg];
+        uint32_t rank = 0;
+        if (cnt > 1) {
+            const uint32_t nseg = r_segcnt[reg], sb = r_seg[reg] - nseg;
+            const bool odd_n = nseg & 1;
+            auto tkey = [&](uint32_t kk) -> uint32_t {
+                uint32_t pc = 0;
+                const uint32_t key = key_of(kk, o_chg[kk]);
+                for (uint32_t q = 0; q < nseg; q++) { const uint32_t e = a_k[sb + q]; pc += key_of(e, o_chg[e]) < key ? 1u : 0u; }
+                return (pc & 1) ? (0x80000000u - pc) : (0x80000000u + pc);
+            };
+            uint32_t my_t = 0;
+            bool have_t = false;
+            for (uint32_t q = 0; q < nseg; q++) {
+                const uint32_t k2 = a_k[sb + q];
+                if (k2 == k || !((s_bits[k2 >> 5] >> (k2 & 31)) & 1)) continue;
+                const uint32_t a2 = c_act[o_chg[k2]];
+                if (a2 > my_a) rank++;
+                else if (a2 == my_a) {
+                    if (!have_t) { my_t = tkey(k); have_t = true; }
+                    const uint32_t t2 = tkey(k2);
+                    if (odd_n ? (t2 > my_t) : (t2 < my_t)) rank++;
+                }
+            }
+        }
+        s_op[r_soff[reg] + rank] = (uint16_t)k;
+    }
+    bsync();
+    LSTAMP(5);
+    // ---- L4: RGA order (Euler tour over the insertion tree, pointer jumping) ----
+    if (lists_flag) {
+        if (tid < 64) {                                            // compact list ids over <= 64 objects
+            const uint32_t t = tid < O ? sh.otype[tid] : 0xFFu;
+            const bool isl = t == HM_MAKE_LIST || t == HM_MAKE_TEXT;
+            const u64 bm = __ballot(isl);
+            sh.listid[tid] = (uint32_t)__popcll(bm & ((1ull << tid) - 1));
+            if (tid == 0) sh.total = (uint32_t)__popcll(bm);
+        }
+        const uint32_t N = sh.nins;
+        for (uint32_t i = tid; i < NP; i += LWG) p_off[i] = p_cnt[i];
+        bsync();
+        const uint32_t nl = sh.total;
+        uint32_t tp;
+        tp = scan_array(sh, p_off, NP);
+        for (uint32_t i = tid; i < N; i += LWG) {
+            const uint32_t pi = n_pi[i];
+            if (p_cnt[pi] > 1) n_pl[atomicAdd(&p_off[pi], 1u)] = (uint16_t)i;
+            n_list[i] = (uint8_t)sh.listid[n_list[i]];
+        }
+        bsync();
+        // siblings: lamport (elem, actor) descending; an only child needs no list
+        for (uint32_t i = tid; i < N; i += LWG) {
+            const uint32_t pi = n_pi[i], np = p_cnt[pi];
+            if (np == 1) { n_ns[i] = N16; p_fc[pi] = (uint16_t)i; continue; }
+            const uint32_t key = n_key[i], b0 = p_off[pi] - np;
+            uint32_t best = 0xFFFFFFFFu, bkey = 0;
+            bool firstc = true;
+            for (uint32_t q = 0; q < np; q++) {
+                const uint32_t j = n_pl[b0 + q], kj = n_key[j];
+                if (kj > key) firstc = false;
+                else if (kj < key && (best == 0xFFFFFFFFu || kj > bkey)) { best = j; bkey = kj; }
+            }
+            n_ns[i] = best == 0xFFFFFFFFu ? N16 : (uint16_t)best;
+            if (firstc) p_fc[pi] = (uint16_t)i;
+        }
+        bsync();
+        LSTAMP(7);
+        // tour words (next << 16 | value, END 0xFFFF) over the dead region, then the visibility array
+        const uint32_t E = 2 * (N + nl);
+        LDS uint32_t *tw = ar, *vis = ar + E;
+        for (uint32_t i = tid; i < N; i += LWG) {
+            const uint32_t hd = N + n_list[i], f = p_fc[n_reg[i]], pi = n_pi[i], ns = n_ns[i];
+            tw[2 * i] = ((f != N16 ? 2 * f : 2 * i + 1) << 16) | 1u;
+            tw[2 * i + 1] = (ns != N16 ? 2 * ns : (pi >= R ? 2 * hd + 1 : 2 * (uint32_t)r_node[pi] + 1)) << 16;
+        }
+        for (uint32_t o = tid; o < O; o += LWG) {
+            const uint32_t t = sh.otype[o];
+            if (!(t == HM_MAKE_LIST || t == HM_MAKE_TEXT)) continue;
+            const uint32_t h = N + sh.listid[o], f = p_fc[R + o];
+            tw[2 * h] = (f != N16 ? 2 * f : 2 * h + 1) << 16;
+            tw[2 * h + 1] = 0xFFFF0000u;
+        }
+        bsync();
+        const uint32_t rounds = E ? 32 - __builtin_clz(E) : 0;
+        for (uint32_t rd = 0; rd < rounds; rd++) {
+            for (uint32_t e = tid; e < E; e += LWG) {
+                const uint32_t w = tw[e], x = w >> 16;
+                if (x == 0xFFFFu) continue;
+                const uint32_t w2 = tw[x];
+                tw[e] = (w2 & 0xFFFF0000u) | ((w & 0xFFFFu) + (w2 & 0xFFFFu));
+            }
+            bsync();
+        }
+        LSTAMP(8);
+        auto tsum = [&](uint32_t e) -> uint32_t { return tw[e] & 0xFFFFu; };
+        if (tid < 64) {                                            // list bases: exclusive scan over list ids
+            const uint32_t t = tid < O ? sh.otype[tid] : 0xFFu;
+            const bool isl = t == HM_MAKE_LIST || t == HM_MAKE_TEXT;
+            const uint32_t len = isl ? tsum(2 * (N + sh.listid[tid])) : 0u;
+            uint32_t x = len;          // inclusive scan over lanes in object order = list-id order
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((tid >= (uint32_t)o ? tid - o : tid) << 2), (int)x);
+                if (tid >= (uint32_t)o) x += y;
+            }
+            if (isl) sh.listbase[sh.listid[tid]] = x - len;
+        }
+        bsync();
+        auto pos_of = [&](uint32_t i, uint32_t l) -> uint32_t { return sh.listbase[l] + tsum(2 * (N + l)) - tsum(2 * i); };
+        for (uint32_t i = tid; i < N; i += LWG) vis[pos_of(i, n_list[i])] = r_scnt[n_reg[i]] > 0 ? 1u : 0u;
+        bsync();
+        uint32_t tv;
+        tv = scan_array(sh, vis, N);
+        for (uint32_t i = tid; i < N; i += LWG) {
+            const uint32_t l = n_list[i], rg = n_reg[i];
+            r_ins[rg] = r_scnt[rg] > 0 ? vis[pos_of(i, l)] - vis[sh.listbase[l]] : 0xFFFFFFFFu;
+        }
+        bsync();
+    }
+    LSTAMP(9);
+    // ---- outputs ----
+    for (uint32_t q = tid; q < total; q += LWG) {
+        const uint32_t k = s_op[q];
+#ifdef HML_DEBUG
+        if (k >= m) { printf("RES bad s_op doc %u q %u total %u k %u m %u nsurv %u n %u H %u\n", doc.reserved[0], q, total, k, m, nsurv, n, H); continue; }
+#endif
+        const hm_op_row o = OP[k];
+        hm_surv_result sr; sr.op = k; sr.vtag = o.vtag; sr.value = o.value;
+        p.res_surv[doc.op_off + q] = sr;
+    }
+    for (uint32_t r = tid; r < R; r += LWG) {
+        hm_reg_result rr;
+        rr.n_surv = r_scnt[r]; rr.surv_off = r_soff[r];
+        rr.obj = r_obj[r] == 0xFFu ? HM_NONE : (uint32_t)r_obj[r];
+        rr.list_index = (lists_flag && r_node[r] != N16 && r_ins[r] != 0xFFFFFFFFu) ? (int32_t)r_ins[r] : -1;
+        p.res_regs[doc.reg_off + r] = rr;
+    }
+    for (uint32_t i = tid; i < n; i += LWG) p.res_hist[doc.change_off + i] = X.hist[i];
+    if (tid == 0) sh.total = total;
+    bsync();
+    LSTAMP(10);
+    if (sh.flags) return LUNSUP;
+    return LOK;
+}
+
+__device__ HML_DOC_ATTR Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_t *ar, const hm_doc_row &doc, uint32_t d,
                                    uint8_t *pool, u64 pool_bytes, u64 *pool_used, int32_t &H_out) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t n = doc.n_changes, A = doc.n_actors, m = doc.n_ops, R = doc.n_regs, O = doc.n_objs;
@@ -386,8 +750,22 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
     if (tid == 0) { sh.flags = 0; sh.errkey = ~0ull; sh.all_ok = 1; sh.H = 0; sh.nins = 0; sh.total = 0; sh.lists = 0; sh.ctrs = 0; }
     bsync();
     if (n == 0 && (m || doc.n_deps)) return LUNSUP;
+    // Change and dep rows staged at the top of the LDS arena (with LDS copies of hist / h2a) when
+    // they take at most a quarter of it: L1 and L2 read them several times each.  The L1 table
+    // joins them in LDS when it and L2's closure rows fit below (ltab); otherwise the pool.
+    const uint32_t nd = doc.n_deps;
+    const bool staged = HML_STAGE && 8 * (size_t)n + 2 * (size_t)nd <= LARENA / 4;
+    const uint32_t stage_base = staged ? (LARENA - (8 * n + 2 * nd)) & ~1u : LARENA;
+    LDS hm_change_row *sCH = (LDS hm_change_row *)(ar + stage_base);
+    LDS hm_dep_row *sDP = (LDS hm_dep_row *)(ar + stage_base + 6 * n);
+    LDS int32_t *lh = (LDS int32_t *)(ar + stage_base + 6 * n + 2 * nd);
+    LDS uint32_t *lh2a = ar + stage_base + 7 * n + 2 * nd;
+    auto chg = [&](uint32_t i) -> hm_change_row { if (staged) return sCH[i]; return CH[i]; };
+    auto dep = [&](uint32_t g) -> hm_dep_row { if (staged) return sDP[g - doc.dep_off]; return p.deps[g]; };
+    if (staged) for (uint32_t j = tid; j < nd; j += LWG) sDP[j] = p.deps[doc.dep_off + j];
     for (uint32_t i = tid; i < n; i += LWG) {
         const hm_change_row c = CH[i];
+        if (staged) sCH[i] = c;
         // layout contract: op and dep rows grouped by change in arrival order, without gaps
         const uint32_t op0 = i ? CH[i - 1].op_first + CH[i - 1].n_ops : doc.op_off;
         const uint32_t dp0 = i ? CH[i - 1].dep_off + CH[i - 1].n_deps : doc.dep_off;
@@ -423,13 +801,22 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
     const uint32_t T = sh.tabo[A];
     Scratch X;
     large_carve((uintptr_t)sh.scratch_base, n, m, R, O, A, T, &X);
-    for (uint32_t i = tid; i < T; i += LWG) X.tab[i] = 0xFFFFFFFFu;
+    const bool regrows = A <= 8;            // L2 rows held in registers: one LDS buffer, updated in place
+    const uint32_t l2words = (regrows ? n * A : 2 * n * A) + T;
+    const bool ltab = staged && l2words <= stage_base;
+    LDS uint32_t *lt = ar;                  // L1 table (ltab) / L2 table
+    auto tabv = [&](uint32_t sl) -> uint32_t { if (ltab) return lt[sl]; return X.tab[sl]; };
+    for (uint32_t i = tid; i < T; i += LWG) { if (ltab) lt[i] = 0xFFFFFFFFu; else X.tab[i] = 0xFFFFFFFFu; }
     bsync();
     auto slot_of = [&](uint32_t a, uint32_t s) -> uint32_t {     // table index of (a, s) or NONE
         if (a >= A || s < sh.base[a] || s > sh.maxs[a] || sh.maxs[a] == 0) return 0xFFFFFFFFu;
         return sh.tabo[a] + (s - sh.base[a]);
     };
-    for (uint32_t i = tid; i < n; i += LWG) { const hm_change_row c = CH[i]; g_min(&X.tab[slot_of(c.actor, c.seq)], i); }
+    for (uint32_t i = tid; i < n; i += LWG) {
+        const hm_change_row c = chg(i);
+        const uint32_t sl = slot_of(c.actor, c.seq);
+        if (ltab) atomicMin(&lt[sl], i); else g_min(&X.tab[sl], i);
+    }
     for (uint32_t i = tid; i < n; i += LWG) {
         const hm_change_row c = CH[i];
         if (!l3_ok(n, m, A)) for (uint32_t j = 0; j < c.n_ops; j++) X.opchg[c.op_first - doc.op_off + j] = i;
@@ -439,18 +826,18 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
     // ---- L1 fast path: every dependency arrived earlier ----
     uint32_t ndup_local = 0;
     for (uint32_t i = tid; i < n; i += LWG) {
-        const hm_change_row c = CH[i];
+        const hm_change_row c = chg(i);
         bool ok = true;
         for (uint32_t j = 0; j < c.n_deps; j++) {
-            const hm_dep_row dp = p.deps[c.dep_off + j];
+            const hm_dep_row dp = dep(c.dep_off + j);
             if (dp.actor >= A) { atomicOr(&sh.flags, LF_UNSUPPORTED); continue; }
             if (dp.actor == c.actor || dp.seq == 0) continue;
             const uint32_t sl = slot_of(dp.actor, dp.seq);
-            if (sl == 0xFFFFFFFFu || X.tab[sl] >= i) ok = false;
+            if (sl == 0xFFFFFFFFu || tabv(sl) >= i) ok = false;
         }
-        if (c.seq > 1) { const uint32_t sl = slot_of(c.actor, c.seq - 1); if (sl == 0xFFFFFFFFu || X.tab[sl] >= i) ok = false; }
-        const uint32_t f = X.tab[slot_of(c.actor, c.seq)];
-        if (f != i && CH[f].content_id != c.content_id) ok = false;   // mismatched duplicate: exact path
+        if (c.seq > 1) { const uint32_t sl = slot_of(c.actor, c.seq - 1); if (sl == 0xFFFFFFFFu || tabv(sl) >= i) ok = false; }
+        const uint32_t f = tabv(slot_of(c.actor, c.seq));
+        if (f != i && chg(f).content_id != c.content_id) ok = false;   // mismatched duplicate: exact path
         if (!ok) sh.all_ok = 0;
     }
     bsync();
@@ -465,15 +852,25 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
         for (uint32_t c0 = 0; c0 < n; c0 += LWG) {
             const uint32_t i = c0 + tid;
             bool app = false;
-            if (i < n) { const hm_change_row c = CH[i]; app = X.tab[slot_of(c.actor, c.seq)] == i; }
+            if (i < n) { const hm_change_row c = chg(i); app = tabv(slot_of(c.actor, c.seq)) == i; }
             uint32_t tot;
             const uint32_t ex = block_excl_scan(sh, app ? 1u : 0u, &tot);
-            if (i < n) { X.hist[i] = app ? (int32_t)(carry + ex) : -2; if (app) X.h2a[carry + ex] = i; }
+            if (i < n) {
+                const int32_t hv = app ? (int32_t)(carry + ex) : -2;
+                X.hist[i] = hv;
+                if (app) X.h2a[carry + ex] = i;
+                if (staged) { lh[i] = hv; if (app) lh2a[carry + ex] = i; }
+            }
             carry += tot;
         }
         if (tid == 0) sh.H = carry;
         (void)ndup_local;
-    } else if (HM_PAR_HIST && parallel_history(p, sh, doc, X, n, A, T)) {
+    } else {
+    if (ltab) {                             // the slow paths keep their tables in the pool
+        for (uint32_t i = tid; i < T; i += LWG) X.tab[i] = lt[i];
+        bsync();
+    }
+    if (HM_PAR_HIST && parallel_history(CH, p.deps, sh, X.vc, X.hx, X.tab, X.h2a, X.hist, n, A, T)) {
         // history from (t, pass, arrival) without the serial queue emulation
     } else if (wave == 0) {
         // ---- exact emulation of addChange / applyQueuedOps; wave 0, wave-uniform control ----
@@ -541,8 +938,17 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
         for (uint32_t i = lane; i < n; i += 64) if (X.hist[i] == -3) X.hist[i] = -1;
         if (lane == 0) sh.H = H;
     }
+    }
     bsync();
     const uint32_t H = sh.H;
+    if (!all_ready && staged) {             // tables back into LDS for L2
+        if (ltab) for (uint32_t i = tid; i < T; i += LWG) lt[i] = X.tab[i];
+        for (uint32_t i = tid; i < n; i += LWG) lh[i] = X.hist[i];
+        for (uint32_t h = tid; h < H; h += LWG) lh2a[h] = X.h2a[h];
+        bsync();
+    }
+    auto hist_i = [&](uint32_t i) -> int32_t { if (staged) return lh[i]; return X.hist[i]; };
+    auto h2a_i = [&](uint32_t h) -> uint32_t { if (staged) return lh2a[h]; return X.h2a[h]; };
     LSTAMP(1);
     H_out = (int32_t)H;
 
@@ -556,18 +962,18 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
     //     Otherwise (a listed dep dominated by another: never for heads-based deps) the literal
     //     fold runs serially in history order below.
     uint32_t *cur = p.res_all_deps + (size_t)doc.change_off * S, *nxt = X.vc;   // row stride S / A
-    const bool regrows = A <= 8;            // rows held in registers: one LDS buffer, updated in place
-    if ((regrows ? n * A : 2 * n * A) + T <= LARENA) {
+    LDS uint32_t *lrows = nullptr;          // the closure rows when L2 ran in LDS (stride A)
+    if (staged ? ltab : l2words <= LARENA) {
         // the same rounds and check with the first-arrival table and both row buffers in LDS
-        LDS uint32_t *lt = ar, *lc = ar + T, *ln = ar + T + n * A;        // row stride A
-        for (uint32_t i = tid; i < T; i += LWG) lt[i] = X.tab[i];
+        LDS uint32_t *lc = ar + T, *ln = ar + T + n * A;        // row stride A
+        if (!ltab) for (uint32_t i = tid; i < T; i += LWG) lt[i] = X.tab[i];
         for (uint32_t i = tid; i < n; i += LWG) {
             LDS uint32_t *row = lc + i * A;
             for (uint32_t a = 0; a < A; a++) row[a] = 0;
-            if (X.hist[i] < 0) continue;
-            const hm_change_row c = CH[i];
+            if (hist_i(i) < 0) continue;
+            const hm_change_row c = chg(i);
             for (uint32_t j = 0; j < c.n_deps; j++) {
-                const hm_dep_row dp = p.deps[c.dep_off + j];
+                const hm_dep_row dp = dep(c.dep_off + j);
                 const uint32_t sq = dp.actor == c.actor ? c.seq - 1 : dp.seq;
                 if (row[dp.actor] < sq) row[dp.actor] = sq;
             }
@@ -579,39 +985,32 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
             return lt[sh.tabo[a] + (sq - sh.base[a])];
         };
         if (regrows) {
-            // in place: every entry is a seq the closure contains, so reading a row another thread
-            // is growing mixes valid lower bounds, and a round in which no row grows is the fixpoint
-            for (;;) {
-                if (tid == 0) sh.grew = 0;
-                bsync();
+            // in place, one work item per (row, actor a): row |= row of the change (a, row[a]) by LDS
+            // atomic max.  Every entry is a seq the closure contains, so reading a row another item
+            // is growing mixes valid lower bounds, and a round in which no item sees a larger entry
+            // is the fixpoint.  One barrier per round: the grew flag of round r is gflag[r % 3],
+            // and thread 0 clears the one of round r + 1 (last read before the barrier of r - 1).
+            if (tid < 3) sh.gflag[tid] = 0;
+            bsync();
+            for (uint32_t round = 0;; round++) {
                 bool grew = false;
-                for (uint32_t i = tid; i < n; i += LWG) {
-                    if (X.hist[i] < 0) continue;
+                for (uint32_t w = tid; w < n * 8; w += LWG) {
+                    const uint32_t i = w >> 3, a = w & 7;
+                    if (a >= A || hist_i(i) < 0) continue;
                     LDS uint32_t *row = lc + i * A;
-                    uint32_t v[8], v0[8];
-#pragma unroll
-                    for (uint32_t b = 0; b < 8; b++) v0[b] = v[b] = b < A ? row[b] : 0u;
-#pragma unroll
-                    for (uint32_t a = 0; a < 8; a++) {
-                        if (a >= A) break;
-                        const uint32_t sq = v[a];
-                        if (!sq) continue;
-                        const uint32_t ti = lslot(a, sq);
-                        if (ti >= n) continue;
-                        const LDS uint32_t *r2 = lc + ti * A;
-#pragma unroll
-                        for (uint32_t b = 0; b < 8; b++)
-                            if (b < A && b != a) { const uint32_t x = r2[b]; v[b] = v[b] > x ? v[b] : x; }
-                    }
+                    const uint32_t sq = row[a];
+                    if (!sq) continue;
+                    const uint32_t ti = lslot(a, sq);
+                    if (ti >= n) continue;
+                    const LDS uint32_t *r2 = lc + ti * A;
 #pragma unroll
                     for (uint32_t b = 0; b < 8; b++)
-                        if (b < A && v[b] != v0[b]) { row[b] = v[b]; grew = true; }
+                        if (b < A && b != a) { const uint32_t x = r2[b]; if (x > row[b]) { atomicMax(&row[b], x); grew = true; } }
                 }
-                if (grew) sh.grew = 1;
+                if (tid == 0) sh.gflag[(round + 1) % 3] = 0;
+                if (grew) sh.gflag[round % 3] = 1;
                 bsync();
-                const bool any = sh.grew != 0;
-                bsync();
-                if (!any) break;
+                if (!sh.gflag[round % 3]) break;
             }
         } else {
             for (;;) {
@@ -650,8 +1049,8 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
             uint32_t *grow_ = cur + (size_t)i * S;
             const LDS uint32_t *row = lc + i * A;
             for (uint32_t a = 0; a < S; a++) grow_[a] = a < A ? row[a] : 0u;
-            if (X.hist[i] < 0) continue;
-            const hm_change_row c = CH[i];
+            if (hist_i(i) < 0) continue;
+            const hm_change_row c = chg(i);
             bool same = true;
             if (regrows) {
                 uint32_t acc[8];
@@ -668,7 +1067,7 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
                 };
                 bool own = false;
                 for (uint32_t j = 0; j < c.n_deps; j++) {
-                    const hm_dep_row dp = p.deps[c.dep_off + j];
+                    const hm_dep_row dp = dep(c.dep_off + j);
                     if (dp.actor == c.actor) { own = true; fold(c.actor, c.seq - 1); }
                     else fold(dp.actor, dp.seq);
                 }
@@ -688,7 +1087,7 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
                 };
                 bool own = false;
                 for (uint32_t j = 0; j < c.n_deps; j++) {
-                    const hm_dep_row dp = p.deps[c.dep_off + j];
+                    const hm_dep_row dp = dep(c.dep_off + j);
                     if (dp.actor == c.actor) { own = true; fold(c.actor, c.seq - 1); }
                     else fold(dp.actor, dp.seq);
                 }
@@ -697,6 +1096,7 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
             }
             if (!same) sh.all_ok = 0;
         }
+        lrows = lc;
         bsync();
     } else {
         for (uint32_t i = tid; i < n; i += LWG) {
@@ -774,8 +1174,13 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
     const bool closure_ok = sh.all_ok != 0;
     if (closure_ok) {
         for (uint32_t h = tid; h < H; h += LWG) {
-            const uint32_t *row = cur + (size_t)X.h2a[h] * S;
-            for (uint32_t a = 0; a < A; a++) atomicMax(&sh.maxad[a], row[a]);
+            if (lrows) {
+                const LDS uint32_t *row = lrows + h2a_i(h) * A;
+                for (uint32_t a = 0; a < A; a++) atomicMax(&sh.maxad[a], row[a]);
+            } else {
+                const uint32_t *row = cur + (size_t)X.h2a[h] * S;
+                for (uint32_t a = 0; a < A; a++) atomicMax(&sh.maxad[a], row[a]);
+            }
         }
     }
     // literal fold, history order, lanes = actors (wave 0)
@@ -786,7 +1191,7 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
             uint32_t acc = 0;
             auto fold = [&](uint32_t a, uint32_t s) {
                 if (s == 0) return;
-                const uint32_t dc = X.tab[slot_of(a, s)];          // the applied change (a, s)
+                const uint32_t dc = tabv(slot_of(a, s));           // the applied change (a, s)
                 const uint32_t t = lane < A ? ad_row(p, doc, dc)[lane] : 0;
                 acc = acc > t ? acc : t;
                 if (lane == a) acc = s;
@@ -810,11 +1215,17 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
     LSTAMP(3);
     // clock / heads: a head survives unless some applied change's allDeps reaches it
     for (uint32_t h = tid; h < H; h += LWG) {
-        const hm_change_row c = CH[X.h2a[h]];
+        const hm_change_row c = chg(h2a_i(h));
         atomicMax(&sh.clock[c.actor], c.seq);
     }
     bsync();
     if (tid < A && sh.clock[tid] && sh.maxad[tid] < sh.clock[tid]) sh.headv[tid] = sh.clock[tid];
+#if HML_RES
+    {
+        const int rc = l34_res(p, sh, ar, doc, X, H);
+        if (rc != RES_FALLBACK) return (Outcome)rc;
+    }
+#endif
 
     // ---- L3: ops ----
     // Op keys: an applied op's position in application order, i.e. (history position, op index)
@@ -822,7 +1233,7 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
     for (uint32_t h = tid; h < H; h += LWG) X.survp[h] = CH[X.h2a[h]].n_ops;     // survp is free until L3 survivors
     bsync();
     uint32_t m_applied;
-    scan_array(sh, X.survp, H, &m_applied);
+    m_applied = scan_array(sh, X.survp, H);
     (void)m_applied;
     // Per-change inputs of the op loops (history position, actor, seq, first op, key base,
     // allDeps row) and the op -> change map (16 bit) are staged in the LDS arena when they fit
@@ -940,7 +1351,7 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
     }
     bsync();
     uint32_t tot2;
-    scan_array(sh, X.segoff, R, &tot2);
+    tot2 = scan_array(sh, X.segoff, R);
     for (uint32_t k = tid; k < m; k += LWG) {
         const OpC o = op_c(k);
         if (o.action < HM_SET || o.action > HM_INC || o.obj >= O) continue;   // exactly the ops segcnt counted
@@ -1016,7 +1427,7 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
     for (uint32_t i = tid; i < R; i += LWG) X.regoff[i] = X.survcnt[i];
     bsync();
     uint32_t total;
-    scan_array(sh, X.regoff, R, &total);
+    total = scan_array(sh, X.regoff, R);
     if (tid == 0) sh.total = total;
     for (uint32_t j = tid; j < nsurv; j += LWG) {
         const uint32_t k = X.survk[j];
@@ -1135,7 +1546,7 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
         for (uint32_t i = tid; i < O; i += LWG) { const uint32_t t = otype_get(i); X.listid[i] = (t == HM_MAKE_LIST || t == HM_MAKE_TEXT) ? 1u : 0u; }
         bsync();
         uint32_t nl;
-        scan_array(sh, X.listid, O, &nl);          // exclusive prefix -> compact list id (valid for list objects)
+        nl = scan_array(sh, X.listid, O);          // exclusive prefix -> compact list id (valid for list objects)
         // per node i: its register nreg[i], its compact list id nlist[i], parent slot, sibling key
         if (!early) {
             for (uint32_t k = tid; k < m; k += LWG) {
@@ -1157,7 +1568,7 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
         for (uint32_t i = tid; i < NP; i += LWG) X.poff[i] = X.pcount[i];
         bsync();
         uint32_t tp;
-        scan_array(sh, X.poff, NP, &tp);
+        tp = scan_array(sh, X.poff, NP);
         // sibling lists (an only child needs none: no next sibling, first child of its parent)
         for (uint32_t i = tid; i < N; i += LWG) {
             const uint32_t pi = X.nodepi[i];
@@ -1241,13 +1652,13 @@ __device__ Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_
         }
         bsync();
         uint32_t tl;
-        scan_array(sh, X.listbase, nl, &tl);
+        tl = scan_array(sh, X.listbase, nl);
         // pre-order position of node i: its list's base + (entries of its list) - (entries from i on)
         auto pos_of = [&](uint32_t i, uint32_t l) -> uint32_t { return X.listbase[l] + tsum(2 * (N + l)) - tsum(2 * i); };
         for (uint32_t i = tid; i < N; i += LWG) X.vis[pos_of(i, X.nlist[i])] = X.survcnt[X.nreg[i]] > 0 ? 1u : 0u;
         bsync();
         uint32_t tv;
-        scan_array(sh, X.vis, N, &tv);             // exclusive scan of visibility over pre-order positions
+        tv = scan_array(sh, X.vis, N);             // exclusive scan of visibility over pre-order positions
         for (uint32_t i = tid; i < N; i += LWG) {
             const uint32_t l = X.nlist[i], rg = X.nreg[i];
             // list elements carry their visible index (or -1) in insmin from here on
@@ -1381,6 +1792,14 @@ extern "C" int hm_debug_lstamps(unsigned long long *out, int n, int reset) {
     return n;
 }
 #endif
+
+// per-lane stack (spills) of merge_large_kernel: the engine raises the device stack limit when a
+// build needs more than the runtime's default (a dispatch beyond the limit faults)
+size_t hm_large_stack_bytes() {
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(&hml::merge_large_kernel)) != hipSuccess) return 0;
+    return fa.localSizeBytes;
+}
 
 hipError_t hm_launch_large(const SmallParams &p, void *pool, size_t pool_bytes, unsigned long long *pool_used,
                            uint32_t grid, hipStream_t s) {
