@@ -43,10 +43,7 @@
 #define HML_STAGE 1     // 0: L1/L2 read change / dep rows from HBM and keep the L1 table in the pool (dev A/B)
 #endif
 #ifndef HML_DOC_ATTR
-#define HML_DOC_ATTR __forceinline__
-#endif
-#ifndef HML_RES_ATTR
-#define HML_RES_ATTR __forceinline__
+#define HML_DOC_ATTR __noinline__   // the general path: its own register allocation, off merge_doc_res's
 #endif
 // Explicit address spaces: LDS pointers -> ds_*, pool pointers -> global_* (a generic pointer
 // would compile to flat_* ops, which count against lgkmcnt too, so every LDS wait would also
@@ -398,11 +395,11 @@ __device__ PH_ATTR bool parallel_history(const hm_change_row *CH, const hm_dep_r
 // register, and the layout below fits the arena.
 #define RES_SEG_MAX 64
 #define RES_FALLBACK 3
-__device__ HML_RES_ATTR int l34_res(const SmallParams &p, Shared &sh, LDS uint32_t *ar, const hm_doc_row &doc, const Scratch &X,
-                       uint32_t H) {
+__device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uint32_t *ar, const hm_doc_row &doc,
+                                       const LDS hm_change_row *sCH, const LDS int32_t *lh, const LDS uint32_t *lh2a,
+                                       uint32_t H, uint32_t limit) {
     const uint32_t tid = threadIdx.x;
     const uint32_t n = doc.n_changes, A = doc.n_actors, m = doc.n_ops, R = doc.n_regs, O = doc.n_objs;
-    const hm_change_row *CH = p.changes + doc.change_off;
     const hm_op_row *OP = p.ops + doc.op_off;
     const uint32_t NP = R + O;
     const uint16_t N16 = 0xFFFFu;
@@ -429,22 +426,22 @@ __device__ HML_RES_ATTR int l34_res(const SmallParams &p, Shared &sh, LDS uint32
     LDS uint32_t *p_cnt = w32(NP), *p_off = w32(NP);
     LDS uint16_t *p_fc = w16(NP);
     const uint32_t tail = off;
-    if (A > 8 || O > LA_MAX || m >= 65536 || NP >= 32767 || n >= 65536 || tail > LARENA) return RES_FALLBACK;
+    if (A > 8 || O > LA_MAX || m >= 65536 || NP >= 32767 || n >= 65536 || tail > limit) return RES_FALLBACK;
     auto dec_reg = [](uint32_t w) { return w & 0xFFFFu; };
     auto dec_act = [](uint32_t w) { return (w >> 16) & 15u; };
     auto dec_obj = [](uint32_t w) { return (w >> 20) & 127u; };
     auto key_of = [&](uint32_t k, uint32_t ci) -> uint32_t { return c_kb[ci] + (k - c_op0[ci]); };
 
     // ---- key bases: ops of the changes before each history position ----
-    for (uint32_t h = tid; h < H; h += LWG) c_tmp[h] = CH[X.h2a[h]].n_ops;
+    for (uint32_t h = tid; h < H; h += LWG) c_tmp[h] = sCH[lh2a[h]].n_ops;
     bsync();
     uint32_t m_applied;
     m_applied = scan_array(sh, c_tmp, H);
     (void)m_applied;
     // ---- staging: per-change inputs, op -> change, object / register / parent tables ----
     for (uint32_t i = tid; i < n; i += LWG) {
-        const hm_change_row c = CH[i];
-        const int32_t hi = X.hist[i];
+        const hm_change_row c = sCH[i];
+        const int32_t hi = lh[i];
         const uint32_t o0 = c.op_first - doc.op_off;
         c_hist[i] = (uint32_t)hi; c_act[i] = c.actor; c_seq[i] = c.seq; c_op0[i] = o0;
         c_kb[i] = hi >= 0 ? c_tmp[hi] : 0xFFFFFFFFu;
@@ -727,12 +724,192 @@ __device__ HML_RES_ATTR int l34_res(const SmallParams &p, Shared &sh, LDS uint32
         rr.list_index = (lists_flag && r_node[r] != N16 && r_ins[r] != 0xFFFFFFFFu) ? (int32_t)r_ins[r] : -1;
         p.res_regs[doc.reg_off + r] = rr;
     }
-    for (uint32_t i = tid; i < n; i += LWG) p.res_hist[doc.change_off + i] = X.hist[i];
+    for (uint32_t i = tid; i < n; i += LWG) p.res_hist[doc.change_off + i] = lh[i];
     if (tid == 0) sh.total = total;
     bsync();
     LSTAMP(10);
     if (sh.flags) return LUNSUP;
     return LOK;
+}
+
+// ---- the whole document in LDS (merge_doc_res): setup, L1 fast path, L2 closure, l34_res ----
+// For documents whose rows, tables and L3/L4 working set fit the arena and that need none of the
+// general path's slow machinery: every change ready on arrival, the closure equal to the literal
+// fold, A <= 8.  No pool scratch at all, so nothing here competes for registers with the general
+// path (merge_doc_large, not inlined), which takes every document this returns RES_FALLBACK for
+// and recomputes it from the start.  Results equal the general path's (same rules, same order).
+__device__ __forceinline__ int merge_doc_res(const SmallParams &p, Shared &sh, LDS uint32_t *ar, const hm_doc_row &doc,
+                                             int32_t &H_out) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t n = doc.n_changes, A = doc.n_actors, m = doc.n_ops, nd = doc.n_deps;
+    const uint32_t S = p.a_stride;
+    const hm_change_row *CH = p.changes + doc.change_off;
+    if (tid < LA_MAX) { sh.base[tid] = 0xFFFFFFFFu; sh.maxs[tid] = 0; sh.clock[tid] = 0; sh.bclock[tid] = 0;
+                        sh.headv[tid] = 0; sh.maxad[tid] = 0; }
+    if (tid == 0) { sh.flags = 0; sh.errkey = ~0ull; sh.all_ok = 1; sh.H = 0; sh.nins = 0; sh.total = 0; sh.lists = 0; sh.ctrs = 0; }
+    // rows at the top of the arena: changes (6n words), deps (2nd), hist (n), h2a (n)
+    const uint32_t stage_base = (LARENA - (8 * n + 2 * nd)) & ~1u;
+    LDS hm_change_row *sCH = (LDS hm_change_row *)(ar + stage_base);
+    LDS hm_dep_row *sDP = (LDS hm_dep_row *)(ar + stage_base + 6 * n);
+    LDS int32_t *lh = (LDS int32_t *)(ar + stage_base + 6 * n + 2 * nd);
+    LDS uint32_t *lh2a = ar + stage_base + 7 * n + 2 * nd;
+    for (uint32_t j = tid; j < nd; j += LWG) sDP[j] = p.deps[doc.dep_off + j];
+    bsync();
+    for (uint32_t i = tid; i < n; i += LWG) {
+        const hm_change_row c = CH[i];
+        sCH[i] = c;
+        const uint32_t op0 = i ? CH[i - 1].op_first + CH[i - 1].n_ops : doc.op_off;
+        const uint32_t dp0 = i ? CH[i - 1].dep_off + CH[i - 1].n_deps : doc.dep_off;
+        const bool last_bad = i == n - 1 && (c.op_first + c.n_ops != doc.op_off + m || c.dep_off + c.n_deps != doc.dep_off + nd);
+        if (c.actor >= A || c.seq == 0 || c.op_first < doc.op_off || c.op_first - doc.op_off + c.n_ops > m ||
+            c.dep_off < doc.dep_off || c.dep_off - doc.dep_off + c.n_deps > nd ||
+            c.op_first != op0 || c.dep_off != dp0 || last_bad)
+            atomicOr(&sh.flags, LF_UNSUPPORTED);
+        else { atomicMin(&sh.base[c.actor], c.seq); atomicMax(&sh.maxs[c.actor], c.seq); atomicMax(&sh.bclock[c.actor], c.seq); }
+    }
+    bsync();
+    if (sh.flags) return RES_FALLBACK;
+    if (tid == 0) {
+        uint32_t t = 0;
+        for (uint32_t a = 0; a < A; a++) { sh.tabo[a] = t; if (sh.maxs[a]) t += sh.maxs[a] - sh.base[a] + 1; }
+        sh.tabo[A] = t;
+    }
+    bsync();
+    const uint32_t T = sh.tabo[A];
+    if (T > 4 * n + 64 || n * A + T > stage_base) return RES_FALLBACK;
+    LDS uint32_t *lt = ar, *lc = ar + T;            // L1 table, L2 closure rows (stride A)
+    for (uint32_t i = tid; i < T; i += LWG) lt[i] = 0xFFFFFFFFu;
+    bsync();
+    auto slot_of = [&](uint32_t a, uint32_t s) -> uint32_t {
+        if (a >= A || s < sh.base[a] || s > sh.maxs[a] || sh.maxs[a] == 0) return 0xFFFFFFFFu;
+        return sh.tabo[a] + (s - sh.base[a]);
+    };
+    for (uint32_t i = tid; i < n; i += LWG) { const hm_change_row c = sCH[i]; atomicMin(&lt[slot_of(c.actor, c.seq)], i); }
+    bsync();
+    LSTAMP(0);
+    // ---- L1: every dependency arrived earlier (else the general path's queue emulation) ----
+    for (uint32_t i = tid; i < n; i += LWG) {
+        const hm_change_row c = sCH[i];
+        bool ok = true;
+        for (uint32_t j = 0; j < c.n_deps; j++) {
+            const hm_dep_row dp = sDP[c.dep_off - doc.dep_off + j];
+            if (dp.actor >= A) { ok = false; continue; }
+            if (dp.actor == c.actor || dp.seq == 0) continue;
+            const uint32_t sl = slot_of(dp.actor, dp.seq);
+            if (sl == 0xFFFFFFFFu || lt[sl] >= i) ok = false;
+        }
+        if (c.seq > 1) { const uint32_t sl = slot_of(c.actor, c.seq - 1); if (sl == 0xFFFFFFFFu || lt[sl] >= i) ok = false; }
+        const uint32_t f = lt[slot_of(c.actor, c.seq)];
+        if (f != i && sCH[f].content_id != c.content_id) ok = false;
+        if (!ok) sh.all_ok = 0;
+    }
+    bsync();
+    const bool all_ready = sh.all_ok != 0;
+    bsync();
+    if (!all_ready) return RES_FALLBACK;
+    {
+        uint32_t carry = 0;
+        for (uint32_t c0 = 0; c0 < n; c0 += LWG) {
+            const uint32_t i = c0 + tid;
+            bool app = false;
+            if (i < n) { const hm_change_row c = sCH[i]; app = lt[slot_of(c.actor, c.seq)] == i; }
+            uint32_t tot;
+            const uint32_t ex = block_excl_scan(sh, app ? 1u : 0u, &tot);
+            if (i < n) { lh[i] = app ? (int32_t)(carry + ex) : -2; if (app) lh2a[carry + ex] = i; }
+            carry += tot;
+        }
+        if (tid == 0) sh.H = carry;
+    }
+    bsync();
+    const uint32_t H = sh.H;
+    LSTAMP(1);
+    // ---- L2: closure rows by pointer jumping per (row, actor), then the literal-fold check ----
+    for (uint32_t i = tid; i < n; i += LWG) {
+        LDS uint32_t *row = lc + i * A;
+        for (uint32_t a = 0; a < A; a++) row[a] = 0;
+        if (lh[i] < 0) continue;
+        const hm_change_row c = sCH[i];
+        for (uint32_t j = 0; j < c.n_deps; j++) {
+            const hm_dep_row dp = sDP[c.dep_off - doc.dep_off + j];
+            const uint32_t sq = dp.actor == c.actor ? c.seq - 1 : dp.seq;
+            if (row[dp.actor] < sq) row[dp.actor] = sq;
+        }
+        if (row[c.actor] < c.seq - 1) row[c.actor] = c.seq - 1;
+    }
+    if (tid < 3) sh.gflag[tid] = 0;
+    bsync();
+    auto lslot = [&](uint32_t a, uint32_t sq) -> uint32_t {      // applied change (a, sq) or >= n
+        if (sq < sh.base[a] || sq > sh.maxs[a] || sh.maxs[a] == 0) return 0xFFFFFFFFu;
+        return lt[sh.tabo[a] + (sq - sh.base[a])];
+    };
+    for (uint32_t round = 0;; round++) {
+        bool grew = false;
+        for (uint32_t w = tid; w < n * 8; w += LWG) {
+            const uint32_t i = w >> 3, a = w & 7;
+            if (a >= A || lh[i] < 0) continue;
+            LDS uint32_t *row = lc + i * A;
+            const uint32_t sq = row[a];
+            if (!sq) continue;
+            const uint32_t ti = lslot(a, sq);
+            if (ti >= n) continue;
+            const LDS uint32_t *r2 = lc + ti * A;
+#pragma unroll
+            for (uint32_t b = 0; b < 8; b++)
+                if (b < A && b != a) { const uint32_t x = r2[b]; if (x > row[b]) { atomicMax(&row[b], x); grew = true; } }
+        }
+        if (tid == 0) sh.gflag[(round + 1) % 3] = 0;
+        if (grew) sh.gflag[round % 3] = 1;
+        bsync();
+        if (!sh.gflag[round % 3]) break;
+    }
+    LSTAMP(2);
+    if (tid == 0) sh.all_ok = 1;
+    bsync();
+    uint32_t *cur = p.res_all_deps + (size_t)doc.change_off * S;
+    for (uint32_t i = tid; i < n; i += LWG) {
+        uint32_t *grow_ = cur + (size_t)i * S;
+        const LDS uint32_t *row = lc + i * A;
+        for (uint32_t a = 0; a < S; a++) grow_[a] = a < A ? row[a] : 0u;
+        if (lh[i] < 0) continue;
+        const hm_change_row c = sCH[i];
+        bool same = true;
+        uint32_t acc[8];
+#pragma unroll
+        for (uint32_t b = 0; b < 8; b++) acc[b] = 0;
+        auto fold = [&](uint32_t a, uint32_t sq) {
+            if (sq == 0) return;
+            const uint32_t ti = lslot(a, sq);
+            if (ti >= n) { same = false; return; }
+            const LDS uint32_t *r2 = lc + ti * A;
+#pragma unroll
+            for (uint32_t b = 0; b < 8; b++)
+                if (b < A) { const uint32_t x = r2[b]; acc[b] = b == a ? sq : (acc[b] > x ? acc[b] : x); }
+        };
+        bool own = false;
+        for (uint32_t j = 0; j < c.n_deps; j++) {
+            const hm_dep_row dp = sDP[c.dep_off - doc.dep_off + j];
+            if (dp.actor == c.actor) { own = true; fold(c.actor, c.seq - 1); }
+            else fold(dp.actor, dp.seq);
+        }
+        if (!own) fold(c.actor, c.seq - 1);
+#pragma unroll
+        for (uint32_t b = 0; b < 8; b++) if (b < A) same = same && acc[b] == row[b];
+        if (!same) sh.all_ok = 0;
+    }
+    bsync();
+    if (!sh.all_ok) return RES_FALLBACK;       // the literal fold lowers an entry: general path
+    LSTAMP(3);
+    for (uint32_t h = tid; h < H; h += LWG) {
+        const uint32_t ci = lh2a[h];
+        const LDS uint32_t *row = lc + ci * A;
+        for (uint32_t a = 0; a < A; a++) atomicMax(&sh.maxad[a], row[a]);
+        const hm_change_row c = sCH[ci];
+        atomicMax(&sh.clock[c.actor], c.seq);
+    }
+    bsync();
+    if (tid < A && sh.clock[tid] && sh.maxad[tid] < sh.clock[tid]) sh.headv[tid] = sh.clock[tid];
+    H_out = (int32_t)H;
+    return l34_res(p, sh, ar, doc, sCH, lh, lh2a, H, stage_base);
 }
 
 __device__ HML_DOC_ATTR Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_t *ar, const hm_doc_row &doc, uint32_t d,
@@ -1220,12 +1397,6 @@ __device__ HML_DOC_ATTR Outcome merge_doc_large(const SmallParams &p, Shared &sh
     }
     bsync();
     if (tid < A && sh.clock[tid] && sh.maxad[tid] < sh.clock[tid]) sh.headv[tid] = sh.clock[tid];
-#if HML_RES
-    {
-        const int rc = l34_res(p, sh, ar, doc, X, H);
-        if (rc != RES_FALLBACK) return (Outcome)rc;
-    }
-#endif
 
     // ---- L3: ops ----
     // Op keys: an applied op's position in application order, i.e. (history position, op index)
@@ -1725,7 +1896,17 @@ __global__ __launch_bounds__(LWG) __attribute__((amdgpu_waves_per_eu(4))) void m
 #if HM_STAMPS
         { const u64 t0 = lstamp_now(); if (tid == 0) hml_st[HML_NSTAMP] = t0; }
 #endif
-        const Outcome oc = merge_doc_large(p, sh, arena, doc, d, pool, pool_bytes, pool_used, H);
+        int rc = RES_FALLBACK;
+        const uint32_t dn = doc.n_changes, dd = doc.n_deps;
+        if (HML_RES && dn >= 1 && doc.n_actors <= 8 && doc.n_objs >= 1 && doc.n_objs <= LA_MAX && doc.n_ops < 65536 &&
+            doc.n_regs + doc.n_objs < 32767 && 8 * (size_t)dn + 2 * (size_t)dd <= LARENA / 4)
+            rc = merge_doc_res(p, sh, arena, doc, H);
+        const bool via_res = rc != RES_FALLBACK;   // (every change ready on arrival: nothing queued)
+        if (!via_res) {
+            bsync();
+            rc = merge_doc_large(p, sh, arena, doc, d, pool, pool_bytes, pool_used, H);
+        }
+        const Outcome oc = (Outcome)rc;
         bsync();
         hm_doc_result r = {};
         r.err_change = HM_NONE; r.err_op = HM_NONE;
@@ -1743,7 +1924,8 @@ __global__ __launch_bounds__(LWG) __attribute__((amdgpu_waves_per_eu(4))) void m
             r.hist_len = (uint32_t)H;
             r.n_surv = sh.total;
             uint32_t q = 0;
-            for (uint32_t i = 0; i < doc.n_changes; i++) q += p.res_hist[doc.change_off + i] == -1 ? 1u : 0u;
+            if (!via_res)
+                for (uint32_t i = 0; i < doc.n_changes; i++) q += p.res_hist[doc.change_off + i] == -1 ? 1u : 0u;
             r.n_queued = q;
             bool ag = true, bg = true;
             for (uint32_t a = 0; a < S; a++) {
