@@ -23,7 +23,11 @@
 #ifndef HML_WGS_PER_CU
 #define HML_WGS_PER_CU 1   // workgroups per CU: 16 waves per CU split into this many documents
 #endif
-#define LWG (1024 / HML_WGS_PER_CU)
+#ifndef HML_LWG
+#define HML_LWG (1024 / HML_WGS_PER_CU)   // threads per workgroup
+#endif
+#define LWG HML_LWG
+#define HML_WPE (LWG * HML_WGS_PER_CU / 256)   // waves per SIMD (register budget 512 / HML_WPE)
 #define LA_MAX 64
 // LDS arena per workgroup (u32 words).  One 1024-thread workgroup per CU owns 150 KB: a
 // document's whole L3/L4 working set (op words, assign lists, register / node / parent tables,
@@ -137,7 +141,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(Shared &sh, uint32_t v, uint
 // entries (its loads are independent, so they overlap), one block scan of the run sums
 // (P: a pool pointer or an LDS pointer)
 template <typename P>
-__device__ uint32_t scan_array(Shared &sh, P arr, uint32_t N) {
+__device__ __forceinline__ uint32_t scan_array(Shared &sh, P arr, uint32_t N) {
     const uint32_t per = (N + LWG - 1) / LWG;
     const uint32_t b0 = threadIdx.x * per < N ? threadIdx.x * per : N;
     const uint32_t b1 = b0 + per < N ? b0 + per : N;
@@ -397,19 +401,19 @@ __device__ PH_ATTR bool parallel_history(const hm_change_row *CH, const hm_dep_r
 #define RES_FALLBACK 3
 __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uint32_t *ar, const hm_doc_row &doc,
                                        const LDS hm_change_row *sCH, const LDS int32_t *lh, const LDS uint32_t *lh2a,
-                                       uint32_t H, uint32_t limit) {
+                                       uint32_t H, uint32_t ad_off, uint32_t limit) {
     const uint32_t tid = threadIdx.x;
     const uint32_t n = doc.n_changes, A = doc.n_actors, m = doc.n_ops, R = doc.n_regs, O = doc.n_objs;
     const hm_op_row *OP = p.ops + doc.op_off;
     const uint32_t NP = R + O;
     const uint16_t N16 = 0xFFFFu;
     // ---- layout (words); region S and the survivor list die after the ranks (L4 reuses them) ----
-    uint32_t off = 0;
+    uint32_t off = ad_off;                      // [0, ad_off): L2's first-arrival table (dead)
     auto w32 = [&](uint32_t cnt) -> LDS uint32_t * { LDS uint32_t *q = ar + off; off += cnt; return q; };
     auto w16 = [&](uint32_t cnt) -> LDS uint16_t * { LDS uint16_t *q = (LDS uint16_t *)(ar + off); off += (cnt + 1) / 2; return q; };
     auto w8 = [&](uint32_t cnt) -> LDS uint8_t * { LDS uint8_t *q = (LDS uint8_t *)(ar + off); off += (cnt + 3) / 4; return q; };
+    LDS uint32_t *c_ad = w32(n * A);            // L2's closure rows (= allDeps), already in place
     LDS uint32_t *c_tmp = w32(n), *c_hist = w32(n), *c_act = w32(n), *c_seq = w32(n), *c_op0 = w32(n), *c_kb = w32(n);
-    LDS uint32_t *c_ad = w32(n * A);
     LDS uint32_t *o_w = w32(m);                 // reg (16) | action (4) << 16 | obj (7, 127 unknown) << 20
     LDS uint16_t *o_chg = w16(m);               // op -> arrival index of its change
     LDS uint16_t *a_k = w16(m);                 // assign lists (set/del/link/inc op indices), by register
@@ -445,8 +449,6 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
         const uint32_t o0 = c.op_first - doc.op_off;
         c_hist[i] = (uint32_t)hi; c_act[i] = c.actor; c_seq[i] = c.seq; c_op0[i] = o0;
         c_kb[i] = hi >= 0 ? c_tmp[hi] : 0xFFFFFFFFu;
-        const uint32_t *ad = ad_row(p, doc, i);
-        for (uint32_t a = 0; a < A; a++) c_ad[i * A + a] = ad[a];
         for (uint32_t j = 0; j < c.n_ops; j++) o_chg[o0 + j] = (uint16_t)i;
     }
     for (uint32_t i = tid; i < O; i += LWG) { sh.oslot[i] = i == 0 ? 0u : 0xFFFFFFFFu; sh.otype[i] = i == 0 ? (uint32_t)HM_MAKE_MAP : 0xFFu; }
@@ -532,9 +534,19 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
     }
     bsync();
     LSTAMP(13);
-    // ---- survivors and per-op checks ----
+    // ---- survivors and per-op checks (insert parents loaded from HBM up front, four per thread) ----
     bool any_list = false;
-    for (uint32_t k = tid; k < m; k += LWG) {
+    for (uint32_t k0 = 0; k0 < m; k0 += 4 * LWG) {
+    uint32_t par[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const uint32_t k = k0 + tid + u * LWG;
+        par[u] = (k < m && dec_act(o_w[k]) == HM_INS) ? OP[k].parent : HM_HEAD;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const uint32_t k = k0 + tid + u * LWG;
+        if (k >= m) continue;
         const uint32_t w = o_w[k], a = dec_act(w), obj = dec_obj(w), reg = dec_reg(w);
         if (a < HM_INS || a > HM_INC) continue;
         const uint32_t ci = o_chg[k];
@@ -550,7 +562,7 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
         const bool is_list = ot == HM_MAKE_LIST || ot == HM_MAKE_TEXT;
         if (a == HM_INS) {
             any_list = true;
-            const uint32_t parent = OP[k].parent;
+            const uint32_t parent = par[u];
             if (r_ins[reg] != key + 1) atomicMin(&sh.errkey, err_key((uint32_t)h, kx + 1, ci, HM_ERR_DUPLICATE_ELEM));
             if (parent != HM_HEAD && !(r_ins[parent] <= key))
                 atomicMin(&sh.errkey, err_key((uint32_t)h, kx + 1, ci, HM_ERR_UNSUPPORTED));
@@ -572,6 +584,7 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
                 s_list[atomicAdd(&sh.nsurv, 1u)] = (uint16_t)k;
             }
         }
+    }
     }
     if (any_list) sh.lists = 1;
     bsync();
@@ -842,25 +855,48 @@ __device__ __forceinline__ int merge_doc_res(const SmallParams &p, Shared &sh, L
         if (sq < sh.base[a] || sq > sh.maxs[a] || sh.maxs[a] == 0) return 0xFFFFFFFFu;
         return lt[sh.tabo[a] + (sq - sh.base[a])];
     };
+    // One lane per (row i, actor a) = lane group of 8 per row: lane a reads row[a], finds the
+    // applied change (a, row[a]) and loads that change's row; the 8 rows of a group are reduced
+    // by DPP (quad xor 1, xor 2, half-row mirror) and lane a keeps entry a — no atomics, one LDS
+    // write per grown entry.  Groups read rows other groups are growing: every entry stays a seq
+    // the closure contains, and a round in which no entry grows is the fixpoint.
+    const uint32_t my_a = tid & 7;
+    const bool a_ok = my_a < A;
+    const uint32_t a_base = a_ok ? sh.base[my_a] : 1u, a_max = a_ok ? sh.maxs[my_a] : 0u, a_off = a_ok ? sh.tabo[my_a] : 0u;
+    auto gmax8 = [](uint32_t x) -> uint32_t {
+        uint32_t y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false); x = x > y ? x : y;   // quad xor 1
+        y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false); x = x > y ? x : y;            // quad xor 2
+        y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false); return x > y ? x : y;        // half-row mirror
+    };
     for (uint32_t round = 0;; round++) {
         bool grew = false;
-        for (uint32_t w = tid; w < n * 8; w += LWG) {
-            const uint32_t i = w >> 3, a = w & 7;
-            if (a >= A || lh[i] < 0) continue;
-            LDS uint32_t *row = lc + i * A;
-            const uint32_t sq = row[a];
-            if (!sq) continue;
-            const uint32_t ti = lslot(a, sq);
-            if (ti >= n) continue;
-            const LDS uint32_t *r2 = lc + ti * A;
+        for (uint32_t w0 = 0; w0 < n * 8; w0 += LWG) {     // whole lane groups: DPP needs them active
+            const uint32_t w = w0 + tid, i = w >> 3;
+            const bool live = w < n * 8 && a_ok && lh[i < n ? i : 0] >= 0;
+            LDS uint32_t *row = lc + (live ? i : 0u) * A;
+            const uint32_t sq = live ? row[my_a] : 0u;
+            const uint32_t ti = (sq && sq >= a_base && sq <= a_max) ? lt[a_off + (sq - a_base)] : 0xFFFFFFFFu;
+            const bool src = ti < n;
+            const LDS uint32_t *r2 = lc + (src ? ti : 0u) * A;
+            uint32_t v[8];
 #pragma unroll
-            for (uint32_t b = 0; b < 8; b++)
-                if (b < A && b != a) { const uint32_t x = r2[b]; if (x > row[b]) { atomicMax(&row[b], x); grew = true; } }
+            for (uint32_t b = 0; b < 8; b++) v[b] = (src && b < A) ? r2[b] : 0u;
+#pragma unroll
+            for (uint32_t b = 0; b < 8; b++) v[b] = gmax8(v[b]);
+            uint32_t mine = v[0];
+#pragma unroll
+            for (uint32_t b = 1; b < 8; b++) mine = my_a == b ? v[b] : mine;
+            if (live && mine > sq) { row[my_a] = mine; grew = true; }
         }
         if (tid == 0) sh.gflag[(round + 1) % 3] = 0;
         if (grew) sh.gflag[round % 3] = 1;
         bsync();
-        if (!sh.gflag[round % 3]) break;
+        if (!sh.gflag[round % 3]) {
+#if HM_STAMPS
+            if (tid == 0) hml_st[14] += round + 1;        // closure rounds (diagnostic builds)
+#endif
+            break;
+        }
     }
     LSTAMP(2);
     if (tid == 0) sh.all_ok = 1;
@@ -909,7 +945,7 @@ __device__ __forceinline__ int merge_doc_res(const SmallParams &p, Shared &sh, L
     bsync();
     if (tid < A && sh.clock[tid] && sh.maxad[tid] < sh.clock[tid]) sh.headv[tid] = sh.clock[tid];
     H_out = (int32_t)H;
-    return l34_res(p, sh, ar, doc, sCH, lh, lh2a, H, stage_base);
+    return l34_res(p, sh, ar, doc, sCH, lh, lh2a, H, T, stage_base);
 }
 
 __device__ HML_DOC_ATTR Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_t *ar, const hm_doc_row &doc, uint32_t d,
@@ -1868,7 +1904,7 @@ __device__ HML_DOC_ATTR Outcome merge_doc_large(const SmallParams &p, Shared &sh
     return LOK;
 }
 
-__global__ __launch_bounds__(LWG) __attribute__((amdgpu_waves_per_eu(4))) void merge_large_kernel(SmallParams p, uint8_t *pool, u64 pool_bytes, u64 *pool_used) {
+__global__ __launch_bounds__(LWG) __attribute__((amdgpu_waves_per_eu(HML_WPE))) void merge_large_kernel(SmallParams p, uint8_t *pool, u64 pool_bytes, u64 *pool_used) {
     __shared__ Shared sh;
     __shared__ __align__(16) uint32_t arena_raw[LARENA];
     LDS uint32_t *arena = (LDS uint32_t *)arena_raw;
@@ -1879,8 +1915,11 @@ __global__ __launch_bounds__(LWG) __attribute__((amdgpu_waves_per_eu(4))) void m
     // per-document claiming balances the grid (one atomic per document is noise beside a
     // long document's merge), and an empty list costs one read per workgroup.
     __shared__ uint32_t claim;
+    // the general path (not inlined) reads the parameter block from an LDS copy: a reference to
+    // the kernel argument itself would copy it to the stack and route every read through scratch
+    __shared__ SmallParams psh;
     const uint32_t nd = *p.n_deferred;
-    if (tid == 0) { sh.ws_base = 0; sh.ws_size = 0; }
+    if (tid == 0) { sh.ws_base = 0; sh.ws_size = 0; psh = p; }
 #if HM_STAMPS
     if (tid <= HML_NSTAMP) hml_st[tid] = 0;
 #endif
@@ -1904,7 +1943,7 @@ __global__ __launch_bounds__(LWG) __attribute__((amdgpu_waves_per_eu(4))) void m
         const bool via_res = rc != RES_FALLBACK;   // (every change ready on arrival: nothing queued)
         if (!via_res) {
             bsync();
-            rc = merge_doc_large(p, sh, arena, doc, d, pool, pool_bytes, pool_used, H);
+            rc = merge_doc_large(psh, sh, arena, doc, d, pool, pool_bytes, pool_used, H);
         }
         const Outcome oc = (Outcome)rc;
         bsync();
