@@ -1253,14 +1253,24 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
 }
 
 // Output phase of one document (all reads from LDS; coalesced stores).
+// Clock.cmp(DocBackend.clock, minimumClock) of a merged document, from the min_clock row loaded
+// before the merge (mc, lane < S): computed before the next document's rows are requested, so
+// no wait for that load sits behind the prefetch and this document's stores
+__device__ __forceinline__ uint32_t min_cmp_of(const SmallParams &p, const SmallLds &L, const hm_doc_row &doc, uint32_t mc) {
+    const uint32_t lane = threadIdx.x, S = p.a_stride;
+    const uint32_t bc = (lane < S && lane < doc.n_actors) ? L.bclock[lane] : 0u;
+    const bool aGTE = __ballot(lane < S && bc < mc) == 0;
+    const bool bGTE = __ballot(lane < S && mc < bc) == 0;
+    return p.min_clock ? ((aGTE && bGTE) ? 0u : (aGTE ? 1u : (bGTE ? 2u : 3u))) : 0u;
+}
+
 template <int OPL, bool LISTS>
-__device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallLds &L, uint32_t d,
-                                              const hm_doc_row &doc, Outcome oc, const DocState &st) {
+__device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallLds &L, uint32_t d, uint32_t ds,
+                                              const hm_doc_row &doc, Outcome oc, const DocState &st, uint32_t mcmp) {
     const uint32_t lane = threadIdx.x;
     const uint32_t S = p.a_stride;
     const uint32_t n = doc.n_changes, A = doc.n_actors, R = doc.n_regs;
-    const uint32_t ds = hm_slot(p, d);      // row of the per-document outputs
-    hm_doc_result *dres = p.res_docs + ds;
+    hm_doc_result *dres = p.res_docs + ds;      // ds: row of the per-document outputs
     if (oc == OUT_ERROR) {
         // an Automerge throw aborted this document's Backend.applyChanges
         const u64 ek = *L.errkey;
@@ -1300,8 +1310,6 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
         }
         return;
     }
-    uint32_t mc = 0;
-    if (p.min_clock && lane < S) mc = p.min_clock[(size_t)ds * S + lane];
     for (uint32_t r = lane; r < R; r += WAVE) {
         hm_reg_result rr;
         rr.n_surv = L.survcnt[r]; rr.surv_off = L.regoff[r]; rr.obj = L.regobj[r];
@@ -1323,16 +1331,12 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
             for (uint32_t a = 0; a < S; a++) row[a] = a < NA_MAX ? (uint32_t)__popcll(an & L.chain[a]) : 0u;
         }
     }
-    uint32_t bc = 0;
     if (lane < S) {
         const bool ar = lane < A;
         p.res_clock[(size_t)ds * S + lane] = ar ? (uint32_t)__popcll(L.chain[lane]) : 0u;
         p.res_heads[(size_t)ds * S + lane] = ar ? L.headv[lane] : 0u;
-        bc = ar ? L.bclock[lane] : 0u;
-        p.res_back_clock[(size_t)ds * S + lane] = bc;              // DocBackend.clock (queued included)
+        p.res_back_clock[(size_t)ds * S + lane] = ar ? L.bclock[lane] : 0u;   // DocBackend.clock (queued included)
     }
-    const bool aGTE = __ballot(lane < S && bc < mc) == 0;
-    const bool bGTE = __ballot(lane < S && mc < bc) == 0;
     const bool act = lane < n;
     const u64 q = __ballot(act && st.hist == -1);
     if (act) p.res_hist[doc.change_off + lane] = st.hist;
@@ -1340,7 +1344,7 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
         hm_doc_result r = {};
         r.status = HM_OK; r.err_change = HM_NONE; r.err_op = HM_NONE;
         r.hist_len = st.H; r.n_queued = (uint32_t)__popcll(q); r.n_surv = st.total;
-        r.min_cmp = p.min_clock ? ((aGTE && bGTE) ? 0u : (aGTE ? 1u : (bGTE ? 2u : 3u))) : 0u;
+        r.min_cmp = mcmp;
         *dres = r;
     }
 #pragma unroll
@@ -1400,12 +1404,18 @@ void merge_small_kernel(SmallParams p) {
                             doc.n_regs <= p.cap_regs && doc.n_objs <= p.cap_objs && doc.n_objs >= 1 &&
                             doc.n_deps <= p.cap_deps && !p.general_only;
         DocState st;
+        // output row and minimumClock row requested before the merge: consumed before the next
+        // document's rows are requested (min_cmp_of), so neither waits behind that prefetch
+        const uint32_t ds = hm_slot(p, d);
+        uint32_t mc = 0;
+        if (p.min_clock && threadIdx.x < p.a_stride) mc = p.min_clock[(size_t)ds * p.a_stride + threadIdx.x];
         const Outcome oc = !dok ? OUT_INVALID : in_env ? merge_doc_small<OPL, LISTS>(p, L, doc, w0, w1, w2, st) : OUT_UNSUPPORTED;
+        const uint32_t mcmp = oc == OUT_OK ? min_cmp_of(p, L, doc, mc) : 0u;
 #if !HM_PREFETCH_EARLY
         if (more) { dokn = check_doc(p, docn); next = load_rows<OPL>(p, docn); }
 #endif
         STAMP(L, 9);
-        write_outputs<OPL, LISTS>(p, L, d, doc, oc, st);
+        write_outputs<OPL, LISTS>(p, L, d, ds, doc, oc, st, mcmp);
         wave_sync();
         STAMP(L, 10);
         if (!more) break;
