@@ -1395,10 +1395,21 @@ void merge_small_kernel(SmallParams p) {
         const bool more = dn < p.n_docs;
         bool dokn = true;
         hm_doc_row docn = {};
-        if (more) docn = p.docs[dn];
+        // the next document's row, one word per lane (lanes 0-11): nothing waits for it until it
+        // is read back after the merge (a uniform load would be moved to scalar registers at once,
+        // putting an HBM round trip in front of every document)
+        static_assert(sizeof(hm_doc_row) == 12 * sizeof(uint32_t), "doc row words");
+        uint32_t docw = 0;
+        if (more && threadIdx.x < 12) docw = reinterpret_cast<const uint32_t *>(p.docs + dn)[threadIdx.x];
+        auto take_docn = [&]() {
+            uint32_t w[12];
+#pragma unroll
+            for (int j = 0; j < 12; j++) w[j] = (uint32_t)__builtin_amdgcn_readlane((int)docw, j);
+            __builtin_memcpy(&docn, w, sizeof docn);
+        };
         Rows next;
 #if HM_PREFETCH_EARLY
-        if (more) { dokn = check_doc(p, docn); next = load_rows<OPL>(p, docn); }
+        if (more) { take_docn(); dokn = check_doc(p, docn); next = load_rows<OPL>(p, docn); }
 #endif
         const bool in_env = doc.n_changes <= 64 && doc.n_actors <= NA_MAX && doc.n_ops <= WAVE * OPL && doc.n_ops < 256 &&
                             doc.n_regs <= p.cap_regs && doc.n_objs <= p.cap_objs && doc.n_objs >= 1 &&
@@ -1412,7 +1423,7 @@ void merge_small_kernel(SmallParams p) {
         const Outcome oc = !dok ? OUT_INVALID : in_env ? merge_doc_small<OPL, LISTS>(p, L, doc, w0, w1, w2, st) : OUT_UNSUPPORTED;
         const uint32_t mcmp = oc == OUT_OK ? min_cmp_of(p, L, doc, mc) : 0u;
 #if !HM_PREFETCH_EARLY
-        if (more) { dokn = check_doc(p, docn); next = load_rows<OPL>(p, docn); }
+        if (more) { take_docn(); dokn = check_doc(p, docn); next = load_rows<OPL>(p, docn); }
 #endif
         STAMP(L, 9);
         write_outputs<OPL, LISTS>(p, L, d, ds, doc, oc, st, mcmp);
