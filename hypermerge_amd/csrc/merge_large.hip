@@ -684,13 +684,23 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
             tw[2 * h + 1] = 0xFFFF0000u;
         }
         bsync();
-        const uint32_t rounds = E ? 32 - __builtin_clz(E) : 0;
+        // in-place pointer jumping, three hops per round: every word keeps "value = sum from this
+        // entry up to its link" at every moment, and if every link spans >= L entries when a round
+        // starts it spans >= 4L after it (links only move forward) -> ceil(log4 E) rounds
+        const uint32_t rounds = E ? (33 - __builtin_clz(E)) / 2 : 0;
         for (uint32_t rd = 0; rd < rounds; rd++) {
             for (uint32_t e = tid; e < E; e += LWG) {
-                const uint32_t w = tw[e], x = w >> 16;
+                const uint32_t w = tw[e];
+                uint32_t x = w >> 16, sum = w & 0xFFFFu;
                 if (x == 0xFFFFu) continue;
-                const uint32_t w2 = tw[x];
-                tw[e] = (w2 & 0xFFFF0000u) | ((w & 0xFFFFu) + (w2 & 0xFFFFu));
+#pragma unroll
+                for (int hop = 0; hop < 3; hop++) {
+                    if (x == 0xFFFFu) break;
+                    const uint32_t w2 = tw[x];
+                    sum += w2 & 0xFFFFu;
+                    x = w2 >> 16;
+                }
+                tw[e] = (x << 16) | sum;
             }
             bsync();
         }
