@@ -71,7 +71,7 @@ def test_synthetic_parity(engine, name, n, extra):
     ("C3", 60, {"arrival": 2, "shuffle_pct": 20, "dup_pct": 3}),
     ("C2", 2000, {"dup_pct": 8, "arrival": 2, "shuffle_pct": 20}),   # > 64 changes with duplicates
     ("C4", 500, {"actors": 12, "changes_per_actor": 10}),  # > 8 actors
-    # general-kernel LDS arena boundaries (36 KB per workgroup):
+    # general-kernel LDS arena boundaries (150 KB per workgroup; the all-LDS path and the general path):
     ("C3", 40, {"actors": 12}),                            # > 8 actors: closure rows double-buffered in LDS
     ("C3", 4, {"changes_per_actor": 6000}),                # tour and L3 inputs too big for LDS, closure in LDS
     ("C3", 2, {"changes_per_actor": 12000}),               # closure rows too big for LDS as well
