@@ -424,7 +424,7 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
     LDS uint8_t *r_obj = w8(R);                 // 0xFF: HM_NONE
     LDS uint16_t *r_node = w16(R);
     LDS uint16_t *s_op = w16(m);                // survivors in output order
-    LDS uint16_t *n_pi = w16(R), *n_reg = w16(R), *n_ns = w16(R), *n_pl = w16(R);
+    LDS uint16_t *n_pi = w16(R), *n_reg = w16(R), *n_ns = w16(R), *n_pl = w16(R), *n_op = w16(R);
     LDS uint32_t *n_key = w32(R);
     LDS uint8_t *n_list = w8(R);
     LDS uint32_t *p_cnt = w32(NP), *p_off = w32(NP);
@@ -491,7 +491,7 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
                     const uint32_t i = atomicAdd(&sh.nins, 1u);
                     if (i < R) {                                   // more inserts than registers: a duplicate throws
                         const uint32_t pi = o.parent == HM_HEAD ? R + o.obj : o.parent;
-                        n_pi[i] = (uint16_t)pi; n_reg[i] = (uint16_t)o.reg; n_list[i] = (uint8_t)o.obj;
+                        n_pi[i] = (uint16_t)pi; n_reg[i] = (uint16_t)o.reg; n_list[i] = (uint8_t)o.obj; n_op[i] = (uint16_t)k;
                         n_key[i] = (o.elem << 8) | c_act[ci];
                         r_node[o.reg] = (uint16_t)i;
                         atomicAdd(&p_cnt[pi], 1u);
@@ -537,11 +537,18 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
     // ---- survivors and per-op checks (insert parents loaded from HBM up front, four per thread) ----
     bool any_list = false;
     for (uint32_t k0 = 0; k0 < m; k0 += 4 * LWG) {
+    // an insert's parent from its node (the op scan recorded it); only an insert whose register's
+    // node is another insert's (a duplicate: it throws) reads its row again
     uint32_t par[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
         const uint32_t k = k0 + tid + u * LWG;
-        par[u] = (k < m && dec_act(o_w[k]) == HM_INS) ? OP[k].parent : HM_HEAD;
+        par[u] = HM_HEAD;
+        if (k < m && dec_act(o_w[k]) == HM_INS) {
+            const uint32_t nd_ = r_node[dec_reg(o_w[k])];
+            if (nd_ != N16 && n_op[nd_] == k) { const uint32_t pi = n_pi[nd_]; par[u] = pi >= R ? HM_HEAD : pi; }
+            else par[u] = OP[k].parent;
+        }
     }
 #pragma unroll
     for (int u = 0; u < 4; u++) {
