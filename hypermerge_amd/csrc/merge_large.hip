@@ -137,22 +137,35 @@ __device__ __forceinline__ uint32_t block_excl_scan(Shared &sh, uint32_t v, uint
     *total = tot;
     return off + x - v;
 }
-// exclusive scan of arr[0..N) in place: each thread owns a contiguous run of ceil(N / LWG)
-// entries (its loads are independent, so they overlap), one block scan of the run sums
-// (P: a pool pointer or an LDS pointer)
-template <typename P>
-__device__ __forceinline__ uint32_t scan_array(Shared &sh, P arr, uint32_t N) {
+// exclusive scan of src[0..N) into dst (dst may be src): each thread owns a contiguous run of
+// ceil(N / LWG) entries (its loads are independent, so they overlap), one block scan of the run
+// sums.  Two barriers: the one after the wave totals are published, and the trailing one (dst
+// complete) — which also orders these reads of sh.scan before the next scan's writes.
+// (P, Q: pool or LDS pointers)
+template <typename P, typename Q>
+__device__ __forceinline__ uint32_t scan_into(Shared &sh, P src, Q dst, uint32_t N) {
     const uint32_t per = (N + LWG - 1) / LWG;
     const uint32_t b0 = threadIdx.x * per < N ? threadIdx.x * per : N;
     const uint32_t b1 = b0 + per < N ? b0 + per : N;
     uint32_t sum = 0;
-    for (uint32_t i = b0; i < b1; i++) sum += arr[i];
-    uint32_t tot;
-    uint32_t ex = block_excl_scan(sh, sum, &tot);
-    for (uint32_t i = b0; i < b1; i++) { const uint32_t v = arr[i]; arr[i] = ex; ex += v; }
+    for (uint32_t i = b0; i < b1; i++) sum += src[i];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane >= (uint32_t)o ? lane - o : lane) << 2), (int)x);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) sh.scan[w] = x;
+    bsync();
+    uint32_t off = 0, tot = 0;
+    for (uint32_t i = 0; i < LWG / 64; i++) { const uint32_t t = sh.scan[i]; off += i < w ? t : 0u; tot += t; }
+    uint32_t ex = off + x - sum;
+    for (uint32_t i = b0; i < b1; i++) { const uint32_t v = src[i]; dst[i] = ex; ex += v; }
     bsync();
     return tot;
 }
+template <typename P>
+__device__ __forceinline__ uint32_t scan_array(Shared &sh, P arr, uint32_t N) { return scan_into(sh, arr, arr, N); }
 
 struct Scratch {
     GLB uint32_t *tab, *h2a, *opchg, *segmax, *segcnt, *survcnt, *regoff, *regobj, *segoff, *segfill;
@@ -507,8 +520,8 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
         // counters, long assign lists, or a tour that does not fit over the dead region: pool path
         const uint32_t N = sh.nins < R ? sh.nins : R;
         const bool out = sh.ctrs || sh.grew || 2 * (N + O) + N > dead_end;
-        bsync();
-        if (out) {
+        if (out) {                                  // (uniform) every thread has read the flags
+            bsync();
             if (tid == 0) { sh.nins = 0; sh.ctrs = 0; }
             bsync();
             return RES_FALLBACK;
@@ -522,10 +535,7 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
         else sh.otype[obj] = dec_act(w);
     }
     // ---- assign lists: r_seg = exclusive offsets, advanced to the segment ends by the fill ----
-    for (uint32_t i = tid; i < R; i += LWG) r_seg[i] = r_segcnt[i];
-    bsync();
-    uint32_t tot2;
-    tot2 = scan_array(sh, r_seg, R);
+    const uint32_t tot2 = scan_into(sh, r_segcnt, r_seg, R);
     for (uint32_t k = tid; k < m; k += LWG) {
         const uint32_t w = o_w[k], a = dec_act(w);
         if (a < HM_SET || a > HM_INC || dec_obj(w) >= O) continue;     // exactly the ops r_segcnt counted
@@ -602,10 +612,7 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
     LSTAMP(4);
     // ---- survivor offsets and ranks: actor descending; equal actors (one change) by the
     //      sortBy(actor).reverse() flip, from the assigns applied on the register before each ----
-    for (uint32_t i = tid; i < R; i += LWG) r_soff[i] = r_scnt[i];
-    bsync();
-    uint32_t total;
-    total = scan_array(sh, r_soff, R);
+    const uint32_t total = scan_into(sh, r_scnt, r_soff, R);
     for (uint32_t j = tid; j < nsurv; j += LWG) {
         const uint32_t k = s_list[j], reg = dec_reg(o_w[k]), ck = o_chg[k], my_a = c_act[ck];
         const uint32_t cnt = r_scnt[reg];
@@ -647,11 +654,9 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
             if (tid == 0) sh.total = (uint32_t)__popcll(bm);
         }
         const uint32_t N = sh.nins;
-        for (uint32_t i = tid; i < NP; i += LWG) p_off[i] = p_cnt[i];
         bsync();
         const uint32_t nl = sh.total;
-        uint32_t tp;
-        tp = scan_array(sh, p_off, NP);
+        const uint32_t tp = scan_into(sh, p_cnt, p_off, NP);
         for (uint32_t i = tid; i < N; i += LWG) {
             const uint32_t pi = n_pi[i];
             if (p_cnt[pi] > 1) n_pl[atomicAdd(&p_off[pi], 1u)] = (uint16_t)i;
