@@ -166,6 +166,24 @@ __device__ __forceinline__ uint32_t scan_into(Shared &sh, P src, Q dst, uint32_t
 }
 template <typename P>
 __device__ __forceinline__ uint32_t scan_array(Shared &sh, P arr, uint32_t N) { return scan_into(sh, arr, arr, N); }
+// exclusive scan of f(0..N) into dst, for N <= LWG (one value per thread; the same two barriers)
+template <typename F, typename Q>
+__device__ __forceinline__ uint32_t scan_fn_small(Shared &sh, F f, Q dst, uint32_t N) {
+    const uint32_t i = threadIdx.x, lane = i & 63, w = i >> 6;
+    const uint32_t v = i < N ? f(i) : 0u;
+    uint32_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane >= (uint32_t)o ? lane - o : lane) << 2), (int)x);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) sh.scan[w] = x;
+    bsync();
+    uint32_t off = 0, tot = 0;
+    for (uint32_t k = 0; k < LWG / 64; k++) { const uint32_t t = sh.scan[k]; off += k < w ? t : 0u; tot += t; }
+    if (i < N) dst[i] = off + x - v;
+    bsync();
+    return tot;
+}
 
 struct Scratch {
     GLB uint32_t *tab, *h2a, *opchg, *segmax, *segcnt, *survcnt, *regoff, *regobj, *segoff, *segfill;
@@ -450,11 +468,13 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
     auto key_of = [&](uint32_t k, uint32_t ci) -> uint32_t { return c_kb[ci] + (k - c_op0[ci]); };
 
     // ---- key bases: ops of the changes before each history position ----
-    for (uint32_t h = tid; h < H; h += LWG) c_tmp[h] = sCH[lh2a[h]].n_ops;
-    bsync();
-    uint32_t m_applied;
-    m_applied = scan_array(sh, c_tmp, H);
-    (void)m_applied;
+    if (H <= LWG) {
+        scan_fn_small(sh, [&](uint32_t h) -> uint32_t { return sCH[lh2a[h]].n_ops; }, c_tmp, H);
+    } else {
+        for (uint32_t h = tid; h < H; h += LWG) c_tmp[h] = sCH[lh2a[h]].n_ops;
+        bsync();
+        scan_array(sh, c_tmp, H);
+    }
     // ---- staging: per-change inputs, op -> change, object / register / parent tables ----
     for (uint32_t i = tid; i < n; i += LWG) {
         const hm_change_row c = sCH[i];
@@ -804,17 +824,14 @@ __device__ __forceinline__ int merge_doc_res(const SmallParams &p, Shared &sh, L
     }
     bsync();
     if (sh.flags) return RES_FALLBACK;
-    if (tid == 0) {
-        uint32_t t = 0;
-        for (uint32_t a = 0; a < A; a++) { sh.tabo[a] = t; if (sh.maxs[a]) t += sh.maxs[a] - sh.base[a] + 1; }
-        sh.tabo[A] = t;
-    }
-    bsync();
-    const uint32_t T = sh.tabo[A];
+    // table offsets per actor, computed by every thread (A <= 8) and published by thread 0
+    uint32_t T = 0;
+    for (uint32_t a = 0; a < A; a++) { if (tid == 0) sh.tabo[a] = T; if (sh.maxs[a]) T += sh.maxs[a] - sh.base[a] + 1; }
+    if (tid == 0) sh.tabo[A] = T;
     if (T > 4 * n + 64 || n * A + T > stage_base) return RES_FALLBACK;
     LDS uint32_t *lt = ar, *lc = ar + T;            // L1 table, L2 closure rows (stride A)
     for (uint32_t i = tid; i < T; i += LWG) lt[i] = 0xFFFFFFFFu;
-    bsync();
+    bsync();                                        // (also publishes sh.tabo)
     auto slot_of = [&](uint32_t a, uint32_t s) -> uint32_t {
         if (a >= A || s < sh.base[a] || s > sh.maxs[a] || sh.maxs[a] == 0) return 0xFFFFFFFFu;
         return sh.tabo[a] + (s - sh.base[a]);
@@ -839,10 +856,21 @@ __device__ __forceinline__ int merge_doc_res(const SmallParams &p, Shared &sh, L
         if (!ok) sh.all_ok = 0;
     }
     bsync();
-    const bool all_ready = sh.all_ok != 0;
-    bsync();
+    const bool all_ready = sh.all_ok != 0;          // (next written after the history scan's barriers)
     if (!all_ready) return RES_FALLBACK;
-    {
+    if (n <= LWG) {
+        H_out = 0;
+        const uint32_t Hc = scan_fn_small(sh, [&](uint32_t i) -> uint32_t {
+            const hm_change_row c = sCH[i];
+            return lt[slot_of(c.actor, c.seq)] == i ? 1u : 0u;
+        }, lh, n);
+        // lh holds exclusive counts: a change is applied iff it is its key's first arrival
+        for (uint32_t i = tid; i < n; i += LWG) {
+            const hm_change_row c = sCH[i];
+            if (lt[slot_of(c.actor, c.seq)] == i) lh2a[lh[i]] = i; else lh[i] = -2;
+        }
+        if (tid == 0) sh.H = Hc;
+    } else {
         uint32_t carry = 0;
         for (uint32_t c0 = 0; c0 < n; c0 += LWG) {
             const uint32_t i = c0 + tid;
@@ -872,6 +900,7 @@ __device__ __forceinline__ int merge_doc_res(const SmallParams &p, Shared &sh, L
         if (row[c.actor] < c.seq - 1) row[c.actor] = c.seq - 1;
     }
     if (tid < 3) sh.gflag[tid] = 0;
+    if (tid == 0) sh.all_ok = 1;                    // the literal-fold check's flag (L1 read it two barriers ago)
     bsync();
     auto lslot = [&](uint32_t a, uint32_t sq) -> uint32_t {      // applied change (a, sq) or >= n
         if (sq < sh.base[a] || sq > sh.maxs[a] || sh.maxs[a] == 0) return 0xFFFFFFFFu;
@@ -921,8 +950,6 @@ __device__ __forceinline__ int merge_doc_res(const SmallParams &p, Shared &sh, L
         }
     }
     LSTAMP(2);
-    if (tid == 0) sh.all_ok = 1;
-    bsync();
     uint32_t *cur = p.res_all_deps + (size_t)doc.change_off * S;
     for (uint32_t i = tid; i < n; i += LWG) {
         uint32_t *grow_ = cur + (size_t)i * S;
