@@ -742,12 +742,15 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
                 uint32_t clo = (uint32_t)dall, chi = (uint32_t)(dall >> 32);
                 const uint32_t Hs = (uint32_t)__builtin_amdgcn_readfirstlane((int)n);
                 const uint32_t H1 = Hs < 32 ? Hs : 32;
+// (both readlanes first: the two SGPR results cover each other's readlane -> VALU hazard)
 #define WARSHALL_LO(k) do { const uint32_t m_ = (uint32_t)__builtin_amdgcn_sbfe((int)clo, (k), 1);              \
-                            clo |= (uint32_t)__builtin_amdgcn_readlane((int)clo, (int)(k)) & m_;                 \
-                            chi |= (uint32_t)__builtin_amdgcn_readlane((int)chi, (int)(k)) & m_; } while (0)
+                            const uint32_t rl_ = (uint32_t)__builtin_amdgcn_readlane((int)clo, (int)(k));        \
+                            const uint32_t rh_ = (uint32_t)__builtin_amdgcn_readlane((int)chi, (int)(k));        \
+                            clo |= rl_ & m_; chi |= rh_ & m_; } while (0)
 #define WARSHALL_HI(k) do { const uint32_t m_ = (uint32_t)__builtin_amdgcn_sbfe((int)chi, (k) - 32, 1);         \
-                            clo |= (uint32_t)__builtin_amdgcn_readlane((int)clo, (int)(k)) & m_;                 \
-                            chi |= (uint32_t)__builtin_amdgcn_readlane((int)chi, (int)(k)) & m_; } while (0)
+                            const uint32_t rl_ = (uint32_t)__builtin_amdgcn_readlane((int)clo, (int)(k));        \
+                            const uint32_t rh_ = (uint32_t)__builtin_amdgcn_readlane((int)chi, (int)(k));        \
+                            clo |= rl_ & m_; chi |= rh_ & m_; } while (0)
 #pragma unroll
                 for (int g = 0; g < 32; g += 8) {
                     if ((uint32_t)g >= H1) break;
@@ -1011,8 +1014,9 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         const uint32_t H1 = Hs < 32 ? Hs : 32;
 #define PUSH_LO(k) alo |= (uint32_t)__builtin_amdgcn_readlane((int)alo, (int)(k)) & (uint32_t)__builtin_amdgcn_sbfe((int)Dlo, (k), 1)
 #define PUSH_HI(k) do { const uint32_t m_ = (uint32_t)__builtin_amdgcn_sbfe((int)Dhi, (k) - 32, 1);          \
-                        alo |= (uint32_t)__builtin_amdgcn_readlane((int)alo, (int)(k)) & m_;              \
-                        ahi |= (uint32_t)__builtin_amdgcn_readlane((int)ahi, (int)(k)) & m_; } while (0)
+                        const uint32_t rl_ = (uint32_t)__builtin_amdgcn_readlane((int)alo, (int)(k));     \
+                        const uint32_t rh_ = (uint32_t)__builtin_amdgcn_readlane((int)ahi, (int)(k));     \
+                        alo |= rl_ & m_; ahi |= rh_ & m_; } while (0)
         // Fully unrolled with immediate lane indices (no scalar index arithmetic per step), one
         // wave-uniform check per group of 8.  Steps at positions >= H are no-ops: those lanes
         // hold no ancestors and no lane depends on them.  (A blocked variant — 4 positions per
