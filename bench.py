@@ -131,7 +131,12 @@ def main() -> int:
     # over RCCL through the C-ABI (hm_clock_allgather), plus the replica min-clock
     xchg = None
     if ws > 1:
-        xchg = _clock_exchange(eng, batch, run, dev, rank, ws, cfg)
+        # off the merge's critical path and outside `value`: a failure here is reported in the
+        # line instead of costing the whole scaling measurement
+        try:
+            xchg = _clock_exchange(eng, batch, run, dev, rank, ws, cfg)
+        except Exception as ex:                       # noqa: BLE001 (reported, not hidden)
+            xchg = {"error": f"{type(ex).__name__}: {ex}"[:300]}
 
     value = applied_all * args.steps / wall_max
     ms_per_step = wall_max * 1000.0 / args.steps
