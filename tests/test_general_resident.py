@@ -76,9 +76,24 @@ def test_text_and_mixed_docs_general_engine(engine_general, name, n, extra):
 
 def test_resident_path_repeatable(engine_general):
     """Workgroups reuse the LDS arena and the pool across documents: merging the same batch
-    twice, and a batch in reverse document order, gives the same per-document results."""
+    twice gives the same results (nothing depends on what an earlier document left behind)."""
     b = synth.generate(synth.config("C3", n_docs=64))
     g1 = engine_general.merge(b)
     g2 = engine_general.merge(b)
     for f in ("docs", "regs", "surv", "hist", "all_deps", "clock", "heads"):
         np.testing.assert_array_equal(getattr(g1, f), getattr(g2, f))
+
+
+def _single_actor_chain(n_changes, keys=128):
+    """One actor, no listed deps (each change's own predecessor only): more changes than the
+    workgroup has threads while the rows still fit the LDS path (the multi-chunk history and
+    key-base scans); <= 64 assigns per key, so the LDS path keeps the document."""
+    return [ch(A, i + 1, {}, s(f"k{i % keys}", i)) for i in range(n_changes)]
+
+
+@pytest.mark.parametrize("n", [1000, 1024, 1025, 1150])
+def test_more_changes_than_threads(engine, engine_general, n):
+    b = encode([_single_actor_chain(n), _single_actor_chain(n // 3)])
+    o = O.merge(b)
+    assert_same(b, engine.merge(b), o)
+    assert_same(b, engine_general.merge(b), o)
