@@ -1233,12 +1233,22 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
             }
         }
     }
+    // survivor slots: op index (8 bits; < 256 ops per document) and, in counter launches, what
+    // the inc pass needs about the survivor without chasing op -> change -> history through LDS:
+    // bit 15 a counter set (int or float), bit 14 an integral one, bits 8-13 its change's
+    // history position
 #pragma unroll
     for (int t = 0; t < OPL; t++) {
         if (!surv[t]) continue;
         const uint32_t pos = rb0[t] + rank[t];
-        L.survop[pos] = (uint16_t)(lane + WAVE * t);
-        if (p.counters) L.survsum[pos] = 0;
+        uint32_t tag = 0;
+        if (p.counters) {
+            const uint32_t mt = L.opmeta[lane + WAVE * t], vt = (mt >> 16) & 0xFF;
+            const bool cset = (mt & 0xFF) == HM_SET && ((mt >> 8) & 0xFF) == HM_DT_COUNTER && (vt == HM_V_INT || vt == HM_V_FLOAT);
+            tag = cset ? (0x8000u | (vt == HM_V_INT ? 0x4000u : 0u) | ((uint32_t)oh[t] << 8)) : 0u;
+            L.survsum[pos] = 0;
+        }
+        L.survop[pos] = (uint16_t)((lane + WAVE * t) | tag);
     }
     wave_sync();
     STAMP(L, 8);
@@ -1262,9 +1272,8 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
             const uint32_t q = lane + WAVE * t;
             basev[t] = 0;
             if (q < total) {
-                const uint32_t k = L.survop[q], mt = L.opmeta[k];
-                if ((mt & 0xFF) == HM_SET && ((mt >> 8) & 0xFF) == HM_DT_COUNTER && ((mt >> 16) & 0xFF) == HM_V_INT)
-                    basev[t] = op_value(L, k);
+                const uint32_t sw = L.survop[q];
+                if ((sw & 0xC000u) == 0xC000u) basev[t] = op_value(L, sw & 0xFFu);     // an integral counter set
             }
         }
 #pragma unroll
@@ -1276,12 +1285,11 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
             const uint32_t my_vtag = (L.opmeta[k] >> 16) & 0xFF;
             const int64_t v = incv[t];
             for (uint32_t q = 0; q < cnt; q++) {
-                const uint32_t k2 = L.survop[b0 + q];
-                const uint32_t m2 = L.opmeta[k2], vt2 = (m2 >> 16) & 0xFF;
-                if ((m2 & 0xFF) != HM_SET || ((m2 >> 8) & 0xFF) != HM_DT_COUNTER || (vt2 != HM_V_INT && vt2 != HM_V_FLOAT)) continue;
-                if (!((an >> L.hist_of[L.opchg[k2] & 0xFFu]) & 1)) continue;
+                const uint32_t sw = L.survop[b0 + q];
+                if (!(sw & 0x8000u)) continue;                                  // not a counter set
+                if (!((an >> ((sw >> 8) & 63u)) & 1)) continue;                  // concurrent inc: no effect
                 // f64 counters need the ordered sum
-                if (vt2 != HM_V_INT || my_vtag != HM_V_INT || (u64)(v < 0 ? -v : v) >= (1ull << 44)) { outside = true; continue; }
+                if (!(sw & 0x4000u) || my_vtag != HM_V_INT || (u64)(v < 0 ? -v : v) >= (1ull << 44)) { outside = true; continue; }
                 lds_add((LDS u64 *)&L.survsum[b0 + q], (unsigned long long)v);
             }
         }
@@ -1396,7 +1404,7 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
     for (int t = 0; t < OPL; t++) {
         const uint32_t q = lane + WAVE * t;
         if (q >= st.total) continue;
-        const uint32_t k = L.survop[q], mt = L.opmeta[k];
+        const uint32_t k = L.survop[q] & 0xFFu, mt = L.opmeta[k];
         const u64 v = op_value(L, k);
         hm_surv_result sr;
         sr.op = k; sr.vtag = (mt >> 16) & 0xFF; sr.value = v;
