@@ -147,7 +147,7 @@ struct SmallLds {
     LDS uint8_t *h2a, *chactor, *objtype;
     LDS uint16_t *opchg;            // op -> arrival index of its change | actor rank << 8
     // K3 (RGA lists); carved only for launches with list documents
-    LDS uint32_t *nins, *pcount, *poff, *pfill, *nodekey, *tour0, *tour1, *listbase;
+    LDS uint32_t *nins, *pcount, *poff, *pfill, *nodekey, *tour0, *listbase;   // tour ranked in place
     LDS uint16_t *nodeop, *nodepi, *regnode, *plist, *fc, *ns, *listid;
     LDS u64 *stamps;                // HM_STAMPS builds: [HM_NSTAMP] cycle sums + last stamp
 };
@@ -189,7 +189,7 @@ __host__ __device__ inline size_t small_carve(P base, uint32_t NOp, uint32_t NR,
         TAKE(opelem, uint32_t, NOp);
         TAKE(nins, uint32_t, 1);      TAKE(pcount, uint32_t, NP);  TAKE(poff, uint32_t, NP);
         TAKE(pfill, uint32_t, NP);    TAKE(nodekey, uint32_t, NOp); TAKE(tour0, uint32_t, NE);
-        TAKE(tour1, uint32_t, NE);    TAKE(listbase, uint32_t, NO + 1);
+        TAKE(listbase, uint32_t, NO + 1);
         TAKE(nodeop, uint16_t, NOp);  TAKE(nodepi, uint16_t, NOp); TAKE(regnode, uint16_t, NR);
         TAKE(plist, uint16_t, NOp);   TAKE(fc, uint16_t, NP);      TAKE(ns, uint16_t, NOp);
         TAKE(listid, uint16_t, NO);
@@ -344,17 +344,25 @@ __device__ __forceinline__ void rga_order(const SmallLds &L, uint32_t R, uint32_
         L.tour0[2 * h + 1] = END << 16;
     }
     wave_sync();
-    LDS uint32_t *cur = L.tour0, *nxt = L.tour1;
-    const uint32_t rounds = E ? 32 - __builtin_clz(E) : 0;
+    // in-place pointer jumping, three hops per round: a word (link << 16 | sum up to the link) is
+    // read and written whole, so every word is consistent at every moment, and links spanning
+    // >= L entries when a round starts span >= 4L after it -> ceil(log4 E) rounds
+    LDS uint32_t *cur = L.tour0;
+    const uint32_t rounds = E ? (33 - __builtin_clz(E)) / 2 : 0;
     for (uint32_t rd = 0; rd < rounds; rd++) {
         for (uint32_t e = lane; e < E; e += WAVE) {
-            uint32_t x = cur[e];
-            const uint32_t nx = x >> 16;
-            if (nx != END) { const uint32_t y = cur[nx]; x = (y & 0xFFFF0000u) | ((x & 0xFFFFu) + (y & 0xFFFFu)); }
-            nxt[e] = x;
+            const uint32_t x = cur[e];
+            uint32_t nx = x >> 16, sum = x & 0xFFFFu;
+#pragma unroll
+            for (int hop = 0; hop < 3; hop++) {
+                if (nx == END) break;
+                const uint32_t y = cur[nx];
+                sum += y & 0xFFFFu;
+                nx = y >> 16;
+            }
+            cur[e] = (nx << 16) | sum;
         }
         wave_sync();
-        LDS uint32_t *tmp = cur; cur = nxt; nxt = tmp;
     }
     // list sizes -> base positions; pre-order position of every node
     uint32_t lb = 0;
