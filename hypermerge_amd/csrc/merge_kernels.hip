@@ -44,7 +44,7 @@
 #ifndef HM_STAMPS
 #define HM_STAMPS 0     // diagnostic builds only: per-phase s_memtime shares (tools/stamps.py); never timed
 #endif
-#define HM_NSTAMP 16
+#define HM_NSTAMP 12
 #ifndef HM_PREFETCH_EARLY
 #define HM_PREFETCH_EARLY 0 // 1: the next document's rows are loaded before this document's merge
 #endif
@@ -739,45 +739,17 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
             const uint32_t INF = 0xFFu;
             const bool has_dup = dupm != 0;
             const bool kl = act && !dup;                            // this lane is its key's first arrival
-            // t(K) from the ancestor closure of the dependency masks (dall: first-arrival lanes),
-            // by Warshall's algorithm over the arrival lanes — any vertex order works, so no
-            // topological order is needed before the history exists: 64 readlane steps instead of
-            // a one-hop-per-iteration fixpoint (as deep as the dependency chains).  t(K) = the
-            // latest arrival among K and its ancestors; INF if K or an ancestor can never apply
-            // (a dep outside the batch, or a dependency cycle: K among its own ancestors).
-            uint32_t t;
-            {
-                uint32_t clo = (uint32_t)dall, chi = (uint32_t)(dall >> 32);
-                const uint32_t Hs = (uint32_t)__builtin_amdgcn_readfirstlane((int)n);
-                const uint32_t H1 = Hs < 32 ? Hs : 32;
-// (both readlanes first: the two SGPR results cover each other's readlane -> VALU hazard)
-#define WARSHALL_LO(k) do { const uint32_t m_ = (uint32_t)__builtin_amdgcn_sbfe((int)clo, (k), 1);              \
-                            const uint32_t rl_ = (uint32_t)__builtin_amdgcn_readlane((int)clo, (int)(k));        \
-                            const uint32_t rh_ = (uint32_t)__builtin_amdgcn_readlane((int)chi, (int)(k));        \
-                            clo |= rl_ & m_; chi |= rh_ & m_; } while (0)
-#define WARSHALL_HI(k) do { const uint32_t m_ = (uint32_t)__builtin_amdgcn_sbfe((int)chi, (k) - 32, 1);         \
-                            const uint32_t rl_ = (uint32_t)__builtin_amdgcn_readlane((int)clo, (int)(k));        \
-                            const uint32_t rh_ = (uint32_t)__builtin_amdgcn_readlane((int)chi, (int)(k));        \
-                            clo |= rl_ & m_; chi |= rh_ & m_; } while (0)
-#pragma unroll
-                for (int g = 0; g < 32; g += 8) {
-                    if ((uint32_t)g >= H1) break;
-                    WARSHALL_LO(g); WARSHALL_LO(g + 1); WARSHALL_LO(g + 2); WARSHALL_LO(g + 3);
-                    WARSHALL_LO(g + 4); WARSHALL_LO(g + 5); WARSHALL_LO(g + 6); WARSHALL_LO(g + 7);
-                }
-#pragma unroll
-                for (int g = 32; g < 64; g += 8) {
-                    if ((uint32_t)g >= Hs) break;
-                    WARSHALL_HI(g); WARSHALL_HI(g + 1); WARSHALL_HI(g + 2); WARSHALL_HI(g + 3);
-                    WARSHALL_HI(g + 4); WARSHALL_HI(g + 5); WARSHALL_HI(g + 6); WARSHALL_HI(g + 7);
-                }
-#undef WARSHALL_LO
-#undef WARSHALL_HI
-                const u64 C = ((u64)chi << 32) | clo;
-                const bool self = (C >> lane) & 1;
-                const u64 dead = __ballot(kl && (never || self));        // keys that never apply
-                const uint32_t hb = C ? 63u - (uint32_t)__builtin_clzll(C) : 0u;
-                t = (!kl || never || self || (C & dead)) ? INF : (hb > lane ? hb : lane);
+            uint32_t t = (!kl || never) ? INF : lane;
+            for (uint32_t it = 0; it <= n; it++) {
+                tx[lane] = t;
+                wave_sync();
+                uint32_t nt = t;
+                if (kl && t != INF)
+                    for (u64 m = dall; m; m &= m - 1) { const uint32_t x = tx[__builtin_ctzll(m)]; nt = nt > x ? nt : x; }
+                wave_sync();
+                const bool grew = nt != t;
+                t = nt;
+                if (__ballot(grew) == 0) break;
             }
             // every copy learns its key's t; key word = t << 16 | pass << 8 | pos
             tx[lane] = t;
@@ -786,7 +758,6 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
             wave_sync();
             uint32_t w = (!kl || t == INF) ? 0xFFFFFFFFu : ((t << 16) | ((t == lane ? 1u : 2u) << 8) | lane);
             bool conv = false;
-            STAMP(L, 12);
             for (uint32_t it = 0; it <= n + 1; it++) {
                 tx[lane] = w;                                       // meaningful on key lanes
                 if (has_dup) tm[lane] = 0xFFFFFFFFu;
@@ -816,7 +787,6 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
             }
             tx[lane] = w;
             wave_sync();
-            STAMP(L, 13);
             const uint32_t wk = act && tk != INF ? tx[key] : 0xFFFFFFFFu;
             const bool apl = wk != 0xFFFFFFFFu && (wk & 0xFFu) == lane;
             const uint32_t hk = apl ? wk : 0xFFFFFFFFu;
@@ -826,29 +796,15 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
                 for (u64 m = dall; m; m &= m - 1) bad |= tx[__builtin_ctzll(m)] >= hk;
             wave_sync();
             if (conv && __ballot(bad) == 0) {
-                // rank of hk among the applied copies' keys: radix by ballots, MSB first (t < 64,
-                // pass <= 0xFE, pos < 64: 20 key bits); eq = lanes whose key prefix equals mine
                 uint32_t rank = 0;
-                {
-                    const uint32_t key20 = ((hk >> 16) << 14) | (((hk >> 8) & 0xFFu) << 6) | (hk & 63u);
-                    u64 eq = __ballot(apl);
-#pragma unroll
-                    for (int bit = 19; bit >= 0; bit--) {
-                        const u64 ones = __ballot(apl && ((key20 >> bit) & 1));
-                        const bool mine = (key20 >> bit) & 1;
-                        rank += mine ? (uint32_t)__popcll(eq & ~ones) : 0u;
-                        eq &= mine ? ones : ~ones;
-                    }
-                }
+                for (uint32_t j = 0; j < n; j++) rank += (uint32_t)__builtin_amdgcn_readlane((int)hk, (int)j) < hk ? 1u : 0u;
                 hist = apl ? (int32_t)rank : (act && tk != INF ? -2 : -1);
                 H = (uint32_t)__popcll(__ballot(apl));
                 if (apl && dup) L.first[a8 * 64 + (slot & 63)] = lane;   // (actor, seq) -> applied copy
                 copy_applied = __ballot(apl && dup) != 0;
                 solved = true;
-                STAMP(L, 14);
             }
         }
-        if (!solved) STAMP(L, 15);
         for (uint32_t i = 0; i < n && !solved; i++) {
             queue |= 1ull << i;
             u64 P = __ballot(lane == i && !never && (dall & ~applied) == 0);
@@ -1022,9 +978,8 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         const uint32_t H1 = Hs < 32 ? Hs : 32;
 #define PUSH_LO(k) alo |= (uint32_t)__builtin_amdgcn_readlane((int)alo, (int)(k)) & (uint32_t)__builtin_amdgcn_sbfe((int)Dlo, (k), 1)
 #define PUSH_HI(k) do { const uint32_t m_ = (uint32_t)__builtin_amdgcn_sbfe((int)Dhi, (k) - 32, 1);          \
-                        const uint32_t rl_ = (uint32_t)__builtin_amdgcn_readlane((int)alo, (int)(k));     \
-                        const uint32_t rh_ = (uint32_t)__builtin_amdgcn_readlane((int)ahi, (int)(k));     \
-                        alo |= rl_ & m_; ahi |= rh_ & m_; } while (0)
+                        alo |= (uint32_t)__builtin_amdgcn_readlane((int)alo, (int)(k)) & m_;              \
+                        ahi |= (uint32_t)__builtin_amdgcn_readlane((int)ahi, (int)(k)) & m_; } while (0)
         // Fully unrolled with immediate lane indices (no scalar index arithmetic per step), one
         // wave-uniform check per group of 8.  Steps at positions >= H are no-ops: those lanes
         // hold no ancestors and no lane depends on them.  (A blocked variant — 4 positions per
