@@ -52,6 +52,16 @@
 #define HM_WAVES_PER_EU_OPL4 3  // 256 ops per document: the op arrays need a larger register budget (measured:
                                 // C2 0.87 -> 0.65 ms at 3 waves/SIMD; list launches (C5) best at 2: 3.99 -> 3.25 ms)
 #endif
+// Wave priority (s_setprio) for the phases other waves should not hold up: the ancestor push
+// (64 dependent readlane steps: a lower-priority wave's VALU issue fills its hazard gaps) and a
+// wave's store / next-row staging (its memory requests go out sooner).  C4 A/B over priorities
+// 0-3 (profiles/r02 commit log): 2.53 -> 2.43-2.44 ms with (2, 1).
+#ifndef HM_PRIO_PUSH
+#define HM_PRIO_PUSH 2
+#endif
+#ifndef HM_PRIO_IO
+#define HM_PRIO_IO 1
+#endif
 #ifndef HM_WAVES_PER_EU
 #define HM_WAVES_PER_EU 4   // register-allocator target: LDS already caps C4-class launches at ~4.25 waves/SIMD
 #endif
@@ -973,6 +983,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     uint32_t alo = hv && lane < 32 ? 1u << lane : 0u, ahi = hv && lane >= 32 ? 1u << (lane - 32) : 0u;
     if (HM_ABLATE & 1024) return OUT_UNSUPPORTED;
     {
+        if (HM_PRIO_PUSH) __builtin_amdgcn_s_setprio(HM_PRIO_PUSH);
         const uint32_t Hs = (uint32_t)__builtin_amdgcn_readfirstlane((int)H);
         const uint32_t Dlo = (uint32_t)D, Dhi = (uint32_t)(D >> 32);
         const uint32_t H1 = Hs < 32 ? Hs : 32;
@@ -998,6 +1009,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         }
 #undef PUSH_LO
 #undef PUSH_HI
+        if (HM_PRIO_PUSH) __builtin_amdgcn_s_setprio(0);
     }
     const u64 anc = hv ? ((((u64)ahi << 32) | alo) & ~(1ull << lane)) : 0ull;   // strict ancestors
     if (hv) L.anc[lane] = anc;
@@ -1442,11 +1454,13 @@ void merge_small_kernel(SmallParams p) {
         if (more) { take_docn(); dokn = check_doc(p, docn); next = load_rows<OPL>(p, docn); }
 #endif
         STAMP(L, 9);
+        if (HM_PRIO_IO) __builtin_amdgcn_s_setprio(HM_PRIO_IO);
         write_outputs<OPL, LISTS>(p, L, d, ds, doc, oc, st, mcmp);
         wave_sync();
         STAMP(L, 10);
         if (!more) break;
         stage_rows<OPL, LISTS>(p, L, docn, next);
+        if (HM_PRIO_IO) __builtin_amdgcn_s_setprio(0);
         w0 = next.c0; w1 = next.c1; w2 = next.c2;
         wave_sync();
         STAMP(L, 11);
