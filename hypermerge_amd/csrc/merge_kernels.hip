@@ -62,6 +62,18 @@
 #ifndef HM_PRIO_IO
 #define HM_PRIO_IO 1
 #endif
+#ifndef HM_PRIO_HIST
+#define HM_PRIO_HIST 2      // through the queued-change history (K1 slow paths): actor-major C4 4.59 -> 4.34 ms
+#endif
+#ifndef HM_PRIO_RANK
+#define HM_PRIO_RANK 2      // through the survivor offsets, ranks and ties: C4 2.42 -> 2.39 ms
+#endif
+#ifndef HM_PRIO_K2
+#define HM_PRIO_K2 0        // dev A/B: priority through the K2 op scan and survivor tests
+#endif
+#ifndef HM_PRIO_K1
+#define HM_PRIO_K1 2        // through validation and the dependency pre-pass: C4 2.41 -> 2.37 ms
+#endif
 #ifndef HM_WAVES_PER_EU
 #define HM_WAVES_PER_EU 4   // register-allocator target: LDS already caps C4-class launches at ~4.25 waves/SIMD
 #endif
@@ -586,6 +598,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     // ---------------- the staged rows (lane = arrival index) ----------------
     if (HM_ABLATE & 8) return OUT_UNSUPPORTED;
     STAMP(L, 0);
+    if (HM_PRIO_K1) __builtin_amdgcn_s_setprio(HM_PRIO_K1);
     const bool act = lane < n;
     const hm_change_row c = change_of(w0, w1, w2);      // zero rows for lanes >= n (load_rows)
     clear_first(L.first);
@@ -688,7 +701,10 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     int32_t hist = -1;
     uint32_t H = 0;
     bool identity = false;                // history == arrival order (no queueing, no duplicates)
-    if (__ballot(act && !ok) == 0) {
+    if (HM_PRIO_K1) __builtin_amdgcn_s_setprio(0);
+    const bool queued_doc = __ballot(act && !ok) != 0;
+    if (HM_PRIO_HIST && queued_doc) __builtin_amdgcn_s_setprio(HM_PRIO_HIST);
+    if (!queued_doc) {
         // every change was ready on arrival: history = arrival order minus duplicates
         const u64 appl = __ballot(act && !dup);
         if (act) hist = dup ? -2 : (int32_t)__popcll(appl & ((1ull << lane) - 1));
@@ -945,6 +961,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         }
     }
 
+    if (HM_PRIO_HIST && queued_doc) __builtin_amdgcn_s_setprio(0);
     STAMP(L, 3);
     if (HM_ABLATE & 512) return OUT_UNSUPPORTED;
     // ---------------- K1b: ancestor sets in history order ----------------
@@ -1051,6 +1068,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     wave_sync();
 
     STAMP(L, 5);
+    if (HM_PRIO_K2) __builtin_amdgcn_s_setprio(HM_PRIO_K2);
     if (HM_ABLATE & 2) return OUT_UNSUPPORTED;
     // ---------------- K2: ops (lane + 64*t) ----------------
     uint32_t oreg[OPL], oobj[OPL], opar[OPL], oact[OPL], okey[OPL], oarr[OPL], oelem[OPL], oactor[OPL];
@@ -1136,6 +1154,8 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     if (*L.flags & FL_UNSUPPORTED) return OUT_UNSUPPORTED;
 
     STAMP(L, 7);
+    if (HM_PRIO_K2 && !HM_PRIO_RANK) __builtin_amdgcn_s_setprio(0);
+    if (HM_PRIO_RANK) __builtin_amdgcn_s_setprio(HM_PRIO_RANK);
     if (HM_ABLATE & 4) return OUT_UNSUPPORTED;
     // survivor offsets: exclusive scan over register ids (a register's count = its byte sum)
     uint32_t total = 0;
@@ -1226,6 +1246,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         L.survop[pos] = (uint16_t)((lane + WAVE * t) | tag);
     }
     wave_sync();
+    if (HM_PRIO_RANK) __builtin_amdgcn_s_setprio(0);
     STAMP(L, 8);
     if (HM_ABLATE & 256) return OUT_UNSUPPORTED;
     if constexpr (LISTS) {
