@@ -63,7 +63,7 @@
 #define HM_PRIO_IO 1
 #endif
 #ifndef HM_PRIO_HIST
-#define HM_PRIO_HIST 2      // through the queued-change history (K1 slow paths): actor-major C4 4.59 -> 4.34 ms
+#define HM_PRIO_HIST 3      // through the queued-change history (K1 slow paths): actor-major C4 4.59 -> 4.34 ms (2), 4.20 ms (3)
 #endif
 #ifndef HM_PRIO_RANK
 #define HM_PRIO_RANK 2      // through the survivor offsets, ranks and ties: C4 2.42 -> 2.39 ms
@@ -72,7 +72,7 @@
 #define HM_PRIO_K2 0        // dev A/B: priority through the K2 op scan and survivor tests
 #endif
 #ifndef HM_PRIO_K1
-#define HM_PRIO_K1 2        // through validation and the dependency pre-pass: C4 2.41 -> 2.37 ms
+#define HM_PRIO_K1 3        // through validation and the dependency pre-pass: C4 2.41 -> 2.37 ms
 #endif
 #ifndef HM_WAVES_PER_EU
 #define HM_WAVES_PER_EU 4   // register-allocator target: LDS already caps C4-class launches at ~4.25 waves/SIMD
