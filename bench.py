@@ -63,7 +63,7 @@ def main() -> int:
                     help="skip the resident-store leg (1-2 new changes per resident document per round)")
     ap.add_argument("--no-node", action="store_true",
                     help="skip the Node DocBackend leg (C2 sample: JS restatement vs the GPU drop-in)")
-    ap.add_argument("--node-docs", type=int, default=2000)
+    ap.add_argument("--node-docs", type=int, default=20000)
     ap.add_argument("--arrival", type=int, default=None,
                     help="override the config's arrival order (0 generation, 1 actor-major as RepoBackend.loadDocument "
                          "concatenates, 2 shuffled)")
@@ -299,8 +299,11 @@ def _from_blocks(eng, batch, cfg, args):
 def _node_e2e(args):
     """C2 documents fed through the DocBackend message API on one Node thread (tools/bench_node.js):
     init() with each document's first 16 changes, then one applyRemoteChanges round per further
-    16.  `cpu` is the JS restatement (oracle/js/backend.js, BASELINE.md's second baseline); `gpu`
-    is the drop-in (GpuDocBackend, batched mode, patch diffs on), one GPU submit per round."""
+    16.  `cpu` is the JS restatement (oracle/js/backend.js, BASELINE.md's second baseline) handed
+    parsed Change objects, `cpu_blocks` the same with Actor.parseBlock (JSON.parse per block) in
+    the timed region; `gpu` / `gpu_async` are the drop-in (GpuDocBackend over the docset, batched /
+    async mode, patch diffs on) handed the raw blocks, `gpu_objects` the drop-in handed Change
+    objects."""
     import shutil
     import subprocess
     import tempfile
@@ -312,18 +315,23 @@ def _node_e2e(args):
     b = synth.generate(synth.config("C2", n_docs=args.node_docs), threads=min(16, os.cpu_count() or 1))
     docs = [decode_doc(b, i) for i in range(b.n_docs)]
     here = os.path.dirname(os.path.abspath(__file__))
+    legs = ["cpu", "cpu_blocks", "gpu", "gpu_async", "gpu_objects"]
     with tempfile.TemporaryDirectory() as td:
         fn = os.path.join(td, "c2.json")
         with open(fn, "w") as f:
             json.dump({"docs": [[d[k:k + 16] for k in range(0, len(d), 16)] for d in docs]}, f)
-        p = subprocess.run([node, os.path.join(here, "tools", "bench_node.js"), fn, "cpu,gpu,gpu_async"],
-                           capture_output=True, text=True, timeout=600)
+        del docs
+        p = subprocess.run([node, "--max-old-space-size=16384", os.path.join(here, "tools", "bench_node.js"), fn,
+                            ",".join(legs)], capture_output=True, text=True, timeout=900)
     if p.returncode != 0:
         return {"error": p.stderr[-800:]}
     out = json.loads(p.stdout.strip().splitlines()[-1])
-    out["same_clocks"] = out["cpu"]["digest"] == out["gpu"]["digest"] == out["gpu_async"]["digest"]
+    out["same_clocks"] = len({out[k]["digest"] for k in legs}) == 1
+    out["same_state"] = len({out[k]["state_digest"] for k in legs}) == 1
     out["sample"] = (f"C2: {b.n_docs} docs x 4 actors x 64 changes, 4 rounds of 16 changes per document "
-                     f"(init + 3 applyRemoteChanges), one Node thread")
+                     f"(init + 3 applyRemoteChanges), one Node thread; blocks = JSON Change texts")
+    out["gpu_async_vs_js"] = out["gpu_async"]["changes_per_s"] / out["cpu"]["changes_per_s"]
+    out["gpu_async_vs_js_blocks"] = out["gpu_async"]["changes_per_s"] / out["cpu_blocks"]["changes_per_s"]
     out["gpu_vs_js"] = out["gpu"]["changes_per_s"] / out["cpu"]["changes_per_s"]
     return out
 

@@ -14,8 +14,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("HM_OFFLOAD_ARCH", "gfx950")
 
 GPU_SRCS = ["merge_kernels.hip", "merge_large.hip", "store_kernels.hip", "exchange.hip", "cursors.hip", "engine.cpp", "store.cpp",
-            "decode.cpp"]
-GPU_DEPS = GPU_SRCS + ["merge_kernels.h", "store_kernels.h", "engine_internal.h", "../../include/hypermerge_amd.h"]
+            "decode.cpp", "docset.cpp"]
+GPU_DEPS = GPU_SRCS + ["scan.h", "merge_kernels.h", "store_kernels.h", "engine_internal.h", "../../include/hypermerge_amd.h"]
 
 
 def _stale(out: str, deps) -> bool:

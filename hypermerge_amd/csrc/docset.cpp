@@ -1,0 +1,1175 @@
+// docset.cpp — the host engine of the Node drop-in (include/hypermerge_amd.h, hm_docset_*).
+//
+// What the reference runs on the JS main thread for every arriving block, per document,
+// natively and over many documents per call:
+//   Actor.parseBlock / Block.unpack / JsonBuffer.parse   (src/Actor.ts:137-141, src/Block.ts:18-29,
+//                                                         src/JsonBuffer.ts:1-4)
+//   DocBackend.applyRemoteChanges -> Backend.applyChanges (src/DocBackend.ts:169-185)
+//   DocBackend.updateClock, the patch of RemotePatchMsg   (src/DocBackend.ts:135-142, :173-183)
+// A docset owns the documents of one device: their interners (actor ids ranked in JS string
+// order, object UUIDs, (object, key|elemId) registers, string values, content identity of
+// changes — columnar.js DocEncoder, kept across rounds), their placement in the resident
+// stores (one hm_store per actor-stride class 8/16/32/64: a document moves to a wider class
+// when a new actor outgrows its rows, its log rows re-submitted from the old store), and the
+// patch base (the document as the last patch left it).  One call = one applyChanges round
+// for every document of the call: decode on host threads, submit per class, wait, commit or
+// roll back each document (a throwing applyChanges leaves DocBackend.back unchanged), read
+// back only the registers the round's ops hit (every register when changes were queued), and
+// render each document's patch, opSet clock / deps and DocBackend.clock as JSON text.
+//
+// Content identity (Automerge's `Inconsistent reuse of sequence number` check, Immutable
+// `equals` of two changes with one (actor, seq)) is a 128-bit hash of each change's
+// canonical form (maps order-insensitive, last duplicate key wins, numbers by value), kept
+// per (actor, seq): the blocks themselves stay with the caller.
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+#include "../../include/hypermerge_amd.h"
+#include "engine_internal.h"
+#include "scan.h"
+
+namespace {
+
+using namespace hmscan;
+
+constexpr uint32_t N_CLASS = 4;
+constexpr uint32_t STRIDES[N_CLASS] = {8, 16, 32, 64};
+constexpr uint8_t NO_CLASS = 0xFF;
+constexpr uint8_t NO_TYPE = 0xFF;
+
+inline uint64_t mix64(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull;
+    return x ^ (x >> 33);
+}
+
+// (tag, bytes) -> dense id in first-insertion order, owning its bytes
+struct Names {
+    std::string arena;
+    struct K { uint32_t off, len, tag, h; };
+    std::vector<K> keys;
+    std::vector<uint32_t> slot;                              // id + 1, 0 = empty
+    uint32_t mask = 0;
+    uint32_t size() const { return (uint32_t)keys.size(); }
+    const char *ptr(uint32_t id) const { return arena.data() + keys[id].off; }
+    uint32_t len(uint32_t id) const { return keys[id].len; }
+    uint32_t tag(uint32_t id) const { return keys[id].tag; }
+    void rehash(size_t cap) {
+        slot.assign(cap, 0);
+        mask = (uint32_t)cap - 1;
+        for (uint32_t id = 0; id < keys.size(); id++) {
+            uint32_t i = keys[id].h & mask;
+            while (slot[i]) i = (i + 1) & mask;
+            slot[i] = id + 1;
+        }
+    }
+    uint32_t get(const char *p, uint32_t n, uint32_t tg, bool &fresh) {
+        if ((keys.size() + 1) * 2 > slot.size()) rehash(std::max<size_t>(16, slot.size() * 2));
+        const uint32_t h = (uint32_t)hash_bytes(p, n, tg);
+        for (uint32_t i = h & mask;; i = (i + 1) & mask) {
+            const uint32_t v = slot[i];
+            if (!v) {
+                slot[i] = size() + 1;
+                keys.push_back({(uint32_t)arena.size(), n, tg, h});
+                arena.append(p, n);
+                fresh = true;
+                return size() - 1;
+            }
+            const K &k = keys[v - 1];
+            if (k.h == h && k.tag == tg && k.len == n && !memcmp(arena.data() + k.off, p, n)) { fresh = false; return v - 1; }
+        }
+    }
+    void truncate(uint32_t n) {
+        if (n >= keys.size()) return;
+        arena.resize(keys[n].off);
+        keys.resize(n);
+        rehash(std::max<size_t>(16, slot.size()));
+    }
+};
+
+// ---------------- content identity: a 128-bit hash of a change's canonical form ----------------
+struct H2 { uint64_t a, b; bool operator==(const H2 &o) const { return a == o.a && b == o.b; } };
+
+H2 leaf(uint64_t tag, const char *p, size_t n) {
+    return {mix64(hash_bytes(p, (uint32_t)n, 0x51ED270B27A1F00Dull ^ tag)), mix64(hash_bytes(p, (uint32_t)n, 0x2545F4914F6CDD1Dull + tag))};
+}
+
+struct CHash {
+    const char *p, *e;
+    std::vector<std::pair<H2, H2>> &stk;                     // (key, value) of the open objects' fields
+    std::string &tmp;
+    void ws() { while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) p++; }
+    bool str(H2 &h) {
+        if (p >= e || *p != '"') return false;
+        const char *s = p + 1, *q = s;
+        while (q < e && *q != '"' && *q != '\\') q++;
+        if (q < e && *q == '"') { h = leaf(5, s, (size_t)(q - s)); p = q + 1; return true; }
+        Parser P{p, e};
+        if (!P.string(tmp)) return false;
+        p = P.p;
+        h = leaf(5, tmp.data(), tmp.size());
+        return true;
+    }
+    bool val(H2 &h, int depth) {
+        if (depth > 256) return false;
+        ws();
+        if (p >= e) return false;
+        const char c = *p;
+        if (c == '"') return str(h);
+        if (c == '{') {
+            p++;
+            const size_t base = stk.size();
+            ws();
+            if (p < e && *p == '}') p++;
+            else for (;;) {
+                ws();
+                H2 k, v;
+                if (!str(k)) return false;
+                ws();
+                if (p >= e || *p != ':') return false;
+                p++;
+                if (!val(v, depth + 1)) return false;
+                bool dup = false;                             // JSON.parse: the last duplicate key wins
+                for (size_t i = base; i < stk.size(); i++) if (stk[i].first == k) { stk[i].second = v; dup = true; }
+                if (!dup) stk.push_back({k, v});
+                ws();
+                if (p < e && *p == ',') { p++; continue; }
+                if (p < e && *p == '}') { p++; break; }
+                return false;
+            }
+            uint64_t A = 0, B = 0;                            // order-insensitive over the fields
+            for (size_t i = base; i < stk.size(); i++) {
+                A += mix64(stk[i].first.a * 0x9E3779B97F4A7C15ull ^ stk[i].second.a);
+                B += mix64(stk[i].first.b + 0xD6E8FEB86659FD93ull * stk[i].second.b);
+            }
+            const uint64_t n = stk.size() - base;
+            stk.resize(base);
+            h = {mix64(A ^ (0x7A11ull << 48) ^ n), mix64(B + 0x0B1Eull + n)};
+            return true;
+        }
+        if (c == '[') {
+            p++;
+            uint64_t A = 0x1234567ull, B = 0x89ABCDEFull, n = 0;
+            ws();
+            if (p < e && *p == ']') p++;
+            else for (;;) {
+                H2 v;
+                if (!val(v, depth + 1)) return false;
+                A = mix64(A * 31 + v.a); B = mix64(B ^ (v.b + n));
+                n++;
+                ws();
+                if (p < e && *p == ',') { p++; continue; }
+                if (p < e && *p == ']') { p++; break; }
+                return false;
+            }
+            h = {A ^ n, B + n};
+            return true;
+        }
+        if (e - p >= 4 && !memcmp(p, "null", 4)) { p += 4; h = leaf(0, "", 0); return true; }
+        if (e - p >= 4 && !memcmp(p, "true", 4)) { p += 4; h = leaf(2, "", 0); return true; }
+        if (e - p >= 5 && !memcmp(p, "false", 5)) { p += 5; h = leaf(1, "", 0); return true; }
+        Parser P{p, e};                                       // a number, compared by value (0 == -0)
+        JV j;
+        if (!P.value(j, 0) || j.t != J_NUM) return false;
+        p = P.p;
+        double v = j.num == 0 ? 0.0 : j.num;
+        h = leaf(3, (const char *)&v, 8);
+        return true;
+    }
+};
+
+// ---------------- one document ----------------
+struct DocSt {
+    bool ready = false;
+    Names actors, objs, regs, strs;                          // actors: ids in first-appearance order
+    std::vector<uint16_t> rank_of, by_rank;                  // actor id -> rank (JS string order) and back
+    // content identity: (actor id, seq) -> chain of (canonical hash, content id)
+    std::vector<uint64_t> ckey;                              // key + 1, 0 = empty slot
+    std::vector<uint32_t> chead;
+    struct CE { uint64_t key; H2 h; uint32_t cid, next; };
+    std::vector<CE> cents;
+    uint32_t n_content = 0;
+    // the log (what the stores hold), per op: its change's actor id and datatype (rendering)
+    std::vector<uint16_t> op_actor;
+    std::vector<uint8_t> op_dt;
+    uint32_t n_changes = 0, n_ops = 0;
+    uint16_t flags = 0;
+    uint8_t cls = NO_CLASS;
+    uint32_t handle = 0;
+    uint32_t hist_len = 0, n_queued = 0;
+    // the patch base: the document as the last patch left it
+    std::vector<uint8_t> obj_type, obj_emitted;
+    std::vector<uint64_t> sig;                               // per register: rendered entry hash, 0 = absent
+    std::vector<std::pair<uint32_t, std::vector<uint32_t>>> lists;   // list object -> visible element registers
+    void setup() {
+        bool f;
+        objs.get(ROOT_ID, 36, 0, f);
+        obj_type.assign(1, HM_MAKE_MAP);
+        obj_emitted.assign(1, 1);
+        ready = true;
+    }
+    void crehash(size_t cap) {
+        ckey.assign(cap, 0);
+        chead.assign(cap, 0);
+        const uint64_t m = cap - 1;
+        for (uint32_t i = 0; i < cents.size(); i++) {
+            uint64_t s = mix64(cents[i].key) & m;
+            while (ckey[s] && ckey[s] != cents[i].key + 1) s = (s + 1) & m;
+            cents[i].next = ckey[s] ? chead[s] : HM_NONE;
+            ckey[s] = cents[i].key + 1;
+            chead[s] = i;
+        }
+    }
+    uint32_t content_id(uint64_t key, const H2 &h) {
+        if ((cents.size() + 1) * 2 > ckey.size()) crehash(std::max<size_t>(64, ckey.size() * 2));
+        const uint64_t m = ckey.size() - 1;
+        uint64_t s = mix64(key) & m;
+        while (ckey[s] && ckey[s] != key + 1) s = (s + 1) & m;
+        uint32_t nx = HM_NONE;
+        if (ckey[s]) {
+            for (uint32_t i = chead[s]; i != HM_NONE; i = cents[i].next)
+                if (cents[i].h == h) return cents[i].cid;
+            nx = chead[s];
+        }
+        cents.push_back({key, h, n_content, nx});
+        ckey[s] = key + 1;
+        chead[s] = (uint32_t)cents.size() - 1;
+        return n_content++;
+    }
+    std::vector<uint32_t> *list_of(uint32_t obj, bool make) {
+        for (auto &l : lists) if (l.first == obj) return &l.second;
+        if (!make) return nullptr;
+        lists.emplace_back(obj, std::vector<uint32_t>());
+        return &lists.back().second;
+    }
+};
+
+// JS string order (UTF-16 code units) of two UTF-8 names
+bool js_less(const char *a, uint32_t na, const char *b, uint32_t nb) {
+    bool ascii = true;
+    for (uint32_t i = 0; i < na && ascii; i++) ascii = (unsigned char)a[i] < 0x80;
+    for (uint32_t i = 0; i < nb && ascii; i++) ascii = (unsigned char)b[i] < 0x80;
+    if (ascii) {
+        const int r = memcmp(a, b, std::min(na, nb));
+        return r ? r < 0 : na < nb;
+    }
+    return u16(std::string(a, na)) < u16(std::string(b, nb));
+}
+
+// One document's part of a call.
+struct Round {
+    uint32_t doc = 0, b0 = 0, b1 = 0;
+    int32_t status = HM_OK;
+    uint32_t err_block = HM_NONE;
+    std::vector<hm_change_row> ch;
+    std::vector<hm_dep_row> dp;
+    std::vector<hm_op_row> op;
+    uint16_t n_actors = 0, flags = 0;
+    uint32_t n_regs = 0, n_objs = 0;
+    std::vector<uint8_t> remap;                              // old rank -> new rank (empty = identity)
+    // snapshot for the rollback
+    uint32_t s_actors = 0, s_objs = 0, s_regs = 0, s_strs = 0, s_cents = 0, s_content = 0, s_ops = 0;
+    std::vector<uint16_t> s_rank_of, s_by_rank;
+    // placement in this call
+    uint8_t cls = NO_CLASS;
+    uint32_t handle = 0, row = 0;
+    bool moved = false, placed = false;
+    hm_doc_result res = {};
+    const uint32_t *clock = nullptr, *back = nullptr, *heads = nullptr;
+    bool full = false;                                       // patch from every register (else the hit ones)
+    uint32_t q0 = 0, q1 = 0;                                 // its register requests
+    std::string patch, bclock, cclock;
+};
+
+struct Scratch {
+    Ctx cx;
+    std::vector<H2> hs;
+    std::vector<std::pair<H2, H2>> stk;
+    std::string tmp;
+    std::vector<uint32_t> t2n;
+};
+
+template <typename F> void par_for(uint32_t n, uint32_t T, F &&f) {
+    T = std::max(1u, std::min(T, n));
+    if (T <= 1) { f(0u, n, 0u); return; }
+    std::vector<std::thread> th;
+    th.reserve(T);
+    for (uint32_t t = 0; t < T; t++)
+        th.emplace_back([&f, n, t, T] { f((uint32_t)((uint64_t)n * t / T), (uint32_t)((uint64_t)n * (t + 1) / T), t); });
+    for (auto &x : th) x.join();
+}
+
+void rollback(DocSt &d, Round &R) {
+    d.actors.truncate(R.s_actors);
+    if (!R.s_rank_of.empty() || R.s_actors == 0) { d.rank_of = R.s_rank_of; d.by_rank = R.s_by_rank; }
+    d.objs.truncate(R.s_objs);
+    d.regs.truncate(R.s_regs);
+    d.strs.truncate(R.s_strs);
+    if (d.cents.size() > R.s_cents) {
+        d.cents.resize(R.s_cents);
+        d.crehash(std::max<size_t>(64, d.ckey.size()));
+    }
+    d.n_content = R.s_content;
+    d.op_actor.resize(R.s_ops);
+    d.op_dt.resize(R.s_ops);
+}
+
+bool unpack(const uint8_t *data, const uint64_t *bo, uint32_t b, Ctx &cx, const char *&s, size_t &len) {
+    s = (const char *)data + bo[b];
+    len = (size_t)(bo[b + 1] - bo[b]);
+    if (len >= 2 && s[0] == 'B' && s[1] == 'R') {
+        cx.arena.emplace_back();
+        if (!brotli_decompress((const uint8_t *)s + 2, len - 2, cx.arena.back())) return false;
+        s = cx.arena.back().data(); len = cx.arena.back().size();
+        return true;
+    }
+    return len >= 2 && s[0] == '{' && s[1] == '"';            // else 'fail to unpack blocks - head is ...'
+}
+
+// decode one document's blocks of the call into rows against its interners
+void decode_round(DocSt &d, Round &R, const uint8_t *data, const uint64_t *bo, Scratch &X) {
+    if (!d.ready) d.setup();
+    R.s_actors = d.actors.size(); R.s_objs = d.objs.size(); R.s_regs = d.regs.size(); R.s_strs = d.strs.size();
+    R.s_cents = (uint32_t)d.cents.size(); R.s_content = d.n_content; R.s_ops = (uint32_t)d.op_actor.size();
+    Ctx &cx = X.cx;
+    const uint32_t n = R.b1 - R.b0;
+    cx.arena.clear();
+    cx.cs.assign(n, ScanChange());
+    cx.ops.clear();
+    cx.deps.clear();
+    cx.actors.reset(16);
+    X.hs.resize(n);
+    auto fail = [&](int32_t st, uint32_t b) { R.status = st; R.err_block = b; };
+    for (uint32_t i = 0; i < n; i++) {
+        const char *s; size_t len;
+        if (!unpack(data, bo, R.b0 + i, cx, s, len)) return fail(HM_ERR_INVALID, i);
+        Scan S{s, s + len, &cx};
+        cx.cs[i].text = s; cx.cs[i].len = (uint32_t)len;
+        if (!S.change(cx.cs[i])) return fail(HM_ERR_INVALID, i);
+        CHash C{s, s + len, X.stk, X.tmp};
+        if (!C.val(X.hs[i], 0)) return fail(HM_ERR_INVALID, i);
+    }
+    // actors: the call's names -> the document's actor ids; a new actor re-ranks (JS string order)
+    const auto &tk = cx.actors.keys;
+    X.t2n.resize(tk.size());
+    bool fresh_any = false;
+    for (size_t k = 0; k < tk.size(); k++) {
+        bool f;
+        X.t2n[k] = d.actors.get(tk[k].s.p, tk[k].s.n, 0, f);
+        fresh_any |= f;
+    }
+    const uint32_t na = d.actors.size();
+    if (na > 64) return fail(HM_ERR_UNSUPPORTED, HM_NONE);
+    if (fresh_any) {
+        R.s_rank_of = d.rank_of; R.s_by_rank = d.by_rank;
+        std::vector<uint16_t> order(na);
+        for (uint32_t i = 0; i < na; i++) order[i] = (uint16_t)i;
+        std::sort(order.begin(), order.end(), [&](uint16_t x, uint16_t y) {
+            return js_less(d.actors.ptr(x), d.actors.len(x), d.actors.ptr(y), d.actors.len(y)); });
+        std::vector<uint16_t> rank_of(na);
+        for (uint32_t r = 0; r < na; r++) rank_of[order[r]] = (uint16_t)r;
+        bool ident = true;
+        std::vector<uint8_t> remap(R.s_actors);
+        for (uint32_t r = 0; r < R.s_actors; r++) {
+            remap[r] = (uint8_t)rank_of[d.by_rank[r]];
+            ident &= remap[r] == r;
+        }
+        if (!ident) R.remap = std::move(remap);
+        d.rank_of = std::move(rank_of);
+        d.by_rank = std::move(order);
+    }
+    R.n_actors = (uint16_t)na;
+    bool f;
+    uint32_t last_obj_id = 0;
+    SV last_obj{ROOT_ID, 36};
+    auto obj = [&](const SV &u) {
+        if (u == last_obj) return last_obj_id;
+        last_obj_id = d.objs.get(u.p, u.n, 0, f);
+        last_obj = u;
+        return last_obj_id;
+    };
+    R.ch.reserve(n); R.dp.reserve(cx.deps.size()); R.op.reserve(cx.ops.size());
+    std::string el;
+    for (uint32_t i = 0; i < n; i++) {
+        const ScanChange &c = cx.cs[i];
+        const uint32_t aid = X.t2n[c.actor];
+        hm_change_row row = {};
+        row.actor = d.rank_of[aid];
+        row.seq = (uint32_t)(int64_t)c.seq;
+        row.content_id = d.content_id(((uint64_t)aid << 32) | row.seq, X.hs[i]);
+        row.dep_off = (uint32_t)R.dp.size();
+        for (uint32_t k = 0; k < c.ndeps; k++) {
+            const ScanDep &dd = cx.deps[c.dep0 + k];
+            hm_dep_row r = {};
+            r.actor = d.rank_of[X.t2n[dd.actor]];
+            r.seq = (uint32_t)(int64_t)dd.seq;
+            R.dp.push_back(r);
+        }
+        row.n_deps = (uint16_t)c.ndeps;
+        row.op_first = (uint32_t)R.op.size();
+        for (uint32_t k = 0; k < c.nops; k++) {
+            const ScanOp &o = cx.ops[c.op0 + k];
+            const int a = o.action;
+            if (a < 0 || !o.obj.p) return fail(HM_ERR_INVALID, i);
+            hm_op_row r = {};
+            r.obj = obj(o.obj);
+            r.reg = HM_NONE; r.parent = HM_NONE;
+            if (a == HM_INS) {
+                if (!o.has_key || !o.has_elem) return fail(HM_ERR_INVALID, i);
+                r.elem = (uint32_t)(int64_t)o.elem;
+                el.assign(d.actors.ptr(aid), d.actors.len(aid));
+                el += ':';
+                el += js_num_text(o.elem);
+                r.reg = d.regs.get(el.data(), (uint32_t)el.size(), r.obj, f);
+                r.parent = Scan::is(o.key, "_head") ? HM_HEAD : d.regs.get(o.key.p, o.key.n, r.obj, f);
+            } else if (a >= HM_SET) {
+                if (!o.has_key) return fail(HM_ERR_INVALID, i);
+                r.reg = d.regs.get(o.key.p, o.key.n, r.obj, f);
+                r.key = d.strs.get(o.key.p, o.key.n, 0, f);
+                if (a == HM_LINK) {
+                    if (o.vt != J_STR) return fail(HM_ERR_INVALID, i);
+                    r.vtag = HM_V_OBJ; r.value = obj(o.sval);
+                } else if (a != HM_DEL) {
+                    if (!o.has_value || o.vt == J_NULL) r.vtag = HM_V_NULL;
+                    else if (o.vt == J_TRUE) r.vtag = HM_V_TRUE;
+                    else if (o.vt == J_FALSE) r.vtag = HM_V_FALSE;
+                    else if (o.vt == J_NUM) {
+                        if (js_int(o.num)) { r.vtag = HM_V_INT; r.value = (uint64_t)(int64_t)o.num; }
+                        else { r.vtag = HM_V_FLOAT; memcpy(&r.value, &o.num, 8); }
+                    } else if (o.vt == J_STR) { r.vtag = HM_V_STR; r.value = d.strs.get(o.sval.p, o.sval.n, 0, f); }
+                    else return fail(HM_ERR_INVALID, i);            // 'unsupported op value'
+                }
+            }
+            r.datatype = o.datatype;
+            r.action = (uint8_t)a;
+            if (a == HM_MAKE_LIST || a == HM_MAKE_TEXT) R.flags |= HM_DOC_HAS_LISTS;
+            if (a == HM_INC || r.datatype == HM_DT_COUNTER) R.flags |= HM_DOC_HAS_COUNTERS;
+            R.op.push_back(r);
+            d.op_actor.push_back((uint16_t)aid);
+            d.op_dt.push_back(r.datatype);
+        }
+        row.n_ops = c.nops;
+        R.ch.push_back(row);
+    }
+    R.n_regs = d.regs.size();
+    R.n_objs = d.objs.size();
+}
+
+// ---------------- JSON rendering (what JSON.parse turns back into the JS values) ----------------
+void jstr(std::string &o, const char *p, size_t n) {
+    static const char *hex = "0123456789abcdef";
+    o += '"';
+    for (size_t i = 0; i < n; i++) {
+        const unsigned char c = (unsigned char)p[i];
+        if (c == '"' || c == '\\') { o += '\\'; o += (char)c; }
+        else if (c < 0x20) {
+            switch (c) {
+            case '\b': o += "\\b"; break; case '\f': o += "\\f"; break; case '\n': o += "\\n"; break;
+            case '\r': o += "\\r"; break; case '\t': o += "\\t"; break;
+            default: o += "\\u00"; o += hex[c >> 4]; o += hex[c & 15];
+            }
+        } else if (c == 0xED && i + 2 < n && ((unsigned char)p[i + 1] & 0xE0) == 0xA0) {
+            // a lone surrogate (kept as its 3-byte form by the decoder): back to \uD8xx / \uDCxx
+            const uint32_t u = 0xD000 | (((unsigned char)p[i + 1] & 0x3F) << 6) | ((unsigned char)p[i + 2] & 0x3F);
+            o += "\\u";
+            for (int s = 12; s >= 0; s -= 4) o += hex[(u >> s) & 15];
+            i += 2;
+        } else o += (char)c;
+    }
+    o += '"';
+}
+
+void jnum(std::string &o, uint32_t vtag, uint64_t value) {
+    char b[48];
+    if (vtag == HM_V_INT) { snprintf(b, sizeof b, "%lld", (long long)(int64_t)value); o += b; return; }
+    double v;
+    memcpy(&v, &value, 8);
+    if (v != v) { o += "null"; return; }                       // JSON.stringify(NaN)
+    if (v == 1.0 / 0.0) { o += "1e999"; return; }              // JSON.parse -> Infinity
+    if (v == -1.0 / 0.0) { o += "-1e999"; return; }
+    snprintf(b, sizeof b, "%.17g", v);                         // round-trips to the same double
+    o += b;
+}
+
+void jvalue(std::string &o, const DocSt &d, const hm_surv_result &s) {
+    o += "\"value\":";
+    switch (s.vtag) {
+    case HM_V_NULL: o += "null"; break;
+    case HM_V_FALSE: o += "false"; break;
+    case HM_V_TRUE: o += "true"; break;
+    case HM_V_INT: case HM_V_FLOAT: jnum(o, s.vtag, s.value); break;
+    case HM_V_STR: {
+        const uint32_t id = (uint32_t)s.value;
+        if (id < d.strs.size()) jstr(o, d.strs.ptr(id), d.strs.len(id)); else o += "null";
+        break;
+    }
+    case HM_V_OBJ: {
+        const uint32_t id = (uint32_t)s.value;
+        if (id < d.objs.size()) jstr(o, d.objs.ptr(id), d.objs.len(id)); else o += "null";
+        o += ",\"link\":true";
+        break;
+    }
+    default: o += "null";
+    }
+    const uint8_t dt = s.op < d.op_dt.size() ? d.op_dt[s.op] : 0;
+    if (dt == HM_DT_COUNTER) o += ",\"datatype\":\"counter\"";
+    else if (dt == HM_DT_TIMESTAMP) o += ",\"datatype\":\"timestamp\"";
+}
+
+// a register's survivors (winner first) -> the fields of its diff entry:
+// value[, link][, datatype][, conflicts: [{actor, value[, link][, datatype]}]]
+void jentry(std::string &o, const DocSt &d, const hm_surv_result *sv, uint32_t n) {
+    jvalue(o, d, sv[0]);
+    if (n <= 1) return;
+    o += ",\"conflicts\":[";
+    for (uint32_t i = 1; i < n; i++) {
+        if (i > 1) o += ',';
+        o += "{\"actor\":";
+        const uint32_t a = sv[i].op < d.op_actor.size() ? d.op_actor[sv[i].op] : 0;
+        jstr(o, d.actors.ptr(a), d.actors.len(a));
+        o += ',';
+        jvalue(o, d, sv[i]);
+        o += '}';
+    }
+    o += ']';
+}
+
+void jclock(std::string &o, const DocSt &d, const uint32_t *row, uint32_t n_actors) {
+    o += '{';
+    bool first = true;
+    for (uint32_t r = 0; r < n_actors; r++) {
+        if (!row[r]) continue;
+        if (!first) o += ',';
+        first = false;
+        const uint32_t a = d.by_rank[r];
+        jstr(o, d.actors.ptr(a), d.actors.len(a));
+        o += ':';
+        o += std::to_string(row[r]);
+    }
+    o += '}';
+}
+
+const char *TYPE_NAME[4] = {"map", "table", "list", "text"};
+
+// The diffs that take the patch base to the registers' new state (hm_reg_result rows of the
+// requested registers, survivors at `surv`): objects created first, then map keys in
+// request order, then per list removals (descending old index), insertions (ascending new
+// index) and value changes.  The base is advanced to the new state.
+void render_diffs(std::string &o, DocSt &d, const uint32_t *req, const hm_reg_result *rows, const hm_surv_result *surv,
+                  uint32_t n) {
+    bool any = false;
+    auto sep = [&] { if (any) o += ','; any = true; };
+    std::string tmp;
+    for (uint32_t ob = 1; ob < d.obj_type.size(); ob++) {
+        if (d.obj_type[ob] == NO_TYPE || d.obj_emitted[ob]) continue;
+        d.obj_emitted[ob] = 1;
+        sep();
+        o += "{\"action\":\"create\",\"obj\":";
+        jstr(o, d.objs.ptr(ob), d.objs.len(ob));
+        o += ",\"type\":\"";
+        o += TYPE_NAME[d.obj_type[ob] & 3];
+        o += "\"}";
+    }
+    struct LOp { uint32_t g, idx; size_t t0, t1; };
+    struct LD { uint32_t obj; std::vector<uint32_t> rem; std::vector<LOp> ins, set; };
+    std::vector<LD> lds;
+    std::string lt;                                           // list entries' text
+    for (uint32_t q = 0; q < n; q++) {
+        const uint32_t g = req[q];
+        const hm_reg_result &r = rows[q];
+        if (r.obj == HM_NONE || r.obj >= d.obj_type.size()) continue;
+        const uint8_t t = d.obj_type[r.obj] == NO_TYPE ? HM_MAKE_MAP : d.obj_type[r.obj];
+        const bool list = t == HM_MAKE_LIST || t == HM_MAKE_TEXT;
+        tmp.clear();
+        if (r.n_surv) jentry(tmp, d, surv + r.surv_off, r.n_surv);
+        const uint64_t sg = r.n_surv ? (mix64(hash_bytes(tmp.data(), (uint32_t)tmp.size(), 7)) | 1) : 0;
+        const uint64_t old = d.sig[g];
+        if (!list) {
+            if (sg == old) continue;
+            d.sig[g] = sg;
+            sep();
+            o += sg ? "{\"action\":\"set\",\"type\":\"" : "{\"action\":\"remove\",\"type\":\"";
+            o += TYPE_NAME[t & 3];
+            o += "\",\"obj\":";
+            jstr(o, d.objs.ptr(r.obj), d.objs.len(r.obj));
+            o += ",\"key\":";
+            jstr(o, d.regs.ptr(g), d.regs.len(g));
+            if (sg) { o += ','; o += tmp; }
+            o += '}';
+            continue;
+        }
+        const bool vis = r.n_surv > 0 && r.list_index >= 0;
+        const uint64_t ns = vis ? sg : 0;
+        if (ns == old) continue;
+        LD *L = nullptr;
+        for (auto &x : lds) if (x.obj == r.obj) L = &x;
+        if (!L) { lds.push_back(LD{r.obj, {}, {}, {}}); L = &lds.back(); }
+        std::vector<uint32_t> &el = *d.list_of(r.obj, true);
+        if (old && !vis) {
+            L->rem.push_back((uint32_t)(std::find(el.begin(), el.end(), g) - el.begin()));
+        } else {
+            const size_t t0 = lt.size();
+            lt += tmp;
+            (old ? L->set : L->ins).push_back(LOp{g, (uint32_t)r.list_index, t0, lt.size()});
+        }
+        d.sig[g] = ns;
+    }
+    for (auto &L : lds) {
+        std::vector<uint32_t> &el = *d.list_of(L.obj, true);
+        const uint8_t t = d.obj_type[L.obj];
+        auto head = [&](const char *action) {
+            sep();
+            o += "{\"action\":\""; o += action; o += "\",\"type\":\""; o += TYPE_NAME[t & 3]; o += "\",\"obj\":";
+            jstr(o, d.objs.ptr(L.obj), d.objs.len(L.obj));
+        };
+        std::sort(L.rem.begin(), L.rem.end(), std::greater<uint32_t>());
+        for (uint32_t i : L.rem) {
+            if (i >= el.size()) continue;
+            el.erase(el.begin() + i);
+            head("remove");
+            o += ",\"index\":" + std::to_string(i) + '}';
+        }
+        std::stable_sort(L.ins.begin(), L.ins.end(), [](const LOp &a, const LOp &b) { return a.idx < b.idx; });
+        for (auto &x : L.ins) {
+            const uint32_t i = std::min<uint32_t>(x.idx, (uint32_t)el.size());
+            el.insert(el.begin() + i, x.g);
+            head("insert");
+            o += ",\"index\":" + std::to_string(i) + ",\"elemId\":";
+            jstr(o, d.regs.ptr(x.g), d.regs.len(x.g));
+            o += ',';
+            o.append(lt, x.t0, x.t1 - x.t0);
+            o += '}';
+        }
+        for (auto &x : L.set) {
+            const uint32_t i = (uint32_t)(std::find(el.begin(), el.end(), x.g) - el.begin());
+            head("set");
+            o += ",\"index\":" + std::to_string(i) + ',';
+            o.append(lt, x.t0, x.t1 - x.t0);
+            o += '}';
+        }
+    }
+}
+
+// the document as the patch base holds it: {uuid: {type, keys: [[key, entry]], elems: [[elemId, entry]]}}
+void render_view(std::string &o, const DocSt &d, const hm_reg_result *rows, const hm_surv_result *surv, uint32_t n_regs) {
+    std::vector<std::string> keys(d.obj_type.size()), elems(d.obj_type.size());
+    std::vector<std::vector<std::pair<int32_t, uint32_t>>> order(d.obj_type.size());
+    std::string tmp;
+    for (uint32_t g = 0; g < n_regs; g++) {
+        const hm_reg_result &r = rows[g];
+        if (!r.n_surv || r.obj == HM_NONE || r.obj >= d.obj_type.size()) continue;
+        const uint8_t t = d.obj_type[r.obj] == NO_TYPE ? HM_MAKE_MAP : d.obj_type[r.obj];
+        if (t == HM_MAKE_LIST || t == HM_MAKE_TEXT) { if (r.list_index >= 0) order[r.obj].push_back({r.list_index, g}); continue; }
+        std::string &k = keys[r.obj];
+        if (!k.empty()) k += ',';
+        k += '[';
+        jstr(k, d.regs.ptr(g), d.regs.len(g));
+        k += ",{";
+        jentry(k, d, surv + r.surv_off, r.n_surv);
+        k += "}]";
+    }
+    o += '{';
+    for (uint32_t ob = 0; ob < d.obj_type.size(); ob++) {
+        if (d.obj_type[ob] == NO_TYPE && keys[ob].empty() && order[ob].empty()) continue;
+        if (o.size() > 1) o += ',';
+        jstr(o, d.objs.ptr(ob), d.objs.len(ob));
+        const uint8_t t = d.obj_type[ob] == NO_TYPE ? HM_MAKE_MAP : d.obj_type[ob];
+        o += ":{\"type\":\""; o += TYPE_NAME[t & 3]; o += "\",\"keys\":[";
+        o += keys[ob];
+        o += "],\"elems\":[";
+        std::sort(order[ob].begin(), order[ob].end());
+        for (size_t i = 0; i < order[ob].size(); i++) {
+            const uint32_t g = order[ob][i].second;
+            if (i) o += ',';
+            o += '[';
+            jstr(o, d.regs.ptr(g), d.regs.len(g));
+            o += ",{";
+            jentry(o, d, surv + rows[g].surv_off, rows[g].n_surv);
+            o += "}]";
+        }
+        o += "]}";
+    }
+    o += '}';
+}
+
+}  // namespace
+
+struct hm_docset {
+    hm_engine *e = nullptr;
+    uint32_t threads = 16;
+    bool patches = true;
+    hm_store *stores[N_CLASS] = {nullptr, nullptr, nullptr, nullptr};
+    // documents: fixed chunks, so hm_docset_open may run while a call works on earlier documents
+    static constexpr uint32_t CHUNK = 4096;
+    std::vector<std::unique_ptr<DocSt[]>> chunks;
+    std::atomic<uint32_t> n_docs{0};
+    std::mutex open_mu;
+    std::atomic<bool> busy{false};
+    uint64_t stat[8] = {0, 0, 0, 0, 0, 0, 0, 0};           // rounds, docs, restrides, hit-register patches, full patches
+    DocSt &doc(uint32_t i) { return chunks[i / CHUNK][i % CHUNK]; }
+};
+
+struct hm_text {
+    std::string s;
+    std::vector<hm_doc_result> res;
+};
+
+namespace {
+
+int store_of(hm_docset *ds, uint32_t c, hm_store **out) {
+    if (!ds->stores[c]) {
+        hm_store_config sc = {STRIDES[c], 0};
+        const int r = hm_store_create(ds->e, &sc, &ds->stores[c]);
+        if (r) return r;
+    }
+    *out = ds->stores[c];
+    return HM_OK;
+}
+
+uint8_t class_for(uint32_t n_actors) {
+    for (uint32_t c = 0; c < N_CLASS; c++) if (n_actors <= STRIDES[c]) return (uint8_t)c;
+    return NO_CLASS;
+}
+
+struct Busy {
+    hm_docset *ds;
+    bool ok;
+    explicit Busy(hm_docset *d) : ds(d) { bool f = false; ok = ds->busy.compare_exchange_strong(f, true); }
+    ~Busy() { if (ok) ds->busy.store(false); }
+};
+
+int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t *doc_block, const uint32_t *docs, uint32_t n,
+          hm_text *out) {
+    const uint32_t nd = ds->n_docs.load();
+    {
+        std::vector<uint8_t> seen(nd, 0);
+        for (uint32_t i = 0; i < n; i++) {
+            if (docs[i] >= nd || seen[docs[i]]) return hm_engine_fail(ds->e, HM_ERR_INVALID, "bad or repeated docset document");
+            seen[docs[i]] = 1;
+            if (doc_block[i] > doc_block[i + 1]) return hm_engine_fail(ds->e, HM_ERR_INVALID, "doc_block not ascending");
+        }
+    }
+    const bool prof = getenv("HM_DOCSET_PROFILE") != nullptr;
+    auto t0 = std::chrono::steady_clock::now();
+    auto mark = [&](const char *what) {
+        if (!prof) return;
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[hm_docset] %-14s %9.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t0).count());
+        t0 = t;
+    };
+    std::vector<Round> R(n);
+    for (uint32_t i = 0; i < n; i++) { R[i].doc = docs[i]; R[i].b0 = doc_block[i]; R[i].b1 = doc_block[i + 1]; }
+    const uint32_t T = std::min<uint32_t>(ds->threads, std::max<uint32_t>(1, n / 64));
+    par_for(n, T, [&](uint32_t lo, uint32_t hi, uint32_t) {
+        Scratch X;
+        for (uint32_t i = lo; i < hi; i++) {
+            DocSt &d = ds->doc(R[i].doc);
+            decode_round(d, R[i], data, bo, X);
+            if (R[i].status != HM_OK) rollback(d, R[i]);
+        }
+    });
+    mark("decode");
+    // placement: a document lives in the narrowest class that holds its actors
+    std::vector<std::vector<uint32_t>> by_cls(N_CLASS);
+    for (uint32_t i = 0; i < n; i++) {
+        Round &x = R[i];
+        if (x.status != HM_OK) continue;
+        DocSt &d = ds->doc(x.doc);
+        uint8_t c = class_for(x.n_actors);
+        if (d.cls != NO_CLASS && d.cls > c) c = d.cls;
+        x.cls = c;
+        x.placed = d.cls == NO_CLASS;
+        x.moved = !x.placed && c != d.cls;
+        x.handle = d.handle;
+        by_cls[c].push_back(i);
+    }
+    struct ClsOut { std::vector<hm_doc_result> res; std::vector<uint32_t> clock, back, heads; uint64_t id = 0; bool sub = false; };
+    std::vector<ClsOut> co(N_CLASS);
+    int rc = HM_OK;
+    for (uint32_t c = 0; c < N_CLASS && rc == HM_OK; c++) {
+        auto &rows = by_cls[c];
+        if (rows.empty()) continue;
+        hm_store *st;
+        if ((rc = store_of(ds, c, &st))) break;
+        const uint32_t S = STRIDES[c];
+        // fresh handles for placed and moved documents
+        uint32_t fresh = 0;
+        for (uint32_t i : rows) fresh += R[i].placed || R[i].moved;
+        uint32_t h0 = 0;
+        if (fresh && (rc = hm_doc_open_n(st, fresh, &h0))) break;
+        std::vector<hm_doc_row> drows(rows.size());
+        std::vector<hm_change_row> ch;
+        std::vector<hm_dep_row> dp;
+        std::vector<hm_op_row> op;
+        std::vector<uint32_t> hand(rows.size());
+        std::vector<uint8_t> remap;
+        bool any_remap = false;
+        for (uint32_t k = 0; k < rows.size(); k++) if (!R[rows[k]].moved && !R[rows[k]].placed && !R[rows[k]].remap.empty()) any_remap = true;
+        if (any_remap) {
+            remap.resize(rows.size() * (size_t)S);
+            for (uint32_t k = 0; k < rows.size(); k++) for (uint32_t a = 0; a < S; a++) remap[(size_t)k * S + a] = (uint8_t)a;
+        }
+        size_t tc = 0, td = 0, to = 0;
+        for (uint32_t i : rows) { tc += R[i].ch.size(); td += R[i].dp.size(); to += R[i].op.size(); }
+        ch.reserve(tc); dp.reserve(td); op.reserve(to);
+        for (uint32_t k = 0; k < rows.size(); k++) {
+            Round &x = R[rows[k]];
+            DocSt &d = ds->doc(x.doc);
+            x.row = k;
+            hm_doc_row &r = drows[k];
+            r = hm_doc_row{};
+            r.change_off = (uint32_t)ch.size(); r.dep_off = (uint32_t)dp.size(); r.op_off = (uint32_t)op.size();
+            const uint32_t c0 = (uint32_t)ch.size(), d0 = (uint32_t)dp.size(), o0 = (uint32_t)op.size();
+            if (x.placed || x.moved) x.handle = h0++;
+            hand[k] = x.handle;
+            if (x.moved) {
+                // the whole log moves: its rows from the old store, ranks re-mapped to this round's
+                ds->stat[2]++;
+                hm_doc_info_t inf;
+                hm_store *old = ds->stores[d.cls];
+                if ((rc = hm_doc_info(old, d.handle, &inf))) break;
+                std::vector<hm_change_row> lc(inf.n_changes);
+                std::vector<hm_dep_row> ld(inf.n_deps);
+                std::vector<hm_op_row> lo(inf.n_ops);
+                if ((rc = hm_doc_log(old, d.handle, lc.data(), ld.data(), lo.data()))) break;
+                for (auto &cr : lc) {
+                    if (!x.remap.empty() && cr.actor < x.remap.size()) cr.actor = x.remap[cr.actor];
+                    cr.dep_off += d0; cr.op_first += o0;
+                    ch.push_back(cr);
+                }
+                for (auto &dr : ld) { if (!x.remap.empty() && dr.actor < x.remap.size()) dr.actor = x.remap[dr.actor]; dp.push_back(dr); }
+                op.insert(op.end(), lo.begin(), lo.end());
+            } else if (!x.placed && !x.remap.empty()) {
+                for (size_t a = 0; a < x.remap.size(); a++) remap[(size_t)k * S + a] = x.remap[a];
+            }
+            const uint32_t d1 = (uint32_t)dp.size(), o1 = (uint32_t)op.size();
+            for (auto cr : x.ch) { cr.dep_off += d1; cr.op_first += o1; ch.push_back(cr); }
+            dp.insert(dp.end(), x.dp.begin(), x.dp.end());
+            op.insert(op.end(), x.op.begin(), x.op.end());
+            r.n_changes = (uint32_t)ch.size() - c0; r.n_deps = (uint32_t)dp.size() - d0; r.n_ops = (uint32_t)op.size() - o0;
+            r.n_regs = x.n_regs; r.n_objs = x.n_objs; r.n_actors = x.n_actors;
+            r.flags = (uint16_t)(x.flags | (x.moved ? d.flags : 0));
+        }
+        if (rc) break;
+        hm_batch b = {};
+        b.n_docs = (uint32_t)rows.size(); b.n_changes = (uint32_t)ch.size(); b.n_deps = (uint32_t)dp.size(); b.n_ops = (uint32_t)op.size();
+        b.a_stride = S;
+        b.docs = drows.data(); b.changes = ch.data(); b.deps = dp.data(); b.ops = op.data();
+        if ((rc = hm_batch_submit(st, &b, hand.data(), any_remap ? remap.data() : nullptr, &co[c].id))) break;
+        co[c].sub = true;
+        ClsOut &O = co[c];
+        O.res.resize(rows.size()); O.clock.resize(rows.size() * (size_t)S); O.back.resize(rows.size() * (size_t)S);
+        O.heads.resize(rows.size() * (size_t)S);
+        if ((rc = hm_batch_wait(st, O.id, O.res.data(), O.clock.data(), O.back.data(), O.heads.data()))) break;
+        O.sub = false;
+        for (uint32_t k = 0; k < rows.size(); k++) {
+            Round &x = R[rows[k]];
+            x.res = O.res[k];
+            x.clock = O.clock.data() + (size_t)k * S; x.back = O.back.data() + (size_t)k * S; x.heads = O.heads.data() + (size_t)k * S;
+        }
+    }
+    if (rc) {
+        // a call-level failure: every document of the call rolls back on the host (a store
+        // whose batch is in flight is waited for first)
+        for (uint32_t c = 0; c < N_CLASS; c++)
+            if (co[c].sub) {
+                std::vector<hm_doc_result> tmp(by_cls[c].size());
+                (void)hm_batch_wait(ds->stores[c], co[c].id, tmp.data(), nullptr, nullptr, nullptr);
+            }
+        for (uint32_t i = 0; i < n; i++) if (R[i].status == HM_OK) rollback(ds->doc(R[i].doc), R[i]);
+        return rc;
+    }
+    mark("merge");
+    // commit or roll back each document; the registers each patch reads
+    std::vector<std::vector<uint32_t>> qdocs(N_CLASS), qregs(N_CLASS);
+    std::vector<uint32_t> cap(N_CLASS, 0);
+    for (uint32_t i = 0; i < n; i++) {
+        Round &x = R[i];
+        DocSt &d = ds->doc(x.doc);
+        if (x.status == HM_OK && x.res.status != HM_OK) x.status = x.res.status;
+        if (x.status != HM_OK) {
+            if (x.cls != NO_CLASS) rollback(d, x);
+            if (x.placed) { d.cls = x.cls; d.handle = x.handle; }          // an empty document in its store
+            continue;
+        }
+        const uint32_t prev_hist = d.hist_len, prev_q = d.n_queued, old_n_ops = d.n_ops;
+        d.cls = x.cls; d.handle = x.handle;
+        d.flags |= x.flags;
+        d.n_changes += (uint32_t)x.ch.size();
+        d.n_ops += (uint32_t)x.op.size();
+        d.hist_len = x.res.hist_len; d.n_queued = x.res.n_queued;
+        d.obj_type.resize(x.n_objs, NO_TYPE);
+        d.obj_emitted.resize(x.n_objs, 0);
+        d.sig.resize(x.n_regs, 0);
+        for (const hm_op_row &o : x.op)
+            if (o.action <= HM_MAKE_TEXT && o.obj < d.obj_type.size() && d.obj_type[o.obj] == NO_TYPE) d.obj_type[o.obj] = o.action;
+        (void)old_n_ops;
+        if (!ds->patches) continue;
+        x.full = !(prev_q == 0 && x.res.n_queued == 0 && x.res.hist_len - prev_hist == x.ch.size());
+        x.q0 = (uint32_t)qregs[x.cls].size();
+        if (x.full) {
+            for (uint32_t g = 0; g < x.n_regs; g++) { qdocs[x.cls].push_back(x.handle); qregs[x.cls].push_back(g); }
+            ds->stat[4]++;
+        } else {
+            // the registers the round's set/del/link/inc ops hit, first hit first
+            std::vector<uint32_t> &q = qregs[x.cls];
+            for (const hm_op_row &o : x.op) {
+                if (o.action < HM_SET || o.reg == HM_NONE) continue;
+                bool dup = false;
+                for (uint32_t j = x.q0; j < q.size() && !dup; j++) dup = q[j] == o.reg;
+                if (dup) continue;
+                q.push_back(o.reg);
+                qdocs[x.cls].push_back(x.handle);
+            }
+            ds->stat[3]++;
+        }
+        x.q1 = (uint32_t)qregs[x.cls].size();
+        cap[x.cls] += x.res.n_surv;
+    }
+    std::vector<std::vector<hm_reg_result>> rrows(N_CLASS);
+    std::vector<std::vector<hm_surv_result>> rsurv(N_CLASS);
+    for (uint32_t c = 0; c < N_CLASS; c++) {
+        if (qregs[c].empty()) continue;
+        rrows[c].resize(qregs[c].size());
+        rsurv[c].resize(std::max<uint32_t>(cap[c], 1));
+        uint32_t got = 0;
+        rc = hm_store_read_regs(ds->stores[c], (uint32_t)qregs[c].size(), qdocs[c].data(), qregs[c].data(), rrows[c].data(),
+                                rsurv[c].data(), (uint32_t)rsurv[c].size(), &got);
+        if (rc) return rc;
+    }
+    mark("read regs");
+    // render every document's patch and DocBackend.clock
+    par_for(n, std::min<uint32_t>(ds->threads, std::max<uint32_t>(1, n / 128)), [&](uint32_t lo, uint32_t hi, uint32_t) {
+        for (uint32_t i = lo; i < hi; i++) {
+            Round &x = R[i];
+            if (x.status != HM_OK) continue;
+            DocSt &d = ds->doc(x.doc);
+            std::string &o = x.patch;
+            o.reserve(256);
+            o += "{\"clock\":";
+            jclock(o, d, x.clock, x.n_actors);
+            o += ",\"deps\":";
+            jclock(o, d, x.heads, x.n_actors);
+            o += ",\"canUndo\":false,\"canRedo\":false,\"diffs\":[";
+            if (ds->patches && x.q1 > x.q0)
+                render_diffs(o, d, qregs[x.cls].data() + x.q0, rrows[x.cls].data() + x.q0, rsurv[x.cls].data(), x.q1 - x.q0);
+            else if (ds->patches) render_diffs(o, d, nullptr, nullptr, nullptr, 0);
+            o += "]}";
+            jclock(x.bclock, d, x.back, x.n_actors);
+            // this call's changes alone: max seq per actor (DocBackend.updateClock(changes))
+            uint32_t rc[64] = {0};
+            for (const hm_change_row &c : x.ch) if (c.actor < 64 && c.seq > rc[c.actor]) rc[c.actor] = c.seq;
+            jclock(x.cclock, d, rc, x.n_actors);
+        }
+    });
+    // {"p": [patch | null per document], "b": [max over the whole log | null], "c": [max over this call's changes | null]}
+    size_t tot = 16;
+    for (auto &x : R) tot += x.patch.size() + x.bclock.size() + x.cclock.size() + 18;
+    std::string &s = out->s;
+    s.clear();
+    s.reserve(tot);
+    s += "{\"p\":[";
+    for (uint32_t i = 0; i < n; i++) { if (i) s += ','; if (R[i].status == HM_OK) s += R[i].patch; else s += "null"; }
+    s += "],\"b\":[";
+    for (uint32_t i = 0; i < n; i++) { if (i) s += ','; if (R[i].status == HM_OK) s += R[i].bclock; else s += "null"; }
+    s += "],\"c\":[";
+    for (uint32_t i = 0; i < n; i++) { if (i) s += ','; if (R[i].status == HM_OK) s += R[i].cclock; else s += "null"; }
+    s += "]}";
+    out->res.resize(n);
+    for (uint32_t i = 0; i < n; i++) {
+        Round &x = R[i];
+        hm_doc_result &r = out->res[i];
+        if (x.cls == NO_CLASS && x.status != HM_OK) {                    // the call's blocks did not decode
+            r = hm_doc_result{};
+            r.status = x.status; r.err_change = x.err_block; r.err_op = HM_NONE;
+            DocSt &d = ds->doc(x.doc);
+            r.hist_len = d.hist_len; r.n_queued = d.n_queued;
+        } else r = x.res;
+    }
+    ds->stat[0]++;
+    ds->stat[1] += n;
+    mark("render");
+    return HM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hm_docset_create(hm_engine *e, const hm_docset_config *cfg, hm_docset **out) {
+    if (!e || !out) return HM_ERR_INVALID;
+    *out = nullptr;
+    hm_docset *ds = new (std::nothrow) hm_docset();
+    if (!ds) return HM_ERR_NOMEM;
+    ds->e = e;
+    const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
+    ds->threads = cfg && cfg->threads ? cfg->threads : std::min<uint32_t>(16, hw);
+    ds->patches = !(cfg && (cfg->flags & HM_DOCSET_NO_PATCHES));
+    ds->chunks.reserve(1u << 16);
+    *out = ds;
+    return HM_OK;
+}
+
+void hm_docset_destroy(hm_docset *ds) {
+    if (!ds) return;
+    for (auto *s : ds->stores) if (s) hm_store_destroy(s);
+    delete ds;
+}
+
+hm_engine *hm_docset_engine(hm_docset *ds) { return ds ? ds->e : nullptr; }
+
+int hm_docset_open(hm_docset *ds, uint32_t n, uint32_t *out_first) {
+    if (!ds || !out_first) return HM_ERR_INVALID;
+    try {
+        std::lock_guard<std::mutex> g(ds->open_mu);
+        const uint32_t first = ds->n_docs.load();
+        const uint64_t need = (uint64_t)first + n;
+        if (need > (uint64_t)hm_docset::CHUNK * (1u << 16)) return HM_ERR_NOMEM;
+        while ((uint64_t)ds->chunks.size() * hm_docset::CHUNK < need) ds->chunks.emplace_back(new DocSt[hm_docset::CHUNK]);
+        ds->n_docs.store((uint32_t)need);
+        *out_first = first;
+        return HM_OK;
+    } catch (...) {
+        return HM_ERR_NOMEM;
+    }
+}
+
+int hm_docset_apply(hm_docset *ds, const uint8_t *data, const uint64_t *block_off, const uint32_t *doc_block,
+                    const uint32_t *docs, uint32_t n_docs, hm_text **out) {
+    if (!ds || !out || (n_docs && (!block_off || !doc_block || !docs))) return HM_ERR_INVALID;
+    *out = nullptr;
+    Busy b(ds);
+    if (!b.ok) return hm_engine_fail(ds->e, HM_ERR_INVALID, "hm_docset_apply: another call on this docset is running");
+    try {
+        std::unique_ptr<hm_text> t(new hm_text());
+        const int rc = apply(ds, data, block_off, doc_block, docs, n_docs, t.get());
+        if (rc) return rc;
+        *out = t.release();
+        return HM_OK;
+    } catch (...) {
+        return hm_engine_fail(ds->e, HM_ERR_NOMEM, "exception in hm_docset_apply");
+    }
+}
+
+const char *hm_text_data(const hm_text *t, size_t *len) {
+    if (!t) return nullptr;
+    if (len) *len = t->s.size();
+    return t->s.data();
+}
+
+const hm_doc_result *hm_text_results(const hm_text *t, uint32_t *n) {
+    if (!t) return nullptr;
+    if (n) *n = (uint32_t)t->res.size();
+    return t->res.data();
+}
+
+void hm_text_free(hm_text *t) { delete t; }
+
+int hm_docset_doc_info(hm_docset *ds, uint32_t doc, hm_docset_doc_info_t *out) {
+    if (!ds || !out || doc >= ds->n_docs.load()) return HM_ERR_INVALID;
+    Busy b(ds);
+    if (!b.ok) return hm_engine_fail(ds->e, HM_ERR_INVALID, "docset busy");
+    DocSt &d = ds->doc(doc);
+    memset(out, 0, sizeof *out);
+    out->a_stride = d.cls == NO_CLASS ? 0 : STRIDES[d.cls];
+    out->n_changes = d.n_changes; out->n_ops = d.n_ops; out->n_actors = d.actors.size();
+    out->n_objs = std::max<uint32_t>(1, d.objs.size()); out->n_regs = d.regs.size();
+    out->hist_len = d.hist_len; out->n_queued = d.n_queued;
+    return HM_OK;
+}
+
+int hm_docset_history_prefix(hm_docset *ds, uint32_t doc, uint32_t n, uint32_t *out) {
+    if (!ds || doc >= ds->n_docs.load() || (n && !out)) return HM_ERR_INVALID;
+    Busy b(ds);
+    if (!b.ok) return hm_engine_fail(ds->e, HM_ERR_INVALID, "docset busy");
+    DocSt &d = ds->doc(doc);
+    if (d.cls == NO_CLASS) return 0;
+    return hm_doc_history_prefix(ds->stores[d.cls], d.handle, n, out);
+}
+
+int hm_docset_clock_update(hm_docset *ds, uint32_t n, const uint32_t *docs, uint8_t *out_written, uint8_t *out_differs,
+                           hm_text **out_stored) {
+    if (!ds || (n && !docs)) return HM_ERR_INVALID;
+    Busy b(ds);
+    if (!b.ok) return hm_engine_fail(ds->e, HM_ERR_INVALID, "docset busy");
+    try {
+        const uint32_t nd = ds->n_docs.load();
+        for (uint32_t i = 0; i < n; i++) if (docs[i] >= nd) return hm_engine_fail(ds->e, HM_ERR_INVALID, "bad docset document");
+        std::vector<std::string> js(n, "{}");
+        for (uint32_t c = 0; c < N_CLASS; c++) {
+            std::vector<uint32_t> idx, hs;
+            for (uint32_t i = 0; i < n; i++) if (ds->doc(docs[i]).cls == c) { idx.push_back(i); hs.push_back(ds->doc(docs[i]).handle); }
+            if (idx.empty()) continue;
+            const uint32_t S = STRIDES[c], k = (uint32_t)idx.size();
+            std::vector<uint8_t> w(k), df(k);
+            std::vector<uint32_t> stv((size_t)k * S);
+            const int rc = hm_store_clock_update(ds->stores[c], k, hs.data(), w.data(), df.data(), stv.data());
+            if (rc) return rc;
+            for (uint32_t j = 0; j < k; j++) {
+                const uint32_t i = idx[j];
+                if (out_written) out_written[i] = w[j];
+                if (out_differs) out_differs[i] = df[j];
+                js[i].clear();
+                const DocSt &d = ds->doc(docs[i]);
+                jclock(js[i], d, stv.data() + (size_t)j * S, d.actors.size());
+            }
+        }
+        for (uint32_t i = 0; i < n; i++) if (ds->doc(docs[i]).cls == NO_CLASS) {
+            if (out_written) out_written[i] = 0;
+            if (out_differs) out_differs[i] = 0;
+        }
+        if (out_stored) {
+            std::unique_ptr<hm_text> t(new hm_text());
+            t->s = "[";
+            for (uint32_t i = 0; i < n; i++) { if (i) t->s += ','; t->s += js[i]; }
+            t->s += ']';
+            *out_stored = t.release();
+        }
+        return HM_OK;
+    } catch (...) {
+        return hm_engine_fail(ds->e, HM_ERR_NOMEM, "exception in hm_docset_clock_update");
+    }
+}
+
+int hm_docset_view(hm_docset *ds, uint32_t doc, hm_text **out) {
+    if (!ds || !out || doc >= ds->n_docs.load()) return HM_ERR_INVALID;
+    *out = nullptr;
+    Busy b(ds);
+    if (!b.ok) return hm_engine_fail(ds->e, HM_ERR_INVALID, "docset busy");
+    try {
+        DocSt &d = ds->doc(doc);
+        if (!d.ready) d.setup();
+        std::unique_ptr<hm_text> t(new hm_text());
+        if (d.cls == NO_CLASS) {
+            render_view(t->s, d, nullptr, nullptr, 0);
+        } else {
+            hm_doc_info_t inf;
+            int rc = hm_doc_info(ds->stores[d.cls], d.handle, &inf);
+            if (rc) return rc;
+            std::vector<hm_reg_result> regs(inf.n_regs + 1);
+            std::vector<hm_surv_result> surv(inf.n_ops + 1);
+            rc = hm_doc_read(ds->stores[d.cls], d.handle, nullptr, nullptr, regs.data(), surv.data(), nullptr, nullptr, nullptr);
+            if (rc) return rc;
+            render_view(t->s, d, regs.data(), surv.data(), inf.n_regs);
+        }
+        *out = t.release();
+        return HM_OK;
+    } catch (...) {
+        return hm_engine_fail(ds->e, HM_ERR_NOMEM, "exception in hm_docset_view");
+    }
+}
+
+int hm_docset_stats(const hm_docset *ds, uint64_t *out8) {
+    if (!ds || !out8) return HM_ERR_INVALID;
+    for (int i = 0; i < 8; i++) out8[i] = ds->stat[i];
+    return HM_OK;
+}
+
+}  // extern "C"

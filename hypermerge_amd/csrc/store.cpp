@@ -21,6 +21,7 @@
 // is a left fold of addChange, so the state after A then B is the state after A ++ B).
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -76,7 +77,7 @@ struct hm_store {
     // staging (device)
     DBuf<uint8_t> stage;
     // in-flight batch
-    bool pending = false;
+    std::atomic<bool> pending{false};             // a submitted batch not yet waited for (other threads may read it)
     uint64_t next_id = 1, pending_id = 0;
     std::vector<uint32_t> p_handles;              // batch rows -> handles
     struct OldMeta { uint32_t n_c, n_d, n_o, n_r, n_objs; uint16_t n_actors, flags; };
@@ -628,9 +629,11 @@ int hm_batch_wait(hm_store *s, uint64_t batch_id, hm_doc_result *out_docs, uint3
         SCHK(s, hipSetDevice(hm_engine_device(s->e)));        // the caller may be a host thread of its own
         hipStream_t st = hm_engine_stream(s->e);
         PhaseTimer T(st);
+        // the batch stays in flight (pending) until this returns: copy-out and rollback below
+        // still read and re-merge the store's documents
+        struct Clear { std::atomic<bool> &p; ~Clear() { p.store(false); } } clear_pending{s->pending};
         SCHK(s, hipStreamSynchronize(st));
         T.mark("wait sync");
-        s->pending = false;
         const uint32_t n = (uint32_t)s->p_handles.size(), S = s->S;
         // results straight from the gathered device rows into the caller's arrays
         std::vector<hm_doc_result> tmp;
@@ -846,6 +849,33 @@ int hm_sync_ranges_device(hm_engine *e, const uint64_t *present, const uint64_t 
     hipError_t r = hm_launch_sync_ranges(present, word_off, lo, hi, out_end, n,
                                          stream ? (hipStream_t)stream : hm_engine_stream(e));
     return r == hipSuccess ? HM_OK : hm_engine_fail(e, HM_ERR_DEVICE, "sync_ranges launch");
+}
+
+int hm_sync_ranges_host(hm_engine *e, const uint64_t *present, const uint64_t *word_off, const uint32_t *lo,
+                        const uint32_t *hi, uint32_t *out_end, uint32_t n, uint32_t n_words) {
+    if (!e || (n && (!present || !word_off || !lo || !hi || !out_end))) return HM_ERR_INVALID;
+    if (!n) return HM_OK;
+    for (uint32_t i = 0; i < n; i++)
+        if (word_off[i] > n_words || hi[i] < lo[i] || word_off[i] + ((uint64_t)hi[i] + 63) / 64 > n_words)
+            return hm_engine_fail(e, HM_ERR_INVALID, "sync range outside the present bitmap");
+    hipStream_t st = hm_engine_stream(e);
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_p = 0, o_w = al(8 * (size_t)n_words + 8), o_lo = o_w + al(8 * (size_t)n), o_hi = o_lo + al(4 * (size_t)n),
+                 o_out = o_hi + al(4 * (size_t)n), total = o_out + al(4 * (size_t)n);
+    uint8_t *sp = nullptr;
+    if (hipMalloc((void **)&sp, total) != hipSuccess) return hm_engine_fail(e, HM_ERR_NOMEM, "hipMalloc sync staging");
+    int rc = HM_OK;
+    if (hipMemcpyAsync(sp + o_p, present, 8 * (size_t)n_words, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(sp + o_w, word_off, 8 * (size_t)n, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(sp + o_lo, lo, 4 * (size_t)n, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(sp + o_hi, hi, 4 * (size_t)n, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hm_launch_sync_ranges((const uint64_t *)(sp + o_p), (const uint64_t *)(sp + o_w), (const uint32_t *)(sp + o_lo),
+                              (const uint32_t *)(sp + o_hi), (uint32_t *)(sp + o_out), n, st) != hipSuccess ||
+        hipMemcpyAsync(out_end, sp + o_out, 4 * (size_t)n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        rc = hm_engine_fail(e, HM_ERR_DEVICE, "hm_sync_ranges_host");
+    (void)hipFree(sp);
+    return rc;
 }
 
 }  // extern "C"

@@ -31,7 +31,10 @@ EXPORTS = ("hm_abi_version", "hm_status_message", "hm_engine_create", "hm_engine
            "hm_decoded_string", "hm_decoded_actor", "hm_decoded_obj", "hm_decoded_reg", "hm_decoded_free",
            "hm_store_set_incremental", "hm_store_last_routing", "hm_doc_open_n", "hm_store_read_regs",
            "hm_cursors_create", "hm_cursors_destroy", "hm_cursors_reserve", "hm_cursors_update", "hm_cursors_get",
-           "hm_cursors_entry", "hm_cursors_docs_with_actors")
+           "hm_cursors_entry", "hm_cursors_docs_with_actors", "hm_docset_create", "hm_docset_destroy",
+           "hm_docset_engine", "hm_docset_open", "hm_docset_apply", "hm_text_data", "hm_text_results", "hm_text_free",
+           "hm_docset_doc_info", "hm_docset_history_prefix", "hm_docset_clock_update", "hm_docset_view",
+           "hm_docset_stats", "hm_sync_ranges_host")
 
 _lib = None
 
@@ -96,6 +99,12 @@ def lib():
             "hm_cursors_update": [vp, u32, vp, vp, vp, vp, vp], "hm_cursors_get": [vp, u32, vp, vp, vp, vp],
             "hm_cursors_entry": [vp, u32, vp, vp, vp],
             "hm_cursors_docs_with_actors": [vp, u32, vp, vp, u32, vp, vp, vp, vp],
+            "hm_docset_create": [vp, vp, vp], "hm_docset_destroy": [vp], "hm_docset_engine": [vp],
+            "hm_docset_open": [vp, u32, vp], "hm_docset_apply": [vp, vp, vp, vp, vp, u32, vp],
+            "hm_text_data": [vp, vp], "hm_text_results": [vp, vp], "hm_text_free": [vp],
+            "hm_docset_doc_info": [vp, u32, vp], "hm_docset_history_prefix": [vp, u32, u32, vp],
+            "hm_docset_clock_update": [vp, u32, vp, vp, vp, vp], "hm_docset_view": [vp, u32, vp],
+            "hm_docset_stats": [vp, vp], "hm_sync_ranges_host": [vp, vp, vp, vp, vp, vp, u32, u32],
         }
         for f, a in sig.items():
             getattr(L, f).argtypes = a
@@ -110,6 +119,11 @@ def lib():
         L.hm_decoded_reg.restype = ctypes.c_void_p
         L.hm_decoded_free.restype = None
         L.hm_clock_records_scratch_bytes.restype = ctypes.c_size_t
+        L.hm_docset_destroy.restype = None
+        L.hm_docset_engine.restype = ctypes.c_void_p
+        L.hm_text_data.restype = ctypes.c_void_p
+        L.hm_text_results.restype = ctypes.c_void_p
+        L.hm_text_free.restype = None
         _lib = L
     return _lib
 

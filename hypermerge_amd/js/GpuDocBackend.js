@@ -10,31 +10,33 @@
 //                (id, actorId, clock, back, changes, ready) and methods (init, initActor,
 //                applyRemoteChanges, applyLocalChange, updateMinimumClock), same
 //                ReadyMsg / ActorIdMsg / RemotePatchMsg / LocalPatchMsg messages.
-//   GpuEngine    owns the device store (N-API addon -> include/hypermerge_amd.h) and runs
-//                every document's applyChanges calls as batched GPU submits: per-document
-//                FIFO job queues, one submit per round over all documents with work.
-//                mode 'sync' flushes inside the caller's stack (the reference's Queue
-//                semantics: a push runs the merge synchronously); mode 'batched' flushes
-//                once per event-loop turn (setImmediate), merging every document that
-//                received changes during the turn in one launch; mode 'async' does the
-//                same but waits for the device on the store's host thread (waitAsync,
-//                completion through a napi_threadsafe_function), so the event loop never
-//                blocks on the GPU.
-//                Patches are incremental: after a round in which a document's new changes
-//                all applied, only the registers its new ops hit are read back
-//                (hm_store_read_regs, one call per store and round) and diffed against the
-//                document's previous view; otherwise the whole document is re-read.
+//   GpuEngine    one docset per device (N-API addon -> hm_docset_* in include/hypermerge_amd.h):
+//                every document's applyChanges calls run as batched rounds, per-document FIFO
+//                job queues, one hm_docset_apply per device and round over all documents
+//                with work.  The docset does everything per document natively: the blocks'
+//                JSON (Actor.parseBlock, src/Actor.ts:137-141), the interning, the merge on
+//                the GPU, the patch diffs and clocks (rendered as JSON, one JSON.parse per
+//                round here).  Changes may be handed over as Change objects (stringified
+//                here), JSON strings or raw hypercore blocks (Buffers: '{"' JSON or 'BR' +
+//                brotli), the last skipping Actor.parseBlock altogether.
+//                mode 'sync' runs the round inside the caller's stack (the reference's Queue
+//                semantics: a push runs the merge synchronously); mode 'batched' once per
+//                event-loop turn (setImmediate) over every document that received changes
+//                during the turn; mode 'async' the same with the round on the docset's host
+//                thread (completion through a napi_threadsafe_function), so the event loop
+//                never blocks on decode, the GPU or the patch rendering.
 //   ClockStore   the reference's clock table semantics (src/ClockStore.ts:24-112) kept in
 //                host memory, with updateDocs(): ClockStore.update(repo, doc, doc.clock)
-//                for many documents from one GPU upsert-max (hm_store_clock_update).
+//                for many documents from one GPU upsert-max per device.
+//   CursorStore  the reference's cursor table (src/CursorStore.ts:19-91) on the device, batched,
+//                and syncPlan(): RepoBackend.syncChanges' ranges (src/RepoBackend.ts:506-531).
 //
-// A document's applyChanges that throws (e.g. 'Inconsistent reuse of sequence number')
-// is rolled back on the device and rethrown here, like the reference's throw out of
+// A document's applyChanges that throws (e.g. 'Inconsistent reuse of sequence number') is
+// rolled back natively and rethrown here, like the reference's throw out of
 // Backend.applyChanges leaves DocBackend.back unchanged.
 
 const path = require('path')
 const addon = require(path.join(__dirname, '..', '_lib', 'hmgpu.node'))
-const C = require('./columnar')
 const Clock = require('./clocks')
 const Channel = require('./channel')
 
@@ -46,6 +48,21 @@ const ERR_TEXT = {
   5: 'Missing index entry for list element',
   16: 'Document outside the engine envelope',
 }
+const NONE = 0xffffffff
+const RESULT_U32 = 8                   // hm_doc_result: 32 B
+
+// a log entry as the docset takes it: raw block (Buffer), JSON text, or a Change object
+const toBlock = (c) => (Buffer.isBuffer(c) || typeof c === 'string' ? c : JSON.stringify(c))
+// ... and as the reference's history holds it (Block.unpack, src/Block.ts:18-29)
+const zlib = require('zlib')
+function toChange(c) {
+  if (typeof c === 'string') return JSON.parse(c)
+  if (!Buffer.isBuffer(c)) return c
+  const header = c.slice(0, 2).toString()
+  if (header === '{"') return JSON.parse(c.toString())
+  if (header === 'BR') return JSON.parse(zlib.brotliDecompressSync(c.slice(2)).toString())
+  throw new Error(`fail to unpack blocks - head is '${header}'`)
+}
 
 class History {
   constructor(state) { this.state = state; this.size = state.histLen }
@@ -53,9 +70,9 @@ class History {
     const st = this.state
     const lo = a || 0
     const hi = b === undefined ? this.size : Math.min(b, this.size)
-    const idx = addon.historyPrefix(st.store, st.handle, Math.max(hi, 0))
+    const idx = addon.docsetHistoryPrefix(st.ds, st.id, Math.max(hi, 0))
     const out = []
-    for (let i = lo; i < idx.length / 4; i++) out.push(st.log[idx.readUInt32LE(4 * i)])
+    for (let i = lo; i < idx.length / 4; i++) out.push(st.change(idx.readUInt32LE(4 * i)))
     return { toArray: () => out, size: out.length }
   }
 }
@@ -69,38 +86,34 @@ function fnv1a64(s) {
   return h
 }
 
-// Row widths of the stores a document can live in: a document starts in the narrowest that
-// holds its actors and moves to a wider one when a new actor outgrows it (its whole log is
-// re-merged there, once).
-const STRIDES = [8, 16, 32, 64]
-
-// The per-document BackendState: a handle into one device store (its shard's, at its stride)
-// plus the host-side interner and the change objects of the log (for history slices and
-// re-striding).  States are linear: applyChanges advances the document in place and returns
-// the same state object.
+// The per-document BackendState: a document of its shard's docset plus the log entries as
+// they were handed over (history slices).  States are linear: applyChanges advances the
+// document in place and returns the same state object.
 class GpuBackendState {
   constructor(engine, docId) {
     this.engine = engine
     this.docId = docId
     this.shard = docId === undefined ? 0 : engine.shardOf(docId)
-    this.stride = engine.minStride
-    this.store = engine.storeFor(this.shard, this.stride)
-    this.handle = addon.openDoc(this.store)
-    this.enc = new C.DocEncoder(engine.pool)
+    this.ds = engine.docsets[this.shard]
+    this.id = addon.docsetOpen(this.ds, 1)
     this.log = []
-    this.opActor = []                // doc-local op index -> [op, actor] (the log's ops in order)
-    this.view = null                 // materialized view of the last patch (diff base)
-    this.objType = new Map([[0, 0]]) // obj id -> make action (ROOT = map), kept per round
-    this.newObjs = []                // objects the last round created
-    this.roundSeq = 0                // rounds applied ...
-    this.patchedSeq = 0              // ... and the round the view reflects
-    this.pendingRegs = null          // registers the last round's ops hit, read back (incremental patch)
     this.histLen = 0
     this.nQueued = 0
     this.clock = {}
     this.deps = {}
-    this.backClock = {}              // DocBackend.clock as the engine computed it (queued included)
+    this.backClock = {}              // max seq per actor over the whole log (queued included)
+    this.patch = null                // the last round's patch
   }
+
+  change(i) {
+    const c = this.log[i]
+    if (c !== null && typeof c === 'object' && !Buffer.isBuffer(c)) return c
+    const o = toChange(c)
+    this.log[i] = o
+    return o
+  }
+
+  get stride() { return addon.docsetInfo(this.ds, this.id).aStride }
 
   getIn(p) {
     if (p.length === 2 && p[0] === 'opSet' && p[1] === 'history') return new History(this)
@@ -112,38 +125,35 @@ class GpuBackendState {
 
 class GpuEngine {
   // opts: devices (HIP ordinals; documents shard over them by FNV-1a64(docId) % devices.length),
-  // aStride (narrowest store stride), mode 'sync' | 'batched', onError, patches
+  // mode 'sync' | 'batched' | 'async', patches (diffs on), threads (host threads per docset),
+  // onError
   constructor(opts) {
     const o = opts || {}
     this.devices = o.devices || [o.device || 0]
-    this.minStride = o.aStride || 8
-    this.aStride = this.minStride
     this.mode = o.mode || 'batched'
-    this.shards = this.devices.map((d) => ({ device: d, stores: new Map() }))
-    this.store = this.storeFor(0, this.minStride)
-    this.pool = new C.StringPool()
+    this.patches = o.patches !== false
+    this.docsets = this.devices.map((d) => addon.docsetCreate(d, o.threads || 0, this.patches))
     this.queues = new Map()          // state -> FIFO of jobs
     this.flushing = false
     this.scheduled = false
     this.onError = o.onError || null
     this.submits = 0
-    this.restrides = 0
-    this.patches = o.patches !== false  // emit patch diffs (one device read per patch)
     this.comm = null
   }
 
-  shardOf(docId) { return Number(fnv1a64(docId) % BigInt(this.shards.length)) }
-
-  storeFor(shard, stride) {
-    const sh = this.shards[shard]
-    let st = sh.stores.get(stride)
-    if (!st) { st = addon.createStore(sh.device, stride); sh.stores.set(stride, st) }
-    return st
-  }
+  shardOf(docId) { return Number(fnv1a64(docId) % BigInt(this.docsets.length)) }
 
   init(docId) { return new GpuBackendState(this, docId) }
 
-  // job: {changes|null, extraActors, done(result|null), fail(err)}
+  stats() {
+    const t = { calls: 0, docs: 0, moves: 0, hitPatches: 0, fullPatches: 0 }
+    for (const ds of this.docsets) { const s = addon.docsetStats(ds); for (const k in t) t[k] += s[k] }
+    return t
+  }
+
+  get restrides() { return this.stats().moves }
+
+  // job: {entries|null, done(payload|null), fail(err)}
   enqueue(state, job) {
     let q = this.queues.get(state)
     if (!q) { q = []; this.queues.set(state, q) }
@@ -160,7 +170,7 @@ class GpuEngine {
     for (;;) {
       const round = []
       for (const [state, q] of Array.from(this.queues)) {
-        while (q.length && q[0].changes === null) q.shift().done(null)
+        while (q.length && q[0].entries === null) q.shift().done(null)
         if (q.length) round.push([state, q.shift()])
         else this.queues.delete(state)
       }
@@ -205,33 +215,44 @@ class GpuEngine {
     })
   }
 
-  // One applyChanges per document of the round: the documents of each store (device shard x
-  // stride) go to that store as one batch; every store's batch is submitted before any is
-  // waited for, so the devices merge at once.
+  // the round's documents grouped by docset (device shard), with their blocks
+  groups(round) {
+    const g = new Map()
+    for (const [state, job] of round) {
+      let x = g.get(state.ds)
+      if (!x) { x = { ds: state.ds, items: [] }; g.set(state.ds, x) }
+      x.items.push({ state, job })
+    }
+    for (const x of g.values()) {
+      x.ids = Uint32Array.from(x.items, (it) => it.state.id)
+      x.blocks = x.items.map((it) => it.job.entries.map(toBlock))
+    }
+    return Array.from(g.values())
+  }
+
+  // One applyChanges per document of the round, one docset call per device
   runRound(round) {
-    const { pending, errors } = this.submitRound(round)
-    for (const p of pending) this.finishStore(p, addon.wait(p.store, p.id), errors)
+    const errors = []
+    for (const g of this.groups(round)) this.finish(g, addon.docsetApply(g.ds, g.ids, g.blocks), errors)
     this.raise(errors)
   }
 
   runRoundAsync(round, done) {
-    let sub
+    let gs
     try {
-      sub = this.submitRound(round)
+      gs = this.groups(round)
     } catch (e) {
       done()
       throw e
     }
-    const { pending, errors } = sub
-    let left = pending.length
+    const errors = []
+    let left = gs.length
     const finish = () => { try { this.raise(errors) } finally { done() } }
-    if (!left) { finish(); return }
-    for (const p of pending) {
-      addon.waitAsync(p.store, p.id, (err, r) => {
+    for (const g of gs) {
+      addon.docsetApply(g.ds, g.ids, g.blocks, (err, r) => {
         try {
-          if (err) {
-            p.items.forEach(({ state, job, snap, moved }) => { if (!moved) state.enc.restore(snap); errors.push([job, err]) })
-          } else this.finishStore(p, r, errors)
+          if (err) g.items.forEach(({ job }) => errors.push([job, err]))
+          else this.finish(g, r, errors)
         } finally {
           if (--left === 0) finish()
         }
@@ -239,121 +260,28 @@ class GpuEngine {
     }
   }
 
-  submitRound(round) {
-    const groups = new Map()         // store -> [{state, job, snap, append, moved}]
-    const errors = []
-    for (const [state, job] of round) {
-      const snap = state.enc.snapshot()
-      let a = state.enc.encode(job.changes, job.extraActors)
-      let moved = null
-      if (a.nActors > state.stride) {
-        // a new actor outgrew the document's store: re-merge its whole log in a wider one
-        state.enc.restore(snap)
-        const stride = STRIDES.find((x) => x >= a.nActors)
-        if (stride === undefined) {
-          errors.push([job, new Error(`document has ${a.nActors} actors > ${STRIDES[STRIDES.length - 1]}`)])
-          continue
-        }
-        const enc = new C.DocEncoder(this.pool)
-        const store = this.storeFor(state.shard, stride)
-        a = enc.encode(state.log.concat(job.changes), job.extraActors)
-        moved = { enc, store, stride, handle: addon.openDoc(store) }
-      }
-      const store = moved ? moved.store : state.store
-      if (!groups.has(store)) groups.set(store, [])
-      groups.get(store).push({ state, job, snap, append: a, moved })
-    }
-    const pending = []
-    for (const [store, items] of groups) {
-      const stride = items[0].moved ? items[0].moved.stride : items[0].state.stride
-      const b = C.buildBatch(items.map((it) => it.append), stride)
-      const handles = Uint32Array.from(items.map((it) => (it.moved ? it.moved.handle : it.state.handle)))
-      pending.push({ store, stride, items, id: addon.submit(store, b.docs, b.changes, b.deps, b.ops, handles, b.remap) })
-    }
-    return { pending, errors }
-  }
-
-  finishStore({ store, stride: S, items }, r, errors) {
+  finish({ items }, r, errors) {
     this.submits++
+    const res = new Uint32Array(r.results.buffer, r.results.byteOffset, r.results.length / 4)
+    const j = JSON.parse(r.json)
     const ok = []
-    items.forEach((it, i) => {
-      const { state, job, snap, moved, append } = it
-      const res = C.readDocResult(r.docs, i)
-      if (res.status !== 0) {
-        if (!moved) state.enc.restore(snap)
-        errors.push([job, this.errorFor(state, job.changes, res)])
+    items.forEach(({ state, job }, i) => {
+      const status = res[RESULT_U32 * i] | 0
+      if (status !== 0) {
+        errors.push([job, this.errorFor(state, job.entries, status, res[RESULT_U32 * i + 1], res[RESULT_U32 * i + 2])])
         return
       }
-      if (moved) {
-        Object.assign(state, { enc: moved.enc, store: moved.store, stride: moved.stride, handle: moved.handle })
-        state.objType = null           // ids re-encoded: rebuilt from the log at the next patch
-        this.restrides++
-      }
-      const base = state.log.length
-      state.log.push(...job.changes)
-      for (const c of job.changes) for (const op of c.ops || []) state.opActor.push([op, c.actor])
-      // objects this round created (make ops, first creation wins)
-      state.newObjs = []
-      if (state.objType && !moved) {
-        for (let k = 0; k < append.ops.length / C.OP_ROW; k++) {
-          const act = append.ops[k * C.OP_ROW + 16]
-          if (act > C.ACTIONS.makeText) continue
-          const o = append.ops.readUInt32LE(k * C.OP_ROW)
-          if (!state.objType.has(o)) { state.objType.set(o, act); state.newObjs.push(o) }
-        }
-      }
-      const prevHist = state.histLen, prevQueued = state.nQueued, prevSeq = state.roundSeq
-      state.roundSeq++
-      state.histLen = res.histLen
-      state.nQueued = res.nQueued
-      state.clock = Clock.fromRow(r.clock, i * S * 4, state.enc.actors)
-      state.deps = Clock.fromRow(r.heads, i * S * 4, state.enc.actors)
-      const backClock = Clock.fromRow(r.backClock, i * S * 4, state.enc.actors)
-      state.backClock = backClock
-      // incremental patch: the view is current up to the previous round (a fresh document's
-      // view is the empty root map) and every new change applied
-      if (state.view === null && prevSeq === 0 && state.patchedSeq === 0)
-        state.view = new Map([[C.ROOT_ID, { type: 'map', keys: new Map(), elems: [] }]])
-      const simple = !moved && state.view !== null && state.objType !== null && state.patchedSeq === prevSeq &&
-        prevQueued === 0 && res.nQueued === 0 && res.histLen - prevHist === job.changes.length
-      ok.push({ state, job, res, append, simple, payload: { res, base, prevHist, backClock, minCmp: Clock.CMP_CODES[res.minCmp] } })
+      for (const c of job.entries) state.log.push(c)
+      state.histLen = res[RESULT_U32 * i + 3]
+      state.nQueued = res[RESULT_U32 * i + 4]
+      const patch = j.p[i]
+      state.patch = patch
+      state.clock = patch.clock
+      state.deps = patch.deps
+      state.backClock = j.b[i]
+      ok.push([job, { patch, roundClock: j.c[i], backClock: j.b[i], minCmp: null }])
     })
-    if (this.patches) this.prefetchRegs(store, ok)
-    for (const e of ok) e.job.done(e.payload)
-  }
-
-  // one read of the registers the round's new ops hit, for every simple document of the store
-  prefetchRegs(store, ok) {
-    const docs = [], regs = [], owners = []
-    let cap = 0
-    for (const e of ok) {
-      const st = e.state
-      st.pendingRegs = null
-      if (!e.simple) continue
-      st.pendingRegs = []
-      const seen = new Set()
-      for (let k = 0; k < e.append.ops.length / C.OP_ROW; k++) {
-        const act = e.append.ops[k * C.OP_ROW + 16]
-        if (act < C.ACTIONS.set) continue                   // make / ins: no visible value of their own
-        const g = e.append.ops.readUInt32LE(k * C.OP_ROW + 4)
-        if (g === C.NONE || seen.has(g)) continue
-        seen.add(g)
-        docs.push(st.handle); regs.push(g); owners.push(st)
-      }
-      cap += e.res.nSurv
-    }
-    if (!regs.length) return
-    const rr = addon.readRegs(store, Uint32Array.from(docs), Uint32Array.from(regs), cap)
-    for (let q = 0; q < regs.length; q++) {
-      const b = q * C.REG_RESULT
-      const n = rr.regs.readUInt32LE(b), off = rr.regs.readUInt32LE(b + 4)
-      const surv = []
-      for (let x = 0; x < n; x++) {
-        const sb = (off + x) * C.SURV_RESULT
-        surv.push([rr.surv.readUInt32LE(sb), rr.surv.readUInt32LE(sb + 4), rr.surv.readUInt32LE(sb + 8), rr.surv.readUInt32LE(sb + 12)])
-      }
-      owners[q].pendingRegs.push({ g: regs[q], n, li: rr.regs.readInt32LE(b + 8), o: rr.regs.readUInt32LE(b + 12), surv })
-    }
+    for (const [job, payload] of ok) job.done(payload)
   }
 
   raise(errors) {
@@ -364,18 +292,34 @@ class GpuEngine {
     }
   }
 
-  errorFor(state, changes, res) {
-    const text = ERR_TEXT[res.status] || `engine status ${res.status}`
-    const all = state.log.concat(changes)
-    const c = res.errChange < all.length ? all[res.errChange] : null
+  // the reference's Error for a document whose round failed (status, change index, op index)
+  errorFor(state, entries, status, errChange, errOp) {
+    if (status === 32) {
+      // a block that does not decode: the throw of Block.unpack / JSON.parse (src/Block.ts:18-29)
+      const c = entries[errChange]
+      try {
+        toChange(toBlock(c))
+      } catch (e) {
+        return e
+      }
+      const e = new Error('Malformed change: not an Automerge 0.12 change')
+      e.status = status
+      return e
+    }
+    const text = ERR_TEXT[status] || `engine status ${status}`
+    const n = state.log.length
+    let c = null
+    try {
+      c = errChange < n ? state.change(errChange) : errChange - n < entries.length ? toChange(entries[errChange - n]) : null
+    } catch (_) { c = null }
     let detail = ''
-    if (c && res.status === 1) detail = ` ${c.seq} by ${c.actor}`
-    else if (c && res.errOp !== C.NONE && c.ops && c.ops[res.errOp]) {
-      const op = c.ops[res.errOp]
-      detail = res.status === 4 ? ` ${c.actor}:${op.elem}` : res.status === 5 ? ` ${op.key}` : ` ${op.obj}`
+    if (c && status === 1) detail = ` ${c.seq} by ${c.actor}`
+    else if (c && errOp !== NONE && c.ops && c.ops[errOp]) {
+      const op = c.ops[errOp]
+      detail = status === 4 ? ` ${c.actor}:${op.elem}` : status === 5 ? ` ${op.key}` : ` ${op.obj}`
     }
     const e = new Error(text + detail)
-    e.status = res.status
+    e.status = status
     return e
   }
 
@@ -386,7 +330,7 @@ class GpuEngine {
     const prevMode = this.mode
     this.mode = 'sync'
     try {
-      this.enqueue(state, { changes, done: (r) => { out = r }, fail: (e) => { err = e } })
+      this.enqueue(state, { entries: changes, done: (r) => { out = r }, fail: (e) => { err = e } })
     } finally {
       this.mode = prevMode
     }
@@ -395,12 +339,12 @@ class GpuEngine {
   }
 
   // ---- the node-wide ClockStore feed (CursorMessage clocks, src/RepoBackend.ts:374-392) ----
-  // Every shard's documents' DocBackend.clock entries as repo-global records
-  // (FNV-1a64(docId), FNV-1a64(actorId), seq) gathered across the devices over RCCL
-  // (hm_comm_create_local + hm_clock_exchange_host) when they are distinct GPUs, and
-  // turned back into {docId: {actorId: seq}} with the host's id tables.
+  // Every shard's documents' clock entries as repo-global records (FNV-1a64(docId),
+  // FNV-1a64(actorId), seq) gathered across the devices over RCCL (hm_comm_create_local +
+  // hm_clock_exchange_host) when they are distinct GPUs, and turned back into
+  // {docId: {actorId: seq}} with the host's id tables.
   exchangeClocks(states) {
-    const perShard = this.shards.map(() => [])
+    const perShard = this.docsets.map(() => [])
     const ids = new Map()
     for (const st of states) {
       const dk = fnv1a64(st.docId)
@@ -419,7 +363,7 @@ class GpuEngine {
     let all
     const distinct = new Set(this.devices).size === this.devices.length
     if (distinct) {
-      if (!this.comm) this.comm = addon.commCreateLocal(this.shards.map((sh) => this.storeFor(this.shards.indexOf(sh), this.minStride)))
+      if (!this.comm) this.comm = addon.commCreateLocalDocsets(this.docsets)
       all = addon.clockExchange(this.comm, bufs)
     } else all = Buffer.concat(bufs)           // shards sharing one device: the host holds them all
     const out = {}
@@ -434,202 +378,48 @@ class GpuEngine {
 }
 
 // ---------------- patches (Automerge makePatch, consumed by Frontend.applyPatch) ----------------
-// clock / deps are applied-only (queued changes excluded).  `diffs` turn the frontend's copy of
-// the document from the state of the previous patch into the current one, in the Automerge 0.12
-// diff vocabulary (SURVEY.md Appendix A.4): {action:'create', obj, type},
-// {action:'set'|'remove', type:'map'|'table', obj, key, value, link?, datatype?, conflicts?},
-// {action:'insert'|'set'|'remove', type:'list'|'text', obj, index, elemId?, value, ...}.
-// They are derived from the GPU's merged registers (one diff per changed register / element,
-// removals before insertions), not replayed op by op: the document a frontend builds from them
-// equals the merged state, but the diff sequence is not Automerge's per-op sequence (parity of
-// that sequence is unpinned: Automerge 0.12 is not available here).
-const TYPE_OF = { 0: 'map', 1: 'table', 2: 'list', 3: 'text' }
-const DT_NAME = { 1: 'counter', 2: 'timestamp' }
-const TWO32 = 4294967296
+// Each round's patch comes from the docset: clock / deps are applied-only (queued changes
+// excluded); `diffs` turn the frontend's copy of the document from the state of the previous
+// patch into the current one, in the Automerge 0.12 diff vocabulary (SURVEY.md Appendix A.4):
+// {action:'create', obj, type}, {action:'set'|'remove', type:'map'|'table', obj, key, value,
+// link?, datatype?, conflicts?}, {action:'insert'|'set'|'remove', type:'list'|'text', obj,
+// index, elemId?, value, ...}: one diff per register whose rendered value changed (map keys in
+// the order the round's ops first hit them; per list removals, insertions, value changes).
+// The document a frontend builds from them equals the merged state; the exact per-op
+// sequence of Automerge is unpinned (Automerge 0.12 is not available here).
 
-function opValue(state, vtag, lo, hi) {
-  switch (vtag) {
-    case C.V.NULL: return { value: null }
-    case C.V.FALSE: return { value: false }
-    case C.V.TRUE: return { value: true }
-    case C.V.INT: return { value: hi >= 0x80000000 ? (hi - TWO32) * TWO32 + lo : hi * TWO32 + lo }
-    case C.V.FLOAT: { const b = Buffer.alloc(8); b.writeUInt32LE(lo, 0); b.writeUInt32LE(hi, 4); return { value: b.readDoubleLE(0) } }
-    case C.V.STR: return { value: state.engine.pool.strings[lo] }
-    case C.V.OBJ: return { value: state.enc.objList[lo], link: true }
-    default: throw new Error(`unknown value tag ${vtag}`)
-  }
-}
-
-function objTypes(state) {
-  if (state.objType) return state.objType
-  const objType = new Map([[0, 0]])
-  for (const [op] of state.opActor) {
-    const a = C.ACTIONS[op.action]
-    if (a <= C.ACTIONS.makeText) { const o = state.enc.objs.get(op.obj); if (!objType.has(o)) objType.set(o, a) }
-  }
-  state.objType = objType
-  return objType
-}
-
-// a register's survivors [[op, vtag, lo, hi]] -> a diff value with conflicts
-function entryOf(state, surv) {
-  const vals = surv.map(([k, vt, lo, hi]) => {
-    const [op, actor] = state.opActor[k]
-    const v = opValue(state, vt, lo, hi)
-    if (op.datatype) v.datatype = op.datatype
-    return [actor, v]
-  })
-  const entry = Object.assign({}, vals[0][1])
-  if (vals.length > 1) entry.conflicts = vals.slice(1).map(([actor, v]) => Object.assign({ actor }, v))
-  return entry
-}
-
-// the merged document as {objUuid -> {type, keys: Map(key -> entry) | elems: [[elemId, entry]]}}
+// the merged document as {objUuid -> {type, keys: Map(key -> entry), elems: [[elemId, entry]]}}
 function materialize(state) {
-  const r = addon.read(state.store, state.handle)
-  const objType = objTypes(state)
+  const v = JSON.parse(addon.docsetView(state.ds, state.id))
   const view = new Map()
-  const nRegs = r.regs.length / C.REG_RESULT
-  for (let g = 0; g < nRegs; g++) {
-    const b = g * C.REG_RESULT
-    const n = r.regs.readUInt32LE(b), off = r.regs.readUInt32LE(b + 4), li = r.regs.readInt32LE(b + 8), o = r.regs.readUInt32LE(b + 12)
-    if (!n || o === C.NONE) continue
-    const t = objType.has(o) ? objType.get(o) : 0
-    const list = t === 2 || t === 3
-    if (list && li < 0) continue
-    const surv = []
-    for (let q = 0; q < n; q++) {
-      const sb = (off + q) * C.SURV_RESULT
-      surv.push([r.surv.readUInt32LE(sb), r.surv.readUInt32LE(sb + 4), r.surv.readUInt32LE(sb + 8), r.surv.readUInt32LE(sb + 12)])
-    }
-    const entry = entryOf(state, surv)
-    const uuid = state.enc.objList[o]
-    let ov = view.get(uuid)
-    if (!ov) { ov = { type: TYPE_OF[t], keys: new Map(), elems: [] }; view.set(uuid, ov) }
-    const key = state.enc.regList[g][1]
-    if (list) ov.elems[li] = [key, entry]
-    else ov.keys.set(key, entry)
-  }
-  // objects created but still empty (a linked empty map/list)
-  for (const [o, t] of objType) {
-    const uuid = state.enc.objList[o]
-    if (!view.has(uuid)) view.set(uuid, { type: TYPE_OF[t], keys: new Map(), elems: [] })
-  }
+  for (const [uuid, ov] of Object.entries(v)) view.set(uuid, { type: ov.type, keys: new Map(ov.keys), elems: ov.elems })
   return view
 }
 
-// the previous view advanced by the registers the round's ops hit (state.pendingRegs): the
-// same diffs diffViews would give for them — objects created, list removals (descending
-// index), insertions (ascending final index), then value changes
-function applyRegs(state) {
-  const view = state.view, diffs = [], sig = (e) => JSON.stringify(e)
-  for (const o of state.newObjs) {
-    const uuid = state.enc.objList[o]
-    if (view.has(uuid)) continue
-    const t = TYPE_OF[state.objType.get(o)]
-    view.set(uuid, { type: t, keys: new Map(), elems: [] })
-    if (uuid !== C.ROOT_ID) diffs.push({ action: 'create', obj: uuid, type: t })
-  }
-  const lists = new Map()
-  for (const r of state.pendingRegs) {
-    if (r.o === C.NONE) continue
-    const t = state.objType.has(r.o) ? state.objType.get(r.o) : 0
-    const list = t === 2 || t === 3
-    const uuid = state.enc.objList[r.o]
-    let ov = view.get(uuid)
-    if (!ov) { ov = { type: TYPE_OF[t], keys: new Map(), elems: [] }; view.set(uuid, ov) }
-    const key = state.enc.regList[r.g][1]
-    const entry = r.n ? entryOf(state, r.surv) : null
-    if (!list) {
-      const old = ov.keys.get(key)
-      if (!entry) {
-        if (old !== undefined) { ov.keys.delete(key); diffs.push({ action: 'remove', type: ov.type, obj: uuid, key }) }
-      } else if (old === undefined || sig(old) !== sig(entry)) {
-        ov.keys.set(key, entry)
-        diffs.push(Object.assign({ action: 'set', type: ov.type, obj: uuid, key }, entry))
-      }
-      continue
-    }
-    let L = lists.get(uuid)
-    if (!L) { L = { ov, rem: [], ins: [], set: [] }; lists.set(uuid, L) }
-    const visible = r.n > 0 && r.li >= 0
-    const oldIdx = ov.elems.findIndex((e) => e[0] === key)
-    if (oldIdx >= 0 && !visible) L.rem.push(oldIdx)
-    else if (oldIdx < 0 && visible) L.ins.push([r.li, key, entry])
-    else if (visible && sig(ov.elems[oldIdx][1]) !== sig(entry)) L.set.push([key, entry])
-  }
-  for (const [uuid, L] of lists) {
-    L.rem.sort((a, b) => b - a).forEach((i) => {
-      L.ov.elems.splice(i, 1)
-      diffs.push({ action: 'remove', type: L.ov.type, obj: uuid, index: i })
-    })
-    L.ins.sort((a, b) => a[0] - b[0]).forEach(([i, key, e]) => {
-      L.ov.elems.splice(i, 0, [key, e])
-      diffs.push(Object.assign({ action: 'insert', type: L.ov.type, obj: uuid, index: i, elemId: key }, e))
-    })
-    L.set.forEach(([key, e]) => {
-      const i = L.ov.elems.findIndex((x) => x[0] === key)
-      L.ov.elems[i] = [key, e]
-      diffs.push(Object.assign({ action: 'set', type: L.ov.type, obj: uuid, index: i }, e))
-    })
-  }
-  return diffs
-}
-
-function diffViews(prev, next) {
+// Backend.getPatch(state): the whole document as diffs from an empty one
+function fullPatch(state) {
   const diffs = []
-  const sig = (e) => JSON.stringify(e)
-  for (const [uuid, ov] of next) if (uuid !== C.ROOT_ID && !prev.has(uuid)) diffs.push({ action: 'create', obj: uuid, type: ov.type })
-  for (const [uuid, ov] of next) {
-    const po = prev.get(uuid) || { keys: new Map(), elems: [] }
-    if (ov.type === 'list' || ov.type === 'text') {
-      const keep = new Set(ov.elems.map(([id]) => id))
-      const was = new Map(po.elems.map(([id, e], i) => [id, [i, e]]))
-      for (let i = po.elems.length - 1; i >= 0; i--)
-        if (!keep.has(po.elems[i][0])) diffs.push({ action: 'remove', type: ov.type, obj: uuid, index: i })
-      ov.elems.forEach(([id, e], i) => {
-        if (!was.has(id)) diffs.push(Object.assign({ action: 'insert', type: ov.type, obj: uuid, index: i, elemId: id }, e))
-      })
-      ov.elems.forEach(([id, e], i) => {
-        if (was.has(id) && sig(was.get(id)[1]) !== sig(e)) diffs.push(Object.assign({ action: 'set', type: ov.type, obj: uuid, index: i }, e))
-      })
-    } else {
-      const keys = Array.from(new Set([...po.keys.keys(), ...ov.keys.keys()])).sort()
-      for (const k of keys) {
-        const a = po.keys.get(k), b = ov.keys.get(k)
-        if (b === undefined) diffs.push({ action: 'remove', type: ov.type, obj: uuid, key: k })
-        else if (a === undefined || sig(a) !== sig(b)) diffs.push(Object.assign({ action: 'set', type: ov.type, obj: uuid, key: k }, b))
-      }
-    }
+  for (const [uuid, ov] of materialize(state)) {
+    if (uuid !== '00000000-0000-0000-0000-000000000000') diffs.push({ action: 'create', obj: uuid, type: ov.type })
   }
-  return diffs
-}
-
-function makePatch(state) {
-  let diffs = []
-  if (state.engine.patches && state.patchedSeq !== state.roundSeq) {
-    if (state.view && state.pendingRegs && state.objType) {
-      diffs = applyRegs(state)
-      state.incrementalPatches = (state.incrementalPatches || 0) + 1
-    } else {
-      const view = materialize(state)
-      diffs = diffViews(state.view || new Map(), view)
-      state.view = view
-    }
-    state.patchedSeq = state.roundSeq
-    state.pendingRegs = null
+  for (const [uuid, ov] of materialize(state)) {
+    for (const [key, e] of ov.keys) diffs.push(Object.assign({ action: 'set', type: ov.type, obj: uuid, key }, e))
+    ov.elems.forEach(([elemId, e], index) => diffs.push(Object.assign({ action: 'insert', type: ov.type, obj: uuid, index, elemId }, e)))
   }
   return { clock: Object.assign({}, state.clock), deps: Object.assign({}, state.deps), canUndo: false, canRedo: false, diffs }
 }
+
+const emptyPatch = (state) => ({ clock: Object.assign({}, state.clock), deps: Object.assign({}, state.deps), canUndo: false,
+  canRedo: false, diffs: [] })
 
 function makeBackend(engine) {
   return {
     init: (docId) => engine.init(docId),
     applyChanges: (state, changes) => {
-      engine.applyChanges(state, changes)
-      return [state, makePatch(state)]
+      const r = engine.applyChanges(state, changes)
+      return [state, r ? r.patch : emptyPatch(state)]
     },
-    getPatch: (state) => makePatch(state),
+    getPatch: (state) => fullPatch(state),
   }
 }
 
@@ -677,7 +467,11 @@ class DocBackend {
     this.testMinimumClockSatisfied()
   }
 
+  // changes: Change objects (the reference's), or raw hypercore blocks / JSON texts of them
   applyRemoteChanges(changes) { this.remoteChangesQ.push(changes) }
+
+  // the blocks of an actor feed as downloaded (Actor.onDownload -> syncChanges without parseBlock)
+  applyRemoteBlocks(blocks) { this.remoteChangesQ.push(blocks) }
 
   applyLocalChange(change) { this.localChangeQ.push(change) }
 
@@ -688,27 +482,29 @@ class DocBackend {
     }
   }
 
-  updateClock(changes) {
-    changes.forEach((change) => {
-      const old = this.clock[change.actor] || 0
-      this.clock[change.actor] = Math.max(old, change.seq)
-    })
+  // DocBackend.updateClock (src/DocBackend.ts:135-142) from the max seq per actor of the
+  // handed changes (queued ones included), which the docset reports per round
+  updateClock(roundClock) {
+    for (const a in roundClock) {
+      const old = this.clock[a] || 0
+      this.clock[a] = Math.max(old, roundClock[a])
+    }
     if (!this.minimumClockSatisfied) this.testMinimumClockSatisfied()
   }
 
   init(changes, actorId) {
     const state = this.engine.init(this.id)
-    this.engine.enqueue(state, { changes, done: () => {
+    this.engine.enqueue(state, { entries: changes, done: (r) => {
       this.actorId = this.actorId || actorId
       this.back = state
-      this.updateClock(changes)
+      this.updateClock(r.roundClock)
       this.minimumClockSatisfied = changes.length > 0
-      const patch = makePatch(state)
+      const patch = r.patch
       this.ready.subscribe((f) => f())
       this.subscribeToLocalChanges()
       this.subscribeToRemoteChanges()
       // ReadyMsg after the buffered remote changes drained above (per-document FIFO)
-      this.engine.enqueue(state, { changes: null, done: () => {
+      this.engine.enqueue(state, { entries: null, done: () => {
         this.notify({ type: 'ReadyMsg', id: this.id, minimumClockSatisfied: this.minimumClockSatisfied,
           actorId: this.actorId, patch, history: this.back.histLen })
       } })
@@ -717,10 +513,10 @@ class DocBackend {
 
   subscribeToRemoteChanges() {
     this.remoteChangesQ.subscribe((changes) => {
-      this.engine.enqueue(this.back, { changes, done: () => {
-        this.updateClock(changes)
+      this.engine.enqueue(this.back, { entries: changes, done: (r) => {
+        this.updateClock(r.roundClock)
         this.notify({ type: 'RemotePatchMsg', id: this.id, minimumClockSatisfied: this.minimumClockSatisfied,
-          patch: makePatch(this.back), history: this.back.histLen })
+          patch: r.patch, history: this.back.histLen })
       } })
     })
   }
@@ -730,9 +526,9 @@ class DocBackend {
       // Backend.applyLocalChange: the change must extend its actor's sequence
       const cur = this.back.clock[change.actor] || 0
       if (change.seq <= cur) throw new Error(`Change request has already been applied: ${change.actor}:${change.seq}`)
-      this.engine.enqueue(this.back, { changes: [change], done: () => {
-        this.updateClock([change])
-        const patch = Object.assign(makePatch(this.back), { actor: change.actor, seq: change.seq })
+      this.engine.enqueue(this.back, { entries: [change], done: (r) => {
+        this.updateClock(r.roundClock)
+        const patch = Object.assign(r.patch, { actor: change.actor, seq: change.seq })
         this.notify({ type: 'LocalPatchMsg', id: this.id, actorId: this.actorId,
           minimumClockSatisfied: this.minimumClockSatisfied, change, patch, history: this.back.histLen })
       } })
@@ -789,32 +585,29 @@ class ClockStore {
 
   getAllRepoIds() { return Array.from(new Set(Array.from(this.rows.keys()).map((k) => k.split('\u0000')[0]))) }
 
-  // ClockStore.update(repoId, doc.id, doc.clock) for many GPU documents at once
+  // ClockStore.update(repoId, doc.id, doc.back's clock) for many GPU documents at once
   // (src/RepoBackend.ts:343-345): the device upsert-max decides which rows change
-  // (written) and which inputs differ from the stored clock (updateQ).
+  // (written) and which inputs differ from the stored clock (updateQ).  Not while an async
+  // round is in flight on the documents' device (the docset refuses the call).
   updateDocs(repoId, docs) {
     if (!docs.length) return []
-    // one device upsert-max per store holding some of the documents
-    const byStore = new Map()
+    const byDs = new Map()
     docs.forEach((doc, i) => {
-      const st = doc.back.store
-      if (!byStore.has(st)) byStore.set(st, [])
-      byStore.get(st).push(i)
+      const ds = doc.back.ds
+      if (!byDs.has(ds)) byDs.set(ds, [])
+      byDs.get(ds).push(i)
     })
     const out = new Array(docs.length)
-    for (const [store, idx] of byStore) {
-      const handles = Uint32Array.from(idx.map((i) => docs[i].back.handle))
-      const r = addon.clockUpdate(store, handles)
-      const S = docs[idx[0]].back.stride
+    for (const [ds, idx] of byDs) {
+      const r = addon.docsetClockUpdate(ds, Uint32Array.from(idx, (i) => docs[i].back.id))
+      const stored = JSON.parse(r.json)
       idx.forEach((i, j) => {
         const doc = docs[i]
-        const actors = doc.back.enc.actors
         const k = this.key(repoId, doc.id)
         if (r.written[j]) {
-          const stored = Clock.fromRow(r.stored, j * S * 4, actors)
           let m = this.rows.get(k)
           if (!m) { m = new Map(); this.rows.set(k, m) }
-          for (const [a, s] of Object.entries(stored)) if (!m.has(a) || s > m.get(a)) m.set(a, s)
+          for (const [a, s] of Object.entries(stored[j])) if (!m.has(a) || s > m.get(a)) m.set(a, s)
         }
         const d = [repoId, doc.id, this.get(repoId, doc.id)]
         if (r.differs[j]) this.updateQ.push(d)
@@ -825,7 +618,140 @@ class ClockStore {
   }
 }
 
-// SQLite's BINARY collation (memcmp of UTF-8) orders the Clocks primary key
+// SQLite's BINARY collation (memcmp of UTF-8) orders the Clocks / Cursors primary keys
 function byteOrder(a, b) { return Buffer.compare(Buffer.from(a, 'utf8'), Buffer.from(b, 'utf8')) }
 
-module.exports = { GpuEngine, GpuBackendState, DocBackend, ClockStore, makeBackend, materialize, fnv1a64, addon }
+// CursorStore (src/CursorStore.ts:19-91) on the device: one table per repo, documents as dense
+// rows, actors as FNV-1a64 keys (the clock exchange's); every batched form is one launch.
+const INFINITY_SEQ = Number.MAX_SAFE_INTEGER
+class CursorStore {
+  constructor(engine, maxActorsPerDoc) {
+    this.engine = engine
+    this.K = maxActorsPerDoc || 64
+    this.tables = new Map()          // repoId -> {c, rows: Map(docId -> row), docs: []}
+    this.actors = new Map()          // key -> actorId
+    this.updateQ = new Channel('cursorstore:updateQ')
+  }
+
+  table(repoId) {
+    let t = this.tables.get(repoId)
+    if (!t) { t = { c: addon.cursorsCreate(this.engine.docsets[0], this.K), rows: new Map(), docs: [] }; this.tables.set(repoId, t) }
+    return t
+  }
+
+  row(t, docId) {
+    let r = t.rows.get(docId)
+    if (r === undefined) { r = t.docs.length; t.rows.set(docId, r); t.docs.push(docId); addon.cursorsReserve(t.c, t.docs.length) }
+    return r
+  }
+
+  key(actorId) { const k = fnv1a64(actorId); this.actors.set(k, actorId); return k }
+
+  getMany(repoId, docIds) {
+    const t = this.table(repoId)
+    const have = docIds.filter((d) => t.rows.has(d))
+    const out = new Map()
+    if (have.length) {
+      const g = addon.cursorsGet(t.c, Uint32Array.from(have, (d) => t.rows.get(d)))
+      have.forEach((d, i) => {
+        const n = g.count.readUInt32LE(4 * i)
+        const ent = []
+        for (let e = 0; e < n; e++) {
+          const o = 8 * (i * this.K + e)
+          ent.push([this.actors.get(g.actors.readBigUInt64LE(o)), Number(g.seqs.readBigUInt64LE(o))])
+        }
+        ent.sort((a, b) => byteOrder(a[0], b[0]))            // SELECT * in primary-key order
+        out.set(d, Object.fromEntries(ent))
+      })
+    }
+    return docIds.map((d) => out.get(d) || {})
+  }
+
+  get(repoId, docId) { return this.getMany(repoId, [docId])[0] }
+
+  // CursorStore.update for many documents in one launch: {docId: cursor} -> descriptors
+  updateMany(repoId, cursors) {
+    const t = this.table(repoId)
+    const docs = Object.keys(cursors)
+    const off = new Uint32Array(docs.length + 1)
+    const keys = [], seqs = []
+    docs.forEach((d, i) => {
+      for (const [a, s] of Object.entries(cursors[d])) { keys.push(this.key(a)); seqs.push(s) }
+      off[i + 1] = keys.length
+    })
+    const rows = Uint32Array.from(docs, (d) => this.row(t, d))
+    const differs = addon.cursorsUpdate(t.c, rows, off, BigUint64Array.from(keys), Float64Array.from(seqs))
+    const stored = this.getMany(repoId, docs)
+    return docs.map((d, i) => {
+      const desc = [stored[i], d, repoId]
+      if (differs[i]) this.updateQ.push(desc)
+      return desc
+    })
+  }
+
+  update(repoId, docId, cursor) { return this.updateMany(repoId, { [docId]: cursor })[0] }
+
+  addActor(repoId, docId, actorId, seq) {
+    const s = seq === undefined ? INFINITY_SEQ : Math.max(0, Math.min(seq, INFINITY_SEQ))
+    return this.update(repoId, docId, { [actorId]: s })
+  }
+
+  // CursorStore.entry for many (docId, actorId) pairs in one launch
+  entries(repoId, pairs) {
+    const t = this.table(repoId)
+    const idx = pairs.map(([d], i) => (t.rows.has(d) ? i : -1)).filter((i) => i >= 0)
+    const out = new Array(pairs.length).fill(0)
+    if (idx.length) {
+      const got = addon.cursorsEntry(t.c, Uint32Array.from(idx, (i) => t.rows.get(pairs[i][0])),
+        BigUint64Array.from(idx, (i) => this.key(pairs[i][1])))
+      idx.forEach((i, j) => { out[i] = Number(got.readBigUInt64LE(8 * j)) })
+    }
+    return out
+  }
+
+  entry(repoId, docId, actorId) { return this.entries(repoId, [[docId, actorId]])[0] }
+
+  // docsWithActor for many actors in one launch: [[docId, actorId, storedSeq]]
+  docsWithActors(repoId, actorSeqs) {
+    const t = this.table(repoId)
+    const names = Object.keys(actorSeqs)
+    if (!names.length || !t.docs.length) return []
+    const r = addon.cursorsDocsWithActors(t.c, BigUint64Array.from(names, (a) => this.key(a)), Float64Array.from(names, (a) => actorSeqs[a]))
+    const out = []
+    for (let i = 0; i < r.rows.length / 4; i++)
+      out.push([t.docs[r.rows.readUInt32LE(4 * i)], names[r.actors.readUInt32LE(4 * i)], Number(r.seqs.readBigUInt64LE(8 * i))])
+    return out
+  }
+
+  docsWithActor(repoId, actorId, seq) {
+    return this.docsWithActors(repoId, { [actorId]: seq || 0 }).map((x) => x[0]).sort(byteOrder)
+  }
+}
+
+// RepoBackend.syncChanges (src/RepoBackend.ts:506-531) for many synced actors at once: for
+// every open document whose cursor has the actor, the block range [min, end) it receives:
+// min = doc.changes.get(actor) || 0, end = the first block missing from the actor's feed
+// (present[actor]: downloaded flags) at or after min, below the cursor entry.  One
+// docsWithActor launch and one contiguity launch; the caller sets doc.changes[actor] = end and
+// hands the blocks [min, end) to applyRemoteChanges / applyRemoteBlocks when end > min.
+function syncPlan(engine, cursors, repoId, actors, docs, present) {
+  const hits = cursors.docsWithActors(repoId, Object.fromEntries(actors.map((a) => [a, 0]))).filter(([d]) => docs.has(d))
+  if (!hits.length) return []
+  const feeds = Array.from(new Set(hits.map((h) => h[1])))
+  const fidx = new Map(feeds.map((a, i) => [a, i]))
+  const wordOff = new BigUint64Array(feeds.length + 1)
+  feeds.forEach((a, i) => { wordOff[i + 1] = wordOff[i] + BigInt(Math.ceil(present[a].length / 64)) })
+  const words = new BigUint64Array(Number(wordOff[feeds.length]) + 1)
+  feeds.forEach((a, i) => {
+    const f = present[a], base = Number(wordOff[i])
+    for (let j = 0; j < f.length; j++) if (f[j]) words[base + (j >> 6)] |= 1n << BigInt(j & 63)
+  })
+  const lo = Uint32Array.from(hits, ([d, a]) => docs.get(d).changes.get(a) || 0)
+  const hi = Uint32Array.from(hits, ([, a, s], i) => Math.max(Math.min(s, present[a].length, 0xffffffff), lo[i]))
+  const off = BigUint64Array.from(hits, ([, a]) => wordOff[fidx.get(a)])
+  const end = addon.syncRanges(engine.docsets[0], words, off, lo, hi)
+  return hits.map(([d, a], i) => [d, a, lo[i], end.readUInt32LE(4 * i)]).sort((x, y) => byteOrder(x[0] + '\0' + x[1], y[0] + '\0' + y[1]))
+}
+
+module.exports = { GpuEngine, GpuBackendState, DocBackend, ClockStore, CursorStore, syncPlan, makeBackend, materialize,
+  fnv1a64, addon, toChange }

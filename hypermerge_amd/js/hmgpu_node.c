@@ -61,6 +61,7 @@ typedef struct {
     pthread_cond_t cv;
     Job *head, *tail;
     int started, stop;
+    int busy;             /* a waitAsync job is in flight: every other call on the store throws */
 } Store;
 
 static void *store_thread(void *arg) {
@@ -110,13 +111,24 @@ static int get_args(napi_env env, napi_callback_info info, size_t want, napi_val
     return 1;
 }
 
-static Store *get_store(napi_env env, napi_value v) {
+static Store *get_store_any(napi_env env, napi_value v) {
     void *p = NULL;
     if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
         napi_throw_type_error(env, NULL, "expected a store handle");
         return NULL;
     }
     return (Store *)p;
+}
+
+/* the store for a call that touches its state: refused while an async wait runs on its host
+ * thread (hm_batch_wait copies out and rolls back documents there) */
+static Store *get_store(napi_env env, napi_value v) {
+    Store *s = get_store_any(env, v);
+    if (s && s->busy) {
+        napi_throw_error(env, NULL, "store busy: a batch is in flight (wait for its waitAsync callback)");
+        return NULL;
+    }
+    return s;
 }
 
 /* bytes of a Buffer / TypedArray / ArrayBuffer view; null/undefined -> NULL */
@@ -255,8 +267,8 @@ static napi_value result_object(napi_env env, const uint8_t *buf, uint32_t n, ui
 
 /* main thread: callback(err, result) for a finished job */
 static void job_call_js(napi_env env, napi_value cb, void *context, void *data) {
-    (void)context;
     Job *j = (Job *)data;
+    if (context) ((Store *)context)->busy = 0;
     if (env && cb) {
         napi_value argv[2], undef, ret;
         napi_get_undefined(env, &undef);
@@ -289,7 +301,7 @@ static napi_value WaitAsync(napi_env env, napi_callback_info info) {
     j->id = (uint64_t)idd; j->n = s->pending_n; j->S = s->a_stride;
     napi_value name;
     napi_create_string_utf8(env, "hmgpu.waitAsync", NAPI_AUTO_LENGTH, &name);
-    if (napi_create_threadsafe_function(env, argv[2], NULL, name, 0, 1, NULL, NULL, NULL, job_call_js, &j->tsfn) != napi_ok) {
+    if (napi_create_threadsafe_function(env, argv[2], NULL, name, 0, 1, NULL, NULL, s, job_call_js, &j->tsfn) != napi_ok) {
         free(j);
         napi_throw_error(env, NULL, "napi_create_threadsafe_function failed");
         return NULL;
@@ -305,6 +317,7 @@ static napi_value WaitAsync(napi_env env, napi_callback_info info) {
         }
         s->started = 1;
     }
+    s->busy = 1;
     pthread_mutex_lock(&s->mu);
     if (s->tail) s->tail->next = j; else s->head = j;
     s->tail = j;
@@ -536,6 +549,552 @@ static napi_value StatusMessage(napi_env env, napi_callback_info info) {
     return out;
 }
 
+/* ---------------- docset: raw blocks in, results + patches out (hm_docset_*) ---------------- */
+typedef struct DsJob {
+    struct DsJob *next;
+    uint8_t *data;
+    uint64_t *bo;
+    uint32_t *db, *ids, n;
+    int st;
+    char err[512];
+    hm_text *out;
+    napi_threadsafe_function tsfn;
+} DsJob;
+
+typedef struct {
+    hm_engine *engine;
+    hm_docset *ds;
+    pthread_t thread;
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    DsJob *head, *tail;
+    int started, stop, busy;
+} Docset;
+
+static void ds_job_free(DsJob *j) {
+    if (!j) return;
+    free(j->data); free(j->bo); free(j->db); free(j->ids);
+    if (j->out) hm_text_free(j->out);
+    free(j);
+}
+
+static void *docset_thread(void *arg) {
+    Docset *d = (Docset *)arg;
+    for (;;) {
+        pthread_mutex_lock(&d->mu);
+        while (!d->head && !d->stop) pthread_cond_wait(&d->cv, &d->mu);
+        if (!d->head) { pthread_mutex_unlock(&d->mu); return NULL; }
+        DsJob *j = d->head;
+        d->head = j->next;
+        if (!d->head) d->tail = NULL;
+        pthread_mutex_unlock(&d->mu);
+        j->st = hm_docset_apply(d->ds, j->data, j->bo, j->db, j->ids, j->n, &j->out);
+        if (j->st) snprintf(j->err, sizeof j->err, "hm_docset_apply: %s — %s", hm_status_message(j->st), hm_engine_last_error(d->engine));
+        napi_call_threadsafe_function(j->tsfn, j, napi_tsfn_blocking);
+        napi_release_threadsafe_function(j->tsfn, napi_tsfn_release);
+    }
+}
+
+static void docset_finalize(napi_env env, void *data, void *hint) {
+    (void)env; (void)hint;
+    Docset *d = (Docset *)data;
+    if (d->started) {
+        pthread_mutex_lock(&d->mu);
+        d->stop = 1;
+        pthread_cond_signal(&d->cv);
+        pthread_mutex_unlock(&d->mu);
+        pthread_join(d->thread, NULL);
+        pthread_mutex_destroy(&d->mu);
+        pthread_cond_destroy(&d->cv);
+    }
+    if (d->ds) hm_docset_destroy(d->ds);
+    if (d->engine) hm_engine_destroy(d->engine);
+    free(d);
+}
+
+static Docset *get_docset_any(napi_env env, napi_value v) {
+    void *p = NULL;
+    if (napi_get_value_external(env, v, &p) != napi_ok || !p) { napi_throw_type_error(env, NULL, "expected a docset handle"); return NULL; }
+    return (Docset *)p;
+}
+
+static Docset *get_docset(napi_env env, napi_value v) {
+    Docset *d = get_docset_any(env, v);
+    if (d && d->busy) { napi_throw_error(env, NULL, "docset busy: an applyAsync round is in flight"); return NULL; }
+    return d;
+}
+
+/* docsetCreate(device, threads, patches) -> docset */
+static napi_value DocsetCreate(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return NULL;
+    Docset *d = (Docset *)calloc(1, sizeof(Docset));
+    hm_config cfg = {(int)get_u32(env, argv[0]), 0};
+    int st = hm_engine_create(&cfg, &d->engine);
+    if (st) { free(d); return throw_status(env, NULL, st, "hm_engine_create"); }
+    bool patches = true;
+    napi_get_value_bool(env, argv[2], &patches);
+    hm_docset_config dc = {get_u32(env, argv[1]), patches ? 0u : HM_DOCSET_NO_PATCHES};
+    st = hm_docset_create(d->engine, &dc, &d->ds);
+    if (st) { napi_value r = throw_status(env, d->engine, st, "hm_docset_create"); hm_engine_destroy(d->engine); free(d); return r; }
+    napi_value out;
+    CHECK_NAPI(napi_create_external(env, d, docset_finalize, NULL, &out));
+    return out;
+}
+
+/* docsetOpen(docset, n) -> first document id (allowed while a round is in flight) */
+static napi_value DocsetOpen(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return NULL;
+    Docset *d = get_docset_any(env, argv[0]);
+    if (!d) return NULL;
+    uint32_t first = 0;
+    int st = hm_docset_open(d->ds, get_u32(env, argv[1]), &first);
+    if (st) return throw_status(env, d->engine, st, "hm_docset_open");
+    return u32v(env, first);
+}
+
+/* the blocks of every document of a call (Array of Arrays of Buffer | string) -> one
+ * contiguous copy + offsets owned by the job (the JS values need not outlive the call) */
+static int gather_blocks(napi_env env, napi_value ids_v, napi_value blocks_v, DsJob *j) {
+    void *ip; size_t il;
+    if (!get_bytes(env, ids_v, &ip, &il)) return 0;
+    uint32_t n = (uint32_t)(il / 4), nd = 0;
+    if (napi_get_array_length(env, blocks_v, &nd) != napi_ok || nd != n) {
+        napi_throw_range_error(env, NULL, "blocks must be an array with one array of blocks per document");
+        return 0;
+    }
+    j->n = n;
+    j->ids = (uint32_t *)malloc((size_t)n * 4 + 4);
+    j->db = (uint32_t *)malloc(((size_t)n + 1) * 4);
+    memcpy(j->ids, ip, (size_t)n * 4);
+    size_t cap_b = 1024, nb = 0, cap = 1 << 16, used = 0;
+    j->bo = (uint64_t *)malloc(cap_b * 8);
+    j->data = (uint8_t *)malloc(cap);
+    j->bo[0] = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        j->db[i] = (uint32_t)nb;
+        napi_value arr;
+        uint32_t k = 0;
+        if (napi_get_element(env, blocks_v, i, &arr) != napi_ok || napi_get_array_length(env, arr, &k) != napi_ok) {
+            napi_throw_type_error(env, NULL, "each document's blocks must be an array");
+            return 0;
+        }
+        for (uint32_t b = 0; b < k; b++) {
+            napi_value v;
+            napi_get_element(env, arr, b, &v);
+            napi_valuetype t;
+            napi_typeof(env, v, &t);
+            size_t len = 0;
+            void *src = NULL;
+            if (t == napi_string) napi_get_value_string_utf8(env, v, NULL, 0, &len);
+            else if (!get_bytes(env, v, &src, &len)) return 0;
+            if (used + len + 1 > cap) {
+                while (used + len + 1 > cap) cap *= 2;
+                j->data = (uint8_t *)realloc(j->data, cap);
+            }
+            if (t == napi_string) { size_t w = 0; napi_get_value_string_utf8(env, v, (char *)j->data + used, len + 1, &w); len = w; }
+            else if (len) memcpy(j->data + used, src, len);
+            used += len;
+            if (nb + 2 > cap_b) { cap_b *= 2; j->bo = (uint64_t *)realloc(j->bo, cap_b * 8); }
+            j->bo[++nb] = used;
+        }
+    }
+    j->db[n] = (uint32_t)nb;
+    return 1;
+}
+
+static napi_value text_object(napi_env env, hm_text *t) {
+    size_t len = 0;
+    const char *p = hm_text_data(t, &len);
+    uint32_t n = 0;
+    const hm_doc_result *r = hm_text_results(t, &n);
+    napi_value o, js;
+    napi_create_object(env, &o);
+    set(env, o, "results", buf_copy(env, r, (size_t)n * sizeof(hm_doc_result)));
+    napi_create_string_utf8(env, p, len, &js);
+    set(env, o, "json", js);
+    return o;
+}
+
+static void ds_call_js(napi_env env, napi_value cb, void *context, void *data) {
+    DsJob *j = (DsJob *)data;
+    if (context) ((Docset *)context)->busy = 0;
+    if (env && cb) {
+        napi_value argv[2], undef, ret;
+        napi_get_undefined(env, &undef);
+        if (j->st) {
+            napi_value msg;
+            napi_create_string_utf8(env, j->err, NAPI_AUTO_LENGTH, &msg);
+            napi_create_error(env, NULL, msg, &argv[0]);
+            argv[1] = undef;
+        } else {
+            napi_get_null(env, &argv[0]);
+            argv[1] = text_object(env, j->out);
+        }
+        napi_call_function(env, undef, cb, 2, argv, &ret);
+    }
+    ds_job_free(j);
+}
+
+/* docsetApply(docset, ids Uint32Array, blocks[][], callback?) -> {results, json} | undefined:
+ * one applyChanges round of every listed document (hm_docset_apply); with a callback the
+ * round runs on the docset's host thread and callback(err, {results, json}) runs on the main
+ * thread when it is done (no other docset call until then, except docsetOpen) */
+static napi_value DocsetApply(napi_env env, napi_callback_info info) {
+    napi_value argv[4];
+    size_t argc = 4;
+    if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < 3) {
+        napi_throw_type_error(env, NULL, "missing arguments");
+        return NULL;
+    }
+    Docset *d = get_docset(env, argv[0]);
+    if (!d) return NULL;
+    DsJob *j = (DsJob *)calloc(1, sizeof(DsJob));
+    if (!gather_blocks(env, argv[1], argv[2], j)) { ds_job_free(j); return NULL; }
+    napi_valuetype cbt = napi_undefined;
+    if (argc >= 4) napi_typeof(env, argv[3], &cbt);
+    if (cbt != napi_function) {
+        int st = hm_docset_apply(d->ds, j->data, j->bo, j->db, j->ids, j->n, &j->out);
+        if (st) { ds_job_free(j); return throw_status(env, d->engine, st, "hm_docset_apply"); }
+        napi_value o = text_object(env, j->out);
+        ds_job_free(j);
+        return o;
+    }
+    napi_value name;
+    napi_create_string_utf8(env, "hmgpu.docsetApply", NAPI_AUTO_LENGTH, &name);
+    if (napi_create_threadsafe_function(env, argv[3], NULL, name, 0, 1, NULL, NULL, d, ds_call_js, &j->tsfn) != napi_ok) {
+        ds_job_free(j);
+        napi_throw_error(env, NULL, "napi_create_threadsafe_function failed");
+        return NULL;
+    }
+    if (!d->started) {
+        pthread_mutex_init(&d->mu, NULL);
+        pthread_cond_init(&d->cv, NULL);
+        if (pthread_create(&d->thread, NULL, docset_thread, d) != 0) {
+            napi_release_threadsafe_function(j->tsfn, napi_tsfn_abort);
+            ds_job_free(j);
+            napi_throw_error(env, NULL, "pthread_create failed");
+            return NULL;
+        }
+        d->started = 1;
+    }
+    d->busy = 1;
+    pthread_mutex_lock(&d->mu);
+    if (d->tail) d->tail->next = j; else d->head = j;
+    d->tail = j;
+    pthread_cond_signal(&d->cv);
+    pthread_mutex_unlock(&d->mu);
+    return NULL;
+}
+
+/* docsetHistoryPrefix(docset, doc, n) -> Buffer of u32 log indices (history order) */
+static napi_value DocsetHistoryPrefix(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return NULL;
+    Docset *d = get_docset(env, argv[0]);
+    if (!d) return NULL;
+    const uint32_t n = get_u32(env, argv[2]);
+    uint32_t *out = (uint32_t *)malloc((size_t)n * 4 + 4);
+    int k = hm_docset_history_prefix(d->ds, get_u32(env, argv[1]), n, out);
+    if (k < 0) { free(out); return throw_status(env, d->engine, -k, "hm_docset_history_prefix"); }
+    napi_value r = buf_copy(env, out, (size_t)k * 4);
+    free(out);
+    return r;
+}
+
+/* docsetClockUpdate(docset, ids Uint32Array) -> {written, differs, json} */
+static napi_value DocsetClockUpdate(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return NULL;
+    Docset *d = get_docset(env, argv[0]);
+    if (!d) return NULL;
+    void *p; size_t n;
+    if (!get_bytes(env, argv[1], &p, &n)) return NULL;
+    const uint32_t k = (uint32_t)(n / 4);
+    uint8_t *w = (uint8_t *)calloc(1, k + 8), *df = (uint8_t *)calloc(1, k + 8);
+    hm_text *t = NULL;
+    int st = hm_docset_clock_update(d->ds, k, (const uint32_t *)p, w, df, &t);
+    napi_value o = NULL;
+    if (!st) {
+        size_t len = 0;
+        const char *s = hm_text_data(t, &len);
+        napi_value js;
+        napi_create_object(env, &o);
+        set(env, o, "written", buf_copy(env, w, k));
+        set(env, o, "differs", buf_copy(env, df, k));
+        napi_create_string_utf8(env, s, len, &js);
+        set(env, o, "json", js);
+    }
+    free(w); free(df);
+    if (t) hm_text_free(t);
+    if (st) return throw_status(env, d->engine, st, "hm_docset_clock_update");
+    return o;
+}
+
+/* docsetView(docset, doc) -> JSON text of the merged document */
+static napi_value DocsetView(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return NULL;
+    Docset *d = get_docset(env, argv[0]);
+    if (!d) return NULL;
+    hm_text *t = NULL;
+    int st = hm_docset_view(d->ds, get_u32(env, argv[1]), &t);
+    if (st) return throw_status(env, d->engine, st, "hm_docset_view");
+    size_t len = 0;
+    const char *s = hm_text_data(t, &len);
+    napi_value js;
+    napi_create_string_utf8(env, s, len, &js);
+    hm_text_free(t);
+    return js;
+}
+
+/* docsetInfo(docset, doc) -> {aStride, nChanges, nOps, nActors, nObjs, nRegs, histLen, nQueued} */
+static napi_value DocsetInfo(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return NULL;
+    Docset *d = get_docset(env, argv[0]);
+    if (!d) return NULL;
+    hm_docset_doc_info_t x;
+    int st = hm_docset_doc_info(d->ds, get_u32(env, argv[1]), &x);
+    if (st) return throw_status(env, d->engine, st, "hm_docset_doc_info");
+    napi_value o;
+    napi_create_object(env, &o);
+    set(env, o, "aStride", u32v(env, x.a_stride)); set(env, o, "nChanges", u32v(env, x.n_changes));
+    set(env, o, "nOps", u32v(env, x.n_ops)); set(env, o, "nActors", u32v(env, x.n_actors));
+    set(env, o, "nObjs", u32v(env, x.n_objs)); set(env, o, "nRegs", u32v(env, x.n_regs));
+    set(env, o, "histLen", u32v(env, x.hist_len)); set(env, o, "nQueued", u32v(env, x.n_queued));
+    return o;
+}
+
+/* docsetStats(docset) -> {calls, docs, moves, hitPatches, fullPatches} */
+static napi_value DocsetStats(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return NULL;
+    Docset *d = get_docset_any(env, argv[0]);
+    if (!d) return NULL;
+    uint64_t x[8];
+    hm_docset_stats(d->ds, x);
+    napi_value o;
+    napi_create_object(env, &o);
+    const char *names[5] = {"calls", "docs", "moves", "hitPatches", "fullPatches"};
+    for (int i = 0; i < 5; i++) { napi_value v; napi_create_double(env, (double)x[i], &v); set(env, o, names[i], v); }
+    return o;
+}
+
+/* commCreateLocalDocsets([docset per device]) -> comm: one rank per docset's engine (distinct GPUs) */
+static napi_value CommCreateLocalDocsets(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return NULL;
+    uint32_t n = 0;
+    if (napi_get_array_length(env, argv[0], &n) != napi_ok || n < 1 || n > 64) {
+        napi_throw_range_error(env, NULL, "expected 1..64 docsets");
+        return NULL;
+    }
+    hm_engine *engines[64];
+    for (uint32_t i = 0; i < n; i++) {
+        napi_value v;
+        CHECK_NAPI(napi_get_element(env, argv[0], i, &v));
+        Docset *d = get_docset(env, v);
+        if (!d) return NULL;
+        engines[i] = d->engine;
+    }
+    Comms *c = (Comms *)calloc(1, sizeof(Comms));
+    c->n = (int)n;
+    int st = hm_comm_create_local(engines, (int)n, c->comms);
+    if (st) { free(c); return throw_status(env, engines[0], st, "hm_comm_create_local"); }
+    napi_value out;
+    CHECK_NAPI(napi_create_external(env, c, comms_finalize, NULL, &out));
+    return out;
+}
+
+/* ---------------- CursorStore on the device (hm_cursors_*) and the syncChanges plan ---------------- */
+typedef struct { hm_cursors *c; hm_engine *e; uint32_t K; } Cursors;
+
+static void cursors_finalize(napi_env env, void *data, void *hint) {
+    (void)env; (void)hint;
+    Cursors *c = (Cursors *)data;
+    if (c->c) hm_cursors_destroy(c->c);
+    free(c);
+}
+
+static Cursors *get_cursors(napi_env env, napi_value v) {
+    void *p = NULL;
+    if (napi_get_value_external(env, v, &p) != napi_ok || !p) { napi_throw_type_error(env, NULL, "expected a cursors handle"); return NULL; }
+    return (Cursors *)p;
+}
+
+/* cursorsCreate(docset, maxActorsPerDoc) -> cursors (one repo's Cursors table on the docset's device).
+ * The table must not outlive its docset. */
+static napi_value CursorsCreate(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return NULL;
+    Docset *d = get_docset(env, argv[0]);
+    if (!d) return NULL;
+    Cursors *c = (Cursors *)calloc(1, sizeof(Cursors));
+    c->e = d->engine; c->K = get_u32(env, argv[1]);
+    int st = hm_cursors_create(c->e, c->K, &c->c);
+    if (st) { free(c); return throw_status(env, d->engine, st, "hm_cursors_create"); }
+    napi_value out;
+    CHECK_NAPI(napi_create_external(env, c, cursors_finalize, NULL, &out));
+    return out;
+}
+
+static napi_value CursorsReserve(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return NULL;
+    Cursors *c = get_cursors(env, argv[0]);
+    if (!c) return NULL;
+    int st = hm_cursors_reserve(c->c, get_u32(env, argv[1]));
+    if (st) return throw_status(env, c->e, st, "hm_cursors_reserve");
+    return NULL;
+}
+
+/* cursorsUpdate(c, rows u32[n], entryOff u32[n+1], actorKeys u64[], seqs f64[]) -> Buffer differs[n] */
+static napi_value CursorsUpdate(napi_env env, napi_callback_info info) {
+    napi_value argv[5];
+    if (!get_args(env, info, 5, argv)) return NULL;
+    Cursors *c = get_cursors(env, argv[0]);
+    if (!c) return NULL;
+    void *p[4]; size_t n[4];
+    for (int i = 0; i < 4; i++) if (!get_bytes(env, argv[1 + i], &p[i], &n[i])) return NULL;
+    const uint32_t nd = (uint32_t)(n[0] / 4);
+    if (n[1] / 4 != (size_t)nd + 1 || n[2] / 8 != n[3] / 8 || (nd && ((uint32_t *)p[1])[nd] != n[2] / 8)) {
+        napi_throw_range_error(env, NULL, "cursorsUpdate: rows / entryOff / keys / seqs disagree");
+        return NULL;
+    }
+    uint8_t *df = (uint8_t *)calloc(1, nd + 8);
+    int st = hm_cursors_update(c->c, nd, (const uint32_t *)p[0], (const uint32_t *)p[1], (const uint64_t *)p[2],
+                               (const double *)p[3], df);
+    napi_value r = st ? NULL : buf_copy(env, df, nd);
+    free(df);
+    if (st) return throw_status(env, c->e, st, "hm_cursors_update");
+    return r;
+}
+
+/* cursorsGet(c, rows u32[n]) -> {count: u32[n], actors: u64[n*K], seqs: u64[n*K]} */
+static napi_value CursorsGet(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return NULL;
+    Cursors *c = get_cursors(env, argv[0]);
+    if (!c) return NULL;
+    void *p; size_t n;
+    if (!get_bytes(env, argv[1], &p, &n)) return NULL;
+    const uint32_t k = (uint32_t)(n / 4);
+    uint32_t *cnt = (uint32_t *)calloc(1, (size_t)k * 4 + 4);
+    uint64_t *ak = (uint64_t *)calloc(1, (size_t)k * c->K * 8 + 8), *sq = (uint64_t *)calloc(1, (size_t)k * c->K * 8 + 8);
+    int st = hm_cursors_get(c->c, k, (const uint32_t *)p, cnt, ak, sq);
+    napi_value o = NULL;
+    if (!st) {
+        napi_create_object(env, &o);
+        set(env, o, "count", buf_copy(env, cnt, (size_t)k * 4));
+        set(env, o, "actors", buf_copy(env, ak, (size_t)k * c->K * 8));
+        set(env, o, "seqs", buf_copy(env, sq, (size_t)k * c->K * 8));
+    }
+    free(cnt); free(ak); free(sq);
+    if (st) return throw_status(env, c->e, st, "hm_cursors_get");
+    return o;
+}
+
+/* cursorsEntry(c, rows u32[n], actorKeys u64[n]) -> Buffer u64[n] (CursorStore.entry) */
+static napi_value CursorsEntry(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return NULL;
+    Cursors *c = get_cursors(env, argv[0]);
+    if (!c) return NULL;
+    void *pr, *pk; size_t nr, nk;
+    if (!get_bytes(env, argv[1], &pr, &nr) || !get_bytes(env, argv[2], &pk, &nk)) return NULL;
+    const uint32_t k = (uint32_t)(nr / 4);
+    if (nk / 8 != k) { napi_throw_range_error(env, NULL, "rows and keys differ in length"); return NULL; }
+    uint64_t *out = (uint64_t *)calloc(1, (size_t)k * 8 + 8);
+    int st = hm_cursors_entry(c->c, k, (const uint32_t *)pr, (const uint64_t *)pk, out);
+    napi_value r = st ? NULL : buf_copy(env, out, (size_t)k * 8);
+    free(out);
+    if (st) return throw_status(env, c->e, st, "hm_cursors_entry");
+    return r;
+}
+
+/* cursorsDocsWithActors(c, actorKeys u64[q], minSeqs f64[q]|null) -> {rows u32[], actors u32[], seqs u64[]} */
+static napi_value CursorsDocsWithActors(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return NULL;
+    Cursors *c = get_cursors(env, argv[0]);
+    if (!c) return NULL;
+    void *pk, *pm; size_t nk, nm;
+    if (!get_bytes(env, argv[1], &pk, &nk) || !get_bytes(env, argv[2], &pm, &nm)) return NULL;
+    const uint32_t q = (uint32_t)(nk / 8);
+    if (pm && nm / 8 != q) { napi_throw_range_error(env, NULL, "keys and minSeqs differ in length"); return NULL; }
+    uint32_t cap = 1024, got = 0;
+    for (;;) {
+        uint32_t *rows = (uint32_t *)malloc((size_t)cap * 4), *act = (uint32_t *)malloc((size_t)cap * 4);
+        uint64_t *seq = (uint64_t *)malloc((size_t)cap * 8);
+        int st = hm_cursors_docs_with_actors(c->c, q, (const uint64_t *)pk, (const double *)pm, cap, rows, act, seq, &got);
+        if (st == HM_ERR_NOMEM && got > cap) { free(rows); free(act); free(seq); cap = got; continue; }
+        napi_value o = NULL;
+        if (!st) {
+            napi_create_object(env, &o);
+            set(env, o, "rows", buf_copy(env, rows, (size_t)got * 4));
+            set(env, o, "actors", buf_copy(env, act, (size_t)got * 4));
+            set(env, o, "seqs", buf_copy(env, seq, (size_t)got * 8));
+        }
+        free(rows); free(act); free(seq);
+        if (st) return throw_status(env, c->e, st, "hm_cursors_docs_with_actors");
+        return o;
+    }
+}
+
+/* syncRanges(docset, present u64 words, wordOff u64[n], lo u32[n], hi u32[n]) -> Buffer u32[n]:
+ * the first missing block of each (doc, actor) range (RepoBackend.syncChanges contiguity) */
+static napi_value SyncRanges(napi_env env, napi_callback_info info) {
+    napi_value argv[5];
+    if (!get_args(env, info, 5, argv)) return NULL;
+    Docset *d = get_docset(env, argv[0]);
+    if (!d) return NULL;
+    void *p[4]; size_t n[4];
+    for (int i = 0; i < 4; i++) if (!get_bytes(env, argv[1 + i], &p[i], &n[i])) return NULL;
+    const uint32_t k = (uint32_t)(n[2] / 4);
+    if (n[1] / 8 != k || n[3] / 4 != k) { napi_throw_range_error(env, NULL, "syncRanges: lengths disagree"); return NULL; }
+    uint32_t *out = (uint32_t *)calloc(1, (size_t)k * 4 + 4);
+    int st = hm_sync_ranges_host(d->engine, (const uint64_t *)p[0], (const uint64_t *)p[1], (const uint32_t *)p[2],
+                                 (const uint32_t *)p[3], out, k, (uint32_t)(n[0] / 8));
+    napi_value r = st ? NULL : buf_copy(env, out, (size_t)k * 4);
+    free(out);
+    if (st) return throw_status(env, d->engine, st, "hm_sync_ranges_host");
+    return r;
+}
+
+/* decodeBlocks(blocks[][], aStride, threads) -> {status, docs, changes, deps, ops}: the
+ * stateless decoder (hm_decode_blocks) for cold batches, tables as Buffers */
+static napi_value DecodeBlocks(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return NULL;
+    uint32_t n = 0;
+    if (napi_get_array_length(env, argv[0], &n) != napi_ok) { napi_throw_type_error(env, NULL, "expected an array"); return NULL; }
+    uint32_t *ids = (uint32_t *)calloc(1, (size_t)n * 4 + 4);
+    napi_value idv;
+    void *idp;
+    napi_create_buffer_copy(env, (size_t)n * 4, ids, &idp, &idv);
+    free(ids);
+    DsJob *j = (DsJob *)calloc(1, sizeof(DsJob));
+    if (!gather_blocks(env, idv, argv[0], j)) { ds_job_free(j); return NULL; }
+    hm_decoded *dd = NULL;
+    int st = hm_decode_blocks(j->data, j->bo, j->db, n, get_u32(env, argv[1]), (int)get_u32(env, argv[2]), &dd);
+    ds_job_free(j);
+    if (st) return throw_status(env, NULL, st, "hm_decode_blocks");
+    hm_batch b;
+    hm_decoded_batch(dd, &b);
+    napi_value o;
+    napi_create_object(env, &o);
+    set(env, o, "status", buf_copy(env, hm_decoded_status(dd), (size_t)n * 4));
+    set(env, o, "docs", buf_copy(env, b.docs, (size_t)b.n_docs * sizeof(hm_doc_row)));
+    set(env, o, "changes", buf_copy(env, b.changes, (size_t)b.n_changes * sizeof(hm_change_row)));
+    set(env, o, "deps", buf_copy(env, b.deps, (size_t)b.n_deps * sizeof(hm_dep_row)));
+    set(env, o, "ops", buf_copy(env, b.ops, (size_t)b.n_ops * sizeof(hm_op_row)));
+    set(env, o, "aStride", u32v(env, b.a_stride));
+    hm_decoded_free(dd);
+    return o;
+}
+
 static napi_value Init(napi_env env, napi_value exports) {
     struct { const char *name; napi_callback fn; } fns[] = {
         {"createStore", CreateStore}, {"openDoc", OpenDoc}, {"submit", Submit}, {"wait", Wait},
@@ -543,6 +1102,12 @@ static napi_value Init(napi_env env, napi_value exports) {
         {"clockUpdate", ClockUpdate}, {"statusMessage", StatusMessage},
         {"commCreateLocal", CommCreateLocal}, {"clockExchange", ClockExchange}, {"clockMin", ClockMin},
         {"waitAsync", WaitAsync}, {"readRegs", ReadRegs},
+        {"docsetCreate", DocsetCreate}, {"docsetOpen", DocsetOpen}, {"docsetApply", DocsetApply},
+        {"docsetHistoryPrefix", DocsetHistoryPrefix}, {"docsetClockUpdate", DocsetClockUpdate},
+        {"docsetView", DocsetView}, {"docsetInfo", DocsetInfo}, {"docsetStats", DocsetStats},
+        {"cursorsCreate", CursorsCreate}, {"cursorsReserve", CursorsReserve}, {"cursorsUpdate", CursorsUpdate},
+        {"cursorsGet", CursorsGet}, {"cursorsEntry", CursorsEntry}, {"cursorsDocsWithActors", CursorsDocsWithActors},
+        {"syncRanges", SyncRanges}, {"decodeBlocks", DecodeBlocks}, {"commCreateLocalDocsets", CommCreateLocalDocsets},
     };
     for (size_t i = 0; i < sizeof fns / sizeof fns[0]; i++) {
         napi_value f;

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define HM_ABI_VERSION 3u
+#define HM_ABI_VERSION 4u
 
 /* ------------------------------------------------------------------ */
 /* Status codes                                                        */
@@ -401,6 +401,10 @@ int  hm_cursors_docs_with_actors(hm_cursors *c, uint32_t n_actors, const uint64_
 int hm_sync_ranges_device(hm_engine *e, const uint64_t *present, const uint64_t *word_off,
                           const uint32_t *lo, const uint32_t *hi, uint32_t *out_end, uint32_t n,
                           void *stream);
+/* The same from host arrays (present: n_words u64 bitmap words; staged through the device,
+ * synchronous): the syncChanges plan of a batch of (doc, actor) pairs. */
+int hm_sync_ranges_host(hm_engine *e, const uint64_t *present, const uint64_t *word_off, const uint32_t *lo,
+                        const uint32_t *hi, uint32_t *out_end, uint32_t n, uint32_t n_words);
 
 /* ------------------------------------------------------------------ */
 /* Blocks -> columnar rows (host, multi-threaded)                      */
@@ -429,6 +433,72 @@ const char *hm_decoded_actor(const hm_decoded *d, uint32_t doc, uint32_t rank, s
 const char *hm_decoded_obj(const hm_decoded *d, uint32_t doc, uint32_t obj, size_t *len);       /* object uuid */
 const char *hm_decoded_reg(const hm_decoded *d, uint32_t doc, uint32_t reg, uint32_t *obj, size_t *len); /* key | elemId */
 void hm_decoded_free(hm_decoded *d);
+
+/* ------------------------------------------------------------------ */
+/* Docset: the Node drop-in's host engine (raw blocks in, patches out)  */
+/* ------------------------------------------------------------------ */
+/*
+ * The documents of one device with everything the JS host used to keep per document: their
+ * interners (actor ids ranked in JS string order, object UUIDs, registers, string values,
+ * change content identity), their placement in resident stores (one hm_store per actor-stride
+ * class 8/16/32/64; a document moves to a wider class when a new actor outgrows its rows) and
+ * their patch base.  One hm_docset_apply = one applyChanges round of every listed document:
+ *
+ *   replaces: src/Actor.ts:137-141 parseBlock, src/Block.ts:18-29 unpack, src/JsonBuffer.ts:1-4
+ *             src/DocBackend.ts:169-185 applyRemoteChanges -> Backend.applyChanges -> updateClock
+ *             src/DocBackend.ts:144-167 init(changes) (the first call on a document)
+ *             Automerge makePatch: {clock, deps, canUndo, canRedo, diffs}
+ *
+ * Input: the blocks of each document (one Change per block, '{"' JSON or 'BR' + brotli JSON),
+ * laid out as in hm_decode_blocks; docs[i] is the docset document of doc_block[i]..[i+1]-1
+ * (each at most once per call).  Output (hm_text): per document an hm_doc_result (status:
+ * HM_ERR_INVALID with err_change = the block index in this call when a block does not decode
+ * (the reference's Block.unpack / JSON.parse throw); an Automerge error status with err_change
+ * = the log index (blocks of all successful calls, in order) when applyChanges throws; the
+ * document is rolled back either way) and one JSON text
+ *   {"p": [patch | null, ...], "b": [clock of the whole log | null, ...], "c": [clock of this call's changes | null, ...]}
+ * patch.clock / deps are opSet.clock / opSet.deps; diffs take the document from the previous
+ * successful call's patch to this one (objects created, map keys set / removed, list elements
+ * removed / inserted / set) in the Automerge 0.12 diff vocabulary; "b" is the max seq per actor
+ * over every change of the document's log and "c" over this call's changes (queued ones
+ * included: DocBackend.updateClock(changes), src/DocBackend.ts:135-142).
+ * Calls on one docset are serialised (a second concurrent call fails); hm_docset_open may run
+ * while a call is in flight (it allocates host state only).
+ */
+typedef struct hm_docset hm_docset;
+typedef struct hm_text hm_text;
+typedef struct {
+    uint32_t threads;     /* host threads for decode / render (0 = min(16, hardware)) */
+    uint32_t flags;       /* HM_DOCSET_* */
+} hm_docset_config;
+#define HM_DOCSET_NO_PATCHES 1u   /* patches carry clock / deps only (no diffs, no register reads) */
+
+int  hm_docset_create(hm_engine *e, const hm_docset_config *cfg, hm_docset **out);
+void hm_docset_destroy(hm_docset *ds);
+hm_engine *hm_docset_engine(hm_docset *ds);
+/* n new, empty documents (Backend.init()) with consecutive ids from *out_first */
+int  hm_docset_open(hm_docset *ds, uint32_t n, uint32_t *out_first);
+int  hm_docset_apply(hm_docset *ds, const uint8_t *data, const uint64_t *block_off, const uint32_t *doc_block,
+                     const uint32_t *docs, uint32_t n_docs, hm_text **out);
+const char *hm_text_data(const hm_text *t, size_t *len);
+const hm_doc_result *hm_text_results(const hm_text *t, uint32_t *n);
+void hm_text_free(hm_text *t);
+
+typedef struct {
+    uint32_t a_stride;    /* class of the store the document lives in (0 = not placed yet) */
+    uint32_t n_changes, n_ops, n_actors, n_objs, n_regs, hist_len, n_queued;
+} hm_docset_doc_info_t;
+int hm_docset_doc_info(hm_docset *ds, uint32_t doc, hm_docset_doc_info_t *out);
+/* history.slice(0, n) (src/RepoBackend.ts:572-576): log indices in history order; returns the count */
+int hm_docset_history_prefix(hm_docset *ds, uint32_t doc, uint32_t n, uint32_t *out_log_index);
+/* ClockStore.update(self, docId, doc.clock) for n documents (hm_store_clock_update per class);
+ * *out_stored (optional) = JSON array of the stored clocks, in call order */
+int hm_docset_clock_update(hm_docset *ds, uint32_t n, const uint32_t *docs, uint8_t *out_written, uint8_t *out_differs,
+                           hm_text **out_stored);
+/* the merged document: {uuid: {"type", "keys": [[key, entry]], "elems": [[elemId, entry]]}} */
+int hm_docset_view(hm_docset *ds, uint32_t doc, hm_text **out);
+/* counters: calls, documents, class moves, patches from the hit registers, patches from every register */
+int hm_docset_stats(const hm_docset *ds, uint64_t *out8);
 
 /* ------------------------------------------------------------------ */
 /* Clock exchange across the node's GPUs (RCCL over xGMI)              */

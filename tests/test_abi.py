@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_messages():
     L = engine.lib()
-    assert L.hm_abi_version() == 3
+    assert L.hm_abi_version() == 4
     assert L.hm_status_message(1) == b"Inconsistent reuse of sequence number"
     assert L.hm_status_message(2) == b"Modification of unknown object"
 

@@ -1,0 +1,161 @@
+"""The docset (hm_docset_*, csrc/docset.cpp): raw JSON blocks of many documents, one
+applyChanges round per call (src/DocBackend.ts:169-185, Actor.parseBlock src/Actor.ts:137-141).
+
+Every document is fed in several rounds; after each round its results, opSet clock / deps and
+DocBackend.clock, and after the last its history order, merged state (hm_docset_view) and the
+document its patches rebuild (a restatement of Frontend.applyPatch) must equal the CPU oracle's
+cold merge of the same log.  Errors roll the document back; documents move to wider stores as
+actors arrive."""
+import json
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _blocks(changes):
+    return [json.dumps(c, separators=(",", ":")).encode() for c in changes]
+
+
+def _oracle(log):
+    import oracle.oracle as O
+    from hypermerge_amd.columnar import encode
+    from hypermerge_amd.render import doc_summary
+    b = encode([log])
+    return doc_summary(b, O.merge(b), 0)
+
+
+def _chunks(docs, rng, k=4):
+    out = []
+    for chs in docs:
+        cuts = sorted(rng.integers(0, len(chs) + 1, size=k - 1))
+        out.append([chs[:cuts[0]]] + [chs[cuts[i]:cuts[i + 1]] for i in range(k - 2)] + [chs[cuts[-1]:]])
+    return out
+
+
+def _run(ds, chunked, check_each_round=True):
+    from hypermerge_amd.docset import apply_diffs, ROOT
+    n = len(chunked)
+    first = ds.open(n)
+    ids = list(range(first, first + n))
+    objects = [{ROOT: {"type": "map", "keys": {}, "elems": []}} for _ in range(n)]
+    logs = [[] for _ in range(n)]
+    last = [None] * n
+    for r in range(max(len(c) for c in chunked)):
+        sel = [i for i in range(n) if r < len(chunked[i])]
+        res, js = ds.apply([ids[i] for i in sel], [_blocks(chunked[i][r]) for i in sel])
+        for k, i in enumerate(sel):
+            assert res[k]["status"] == 0, (i, r, res[k])
+            logs[i] += chunked[i][r]
+            apply_diffs(objects[i], js["p"][k]["diffs"])
+            last[i] = (res[k], js["p"][k], js["b"][k])
+            if check_each_round:
+                s = _oracle(logs[i])
+                assert int(res[k]["hist_len"]) == len(s["history"]) and int(res[k]["n_queued"]) == s["queued"]
+                assert js["p"][k]["clock"] == s["clock"] and js["p"][k]["deps"] == s["deps"], (i, r)
+                assert js["b"][k] == s["backend_clock"], (i, r)
+    return ids, objects, logs, last
+
+
+@pytest.mark.parametrize("name,n", [("C2", 60), ("C4", 80), ("C5", 60), ("C3", 6)])
+def test_docset_rounds_equal_oracle(name, n):
+    from hypermerge_amd import synth
+    from hypermerge_amd.columnar import decode_doc
+    from hypermerge_amd.docset import DocSet, render_objects, view_objects
+    from hypermerge_amd.engine import Engine
+    over = {"changes_per_actor": 30} if name == "C3" else {}
+    b = synth.generate(synth.config(name, n_docs=n, **over))
+    docs = [decode_doc(b, i) for i in range(b.n_docs)]
+    ds = DocSet(Engine(0))
+    ids, objects, logs, last = _run(ds, _chunks(docs, np.random.default_rng(7)), check_each_round=name != "C3")
+    for i, d in enumerate(ids):
+        s = _oracle(logs[i])
+        assert s["status"] == "OK"
+        assert render_objects(objects[i]) == json.loads(json.dumps(s["state"])), i       # patches rebuild it
+        assert render_objects(view_objects(ds.view(d))) == json.loads(json.dumps(s["state"])), i
+        order = ds.history_prefix(d, 1 << 20)
+        assert [[logs[i][k]["actor"], logs[i][k]["seq"]] for k in order] == s["history"], i
+        assert last[i][1]["clock"] == s["clock"] and last[i][2] == s["backend_clock"]
+    st = ds.stats()
+    assert st["hit_patches"] > 0 and st["calls"] == 4
+
+
+def test_docset_errors_roll_back():
+    """A mismatched duplicate (Inconsistent reuse of sequence number) and an undecodable block
+    leave the document as it was; the next good round continues from there."""
+    from hypermerge_amd.columnar import ROOT_ID as R
+    from hypermerge_amd.docset import DocSet
+    from hypermerge_amd.engine import Engine
+    ds = DocSet(Engine(0))
+    d = ds.open(2)
+    a, b = "actorA", "actorB"
+    c1 = {"actor": a, "seq": 1, "deps": {}, "ops": [{"action": "set", "obj": R, "key": "x", "value": 1}]}
+    c2 = {"actor": b, "seq": 1, "deps": {a: 1}, "ops": [{"action": "set", "obj": R, "key": "x", "value": 2}]}
+    res, js = ds.apply([d, d + 1], [_blocks([c1]), _blocks([c1])])
+    assert (res["status"] == 0).all()
+    # the same content with its keys in another order is the same change (a no-op duplicate)
+    same = json.dumps({"ops": c1["ops"], "deps": {}, "seq": 1, "actor": a}).encode()
+    bad = dict(c1, ops=[{"action": "set", "obj": R, "key": "x", "value": 99}])
+    res, js = ds.apply([d, d + 1], [[same] + _blocks([c2]), _blocks([c2, bad])])
+    assert res[0]["status"] == 0 and res[1]["status"] == 1
+    assert js["p"][1] is None and js["p"][0]["diffs"] == [{"action": "set", "type": "map", "obj": R, "key": "x", "value": 2}]
+    assert ds.info(d + 1)["n_changes"] == 1 and ds.info(d + 1)["hist_len"] == 1
+    res, js = ds.apply([d + 1], [[b'{"actor": "x", oops'] + _blocks([c2])])
+    assert res[0]["status"] == 32 and res[0]["err_change"] == 0
+    assert ds.info(d + 1)["n_actors"] == 1
+    res, js = ds.apply([d + 1], [_blocks([c2])])
+    assert res[0]["status"] == 0 and js["p"][0]["clock"] == {a: 1, b: 1} and js["b"][0] == {a: 1, b: 1}
+    assert js["p"][0]["diffs"] == [{"action": "set", "type": "map", "obj": R, "key": "x", "value": 2}]
+    assert ds.view(d) == ds.view(d + 1)
+
+
+def test_docset_moves_documents_to_wider_stores():
+    """Documents whose actors outgrow 8 / 16 / 32 move to the wider store class with their
+    whole log; the merged state equals the oracle's, patches included."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_gpu_parity import _float_counter_docs
+    from hypermerge_amd.docset import DocSet, render_objects, view_objects
+    from hypermerge_amd.engine import Engine
+    docs = _float_counter_docs(24, 77, wide=True)
+    rng = random.Random(3)
+    chunked = []
+    for chs in docs:
+        cuts = sorted(rng.sample(range(1, len(chs)), min(3, len(chs) - 1))) if len(chs) > 1 else []
+        parts, prev = [], 0
+        for c in cuts + [len(chs)]:
+            parts.append(chs[prev:c])
+            prev = c
+        chunked.append(parts)
+    ds = DocSet(Engine(0))
+    ids, objects, logs, last = _run(ds, chunked)
+    for i, d in enumerate(ids):
+        s = _oracle(logs[i])
+        assert render_objects(objects[i]) == json.loads(json.dumps(s["state"])), i
+        assert render_objects(view_objects(ds.view(d))) == json.loads(json.dumps(s["state"])), i
+        assert ds.info(d)["a_stride"] >= len(s["backend_clock"])
+    assert ds.stats()["moves"] > 0
+
+
+def test_docset_clock_update_matches_reference_sql():
+    """ClockStore.update(self, doc, doc.clock) after a round (src/ClockStore.ts:78-91): the
+    first update writes, a repeat does not, and the stored clocks are the DocBackend clocks."""
+    from hypermerge_amd import synth
+    from hypermerge_amd.columnar import decode_doc
+    from hypermerge_amd.docset import DocSet
+    from hypermerge_amd.engine import Engine
+    b = synth.generate(synth.config("C5", n_docs=30))
+    docs = [decode_doc(b, i) for i in range(b.n_docs)]
+    ds = DocSet(Engine(0), patches=False)
+    first = ds.open(len(docs))
+    ids = list(range(first, first + len(docs)))
+    res, js = ds.apply(ids, [_blocks(c) for c in docs])
+    assert all(p["diffs"] == [] for p in js["p"])
+    w, df, stored = ds.clock_update(ids + [ds.open(1)])
+    assert w[:-1].all() and not w[-1] and not df.any()
+    assert stored[:-1] == js["b"] and stored[-1] == {}
+    w, df, stored = ds.clock_update(ids)
+    assert not w.any() and not df.any()

@@ -175,3 +175,85 @@ def test_sharded_engine_restride_and_clock_exchange(devices):
         assert g["clock"] == clock
         assert got["exchanged"][d] == clock
     assert shards == set(range(len(devices)))
+
+
+def test_raw_blocks_and_device_cursors_sync_equal_oracle():
+    """RepoBackend.syncChanges (src/RepoBackend.ts:506-531) on the drop-in: the device
+    CursorStore picks the documents of each synced actor, the device contiguity scan stops
+    each range at the first block not downloaded, and the ranges' raw blocks go to
+    DocBackend.applyRemoteBlocks (parsed natively, Actor.parseBlock src/Actor.ts:137-141).
+    The plan equals a host restatement of syncChanges, and every document equals the oracle's
+    merge of exactly the blocks it received, in delivery order (two sync rounds: with holes in
+    the feeds, then complete)."""
+    import numpy as np
+    from hypermerge_amd import synth
+    from hypermerge_amd.columnar import decode_doc, encode
+    from hypermerge_amd.render import doc_summary
+    from repo_harness import plain
+    from hypermerge_amd.render import doc_state
+    import oracle.oracle as O
+    b = synth.generate(synth.config("C5", n_docs=40))
+    rng = np.random.default_rng(4)
+    docs, feeds = {}, {}
+    for i in range(b.n_docs):
+        chs = decode_doc(b, i)
+        actors = sorted({c["actor"] for c in chs})
+        docs[f"doc{i:03d}"] = actors
+        for a in actors:                      # an actor feed: its changes in seq order (one per block)
+            feeds[a] = [json.dumps(c) for c in sorted((c for c in chs if c["actor"] == a), key=lambda c: c["seq"])]
+    holes = {a: [int(rng.random() > 0.15) for _ in f] for a, f in feeds.items()}
+    present = [holes, {a: [1] * len(f) for a, f in feeds.items()}]
+    p = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "run_sync_blocks.js"), "async"],
+                       input=json.dumps({"docs": docs, "feeds": feeds, "present": present}),
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    got = json.loads(p.stdout)
+    # host restatement of syncChanges: per (doc, actor) from doc.changes[actor] to the first hole
+    pos = {(d, a): 0 for d, acts in docs.items() for a in acts}
+    delivered = {d: [] for d in docs}
+    for rnd, pres in enumerate(present):
+        want = []
+        for d in sorted(docs, key=lambda x: x.encode()):
+            for a in sorted(docs[d], key=lambda x: x.encode()):
+                lo = pos[(d, a)]
+                end = lo
+                while end < len(feeds[a]) and pres[a][end]:
+                    end += 1
+                want.append([d, a, lo, end])
+                pos[(d, a)] = end
+                delivered[d] += [json.loads(t) for t in feeds[a][lo:end]]
+        assert sorted(got["plans"][rnd]) == sorted(want), rnd
+    for d in docs:
+        log = delivered[d]
+        bb = encode([log])
+        o = O.merge(bb)
+        s = doc_summary(bb, o, 0)
+        g = got["docs"][d]
+        assert g["history"] == s["history"], d
+        assert g["clock"] == s["backend_clock"], d
+        assert g["view"] == plain(doc_state(bb, o, 0)), d
+        assert g["cursor"] == {a: 9007199254740991 for a in docs[d]}
+        assert g["entry"] == [9007199254740991] * len(docs[d])
+
+
+def test_documents_open_while_an_async_round_is_in_flight():
+    """opening documents while an async round runs on the docset's host thread
+    is safe (host state only), every other call on the busy device throws instead of racing, and
+    all documents come out as the oracle merges them."""
+    from hypermerge_amd import synth
+    from hypermerge_amd.columnar import decode_doc, encode
+    from hypermerge_amd.render import doc_summary
+    import oracle.oracle as O
+    b = synth.generate(synth.config("C4", n_docs=4000))
+    docs = [decode_doc(b, i) for i in range(b.n_docs)]
+    p = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "run_async_open.js")], input=json.dumps({"docs": docs}),
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    got = json.loads(p.stdout)
+    assert got["busyDuring"] and "busy" in (got["busyThrow"] or "")
+    cold = encode(docs, 8)
+    o = O.merge(cold)
+    assert len(got["docs"]) == len(docs)
+    for i, g in enumerate(got["docs"]):
+        s = doc_summary(cold, o, i)
+        assert g["clock"] == s["backend_clock"] and g["hist"] == len(s["history"]) and g["stored"] == s["backend_clock"], i
