@@ -263,6 +263,22 @@ bool js_less(const char *a, uint32_t na, const char *b, uint32_t nb) {
     return u16(std::string(a, na)) < u16(std::string(b, nb));
 }
 
+// One document's binary patch: u32 words, f64 numbers, and the strings it names (pointers into
+// the document's name tables, local indices).  Words:
+//   clock, deps, DocBackend.clock of the log, of this call: each n, then n x (actor string, seq)
+//   n_diffs, then per diff a head word (action 0 create | 1 set | 2 remove | 3 insert, type << 3)
+//   and: create: obj | set (map): obj key entry | remove (map): obj key | remove (list): obj index
+//        insert: obj index elemId entry | set (list): obj index entry
+//   entry: n_surv, the winner's value word, then per conflict: actor string, value word
+//   value word: vtag | datatype << 3 | payload << 5 (payload: string index for STR / OBJ, number
+//   index for INT / FLOAT)
+struct BinDoc {
+    std::vector<uint32_t> w;
+    std::vector<double> nums;
+    std::vector<std::pair<const char *, uint32_t>> strs;
+    bool exotic = false;                                      // a lone surrogate: the call falls back to JSON
+};
+
 // One document's part of a call.
 struct Round {
     uint32_t doc = 0, b0 = 0, b1 = 0;
@@ -286,6 +302,7 @@ struct Round {
     bool full = false;                                       // patch from every register (else the hit ones)
     uint32_t q0 = 0, q1 = 0;                                 // its register requests
     std::string patch, bclock, cclock;
+    BinDoc bin;
 };
 
 struct Scratch {
@@ -558,51 +575,249 @@ void jclock(std::string &o, const DocSt &d, const uint32_t *row, uint32_t n_acto
 
 const char *TYPE_NAME[4] = {"map", "table", "list", "text"};
 
+// What the frontend sees of a register's survivors (the winner's value / link / datatype, each
+// conflict's actor, value, link, datatype): equal signatures render equal diff entries.
+uint64_t entry_sig(const DocSt &d, const hm_surv_result *sv, uint32_t n) {
+    if (!n) return 0;
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t op = sv[i].op;
+        const uint64_t dt = op < d.op_dt.size() ? d.op_dt[op] : 0;
+        const uint64_t act = i && op < d.op_actor.size() ? (uint64_t)d.op_actor[op] + 1 : 0;
+        h = mix64(h ^ ((uint64_t)sv[i].vtag | dt << 8 | act << 16));
+        h = mix64(h + sv[i].value);
+    }
+    return h | 1;
+}
+
+// Patch writers: JSON text (what JSON.parse turns back into the patch) and a compact binary
+// form the Node host turns into the same objects without a JSON parse (HM_DOCSET_BINARY).
+struct JsonW {
+    std::string &o;
+    const DocSt &d;
+    bool any = false;
+    void sep() { if (any) o += ','; any = true; }
+    void clock(const uint32_t *row, uint32_t n_actors) { jclock(o, d, row, n_actors); }
+    void head(const char *action, uint8_t t, uint32_t obj) {
+        sep();
+        o += "{\"action\":\""; o += action; o += "\",\"type\":\""; o += TYPE_NAME[t & 3]; o += "\",\"obj\":";
+        jstr(o, d.objs.ptr(obj), d.objs.len(obj));
+    }
+    void create(uint32_t obj, uint8_t t) {
+        sep();
+        o += "{\"action\":\"create\",\"obj\":";
+        jstr(o, d.objs.ptr(obj), d.objs.len(obj));
+        o += ",\"type\":\""; o += TYPE_NAME[t & 3]; o += "\"}";
+    }
+    void map_set(uint8_t t, uint32_t obj, uint32_t g, const hm_surv_result *sv, uint32_t n) {
+        head("set", t, obj);
+        o += ",\"key\":"; jstr(o, d.regs.ptr(g), d.regs.len(g)); o += ','; jentry(o, d, sv, n); o += '}';
+    }
+    void map_remove(uint8_t t, uint32_t obj, uint32_t g) {
+        head("remove", t, obj);
+        o += ",\"key\":"; jstr(o, d.regs.ptr(g), d.regs.len(g)); o += '}';
+    }
+    void list_remove(uint8_t t, uint32_t obj, uint32_t i) { head("remove", t, obj); o += ",\"index\":" + std::to_string(i) + '}'; }
+    void list_insert(uint8_t t, uint32_t obj, uint32_t i, uint32_t g, const hm_surv_result *sv, uint32_t n) {
+        head("insert", t, obj);
+        o += ",\"index\":" + std::to_string(i) + ",\"elemId\":";
+        jstr(o, d.regs.ptr(g), d.regs.len(g));
+        o += ','; jentry(o, d, sv, n); o += '}';
+    }
+    void list_set(uint8_t t, uint32_t obj, uint32_t i, const hm_surv_result *sv, uint32_t n) {
+        head("set", t, obj);
+        o += ",\"index\":" + std::to_string(i) + ','; jentry(o, d, sv, n); o += '}';
+    }
+};
+
+struct StrMap {                                              // (kind, id) -> local string index, per document
+    std::vector<uint64_t> key;
+    std::vector<uint32_t> val, gen;
+    uint32_t g = 0, mask = 0;
+    void reset() {
+        if (key.empty()) { key.assign(256, 0); val.assign(256, 0); gen.assign(256, 0); mask = 255; }
+        if (++g == 0) { std::fill(gen.begin(), gen.end(), 0u); g = 1; }
+    }
+    void grow() {
+        std::vector<uint64_t> k2 = key; std::vector<uint32_t> v2 = val, g2 = gen;
+        const size_t cap = key.size() * 2;
+        key.assign(cap, 0); val.assign(cap, 0); gen.assign(cap, 0); mask = (uint32_t)cap - 1;
+        for (size_t i = 0; i < k2.size(); i++) if (g2[i] == g) {
+            uint32_t s = (uint32_t)mix64(k2[i]) & mask;
+            while (gen[s] == g) s = (s + 1) & mask;
+            key[s] = k2[i]; val[s] = v2[i]; gen[s] = g;
+        }
+    }
+};
+
+struct BinW {
+    BinDoc &b;
+    const DocSt &d;
+    StrMap &m;
+    uint32_t n_diffs = 0;
+    size_t diffs_at = 0;
+    uint32_t str(uint32_t kind, uint32_t id) {
+        const uint64_t k = ((uint64_t)kind << 32) | id;
+        if ((b.strs.size() + 1) * 2 > m.key.size()) m.grow();
+        uint32_t s = (uint32_t)mix64(k) & m.mask;
+        while (m.gen[s] == m.g) { if (m.key[s] == k) return m.val[s]; s = (s + 1) & m.mask; }
+        const Names &nm = kind == 0 ? d.actors : kind == 1 ? d.objs : kind == 2 ? d.regs : d.strs;
+        const char *p = nm.ptr(id);
+        const uint32_t n = nm.len(id);
+        for (uint32_t i = 0; i + 2 < n; i++) if ((unsigned char)p[i] == 0xED && ((unsigned char)p[i + 1] & 0xE0) == 0xA0) b.exotic = true;
+        m.key[s] = k; m.val[s] = (uint32_t)b.strs.size(); m.gen[s] = m.g;
+        b.strs.emplace_back(p, n);
+        return (uint32_t)b.strs.size() - 1;
+    }
+    void clock(const uint32_t *row, uint32_t n_actors) {
+        const size_t at = b.w.size();
+        b.w.push_back(0);
+        for (uint32_t r = 0; r < n_actors; r++) {
+            if (!row[r]) continue;
+            b.w.push_back(str(0, d.by_rank[r]));
+            b.w.push_back(row[r]);
+            b.w[at]++;
+        }
+    }
+    void begin() { diffs_at = b.w.size(); b.w.push_back(0); }
+    void end() { b.w[diffs_at] = n_diffs; }
+    void head(uint32_t action, uint8_t t, uint32_t obj) { n_diffs++; b.w.push_back(action | (uint32_t)(t & 3) << 3); b.w.push_back(str(1, obj)); }
+    void value(const hm_surv_result &s) {
+        const uint8_t dt = s.op < d.op_dt.size() ? d.op_dt[s.op] : 0;
+        uint32_t payload = 0;
+        switch (s.vtag) {
+        case HM_V_INT: payload = (uint32_t)b.nums.size(); b.nums.push_back((double)(int64_t)s.value); break;
+        case HM_V_FLOAT: { double v; memcpy(&v, &s.value, 8); payload = (uint32_t)b.nums.size(); b.nums.push_back(v); break; }
+        case HM_V_STR: payload = str(3, (uint32_t)s.value); break;
+        case HM_V_OBJ: payload = str(1, (uint32_t)s.value); break;
+        default: break;
+        }
+        b.w.push_back((s.vtag & 7) | (uint32_t)(dt & 3) << 3 | payload << 5);
+    }
+    void entry(const hm_surv_result *sv, uint32_t n) {
+        b.w.push_back(n);
+        value(sv[0]);
+        for (uint32_t i = 1; i < n; i++) {
+            b.w.push_back(str(0, sv[i].op < d.op_actor.size() ? d.op_actor[sv[i].op] : 0));
+            value(sv[i]);
+        }
+    }
+    void create(uint32_t obj, uint8_t t) { head(0, t, obj); }
+    void map_set(uint8_t t, uint32_t obj, uint32_t g, const hm_surv_result *sv, uint32_t n) { head(1, t, obj); b.w.push_back(str(2, g)); entry(sv, n); }
+    void map_remove(uint8_t t, uint32_t obj, uint32_t g) { head(2, t, obj); b.w.push_back(str(2, g)); }
+    void list_remove(uint8_t t, uint32_t obj, uint32_t i) { head(2, t, obj); b.w.push_back(i); }
+    void list_insert(uint8_t t, uint32_t obj, uint32_t i, uint32_t g, const hm_surv_result *sv, uint32_t n) {
+        head(3, t, obj); b.w.push_back(i); b.w.push_back(str(2, g)); entry(sv, n);
+    }
+    void list_set(uint8_t t, uint32_t obj, uint32_t i, const hm_surv_result *sv, uint32_t n) { head(1, t, obj); b.w.push_back(i); entry(sv, n); }
+};
+
+// A document's binary patch as the JSON form (the exotic-string fallback: JSON escapes lone
+// surrogates, the binary blob cannot carry them through Buffer.toString)
+void bin_to_json(const BinDoc &b, std::string &patch, std::string &bclock, std::string &cclock) {
+    size_t p = 0;
+    const auto &w = b.w;
+    auto S = [&](uint32_t i, std::string &o) { jstr(o, b.strs[i].first, b.strs[i].second); };
+    auto clock = [&](std::string &o) {
+        const uint32_t n = w[p++];
+        o += '{';
+        for (uint32_t i = 0; i < n; i++) {
+            if (i) o += ',';
+            S(w[p], o);
+            o += ':' + std::to_string(w[p + 1]);
+            p += 2;
+        }
+        o += '}';
+    };
+    auto value = [&](std::string &o) {
+        const uint32_t v = w[p++], tag = v & 7, dt = (v >> 3) & 3, pay = v >> 5;
+        o += "\"value\":";
+        switch (tag) {
+        case HM_V_NULL: o += "null"; break;
+        case HM_V_FALSE: o += "false"; break;
+        case HM_V_TRUE: o += "true"; break;
+        case HM_V_INT: case HM_V_FLOAT: { uint64_t bits; memcpy(&bits, &b.nums[pay], 8); jnum(o, HM_V_FLOAT, bits); break; }
+        case HM_V_STR: S(pay, o); break;
+        case HM_V_OBJ: S(pay, o); o += ",\"link\":true"; break;
+        default: o += "null";
+        }
+        if (dt == HM_DT_COUNTER) o += ",\"datatype\":\"counter\"";
+        else if (dt == HM_DT_TIMESTAMP) o += ",\"datatype\":\"timestamp\"";
+    };
+    auto entry = [&](std::string &o) {
+        const uint32_t n = w[p++];
+        value(o);
+        if (n <= 1) return;
+        o += ",\"conflicts\":[";
+        for (uint32_t i = 1; i < n; i++) {
+            if (i > 1) o += ',';
+            o += "{\"actor\":";
+            S(w[p++], o);
+            o += ',';
+            value(o);
+            o += '}';
+        }
+        o += ']';
+    };
+    std::string &o = patch;
+    o += "{\"clock\":"; clock(o);
+    o += ",\"deps\":"; clock(o);
+    clock(bclock);
+    clock(cclock);
+    o += ",\"canUndo\":false,\"canRedo\":false,\"diffs\":[";
+    const uint32_t nd = w[p++];
+    for (uint32_t k = 0; k < nd; k++) {
+        if (k) o += ',';
+        const uint32_t hd = w[p++], action = hd & 7, t = (hd >> 3) & 3;
+        const bool list = t >= 2;
+        static const char *ACT[4] = {"create", "set", "remove", "insert"};
+        if (action == 0) {
+            o += "{\"action\":\"create\",\"obj\":"; S(w[p++], o);
+            o += ",\"type\":\""; o += TYPE_NAME[t]; o += "\"}";
+            continue;
+        }
+        o += "{\"action\":\""; o += ACT[action]; o += "\",\"type\":\""; o += TYPE_NAME[t]; o += "\",\"obj\":";
+        S(w[p++], o);
+        if (!list) {
+            o += ",\"key\":"; S(w[p++], o);
+            if (action == 1) { o += ','; entry(o); }
+        } else {
+            o += ",\"index\":" + std::to_string(w[p++]);
+            if (action == 3) { o += ",\"elemId\":"; S(w[p++], o); }
+            if (action != 2) { o += ','; entry(o); }
+        }
+        o += '}';
+    }
+    o += "]}";
+}
+
 // The diffs that take the patch base to the registers' new state (hm_reg_result rows of the
 // requested registers, survivors at `surv`): objects created first, then map keys in
 // request order, then per list removals (descending old index), insertions (ascending new
 // index) and value changes.  The base is advanced to the new state.
-void render_diffs(std::string &o, DocSt &d, const uint32_t *req, const hm_reg_result *rows, const hm_surv_result *surv,
-                  uint32_t n) {
-    bool any = false;
-    auto sep = [&] { if (any) o += ','; any = true; };
-    std::string tmp;
+template <typename W>
+void render_diffs(W &w, DocSt &d, const uint32_t *req, const hm_reg_result *rows, const hm_surv_result *surv, uint32_t n) {
     for (uint32_t ob = 1; ob < d.obj_type.size(); ob++) {
         if (d.obj_type[ob] == NO_TYPE || d.obj_emitted[ob]) continue;
         d.obj_emitted[ob] = 1;
-        sep();
-        o += "{\"action\":\"create\",\"obj\":";
-        jstr(o, d.objs.ptr(ob), d.objs.len(ob));
-        o += ",\"type\":\"";
-        o += TYPE_NAME[d.obj_type[ob] & 3];
-        o += "\"}";
+        w.create(ob, d.obj_type[ob]);
     }
-    struct LOp { uint32_t g, idx; size_t t0, t1; };
+    struct LOp { uint32_t g, idx, q; };
     struct LD { uint32_t obj; std::vector<uint32_t> rem; std::vector<LOp> ins, set; };
     std::vector<LD> lds;
-    std::string lt;                                           // list entries' text
     for (uint32_t q = 0; q < n; q++) {
         const uint32_t g = req[q];
         const hm_reg_result &r = rows[q];
         if (r.obj == HM_NONE || r.obj >= d.obj_type.size()) continue;
         const uint8_t t = d.obj_type[r.obj] == NO_TYPE ? HM_MAKE_MAP : d.obj_type[r.obj];
         const bool list = t == HM_MAKE_LIST || t == HM_MAKE_TEXT;
-        tmp.clear();
-        if (r.n_surv) jentry(tmp, d, surv + r.surv_off, r.n_surv);
-        const uint64_t sg = r.n_surv ? (mix64(hash_bytes(tmp.data(), (uint32_t)tmp.size(), 7)) | 1) : 0;
+        const uint64_t sg = entry_sig(d, surv + r.surv_off, r.n_surv);
         const uint64_t old = d.sig[g];
         if (!list) {
             if (sg == old) continue;
             d.sig[g] = sg;
-            sep();
-            o += sg ? "{\"action\":\"set\",\"type\":\"" : "{\"action\":\"remove\",\"type\":\"";
-            o += TYPE_NAME[t & 3];
-            o += "\",\"obj\":";
-            jstr(o, d.objs.ptr(r.obj), d.objs.len(r.obj));
-            o += ",\"key\":";
-            jstr(o, d.regs.ptr(g), d.regs.len(g));
-            if (sg) { o += ','; o += tmp; }
-            o += '}';
+            if (sg) w.map_set(t, r.obj, g, surv + r.surv_off, r.n_surv);
+            else w.map_remove(t, r.obj, g);
             continue;
         }
         const bool vis = r.n_surv > 0 && r.list_index >= 0;
@@ -612,47 +827,28 @@ void render_diffs(std::string &o, DocSt &d, const uint32_t *req, const hm_reg_re
         for (auto &x : lds) if (x.obj == r.obj) L = &x;
         if (!L) { lds.push_back(LD{r.obj, {}, {}, {}}); L = &lds.back(); }
         std::vector<uint32_t> &el = *d.list_of(r.obj, true);
-        if (old && !vis) {
-            L->rem.push_back((uint32_t)(std::find(el.begin(), el.end(), g) - el.begin()));
-        } else {
-            const size_t t0 = lt.size();
-            lt += tmp;
-            (old ? L->set : L->ins).push_back(LOp{g, (uint32_t)r.list_index, t0, lt.size()});
-        }
+        if (old && !vis) L->rem.push_back((uint32_t)(std::find(el.begin(), el.end(), g) - el.begin()));
+        else (old ? L->set : L->ins).push_back(LOp{g, (uint32_t)r.list_index, q});
         d.sig[g] = ns;
     }
     for (auto &L : lds) {
         std::vector<uint32_t> &el = *d.list_of(L.obj, true);
         const uint8_t t = d.obj_type[L.obj];
-        auto head = [&](const char *action) {
-            sep();
-            o += "{\"action\":\""; o += action; o += "\",\"type\":\""; o += TYPE_NAME[t & 3]; o += "\",\"obj\":";
-            jstr(o, d.objs.ptr(L.obj), d.objs.len(L.obj));
-        };
         std::sort(L.rem.begin(), L.rem.end(), std::greater<uint32_t>());
         for (uint32_t i : L.rem) {
             if (i >= el.size()) continue;
             el.erase(el.begin() + i);
-            head("remove");
-            o += ",\"index\":" + std::to_string(i) + '}';
+            w.list_remove(t, L.obj, i);
         }
         std::stable_sort(L.ins.begin(), L.ins.end(), [](const LOp &a, const LOp &b) { return a.idx < b.idx; });
         for (auto &x : L.ins) {
             const uint32_t i = std::min<uint32_t>(x.idx, (uint32_t)el.size());
             el.insert(el.begin() + i, x.g);
-            head("insert");
-            o += ",\"index\":" + std::to_string(i) + ",\"elemId\":";
-            jstr(o, d.regs.ptr(x.g), d.regs.len(x.g));
-            o += ',';
-            o.append(lt, x.t0, x.t1 - x.t0);
-            o += '}';
+            w.list_insert(t, L.obj, i, x.g, surv + rows[x.q].surv_off, rows[x.q].n_surv);
         }
         for (auto &x : L.set) {
             const uint32_t i = (uint32_t)(std::find(el.begin(), el.end(), x.g) - el.begin());
-            head("set");
-            o += ",\"index\":" + std::to_string(i) + ',';
-            o.append(lt, x.t0, x.t1 - x.t0);
-            o += '}';
+            w.list_set(t, L.obj, i, surv + rows[x.q].surv_off, rows[x.q].n_surv);
         }
     }
 }
@@ -705,6 +901,7 @@ struct hm_docset {
     hm_engine *e = nullptr;
     uint32_t threads = 16;
     bool patches = true;
+    bool binary = false;                                     // HM_DOCSET_BINARY results
     hm_store *stores[N_CLASS] = {nullptr, nullptr, nullptr, nullptr};
     // documents: fixed chunks, so hm_docset_open may run while a call works on earlier documents
     static constexpr uint32_t CHUNK = 4096;
@@ -946,42 +1143,126 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
     }
     mark("read regs");
     // render every document's patch and DocBackend.clock
-    par_for(n, std::min<uint32_t>(ds->threads, std::max<uint32_t>(1, n / 128)), [&](uint32_t lo, uint32_t hi, uint32_t) {
-        for (uint32_t i = lo; i < hi; i++) {
-            Round &x = R[i];
-            if (x.status != HM_OK) continue;
-            DocSt &d = ds->doc(x.doc);
-            std::string &o = x.patch;
-            o.reserve(256);
-            o += "{\"clock\":";
-            jclock(o, d, x.clock, x.n_actors);
-            o += ",\"deps\":";
-            jclock(o, d, x.heads, x.n_actors);
-            o += ",\"canUndo\":false,\"canRedo\":false,\"diffs\":[";
-            if (ds->patches && x.q1 > x.q0)
-                render_diffs(o, d, qregs[x.cls].data() + x.q0, rrows[x.cls].data() + x.q0, rsurv[x.cls].data(), x.q1 - x.q0);
-            else if (ds->patches) render_diffs(o, d, nullptr, nullptr, nullptr, 0);
-            o += "]}";
-            jclock(x.bclock, d, x.back, x.n_actors);
-            // this call's changes alone: max seq per actor (DocBackend.updateClock(changes))
-            uint32_t rc[64] = {0};
-            for (const hm_change_row &c : x.ch) if (c.actor < 64 && c.seq > rc[c.actor]) rc[c.actor] = c.seq;
-            jclock(x.cclock, d, rc, x.n_actors);
-        }
-    });
-    // {"p": [patch | null per document], "b": [max over the whole log | null], "c": [max over this call's changes | null]}
-    size_t tot = 16;
-    for (auto &x : R) tot += x.patch.size() + x.bclock.size() + x.cclock.size() + 18;
+    auto round_clock = [](const Round &x, uint32_t *rc) {      // this call's changes alone (updateClock(changes))
+        for (uint32_t a = 0; a < 64; a++) rc[a] = 0;
+        for (const hm_change_row &c : x.ch) if (c.actor < 64 && c.seq > rc[c.actor]) rc[c.actor] = c.seq;
+    };
+    bool exotic = false;
+    if (ds->binary) {
+        par_for(n, std::min<uint32_t>(ds->threads, std::max<uint32_t>(1, n / 128)), [&](uint32_t lo, uint32_t hi, uint32_t) {
+            StrMap m;
+            for (uint32_t i = lo; i < hi; i++) {
+                Round &x = R[i];
+                if (x.status != HM_OK) continue;
+                DocSt &d = ds->doc(x.doc);
+                m.reset();
+                BinW w{x.bin, d, m};
+                x.bin.w.reserve(64);
+                w.clock(x.clock, x.n_actors);
+                w.clock(x.heads, x.n_actors);
+                w.clock(x.back, x.n_actors);
+                uint32_t rc[64];
+                round_clock(x, rc);
+                w.clock(rc, x.n_actors);
+                w.begin();
+                if (ds->patches) {
+                    if (x.q1 > x.q0) render_diffs(w, d, qregs[x.cls].data() + x.q0, rrows[x.cls].data() + x.q0, rsurv[x.cls].data(), x.q1 - x.q0);
+                    else render_diffs(w, d, nullptr, nullptr, nullptr, 0);
+                }
+                w.end();
+            }
+        });
+        for (auto &x : R) exotic |= x.bin.exotic;
+    }
+    if (!ds->binary || exotic) {
+        par_for(n, std::min<uint32_t>(ds->threads, std::max<uint32_t>(1, n / 128)), [&](uint32_t lo, uint32_t hi, uint32_t) {
+            for (uint32_t i = lo; i < hi; i++) {
+                Round &x = R[i];
+                if (x.status != HM_OK) continue;
+                DocSt &d = ds->doc(x.doc);
+                if (exotic) {                                  // the binary pass already advanced the patch base
+                    // re-render from the words is not possible in JSON form without the base: rebuild
+                    // the JSON from the binary document (same diffs, same order)
+                    bin_to_json(x.bin, x.patch, x.bclock, x.cclock);
+                    continue;
+                }
+                std::string &o = x.patch;
+                o.reserve(256);
+                JsonW w{o, d};
+                o += "{\"clock\":";
+                jclock(o, d, x.clock, x.n_actors);
+                o += ",\"deps\":";
+                jclock(o, d, x.heads, x.n_actors);
+                o += ",\"canUndo\":false,\"canRedo\":false,\"diffs\":[";
+                if (ds->patches) {
+                    if (x.q1 > x.q0) render_diffs(w, d, qregs[x.cls].data() + x.q0, rrows[x.cls].data() + x.q0, rsurv[x.cls].data(), x.q1 - x.q0);
+                    else render_diffs(w, d, nullptr, nullptr, nullptr, 0);
+                }
+                o += "]}";
+                jclock(x.bclock, d, x.back, x.n_actors);
+                uint32_t rc[64];
+                round_clock(x, rc);
+                jclock(x.cclock, d, rc, x.n_actors);
+            }
+        });
+    }
     std::string &s = out->s;
     s.clear();
-    s.reserve(tot);
-    s += "{\"p\":[";
-    for (uint32_t i = 0; i < n; i++) { if (i) s += ','; if (R[i].status == HM_OK) s += R[i].patch; else s += "null"; }
-    s += "],\"b\":[";
-    for (uint32_t i = 0; i < n; i++) { if (i) s += ','; if (R[i].status == HM_OK) s += R[i].bclock; else s += "null"; }
-    s += "],\"c\":[";
-    for (uint32_t i = 0; i < n; i++) { if (i) s += ','; if (R[i].status == HM_OK) s += R[i].cclock; else s += "null"; }
-    s += "]}";
+    if (ds->binary && !exotic) {
+        // HMP1 layout: header u32[8] {magic, n_docs, n_strings, n_words, n_nums, blob_bytes, ascii, 0},
+        // doc_word_off / doc_str_base / doc_num_base u32[n_docs + 1] each, str_off u32[n_strings + 1]
+        // (byte offsets into the blob), words u32[n_words], (8-aligned) nums f64[n_nums], blob
+        std::vector<uint32_t> wo(n + 1, 0), sb(n + 1, 0), nb(n + 1, 0);
+        uint64_t blob = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            const BinDoc &x = R[i].bin;
+            wo[i + 1] = wo[i] + (uint32_t)x.w.size(); sb[i + 1] = sb[i] + (uint32_t)x.strs.size(); nb[i + 1] = nb[i] + (uint32_t)x.nums.size();
+            for (auto &t : x.strs) blob += t.second;
+        }
+        const uint32_t ns = sb[n], nw = wo[n], nn = nb[n];
+        size_t head = 4 * (8 + 3 * ((size_t)n + 1) + (size_t)ns + 1 + nw);
+        const size_t pad = (8 - head % 8) % 8;
+        s.resize(head + pad + 8 * (size_t)nn + blob);
+        uint32_t *h = (uint32_t *)&s[0];
+        h[0] = 0x31504D48u; h[1] = n; h[2] = ns; h[3] = nw; h[4] = nn; h[5] = (uint32_t)blob; h[6] = 1; h[7] = 0;
+        uint32_t *p = h + 8;
+        memcpy(p, wo.data(), 4 * ((size_t)n + 1)); p += n + 1;
+        memcpy(p, sb.data(), 4 * ((size_t)n + 1)); p += n + 1;
+        memcpy(p, nb.data(), 4 * ((size_t)n + 1)); p += n + 1;
+        uint32_t *so = p;
+        p += ns + 1;
+        uint32_t *words = p;
+        double *nums = (double *)(&s[0] + head + pad);
+        char *bl = &s[0] + head + pad + 8 * (size_t)nn;
+        so[0] = 0;
+        uint32_t k = 0;
+        uint64_t at = 0;
+        bool ascii = true;
+        for (uint32_t i = 0; i < n; i++) {
+            const BinDoc &x = R[i].bin;
+            if (!x.w.empty()) memcpy(words + wo[i], x.w.data(), 4 * x.w.size());
+            if (!x.nums.empty()) memcpy(nums + nb[i], x.nums.data(), 8 * x.nums.size());
+            for (auto &t : x.strs) {
+                memcpy(bl + at, t.first, t.second);
+                for (uint32_t c = 0; c < t.second && ascii; c++) ascii = (unsigned char)t.first[c] < 0x80;
+                at += t.second;
+                so[++k] = (uint32_t)at;
+            }
+        }
+        h[6] = ascii ? 1 : 0;
+    } else {
+        // {"p": [patch | null per document], "b": [max over the whole log | null], "c": [max over this call's changes | null]}
+        size_t tot = 16;
+        for (auto &x : R) tot += x.patch.size() + x.bclock.size() + x.cclock.size() + 18;
+        s.reserve(tot);
+        s += "{\"p\":[";
+        for (uint32_t i = 0; i < n; i++) { if (i) s += ','; if (R[i].status == HM_OK) s += R[i].patch; else s += "null"; }
+        s += "],\"b\":[";
+        for (uint32_t i = 0; i < n; i++) { if (i) s += ','; if (R[i].status == HM_OK) s += R[i].bclock; else s += "null"; }
+        s += "],\"c\":[";
+        for (uint32_t i = 0; i < n; i++) { if (i) s += ','; if (R[i].status == HM_OK) s += R[i].cclock; else s += "null"; }
+        s += "]}";
+    }
     out->res.resize(n);
     for (uint32_t i = 0; i < n; i++) {
         Round &x = R[i];
@@ -1012,6 +1293,7 @@ int hm_docset_create(hm_engine *e, const hm_docset_config *cfg, hm_docset **out)
     const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
     ds->threads = cfg && cfg->threads ? cfg->threads : std::min<uint32_t>(16, hw);
     ds->patches = !(cfg && (cfg->flags & HM_DOCSET_NO_PATCHES));
+    ds->binary = cfg && (cfg->flags & HM_DOCSET_BINARY);
     ds->chunks.reserve(1u << 16);
     *out = ds;
     return HM_OK;

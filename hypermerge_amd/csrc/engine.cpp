@@ -5,6 +5,7 @@
 // catches and returns an hm_status.  There is no CPU fallback: if the HIP
 // library cannot run, calls fail with HM_ERR_DEVICE.
 #include <hip/hip_runtime.h>
+#include <cstdio>
 #include <cstring>
 #include <cstdlib>
 #include <string>
@@ -193,19 +194,26 @@ int hm_engine_create(const hm_config *cfg, hm_engine **out) {
     e->device = cfg ? cfg->device : 0;
     e->flags = cfg ? cfg->flags : 0;
     int n = 0;
+    // a failing step is named on stderr (there is no engine to hold the message)
+    auto fail = [&](const char *what, hipError_t r) {
+        fprintf(stderr, "hm_engine_create: %s failed: %s (device %d, %d devices)\n", what, hipGetErrorString(r), e->device, n);
+        delete e;
+        return HM_ERR_DEVICE;
+    };
     hipError_t r = hipGetDeviceCount(&n);
-    if (r != hipSuccess || n <= e->device) { delete e; return HM_ERR_DEVICE; }
-    if (hipSetDevice(e->device) != hipSuccess) { delete e; return HM_ERR_DEVICE; }
+    if (r != hipSuccess) return fail("hipGetDeviceCount", r);
+    if (n <= e->device) return fail("device ordinal", hipErrorInvalidDevice);
+    if ((r = hipSetDevice(e->device)) != hipSuccess) return fail("hipSetDevice", r);
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, e->device) == hipSuccess) e->num_cus = prop.multiProcessorCount;
     {
         size_t lim = 0, need = hm_large_stack_bytes();
         if (hipDeviceGetLimit(&lim, hipLimitStackSize) == hipSuccess && need > lim &&
-            hipDeviceSetLimit(hipLimitStackSize, need) != hipSuccess) { delete e; return HM_ERR_DEVICE; }
+            (r = hipDeviceSetLimit(hipLimitStackSize, need)) != hipSuccess) return fail("hipDeviceSetLimit(stack)", r);
     }
-    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { delete e; return HM_ERR_DEVICE; }
+    if ((r = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking)) != hipSuccess) return fail("hipStreamCreate", r);
     for (auto &ev : e->ev)
-        if (hipEventCreate(&ev) != hipSuccess) { delete e; return HM_ERR_DEVICE; }
+        if ((r = hipEventCreate(&ev)) != hipSuccess) return fail("hipEventCreate", r);
     *out = e;
     return HM_OK;
 }

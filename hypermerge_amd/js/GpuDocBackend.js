@@ -64,6 +64,96 @@ function toChange(c) {
   throw new Error(`fail to unpack blocks - head is '${header}'`)
 }
 
+// A round's results as the docset renders them: JSON text ('{"p": ...}') or the HMP1 binary
+// form (include/hypermerge_amd.h, HM_DOCSET_BINARY) -> {p: [patch], b: [log clock], c: [call clock]}
+// per document of the call.  The binary form builds the same objects JSON.parse would, without
+// the parse (the round's strings decoded once, numbers read from a Float64Array).
+const TYPES = ['map', 'table', 'list', 'text']
+const ACTIONS = ['create', 'set', 'remove', 'insert']
+function decodeRound(buf, n) {
+  if (buf.length === 0 || buf[0] === 0x7b) return JSON.parse(buf.toString())
+  if (buf.byteOffset % 8) buf = Buffer.from(buf)           // a fresh, aligned copy
+  const u = new Uint32Array(buf.buffer, buf.byteOffset, buf.length >>> 2)
+  if (u[0] !== 0x31504d48 || u[1] !== n) throw new Error('docset results: bad HMP1 header')
+  const ns = u[2], nw = u[3], nn = u[4], blobBytes = u[5], ascii = u[6]
+  let at = 8
+  const woff = u.subarray(at, at + n + 1); at += n + 1
+  const sbase = u.subarray(at, at + n + 1); at += n + 1
+  const nbase = u.subarray(at, at + n + 1); at += n + 1
+  const soff = u.subarray(at, at + ns + 1); at += ns + 1
+  const w = u.subarray(at, at + nw); at += nw
+  const numsAt = ((4 * at + 7) >> 3) << 3
+  const nums = new Float64Array(buf.buffer, buf.byteOffset + numsAt, nn)
+  const blobAt = numsAt + 8 * nn
+  const strs = new Array(ns)
+  if (ascii) {
+    const text = buf.toString('latin1', blobAt, blobAt + blobBytes)
+    for (let i = 0; i < ns; i++) strs[i] = text.substring(soff[i], soff[i + 1])
+  } else {
+    for (let i = 0; i < ns; i++) strs[i] = buf.toString('utf8', blobAt + soff[i], blobAt + soff[i + 1])
+  }
+  const P = new Array(n), B = new Array(n), C = new Array(n)
+  for (let d = 0; d < n; d++) {
+    let p = woff[d]
+    if (p === woff[d + 1]) { P[d] = B[d] = C[d] = null; continue }
+    const sb = sbase[d], nb = nbase[d]
+    const clock = () => {
+      const c = {}
+      for (let k = w[p++]; k > 0; k--) { c[strs[sb + w[p]]] = w[p + 1]; p += 2 }
+      return c
+    }
+    const value = (e) => {
+      const v = w[p++], tag = v & 7, dt = (v >>> 3) & 3, pay = v >>> 5
+      switch (tag) {
+        case 0: e.value = null; break
+        case 1: e.value = false; break
+        case 2: e.value = true; break
+        case 3: case 4: e.value = nums[nb + pay]; break
+        case 5: e.value = strs[sb + pay]; break
+        case 6: e.value = strs[sb + pay]; e.link = true; break
+        default: e.value = null
+      }
+      if (dt === 1) e.datatype = 'counter'
+      else if (dt === 2) e.datatype = 'timestamp'
+    }
+    const entry = (e) => {
+      const k = w[p++]
+      value(e)
+      if (k > 1) {
+        const cs = new Array(k - 1)
+        for (let i = 1; i < k; i++) { const c = { actor: strs[sb + w[p++]] }; value(c); cs[i - 1] = c }
+        e.conflicts = cs
+      }
+    }
+    const patch = { clock: clock(), deps: clock(), canUndo: false, canRedo: false, diffs: null }
+    B[d] = clock()
+    C[d] = clock()
+    const nd = w[p++]
+    const diffs = new Array(nd)
+    for (let k = 0; k < nd; k++) {
+      const h = w[p++], action = h & 7, t = (h >>> 3) & 3
+      const obj = strs[sb + w[p++]]
+      let e
+      if (action === 0) e = { action: 'create', obj, type: TYPES[t] }
+      else if (t < 2) {
+        e = { action: ACTIONS[action], type: TYPES[t], obj, key: strs[sb + w[p++]] }
+        if (action === 1) entry(e)
+      } else if (action === 3) {
+        e = { action: 'insert', type: TYPES[t], obj, index: w[p++], elemId: null }
+        e.elemId = strs[sb + w[p++]]
+        entry(e)
+      } else {
+        e = { action: ACTIONS[action], type: TYPES[t], obj, index: w[p++] }
+        if (action === 1) entry(e)
+      }
+      diffs[k] = e
+    }
+    patch.diffs = diffs
+    P[d] = patch
+  }
+  return { p: P, b: B, c: C }
+}
+
 class History {
   constructor(state) { this.state = state; this.size = state.histLen }
   slice(a, b) {
@@ -132,13 +222,14 @@ class GpuEngine {
     this.devices = o.devices || [o.device || 0]
     this.mode = o.mode || 'batched'
     this.patches = o.patches !== false
-    this.docsets = this.devices.map((d) => addon.docsetCreate(d, o.threads || 0, this.patches))
+    this.docsets = this.devices.map((d) => addon.docsetCreate(d, o.threads || 0, this.patches, o.binary !== false))
     this.queues = new Map()          // state -> FIFO of jobs
     this.flushing = false
     this.scheduled = false
     this.onError = o.onError || null
     this.submits = 0
     this.comm = null
+    this.slice = o.slice || 4096     // documents per docset call in async mode (pipelined)
   }
 
   shardOf(docId) { return Number(fnv1a64(docId) % BigInt(this.docsets.length)) }
@@ -215,32 +306,48 @@ class GpuEngine {
     })
   }
 
-  // the round's documents grouped by docset (device shard), with their blocks
-  groups(round) {
+  // the round's documents grouped by docset (device shard), in slices of at most `slice`
+  // documents (async mode queues the slices on the docset's host thread, so the main thread
+  // hands over the next slice and builds the previous one's messages while a slice merges)
+  groups(round, slice) {
     const g = new Map()
     for (const [state, job] of round) {
       let x = g.get(state.ds)
-      if (!x) { x = { ds: state.ds, items: [] }; g.set(state.ds, x) }
-      x.items.push({ state, job })
+      if (!x) { x = []; g.set(state.ds, x) }
+      x.push({ state, job })
     }
-    for (const x of g.values()) {
-      x.ids = Uint32Array.from(x.items, (it) => it.state.id)
-      x.blocks = x.items.map((it) => it.job.entries.map(toBlock))
+    const out = []
+    for (const [ds, items] of g) {
+      const k = slice || items.length
+      for (let a = 0; a < items.length; a += k) out.push({ ds, items: items.slice(a, a + k) })
     }
-    return Array.from(g.values())
+    return out
+  }
+
+  static prepare(g) {
+    g.ids = Uint32Array.from(g.items, (it) => it.state.id)
+    g.blocks = g.items.map((it) => {
+      const e = it.job.entries
+      for (let i = 0; i < e.length; i++) if (!Buffer.isBuffer(e[i]) && typeof e[i] !== 'string') return e.map(toBlock)
+      return e                          // raw blocks / JSON texts go over as they are
+    })
+    return g
   }
 
   // One applyChanges per document of the round, one docset call per device
   runRound(round) {
     const errors = []
-    for (const g of this.groups(round)) this.finish(g, addon.docsetApply(g.ds, g.ids, g.blocks), errors)
+    for (const g of this.groups(round, 0)) {
+      GpuEngine.prepare(g)
+      this.finish(g, addon.docsetApply(g.ds, g.ids, g.blocks), errors)
+    }
     this.raise(errors)
   }
 
   runRoundAsync(round, done) {
     let gs
     try {
-      gs = this.groups(round)
+      gs = this.groups(round, this.slice)
     } catch (e) {
       done()
       throw e
@@ -249,6 +356,7 @@ class GpuEngine {
     let left = gs.length
     const finish = () => { try { this.raise(errors) } finally { done() } }
     for (const g of gs) {
+      GpuEngine.prepare(g)
       addon.docsetApply(g.ds, g.ids, g.blocks, (err, r) => {
         try {
           if (err) g.items.forEach(({ job }) => errors.push([job, err]))
@@ -263,7 +371,7 @@ class GpuEngine {
   finish({ items }, r, errors) {
     this.submits++
     const res = new Uint32Array(r.results.buffer, r.results.byteOffset, r.results.length / 4)
-    const j = JSON.parse(r.json)
+    const j = decodeRound(r.data, items.length)
     const ok = []
     items.forEach(({ state, job }, i) => {
       const status = res[RESULT_U32 * i] | 0
@@ -754,4 +862,4 @@ function syncPlan(engine, cursors, repoId, actors, docs, present) {
 }
 
 module.exports = { GpuEngine, GpuBackendState, DocBackend, ClockStore, CursorStore, syncPlan, makeBackend, materialize,
-  fnv1a64, addon, toChange }
+  fnv1a64, addon, toChange, decodeRound }

@@ -624,17 +624,23 @@ static Docset *get_docset(napi_env env, napi_value v) {
     return d;
 }
 
-/* docsetCreate(device, threads, patches) -> docset */
+/* docsetCreate(device, threads, patches[, binary]) -> docset (binary: results in the HMP1 form) */
 static napi_value DocsetCreate(napi_env env, napi_callback_info info) {
-    napi_value argv[3];
-    if (!get_args(env, info, 3, argv)) return NULL;
+    napi_value argv[4];
+    size_t argc = 4;
+    if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < 3) {
+        napi_throw_type_error(env, NULL, "missing arguments");
+        return NULL;
+    }
+    bool binary = false;
+    if (argc >= 4) napi_get_value_bool(env, argv[3], &binary);
     Docset *d = (Docset *)calloc(1, sizeof(Docset));
     hm_config cfg = {(int)get_u32(env, argv[0]), 0};
     int st = hm_engine_create(&cfg, &d->engine);
     if (st) { free(d); return throw_status(env, NULL, st, "hm_engine_create"); }
     bool patches = true;
     napi_get_value_bool(env, argv[2], &patches);
-    hm_docset_config dc = {get_u32(env, argv[1]), patches ? 0u : HM_DOCSET_NO_PATCHES};
+    hm_docset_config dc = {get_u32(env, argv[1]), (patches ? 0u : HM_DOCSET_NO_PATCHES) | (binary ? HM_DOCSET_BINARY : 0u)};
     st = hm_docset_create(d->engine, &dc, &d->ds);
     if (st) { napi_value r = throw_status(env, d->engine, st, "hm_docset_create"); hm_engine_destroy(d->engine); free(d); return r; }
     napi_value out;
@@ -709,17 +715,16 @@ static napi_value text_object(napi_env env, hm_text *t) {
     const char *p = hm_text_data(t, &len);
     uint32_t n = 0;
     const hm_doc_result *r = hm_text_results(t, &n);
-    napi_value o, js;
+    napi_value o;
     napi_create_object(env, &o);
     set(env, o, "results", buf_copy(env, r, (size_t)n * sizeof(hm_doc_result)));
-    napi_create_string_utf8(env, p, len, &js);
-    set(env, o, "json", js);
+    set(env, o, "data", buf_copy(env, p, len));
     return o;
 }
 
 static void ds_call_js(napi_env env, napi_value cb, void *context, void *data) {
     DsJob *j = (DsJob *)data;
-    if (context) ((Docset *)context)->busy = 0;
+    if (context) ((Docset *)context)->busy--;
     if (env && cb) {
         napi_value argv[2], undef, ret;
         napi_get_undefined(env, &undef);
@@ -737,10 +742,12 @@ static void ds_call_js(napi_env env, napi_value cb, void *context, void *data) {
     ds_job_free(j);
 }
 
-/* docsetApply(docset, ids Uint32Array, blocks[][], callback?) -> {results, json} | undefined:
+/* docsetApply(docset, ids Uint32Array, blocks[][], callback?) -> {results, data} | undefined
+ * (data: the JSON text, or the HMP1 binary form when the docset was created binary):
  * one applyChanges round of every listed document (hm_docset_apply); with a callback the
- * round runs on the docset's host thread and callback(err, {results, json}) runs on the main
- * thread when it is done (no other docset call until then, except docsetOpen) */
+ * round runs on the docset's host thread and callback(err, {results, data}) runs on the main
+ * thread when it is done; further async calls queue behind it (run in call order), any other
+ * docset call except docsetOpen throws until every queued round has called back */
 static napi_value DocsetApply(napi_env env, napi_callback_info info) {
     napi_value argv[4];
     size_t argc = 4;
@@ -748,12 +755,14 @@ static napi_value DocsetApply(napi_env env, napi_callback_info info) {
         napi_throw_type_error(env, NULL, "missing arguments");
         return NULL;
     }
-    Docset *d = get_docset(env, argv[0]);
+    napi_valuetype cbt = napi_undefined;
+    if (argc >= 4) napi_typeof(env, argv[3], &cbt);
+    /* async calls queue behind the ones in flight (the host thread runs them in order); a
+     * synchronous call needs the docset idle */
+    Docset *d = cbt == napi_function ? get_docset_any(env, argv[0]) : get_docset(env, argv[0]);
     if (!d) return NULL;
     DsJob *j = (DsJob *)calloc(1, sizeof(DsJob));
     if (!gather_blocks(env, argv[1], argv[2], j)) { ds_job_free(j); return NULL; }
-    napi_valuetype cbt = napi_undefined;
-    if (argc >= 4) napi_typeof(env, argv[3], &cbt);
     if (cbt != napi_function) {
         int st = hm_docset_apply(d->ds, j->data, j->bo, j->db, j->ids, j->n, &j->out);
         if (st) { ds_job_free(j); return throw_status(env, d->engine, st, "hm_docset_apply"); }
@@ -779,7 +788,7 @@ static napi_value DocsetApply(napi_env env, napi_callback_info info) {
         }
         d->started = 1;
     }
-    d->busy = 1;
+    d->busy++;
     pthread_mutex_lock(&d->mu);
     if (d->tail) d->tail->next = j; else d->head = j;
     d->tail = j;

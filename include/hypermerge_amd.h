@@ -472,6 +472,21 @@ typedef struct {
     uint32_t flags;       /* HM_DOCSET_* */
 } hm_docset_config;
 #define HM_DOCSET_NO_PATCHES 1u   /* patches carry clock / deps only (no diffs, no register reads) */
+#define HM_DOCSET_BINARY 2u       /* hm_docset_apply's text is the binary form below instead of JSON */
+/* Binary results ('HMP1', for a host that builds the patch objects itself instead of parsing
+ * JSON; a call whose strings hold a lone surrogate falls back to the JSON form, first byte '{'):
+ *   u32 header[8] = {0x31504D48, n_docs, n_strings, n_words, n_nums, blob_bytes, ascii, 0}
+ *   u32 doc_word_off[n_docs + 1], doc_str_base[n_docs + 1], doc_num_base[n_docs + 1]
+ *   u32 str_off[n_strings + 1] (byte offsets into blob), u32 words[n_words], pad to 8,
+ *   f64 nums[n_nums], u8 blob[blob_bytes]
+ * A document's words (string and number indices local to the document): opSet.clock, opSet.deps,
+ * the log's clock, this call's clock, each as n then n x (actor string, seq); then n_diffs and
+ * per diff a head word (action 0 create | 1 set | 2 remove | 3 insert, type << 3 with type 0 map
+ * | 1 table | 2 list | 3 text) followed by: create: obj; map set: obj, key, entry; map remove:
+ * obj, key; list remove: obj, index; list insert: obj, index, elemId, entry; list set: obj,
+ * index, entry.  entry = n_surv, the winner's value word, then per conflict (actor string, value
+ * word); value word = vtag | datatype << 3 | payload << 5 (STR / OBJ: string index, INT / FLOAT:
+ * number index). */
 
 int  hm_docset_create(hm_engine *e, const hm_docset_config *cfg, hm_docset **out);
 void hm_docset_destroy(hm_docset *ds);

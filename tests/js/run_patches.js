@@ -41,7 +41,7 @@ function render(objects, uuid, depth) {
 }
 
 const input = JSON.parse(require('fs').readFileSync(0, 'utf8'))
-const engine = new GpuEngine({ mode: input.mode || 'batched', aStride: 8 })
+const engine = new GpuEngine({ mode: input.mode || 'batched', binary: input.binary !== false })
 const tick = () => new Promise((r) => setImmediate(r))
 ;(async () => {
   const docs = input.docs.map((chunks, i) => {

@@ -70,9 +70,11 @@ def test_batched_feed_matches_oracle(mode):
         assert g["types"][-1] in ("RemotePatchMsg", "ReadyMsg")
 
 
-@pytest.mark.parametrize("name,n,mode", [("C5", 200, "batched"), ("C3", 12, "batched"), ("C2", 100, "batched"),
-                                         ("C5", 200, "async"), ("C4", 300, "async")])
-def test_patch_diffs_rebuild_the_merged_document(name, n, mode):
+@pytest.mark.parametrize("name,n,mode,binary", [("C5", 200, "batched", True), ("C3", 12, "batched", True),
+                                                ("C2", 100, "batched", True), ("C5", 200, "async", True),
+                                                ("C4", 300, "async", True), ("C5", 200, "async", False),
+                                                ("C3", 12, "batched", False)])
+def test_patch_diffs_rebuild_the_merged_document(name, n, mode, binary):
     """Applying every patch's diffs in order (a restatement of Frontend.applyPatch's effect,
     src/DocFrontend.ts:162-179) rebuilds exactly the canonical merged document of the oracle's
     cold merge of the same changes — maps, conflicts, counters, links, lists and text."""
@@ -90,7 +92,7 @@ def test_patch_diffs_rebuild_the_merged_document(name, n, mode):
         cuts = sorted(rng.integers(1, len(chs) + 1, size=3))
         chunked.append([chs[:cuts[0]], chs[cuts[0]:cuts[1]], chs[cuts[1]:cuts[2]], chs[cuts[2]:]])
     p = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "run_patches.js")],
-                       input=json.dumps({"docs": chunked, "mode": mode}),
+                       input=json.dumps({"docs": chunked, "mode": mode, "binary": binary}),
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr
     got = json.loads(p.stdout)["docs"]

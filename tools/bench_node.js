@@ -54,6 +54,7 @@ async function runCpu(fromBlocks) {
   let patches = 0, diffs = 0
   const docs = input.docs.map((_, i) => new DocBackend('doc' + i, (m) => { patches++; if (m.patch) diffs += m.patch.diffs.length }))
   const parsed = fromBlocks ? null : input.docs
+  profStart()
   const t0 = process.hrtime.bigint()
   for (let r = 0; r < rounds; r++) {
     input.docs.forEach((chunks, i) => {
@@ -64,6 +65,7 @@ async function runCpu(fromBlocks) {
     })
   }
   const s = Number(process.hrtime.bigint() - t0) / 1e9
+  await profStop()
   return { changes: nChanges, seconds: s, changes_per_s: nChanges / s, patches, diffs,
     digest: digest(docs.map((d) => ({ id: d.id, clock: d.clock, hist: d.back.history.length }))),
     state_digest: stateDigest(docs.map((d) => materialize(d.back))) }
@@ -79,6 +81,29 @@ function plain(view, uuid) {
   return o
 }
 
+// HM_NODE_PROF=file: a V8 CPU profile of the timed region (the inspector's profiler, started
+// after the device is open: `node --cpu-prof` from process start makes HSA device discovery
+// fail under the profiler's signals)
+let prof = null
+function profStart() {
+  if (!process.env.HM_NODE_PROF) return
+  const inspector = require('inspector')
+  prof = new inspector.Session()
+  prof.connect()
+  prof.post('Profiler.enable')
+  prof.post('Profiler.setSamplingInterval', { interval: 200 })
+  prof.post('Profiler.start')
+}
+function profStop() {
+  if (!prof) return Promise.resolve()
+  return new Promise((resolve) => prof.post('Profiler.stop', (err, r) => {
+    if (!err) fs.writeFileSync(process.env.HM_NODE_PROF, JSON.stringify(r.profile))
+    prof.disconnect()
+    prof = null
+    resolve()
+  }))
+}
+
 async function runGpu(mode, objects) {
   const G = require(path.join(__dirname, '..', 'hypermerge_amd', 'js', 'GpuDocBackend.js'))
   const engine = new G.GpuEngine({ mode, patches: patchesOn })
@@ -92,6 +117,7 @@ async function runGpu(mode, objects) {
     undefined, engine))
   const src = objects ? input.docs : blocks
   const st0 = engine.stats()
+  profStart()
   const t0 = process.hrtime.bigint()
   for (let r = 0; r < rounds; r++) {
     src.forEach((chunks, i) => {
@@ -103,6 +129,7 @@ async function runGpu(mode, objects) {
   }
   await engine.idle()
   const s = Number(process.hrtime.bigint() - t0) / 1e9
+  await profStop()
   const st = engine.stats()
   return { changes: nChanges, seconds: s, changes_per_s: nChanges / s, patches, diffs, submits: engine.submits,
     patch_diffs: patchesOn, hit_register_patches: st.hitPatches - st0.hitPatches, full_patches: st.fullPatches - st0.fullPatches,
