@@ -72,6 +72,28 @@ __global__ __launch_bounds__(64) void cursor_update_kernel(uint32_t n_docs, cons
     }
 }
 
+// capacity pre-check of an update (all-or-nothing, as the reference's SQLite transaction):
+// status |= 1 if a row would outgrow K with the call's new actors; nothing is written
+__global__ __launch_bounds__(64) void cursor_capacity_kernel(uint32_t n_docs, const uint32_t *rows, const uint32_t *off,
+                                                             const u64 *akey, const u64 *tkey, const uint32_t *tcnt,
+                                                             uint32_t K, uint32_t *status) {
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t d = blockIdx.x; d < n_docs; d += gridDim.x) {
+        const uint32_t r = rows[d], e0 = off[d], e1 = off[d + 1];
+        const u64 *rk = tkey + (size_t)r * K;
+        const uint32_t c0 = tcnt[r] < K ? tcnt[r] : K;
+        uint32_t fresh = 0;
+        for (uint32_t e = e0 + lane; e < e1; e += 64) {
+            const u64 k = akey[e];
+            bool have = false;
+            for (uint32_t j = 0; j < c0 && !have; j++) have = rk[j] == k;
+            fresh += have ? 0u : 1u;
+        }
+        for (int o = 32; o > 0; o >>= 1) fresh += (uint32_t)__shfl_xor((int)fresh, o);
+        if (lane == 0 && c0 + fresh > K) atomicOr(status, 1u);
+    }
+}
+
 // entry(doc, actor): stored seq or 0 (src/CursorStore.ts:68-70)
 __global__ void cursor_entry_kernel(uint32_t n, const uint32_t *rows, const u64 *akey, const u64 *tkey,
                                     const u64 *tseq, const uint32_t *tcnt, uint32_t K, u64 *out) {
@@ -193,6 +215,21 @@ int hm_cursors_update(hm_cursors *c, uint32_t n_docs, const uint32_t *rows, cons
         if (entry_off[d] > entry_off[d + 1]) return hm_engine_fail(c->e, HM_ERR_INVALID, "entry offsets not ascending");
     }
     try {
+        // one entry per (row, actor) in a call: the kernel upserts rows in parallel, so a repeated
+        // row or actor would race (the reference applies one cursor object per document)
+        {
+            std::vector<uint32_t> rs(rows, rows + n_docs);
+            std::sort(rs.begin(), rs.end());
+            if (std::adjacent_find(rs.begin(), rs.end()) != rs.end())
+                return hm_engine_fail(c->e, HM_ERR_INVALID, "a cursor row appears twice in one update");
+            std::vector<u64> ks;
+            for (uint32_t d = 0; d < n_docs; d++) {
+                ks.assign(actor_keys + entry_off[d], actor_keys + entry_off[d + 1]);
+                std::sort(ks.begin(), ks.end());
+                if (std::adjacent_find(ks.begin(), ks.end()) != ks.end())
+                    return hm_engine_fail(c->e, HM_ERR_INVALID, "an actor appears twice in one document's cursor");
+            }
+        }
         CCHK(c, hipSetDevice(hm_engine_device(c->e)));
         hipStream_t st = hm_engine_stream(c->e);
         const size_t o_rows = 0, o_off = al(4 * (size_t)n_docs), o_key = o_off + al(4 * ((size_t)n_docs + 1)),
@@ -209,6 +246,15 @@ int hm_cursors_update(hm_cursors *c, uint32_t n_docs, const uint32_t *rows, cons
         }
         CCHK(c, hipMemsetAsync(sp + o_st, 0, 4, st));
         const uint32_t grid = std::min<uint32_t>(n_docs, 65535u * 4);
+        // all or nothing: a row that would outgrow K fails the call before anything is written
+        hipLaunchKernelGGL(cursor_capacity_kernel, dim3(grid), dim3(64), 0, st, n_docs, (const uint32_t *)(sp + o_rows),
+                           (const uint32_t *)(sp + o_off), (const u64 *)(sp + o_key), c->key, c->cnt, c->K,
+                           (uint32_t *)(sp + o_st));
+        CCHK(c, hipGetLastError());
+        uint32_t over = 0;
+        CCHK(c, hipMemcpyAsync(&over, sp + o_st, 4, hipMemcpyDeviceToHost, st));
+        CCHK(c, hipStreamSynchronize(st));
+        if (over) return hm_engine_fail(c->e, HM_ERR_INVALID, "a document's cursor would exceed max_actors_per_doc (nothing written)");
         hipLaunchKernelGGL(cursor_update_kernel, dim3(grid), dim3(64), 0, st, n_docs, (const uint32_t *)(sp + o_rows),
                            (const uint32_t *)(sp + o_off), (const u64 *)(sp + o_key), (const double *)(sp + o_seq), c->key,
                            c->seq, c->cnt, c->K, sp + o_dif, (uint32_t *)(sp + o_st));

@@ -55,7 +55,7 @@ struct Caps { uint32_t opl, cls; bool lists, counters; };
 Caps launch_caps(const hm_batch *b) {
     Caps c;
     uint32_t mo = b->max_ops;
-    c.opl = mo <= 64 ? 1 : (mo <= 128 ? 2 : 4);
+    c.opl = mo <= 64 ? 1 : (mo <= 128 ? 2 : (mo <= 192 ? 3 : 4));
     // 0 = unknown hint -> the larger class (documents outside it are deferred)
     c.cls = (b->max_regs && b->max_objs && b->max_deps) ? hm_small_class(b->max_regs, b->max_objs, b->max_deps) : 1u;
     c.lists = (b->doc_flags & HM_DOC_HAS_LISTS) != 0;
@@ -118,7 +118,9 @@ int launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, hipStream
     if (r != hipSuccess) return hip_fail(e, r, "merge_large_kernel launch");
     HIPCHK(e, hipEventRecord(e->ev[3], s));
     e->n_last = 2;
-    e->last_scratch = pb;
+    // the deferred list lives in the scratch: only the engine's own pool outlives this call
+    // (caller scratch may be freed or reused before hm_last_deferred)
+    e->last_scratch = scratch ? nullptr : pb;
     return HM_OK;
 }
 
@@ -387,7 +389,8 @@ int hm_last_kernel_ms(hm_engine *e, float *ms, int max_kernels) {
 
 int hm_last_deferred(hm_engine *e, uint32_t *out_docs, uint32_t cap) {
     if (!e) return -HM_ERR_INVALID;
-    if (!e->last_scratch || e->n_last < 2) return 0;
+    if (e->n_last < 2) return 0;
+    if (!e->last_scratch) return -fail(e, HM_ERR_INVALID, "the last launch used caller scratch: its deferred list is the caller's");
     if (hipEventSynchronize(e->ev[3]) != hipSuccess) return -HM_ERR_DEVICE;
     uint32_t n = 0;
     if (hipMemcpy(&n, e->last_scratch + 16, 4, hipMemcpyDeviceToHost) != hipSuccess) return -HM_ERR_DEVICE;

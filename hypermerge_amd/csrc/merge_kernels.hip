@@ -179,6 +179,9 @@ struct SmallLds {
 template <int CLS> struct SizeClass;
 template <> struct SizeClass<0> { static constexpr uint32_t NR = 32, NO = 16, ND = 128; };
 template <> struct SizeClass<1> { static constexpr uint32_t NR = 256, NO = 64, ND = 512; };
+// nested map / list documents of a few dozen changes (C5: <= 108 registers, <= 20 objects): the
+// class-1 carve would hold a list launch to 4 waves per CU (35.8 KB), this one to 6 (24.3 KB)
+template <> struct SizeClass<2> { static constexpr uint32_t NR = 128, NO = 32, ND = 256; };
 
 // LDS carve, identical for the host size query and the device pointers.  Sized per launch
 // (ops, registers, objects, dep rows, lists, counters): LDS is what bounds the number of
@@ -199,8 +202,11 @@ __host__ __device__ inline size_t small_carve(P base, uint32_t NOp, uint32_t NR,
     TAKE(base, uint32_t, NA_MAX * 3);
     TAKE(objslot, uint32_t, NO); TAKE(segcnt, uint32_t, NR);   TAKE(survcnt, uint32_t, NR);
     TAKE(regoff, uint32_t, NR);  TAKE(regobj, uint32_t, NR);   TAKE(insmin, uint32_t, NR);
-    TAKE(flags, uint32_t, 2);    TAKE(deps, uint32_t, ND > NOp ? ND : NOp);   // flags[1]: max n_deps
+    TAKE(flags, uint32_t, 2);
+    const size_t deps_at = o;                                      // deps + depinfo: dead after K1b's fold check
+    TAKE(deps, uint32_t, ND > NOp ? ND : NOp);                     // flags[1]: max n_deps
     TAKE(depinfo, uint32_t, ND);
+    const size_t deps_bytes = o - deps_at;
     TAKE(opmeta, uint32_t, NOp); TAKE(opro, uint32_t, NOp);
     TAKE(hist_of, int32_t, 64);
     TAKE(survop, uint16_t, NOp); TAKE(opbase, uint16_t, 64);   TAKE(oppar, uint16_t, NOp);
@@ -209,8 +215,11 @@ __host__ __device__ inline size_t small_carve(P base, uint32_t NOp, uint32_t NR,
     if (lists) {
         const uint32_t NP = NR + NO, NE = 2 * (NOp + NO);
         TAKE(opelem, uint32_t, NOp);
+        L->nodekey = L->opelem;                                    // opelem is dead after K2's op scan (K3 runs later)
         TAKE(nins, uint32_t, 1);      TAKE(pcount, uint32_t, NP);  TAKE(poff, uint32_t, NP);
-        TAKE(pfill, uint32_t, NP);    TAKE(nodekey, uint32_t, NOp); TAKE(tour0, uint32_t, NE);
+        TAKE(pfill, uint32_t, NP);
+        if ((size_t)NE * sizeof(uint32_t) <= deps_bytes) L->tour0 = (decltype(L->tour0))(base + deps_at);   // K3's tour in the dep tables
+        else TAKE(tour0, uint32_t, NE);
         TAKE(listbase, uint32_t, NO + 1);
         TAKE(nodeop, uint16_t, NOp);  TAKE(nodepi, uint16_t, NOp); TAKE(regnode, uint16_t, NR);
         TAKE(plist, uint16_t, NOp);   TAKE(fc, uint16_t, NP);      TAKE(ns, uint16_t, NOp);
@@ -503,7 +512,8 @@ __device__ __forceinline__ Rows load_rows(const SmallParams &p, const hm_doc_row
     }
     load_op(p, doc, lane, r.a0, r.b0);
     if (OPL > 1) load_op(p, doc, lane + WAVE, r.a1, r.b1);
-    if (OPL > 2) { load_op(p, doc, lane + 2 * WAVE, r.a2, r.b2); load_op(p, doc, lane + 3 * WAVE, r.a3, r.b3); }
+    if (OPL > 2) load_op(p, doc, lane + 2 * WAVE, r.a2, r.b2);
+    if (OPL > 3) load_op(p, doc, lane + 3 * WAVE, r.a3, r.b3);
     const hm_dep_row *dp = p.deps + doc.dep_off;
     if (lane < doc.n_deps) r.d0 = *reinterpret_cast<const uint2 *>(dp + lane);
     if (lane + WAVE < doc.n_deps) r.d1 = *reinterpret_cast<const uint2 *>(dp + lane + WAVE);
@@ -533,7 +543,8 @@ __device__ __forceinline__ void stage_rows(const SmallParams &p, const SmallLds 
     const uint32_t lane = threadIdx.x, m = doc.n_ops;
     stage_op<LISTS>(L, lane, m, r.a0, r.b0);
     if (OPL > 1) stage_op<LISTS>(L, lane + WAVE, m, r.a1, r.b1);
-    if (OPL > 2) { stage_op<LISTS>(L, lane + 2 * WAVE, m, r.a2, r.b2); stage_op<LISTS>(L, lane + 3 * WAVE, m, r.a3, r.b3); }
+    if (OPL > 2) stage_op<LISTS>(L, lane + 2 * WAVE, m, r.a2, r.b2);
+    if (OPL > 3) stage_op<LISTS>(L, lane + 3 * WAVE, m, r.a3, r.b3);
     const uint32_t nd = doc.n_deps < p.cap_deps ? doc.n_deps : p.cap_deps;
     if (lane < nd) L.deps[lane] = pack_dep(r.d0);
     if (lane + WAVE < nd) L.deps[lane + WAVE] = pack_dep(r.d1);
@@ -1412,7 +1423,7 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
 }
 
 template <int OPL, bool LISTS, int CLS>
-__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(OPL >= 4 ? (LISTS ? HM_WAVES_PER_EU_OPL4 - 1 : HM_WAVES_PER_EU_OPL4) : HM_WAVES_PER_EU)))
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(OPL >= 3 ? (LISTS ? HM_WAVES_PER_EU_OPL4 - 1 : HM_WAVES_PER_EU_OPL4) : HM_WAVES_PER_EU)))
 void merge_small_kernel(SmallParams p) {
     extern __shared__ __align__(16) uint8_t lds_raw[];
     typedef SizeClass<CLS> C;
@@ -1536,16 +1547,21 @@ extern "C" int hm_debug_stamps(unsigned long long *out, int n, int reset) {
 }
 #endif
 uint32_t hm_small_class(uint32_t max_regs, uint32_t max_objs, uint32_t max_deps) {
-    typedef hm::SizeClass<0> S;
-    return (max_regs <= S::NR && max_objs <= S::NO && max_deps <= S::ND) ? 0u : 1u;
+    typedef hm::SizeClass<0> S0;
+    typedef hm::SizeClass<2> S2;
+    if (max_regs <= S0::NR && max_objs <= S0::NO && max_deps <= S0::ND) return 0u;
+    if (max_regs <= S2::NR && max_objs <= S2::NO && max_deps <= S2::ND) return 2u;
+    return 1u;
+}
+
+template <int CLS> static size_t carve_of(uint32_t opl, bool lists, bool counters) {
+    hm::SmallLds L;
+    typedef hm::SizeClass<CLS> C;
+    return hm::small_carve((uintptr_t)0, 64 * opl, C::NR, C::NO, C::ND, lists, counters, &L);
 }
 
 size_t hm_small_lds_bytes(uint32_t opl, uint32_t cls, bool lists, bool counters) {
-    hm::SmallLds L;
-    return cls == 0 ? hm::small_carve((uintptr_t)0, 64 * opl, hm::SizeClass<0>::NR, hm::SizeClass<0>::NO,
-                                      hm::SizeClass<0>::ND, lists, counters, &L)
-                    : hm::small_carve((uintptr_t)0, 64 * opl, hm::SizeClass<1>::NR, hm::SizeClass<1>::NO,
-                                      hm::SizeClass<1>::ND, lists, counters, &L);
+    return cls == 0 ? carve_of<0>(opl, lists, counters) : cls == 2 ? carve_of<2>(opl, lists, counters) : carve_of<1>(opl, lists, counters);
 }
 
 // resident 1-wave workgroups per CU for the instantiation a launch will use (VGPRs and LDS)
@@ -1553,9 +1569,10 @@ uint32_t hm_small_occupancy(uint32_t opl, uint32_t cls, bool lists, bool counter
     const size_t lds = hm_small_lds_bytes(opl, cls, lists, counters);
     int n = 0;
 #define HM_OCC(O_, L_, C_) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, hm::merge_small_kernel<O_, L_, C_>, WAVE, lds)
-#define HM_OCC_OPL(L_, C_) switch (opl) { case 1: HM_OCC(1, L_, C_); break; case 2: HM_OCC(2, L_, C_); break; default: HM_OCC(4, L_, C_); }
-    if (cls == 0) { if (lists) { HM_OCC_OPL(true, 0) } else { HM_OCC_OPL(false, 0) } }
-    else          { if (lists) { HM_OCC_OPL(true, 1) } else { HM_OCC_OPL(false, 1) } }
+#define HM_OCC_OPL(L_, C_) switch (opl) { case 1: HM_OCC(1, L_, C_); break; case 2: HM_OCC(2, L_, C_); break; case 3: HM_OCC(3, L_, C_); break; default: HM_OCC(4, L_, C_); }
+    if (cls == 0)      { if (lists) { HM_OCC_OPL(true, 0) } else { HM_OCC_OPL(false, 0) } }
+    else if (cls == 2) { if (lists) { HM_OCC_OPL(true, 2) } else { HM_OCC_OPL(false, 2) } }
+    else               { if (lists) { HM_OCC_OPL(true, 1) } else { HM_OCC_OPL(false, 1) } }
 #undef HM_OCC_OPL
 #undef HM_OCC
     return n > 0 ? (uint32_t)n : 1u;
@@ -1564,9 +1581,10 @@ uint32_t hm_small_occupancy(uint32_t opl, uint32_t cls, bool lists, bool counter
 hipError_t hm_launch_small(const SmallParams &p, uint32_t opl, uint32_t cls, bool lists, uint32_t grid, hipStream_t s) {
     const size_t lds = hm_small_lds_bytes(opl, cls, lists, p.counters != 0);
 #define HM_LAUNCH(O_, L_, C_) hipLaunchKernelGGL((hm::merge_small_kernel<O_, L_, C_>), dim3(grid), dim3(WAVE), lds, s, p)
-#define HM_OPL(L_, C_) switch (opl) { case 1: HM_LAUNCH(1, L_, C_); break; case 2: HM_LAUNCH(2, L_, C_); break; default: HM_LAUNCH(4, L_, C_); }
-    if (cls == 0) { if (lists) { HM_OPL(true, 0) } else { HM_OPL(false, 0) } }
-    else          { if (lists) { HM_OPL(true, 1) } else { HM_OPL(false, 1) } }
+#define HM_OPL(L_, C_) switch (opl) { case 1: HM_LAUNCH(1, L_, C_); break; case 2: HM_LAUNCH(2, L_, C_); break; case 3: HM_LAUNCH(3, L_, C_); break; default: HM_LAUNCH(4, L_, C_); }
+    if (cls == 0)      { if (lists) { HM_OPL(true, 0) } else { HM_OPL(false, 0) } }
+    else if (cls == 2) { if (lists) { HM_OPL(true, 2) } else { HM_OPL(false, 2) } }
+    else               { if (lists) { HM_OPL(true, 1) } else { HM_OPL(false, 1) } }
 #undef HM_OPL
 #undef HM_LAUNCH
     return hipGetLastError();

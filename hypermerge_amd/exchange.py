@@ -257,16 +257,20 @@ class RcclTransport:
         return d.cpu().numpy().view(np.uint32).copy()
 
 
-def align(all_recs: np.ndarray, own: np.ndarray):
+def align(all_recs: np.ndarray, own: np.ndarray, held: Optional[np.ndarray] = None):
     """The (doc, actor) key universe of the gathered records, sorted (identical on every
     rank), and this rank's contribution to the min-clock over it: its seq for an entry it
     has, 0 for an actor it lacks on a document it holds, NOT_HELD for a document it does
-    not hold."""
+    not hold.  `held` = the doc keys this rank holds; None = the documents `own` has records
+    for (right only when `own` carries every held document's full clock row: delta records
+    or an empty clock would make a held document look not held)."""
     pairs = np.unique(np.stack([all_recs["doc_key"], all_recs["actor_key"]], axis=1), axis=0) \
         if len(all_recs) else np.zeros((0, 2), np.uint64)
     mine = np.full(len(pairs), NOT_HELD, np.uint32)
+    held_keys = own["doc_key"] if held is None else np.asarray(held, np.uint64)
+    if len(pairs) and len(held_keys):
+        mine[np.isin(pairs[:, 0], held_keys)] = 0
     if len(pairs) and len(own):
-        mine[np.isin(pairs[:, 0], own["doc_key"])] = 0
         # own entries' positions in the (lexicographically sorted) universe
         keyed = pairs[:, 0].astype(object) * (1 << 64) + pairs[:, 1].astype(object)
         own_k = own["doc_key"].astype(object) * (1 << 64) + own["actor_key"].astype(object)
@@ -290,9 +294,9 @@ class ClockExchange:
     def clocks(self, all_recs: np.ndarray) -> Dict[str, Dict[str, int]]:
         return clocks_of(all_recs, self.keys)
 
-    def min_clock(self, all_recs: np.ndarray, own: np.ndarray) -> Dict[str, Dict[str, int]]:
-        """Clock.intersection across the ranks holding each document."""
-        pairs, mine = align(all_recs, own)
+    def min_clock(self, all_recs: np.ndarray, own: np.ndarray, held: Optional[np.ndarray] = None) -> Dict[str, Dict[str, int]]:
+        """Clock.intersection across the ranks holding each document (`held`: see align)."""
+        pairs, mine = align(all_recs, own, held)
         m = self.t.min_allreduce(mine)
         out: Dict[str, Dict[str, int]] = {}
         for (dk, ak), v in zip(pairs, m):

@@ -227,8 +227,9 @@ int hm_merge_device(hm_engine *e, const hm_batch *batch, const hm_results *out,
 int hm_last_kernel_ms(hm_engine *e, float *ms, int max_kernels);
 /* Documents the last hm_merge_* launch routed to the general (workgroup) kernel: waits
  * for that launch, copies up to `cap` of their launch-row indices (in hand-over order)
- * and returns their count (negative hm_status on failure).  Diagnostics / roofline
- * attribution: the two kernels' algorithmic bytes are split by it. */
+ * and returns their count (negative hm_status on failure; -HM_ERR_INVALID after a
+ * hm_merge_device with caller scratch, whose list the engine cannot know is still valid).
+ * Diagnostics / roofline attribution: the two kernels' algorithmic bytes are split by it. */
 int hm_last_deferred(hm_engine *e, uint32_t *out_docs, uint32_t cap);
 
 /* ------------------------------------------------------------------ */
@@ -378,7 +379,8 @@ int  hm_cursors_reserve(hm_cursors *c, uint32_t n_rows);
  * actors per document; seqs as JS numbers, Infinity allowed); each is an upsert-max
  * (ON CONFLICT DO UPDATE ... WHERE excluded.seq > seq).  out_differs[d] (optional) = 1 if
  * !Clock.equal(cursor, stored cursor after the update), i.e. updateQ is pushed.
- * HM_ERR_INVALID if a row outgrows max_actors_per_doc. */
+ * All or nothing: HM_ERR_INVALID with nothing written if a row would outgrow
+ * max_actors_per_doc, a row appears twice in the call, or an actor twice in one row's entries. */
 int  hm_cursors_update(hm_cursors *c, uint32_t n_docs, const uint32_t *rows, const uint32_t *entry_off,
                        const uint64_t *actor_keys, const double *seqs, uint8_t *out_differs);
 /* CursorStore.get for n rows: out_count[i] entries in out_actor/out_seq [i * max_actors_per_doc ...] */

@@ -116,6 +116,14 @@ function runScenario(steps) {
       const got = repo(st[1]).cursors.get(st[2]) || {}
       if (!Clock.equal(got, want) || Object.keys(got).length !== Object.keys(want).length)
         throw new Error(`cursor ${JSON.stringify(st)}: ${JSON.stringify(got)}`)
+    } else if (op === 'expect_clockstore') {
+      const got = clocksGet(st[1], st[2])
+      if (!Clock.equal(got, st[3]) || Object.keys(got).length !== Object.keys(st[3]).length)
+        throw new Error(`clockstore ${JSON.stringify(st)}: ${JSON.stringify(got)}`)
+    } else if (op === 'expect_doc_clock') {
+      const got = repo(st[1]).docs.get(st[2]).clock
+      if (!Clock.equal(got, st[3]) || Object.keys(got).length !== Object.keys(st[3]).length)
+        throw new Error(`doc clock ${JSON.stringify(st)}: ${JSON.stringify(got)}`)
     } else throw new Error(op)
   }
   const out = {}

@@ -226,6 +226,12 @@ class World:
                 want = {a: (inf if v == "INF" else v) for a, v in st[3].items()}
                 got = self.repo(st[1]).cursors.get(st[2], {})
                 assert got == want, (st, got)
+            elif op == "expect_clockstore":                 # ClockStore.get(repoId, docId)
+                got = self.clocks_get(st[1], st[2])
+                assert got == st[3], (st, got)
+            elif op == "expect_doc_clock":                  # DocBackend.clock
+                got = self.repo(st[1]).docs[st[2]].clock
+                assert got == st[3], (st, got)
             else:
                 raise ValueError(op)
         return {f"{r.id}/{d}": v for r in self.repos.values() for d, v in r.watched.items()}

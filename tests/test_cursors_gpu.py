@@ -124,3 +124,34 @@ def test_sync_plan_matches_sync_changes_loop(engine):
                 i += 1
             want.append((d, a, lo, i))
     assert got == sorted(want)
+
+
+def test_cursor_update_is_all_or_nothing(engine):
+    """an update that would overflow a row, or that names a row or an actor twice,
+    fails with nothing written (the reference's update is one SQLite transaction)."""
+    import ctypes
+    import numpy as np
+    from hypermerge_amd.cursors import CursorStore
+    from hypermerge_amd.engine import EngineError
+    cs = CursorStore(engine, max_actors_per_doc=3)
+    cs.update("r", "d1", {"a": 1, "b": 2})
+    cs.update("r", "d2", {"a": 5})
+    before = cs.get_many("r", ["d1", "d2"])
+    with pytest.raises(EngineError):
+        cs.update_many("r", {"d2": {"a": 9}, "d1": {"c": 1, "d": 1, "a": 7}})     # d1 would hold 4 actors
+    assert cs.get_many("r", ["d1", "d2"]) == before
+    t = cs._t("r")
+    rows = np.array([t.rows["d1"], t.rows["d1"]], np.uint32)
+    off = np.array([0, 1, 2], np.uint32)
+    keys = np.array([cs._key("a"), cs._key("b")], np.uint64)
+    seqs = np.array([9.0, 9.0])
+    st = t._L.hm_cursors_update(t._h, 2, rows.ctypes.data, off.ctypes.data, keys.ctypes.data, seqs.ctypes.data, None)
+    assert st == 32
+    rows1 = np.array([t.rows["d1"]], np.uint32)
+    off1 = np.array([0, 2], np.uint32)
+    keys1 = np.array([cs._key("a"), cs._key("a")], np.uint64)
+    st = t._L.hm_cursors_update(t._h, 1, rows1.ctypes.data, off1.ctypes.data, keys1.ctypes.data, seqs.ctypes.data, None)
+    assert st == 32
+    assert cs.get_many("r", ["d1", "d2"]) == before
+    cs.update("r", "d1", {"c": 4})
+    assert cs.get("r", "d1") == {"a": 1, "b": 2, "c": 4}

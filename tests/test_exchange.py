@@ -196,3 +196,21 @@ def test_alignment_and_records_host():
     assert inter == {("docA", "a"): 1, ("docB", "c"): 2}
     assert C.intersection({"a": 1, "b": 3}, {"a": 5, "d": 1}) == {"a": 1}
     assert X.fnv1a64("") == 0xCBF29CE484222325 and X.fnv1a64("a") == 0xAF63DC4C8601EC8C
+
+
+def test_align_counts_held_documents_without_records():
+    """a rank that holds a document but sends no record for it (an empty clock,
+    or delta records) contributes 0, not NOT_HELD, when the held set is given explicitly."""
+    from hypermerge_amd.exchange import align, NOT_HELD, CLOCK_REC_DT
+    allr = np.zeros(2, CLOCK_REC_DT)
+    allr["doc_key"] = [1, 1]
+    allr["actor_key"] = [10, 11]
+    allr["seq"] = [3, 4]
+    own = np.zeros(0, CLOCK_REC_DT)
+    _, mine = align(allr, own)
+    assert (mine == NOT_HELD).all()
+    _, mine = align(allr, own, held=np.array([1], np.uint64))
+    assert (mine == 0).all()                 # Clock.intersection with {} drops both entries
+    own2 = allr[:1].copy()
+    _, mine = align(allr, own2, held=np.array([1, 7], np.uint64))
+    assert list(mine) == [3, 0]
