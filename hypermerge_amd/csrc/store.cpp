@@ -19,6 +19,12 @@
 // advanced in place by inc_apply_kernel, touching only the registers the new ops hit;
 // any other document re-merges its whole log with the batch merge kernels (applyChanges
 // is a left fold of addChange, so the state after A then B is the state after A ++ B).
+//
+// The documents' segments and totals live on the device (DevDoc, 64 B per handle) and a
+// submit is planned there: plan_kernel checks every row and routes it, alloc_kernel takes
+// the new segments from device bump pointers and writes the append descriptors, the
+// rollback of failed documents is a kernel too.  The host moves only the batch tables, a
+// few 64-byte plan summaries, and the per-document results.
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <atomic>
@@ -35,15 +41,6 @@
 #include "store_kernels.h"
 
 namespace {
-
-struct Seg { uint32_t off = 0, cap = 0; };
-
-struct DocMeta {
-    Seg c, d, o, r;                     // change, dep, op, register segments
-    uint32_t n_c = 0, n_d = 0, n_o = 0, n_r = 0, n_objs = 1, n_actors = 0;
-    uint16_t flags = 0;
-    hm_doc_result last = {};            // result of the last successful merge
-};
 
 template <typename T>
 struct DBuf {                            // device buffer of T with capacity
@@ -62,33 +59,37 @@ uint32_t pow2ceil(uint32_t x) {
 struct hm_store {
     hm_engine *e = nullptr;
     uint32_t S = 8;
-    std::vector<DocMeta> docs;
-    // arenas (capacity in rows) and bump pointers
+    uint32_t n_handles = 0;
+    // arenas (capacity in rows); the bump pointers live in the device PlanStats
     size_t cap_c = 0, cap_d = 0, cap_o = 0, cap_r = 0;
-    size_t used_c = 0, used_d = 0, used_o = 0, used_r = 0;
     hm_change_row *changes = nullptr; int32_t *hist = nullptr; uint32_t *all_deps = nullptr;
     hm_dep_row *deps = nullptr;
     hm_op_row *ops = nullptr; hm_surv_result *surv = nullptr;
     hm_reg_result *regs = nullptr;
     // per handle
     size_t cap_h = 0;
+    DevDoc *dm = nullptr;                         // segments and totals
+    uint32_t *seen = nullptr;                     // submit stamps (repeated-handle check)
     hm_doc_result *res_docs = nullptr;
     uint32_t *clock = nullptr, *back_clock = nullptr, *heads = nullptr, *min_clock = nullptr, *stored = nullptr;
+    // per submit (device): plan rows, descriptors, lists, stats
+    DBuf<PlanRow> plan;
+    DBuf<AppendDesc> descs, bdescs;
+    DBuf<uint32_t> list;                          // re-merge list (cold, then handed back)
+    DBuf<uint32_t> blist;                         // rollback list
+    DBuf<uint8_t> remap, inv;
+    DBuf<hm_doc_row> rows;
+    PlanStats *st = nullptr;
+    uint32_t stamp = 0;
     // staging (device)
     DBuf<uint8_t> stage;
     // in-flight batch
     std::atomic<bool> pending{false};             // a submitted batch not yet waited for (other threads may read it)
     uint64_t next_id = 1, pending_id = 0;
     std::vector<uint32_t> p_handles;              // batch rows -> handles
-    struct OldMeta { uint32_t n_c, n_d, n_o, n_r, n_objs; uint16_t n_actors, flags; };
-    std::vector<OldMeta> p_old;                   // log sizes before the append (rollback)
-    std::vector<int32_t> p_inv_row;               // batch row -> offset of its inverse remap in p_inv (-1 = none)
-    std::vector<uint8_t> p_inv;                   // inverse remap rows [S]
+    uint32_t *p_handles_dev = nullptr;            // (staged)
+    bool p_remap = false;
     uint8_t *p_gather_dev = nullptr;
-    // per-submit host scratch kept between submits (a 1M-document submit would otherwise
-    // allocate and first-touch ~130 MB every round)
-    std::vector<AppendDesc> descs;
-    std::vector<uint32_t> grow;
     // incremental applyRemoteChanges (inc_apply_kernel) and the last submit's routing
     bool incremental = true;
     uint32_t st_inc = 0, st_cold = 0, st_bail = 0;
@@ -111,15 +112,44 @@ int dev_alloc(hm_store *s, T **p, size_t n) {
     return HM_OK;
 }
 
-int ensure_stage(hm_store *s, size_t bytes) {
-    if (bytes <= s->stage.cap) return HM_OK;
+// a per-submit device buffer of at least n elements (contents not kept)
+template <typename T>
+int ensure_buf(hm_store *s, DBuf<T> &b, size_t n) {
+    if (n <= b.cap && b.p) return HM_OK;
     SCHK(s, hipStreamSynchronize(hm_engine_stream(s->e)));
-    if (s->stage.p) (void)hipFree(s->stage.p);
-    s->stage.p = nullptr; s->stage.cap = 0;
-    const size_t cap = std::max(bytes, (size_t)1 << 20) * 2;
-    if (hipMalloc((void **)&s->stage.p, cap) != hipSuccess) return hm_engine_fail(s->e, HM_ERR_NOMEM, "hipMalloc store staging");
-    s->stage.cap = cap;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr; b.cap = 0;
+    const size_t cap = std::max<size_t>(n, 1024) * 3 / 2;
+    if (hipMalloc((void **)&b.p, cap * sizeof(T)) != hipSuccess) return hm_engine_fail(s->e, HM_ERR_NOMEM, "hipMalloc store buffer");
+    b.cap = cap;
     return HM_OK;
+}
+
+int ensure_stage(hm_store *s, size_t bytes) { return ensure_buf(s, s->stage, bytes); }
+
+PlanStats read_stats(hm_store *s, int *rc) {
+    PlanStats st;
+    memset(&st, 0, sizeof st);
+    hipStream_t q = hm_engine_stream(s->e);
+    if (hipMemcpyAsync(&st, s->st, sizeof st, hipMemcpyDeviceToHost, q) != hipSuccess || hipStreamSynchronize(q) != hipSuccess)
+        *rc = hm_engine_fail(s->e, HM_ERR_DEVICE, "reading the submit plan");
+    return st;
+}
+
+// zero the per-phase fields of the device stats, keeping the bump pointers
+int reset_stats(hm_store *s) {
+    SCHK(s, hipMemsetAsync(s->st, 0, offsetof(PlanStats, bump), hm_engine_stream(s->e)));
+    SCHK(s, hipMemsetAsync(&s->st->tot_c, 0, 4 * sizeof(unsigned long long), hm_engine_stream(s->e)));
+    return HM_OK;
+}
+
+DevDoc read_doc(hm_store *s, uint32_t h, int *rc) {
+    DevDoc m;
+    memset(&m, 0, sizeof m);
+    hipStream_t q = hm_engine_stream(s->e);
+    if (hipMemcpyAsync(&m, s->dm + h, sizeof m, hipMemcpyDeviceToHost, q) != hipSuccess || hipStreamSynchronize(q) != hipSuccess)
+        *rc = hm_engine_fail(s->e, HM_ERR_DEVICE, "reading a document's meta");
+    return m;
 }
 
 // grow the per-handle tables to hold `need` documents (contents preserved)
@@ -128,10 +158,16 @@ int ensure_handles(hm_store *s, size_t need) {
     const size_t cap = std::max<size_t>(need, std::max<size_t>(1024, s->cap_h * 2));
     hipStream_t st = hm_engine_stream(s->e);
     const uint32_t S = s->S;
-    hm_doc_result *rd; int r;
-    if ((r = dev_alloc(s, &rd, cap))) return r;
+    hm_doc_result *rd; DevDoc *dm; uint32_t *seen; int r;
+    if ((r = dev_alloc(s, &rd, cap)) || (r = dev_alloc(s, &dm, cap)) || (r = dev_alloc(s, &seen, cap))) return r;
     SCHK(s, hipMemsetAsync(rd, 0, cap * sizeof(hm_doc_result), st));
-    if (s->cap_h) SCHK(s, hipMemcpyAsync(rd, s->res_docs, s->cap_h * sizeof(hm_doc_result), hipMemcpyDeviceToDevice, st));
+    SCHK(s, hipMemsetAsync(dm, 0, cap * sizeof(DevDoc), st));
+    SCHK(s, hipMemsetAsync(seen, 0, cap * 4, st));
+    if (s->cap_h) {
+        SCHK(s, hipMemcpyAsync(rd, s->res_docs, s->cap_h * sizeof(hm_doc_result), hipMemcpyDeviceToDevice, st));
+        SCHK(s, hipMemcpyAsync(dm, s->dm, s->cap_h * sizeof(DevDoc), hipMemcpyDeviceToDevice, st));
+        SCHK(s, hipMemcpyAsync(seen, s->seen, s->cap_h * 4, hipMemcpyDeviceToDevice, st));
+    }
     uint32_t **tabs[5] = {&s->clock, &s->back_clock, &s->heads, &s->min_clock, &s->stored};
     uint32_t *nt[5];
     for (int i = 0; i < 5; i++) {
@@ -141,7 +177,9 @@ int ensure_handles(hm_store *s, size_t need) {
     }
     SCHK(s, hipStreamSynchronize(st));
     if (s->res_docs) (void)hipFree(s->res_docs);
-    s->res_docs = rd;
+    if (s->dm) (void)hipFree(s->dm);
+    if (s->seen) (void)hipFree(s->seen);
+    s->res_docs = rd; s->dm = dm; s->seen = seen;
     for (int i = 0; i < 5; i++) { if (*tabs[i]) (void)hipFree(*tabs[i]); *tabs[i] = nt[i]; }
     s->cap_h = cap;
     return HM_OK;
@@ -163,102 +201,72 @@ struct PhaseTimer {
     }
 };
 
-// f(lo, hi, t) over [0, n) split in contiguous ranges; host threads for big submits only
-// (the box's CPU share is 16 threads)
-template <typename F> uint32_t par_for(uint32_t n, F &&f) {
-    const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
-    const uint32_t T = n >= 65536 ? std::min<uint32_t>(16, hw) : 1;
-    if (T == 1) { f(0u, n, 0u); return 1; }
-    std::vector<std::thread> th;
-    th.reserve(T);
-    for (uint32_t t = 0; t < T; t++)
-        th.emplace_back([&f, n, t, T] { f((uint32_t)((uint64_t)n * t / T), (uint32_t)((uint64_t)n * (t + 1) / T), t); });
-    for (auto &x : th) x.join();
-    return T;
-}
-
-struct Plan {
-    std::vector<AppendDesc> descs;      // documents touched by the append kernel
-    std::vector<uint32_t> merge;        // handles to re-merge (batch rows first)
-};
-
-// Staged batch layout on the device: [changes][deps][ops][descs][remap][launch docs][handles]
+// Staged batch layout on the device: [changes][deps][ops][docs][handles][remap][gather][bail]
 struct StageLayout {
-    size_t o_ch, o_dp, o_op, o_desc, o_remap, o_docs, o_hand, o_gather, o_bail, total;
+    size_t o_ch, o_dp, o_op, o_docs, o_hand, o_remap, o_gather, o_bail, total;
 };
-StageLayout layout(size_t nc, size_t nd, size_t no, size_t ndesc, size_t nremap, size_t nmerge, size_t ngather, uint32_t S,
-                   size_t ninc = 0) {
+StageLayout layout(size_t nc, size_t nd, size_t no, size_t n, size_t nremap, uint32_t S) {
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     StageLayout L;
     size_t o = 0;
     L.o_ch = o; o += al(nc * sizeof(hm_change_row) + 1);
     L.o_dp = o; o += al(nd * sizeof(hm_dep_row) + 1);
     L.o_op = o; o += al(no * sizeof(hm_op_row) + 1);
-    L.o_desc = o; o += al(ndesc * sizeof(AppendDesc) + 1);
+    L.o_docs = o; o += al(n * sizeof(hm_doc_row) + 1);
+    L.o_hand = o; o += al(n * 4 + 1);
     L.o_remap = o; o += al(nremap + 1);
-    L.o_docs = o; o += al(nmerge * sizeof(hm_doc_row) + 1);
-    L.o_hand = o; o += al(nmerge * 4 + 1);
-    L.o_gather = o; o += al(ngather * (sizeof(hm_doc_result) + 3 * 4 * (size_t)S) + 1);
-    L.o_bail = o; o += al(4 * (ninc + 1));
+    L.o_gather = o; o += al(n * (sizeof(hm_doc_result) + 3 * 4 * (size_t)S) + 1);
+    L.o_bail = o; o += al(4 * (n + 1));
     L.total = o;
     return L;
 }
 
-// Launch the merge kernels over `handles` (their current metas) on the engine stream.
-int launch_store_merge(hm_store *s, const std::vector<uint32_t> &handles, uint8_t *dev_docs, uint32_t *dev_handles) {
-    if (handles.empty()) return HM_OK;
+// Re-merge the `n` documents listed (handles, device) on the engine stream: their launch rows
+// built on the device from their metas, the launch hints read back.
+int launch_list_merge(hm_store *s, const uint32_t *dev_list, uint32_t n) {
+    if (!n) return HM_OK;
     hipStream_t st = hm_engine_stream(s->e);
-    std::vector<hm_doc_row> rows(handles.size());
+    int rc;
+    if ((rc = ensure_buf(s, s->rows, n))) return rc;
+    if ((rc = reset_stats(s))) return rc;
+    SCHK(s, hm_launch_doc_rows(dev_list, n, s->dm, s->rows.p, s->st, st));
+    rc = HM_OK;
+    const PlanStats P = read_stats(s, &rc);
+    if (rc) return rc;
     hm_batch b = {};
     b.a_stride = s->S;
-    size_t tc = 0, td = 0, to = 0, tr = 0;
-    for (size_t i = 0; i < handles.size(); i++) {
-        const DocMeta &m = s->docs[handles[i]];
-        hm_doc_row &r = rows[i];
-        r = hm_doc_row{};
-        r.change_off = m.c.off; r.n_changes = m.n_c; r.dep_off = m.d.off; r.n_deps = m.n_d;
-        r.op_off = m.o.off; r.n_ops = m.n_o; r.reg_off = m.r.off; r.n_regs = m.n_r;
-        r.n_objs = m.n_objs; r.n_actors = (uint16_t)m.n_actors; r.flags = m.flags;
-        b.max_changes = std::max(b.max_changes, m.n_c); b.max_ops = std::max(b.max_ops, m.n_o);
-        b.max_regs = std::max(b.max_regs, m.n_r); b.max_objs = std::max(b.max_objs, m.n_objs);
-        b.max_deps = std::max(b.max_deps, m.n_d); b.doc_flags |= m.flags;
-        tc += m.n_c; td += m.n_d; to += m.n_o; tr += m.n_r;
-    }
-    // the large kernel's scratch bound reads the launch totals
-    b.n_docs = (uint32_t)handles.size(); b.n_changes = (uint32_t)tc; b.n_deps = (uint32_t)td;
-    b.n_ops = (uint32_t)to; b.n_regs = (uint32_t)tr;
+    b.n_docs = n;
+    b.n_changes = (uint32_t)std::min<unsigned long long>(P.tot_c, 0xFFFFFFFFull);
+    b.n_deps = (uint32_t)std::min<unsigned long long>(P.tot_d, 0xFFFFFFFFull);
+    b.n_ops = (uint32_t)std::min<unsigned long long>(P.tot_o, 0xFFFFFFFFull);
+    b.n_regs = (uint32_t)std::min<unsigned long long>(P.tot_r, 0xFFFFFFFFull);
+    b.max_changes = P.max_c; b.max_ops = P.max_o; b.max_regs = P.max_r; b.max_objs = P.max_objs; b.max_deps = P.max_d;
+    b.doc_flags = P.flags;
     if (!b.max_changes && !b.max_ops && !b.max_regs && !b.max_objs) b.max_objs = 1;   // device hints present
-    SCHK(s, hipMemcpyAsync(dev_docs, rows.data(), rows.size() * sizeof(hm_doc_row), hipMemcpyHostToDevice, st));
-    SCHK(s, hipMemcpyAsync(dev_handles, handles.data(), handles.size() * 4, hipMemcpyHostToDevice, st));
-    b.docs = (const hm_doc_row *)dev_docs;
+    b.docs = s->rows.p;
     b.changes = s->changes; b.deps = s->deps; b.ops = s->ops; b.min_clock = s->min_clock;
     hm_results o;
     o.docs = s->res_docs; o.clock = s->clock; o.back_clock = s->back_clock; o.heads = s->heads;
     o.hist = s->hist; o.all_deps = s->all_deps; o.regs = s->regs; o.surv = s->surv;
-    // the launch's host copies must outlive the async H2D copies: synchronise here
     const hm_extents ext = {(uint32_t)s->cap_c, (uint32_t)s->cap_d, (uint32_t)s->cap_o, (uint32_t)s->cap_r};
-    int rc = hm_engine_launch_merge(s->e, &b, &o, dev_handles, &ext);
+    rc = hm_engine_launch_merge(s->e, &b, &o, dev_list, &ext);
     SCHK(s, hipStreamSynchronize(st));
     return rc;
 }
 
-// Allocate a segment of `need` rows from an arena; false if the arena is full.
-bool seg_alloc(size_t &used, size_t cap, uint32_t need, Seg &out) {
-    const uint32_t c = pow2ceil(std::max<uint32_t>(need, 16));
-    if (used + c > cap) return false;
-    out.off = (uint32_t)used; out.cap = c;
-    used += c;
-    return true;
-}
-
 // Rebuild every arena larger and compact all documents into it; every document is
 // re-merged (its outputs live in the arenas too).  `extra` = rows the caller is about
-// to append per space, so the new arenas fit them.
+// to append per space, so the new arenas fit them.  The metas come to the host for it.
 int compact(hm_store *s, size_t extra_c, size_t extra_d, size_t extra_o, size_t extra_r) {
     hipStream_t st = hm_engine_stream(s->e);
-    const uint32_t S = s->S;
+    const uint32_t S = s->S, n = s->n_handles;
+    std::vector<DevDoc> old(n);
+    if (n) {
+        SCHK(s, hipMemcpyAsync(old.data(), s->dm, (size_t)n * sizeof(DevDoc), hipMemcpyDeviceToHost, st));
+        SCHK(s, hipStreamSynchronize(st));
+    }
     size_t live_c = extra_c, live_d = extra_d, live_o = extra_o, live_r = extra_r;
-    for (auto &m : s->docs) {
+    for (auto &m : old) {
         live_c += pow2ceil(std::max<uint32_t>(m.n_c, 16)); live_d += pow2ceil(std::max<uint32_t>(m.n_d, 16));
         live_o += pow2ceil(std::max<uint32_t>(m.n_o, 16)); live_r += pow2ceil(std::max<uint32_t>(m.n_r, 16));
     }
@@ -271,44 +279,48 @@ int compact(hm_store *s, size_t extra_c, size_t extra_d, size_t extra_o, size_t 
         (r = dev_alloc(s, &rg, nr)))
         return r;
     // relocate every document (old rows only; no new rows, no remap)
-    std::vector<AppendDesc> descs;
-    std::vector<uint32_t> all;
-    size_t uc = 0, ud = 0, uo = 0, ur = 0;
-    std::vector<DocMeta> nm = s->docs;
-    for (uint32_t h = 0; h < s->docs.size(); h++) {
-        DocMeta &m = nm[h];
-        const DocMeta &o = s->docs[h];
-        seg_alloc(uc, nc, m.n_c, m.c); seg_alloc(ud, nd, m.n_d, m.d);
-        seg_alloc(uo, no, m.n_o, m.o); seg_alloc(ur, nr, m.n_r, m.r);
+    std::vector<AppendDesc> descs(n);
+    std::vector<DevDoc> nm = old;
+    std::vector<uint32_t> all(n);
+    uint64_t uc = 0, ud = 0, uo = 0, ur = 0;
+    auto seg = [](uint64_t &used, uint32_t need, uint32_t &off, uint32_t &cap) {
+        cap = pow2ceil(std::max<uint32_t>(need, 16));
+        off = (uint32_t)used;
+        used += cap;
+    };
+    for (uint32_t h = 0; h < n; h++) {
+        DevDoc &m = nm[h];
+        const DevDoc &o = old[h];
+        seg(uc, m.n_c, m.c_off, m.c_cap); seg(ud, m.n_d, m.d_off, m.d_cap);
+        seg(uo, m.n_o, m.o_off, m.o_cap); seg(ur, m.n_r, m.r_off, m.r_cap);
         AppendDesc D = {};
         D.handle = h;
-        D.src_c = o.c.off; D.dst_c = m.c.off; D.n_old_c = o.n_c;
-        D.src_d = o.d.off; D.dst_d = m.d.off; D.n_old_d = o.n_d;
-        D.src_o = o.o.off; D.dst_o = m.o.off; D.n_old_o = o.n_o;
+        D.src_c = o.c_off; D.dst_c = m.c_off; D.n_old_c = o.n_c;
+        D.src_d = o.d_off; D.dst_d = m.d_off; D.n_old_d = o.n_d;
+        D.src_o = o.o_off; D.dst_o = m.o_off; D.n_old_o = o.n_o;
         D.remap_row = 0xFFFFFFFFu;
-        descs.push_back(D);
-        all.push_back(h);
+        descs[h] = D;
+        all[h] = h;
     }
     StoreArenas src = {s->changes, s->deps, s->ops, s->min_clock, s->stored};
     StoreArenas dst = {ch, dp, op, s->min_clock, s->stored};
-    if (!descs.empty()) {
-        const StageLayout L = layout(0, 0, 0, descs.size(), 0, all.size(), 0, S);
-        if ((r = ensure_stage(s, L.total))) return r;
-        SCHK(s, hipMemcpyAsync(s->stage.p + L.o_desc, descs.data(), descs.size() * sizeof(AppendDesc), hipMemcpyHostToDevice, st));
-        SCHK(s, hm_launch_append((const AppendDesc *)(s->stage.p + L.o_desc), (uint32_t)descs.size(), src, dst,
-                                 nullptr, nullptr, nullptr, nullptr, S, st));
+    if (n) {
+        if ((r = ensure_buf(s, s->descs, n))) return r;
+        SCHK(s, hipMemcpyAsync(s->descs.p, descs.data(), (size_t)n * sizeof(AppendDesc), hipMemcpyHostToDevice, st));
+        SCHK(s, hm_launch_append(s->descs.p, n, src, dst, nullptr, nullptr, nullptr, nullptr, S, st));
+        SCHK(s, hipMemcpyAsync(s->dm, nm.data(), (size_t)n * sizeof(DevDoc), hipMemcpyHostToDevice, st));
         SCHK(s, hipStreamSynchronize(st));
     }
     (void)hipFree(s->changes); (void)hipFree(s->hist); (void)hipFree(s->all_deps); (void)hipFree(s->deps);
     (void)hipFree(s->ops); (void)hipFree(s->surv); (void)hipFree(s->regs);
     s->changes = ch; s->hist = hi; s->all_deps = ad; s->deps = dp; s->ops = op; s->surv = sv; s->regs = rg;
     s->cap_c = nc; s->cap_d = nd; s->cap_o = no; s->cap_r = nr;
-    s->used_c = uc; s->used_d = ud; s->used_o = uo; s->used_r = ur;
-    s->docs = nm;
-    if (all.empty()) return HM_OK;
-    const StageLayout L = layout(0, 0, 0, 0, 0, all.size(), 0, S);
-    if ((r = ensure_stage(s, L.total))) return r;
-    return launch_store_merge(s, all, s->stage.p + L.o_docs, (uint32_t *)(s->stage.p + L.o_hand));
+    const unsigned long long bump[4] = {uc, ud, uo, ur};
+    SCHK(s, hipMemcpyAsync(s->st->bump, bump, sizeof bump, hipMemcpyHostToDevice, st));
+    if (!n) { SCHK(s, hipStreamSynchronize(st)); return HM_OK; }
+    if ((r = ensure_buf(s, s->list, n))) return r;
+    SCHK(s, hipMemcpyAsync(s->list.p, all.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
+    return launch_list_merge(s, s->list.p, n);
 }
 
 }  // namespace
@@ -324,7 +336,9 @@ int hm_store_create(hm_engine *e, const hm_store_config *cfg, hm_store **out) {
     if (!s) return HM_ERR_NOMEM;
     s->e = e; s->S = S;
     if (hipSetDevice(hm_engine_device(e)) != hipSuccess) { delete s; return HM_ERR_DEVICE; }
-    int r = compact(s, 0, 0, 0, 0);
+    int r = dev_alloc(s, &s->st, 1);
+    if (r == HM_OK && hipMemset(s->st, 0, sizeof(PlanStats)) != hipSuccess) r = HM_ERR_DEVICE;
+    if (r == HM_OK) r = compact(s, 0, 0, 0, 0);
     if (r == HM_OK) r = ensure_handles(s, 1024);
     if (r != HM_OK) { hm_store_destroy(s); return r; }
     *out = s;
@@ -335,45 +349,33 @@ void hm_store_destroy(hm_store *s) {
     if (!s) return;
     (void)hipStreamSynchronize(hm_engine_stream(s->e));
     void *bufs[] = {s->changes, s->hist, s->all_deps, s->deps, s->ops, s->surv, s->regs, s->res_docs, s->clock,
-                    s->back_clock, s->heads, s->min_clock, s->stored, s->stage.p};
+                    s->back_clock, s->heads, s->min_clock, s->stored, s->stage.p, s->dm, s->seen, s->plan.p, s->descs.p,
+                    s->bdescs.p, s->list.p, s->blist.p, s->remap.p, s->inv.p, s->rows.p, s->st};
     for (void *b : bufs) if (b) (void)hipFree(b);
     delete s;
 }
 
-int hm_doc_open(hm_store *s, uint32_t *out_doc) {
-    if (!s || !out_doc) return HM_ERR_INVALID;
-    try {
-        if (s->pending) return hm_engine_fail(s->e, HM_ERR_INVALID, "hm_doc_open while a batch is in flight");
-        int r = ensure_handles(s, s->docs.size() + 1);
-        if (r) return r;
-        DocMeta m;
-        m.last.err_change = HM_NONE; m.last.err_op = HM_NONE;
-        // the new document's merged state is Backend.init(): its result row, written on the
-        // engine stream (ordered before any submit; the reads below synchronise the stream)
-        const uint32_t h = (uint32_t)s->docs.size();
-        s->docs.push_back(m);
-        hipStream_t st = hm_engine_stream(s->e);
-        SCHK(s, hipMemsetAsync(s->res_docs + h, 0, sizeof(hm_doc_result), st));
-        SCHK(s, hipMemsetAsync(&s->res_docs[h].err_change, 0xFF, 2 * sizeof(uint32_t), st));
-        *out_doc = h;
-        return HM_OK;
-    } catch (...) {
-        return HM_ERR_NOMEM;
-    }
-}
+int hm_doc_open(hm_store *s, uint32_t *out_doc) { return hm_doc_open_n(s, 1, out_doc); }
 
 int hm_doc_open_n(hm_store *s, uint32_t n, uint32_t *out_first) {
     if (!s || !out_first) return HM_ERR_INVALID;
     try {
-        if (s->pending) return hm_engine_fail(s->e, HM_ERR_INVALID, "hm_doc_open_n while a batch is in flight");
-        const uint32_t h0 = (uint32_t)s->docs.size();
+        if (s->pending) return hm_engine_fail(s->e, HM_ERR_INVALID, "hm_doc_open while a batch is in flight");
+        const uint32_t h0 = s->n_handles;
         int r = ensure_handles(s, (size_t)h0 + n);
         if (r) return r;
-        DocMeta m;
-        m.last.err_change = HM_NONE; m.last.err_op = HM_NONE;
-        s->docs.resize((size_t)h0 + n, m);
-        std::vector<hm_doc_result> rows(n, m.last);
-        if (n) SCHK(s, hipMemcpy(s->res_docs + h0, rows.data(), (size_t)n * sizeof(hm_doc_result), hipMemcpyHostToDevice));
+        // Backend.init(): an empty log (ROOT only) and its result row, written on the engine
+        // stream (ordered before any submit; the reads below synchronise the stream)
+        hipStream_t st = hm_engine_stream(s->e);
+        SCHK(s, hm_launch_init_docs(s->dm, h0, n, st));
+        if (n) {
+            SCHK(s, hipMemsetAsync(s->res_docs + h0, 0, (size_t)n * sizeof(hm_doc_result), st));
+            std::vector<hm_doc_result> rows(n);
+            for (auto &x : rows) { x = hm_doc_result{}; x.err_change = HM_NONE; x.err_op = HM_NONE; }
+            SCHK(s, hipMemcpyAsync(s->res_docs + h0, rows.data(), (size_t)n * sizeof(hm_doc_result), hipMemcpyHostToDevice, st));
+            SCHK(s, hipStreamSynchronize(st));
+        }
+        s->n_handles = h0 + n;
         *out_first = h0;
         return HM_OK;
     } catch (...) {
@@ -391,227 +393,93 @@ int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
         SCHK(s, hipSetDevice(hm_engine_device(s->e)));
         hipStream_t st = hm_engine_stream(s->e);
         PhaseTimer T(st);
-        // validate rows (threads over documents; the first error wins)
-        std::vector<uint8_t> seen(s->docs.size(), 0);
-        const char *bad = nullptr;
-        auto fail_with = [&](const char *m) { const char *expect = nullptr; __atomic_compare_exchange_n(&bad, &expect, m, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED); };
-        par_for(n, [&](uint32_t lo, uint32_t hi, uint32_t) {
-            for (uint32_t i = lo; i < hi; i++) {
-                const uint32_t h = doc_handles[i];
-                if (h >= s->docs.size() || __atomic_exchange_n(&seen[h], (uint8_t)1, __ATOMIC_RELAXED)) {
-                    fail_with("bad or repeated document handle"); return;
-                }
-                const hm_doc_row &r = b->docs[i];
-                const DocMeta &m = s->docs[h];
-                if ((uint64_t)r.change_off + r.n_changes > b->n_changes || (uint64_t)r.dep_off + r.n_deps > b->n_deps ||
-                    (uint64_t)r.op_off + r.n_ops > b->n_ops) { fail_with("document rows outside the batch tables"); return; }
-                if (r.n_actors > S || r.n_actors < m.n_actors || r.n_regs < m.n_r || r.n_objs < m.n_objs || r.n_objs == 0) {
-                    fail_with("document totals must cover the existing log (and n_actors <= a_stride)"); return;
-                }
-                // every change row must lie inside its document's slice of the batch tables
-                for (uint32_t c = r.change_off; c < r.change_off + r.n_changes; c++) {
-                    const hm_change_row &cr = b->changes[c];
-                    if ((uint64_t)cr.dep_off < r.dep_off || (uint64_t)cr.dep_off + cr.n_deps > (uint64_t)r.dep_off + r.n_deps ||
-                        (uint64_t)cr.op_first < r.op_off || (uint64_t)cr.op_first + cr.n_ops > (uint64_t)r.op_off + r.n_ops) {
-                        fail_with("change rows outside their document's deps/ops"); return;
-                    }
-                }
-                // the actor re-rank of the existing rows: a permutation into the new ranks.  Checked
-                // here, before any document meta or arena pointer moves (a failure leaves the store as it was)
-                if (actor_remap) {
-                    const uint8_t *mp = actor_remap + (size_t)i * S;
-                    uint64_t used = 0;
-                    for (uint32_t a = 0; a < m.n_actors; a++) {
-                        if (mp[a] >= r.n_actors || ((used >> mp[a]) & 1)) {
-                            fail_with("actor remap is not a permutation into the new ranks"); return;
-                        }
-                        used |= 1ull << mp[a];
-                    }
-                }
-            }
-        });
-        if (bad) return hm_engine_fail(s->e, HM_ERR_INVALID, bad);
-        T.mark("validate");
-        // plan segments: a document outgrowing a segment moves to a fresh one at the arena's end;
-        // the arenas are compacted first when the worst case would not fit
-        {
-            std::vector<size_t> part(4 * 16, 0);
-            par_for(n, [&](uint32_t lo, uint32_t hi, uint32_t t) {
-                size_t c = 0, d = 0, o = 0, g = 0;
-                for (uint32_t i = lo; i < hi; i++) {
-                    const DocMeta &m = s->docs[doc_handles[i]];
-                    c += pow2ceil(std::max<uint32_t>(m.n_c + b->docs[i].n_changes, 16));
-                    d += pow2ceil(std::max<uint32_t>(m.n_d + b->docs[i].n_deps, 16));
-                    o += pow2ceil(std::max<uint32_t>(m.n_o + b->docs[i].n_ops, 16));
-                    g += pow2ceil(std::max<uint32_t>(b->docs[i].n_regs, 16));
-                }
-                part[4 * t] = c; part[4 * t + 1] = d; part[4 * t + 2] = o; part[4 * t + 3] = g;
-            });
-            size_t need_c = 0, need_d = 0, need_o = 0, need_r = 0;
-            for (uint32_t t = 0; t < 16; t++) { need_c += part[4 * t]; need_d += part[4 * t + 1]; need_o += part[4 * t + 2]; need_r += part[4 * t + 3]; }
-            if (s->used_c + need_c > s->cap_c || s->used_d + need_d > s->cap_d || s->used_o + need_o > s->cap_o ||
-                s->used_r + need_r > s->cap_r) {
-                int r = compact(s, need_c, need_d, need_o, need_r);
-                if (r) return r;
-            }
-        }
-        T.mark("plan: sizes");
-        s->p_old.resize(n);
-        s->p_inv_row.resize(n);
-        s->p_inv.clear();
-        s->p_handles.assign(doc_handles, doc_handles + n);
-        s->descs.resize(n);
-        std::vector<AppendDesc> &descs = s->descs;
-        uint32_t n_remap = 0;
-        std::vector<uint8_t> remap_rows;
-        // re-ranked documents (rare): their remap rows, in batch order
-        if (actor_remap) {
-            for (uint32_t i = 0; i < n; i++) {
-                const DocMeta &m = s->docs[doc_handles[i]];
-                const uint8_t *mp = actor_remap + (size_t)i * S;
-                bool ident = true;
-                for (uint32_t a = 0; a < m.n_actors; a++) if (mp[a] != a) ident = false;
-                s->p_inv_row[i] = -1;
-                if (ident) continue;
-                const size_t at = remap_rows.size();
-                remap_rows.resize(at + S, 0xFF);
-                s->p_inv_row[i] = (int32_t)s->p_inv.size();
-                s->p_inv.resize(s->p_inv.size() + S, 0xFF);
-                uint8_t *inv = s->p_inv.data() + s->p_inv_row[i];
-                for (uint32_t a = 0; a < m.n_actors; a++) { remap_rows[at + a] = mp[a]; inv[mp[a]] = (uint8_t)a; }   // validated above
-                descs[i].remap_row = n_remap++;
-            }
-        }
-        // new segments: sizes per document (0 = fits), then arena offsets by a prefix over the
-        // batch (threads sum their ranges, one serial pass over the partial sums)
-        s->grow.resize(4 * (size_t)n);
-        std::vector<uint32_t> &grow = s->grow;
-        std::vector<size_t> base(4 * 17, 0);
-        const uint32_t TT = par_for(n, [&](uint32_t lo, uint32_t hi, uint32_t t) {
-            size_t acc[4] = {0, 0, 0, 0};
-            for (uint32_t i = lo; i < hi; i++) {
-                const DocMeta &m = s->docs[doc_handles[i]];
-                const hm_doc_row &r = b->docs[i];
-                uint32_t *g = &grow[4 * (size_t)i];
-                g[0] = g[1] = g[2] = g[3] = 0;
-                if (m.n_c + r.n_changes > m.c.cap) g[0] = pow2ceil(std::max<uint32_t>(m.n_c + r.n_changes, 16));
-                if (m.n_d + r.n_deps > m.d.cap) g[1] = pow2ceil(std::max<uint32_t>(m.n_d + r.n_deps, 16));
-                if (m.n_o + r.n_ops > m.o.cap) g[2] = pow2ceil(std::max<uint32_t>(m.n_o + r.n_ops, 16));
-                if (r.n_regs > m.r.cap) g[3] = pow2ceil(std::max<uint32_t>(r.n_regs, 16));
-                for (int k = 0; k < 4; k++) acc[k] += g[k];
-            }
-            for (int k = 0; k < 4; k++) base[4 * (t + 1) + k] = acc[k];
-        });
-        T.mark("plan: grow");
-        base[0] = s->used_c; base[1] = s->used_d; base[2] = s->used_o; base[3] = s->used_r;
-        for (uint32_t t = 1; t <= TT; t++) for (int k = 0; k < 4; k++) base[4 * t + k] += base[4 * (t - 1) + k];
-        s->used_c = base[4 * TT]; s->used_d = base[4 * TT + 1]; s->used_o = base[4 * TT + 2]; s->used_r = base[4 * TT + 3];
-        // route: a document whose resident state is clean (last merge ok, nothing queued, no
-        // re-rank) and whose new rows fit the incremental tiles is applied by inc_apply_kernel;
-        // the rest re-merge their whole log (DocBackend.applyRemoteChanges either way)
-        struct Part { std::vector<uint32_t> cold; uint32_t n_inc = 0, mx[6] = {0, 0, 0, 0, 0, 0}; };
-        std::vector<Part> parts(16);
-        par_for(n, [&](uint32_t lo, uint32_t hi, uint32_t t) {
-            size_t at[4] = {base[4 * t], base[4 * t + 1], base[4 * t + 2], base[4 * t + 3]};
-            Part P;                                                   // thread-local (no false sharing)
-            for (uint32_t i = lo; i < hi; i++) {
-                const uint32_t h = doc_handles[i];
-                DocMeta &m = s->docs[h];
-                const hm_store::OldMeta o = {m.n_c, m.n_d, m.n_o, m.n_r, m.n_objs, (uint16_t)m.n_actors, m.flags};
-                s->p_old[i] = o;
-                const hm_doc_result last = m.last;
-                const hm_doc_row &r = b->docs[i];
-                AppendDesc &D = descs[i];
-                const uint32_t remap_row = D.remap_row;
-                D = AppendDesc{};
-                D.handle = h;
-                D.src_c = m.c.off; D.n_old_c = m.n_c; D.new_c = r.change_off; D.n_new_c = r.n_changes;
-                D.src_d = m.d.off; D.n_old_d = m.n_d; D.new_d = r.dep_off; D.n_new_d = r.n_deps;
-                D.src_o = m.o.off; D.n_old_o = m.n_o; D.new_o = r.op_off; D.n_new_o = r.n_ops;
-                D.src_r = m.r.off; D.n_old_r = m.n_r;
-                const uint32_t *g = &grow[4 * (size_t)i];
-                Seg *segs[4] = {&m.c, &m.d, &m.o, &m.r};
-                for (int k = 0; k < 4; k++) if (g[k]) { segs[k]->off = (uint32_t)at[k]; segs[k]->cap = g[k]; at[k] += g[k]; }
-                D.dst_c = m.c.off; D.dst_d = m.d.off; D.dst_o = m.o.off; D.dst_r = m.r.off;
-                if (!actor_remap) s->p_inv_row[i] = -1;
-                D.remap_row = actor_remap && s->p_inv_row[i] >= 0 ? remap_row : 0xFFFFFFFFu;
-                const bool reranked = D.remap_row != 0xFFFFFFFFu;
-                m.n_c += r.n_changes; m.n_d += r.n_deps; m.n_o += r.n_ops;
-                m.n_r = r.n_regs; m.n_objs = r.n_objs; m.n_actors = r.n_actors; m.flags |= r.flags;
-                D.n_r = m.n_r; D.n_actors = (uint16_t)m.n_actors; D.n_objs = m.n_objs;
-                const uint32_t tgt = r.n_deps + r.n_changes;            // fold steps: deps + own predecessor
-                const bool inc = s->incremental && last.status == HM_OK && last.n_queued == 0 && !reranked &&
-                                 r.n_changes > 0 && r.n_changes <= HM_INC_MAX_NEW_C && r.n_ops <= HM_INC_MAX_NEW_O &&
-                                 tgt <= HM_INC_MAX_TGT && m.n_r <= HM_INC_MAX_REGS && last.n_surv <= HM_INC_MAX_SURV &&
-                                 o.n_r <= m.n_r && m.n_actors <= S && !((o.flags | r.flags) & HM_DOC_HAS_LISTS);
-                if (!inc) { P.cold.push_back(h); continue; }
-                D.inc = 1;
-                P.n_inc++;
-                const uint32_t v[6] = {r.n_changes, tgt, std::min<uint32_t>(o.n_c, HM_INC_MAX_STAGE), m.n_r, last.n_surv,
-                                       std::min<uint32_t>(r.n_ops, HM_INC_SLOTS)};
-                for (int k = 0; k < 6; k++) P.mx[k] = std::max(P.mx[k], v[k]);
-            }
-            parts[t] = std::move(P);
-        });
-        T.mark("plan: route");
-        std::vector<uint32_t> cold;
-        uint32_t n_inc = 0, mx[6] = {0, 0, 0, 0, 0, 0};
-        for (auto &P : parts) {
-            cold.insert(cold.end(), P.cold.begin(), P.cold.end());
-            n_inc += P.n_inc;
-            for (int k = 0; k < 6; k++) mx[k] = std::max(mx[k], P.mx[k]);
-        }
-        const uint32_t mx_new_c = mx[0], mx_tgt = mx[1], mx_stage = mx[2], mx_regs = mx[3], mx_surv = mx[4], mx_slots = mx[5];
-        T.mark("plan+route");
-        // stage and launch: append, merge, gather
-        const StageLayout L = layout(b->n_changes, b->n_deps, b->n_ops, n, remap_rows.size(), n, n, S, n_inc ? n : 0);
-        int rc = ensure_stage(s, L.total);
-        if (rc) return rc;
+        int rc;
+        // stage the batch (its tables, rows, handles and remap) on the device
+        const size_t nremap = actor_remap ? (size_t)n * S : 0;
+        const StageLayout L = layout(b->n_changes, b->n_deps, b->n_ops, n, nremap, S);
+        if ((rc = ensure_stage(s, L.total)) || (rc = ensure_buf(s, s->plan, n)) || (rc = ensure_buf(s, s->descs, n)) ||
+            (rc = ensure_buf(s, s->list, n)))
+            return rc;
         uint8_t *sp = s->stage.p;
         if (b->n_changes) SCHK(s, hipMemcpyAsync(sp + L.o_ch, b->changes, b->n_changes * sizeof(hm_change_row), hipMemcpyHostToDevice, st));
         if (b->n_deps) SCHK(s, hipMemcpyAsync(sp + L.o_dp, b->deps, b->n_deps * sizeof(hm_dep_row), hipMemcpyHostToDevice, st));
         if (b->n_ops) SCHK(s, hipMemcpyAsync(sp + L.o_op, b->ops, b->n_ops * sizeof(hm_op_row), hipMemcpyHostToDevice, st));
-        if (n) SCHK(s, hipMemcpyAsync(sp + L.o_desc, descs.data(), n * sizeof(AppendDesc), hipMemcpyHostToDevice, st));
+        if (n) {
+            SCHK(s, hipMemcpyAsync(sp + L.o_docs, b->docs, (size_t)n * sizeof(hm_doc_row), hipMemcpyHostToDevice, st));
+            SCHK(s, hipMemcpyAsync(sp + L.o_hand, doc_handles, (size_t)n * 4, hipMemcpyHostToDevice, st));
+        }
+        if (nremap) SCHK(s, hipMemcpyAsync(sp + L.o_remap, actor_remap, nremap, hipMemcpyHostToDevice, st));
         T.mark("stage: h2d");
-        if (!remap_rows.empty()) SCHK(s, hipMemcpyAsync(sp + L.o_remap, remap_rows.data(), remap_rows.size(), hipMemcpyHostToDevice, st));
+        PlanArgs A;
+        A.docs = (const hm_doc_row *)(sp + L.o_docs); A.changes = (const hm_change_row *)(sp + L.o_ch);
+        A.handles = (const uint32_t *)(sp + L.o_hand); A.remap = nremap ? sp + L.o_remap : nullptr;
+        A.n = n; A.n_changes = b->n_changes; A.n_deps = b->n_deps; A.n_ops = b->n_ops; A.n_handles = s->n_handles;
+        A.S = S; A.stamp = ++s->stamp ? s->stamp : ++s->stamp; A.incremental = s->incremental ? 1u : 0u;
+        A.dm = s->dm; A.res_docs = s->res_docs; A.seen = s->seen; A.plan = s->plan.p; A.descs = s->descs.p;
+        A.list = s->list.p; A.st = s->st;
+        // plan: checks, growth, routes (nothing in the store changes)
+        if ((rc = reset_stats(s))) return rc;
+        SCHK(s, hm_launch_plan(A, st));
+        rc = HM_OK;
+        PlanStats P = read_stats(s, &rc);
+        if (rc) return rc;
+        T.mark("plan");
+        if (P.err) {
+            const char *why = (P.err & HM_PLAN_BAD_HANDLE) || (P.err & HM_PLAN_REPEATED) ? "bad or repeated document handle"
+                            : (P.err & HM_PLAN_ROWS) ? "document rows outside the batch tables"
+                            : (P.err & HM_PLAN_TOTALS) ? "document totals must cover the existing log (and n_actors <= a_stride)"
+                            : (P.err & HM_PLAN_CHANGE_ROWS) ? "change rows outside their document's deps/ops"
+                            : "actor remap is not a permutation into the new ranks";
+            return hm_engine_fail(s->e, HM_ERR_INVALID, why);
+        }
+        if (P.bump[0] + P.need[0] > s->cap_c || P.bump[1] + P.need[1] > s->cap_d || P.bump[2] + P.need[2] > s->cap_o ||
+            P.bump[3] + P.need[3] > s->cap_r) {
+            // the arenas cannot take the growth: compact (every document re-merged), then plan again
+            if ((rc = compact(s, P.need[0], P.need[1], P.need[2], P.need[3]))) return rc;
+            A.stamp = ++s->stamp ? s->stamp : ++s->stamp;
+            A.dm = s->dm; A.descs = s->descs.p; A.list = s->list.p;     // (compaction may have regrown them)
+            if ((rc = reset_stats(s))) return rc;
+            SCHK(s, hm_launch_plan(A, st));
+            P = read_stats(s, &rc);
+            if (rc) return rc;
+            if (P.err) return hm_engine_fail(s->e, HM_ERR_INVALID, "submit plan failed after compaction");
+            T.mark("compact+plan");
+        }
+        // segments, descriptors, totals, re-merge list; append; incremental apply
+        SCHK(s, hm_launch_alloc(A, st));
         StoreArenas ar = {s->changes, s->deps, s->ops, s->min_clock, s->stored};
-        SCHK(s, hm_launch_append((const AppendDesc *)(sp + L.o_desc), n, ar, ar, (const hm_change_row *)(sp + L.o_ch),
-                                 (const hm_dep_row *)(sp + L.o_dp), (const hm_op_row *)(sp + L.o_op),
-                                 remap_rows.empty() ? nullptr : sp + L.o_remap, S, st));
-        T.mark("stage+append");
-        if (n_inc) {
-            const IncDims M = hm_inc_dims(S, mx_new_c, mx_tgt, mx_stage, mx_regs, mx_surv, mx_slots);
-            IncArenas A = {s->changes, s->deps, s->ops, s->hist, s->all_deps, s->regs, s->surv,
-                           s->res_docs, s->clock, s->back_clock, s->heads, s->min_clock};
-            SCHK(s, hm_launch_inc_apply((const AppendDesc *)(sp + L.o_desc), n, A, M, (uint32_t *)(sp + L.o_bail), st));
+        SCHK(s, hm_launch_append(s->descs.p, n, ar, ar, A.changes, (const hm_dep_row *)(sp + L.o_dp),
+                                 (const hm_op_row *)(sp + L.o_op), A.remap, S, st));
+        T.mark("alloc+append");
+        uint32_t *bail = (uint32_t *)(sp + L.o_bail);
+        SCHK(s, hipMemsetAsync(bail, 0, 4, st));
+        if (P.n_inc) {
+            const IncDims M = hm_inc_dims(S, P.mx[0], P.mx[1], P.mx[2], P.mx[3], P.mx[4], P.mx[5]);
+            IncArenas IA = {s->changes, s->deps, s->ops, s->hist, s->all_deps, s->regs, s->surv,
+                            s->res_docs, s->clock, s->back_clock, s->heads, s->min_clock};
+            SCHK(s, hm_launch_inc_apply(s->descs.p, n, IA, M, bail, st));
         }
         T.mark("incremental");
-        rc = launch_store_merge(s, cold, sp + L.o_docs, (uint32_t *)(sp + L.o_hand));
-        if (rc) return rc;
+        // the re-merge list: cold documents, then those the incremental kernel handed back
+        uint32_t counts[2] = {0, 0};
+        SCHK(s, hipMemcpyAsync(&counts[0], &s->st->n_cold, 4, hipMemcpyDeviceToHost, st));
+        SCHK(s, hipMemcpyAsync(&counts[1], bail, 4, hipMemcpyDeviceToHost, st));
+        SCHK(s, hipStreamSynchronize(st));
+        if (counts[1]) SCHK(s, hipMemcpyAsync(s->list.p + counts[0], bail + 1, (size_t)counts[1] * 4, hipMemcpyDeviceToDevice, st));
+        if ((rc = launch_list_merge(s, s->list.p, counts[0] + counts[1]))) return rc;
         T.mark("remerge");
-        s->st_inc = n_inc; s->st_cold = (uint32_t)cold.size(); s->st_bail = 0;
-        if (n_inc) {
-            // documents the incremental kernel handed back re-merge their whole log
-            uint32_t nb = 0;
-            SCHK(s, hipMemcpyAsync(&nb, sp + L.o_bail, 4, hipMemcpyDeviceToHost, st));
-            SCHK(s, hipStreamSynchronize(st));
-            std::vector<uint32_t> again(nb);
-            if (nb) {
-                SCHK(s, hipMemcpyAsync(again.data(), sp + L.o_bail + 4, (size_t)nb * 4, hipMemcpyDeviceToHost, st));
-                SCHK(s, hipStreamSynchronize(st));
-                std::sort(again.begin(), again.end());
-            }
-            s->st_bail = (uint32_t)again.size(); s->st_inc -= s->st_bail;
-            rc = launch_store_merge(s, again, sp + L.o_docs, (uint32_t *)(sp + L.o_hand));
-            if (rc) return rc;
-        }
-        T.mark("handed back");
-        // the merges above used the handle region for their own document lists
-        if (n) SCHK(s, hipMemcpyAsync(sp + L.o_hand, s->p_handles.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
-        SCHK(s, hm_launch_gather((const uint32_t *)(sp + L.o_hand), n, S, s->res_docs, s->clock, s->back_clock, s->heads,
-                                 sp + L.o_gather, st));
+        s->st_inc = P.n_inc - counts[1]; s->st_cold = counts[0]; s->st_bail = counts[1];
+        SCHK(s, hm_launch_gather(A.handles, n, S, s->res_docs, s->clock, s->back_clock, s->heads, sp + L.o_gather, st));
         s->p_gather_dev = sp + L.o_gather;
-        T.mark("gather+d2h");
+        s->p_handles_dev = (uint32_t *)(sp + L.o_hand);
+        s->p_handles.assign(doc_handles, doc_handles + n);
+        s->p_remap = nremap != 0;
+        if (nremap) {
+            // the rollback needs the remap rows after the staging area is reused
+            if ((rc = ensure_buf(s, s->remap, nremap))) return rc;
+            SCHK(s, hipMemcpyAsync(s->remap.p, sp + L.o_remap, nremap, hipMemcpyDeviceToDevice, st));
+        }
+        T.mark("gather");
         s->pending = true;
         s->pending_id = s->next_id++;
         if (out_batch_id) *out_batch_id = s->pending_id;
@@ -632,8 +500,6 @@ int hm_batch_wait(hm_store *s, uint64_t batch_id, hm_doc_result *out_docs, uint3
         // the batch stays in flight (pending) until this returns: copy-out and rollback below
         // still read and re-merge the store's documents
         struct Clear { std::atomic<bool> &p; ~Clear() { p.store(false); } } clear_pending{s->pending};
-        SCHK(s, hipStreamSynchronize(st));
-        T.mark("wait sync");
         const uint32_t n = (uint32_t)s->p_handles.size(), S = s->S;
         // results straight from the gathered device rows into the caller's arrays
         std::vector<hm_doc_result> tmp;
@@ -650,46 +516,26 @@ int hm_batch_wait(hm_store *s, uint64_t batch_id, hm_doc_result *out_docs, uint3
             SCHK(s, hipStreamSynchronize(st));
         }
         T.mark("wait copy-out");
-        // roll back documents whose merge threw (or left the envelope): the log returns to
-        // its previous length (rows stay where they are), ranks are re-ranked back, and the
-        // previous state is re-merged
-        std::vector<uint32_t> back;
-        std::vector<AppendDesc> descs;
-        std::vector<uint8_t> remap_rows;
-        uint32_t n_remap = 0;
-        for (uint32_t i = 0; i < n; i++) {
-            const uint32_t h = s->p_handles[i];
-            if (res[i].status == HM_OK) { s->docs[h].last = res[i]; continue; }
-            DocMeta &m = s->docs[h];
-            const hm_store::OldMeta &o = s->p_old[i];
-            AppendDesc D = {};
-            D.handle = h;
-            D.src_c = D.dst_c = m.c.off; D.n_old_c = o.n_c;
-            D.src_d = D.dst_d = m.d.off; D.n_old_d = o.n_d;
-            D.src_o = D.dst_o = m.o.off; D.n_old_o = o.n_o;
-            D.remap_row = 0xFFFFFFFFu;
-            if (s->p_inv_row[i] >= 0) {
-                D.remap_row = n_remap++;
-                const uint8_t *inv = s->p_inv.data() + s->p_inv_row[i];
-                remap_rows.insert(remap_rows.end(), inv, inv + S);
-            }
-            m.n_c = o.n_c; m.n_d = o.n_d; m.n_o = o.n_o; m.n_r = o.n_r; m.n_objs = o.n_objs;
-            m.n_actors = o.n_actors; m.flags = o.flags;
-            descs.push_back(D);
-            back.push_back(h);
-        }
-        if (!back.empty()) {
-            const StageLayout L = layout(0, 0, 0, descs.size(), remap_rows.size(), back.size(), 0, S);
-            int rc = ensure_stage(s, L.total);
-            if (rc) return rc;
-            uint8_t *sp = s->stage.p;
-            SCHK(s, hipMemcpyAsync(sp + L.o_desc, descs.data(), descs.size() * sizeof(AppendDesc), hipMemcpyHostToDevice, st));
-            if (!remap_rows.empty()) SCHK(s, hipMemcpyAsync(sp + L.o_remap, remap_rows.data(), remap_rows.size(), hipMemcpyHostToDevice, st));
+        // roll back documents whose merge threw (or left the envelope): the log returns to its
+        // previous length (rows stay where they are), ranks are re-ranked back, and the previous
+        // state is re-merged
+        bool any = false;
+        for (uint32_t i = 0; i < n && !any; i++) any = res[i].status != HM_OK;
+        if (any) {
+            int rc;
+            if ((rc = ensure_buf(s, s->bdescs, n)) || (rc = ensure_buf(s, s->blist, n)) ||
+                (s->p_remap && (rc = ensure_buf(s, s->inv, (size_t)n * S))))
+                return rc;
+            if ((rc = reset_stats(s))) return rc;
+            SCHK(s, hm_launch_rollback(s->p_handles_dev, n, s->res_docs, s->plan.p, s->p_remap ? s->remap.p : nullptr, S, s->dm,
+                                       s->bdescs.p, s->p_remap ? s->inv.p : nullptr, s->blist.p, s->st, st));
+            uint32_t nb = 0;
+            SCHK(s, hipMemcpyAsync(&nb, &s->st->n_back, 4, hipMemcpyDeviceToHost, st));
+            SCHK(s, hipStreamSynchronize(st));
             StoreArenas ar = {s->changes, s->deps, s->ops, s->min_clock, s->stored};
-            SCHK(s, hm_launch_append((const AppendDesc *)(sp + L.o_desc), (uint32_t)descs.size(), ar, ar, nullptr, nullptr,
-                                     nullptr, remap_rows.empty() ? nullptr : sp + L.o_remap, S, st));
-            rc = launch_store_merge(s, back, sp + L.o_docs, (uint32_t *)(sp + L.o_hand));
-            if (rc) return rc;
+            SCHK(s, hm_launch_append(s->bdescs.p, nb, ar, ar, nullptr, nullptr, nullptr, s->p_remap ? s->inv.p : nullptr, S, st));
+            if ((rc = launch_list_merge(s, s->blist.p, nb))) return rc;
+            T.mark("rollback");
         }
         return HM_OK;
     } catch (...) {
@@ -711,10 +557,11 @@ int hm_store_last_routing(const hm_store *s, uint32_t *out3) {
 }
 
 int hm_doc_info(hm_store *s, uint32_t doc, hm_doc_info_t *out) {
-    if (!s || !out || doc >= s->docs.size()) return HM_ERR_INVALID;
+    if (!s || !out || doc >= s->n_handles) return HM_ERR_INVALID;
     if (s->pending) return hm_engine_fail(s->e, HM_ERR_INVALID, "batch in flight");
-    SCHK(s, hipStreamSynchronize(hm_engine_stream(s->e)));
-    const DocMeta &m = s->docs[doc];
+    int rc = HM_OK;
+    const DevDoc m = read_doc(s, doc, &rc);
+    if (rc) return rc;
     hm_doc_result r;
     SCHK(s, hipMemcpy(&r, s->res_docs + doc, sizeof(r), hipMemcpyDeviceToHost));
     out->n_changes = m.n_c; out->n_deps = m.n_d; out->n_ops = m.n_o; out->n_regs = m.n_r;
@@ -725,15 +572,16 @@ int hm_doc_info(hm_store *s, uint32_t doc, hm_doc_info_t *out) {
 
 int hm_doc_read(hm_store *s, uint32_t doc, int32_t *hist, uint32_t *all_deps, hm_reg_result *regs,
                 hm_surv_result *surv, uint32_t *clock, uint32_t *back_clock, uint32_t *heads) {
-    if (!s || doc >= s->docs.size()) return HM_ERR_INVALID;
+    if (!s || doc >= s->n_handles) return HM_ERR_INVALID;
     if (s->pending) return hm_engine_fail(s->e, HM_ERR_INVALID, "batch in flight");
-    SCHK(s, hipStreamSynchronize(hm_engine_stream(s->e)));
-    const DocMeta &m = s->docs[doc];
+    int rc = HM_OK;
+    const DevDoc m = read_doc(s, doc, &rc);
+    if (rc) return rc;
     const uint32_t S = s->S;
-    if (hist && m.n_c) SCHK(s, hipMemcpy(hist, s->hist + m.c.off, m.n_c * 4, hipMemcpyDeviceToHost));
-    if (all_deps && m.n_c) SCHK(s, hipMemcpy(all_deps, s->all_deps + (size_t)m.c.off * S, (size_t)m.n_c * S * 4, hipMemcpyDeviceToHost));
-    if (regs && m.n_r) SCHK(s, hipMemcpy(regs, s->regs + m.r.off, m.n_r * sizeof(hm_reg_result), hipMemcpyDeviceToHost));
-    if (surv && m.n_o) SCHK(s, hipMemcpy(surv, s->surv + m.o.off, m.n_o * sizeof(hm_surv_result), hipMemcpyDeviceToHost));
+    if (hist && m.n_c) SCHK(s, hipMemcpy(hist, s->hist + m.c_off, m.n_c * 4, hipMemcpyDeviceToHost));
+    if (all_deps && m.n_c) SCHK(s, hipMemcpy(all_deps, s->all_deps + (size_t)m.c_off * S, (size_t)m.n_c * S * 4, hipMemcpyDeviceToHost));
+    if (regs && m.n_r) SCHK(s, hipMemcpy(regs, s->regs + m.r_off, m.n_r * sizeof(hm_reg_result), hipMemcpyDeviceToHost));
+    if (surv && m.n_o) SCHK(s, hipMemcpy(surv, s->surv + m.o_off, m.n_o * sizeof(hm_surv_result), hipMemcpyDeviceToHost));
     if (clock) SCHK(s, hipMemcpy(clock, s->clock + (size_t)doc * S, S * 4, hipMemcpyDeviceToHost));
     if (back_clock) SCHK(s, hipMemcpy(back_clock, s->back_clock + (size_t)doc * S, S * 4, hipMemcpyDeviceToHost));
     if (heads) SCHK(s, hipMemcpy(heads, s->heads + (size_t)doc * S, S * 4, hipMemcpyDeviceToHost));
@@ -741,15 +589,17 @@ int hm_doc_read(hm_store *s, uint32_t doc, int32_t *hist, uint32_t *all_deps, hm
 }
 
 int hm_doc_log(hm_store *s, uint32_t doc, hm_change_row *changes, hm_dep_row *deps, hm_op_row *ops) {
-    if (!s || doc >= s->docs.size()) return HM_ERR_INVALID;
+    if (!s || doc >= s->n_handles) return HM_ERR_INVALID;
     if (s->pending) return hm_engine_fail(s->e, HM_ERR_INVALID, "batch in flight");
-    const DocMeta &m = s->docs[doc];
+    int rc = HM_OK;
+    const DevDoc m = read_doc(s, doc, &rc);
+    if (rc) return rc;
     if (changes && m.n_c) {
-        SCHK(s, hipMemcpy(changes, s->changes + m.c.off, m.n_c * sizeof(hm_change_row), hipMemcpyDeviceToHost));
-        for (uint32_t i = 0; i < m.n_c; i++) { changes[i].dep_off -= m.d.off; changes[i].op_first -= m.o.off; }
+        SCHK(s, hipMemcpy(changes, s->changes + m.c_off, m.n_c * sizeof(hm_change_row), hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < m.n_c; i++) { changes[i].dep_off -= m.d_off; changes[i].op_first -= m.o_off; }
     }
-    if (deps && m.n_d) SCHK(s, hipMemcpy(deps, s->deps + m.d.off, m.n_d * sizeof(hm_dep_row), hipMemcpyDeviceToHost));
-    if (ops && m.n_o) SCHK(s, hipMemcpy(ops, s->ops + m.o.off, m.n_o * sizeof(hm_op_row), hipMemcpyDeviceToHost));
+    if (deps && m.n_d) SCHK(s, hipMemcpy(deps, s->deps + m.d_off, m.n_d * sizeof(hm_dep_row), hipMemcpyDeviceToHost));
+    if (ops && m.n_o) SCHK(s, hipMemcpy(ops, s->ops + m.o_off, m.n_o * sizeof(hm_op_row), hipMemcpyDeviceToHost));
     return HM_OK;
 }
 
@@ -758,35 +608,30 @@ int hm_store_read_regs(hm_store *s, uint32_t n, const uint32_t *doc_handles, con
     if (!s || (n && (!doc_handles || !regs || !out_regs || (surv_cap && !out_surv)))) return HM_ERR_INVALID;
     if (s->pending) return hm_engine_fail(s->e, HM_ERR_INVALID, "batch in flight");
     try {
-        std::vector<uint32_t> req(2 * (size_t)n);
-        for (uint32_t i = 0; i < n; i++) {
-            if (doc_handles[i] >= s->docs.size()) return hm_engine_fail(s->e, HM_ERR_INVALID, "bad handle");
-            const DocMeta &m = s->docs[doc_handles[i]];
-            if (regs[i] >= m.n_r) return hm_engine_fail(s->e, HM_ERR_INVALID, "register outside its document");
-            req[i] = m.r.off + regs[i];
-            req[n + i] = m.o.off;
-        }
         if (out_n_surv) *out_n_surv = 0;
         if (!n) return HM_OK;
         hipStream_t st = hm_engine_stream(s->e);
         auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-        const size_t o_req = 0, o_cnt = al(8 * (size_t)n), o_regs = o_cnt + 256,
+        const size_t o_h = 0, o_r = al(4 * (size_t)n), o_cnt = o_r + al(4 * (size_t)n), o_regs = o_cnt + 256,
                      o_surv = o_regs + al((size_t)n * sizeof(hm_reg_result)), total = o_surv + al((size_t)surv_cap * sizeof(hm_surv_result) + 1);
         int rc = ensure_stage(s, total);
         if (rc) return rc;
         uint8_t *sp = s->stage.p;
-        SCHK(s, hipMemcpyAsync(sp + o_req, req.data(), req.size() * 4, hipMemcpyHostToDevice, st));
-        SCHK(s, hipMemsetAsync(sp + o_cnt, 0, 4, st));
-        SCHK(s, hm_launch_read_regs(n, (const uint32_t *)(sp + o_req), (const uint32_t *)(sp + o_req) + n, s->regs, s->surv,
-                                    (hm_reg_result *)(sp + o_regs), (hm_surv_result *)(sp + o_surv), surv_cap,
-                                    (uint32_t *)(sp + o_cnt), st));
-        uint32_t total_surv = 0;
-        SCHK(s, hipMemcpyAsync(&total_surv, sp + o_cnt, 4, hipMemcpyDeviceToHost, st));
-        SCHK(s, hipMemcpyAsync(out_regs, sp + o_regs, (size_t)n * sizeof(hm_reg_result), hipMemcpyDeviceToHost, st));
+        SCHK(s, hipMemcpyAsync(sp + o_h, doc_handles, (size_t)n * 4, hipMemcpyHostToDevice, st));
+        SCHK(s, hipMemcpyAsync(sp + o_r, regs, (size_t)n * 4, hipMemcpyHostToDevice, st));
+        SCHK(s, hipMemsetAsync(sp + o_cnt, 0, 8, st));
+        SCHK(s, hm_launch_read_regs_h(n, (const uint32_t *)(sp + o_h), (const uint32_t *)(sp + o_r), s->dm, s->n_handles, s->regs,
+                                      s->surv, (hm_reg_result *)(sp + o_regs), (hm_surv_result *)(sp + o_surv), surv_cap,
+                                      (uint32_t *)(sp + o_cnt), (uint32_t *)(sp + o_cnt) + 1, st));
+        uint32_t cb[2] = {0, 0};
+        SCHK(s, hipMemcpyAsync(cb, sp + o_cnt, 8, hipMemcpyDeviceToHost, st));
         SCHK(s, hipStreamSynchronize(st));
-        if (out_n_surv) *out_n_surv = total_surv;
-        if (total_surv > surv_cap) return hm_engine_fail(s->e, HM_ERR_NOMEM, "surv_cap below the survivors of the registers");
-        if (total_surv) SCHK(s, hipMemcpy(out_surv, sp + o_surv, (size_t)total_surv * sizeof(hm_surv_result), hipMemcpyDeviceToHost));
+        if (cb[1] & 1) return hm_engine_fail(s->e, HM_ERR_INVALID, "bad handle");
+        if (cb[1] & 2) return hm_engine_fail(s->e, HM_ERR_INVALID, "register outside its document");
+        SCHK(s, hipMemcpy(out_regs, sp + o_regs, (size_t)n * sizeof(hm_reg_result), hipMemcpyDeviceToHost));
+        if (out_n_surv) *out_n_surv = cb[0];
+        if (cb[0] > surv_cap) return hm_engine_fail(s->e, HM_ERR_NOMEM, "surv_cap below the survivors of the registers");
+        if (cb[0]) SCHK(s, hipMemcpy(out_surv, sp + o_surv, (size_t)cb[0] * sizeof(hm_surv_result), hipMemcpyDeviceToHost));
         return HM_OK;
     } catch (...) {
         return hm_engine_fail(s->e, HM_ERR_NOMEM, "exception in hm_store_read_regs");
@@ -794,11 +639,13 @@ int hm_store_read_regs(hm_store *s, uint32_t n, const uint32_t *doc_handles, con
 }
 
 int hm_doc_history_prefix(hm_store *s, uint32_t doc, uint32_t n, uint32_t *out) {
-    if (!s || doc >= s->docs.size() || (n && !out)) return HM_ERR_INVALID;
+    if (!s || doc >= s->n_handles || (n && !out)) return HM_ERR_INVALID;
     if (s->pending) return hm_engine_fail(s->e, HM_ERR_INVALID, "batch in flight");
-    const DocMeta &m = s->docs[doc];
+    int rc = HM_OK;
+    const DevDoc m = read_doc(s, doc, &rc);
+    if (rc) return -rc;
     std::vector<int32_t> h(m.n_c);
-    if (m.n_c) SCHK(s, hipMemcpy(h.data(), s->hist + m.c.off, m.n_c * 4, hipMemcpyDeviceToHost));
+    if (m.n_c) SCHK(s, hipMemcpy(h.data(), s->hist + m.c_off, m.n_c * 4, hipMemcpyDeviceToHost));
     std::vector<uint32_t> by_pos(m.n_c, HM_NONE);
     uint32_t H = 0;
     for (uint32_t i = 0; i < m.n_c; i++)
@@ -809,7 +656,7 @@ int hm_doc_history_prefix(hm_store *s, uint32_t doc, uint32_t n, uint32_t *out) 
 }
 
 int hm_doc_set_min_clock(hm_store *s, uint32_t doc, const uint32_t *clock) {
-    if (!s || doc >= s->docs.size() || !clock) return HM_ERR_INVALID;
+    if (!s || doc >= s->n_handles || !clock) return HM_ERR_INVALID;
     if (s->pending) return hm_engine_fail(s->e, HM_ERR_INVALID, "batch in flight");
     SCHK(s, hipMemcpy(s->min_clock + (size_t)doc * s->S, clock, s->S * 4, hipMemcpyHostToDevice));
     return HM_OK;
@@ -820,7 +667,7 @@ int hm_store_clock_update(hm_store *s, uint32_t n, const uint32_t *docs, uint8_t
     if (!s || (n && !docs)) return HM_ERR_INVALID;
     if (s->pending) return hm_engine_fail(s->e, HM_ERR_INVALID, "batch in flight");
     try {
-        for (uint32_t i = 0; i < n; i++) if (docs[i] >= s->docs.size()) return hm_engine_fail(s->e, HM_ERR_INVALID, "bad handle");
+        for (uint32_t i = 0; i < n; i++) if (docs[i] >= s->n_handles) return hm_engine_fail(s->e, HM_ERR_INVALID, "bad handle");
         if (!n) return HM_OK;
         const uint32_t S = s->S;
         hipStream_t st = hm_engine_stream(s->e);

@@ -19,6 +19,42 @@ struct AppendDesc {
     uint32_t n_objs;
 };
 
+// A document's log segments and totals, resident on the device (the store plans submits there:
+// a million-document round is too much host memory traffic to plan on the host).
+struct DevDoc {
+    uint32_t c_off, c_cap, d_off, d_cap, o_off, o_cap, r_off, r_cap;
+    uint32_t n_c, n_d, n_o, n_r, n_objs;
+    uint16_t n_actors, flags;
+    uint32_t pad[2];
+};
+static_assert(sizeof(DevDoc) == 64, "DevDoc is 64 B");
+
+// One batch row's plan: the document's totals before the append (the rollback restores them),
+// the capacities of the segments it outgrows (0 = fits) and its route.
+struct PlanRow {
+    uint32_t n_c, n_d, n_o, n_r, n_objs;
+    uint16_t n_actors, flags;
+    uint32_t g[4];
+    uint32_t inc, remapped;
+};
+
+// What the host reads back of a submit's device-side plan (one small copy per phase).
+struct PlanStats {
+    uint32_t err;                              // HM_PLAN_* bits of the failed checks
+    uint32_t n_inc, n_cold, n_back;
+    uint32_t mx[6];                            // incremental tile maxima (hm_inc_dims)
+    uint32_t max_c, max_o, max_r, max_objs, max_d, flags;   // launch hints of a merge list
+    unsigned long long need[4];                // rows the submit's growing segments take, per space
+    unsigned long long bump[4];                // arena bump pointers (device-side segment allocation)
+    unsigned long long tot_c, tot_d, tot_o, tot_r;
+};
+#define HM_PLAN_BAD_HANDLE 1u
+#define HM_PLAN_REPEATED 2u
+#define HM_PLAN_ROWS 4u
+#define HM_PLAN_TOTALS 8u
+#define HM_PLAN_CHANGE_ROWS 16u
+#define HM_PLAN_REMAP 32u
+
 struct StoreArenas {
     hm_change_row *changes;
     hm_dep_row *deps;
@@ -57,6 +93,36 @@ struct IncDims {
 };
 IncDims hm_inc_dims(uint32_t S, uint32_t new_c, uint32_t tgt, uint32_t stage, uint32_t regs, uint32_t surv,
                     uint32_t slots);
+
+struct PlanArgs {
+    const hm_doc_row *docs;
+    const hm_change_row *changes;
+    const uint32_t *handles;
+    const uint8_t *remap;                      // [n * S] or NULL
+    uint32_t n, n_changes, n_deps, n_ops, n_handles, S, stamp, incremental;
+    DevDoc *dm;
+    const hm_doc_result *res_docs;
+    uint32_t *seen;
+    PlanRow *plan;
+    AppendDesc *descs;
+    uint32_t *list;                            // cold handles
+    PlanStats *st;
+};
+hipError_t hm_launch_plan(const PlanArgs &a, hipStream_t s);
+hipError_t hm_launch_alloc(const PlanArgs &a, hipStream_t s);
+// hm_doc_row of each listed handle from its device meta (+ the launch hints in st)
+hipError_t hm_launch_doc_rows(const uint32_t *list, uint32_t n, const DevDoc *dm, hm_doc_row *rows, PlanStats *st,
+                              hipStream_t s);
+// documents of a batch whose merge failed: totals restored, rows re-ranked back, listed for re-merge
+hipError_t hm_launch_rollback(const uint32_t *handles, uint32_t n, const hm_doc_result *res_docs, const PlanRow *plan,
+                              const uint8_t *remap, uint32_t S, DevDoc *dm, AppendDesc *descs, uint8_t *inv,
+                              uint32_t *list, PlanStats *st, hipStream_t s);
+hipError_t hm_launch_init_docs(DevDoc *dm, uint32_t h0, uint32_t n, hipStream_t s);
+// chosen registers of resident documents by (handle, register): validated on the device
+hipError_t hm_launch_read_regs_h(uint32_t n, const uint32_t *handles, const uint32_t *regs, const DevDoc *dm,
+                                 uint32_t n_handles, const hm_reg_result *rr, const hm_surv_result *surv,
+                                 hm_reg_result *out_regs, hm_surv_result *out_surv, uint32_t cap, uint32_t *counter,
+                                 uint32_t *bad, hipStream_t s);
 
 hipError_t hm_launch_inc_apply(const AppendDesc *descs, uint32_t n, const IncArenas &A, const IncDims &M,
                                uint32_t *bail, hipStream_t s);

@@ -30,8 +30,10 @@ __global__ __launch_bounds__(SWG) void append_kernel(const AppendDesc *descs, ui
                                                      StoreArenas dst, const hm_change_row *st_changes,
                                                      const hm_dep_row *st_deps, const hm_op_row *st_ops,
                                                      const uint8_t *remap, uint32_t S) {
-    const uint32_t t = threadIdx.x;
-    for (uint32_t di = blockIdx.x; di < n_desc; di += gridDim.x) {
+    // one wave per document (a submit's appends are a few rows each; a 256-lane group per
+    // document would idle most of its lanes), four documents per workgroup
+    const uint32_t t = threadIdx.x & 63, W = 64;
+    for (uint32_t di = blockIdx.x * 4 + (threadIdx.x >> 6); di < n_desc; di += gridDim.x * 4) {
         const AppendDesc D = descs[di];
         const bool moved = D.src_c != D.dst_c || D.src_d != D.dst_d || D.src_o != D.dst_o || src.changes != dst.changes;
         const bool rm = D.remap_row != 0xFFFFFFFFu;
@@ -39,14 +41,14 @@ __global__ __launch_bounds__(SWG) void append_kernel(const AppendDesc *descs, ui
         // old rows: moved (rebased) and/or re-ranked
         if (moved || rm) {
             const int64_t dd = (int64_t)D.dst_d - (int64_t)D.src_d, dop = (int64_t)D.dst_o - (int64_t)D.src_o;
-            for (uint32_t i = t; i < D.n_old_c; i += SWG) {
+            for (uint32_t i = t; i < D.n_old_c; i += W) {
                 hm_change_row c = src.changes[D.src_c + i];
                 c.dep_off = (uint32_t)((int64_t)c.dep_off + dd);
                 c.op_first = (uint32_t)((int64_t)c.op_first + dop);
                 if (rm && c.actor < S) c.actor = mp[c.actor];
                 dst.changes[D.dst_c + i] = c;
             }
-            for (uint32_t i = t; i < D.n_old_d; i += SWG) {
+            for (uint32_t i = t; i < D.n_old_d; i += W) {
                 hm_dep_row r = src.deps[D.src_d + i];
                 if (rm && r.actor < S) r.actor = mp[r.actor];
                 dst.deps[D.dst_d + i] = r;
@@ -56,21 +58,21 @@ __global__ __launch_bounds__(SWG) void append_kernel(const AppendDesc *descs, ui
             // 32-byte op rows as two 16-byte words per thread
             const uint4 *so = reinterpret_cast<const uint4 *>(src.ops + D.src_o);
             uint4 *dop = reinterpret_cast<uint4 *>(dst.ops + D.dst_o);
-            for (uint32_t i = t; i < 2 * D.n_old_o; i += SWG) dop[i] = so[i];
+            for (uint32_t i = t; i < 2 * D.n_old_o; i += W) dop[i] = so[i];
         }
         // new rows: batch-local offsets -> arena offsets
         const uint32_t c_at = D.dst_c + D.n_old_c, d_at = D.dst_d + D.n_old_d, o_at = D.dst_o + D.n_old_o;
-        for (uint32_t i = t; i < D.n_new_c; i += SWG) {
+        for (uint32_t i = t; i < D.n_new_c; i += W) {
             hm_change_row c = st_changes[D.new_c + i];
             c.dep_off = d_at + (c.dep_off - D.new_d);
             c.op_first = o_at + (c.op_first - D.new_o);
             dst.changes[c_at + i] = c;
         }
-        for (uint32_t i = t; i < D.n_new_d; i += SWG) dst.deps[d_at + i] = st_deps[D.new_d + i];
+        for (uint32_t i = t; i < D.n_new_d; i += W) dst.deps[d_at + i] = st_deps[D.new_d + i];
         {
             const uint4 *so = reinterpret_cast<const uint4 *>(st_ops + D.new_o);
             uint4 *dop = reinterpret_cast<uint4 *>(dst.ops + o_at);
-            for (uint32_t i = t; i < 2 * D.n_new_o; i += SWG) dop[i] = so[i];
+            for (uint32_t i = t; i < 2 * D.n_new_o; i += W) dop[i] = so[i];
         }
         // rank-indexed per-document rows follow the remap
         if (rm && t == 0) {
@@ -85,7 +87,6 @@ __global__ __launch_bounds__(SWG) void append_kernel(const AppendDesc *descs, ui
                 for (uint32_t a = 0; a < S && a < 64; a++) rows[w][a] = tmp[a];
             }
         }
-        __syncthreads();
     }
 }
 
@@ -262,11 +263,34 @@ __device__ bool inc_doc(const AppendDesc &D, const IncArenas &A, const IncDims &
     const uint32_t xd = sd - (lane < nnc ? cnd : 0u), xo = so - (lane < nnc ? cno : 0u);
     const uint32_t total_d = lane_bcast(sd, nnc - 1), total_o = lane_bcast(so, nnc - 1);
     const bool bad_c = lane < nnc && (ca >= NA || cq == 0 || cdo != D.n_old_d + xd || coo != D.n_old_o + xo);
-    const bool bad_o = lane < nno && ((o_act != HM_SET && o_act != HM_DEL && o_act != HM_LINK) || o_dt == HM_DT_COUNTER ||
+    // set / del / link, counter sets, and incs by a number (an inc of anything else is left to
+    // the re-merge); an inc must stay inside the exact-integer envelope checked below
+    const bool bad_o = lane < nno && ((o_act != HM_SET && o_act != HM_DEL && o_act != HM_LINK && o_act != HM_INC) ||
+                                      (o_act == HM_INC && o_vt != HM_V_INT && o_vt != HM_V_FLOAT) ||
+                                      (o_act == HM_INC && o_vt == HM_V_INT &&
+                                       ((int64_t)(((uint64_t)o_vhi << 32) | o_vlo) >= (1ll << 43) ||
+                                        (int64_t)(((uint64_t)o_vhi << 32) | o_vlo) <= -(1ll << 43))) ||
+                                      (o_act == HM_INC && D.n_old_o + nno > 256) ||
                                       o_obj >= D.n_objs || o_reg >= D.n_r ||
                                       (o_vt == HM_V_INT && ((int64_t)(((uint64_t)o_vhi << 32) | o_vlo) > 9007199254740992ll ||
                                                             (int64_t)(((uint64_t)o_vhi << 32) | o_vlo) < -9007199254740992ll)));
     if (wave_ballot(bad_c || bad_o) || total_o != nno || total_d != D.n_new_d || total_d + nnc > M.tgt) return false;
+    if (wave_ballot(lane < nno && o_act == HM_INC)) {
+        // the exact-integer envelope over the whole log (the oracle's |partial sums| <= 2^53 rule):
+        // every integer counter base |v| < 2^50 and inc |v| < 2^43 in <= 256 ops bound any sum
+        bool big = false;
+        for (uint32_t i = lane; i < D.n_old_o; i += 64) {
+            const hm_op_row &r = A.ops[D.dst_o + i];
+            const int64_t v = (int64_t)r.value;
+            if (r.vtag == HM_V_INT && r.action == HM_INC) big |= v >= (1ll << 43) || v <= -(1ll << 43);
+            if (r.vtag == HM_V_INT && r.action == HM_SET && r.datatype == HM_DT_COUNTER) big |= v >= (1ll << 50) || v <= -(1ll << 50);
+        }
+        if (lane < nno && o_act == HM_SET && o_dt == HM_DT_COUNTER && o_vt == HM_V_INT) {
+            const int64_t v = (int64_t)(((uint64_t)o_vhi << 32) | o_vlo);
+            big |= v >= (1ll << 50) || v <= -(1ll << 50);
+        }
+        if (wave_ballot(big)) return false;
+    }
     if (lane < nnc) {
         uint32_t *w = nc + lane * 8;
         w[0] = ca; w[1] = cq; w[2] = cnd; w[3] = xd; w[4] = cno; w[5] = xo;
@@ -388,14 +412,48 @@ __device__ bool inc_doc(const AppendDesc &D, const IncArenas &A, const IncDims &
                     if (f <= x.op) lo = mid; else hi = mid;
                 }
                 const uint64_t kk = staged ? skey[lo] : key_of(A.changes + D.dst_c + lo);
+                const hm_op_row &xo = A.ops[D.dst_o + x.op];
+                const uint32_t cset = (xo.action == HM_SET && xo.datatype == HM_DT_COUNTER) ? 0x80u : 0u;
                 wl[slot * HM_INC_SLOT_CAP + lane] = x;
-                wla[slot * HM_INC_SLOT_CAP + lane] = (uint8_t)(kk >> 32);
+                wla[slot * HM_INC_SLOT_CAP + lane] = (uint8_t)((kk >> 32) | cset);
                 wls[slot * HM_INC_SLOT_CAP + lane] = (uint32_t)kk;
             }
             if (lane == 0) { scnt[slot] = c0; r_slot[g] = (uint8_t)slot; }
             __syncthreads();
         }
         const uint32_t base = slot * HM_INC_SLOT_CAP, cnt = uni(scnt[slot]);
+        if (act == HM_INC) {
+            // applyAssign for inc (A.2): every surviving counter set that is causally before the
+            // inc (its change an ancestor of the inc's: allDeps(inc)[x.actor] >= x.seq) adds the
+            // inc, integer + integer exactly, anything else in f64 (the application order); nothing
+            // is removed or reordered.  Integer sums stay inside the exact range: |value| < 2^50,
+            // |inc| < 2^43, at most 256 ops in the log (else the re-merge decides)
+            bool out = false;
+            if (lane < cnt) {
+                hm_surv_result x = wl[base + lane];
+                const uint32_t xa = wla[base + lane], xs = wls[base + lane];
+                const bool numeric = x.vtag == HM_V_INT || x.vtag == HM_V_FLOAT;
+                if ((xa & 0x80u) && numeric && adn[j * S + (xa & 0x7Fu)] >= xs) {
+                    if (x.vtag == HM_V_INT && vtag == HM_V_INT) {
+                        const int64_t cur = (int64_t)x.value;
+                        out = cur >= (1ll << 50) || cur <= -(1ll << 50);
+                        x.value = (uint64_t)(cur + (int64_t)val);
+                    } else {
+                        double xv, iv;
+                        if (x.vtag == HM_V_INT) xv = (double)(int64_t)x.value; else __builtin_memcpy(&xv, &x.value, 8);
+                        if (vtag == HM_V_INT) iv = (double)(int64_t)val; else __builtin_memcpy(&iv, &val, 8);
+                        const double r = xv + iv;
+                        __builtin_memcpy(&x.value, &r, 8);
+                        x.vtag = HM_V_FLOAT;
+                    }
+                    wl[base + lane] = x;
+                }
+            }
+            if (wave_ballot(out)) return false;
+            __syncthreads();
+            // (then, like every assign, the stable sortBy(actor).reverse() below: an inc flips
+            // the order of a change's equal-actor survivors too)
+        }
         // survivors concurrent with the new op stay (isConcurrent reduces to
         // allDeps(new)[x.actor] < x.seq: no resident change can depend on the new one)
         hm_surv_result x = {};
@@ -403,11 +461,11 @@ __device__ bool inc_doc(const AppendDesc &D, const IncArenas &A, const IncDims &
         bool keep = false;
         if (lane < cnt) {
             x = wl[base + lane]; xa = wla[base + lane]; xs = wls[base + lane];
-            keep = adn[j * S + xa] < xs;
+            keep = act == HM_INC || adn[j * S + (xa & 0x7Fu)] < xs;      // an inc removes nothing
         }
         const uint64_t km = wave_ballot(keep);
         const uint32_t nk = (uint32_t)__builtin_popcountll(km), pos = lanes_below(km);
-        const bool push = act != HM_DEL;
+        const bool push = act != HM_DEL && act != HM_INC;
         const uint32_t ncnt = nk + (push ? 1u : 0u);
         if (ncnt > HM_INC_SLOT_CAP) return false;
         __syncthreads();
@@ -415,15 +473,16 @@ __device__ bool inc_doc(const AppendDesc &D, const IncArenas &A, const IncDims &
         if (push && lane == 0) {
             hm_surv_result y;
             y.op = D.n_old_o + k; y.vtag = vtag; y.value = val;
-            wl[base + nk] = y; wla[base + nk] = (uint8_t)a; wls[base + nk] = q;
+            const uint32_t cset = (act == HM_SET && lane_bcast(o_dt, k) == HM_DT_COUNTER) ? 0x80u : 0u;
+            wl[base + nk] = y; wla[base + nk] = (uint8_t)(a | cset); wls[base + nk] = q;
         }
         __syncthreads();
         // sortBy(actor) (stable) then reverse
         if (lane < ncnt) { x = wl[base + lane]; xa = wla[base + lane]; xs = wls[base + lane]; }
         uint32_t rank = 0;
         for (uint32_t e = 0; e < ncnt; e++) {
-            const uint32_t ea = wla[base + e];
-            rank += (ea < xa || (ea == xa && e < lane)) ? 1u : 0u;
+            const uint32_t ea = wla[base + e] & 0x7Fu, xr = xa & 0x7Fu;
+            rank += (ea < xr || (ea == xr && e < lane)) ? 1u : 0u;
         }
         __syncthreads();
         if (lane < ncnt) {
@@ -516,13 +575,239 @@ __global__ void read_regs_kernel(uint32_t n, const uint32_t *abs_reg, const uint
     out_regs[i] = r;
 }
 
+
+// ---------------- the submit plan on the device ----------------
+// plan_kernel: one thread per batch row — the checks of hm_batch_submit (handle, repeated handle
+// by a per-submit stamp, row ranges, document totals, every change row inside its document's
+// deps / ops, the actor remap a permutation into the new ranks), the segments the append
+// outgrows and the route (incremental or re-merge).  Nothing in the store changes here: a
+// failed check fails the submit with the store as it was.
+__device__ __forceinline__ uint32_t pow2c(uint32_t x) {
+    x = x < 16u ? 16u : x;
+    return x <= 1u ? 1u : 1u << (32 - __builtin_clz(x - 1));
+}
+
+__global__ void plan_kernel(PlanArgs a) {
+    const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+    if (__ballot(i0 < a.n) == 0) return;                          // whole waves stay (reductions below)
+    const bool live = i0 < a.n;
+    const uint32_t i = live ? i0 : 0u;
+    uint32_t err = 0;
+    const uint32_t h = live ? a.handles[i] : 0u;
+    if (live && h >= a.n_handles) err |= HM_PLAN_BAD_HANDLE;
+    if (live && !err && atomicExch(&a.seen[h], a.stamp) == a.stamp) err |= HM_PLAN_REPEATED;
+    const hm_doc_row r = err ? hm_doc_row{} : a.docs[i];
+    const DevDoc m = err ? DevDoc{} : a.dm[live ? h : 0u];
+    if ((uint64_t)r.change_off + r.n_changes > a.n_changes || (uint64_t)r.dep_off + r.n_deps > a.n_deps ||
+        (uint64_t)r.op_off + r.n_ops > a.n_ops) err |= HM_PLAN_ROWS;
+    if (live && (r.n_actors > a.S || r.n_actors < m.n_actors || r.n_regs < m.n_r || r.n_objs < m.n_objs || r.n_objs == 0))
+        err |= HM_PLAN_TOTALS;
+    if (live && !(err & (HM_PLAN_ROWS | HM_PLAN_BAD_HANDLE)))
+        for (uint32_t c = r.change_off; c < r.change_off + r.n_changes; c++) {
+            const hm_change_row cr = a.changes[c];
+            if ((uint64_t)cr.dep_off < r.dep_off || (uint64_t)cr.dep_off + cr.n_deps > (uint64_t)r.dep_off + r.n_deps ||
+                (uint64_t)cr.op_first < r.op_off || (uint64_t)cr.op_first + cr.n_ops > (uint64_t)r.op_off + r.n_ops) {
+                err |= HM_PLAN_CHANGE_ROWS;
+                break;
+            }
+        }
+    bool remapped = false;
+    if (live && !err && a.remap) {
+        const uint8_t *mp = a.remap + (size_t)i * a.S;
+        unsigned long long used = 0;
+        for (uint32_t x = 0; x < m.n_actors; x++) {
+            if (mp[x] >= r.n_actors || ((used >> mp[x]) & 1ull)) { err |= HM_PLAN_REMAP; break; }
+            used |= 1ull << mp[x];
+            remapped |= mp[x] != x;
+        }
+    }
+    if (__ballot(err != 0)) {                                     // (rare) one atomic per failing lane
+        if (err) atomicOr(&a.st->err, err);
+        return;
+    }
+    PlanRow p;
+    p.n_c = m.n_c; p.n_d = m.n_d; p.n_o = m.n_o; p.n_r = m.n_r; p.n_objs = m.n_objs; p.n_actors = m.n_actors; p.flags = m.flags;
+    p.g[0] = live && m.n_c + r.n_changes > m.c_cap ? pow2c(m.n_c + r.n_changes) : 0u;
+    p.g[1] = live && m.n_d + r.n_deps > m.d_cap ? pow2c(m.n_d + r.n_deps) : 0u;
+    p.g[2] = live && m.n_o + r.n_ops > m.o_cap ? pow2c(m.n_o + r.n_ops) : 0u;
+    p.g[3] = live && r.n_regs > m.r_cap ? pow2c(r.n_regs) : 0u;
+    // the submit's reductions: one atomic per wave (a million lanes on one address would queue at the L2)
+    for (int k = 0; k < 4; k++) {
+        unsigned long long g = p.g[k];
+        for (int o = 32; o > 0; o >>= 1) g += (unsigned long long)__shfl_xor((long long)g, o);
+        if ((threadIdx.x & 63) == 0 && g) atomicAdd(&a.st->need[k], g);
+    }
+    // route: a clean resident state (last merge ok, nothing queued, no re-rank) and new rows that
+    // fit the incremental tiles -> inc_apply_kernel; the rest re-merge their whole log
+    const hm_doc_result last = a.res_docs[live ? h : 0u];
+    const uint32_t tgt = r.n_deps + r.n_changes;
+    const bool inc = live && a.incremental && last.status == HM_OK && last.n_queued == 0 && !remapped && r.n_changes > 0 &&
+                     r.n_changes <= HM_INC_MAX_NEW_C && r.n_ops <= HM_INC_MAX_NEW_O && tgt <= HM_INC_MAX_TGT &&
+                     r.n_regs <= HM_INC_MAX_REGS && last.n_surv <= HM_INC_MAX_SURV && m.n_r <= r.n_regs &&
+                     r.n_actors <= a.S && !((m.flags | r.flags) & HM_DOC_HAS_LISTS);
+    p.inc = inc ? 1u : 0u;
+    p.remapped = remapped ? 1u : 0u;
+    if (live) a.plan[i] = p;
+    const unsigned long long im = __ballot(inc);
+    if ((threadIdx.x & 63) == 0 && im) atomicAdd(&a.st->n_inc, (uint32_t)__popcll(im));
+    if (im) {
+        uint32_t v[6] = {inc ? r.n_changes : 0u, inc ? tgt : 0u,
+                         inc ? (m.n_c < HM_INC_MAX_STAGE ? m.n_c : (uint32_t)HM_INC_MAX_STAGE) : 0u, inc ? r.n_regs : 0u,
+                         inc ? last.n_surv : 0u, inc ? (r.n_ops < HM_INC_SLOTS ? r.n_ops : (uint32_t)HM_INC_SLOTS) : 0u};
+        for (int k = 0; k < 6; k++) {
+            for (int o = 32; o > 0; o >>= 1) { const uint32_t y = (uint32_t)__shfl_xor((int)v[k], o); v[k] = v[k] > y ? v[k] : y; }
+            if ((threadIdx.x & 63) == 0) atomicMax(&a.st->mx[k], v[k]);
+        }
+    }
+}
+
+// alloc_kernel: segments for the rows that outgrow theirs (bump allocation at the arenas'
+// ends), the append descriptor, the document's new totals, and the re-merge list
+__global__ void alloc_kernel(PlanArgs a) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    const uint32_t h = a.handles[i];
+    const hm_doc_row r = a.docs[i];
+    const PlanRow p = a.plan[i];
+    DevDoc m = a.dm[h];
+    AppendDesc D;
+    D.handle = h;
+    D.src_c = m.c_off; D.n_old_c = m.n_c; D.new_c = r.change_off; D.n_new_c = r.n_changes;
+    D.src_d = m.d_off; D.n_old_d = m.n_d; D.new_d = r.dep_off; D.n_new_d = r.n_deps;
+    D.src_o = m.o_off; D.n_old_o = m.n_o; D.new_o = r.op_off; D.n_new_o = r.n_ops;
+    D.src_r = m.r_off; D.n_old_r = m.n_r;
+    if (p.g[0]) { m.c_off = (uint32_t)atomicAdd(&a.st->bump[0], (unsigned long long)p.g[0]); m.c_cap = p.g[0]; }
+    if (p.g[1]) { m.d_off = (uint32_t)atomicAdd(&a.st->bump[1], (unsigned long long)p.g[1]); m.d_cap = p.g[1]; }
+    if (p.g[2]) { m.o_off = (uint32_t)atomicAdd(&a.st->bump[2], (unsigned long long)p.g[2]); m.o_cap = p.g[2]; }
+    if (p.g[3]) { m.r_off = (uint32_t)atomicAdd(&a.st->bump[3], (unsigned long long)p.g[3]); m.r_cap = p.g[3]; }
+    D.dst_c = m.c_off; D.dst_d = m.d_off; D.dst_o = m.o_off; D.dst_r = m.r_off;
+    D.remap_row = p.remapped ? i : 0xFFFFFFFFu;
+    m.n_c += r.n_changes; m.n_d += r.n_deps; m.n_o += r.n_ops;
+    m.n_r = r.n_regs; m.n_objs = r.n_objs; m.n_actors = r.n_actors; m.flags |= r.flags;
+    D.n_r = m.n_r; D.n_actors = m.n_actors; D.n_objs = m.n_objs;
+    D.inc = (uint16_t)p.inc;
+    a.descs[i] = D;
+    a.dm[h] = m;
+    if (!p.inc) a.list[atomicAdd(&a.st->n_cold, 1u)] = h;
+}
+
+__global__ void doc_rows_kernel(const uint32_t *list, uint32_t n, const DevDoc *dm, hm_doc_row *rows, PlanStats *st) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const DevDoc m = dm[list[i]];
+    hm_doc_row r;
+    r.change_off = m.c_off; r.n_changes = m.n_c; r.dep_off = m.d_off; r.n_deps = m.n_d;
+    r.op_off = m.o_off; r.n_ops = m.n_o; r.reg_off = m.r_off; r.n_regs = m.n_r;
+    r.n_objs = m.n_objs; r.n_actors = m.n_actors; r.flags = m.flags; r.reserved[0] = r.reserved[1] = 0;
+    rows[i] = r;
+    atomicMax(&st->max_c, m.n_c); atomicMax(&st->max_o, m.n_o); atomicMax(&st->max_r, m.n_r);
+    atomicMax(&st->max_objs, m.n_objs); atomicMax(&st->max_d, m.n_d); atomicOr(&st->flags, (uint32_t)m.flags);
+    atomicAdd(&st->tot_c, (unsigned long long)m.n_c); atomicAdd(&st->tot_d, (unsigned long long)m.n_d);
+    atomicAdd(&st->tot_o, (unsigned long long)m.n_o); atomicAdd(&st->tot_r, (unsigned long long)m.n_r);
+}
+
+__global__ void rollback_kernel(const uint32_t *handles, uint32_t n, const hm_doc_result *res_docs, const PlanRow *plan,
+                                const uint8_t *remap, uint32_t S, DevDoc *dm, AppendDesc *descs, uint8_t *inv,
+                                uint32_t *list, PlanStats *st) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t h = handles[i];
+    if (res_docs[h].status == HM_OK) return;
+    const PlanRow p = plan[i];
+    DevDoc m = dm[h];
+    const uint32_t k = atomicAdd(&st->n_back, 1u);
+    AppendDesc D = {};
+    D.handle = h;
+    D.src_c = D.dst_c = m.c_off; D.n_old_c = p.n_c;
+    D.src_d = D.dst_d = m.d_off; D.n_old_d = p.n_d;
+    D.src_o = D.dst_o = m.o_off; D.n_old_o = p.n_o;
+    D.remap_row = 0xFFFFFFFFu;
+    if (p.remapped && remap) {
+        // the old ranks back: the inverse of the submit's remap row
+        uint8_t *iv = inv + (size_t)k * S;
+        for (uint32_t x = 0; x < S; x++) iv[x] = 0xFF;
+        const uint8_t *mp = remap + (size_t)i * S;
+        for (uint32_t x = 0; x < p.n_actors; x++) iv[mp[x]] = (uint8_t)x;
+        D.remap_row = k;
+    }
+    m.n_c = p.n_c; m.n_d = p.n_d; m.n_o = p.n_o; m.n_r = p.n_r; m.n_objs = p.n_objs; m.n_actors = p.n_actors; m.flags = p.flags;
+    dm[h] = m;
+    descs[k] = D;
+    list[k] = h;
+}
+
+__global__ void init_docs_kernel(DevDoc *dm, uint32_t h0, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    DevDoc m = {};
+    m.n_objs = 1;                                            // ROOT
+    dm[h0 + i] = m;
+}
+
+__global__ void read_regs_h_kernel(uint32_t n, const uint32_t *handles, const uint32_t *regs, const DevDoc *dm,
+                                   uint32_t n_handles, const hm_reg_result *rr, const hm_surv_result *surv,
+                                   hm_reg_result *out_regs, hm_surv_result *out_surv, uint32_t cap, uint32_t *counter,
+                                   uint32_t *bad) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t h = handles[i];
+    if (h >= n_handles) { atomicOr(bad, 1u); return; }
+    const DevDoc m = dm[h];
+    if (regs[i] >= m.n_r) { atomicOr(bad, 2u); return; }
+    hm_reg_result r = rr[m.r_off + regs[i]];
+    const uint32_t off = atomicAdd(counter, r.n_surv);
+    if (off + r.n_surv <= cap)
+        for (uint32_t k = 0; k < r.n_surv; k++) out_surv[off + k] = surv[m.o_off + r.surv_off + k];
+    r.surv_off = off;
+    out_regs[i] = r;
+}
+
 }  // namespace hms
+
+hipError_t hm_launch_plan(const PlanArgs &a, hipStream_t s) {
+    if (!a.n) return hipSuccess;
+    hipLaunchKernelGGL(hms::plan_kernel, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t hm_launch_alloc(const PlanArgs &a, hipStream_t s) {
+    if (!a.n) return hipSuccess;
+    hipLaunchKernelGGL(hms::alloc_kernel, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t hm_launch_doc_rows(const uint32_t *list, uint32_t n, const DevDoc *dm, hm_doc_row *rows, PlanStats *st,
+                              hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(hms::doc_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, s, list, n, dm, rows, st);
+    return hipGetLastError();
+}
+hipError_t hm_launch_rollback(const uint32_t *handles, uint32_t n, const hm_doc_result *res_docs, const PlanRow *plan,
+                              const uint8_t *remap, uint32_t S, DevDoc *dm, AppendDesc *descs, uint8_t *inv,
+                              uint32_t *list, PlanStats *st, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(hms::rollback_kernel, dim3((n + 255) / 256), dim3(256), 0, s, handles, n, res_docs, plan, remap, S, dm,
+                       descs, inv, list, st);
+    return hipGetLastError();
+}
+hipError_t hm_launch_init_docs(DevDoc *dm, uint32_t h0, uint32_t n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(hms::init_docs_kernel, dim3((n + 255) / 256), dim3(256), 0, s, dm, h0, n);
+    return hipGetLastError();
+}
+hipError_t hm_launch_read_regs_h(uint32_t n, const uint32_t *handles, const uint32_t *regs, const DevDoc *dm,
+                                 uint32_t n_handles, const hm_reg_result *rr, const hm_surv_result *surv,
+                                 hm_reg_result *out_regs, hm_surv_result *out_surv, uint32_t cap, uint32_t *counter,
+                                 uint32_t *bad, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(hms::read_regs_h_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, handles, regs, dm, n_handles, rr,
+                       surv, out_regs, out_surv, cap, counter, bad);
+    return hipGetLastError();
+}
 
 hipError_t hm_launch_append(const AppendDesc *descs, uint32_t n_desc, const StoreArenas &src, const StoreArenas &dst,
                             const hm_change_row *st_changes, const hm_dep_row *st_deps, const hm_op_row *st_ops,
                             const uint8_t *remap, uint32_t S, hipStream_t s) {
     if (!n_desc) return hipSuccess;
-    const uint32_t grid = n_desc < 65535u ? n_desc : 65535u;
+    const uint32_t grid = (n_desc + 3) / 4 < 65535u ? (n_desc + 3) / 4 : 65535u;
     hipLaunchKernelGGL(hms::append_kernel, dim3(grid), dim3(SWG), 0, s, descs, n_desc, src, dst, st_changes, st_deps,
                        st_ops, remap, S);
     return hipGetLastError();
