@@ -566,10 +566,12 @@ struct DocState {
 
 // Per-op checks of K2 against the document's objects / elements: the first throw kind of the
 // op (0 none; ordered as the reference checks them: unknown object, then duplicate or
-// missing list element, the engine's insert-after-unknown envelope), whether a set/link
-// survives, and whether it touches a list.  Reads only LDS (K2's tables), so the rare
-// error-key pass can recompute it instead of keeping it live.
-struct OpCheck { uint32_t err; bool surv, has_list; };
+// missing list element), whether a set/link survives, whether it touches a list, and whether
+// it is an insert after an element not inserted yet (Automerge accepts it; whether a later set
+// throws depends on the whole insertion chain, which merge_large_kernel climbs: the document
+// is deferred).  Reads only LDS (K2's tables), so the rare error-key pass can recompute it
+// instead of keeping it live.
+struct OpCheck { uint32_t err; bool surv, has_list, late; };
 __device__ __forceinline__ OpCheck op_check(const SmallLds &L, int32_t ohv, uint32_t act, uint32_t obj, uint32_t reg,
                                             uint32_t par, uint32_t okey, uint32_t R, uint32_t O) {
     const bool asg = ohv >= 0 && act >= HM_INS && act <= HM_INC && reg < R;
@@ -587,10 +589,10 @@ __device__ __forceinline__ OpCheck op_check(const SmallLds &L, int32_t ohv, uint
     OpCheck r;
     r.has_list = ins || (known && is_list);
     r.surv = sl && !((so >> h) & 1);
+    r.late = ins && par != HM_HEAD && !(ip <= okey);
     // (history, op) keys are shared by an op's checks, so the earliest code of one op wins:
-    // unknown object < duplicate element < missing element < the insert-after envelope
+    // unknown object < duplicate element < missing element
     uint32_t e = 0;
-    if (ins && par != HM_HEAD && !(ip <= okey)) e = HM_ERR_UNSUPPORTED;      // insert after an element not yet inserted
     if (sl && is_list && !(im <= okey)) e = HM_ERR_MISSING_ELEM;            // 'Missing index entry for list element'
     if (ins && im != okey + 1) e = HM_ERR_DUPLICATE_ELEM;                   // 'Duplicate list element ID'
     if (unknown) e = HM_ERR_UNKNOWN_OBJECT;
@@ -1135,17 +1137,19 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         }
     wave_sync();
     bool surv[OPL];
-    bool has_list = false, anyerr = false;
+    bool has_list = false, anyerr = false, late = false;
 #pragma unroll
     for (int t = 0; t < OPL; t++) {
         // predicated: every lane reads (clamped) and decides with selects, no per-op branches
         const OpCheck ck = op_check(L, oh[t], oact[t], oobj[t], oreg[t], opar[t], okey[t], R, O);
         has_list |= ck.has_list;
         anyerr |= ck.err != 0;
+        late |= ck.late;
         surv[t] = ck.surv;
         // survivors counted per (register, actor rank): the rank below needs no survivor list
         if (surv[t]) lds_add(&L.survpk[oreg[t]], 1ull << (8 * oactor[t]));
     }
+    if (__ballot(late)) return OUT_UNSUPPORTED;                  // the general kernel climbs the chains
     if (__ballot(anyerr)) {
         // a throw: its key (history position, op, arrival) orders it against the others
         u64 errk = ~0ull;                // this lane's earliest throw (one wave-wide min below)

@@ -106,6 +106,7 @@ struct Shared {
     uint32_t oslot[LA_MAX], otype[LA_MAX];   // objslot / objtype of documents with <= LA_MAX objects
     uint32_t listid[LA_MAX], listbase[LA_MAX + 1];   // l34_res: compact list ids, list bases
     uint32_t flags, all_ok, H, nins, nl, total, lists, grew, nmake, nodup, ctrs, nsurv;
+    uint32_t late;                      // an insert after an element not yet inserted
     uint32_t gflag[3];
     u64 errkey;
     uint32_t scan[LWG / 64 + 1];
@@ -601,8 +602,7 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
             any_list = true;
             const uint32_t parent = par[u];
             if (r_ins[reg] != key + 1) atomicMin(&sh.errkey, err_key((uint32_t)h, kx + 1, ci, HM_ERR_DUPLICATE_ELEM));
-            if (parent != HM_HEAD && !(r_ins[parent] <= key))
-                atomicMin(&sh.errkey, err_key((uint32_t)h, kx + 1, ci, HM_ERR_UNSUPPORTED));
+            if (parent != HM_HEAD && !(r_ins[parent] <= key)) sh.late = 1;   // the general path climbs chains
             continue;
         }
         any_list |= is_list;
@@ -625,6 +625,12 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
     }
     if (any_list) sh.lists = 1;
     bsync();
+    if (sh.late) {                                  // (uniform) every thread has read the flag
+        bsync();
+        if (tid == 0) { sh.nins = 0; sh.ctrs = 0; }
+        bsync();
+        return RES_FALLBACK;
+    }
     const bool lists_flag = sh.lists != 0;
     const uint32_t nsurv = sh.nsurv;
     if (sh.errkey != ~0ull) return LERR;
@@ -801,7 +807,7 @@ __device__ __forceinline__ int merge_doc_res(const SmallParams &p, Shared &sh, L
     const hm_change_row *CH = p.changes + doc.change_off;
     if (tid < LA_MAX) { sh.base[tid] = 0xFFFFFFFFu; sh.maxs[tid] = 0; sh.clock[tid] = 0; sh.bclock[tid] = 0;
                         sh.headv[tid] = 0; sh.maxad[tid] = 0; }
-    if (tid == 0) { sh.flags = 0; sh.errkey = ~0ull; sh.all_ok = 1; sh.H = 0; sh.nins = 0; sh.total = 0; sh.lists = 0; sh.ctrs = 0; }
+    if (tid == 0) { sh.flags = 0; sh.errkey = ~0ull; sh.all_ok = 1; sh.H = 0; sh.nins = 0; sh.total = 0; sh.lists = 0; sh.ctrs = 0; sh.late = 0; }
     // rows at the top of the arena: changes (6n words), deps (2nd), hist (n), h2a (n)
     const uint32_t stage_base = (LARENA - (8 * n + 2 * nd)) & ~1u;
     LDS hm_change_row *sCH = (LDS hm_change_row *)(ar + stage_base);
@@ -1009,7 +1015,7 @@ __device__ HML_DOC_ATTR Outcome merge_doc_large(const SmallParams &p, Shared &sh
     // ---- per-actor seq ranges -> first-arrival table size ----
     if (tid < LA_MAX) { sh.base[tid] = 0xFFFFFFFFu; sh.maxs[tid] = 0; sh.clock[tid] = 0; sh.bclock[tid] = 0;
                         sh.headv[tid] = 0; sh.maxad[tid] = 0; }
-    if (tid == 0) { sh.flags = 0; sh.errkey = ~0ull; sh.all_ok = 1; sh.H = 0; sh.nins = 0; sh.total = 0; sh.lists = 0; sh.ctrs = 0; }
+    if (tid == 0) { sh.flags = 0; sh.errkey = ~0ull; sh.all_ok = 1; sh.H = 0; sh.nins = 0; sh.total = 0; sh.lists = 0; sh.ctrs = 0; sh.late = 0; }
     bsync();
     if (n == 0 && (m || doc.n_deps)) return LUNSUP;
     // Change and dep rows staged at the top of the LDS arena (with LDS copies of hist / h2a) when
@@ -1645,9 +1651,7 @@ __device__ HML_DOC_ATTR Outcome merge_doc_large(const SmallParams &p, Shared &sh
             const uint32_t parent = OP[k].parent;
             if (X.insmin[o.reg] != key + 1)
                 atomicMin(&sh.errkey, err_key((uint32_t)h, kx + 1, ci, HM_ERR_DUPLICATE_ELEM));
-            // engine envelope, ordered like a throw: insert after an element not yet inserted
-            if (parent != HM_HEAD && !(X.insmin[parent] <= key))
-                atomicMin(&sh.errkey, err_key((uint32_t)h, kx + 1, ci, HM_ERR_UNSUPPORTED));
+            if (parent != HM_HEAD && !(X.insmin[parent] <= key)) sh.late = 1;   // see the chain pass below
             continue;
         }
         any_list |= is_list;
@@ -1674,6 +1678,54 @@ __device__ HML_DOC_ATTR Outcome merge_doc_large(const SmallParams &p, Shared &sh
     }
     if (any_list) sh.lists = 1;
     bsync();
+    // Inserts after an element not yet inserted (Automerge 0.12 applyInsert accepts them: the op
+    // waits in its parent's _following until the parent arrives).  A set
+    // or link on a list element runs updateListElement -> getPrevious, which climbs the element's
+    // insertion chain and throws 'Missing index entry' at the first element not inserted yet; so
+    // the set throws iff attach(e) = max insmin over e's chain exceeds its key.  An element whose
+    // chain never reaches '_head' (a missing or cyclic ancestor) is never visible: L4 leaves it
+    // out.  attach by pointer jumping over (parent, max) pairs in the (still free) tour arrays.
+    const bool late = sh.late != 0;
+    uint32_t *cjp = X.tour0, *cmx = X.tval0;       // final chain pointers / maxima (late documents)
+    constexpr uint32_t CH_HEAD = 0xFFFFFFFFu;
+    if (late) {
+        if (R > 2 * (m + O)) return LUNSUP;        // (register ids beyond the tour arrays: no such encoder)
+        uint32_t *jp1 = X.tour1, *mx1 = X.tval1;
+        for (uint32_t r = tid; r < R; r += LWG) { cjp[r] = CH_HEAD; cmx[r] = X.insmin[r]; }
+        bsync();
+        for (uint32_t k = tid; k < m; k += LWG) {
+            const OpC o = op_c(k);
+            if (o.action != HM_INS || o.obj >= O) continue;
+            const uint32_t ci = opchg_of(k);
+            if (hist_of(ci) < 0 || X.insmin[o.reg] != key_of(k, ci) + 1) continue;   // the applied insertion
+            const uint32_t par = OP[k].parent;
+            if (par != HM_HEAD) cjp[o.reg] = par;
+        }
+        bsync();
+        const uint32_t rounds = 33 - __builtin_clz(R | 1);
+        for (uint32_t rd = 0; rd < rounds; rd++) {
+            for (uint32_t r = tid; r < R; r += LWG) {
+                const uint32_t j = cjp[r], a = cmx[r];
+                if (j == CH_HEAD) { jp1[r] = CH_HEAD; mx1[r] = a; }
+                else { jp1[r] = cjp[j]; const uint32_t b = cmx[j]; mx1[r] = a > b ? a : b; }
+            }
+            bsync();
+            uint32_t *t = cjp; cjp = jp1; jp1 = t; t = cmx; cmx = mx1; mx1 = t;
+        }
+        for (uint32_t k = tid; k < m; k += LWG) {
+            const OpC o = op_c(k);
+            if ((o.action != HM_SET && o.action != HM_LINK) || o.obj >= O) continue;
+            const uint32_t ot = otype_get(o.obj);
+            if (!(ot == HM_MAKE_LIST || ot == HM_MAKE_TEXT)) continue;
+            const uint32_t ci = opchg_of(k);
+            const int32_t h = hist_of(ci);
+            if (h < 0) continue;
+            const uint32_t kx = k - op0_of(ci), key = kb_of(ci) + kx;
+            if (!(cmx[o.reg] <= key)) atomicMin(&sh.errkey, err_key((uint32_t)h, kx + 1, ci, HM_ERR_MISSING_ELEM));
+            else if (cjp[o.reg] != CH_HEAD) atomicOr(&sh.flags, LF_UNSUPPORTED);   // a cyclic chain: getPrevious never returns
+        }
+        bsync();
+    }
     const bool lists_flag = sh.lists != 0;
     const uint32_t nsurv = sh.nsurv;
     if (sh.errkey != ~0ull) return LERR;
@@ -1795,21 +1847,25 @@ __device__ HML_DOC_ATTR Outcome merge_doc_large(const SmallParams &p, Shared &sh
     LSTAMP(6);
     // ---- L4: RGA order ----
     if (lists_flag) {
-        if (!early) {
+        // late documents rebuild the nodes without the detached elements
+        const bool early_nodes = early && !late;
+        if (!early_nodes) {
             for (uint32_t i = tid; i < NP; i += LWG) { X.pcount[i] = 0; X.pfill[i] = 0; X.fc[i] = 0xFFFFFFFFu; }
             for (uint32_t i = tid; i < R; i += LWG) X.regnode[i] = 0xFFFFFFFFu;
+            if (tid == 0) sh.nins = 0;
         }
         for (uint32_t i = tid; i < O; i += LWG) { const uint32_t t = otype_get(i); X.listid[i] = (t == HM_MAKE_LIST || t == HM_MAKE_TEXT) ? 1u : 0u; }
         bsync();
         uint32_t nl;
         nl = scan_array(sh, X.listid, O);          // exclusive prefix -> compact list id (valid for list objects)
         // per node i: its register nreg[i], its compact list id nlist[i], parent slot, sibling key
-        if (!early) {
+        if (!early_nodes) {
             for (uint32_t k = tid; k < m; k += LWG) {
                 const OpC c = op_c(k);
                 if (c.action != HM_INS) continue;
                 const uint32_t ci = opchg_of(k);
                 if (hist_of(ci) < 0) continue;
+                if (late && (cjp[c.reg] != CH_HEAD || cmx[c.reg] == 0xFFFFFFFFu)) continue;   // detached: never visible
                 const uint32_t parent = OP[k].parent, elem = OP[k].elem;
                 const uint32_t i = atomicAdd(&sh.nins, 1u);
                 const uint32_t pi = parent == HM_HEAD ? R + c.obj : parent;
@@ -1829,7 +1885,7 @@ __device__ HML_DOC_ATTR Outcome merge_doc_large(const SmallParams &p, Shared &sh
         for (uint32_t i = tid; i < N; i += LWG) {
             const uint32_t pi = X.nodepi[i];
             if (X.pcount[pi] > 1) X.plist[X.poff[pi] + g_add(&X.pfill[pi], 1u)] = i;
-            if (early) X.nlist[i] = X.listid[X.nlist[i]];
+            if (early_nodes) X.nlist[i] = X.listid[X.nlist[i]];
         }
         bsync();
         for (uint32_t i = tid; i < N; i += LWG) {

@@ -149,8 +149,12 @@ static int64_t get_parent(docst_t *s, uint32_t obj, uint32_t reg) {
     return p == HM_HEAD ? (int64_t)(s->doc->n_regs + obj) : (int64_t)p;
 }
 
-/* getPrevious: returns the predecessor element reg, NONE for the head */
-static uint32_t get_previous(docst_t *s, uint32_t obj, uint32_t reg, int *err) {
+/* getPrevious: returns the predecessor element reg, NONE for the head.  *steps counts the
+ * elements visited: a walk over an acyclic insertion tree visits each at most twice, so a walk
+ * past the bound is going round a cycle of inserts (each after the next, all detached from
+ * '_head'), on which the reference's getPrevious never returns: *err = 2 */
+static uint32_t get_previous(docst_t *s, uint32_t obj, uint32_t reg, int *err, uint64_t *steps) {
+    const uint64_t bound = 4 * (uint64_t)s->doc->n_regs + 8;
     int64_t parent = get_parent(s, obj, reg);
     if (parent < 0) { *err = 1; return NONE; }
     uint32_t *kids = s->kids;
@@ -160,6 +164,7 @@ static uint32_t get_previous(docst_t *s, uint32_t obj, uint32_t reg, int *err) {
     uint32_t prev = NONE;
     for (uint32_t i = 0; i < n; i++) { if (kids[i] == reg) break; prev = kids[i]; }
     while (1) {
+        if (++*steps > bound) { *err = 2; return NONE; }
         uint32_t m = insertions_after(s, prev, kids);
         if (m == 0) return prev;
         prev = kids[m - 1];
@@ -177,11 +182,14 @@ static int update_list_element(docst_t *s, uint32_t obj, uint32_t reg) {
     }
     if (ops->n == 0) return 0;                              /* deleting a non-existent element */
     uint32_t prev = reg;
+    uint64_t steps = 0;
     while (1) {
         index = -1;
         int err = 0;
-        prev = get_previous(s, obj, prev, &err);
+        prev = get_previous(s, obj, prev, &err, &steps);
+        if (err == 2) { s->unsupported = 1; return HM_ERR_UNSUPPORTED; }   /* the reference loops forever */
         if (err) return HM_ERR_MISSING_ELEM;
+        if (++steps > 4 * (uint64_t)s->doc->n_regs + 8) { s->unsupported = 1; return HM_ERR_UNSUPPORTED; }
         if (prev == NONE) break;
         index = u32_index_of(el, prev);
         if (index >= 0) break;
@@ -295,9 +303,9 @@ static void apply_change(docst_t *s, uint32_t ci) {
             if (op->obj >= s->doc->n_objs || s->objtype[op->obj] < 0) { err = HM_ERR_UNKNOWN_OBJECT; break; }
             if (op->reg >= s->doc->n_regs || (op->parent != HM_HEAD && op->parent >= s->doc->n_regs)) { s->unsupported = 1; break; }
             if (s->insertion[op->reg] != NONE) { err = HM_ERR_DUPLICATE_ELEM; break; }
-            /* engine envelope (not a reference rule): an element must be inserted after
-             * an element that already exists; otherwise getPrevious may throw later */
-            if (op->parent != HM_HEAD && s->insertion[op->parent] == NONE) { fail(s, HM_ERR_UNSUPPORTED, ci, j); return; }
+            /* an insert after an element not inserted yet waits in its parent's _following
+             * (applyInsert does not look the parent up); getPrevious throws later if a set
+             * lands on an element whose insertion chain is still incomplete */
             s->reg_obj[op->reg] = op->obj;
             u32_push(&s->following[op->parent == HM_HEAD ? s->doc->n_regs + op->obj : op->parent], k);
             s->insertion[op->reg] = k;

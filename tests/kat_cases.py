@@ -153,15 +153,44 @@ CASES = [
      {"status": "DUPLICATE_ELEM", "error_at": [0, 2]}),
     ("rga_missing_elem", [ch(A, 1, {}, mk("makeList", "L"), s(f"{A}:9", "q", obj="L"))],
      {"status": "MISSING_ELEM", "error_at": [0, 1]}),
+    # A.3: applyInsert does not look the parent up -- an insert after an element not inserted
+    # yet waits in the parent's _following; once the parent arrives, its subtree is in order
+    ("rga_insert_before_parent", [ch(A, 1, {}, mk("makeList", "L"), link("l", "L"),
+                                     ins("L", f"{A}:1", 2), ins("L", "_head", 1),
+                                     s(f"{A}:1", "a", obj="L"), s(f"{A}:2", "b", obj="L"))],
+     {"state": {"map": [["l", {"value": {"list": [{"value": "a"}, {"value": "b"}]}}]]}}),
+    # ... across changes: B's element arrives after A's insert that names it
+    ("rga_parent_from_later_change", [ch(A, 1, {}, mk("makeList", "L"), link("l", "L"), ins("L", f"{B}:1", 1)),
+                                      ch(B, 1, {A: 1}, ins("L", "_head", 1), s(f"{B}:1", "x", obj="L"),
+                                         s(f"{A}:1", "y", obj="L"))],
+     {"state": {"map": [["l", {"value": {"list": [{"value": "x"}, {"value": "y"}]}}]]}}),
+    # a set on an element whose chain is incomplete: getPrevious climbs to the missing parent
+    ("rga_set_under_missing_parent", [ch(A, 1, {}, mk("makeList", "L"), ins("L", "zzzz:9", 1),
+                                         ins("L", f"{A}:1", 2), s(f"{A}:2", "q", obj="L"))],
+     {"status": "MISSING_ELEM", "error_at": [0, 3]}),
+    # ... the grandparent arrives in a later change, after the set: still a throw
+    ("rga_set_before_grandparent", [ch(A, 1, {}, mk("makeList", "L"), ins("L", f"{B}:1", 1),
+                                       ins("L", f"{A}:1", 2)),
+                                    ch(A, 2, {}, s(f"{A}:2", "q", obj="L")),
+                                    ch(B, 1, {A: 2}, ins("L", "_head", 1))],
+     {"status": "MISSING_ELEM", "error_at": [1, 0]}),
+    # elements never attached to '_head' (a missing parent, or a cycle of inserts) stay hidden;
+    # a delete on one is a no-op
+    ("rga_detached_elements_hidden", [ch(A, 1, {}, mk("makeList", "L"), link("l", "L"),
+                                         ins("L", "zzzz:9", 1), ins("L", f"{A}:3", 2), ins("L", f"{A}:2", 3),
+                                         ins("L", "_head", 4), s(f"{A}:4", "v", obj="L"), d(f"{A}:1", obj="L"))],
+     {"state": {"map": [["l", {"value": {"list": [{"value": "v"}]}}]]}}),
 ]
 
 
 # ---------------------------------------------------------------------------
 # Engine-envelope precedence (not Automerge rules; DESIGN.md "Envelope").
-# An insert after an element that is not yet inserted is ordered like a throw:
-# the first event in (history position, op) order wins.  Malformed rows
-# (ids outside the doc's tables, gaps/overlaps in the change->op/dep layout)
-# put the whole document outside, whatever would throw first.
+# Inserts after elements not yet inserted are Automerge rules now (CASES above);
+# these pin that they no longer leave the envelope, and that a set on an
+# element of a cycle of inserts (where the reference's getPrevious never
+# returns) does.  Malformed rows (ids outside the doc's tables, gaps/overlaps in
+# the change->op/dep layout) put the whole document outside, whatever would
+# throw first.
 # Each case: (name, changes, mutate(batch) or None, expected summary subset).
 # ---------------------------------------------------------------------------
 def _orphan_reg_in_queued(b):
@@ -186,14 +215,22 @@ ENVELOPE_CASES = [
     ("orphan_insert_before_error",
      [ch(A, 1, {}, mk("makeList", "L"), ins("L", "zzzz:99", 1)),
       ch(A, 2, {}, mk("makeMap", "M"), mk("makeMap", "M"))],
-     None, {"status": "UNSUPPORTED"}),
+     None, {"status": "DUPLICATE_OBJECT", "error_at": [1, 1]}),
     ("orphan_insert_then_error_same_change",
      [ch(A, 1, {}, mk("makeList", "L"), ins("L", "zzzz:5", 1), mk("makeList", "L"))],
-     None, {"status": "UNSUPPORTED"}),
+     None, {"status": "DUPLICATE_OBJECT", "error_at": [0, 2]}),
     ("duplicate_elem_outranks_orphan_on_same_op",
      [ch(A, 1, {}, mk("makeList", "L"), ins("L", "_head", 1)),
       ch(A, 2, {}, ins("L", "zzzz:9", 1))],
      None, {"status": "DUPLICATE_ELEM", "error_at": [1, 0]}),
+    ("orphan_insert_ok",
+     [ch(A, 1, {}, mk("makeList", "L"), link("l", "L"), ins("L", "zzzz:99", 1), ins("L", "_head", 2),
+         s(f"{A}:2", 7, obj="L"))],
+     None, {"status": "OK", "state": {"map": [["l", {"value": {"list": [{"value": 7}]}}]]}}),
+    ("set_on_insert_cycle",
+     [ch(A, 1, {}, mk("makeList", "L"), ins("L", f"{A}:2", 1), ins("L", f"{A}:1", 2),
+         s(f"{A}:1", "q", obj="L"))],
+     None, {"status": "UNSUPPORTED"}),
     ("malformed_register_in_queued_change",
      [ch(A, 1, {}, s("x", 1)), ch(B, 2, {}, s("y", 2))],
      _orphan_reg_in_queued, {"status": "UNSUPPORTED"}),

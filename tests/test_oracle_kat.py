@@ -43,13 +43,18 @@ def test_transitive_deps_literal_fold():
     assert got["state"] == {"map": [["k", {"value": "c1", "conflicts": [[A, "a2"]]}]]}
 
 
-def test_oracle_envelope_flags():
-    """An ins after a never-inserted element leaves the engine envelope."""
-    from hypermerge_amd.columnar import ROOT_ID as R
+def test_oracle_insert_after_never_inserted_element():
+    """An ins after a never-inserted element is accepted (Automerge 0.12 applyInsert does not
+    look the parent up); the element stays hidden, and a set on it throws from getPrevious."""
     changes = [{"actor": "a", "seq": 1, "deps": {}, "ops": [
         {"action": "makeList", "obj": "L"}, {"action": "ins", "obj": "L", "key": "a:7", "elem": 8}]}]
     b = encode([changes])
-    assert doc_summary(b, O.merge(b), 0)["status"] == "UNSUPPORTED"
+    assert doc_summary(b, O.merge(b), 0)["status"] == "OK"
+    changes.append({"actor": "a", "seq": 2, "deps": {}, "ops": [
+        {"action": "set", "obj": "L", "key": "a:8", "value": 1}]})
+    b = encode([changes])
+    got = doc_summary(b, O.merge(b), 0)
+    assert got["status"] == "MISSING_ELEM" and got["error_at"] == [1, 0]
 
 
 @pytest.mark.parametrize("name,changes,mutate,expect", ENVELOPE_CASES, ids=[c[0] for c in ENVELOPE_CASES])
