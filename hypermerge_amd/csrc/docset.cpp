@@ -9,7 +9,7 @@
 // A docset owns the documents of one device: their interners (actor ids ranked in JS string
 // order, object UUIDs, (object, key|elemId) registers, string values, content identity of
 // changes — columnar.js DocEncoder, kept across rounds), their placement in the resident
-// stores (one hm_store per actor-stride class 8/16/32/64: a document moves to a wider class
+// stores (one hm_store per actor-stride class 8/16/32/64/128/256: a document moves to a wider class
 // when a new actor outgrows its rows, its log rows re-submitted from the old store), and the
 // patch base (the document as the last patch left it).  One call = one applyChanges round
 // for every document of the call: decode on host threads, submit per class, wait, commit or
@@ -39,8 +39,10 @@ namespace {
 
 using namespace hmscan;
 
-constexpr uint32_t N_CLASS = 4;
-constexpr uint32_t STRIDES[N_CLASS] = {8, 16, 32, 64};
+constexpr uint32_t N_CLASS = 6;
+constexpr uint32_t STRIDES[N_CLASS] = {8, 16, 32, 64, 128, 256};
+// a document's actors: rank 255 stays free for the stores' 0xFF "no rank" entries
+constexpr uint32_t MAX_ACTORS = HM_MAX_STRIDE - 1;
 constexpr uint8_t NO_CLASS = 0xFF;
 constexpr uint8_t NO_TYPE = 0xFF;
 
@@ -383,7 +385,7 @@ void decode_round(DocSt &d, Round &R, const uint8_t *data, const uint64_t *bo, S
         fresh_any |= f;
     }
     const uint32_t na = d.actors.size();
-    if (na > 64) return fail(HM_ERR_UNSUPPORTED, HM_NONE);
+    if (na > MAX_ACTORS) return fail(HM_ERR_UNSUPPORTED, HM_NONE);
     if (fresh_any) {
         R.s_rank_of = d.rank_of; R.s_by_rank = d.by_rank;
         std::vector<uint16_t> order(na);
@@ -902,7 +904,7 @@ struct hm_docset {
     uint32_t threads = 16;
     bool patches = true;
     bool binary = false;                                     // HM_DOCSET_BINARY results
-    hm_store *stores[N_CLASS] = {nullptr, nullptr, nullptr, nullptr};
+    hm_store *stores[N_CLASS] = {};
     // documents: fixed chunks, so hm_docset_open may run while a call works on earlier documents
     static constexpr uint32_t CHUNK = 4096;
     std::vector<std::unique_ptr<DocSt[]>> chunks;
@@ -1144,8 +1146,8 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
     mark("read regs");
     // render every document's patch and DocBackend.clock
     auto round_clock = [](const Round &x, uint32_t *rc) {      // this call's changes alone (updateClock(changes))
-        for (uint32_t a = 0; a < 64; a++) rc[a] = 0;
-        for (const hm_change_row &c : x.ch) if (c.actor < 64 && c.seq > rc[c.actor]) rc[c.actor] = c.seq;
+        for (uint32_t a = 0; a < HM_MAX_STRIDE; a++) rc[a] = 0;
+        for (const hm_change_row &c : x.ch) if (c.actor < HM_MAX_STRIDE && c.seq > rc[c.actor]) rc[c.actor] = c.seq;
     };
     bool exotic = false;
     if (ds->binary) {
@@ -1161,7 +1163,7 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
                 w.clock(x.clock, x.n_actors);
                 w.clock(x.heads, x.n_actors);
                 w.clock(x.back, x.n_actors);
-                uint32_t rc[64];
+                uint32_t rc[HM_MAX_STRIDE];
                 round_clock(x, rc);
                 w.clock(rc, x.n_actors);
                 w.begin();
@@ -1200,7 +1202,7 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
                 }
                 o += "]}";
                 jclock(x.bclock, d, x.back, x.n_actors);
-                uint32_t rc[64];
+                uint32_t rc[HM_MAX_STRIDE];
                 round_clock(x, rc);
                 jclock(x.cclock, d, rc, x.n_actors);
             }

@@ -150,7 +150,7 @@ uint32_t host_chunks(const hm_batch *b) {
 }
 
 int check_batch(hm_engine *e, const hm_batch *b) {
-    if (!b || b->a_stride == 0 || b->a_stride > 64) return fail(e, HM_ERR_INVALID, "a_stride must be in [1,64]");
+    if (!b || b->a_stride == 0 || b->a_stride > HM_MAX_STRIDE) return fail(e, HM_ERR_INVALID, "a_stride must be in [1,256]");
     if (b->n_docs && !b->docs) return fail(e, HM_ERR_INVALID, "docs table missing");
     if ((b->n_changes && !b->changes) || (b->n_deps && !b->deps) || (b->n_ops && !b->ops))
         return fail(e, HM_ERR_INVALID, "row table missing");

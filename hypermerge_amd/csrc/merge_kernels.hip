@@ -1356,9 +1356,9 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
             r.status = HM_ERR_INVALID; r.err_change = HM_NONE; r.err_op = HM_NONE;
             *dres = r;
         }
-        if (lane < S) {
-            p.res_clock[(size_t)ds * S + lane] = 0u; p.res_heads[(size_t)ds * S + lane] = 0u;
-            p.res_back_clock[(size_t)ds * S + lane] = 0u;
+        for (uint32_t a = lane; a < S; a += WAVE) {
+            p.res_clock[(size_t)ds * S + a] = 0u; p.res_heads[(size_t)ds * S + a] = 0u;
+            p.res_back_clock[(size_t)ds * S + a] = 0u;
         }
         return;
     }
@@ -1400,6 +1400,9 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
         p.res_clock[(size_t)ds * S + lane] = ar ? (uint32_t)__popcll(L.chain[lane]) : 0u;
         p.res_heads[(size_t)ds * S + lane] = ar ? L.headv[lane] : 0u;
         p.res_back_clock[(size_t)ds * S + lane] = ar ? L.bclock[lane] : 0u;   // DocBackend.clock (queued included)
+    }
+    for (uint32_t a = WAVE + lane; a < S; a += WAVE) {                   // wide rows: actors >= 64 are absent
+        p.res_clock[(size_t)ds * S + a] = 0u; p.res_heads[(size_t)ds * S + a] = 0u; p.res_back_clock[(size_t)ds * S + a] = 0u;
     }
     const bool act = lane < n;
     const u64 q = __ballot(act && st.hist == -1);
@@ -1484,6 +1487,14 @@ void merge_small_kernel(SmallParams p) {
         const uint32_t ds = hm_slot(p, d);
         uint32_t mc = 0;
         if (p.min_clock && threadIdx.x < p.a_stride) mc = p.min_clock[(size_t)ds * p.a_stride + threadIdx.x];
+        if (p.min_clock && p.a_stride > WAVE) {
+            // wide rows (> 64 actors; this kernel merges documents of <= 8): actors >= 64 have
+            // DocBackend.clock 0, so they only decide whether any minimumClock entry there is
+            // set; lane NA_MAX (clock 0 too) carries that for the comparison
+            uint32_t extra = 0;
+            for (uint32_t a = WAVE + threadIdx.x; a < p.a_stride; a += WAVE) extra |= p.min_clock[(size_t)ds * p.a_stride + a];
+            if (__ballot(extra != 0) && threadIdx.x == NA_MAX) mc |= 1u;
+        }
         const Outcome oc = !dok ? OUT_INVALID : in_env ? merge_doc_small<OPL, LISTS>(p, L, doc, w0, w1, w2, st) : OUT_UNSUPPORTED;
         const uint32_t mcmp = oc == OUT_OK ? min_cmp_of(p, L, doc, mc) : 0u;
 #if !HM_PREFETCH_EARLY
@@ -1597,7 +1608,7 @@ hipError_t hm_launch_small(const SmallParams &p, uint32_t opl, uint32_t cls, boo
 hipError_t hm_launch_clock(int which, const uint32_t *a, const uint32_t *b, void *out, uint32_t n_docs,
                            uint32_t S, hipStream_t s) {
     if (which == 0) {
-        if (S == 0 || S > 64) return hipErrorInvalidValue;
+        if (S == 0 || S > HM_MAX_STRIDE) return hipErrorInvalidValue;
         const uint32_t rows_per_wave = 64 / S;
         const uint32_t waves = (n_docs + rows_per_wave - 1) / rows_per_wave;
         const uint32_t blocks = (waves + 3) / 4;

@@ -28,7 +28,8 @@
 #endif
 #define LWG HML_LWG
 #define HML_WPE (LWG * HML_WGS_PER_CU / 256)   // waves per SIMD (register budget 512 / HML_WPE)
-#define LA_MAX 64
+#define LA_MAX 64    // objects whose tables live in LDS (Shared) rather than the pool
+#define LA_ACT 256   // actors per document (HM_MAX_STRIDE): the per-actor tables in Shared
 // LDS arena per workgroup (u32 words).  One 1024-thread workgroup per CU owns 150 KB: a
 // document's whole L3/L4 working set (op words, assign lists, register / node / parent tables,
 // Euler tour) is resident there (l34_res) instead of in the pool, whose per-document tables
@@ -101,8 +102,8 @@ __device__ __forceinline__ u64 err_key(uint32_t h, uint32_t op_plus1, uint32_t a
 }
 
 struct Shared {
-    uint32_t base[LA_MAX], maxs[LA_MAX], tabo[LA_MAX + 1], clock[LA_MAX], bclock[LA_MAX], headv[LA_MAX];
-    uint32_t maxad[LA_MAX];
+    uint32_t base[LA_ACT], maxs[LA_ACT], tabo[LA_ACT + 1], clock[LA_ACT], bclock[LA_ACT], headv[LA_ACT];
+    uint32_t maxad[LA_ACT];
     uint32_t oslot[LA_MAX], otype[LA_MAX];   // objslot / objtype of documents with <= LA_MAX objects
     uint32_t listid[LA_MAX], listbase[LA_MAX + 1];   // l34_res: compact list ids, list bases
     uint32_t flags, all_ok, H, nins, nl, total, lists, grew, nmake, nodup, ctrs, nsurv;
@@ -805,7 +806,7 @@ __device__ __forceinline__ int merge_doc_res(const SmallParams &p, Shared &sh, L
     const uint32_t n = doc.n_changes, A = doc.n_actors, m = doc.n_ops, nd = doc.n_deps;
     const uint32_t S = p.a_stride;
     const hm_change_row *CH = p.changes + doc.change_off;
-    if (tid < LA_MAX) { sh.base[tid] = 0xFFFFFFFFu; sh.maxs[tid] = 0; sh.clock[tid] = 0; sh.bclock[tid] = 0;
+    if (tid < LA_ACT) { sh.base[tid] = 0xFFFFFFFFu; sh.maxs[tid] = 0; sh.clock[tid] = 0; sh.bclock[tid] = 0;
                         sh.headv[tid] = 0; sh.maxad[tid] = 0; }
     if (tid == 0) { sh.flags = 0; sh.errkey = ~0ull; sh.all_ok = 1; sh.H = 0; sh.nins = 0; sh.total = 0; sh.lists = 0; sh.ctrs = 0; sh.late = 0; }
     // rows at the top of the arena: changes (6n words), deps (2nd), hist (n), h2a (n)
@@ -1010,10 +1011,10 @@ __device__ HML_DOC_ATTR Outcome merge_doc_large(const SmallParams &p, Shared &sh
     const uint32_t S = p.a_stride;
     const hm_change_row *CH = p.changes + doc.change_off;
     const hm_op_row *OP = p.ops + doc.op_off;
-    if (A > LA_MAX || O < 1 || n >= (1u << 20) || m >= (1u << 24)) return LUNSUP;
+    if (A > LA_ACT || O < 1 || n >= (1u << 20) || m >= (1u << 24)) return LUNSUP;
 
     // ---- per-actor seq ranges -> first-arrival table size ----
-    if (tid < LA_MAX) { sh.base[tid] = 0xFFFFFFFFu; sh.maxs[tid] = 0; sh.clock[tid] = 0; sh.bclock[tid] = 0;
+    if (tid < LA_ACT) { sh.base[tid] = 0xFFFFFFFFu; sh.maxs[tid] = 0; sh.clock[tid] = 0; sh.bclock[tid] = 0;
                         sh.headv[tid] = 0; sh.maxad[tid] = 0; }
     if (tid == 0) { sh.flags = 0; sh.errkey = ~0ull; sh.all_ok = 1; sh.H = 0; sh.nins = 0; sh.total = 0; sh.lists = 0; sh.ctrs = 0; sh.late = 0; }
     bsync();
@@ -1451,28 +1452,31 @@ __device__ HML_DOC_ATTR Outcome merge_doc_large(const SmallParams &p, Shared &sh
             }
         }
     }
-    // literal fold, history order, lanes = actors (wave 0)
+    // literal fold, history order, lanes = actors (wave 0; actors a0 + lane per 64-actor slice)
     if (!closure_ok && wave == 0) {
         for (uint32_t h = 0; h < H; h++) {
             const uint32_t ci = X.h2a[h];
             const hm_change_row c = CH[ci];
-            uint32_t acc = 0;
-            auto fold = [&](uint32_t a, uint32_t s) {
-                if (s == 0) return;
-                const uint32_t dc = tabv(slot_of(a, s));           // the applied change (a, s)
-                const uint32_t t = lane < A ? ad_row(p, doc, dc)[lane] : 0;
-                acc = acc > t ? acc : t;
-                if (lane == a) acc = s;
-            };
-            bool own = false;
-            for (uint32_t j = 0; j < c.n_deps; j++) {
-                const hm_dep_row dp = p.deps[c.dep_off + j];
-                if (dp.actor == c.actor) { own = true; fold(c.actor, c.seq - 1); }
-                else fold(dp.actor, dp.seq);
+            for (uint32_t a0 = 0; a0 < S; a0 += 64) {
+                const uint32_t la = a0 + lane;
+                uint32_t acc = 0;
+                auto fold = [&](uint32_t a, uint32_t s) {
+                    if (s == 0) return;
+                    const uint32_t dc = tabv(slot_of(a, s));       // the applied change (a, s)
+                    const uint32_t t = la < A ? ad_row(p, doc, dc)[la] : 0;
+                    acc = acc > t ? acc : t;
+                    if (la == a) acc = s;
+                };
+                bool own = false;
+                for (uint32_t j = 0; j < c.n_deps; j++) {
+                    const hm_dep_row dp = p.deps[c.dep_off + j];
+                    if (dp.actor == c.actor) { own = true; fold(c.actor, c.seq - 1); }
+                    else fold(dp.actor, dp.seq);
+                }
+                if (!own) fold(c.actor, c.seq - 1);
+                if (la < S) ad_row(p, doc, ci)[la] = la < A ? acc : 0;
+                if (la < A) sh.maxad[la] = sh.maxad[la] > acc ? sh.maxad[la] : acc;
             }
-            if (!own) fold(c.actor, c.seq - 1);
-            if (lane < S) ad_row(p, doc, ci)[lane] = lane < A ? acc : 0;
-            if (lane < A) sh.maxad[lane] = sh.maxad[lane] > acc ? sh.maxad[lane] : acc;
             wfence();                                          // rows are re-read by later changes
         }
         // rows of unapplied changes are zero

@@ -331,7 +331,7 @@ int hm_store_create(hm_engine *e, const hm_store_config *cfg, hm_store **out) {
     if (!e || !out) return HM_ERR_INVALID;
     *out = nullptr;
     const uint32_t S = cfg ? cfg->a_stride : 8;
-    if (S == 0 || S > 64) return hm_engine_fail(e, HM_ERR_INVALID, "store a_stride must be in [1,64]");
+    if (S == 0 || S > HM_MAX_STRIDE) return hm_engine_fail(e, HM_ERR_INVALID, "store a_stride must be in [1,256]");
     hm_store *s = new (std::nothrow) hm_store();
     if (!s) return HM_ERR_NOMEM;
     s->e = e; s->S = S;

@@ -74,17 +74,24 @@ __global__ __launch_bounds__(SWG) void append_kernel(const AppendDesc *descs, ui
             uint4 *dop = reinterpret_cast<uint4 *>(dst.ops + o_at);
             for (uint32_t i = t; i < 2 * D.n_new_o; i += W) dop[i] = so[i];
         }
-        // rank-indexed per-document rows follow the remap
-        if (rm && t == 0) {
+        // rank-indexed per-document rows follow the remap: lane t gathers the new ranks t + 64k
+        // (k < 4: S <= HM_MAX_STRIDE) from every old rank, all loads before any store (one wave)
+        if (rm) {
             uint32_t *rows[2] = {dst.min_clock + (size_t)D.handle * S, dst.stored_clock + (size_t)D.handle * S};
             for (int w = 0; w < 2; w++) {
-                uint32_t tmp[64];
-                for (uint32_t a = 0; a < S && a < 64; a++) tmp[a] = 0;
-                for (uint32_t a = 0; a < S && a < 64; a++) {
+                uint32_t v0 = 0, v1 = 0, v2 = 0, v3 = 0;
+                for (uint32_t a = 0; a < S; a++) {
                     const uint32_t na = mp[a];
-                    if (na < S && na < 64) tmp[na] = rows[w][a];
+                    if (na >= S || (na & 63) != t) continue;
+                    const uint32_t x = rows[w][a];
+                    const uint32_t k = na >> 6;
+                    v0 = k == 0 ? x : v0; v1 = k == 1 ? x : v1; v2 = k == 2 ? x : v2; v3 = k == 3 ? x : v3;
                 }
-                for (uint32_t a = 0; a < S && a < 64; a++) rows[w][a] = tmp[a];
+                __builtin_amdgcn_wave_barrier();
+                if (t < S) rows[w][t] = v0;
+                if (t + 64 < S) rows[w][t + 64] = v1;
+                if (t + 128 < S) rows[w][t + 128] = v2;
+                if (t + 192 < S) rows[w][t + 192] = v3;
             }
         }
     }
@@ -216,7 +223,8 @@ __device__ bool inc_doc(const AppendDesc &D, const IncArenas &A, const IncDims &
     uint8_t *wla = lds + M.o_wla;
 
     const uint32_t hist_len = uni(A.res_docs[h].hist_len), n_old_surv = uni(A.res_docs[h].n_surv);
-    if (NA > S || nnc == 0 || nnc > M.new_c || nno > 64 || D.n_r > M.regs || n_old_surv > M.surv || D.n_old_r > D.n_r)
+    // (lane-per-actor rows: wide strides re-merge; survivor actor bytes keep 7 bits)
+    if (S > 64 || NA > S || nnc == 0 || nnc > M.new_c || nno > 64 || D.n_r > M.regs || n_old_surv > M.surv || D.n_old_r > D.n_r)
         return false;
     const bool staged = D.n_old_c <= M.stage;
 
@@ -614,11 +622,14 @@ __global__ void plan_kernel(PlanArgs a) {
     bool remapped = false;
     if (live && !err && a.remap) {
         const uint8_t *mp = a.remap + (size_t)i * a.S;
-        unsigned long long used = 0;
+        unsigned long long u0 = 0, u1 = 0, u2 = 0, u3 = 0;          // ranks taken (S <= 256)
         for (uint32_t x = 0; x < m.n_actors; x++) {
-            if (mp[x] >= r.n_actors || ((used >> mp[x]) & 1ull)) { err |= HM_PLAN_REMAP; break; }
-            used |= 1ull << mp[x];
-            remapped |= mp[x] != x;
+            const uint32_t y = mp[x], k = y >> 6;
+            const unsigned long long b = 1ull << (y & 63);
+            const unsigned long long u = k == 0 ? u0 : (k == 1 ? u1 : (k == 2 ? u2 : u3));
+            if (y >= r.n_actors || (u & b)) { err |= HM_PLAN_REMAP; break; }
+            u0 |= k == 0 ? b : 0ull; u1 |= k == 1 ? b : 0ull; u2 |= k == 2 ? b : 0ull; u3 |= k == 3 ? b : 0ull;
+            remapped |= y != x;
         }
     }
     if (__ballot(err != 0)) {                                     // (rare) one atomic per failing lane

@@ -134,9 +134,14 @@ typedef struct {
     uint64_t value;       /* int64 / f64 bits / string id / object id, by vtag */
 } hm_op_row;
 
+/* Widest per-actor row (actors per document): the reference mints one actor per writer
+ * (src/RepoBackend.ts:286-293), so a shared document can have many.  Documents of more than
+ * 8 actors merge in the general kernel; rows wider than 64 are the "wide" strides. */
+#define HM_MAX_STRIDE 256u
+
 typedef struct {
     uint32_t n_docs, n_changes, n_deps, n_ops, n_regs;
-    uint32_t a_stride;    /* >= max n_actors; stride of every per-actor output row */
+    uint32_t a_stride;    /* >= max n_actors; stride of every per-actor output row (1..HM_MAX_STRIDE) */
     /* per-document maxima over the batch (launch sizing hints); 0 = unknown,
      * computed by the engine from the doc table */
     uint32_t max_changes, max_ops, max_regs, max_objs;

@@ -65,3 +65,20 @@ def test_oracle_envelope_precedence(name, changes, mutate, expect):
     got = doc_summary(b, O.merge(b), 0)
     for k, v in expect.items():
         assert got.get(k) == v, (name, k, got)
+
+
+@pytest.mark.parametrize("S", [128, 256])
+def test_oracle_wide_rows(S):
+    """More than 64 actors (one per writer, src/RepoBackend.ts:286-293): concurrent sets keep
+    every writer's value, the highest actor string wins (A.2), clocks span the wide row."""
+    from hypermerge_amd.columnar import ROOT_ID as R
+    n = S - 1 if S == 256 else 100
+    changes = [{"actor": f"w{i:03d}", "seq": 1, "deps": {}, "ops": [{"action": "set", "obj": R, "key": "x", "value": i}]}
+               for i in range(n)]
+    changes.append({"actor": "w000", "seq": 2, "deps": {f"w{i:03d}": 1 for i in range(n)},
+                    "ops": [{"action": "set", "obj": R, "key": "y", "value": "last"}]})
+    b = encode([changes], a_stride=S)
+    got = doc_summary(b, O.merge(b), 0)
+    assert got["status"] == "OK" and len(got["clock"]) == n and got["deps"] == {"w000": 2}
+    x = dict(got["state"]["map"])["x"]
+    assert x["value"] == n - 1 and len(x["conflicts"]) == n - 1
