@@ -30,6 +30,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 #include "../../include/hypermerge_amd.h"
 #include "engine_internal.h"
@@ -210,6 +211,18 @@ struct DocSt {
     std::vector<uint8_t> obj_type, obj_emitted;
     std::vector<uint64_t> sig;                               // per register: rendered entry hash, 0 = absent
     std::vector<std::pair<uint32_t, std::vector<uint32_t>>> lists;   // list object -> visible element registers
+    // the per-op patch base (op_diffs): the log's op rows, and the document as the last
+    // applied op left it — per register its survivors (winner first), per list element its
+    // insertion and place in the insertion tree, per list object its reachable elements in
+    // document order
+    std::vector<hm_op_row> oplog;
+    std::vector<uint32_t> op_seq;                            // per op: its change's seq
+    std::vector<uint32_t> ch_op0;                            // per change: its first op
+    std::vector<std::vector<hm_surv_result>> rs;             // per register
+    std::vector<uint32_t> el_op;                             // per register: its ins op, or HM_NONE
+    std::vector<uint8_t> el_in;                              // per register: placed in its list's order
+    std::unordered_map<uint32_t, std::vector<uint32_t>> kids;      // parent key -> children, (elem, actor) descending
+    std::vector<std::pair<uint32_t, std::vector<uint32_t>>> ord;    // list object -> placed elements in document order
     void setup() {
         bool f;
         objs.get(ROOT_ID, 36, 0, f);
@@ -250,6 +263,11 @@ struct DocSt {
         if (!make) return nullptr;
         lists.emplace_back(obj, std::vector<uint32_t>());
         return &lists.back().second;
+    }
+    static std::vector<uint32_t> &keyed(std::vector<std::pair<uint32_t, std::vector<uint32_t>>> &v, uint32_t k) {
+        for (auto &x : v) if (x.first == k) return x.second;
+        v.emplace_back(k, std::vector<uint32_t>());
+        return v.back().second;
     }
 };
 
@@ -305,6 +323,8 @@ struct Round {
     uint32_t q0 = 0, q1 = 0;                                 // its register requests
     std::string patch, bclock, cclock;
     BinDoc bin;
+    uint32_t h0 = 0, h1 = 0, prev_hist = 0;                  // op diffs: its rows of the class's history slices
+    std::vector<uint32_t> touched;                           // op diffs: the registers its applied ops hit
 };
 
 struct Scratch {
@@ -855,6 +875,165 @@ void render_diffs(W &w, DocSt &d, const uint32_t *req, const hm_reg_result *rows
     }
 }
 
+// ---------------- per-op diffs (Automerge makePatch) ----------------
+// Automerge collects one diff per applied op, in application order: `create` per make op,
+// per map assign the key's state after it (`set` with the winner and its conflicts, or
+// `remove`), per list-element assign `insert` / `set` / `remove` at the element's index at
+// that moment, nothing for `ins` (oracle/js/backend.js:92-170 restates the same sequence).
+// The GPU fixes what was applied and in which order (the round's history slice, with every
+// applied change's allDeps row: hm_store_read_history); the renderer walks those changes' ops
+// over the patch base — per register the survivors the previous op left, per list the
+// insertion tree and document order of the placed elements — applying exactly
+// applyAssign's filter (isConcurrent reduces to allDeps(new)[x.actor] < x.seq: nothing
+// resident depends on the new op), inc's counter sums and the sortBy(actor).reverse(), and
+// RGA placement ((elem, actor) descending siblings, pre-order), to know each op's diff.  The
+// registers it ends on are compared with the device's merged registers afterwards.
+struct Replay {
+    DocSt &d;
+    uint32_t S;
+    static uint32_t pkey(const hm_op_row &o) { return o.parent == HM_HEAD ? (0x80000000u | o.obj) : o.parent; }
+    static uint32_t find(const std::vector<uint32_t> &v, uint32_t x) {
+        return (uint32_t)(std::find(v.begin(), v.end(), x) - v.begin());
+    }
+    uint32_t rank(uint32_t op) const { return d.rank_of[d.op_actor[op]]; }
+    // lamportCompare (elem, actor) of two element registers: a after b in sibling order?
+    bool sib_before(uint32_t a, uint32_t b) const {
+        const uint32_t oa = d.el_op[a], ob = d.el_op[b];
+        if (d.oplog[oa].elem != d.oplog[ob].elem) return d.oplog[oa].elem > d.oplog[ob].elem;
+        return rank(oa) > rank(ob);
+    }
+    // applyInsert: the element joins its parent's children; once its chain reaches _head it
+    // (and any subtree inserted under it earlier) takes its pre-order place
+    void insert(uint32_t k) {
+        const hm_op_row &o = d.oplog[k];
+        const uint32_t e = o.reg;
+        d.el_op[e] = k;
+        std::vector<uint32_t> &sib = d.kids[pkey(o)];
+        uint32_t i = 0;
+        while (i < sib.size() && sib_before(sib[i], e)) i++;
+        sib.insert(sib.begin() + i, e);
+        if (o.parent != HM_HEAD && !(o.parent < d.el_in.size() && d.el_in[o.parent])) return;
+        std::vector<uint32_t> &ov = DocSt::keyed(d.ord, o.obj);
+        uint32_t pos;
+        if (i == 0) pos = o.parent == HM_HEAD ? 0u : find(ov, o.parent) + 1;
+        else if (i + 1 < sib.size()) pos = find(ov, sib[i + 1]);
+        else {                                               // after the parent's subtree
+            pos = (uint32_t)ov.size();
+            for (uint32_t x = o.parent; x != HM_HEAD;) {
+                const hm_op_row &xo = d.oplog[d.el_op[x]];
+                const std::vector<uint32_t> &xs = d.kids[pkey(xo)];
+                const uint32_t j = find(xs, x);
+                if (j + 1 < xs.size()) { pos = find(ov, xs[j + 1]); break; }
+                x = xo.parent;
+            }
+        }
+        std::vector<uint32_t> sub, stk{e};
+        while (!stk.empty()) {
+            const uint32_t x = stk.back();
+            stk.pop_back();
+            sub.push_back(x);
+            d.el_in[x] = 1;
+            auto it = d.kids.find(x);
+            if (it != d.kids.end())
+                for (size_t c = it->second.size(); c-- > 0;) stk.push_back(it->second[c]);
+        }
+        ov.insert(ov.begin() + pos, sub.begin(), sub.end());
+    }
+    uint32_t visible_before(uint32_t obj, uint32_t e) {
+        const std::vector<uint32_t> &ov = DocSt::keyed(d.ord, obj);
+        uint32_t n = 0;
+        for (uint32_t x : ov) {
+            if (x == e) break;
+            n += !d.rs[x].empty();
+        }
+        return n;
+    }
+    static bool numeric(uint32_t vt) { return vt == HM_V_INT || vt == HM_V_FLOAT; }
+    static double num(uint32_t vt, uint64_t v) {
+        if (vt == HM_V_INT) return (double)(int64_t)v;
+        double x;
+        memcpy(&x, &v, 8);
+        return x;
+    }
+    // applyAssign (A.2) of op k of a change whose allDeps row is ad
+    template <typename W>
+    void assign(W &w, uint32_t k, const uint32_t *ad) {
+        const hm_op_row &o = d.oplog[k];
+        std::vector<hm_surv_result> &sv = d.rs[o.reg];
+        const bool was = !sv.empty();
+        auto concurrent = [&](const hm_surv_result &x) {
+            const uint32_t r = rank(x.op);
+            return (r < S ? ad[r] : 0u) < d.op_seq[x.op];
+        };
+        if (o.action == HM_INC) {
+            for (hm_surv_result &x : sv) {
+                if (d.oplog[x.op].datatype != HM_DT_COUNTER || !numeric(x.vtag) || concurrent(x)) continue;
+                if (x.vtag == HM_V_INT && o.vtag == HM_V_INT) x.value = (uint64_t)((int64_t)x.value + (int64_t)o.value);
+                else {
+                    const double r = num(x.vtag, x.value) + num(o.vtag, o.value);
+                    memcpy(&x.value, &r, 8);
+                    x.vtag = HM_V_FLOAT;
+                }
+            }
+        } else {
+            sv.erase(std::remove_if(sv.begin(), sv.end(), [&](const hm_surv_result &x) { return !concurrent(x); }), sv.end());
+        }
+        if (o.action == HM_SET || o.action == HM_LINK) {
+            hm_surv_result y;
+            y.op = k; y.vtag = o.vtag; y.value = o.value;
+            sv.push_back(y);
+        }
+        std::stable_sort(sv.begin(), sv.end(), [&](const hm_surv_result &a, const hm_surv_result &b) { return rank(a.op) < rank(b.op); });
+        std::reverse(sv.begin(), sv.end());
+        const uint8_t t = o.obj < d.obj_type.size() && d.obj_type[o.obj] != NO_TYPE ? d.obj_type[o.obj] : (uint8_t)HM_MAKE_MAP;
+        if (t != HM_MAKE_LIST && t != HM_MAKE_TEXT) {
+            if (sv.empty()) w.map_remove(t, o.obj, o.reg);
+            else w.map_set(t, o.obj, o.reg, sv.data(), (uint32_t)sv.size());
+            return;
+        }
+        // updateListElement
+        if (was) {
+            const uint32_t i = visible_before(o.obj, o.reg);
+            if (sv.empty()) w.list_remove(t, o.obj, i);
+            else w.list_set(t, o.obj, i, sv.data(), (uint32_t)sv.size());
+        } else if (!sv.empty() && o.reg < d.el_in.size() && d.el_in[o.reg]) {
+            w.list_insert(t, o.obj, visible_before(o.obj, o.reg), o.reg, sv.data(), (uint32_t)sv.size());
+        }
+    }
+    // the round: n applied changes (log indices, application order) with their allDeps rows
+    template <typename W>
+    void round(W &w, const uint32_t *log, const uint32_t *ads, uint32_t n, std::vector<uint32_t> &touched) {
+        for (uint32_t r = 0; r < n; r++) {
+            const uint32_t ci = log[r];
+            const uint32_t k0 = d.ch_op0[ci], k1 = ci + 1 < d.ch_op0.size() ? d.ch_op0[ci + 1] : (uint32_t)d.oplog.size();
+            for (uint32_t k = k0; k < k1; k++) {
+                const hm_op_row &o = d.oplog[k];
+                if (o.action <= HM_MAKE_TEXT) { w.create(o.obj, o.action); continue; }
+                if (o.action == HM_INS) { insert(k); continue; }
+                if (o.reg == HM_NONE || o.reg >= d.rs.size()) continue;
+                assign(w, k, ads + (size_t)r * S);
+                touched.push_back(o.reg);
+            }
+        }
+        std::sort(touched.begin(), touched.end());
+        touched.erase(std::unique(touched.begin(), touched.end()), touched.end());
+    }
+};
+
+// a replayed register against the device's merged register (numbers compared by value)
+bool same_register(const DocSt &d, uint32_t g, const hm_reg_result &r, const hm_surv_result *sv) {
+    const std::vector<hm_surv_result> &h = d.rs[g];
+    if (h.size() != r.n_surv) return false;
+    for (uint32_t i = 0; i < r.n_surv; i++) {
+        const hm_surv_result &a = h[i], &b = sv[r.surv_off + i];
+        if (a.op != b.op) return false;
+        if (Replay::numeric(a.vtag) && Replay::numeric(b.vtag)) {
+            if (Replay::num(a.vtag, a.value) != Replay::num(b.vtag, b.value)) return false;
+        } else if (a.vtag != b.vtag || a.value != b.value) return false;
+    }
+    return true;
+}
+
 // the document as the patch base holds it: {uuid: {type, keys: [[key, entry]], elems: [[elemId, entry]]}}
 void render_view(std::string &o, const DocSt &d, const hm_reg_result *rows, const hm_surv_result *surv, uint32_t n_regs) {
     std::vector<std::string> keys(d.obj_type.size()), elems(d.obj_type.size());
@@ -904,6 +1083,7 @@ struct hm_docset {
     uint32_t threads = 16;
     bool patches = true;
     bool binary = false;                                     // HM_DOCSET_BINARY results
+    bool op_diffs = true;                                    // Automerge's per-op diff sequence (else HM_DOCSET_NET_DIFFS)
     hm_store *stores[N_CLASS] = {};
     // documents: fixed chunks, so hm_docset_open may run while a call works on earlier documents
     static constexpr uint32_t CHUNK = 4096;
@@ -911,7 +1091,8 @@ struct hm_docset {
     std::atomic<uint32_t> n_docs{0};
     std::mutex open_mu;
     std::atomic<bool> busy{false};
-    uint64_t stat[8] = {0, 0, 0, 0, 0, 0, 0, 0};           // rounds, docs, restrides, hit-register patches, full patches
+    uint64_t stat[8] = {0, 0, 0, 0, 0, 0, 0, 0};           // rounds, docs, restrides, hit-register patches, full patches,
+                                                             // per-op patches, replay mismatches
     DocSt &doc(uint32_t i) { return chunks[i / CHUNK][i % CHUNK]; }
 };
 
@@ -1087,7 +1268,7 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
     }
     mark("merge");
     // commit or roll back each document; the registers each patch reads
-    std::vector<std::vector<uint32_t>> qdocs(N_CLASS), qregs(N_CLASS);
+    std::vector<std::vector<uint32_t>> qdocs(N_CLASS), qregs(N_CLASS), hreq(N_CLASS);
     std::vector<uint32_t> cap(N_CLASS, 0);
     for (uint32_t i = 0; i < n; i++) {
         Round &x = R[i];
@@ -1099,6 +1280,7 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
             continue;
         }
         const uint32_t prev_hist = d.hist_len, prev_q = d.n_queued, old_n_ops = d.n_ops;
+        x.prev_hist = prev_hist;
         d.cls = x.cls; d.handle = x.handle;
         d.flags |= x.flags;
         d.n_changes += (uint32_t)x.ch.size();
@@ -1109,8 +1291,20 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
         d.sig.resize(x.n_regs, 0);
         for (const hm_op_row &o : x.op)
             if (o.action <= HM_MAKE_TEXT && o.obj < d.obj_type.size() && d.obj_type[o.obj] == NO_TYPE) d.obj_type[o.obj] = o.action;
-        (void)old_n_ops;
         if (!ds->patches) continue;
+        if (ds->op_diffs) {
+            // the replay's view of the log (op indices are the store's: appended in order)
+            for (const hm_change_row &c : x.ch) {
+                d.ch_op0.push_back(old_n_ops + c.op_first);
+                d.op_seq.insert(d.op_seq.end(), c.n_ops, c.seq);
+            }
+            d.oplog.insert(d.oplog.end(), x.op.begin(), x.op.end());
+            d.rs.resize(x.n_regs);
+            d.el_op.resize(x.n_regs, HM_NONE);
+            d.el_in.resize(x.n_regs, 0);
+            hreq[x.cls].push_back(i);
+            continue;
+        }
         x.full = !(prev_q == 0 && x.res.n_queued == 0 && x.res.hist_len - prev_hist == x.ch.size());
         x.q0 = (uint32_t)qregs[x.cls].size();
         if (x.full) {
@@ -1143,6 +1337,28 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
                                 rsurv[c].data(), (uint32_t)rsurv[c].size(), &got);
         if (rc) return rc;
     }
+    // op diffs: each document's history slice of this round (the changes the GPU applied, in
+    // application order) with their allDeps rows
+    std::vector<std::vector<uint32_t>> hlog(N_CLASS), had(N_CLASS);
+    for (uint32_t c = 0; c < N_CLASS; c++) {
+        if (hreq[c].empty()) continue;
+        const uint32_t m = (uint32_t)hreq[c].size();
+        std::vector<uint32_t> hh(m), from(m), to(m), off(m + 1, 0);
+        for (uint32_t k = 0; k < m; k++) {
+            Round &x = R[hreq[c][k]];
+            const DocSt &d = ds->doc(x.doc);
+            hh[k] = x.handle;
+            to[k] = x.res.hist_len;
+            from[k] = x.prev_hist;
+            off[k + 1] = off[k] + (to[k] - from[k]);
+            x.h0 = off[k]; x.h1 = off[k + 1];
+            (void)d;
+        }
+        hlog[c].resize(std::max(1u, off[m]));                 // (rounds that applied nothing: no rows)
+        had[c].resize(std::max<size_t>(1, (size_t)off[m] * STRIDES[c]));
+        rc = hm_store_read_history(ds->stores[c], m, hh.data(), from.data(), to.data(), off.data(), hlog[c].data(), had[c].data());
+        if (rc) return rc;
+    }
     mark("read regs");
     // render every document's patch and DocBackend.clock
     auto round_clock = [](const Round &x, uint32_t *rc) {      // this call's changes alone (updateClock(changes))
@@ -1167,7 +1383,10 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
                 round_clock(x, rc);
                 w.clock(rc, x.n_actors);
                 w.begin();
-                if (ds->patches) {
+                if (ds->patches && ds->op_diffs) {
+                    Replay rp{d, STRIDES[x.cls]};
+                    rp.round(w, hlog[x.cls].data() + x.h0, had[x.cls].data() + (size_t)x.h0 * STRIDES[x.cls], x.h1 - x.h0, x.touched);
+                } else if (ds->patches) {
                     if (x.q1 > x.q0) render_diffs(w, d, qregs[x.cls].data() + x.q0, rrows[x.cls].data() + x.q0, rsurv[x.cls].data(), x.q1 - x.q0);
                     else render_diffs(w, d, nullptr, nullptr, nullptr, 0);
                 }
@@ -1196,7 +1415,10 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
                 o += ",\"deps\":";
                 jclock(o, d, x.heads, x.n_actors);
                 o += ",\"canUndo\":false,\"canRedo\":false,\"diffs\":[";
-                if (ds->patches) {
+                if (ds->patches && ds->op_diffs) {
+                    Replay rp{d, STRIDES[x.cls]};
+                    rp.round(w, hlog[x.cls].data() + x.h0, had[x.cls].data() + (size_t)x.h0 * STRIDES[x.cls], x.h1 - x.h0, x.touched);
+                } else if (ds->patches) {
                     if (x.q1 > x.q0) render_diffs(w, d, qregs[x.cls].data() + x.q0, rrows[x.cls].data() + x.q0, rsurv[x.cls].data(), x.q1 - x.q0);
                     else render_diffs(w, d, nullptr, nullptr, nullptr, 0);
                 }
@@ -1207,6 +1429,38 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
                 jclock(x.cclock, d, rc, x.n_actors);
             }
         });
+    }
+    if (ds->patches && ds->op_diffs) {
+        // the replay's registers against the device's merged registers
+        for (uint32_t c = 0; c < N_CLASS; c++) {
+            std::vector<uint32_t> vd, vr, vx;
+            uint32_t vcap = 0;
+            for (uint32_t i : hreq[c]) {
+                Round &x = R[i];
+                for (uint32_t g : x.touched) { vd.push_back(x.handle); vr.push_back(g); vx.push_back(i); }
+                vcap += x.res.n_surv;
+            }
+            if (vr.empty()) continue;
+            std::vector<hm_reg_result> gr(vr.size());
+            std::vector<hm_surv_result> gs(std::max<uint32_t>(vcap, 1));
+            uint32_t got = 0;
+            rc = hm_store_read_regs(ds->stores[c], (uint32_t)vr.size(), vd.data(), vr.data(), gr.data(), gs.data(),
+                                    (uint32_t)gs.size(), &got);
+            if (rc) return rc;
+            uint32_t bad_doc = HM_NONE;
+            for (size_t q = 0; q < vr.size(); q++) {
+                DocSt &d = ds->doc(R[vx[q]].doc);
+                bool ok = same_register(d, vr[q], gr[q], gs.data());
+                const uint32_t ob = gr[q].obj;
+                if (ok && !d.rs[vr[q]].empty() && ob < d.obj_type.size() &&
+                    (d.obj_type[ob] == HM_MAKE_LIST || d.obj_type[ob] == HM_MAKE_TEXT)) {
+                    Replay rp{d, STRIDES[c]};
+                    ok = gr[q].list_index == (int32_t)rp.visible_before(ob, vr[q]);
+                }
+                if (!ok && bad_doc != vx[q]) { ds->stat[6]++; bad_doc = vx[q]; }
+            }
+        }
+        for (uint32_t c = 0; c < N_CLASS; c++) ds->stat[5] += hreq[c].size();
     }
     std::string &s = out->s;
     s.clear();
@@ -1296,6 +1550,7 @@ int hm_docset_create(hm_engine *e, const hm_docset_config *cfg, hm_docset **out)
     ds->threads = cfg && cfg->threads ? cfg->threads : std::min<uint32_t>(16, hw);
     ds->patches = !(cfg && (cfg->flags & HM_DOCSET_NO_PATCHES));
     ds->binary = cfg && (cfg->flags & HM_DOCSET_BINARY);
+    ds->op_diffs = !(cfg && (cfg->flags & HM_DOCSET_NET_DIFFS));
     ds->chunks.reserve(1u << 16);
     *out = ds;
     return HM_OK;

@@ -638,6 +638,48 @@ int hm_store_read_regs(hm_store *s, uint32_t n, const uint32_t *doc_handles, con
     }
 }
 
+int hm_store_read_history(hm_store *s, uint32_t n, const uint32_t *doc_handles, const uint32_t *from, const uint32_t *to,
+                          const uint32_t *out_off, uint32_t *out_log_index, uint32_t *out_all_deps) {
+    if (!s || (n && (!doc_handles || !from || !to || !out_off || !out_log_index))) return HM_ERR_INVALID;
+    if (s->pending) return hm_engine_fail(s->e, HM_ERR_INVALID, "batch in flight");
+    try {
+        if (!n) return HM_OK;
+        for (uint32_t i = 0; i < n; i++)
+            if (to[i] < from[i] || out_off[i + 1] - out_off[i] != to[i] - from[i] || out_off[i + 1] < out_off[i])
+                return hm_engine_fail(s->e, HM_ERR_INVALID, "history slice rows do not match out_off");
+        const uint32_t rows = out_off[n], S = s->S;
+        hipStream_t st = hm_engine_stream(s->e);
+        auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+        const size_t o_h = 0, o_f = al(4 * (size_t)n), o_t = o_f + al(4 * (size_t)n), o_o = o_t + al(4 * (size_t)n),
+                     o_bad = o_o + al(4 * ((size_t)n + 1)), o_log = o_bad + 256, o_ad = o_log + al(4 * (size_t)rows + 4),
+                     total = o_ad + (out_all_deps ? al(4 * (size_t)rows * S + 4) : 0);
+        int rc = ensure_stage(s, total);
+        if (rc) return rc;
+        uint8_t *sp = s->stage.p;
+        SCHK(s, hipMemcpyAsync(sp + o_h, doc_handles, (size_t)n * 4, hipMemcpyHostToDevice, st));
+        SCHK(s, hipMemcpyAsync(sp + o_f, from, (size_t)n * 4, hipMemcpyHostToDevice, st));
+        SCHK(s, hipMemcpyAsync(sp + o_t, to, (size_t)n * 4, hipMemcpyHostToDevice, st));
+        SCHK(s, hipMemcpyAsync(sp + o_o, out_off, (size_t)n * 4, hipMemcpyHostToDevice, st));
+        SCHK(s, hipMemsetAsync(sp + o_bad, 0, 4, st));
+        SCHK(s, hipMemsetAsync(sp + o_log, 0xFF, 4 * (size_t)rows + 4, st));
+        SCHK(s, hm_launch_read_hist(n, (const uint32_t *)(sp + o_h), (const uint32_t *)(sp + o_f), (const uint32_t *)(sp + o_t),
+                                    (const uint32_t *)(sp + o_o), s->dm, s->n_handles, s->hist, s->all_deps, S,
+                                    (uint32_t *)(sp + o_log), out_all_deps ? (uint32_t *)(sp + o_ad) : nullptr,
+                                    (uint32_t *)(sp + o_bad), st));
+        uint32_t bad = 0;
+        SCHK(s, hipMemcpyAsync(&bad, sp + o_bad, 4, hipMemcpyDeviceToHost, st));
+        if (rows) SCHK(s, hipMemcpyAsync(out_log_index, sp + o_log, 4 * (size_t)rows, hipMemcpyDeviceToHost, st));
+        if (rows && out_all_deps) SCHK(s, hipMemcpyAsync(out_all_deps, sp + o_ad, 4 * (size_t)rows * S, hipMemcpyDeviceToHost, st));
+        SCHK(s, hipStreamSynchronize(st));
+        if (bad) return hm_engine_fail(s->e, HM_ERR_INVALID, "bad handle");
+        for (uint32_t r = 0; r < rows; r++)
+            if (out_log_index[r] == HM_NONE) return hm_engine_fail(s->e, HM_ERR_INVALID, "history slice past the history");
+        return HM_OK;
+    } catch (...) {
+        return hm_engine_fail(s->e, HM_ERR_NOMEM, "exception in hm_store_read_history");
+    }
+}
+
 int hm_doc_history_prefix(hm_store *s, uint32_t doc, uint32_t n, uint32_t *out) {
     if (!s || doc >= s->n_handles || (n && !out)) return HM_ERR_INVALID;
     if (s->pending) return hm_engine_fail(s->e, HM_ERR_INVALID, "batch in flight");

@@ -119,6 +119,10 @@ hipError_t hm_launch_rollback(const uint32_t *handles, uint32_t n, const hm_doc_
                               uint32_t *list, PlanStats *st, hipStream_t s);
 hipError_t hm_launch_init_docs(DevDoc *dm, uint32_t h0, uint32_t n, hipStream_t s);
 // chosen registers of resident documents by (handle, register): validated on the device
+hipError_t hm_launch_read_hist(uint32_t n, const uint32_t *handles, const uint32_t *from, const uint32_t *to,
+                               const uint32_t *out_off, const DevDoc *dm, uint32_t n_handles, const int32_t *hist,
+                               const uint32_t *all_deps, uint32_t S, uint32_t *out_log, uint32_t *out_ad, uint32_t *bad,
+                               hipStream_t s);
 hipError_t hm_launch_read_regs_h(uint32_t n, const uint32_t *handles, const uint32_t *regs, const DevDoc *dm,
                                  uint32_t n_handles, const hm_reg_result *rr, const hm_surv_result *surv,
                                  hm_reg_result *out_regs, hm_surv_result *out_surv, uint32_t cap, uint32_t *counter,

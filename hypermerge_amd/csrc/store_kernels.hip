@@ -773,6 +773,28 @@ __global__ void read_regs_h_kernel(uint32_t n, const uint32_t *handles, const ui
     out_regs[i] = r;
 }
 
+// history.slice(from, to) of many documents (the changes a round applied, in application order):
+// one 64-lane workgroup per request scans the document's history positions; change i with
+// from <= hist[i] < to lands at out_off + hist[i] - from (log index, and its allDeps row)
+__global__ void read_hist_kernel(uint32_t n, const uint32_t *handles, const uint32_t *from, const uint32_t *to,
+                                 const uint32_t *out_off, const DevDoc *dm, uint32_t n_handles, const int32_t *hist,
+                                 const uint32_t *all_deps, uint32_t S, uint32_t *out_log, uint32_t *out_ad, uint32_t *bad) {
+    for (uint32_t q = blockIdx.x; q < n; q += gridDim.x) {
+        const uint32_t h = handles[q];
+        if (h >= n_handles) { if (threadIdx.x == 0) atomicOr(bad, 1u); continue; }
+        const DevDoc m = dm[h];
+        const uint32_t f = from[q], t = to[q], o = out_off[q];
+        for (uint32_t i = threadIdx.x; i < m.n_c; i += blockDim.x) {
+            const int32_t p = hist[m.c_off + i];
+            if (p < 0 || (uint32_t)p < f || (uint32_t)p >= t) continue;
+            const uint32_t at = o + (uint32_t)p - f;
+            out_log[at] = i;
+            if (out_ad)
+                for (uint32_t a = 0; a < S; a++) out_ad[(size_t)at * S + a] = all_deps[((size_t)m.c_off + i) * S + a];
+        }
+    }
+}
+
 }  // namespace hms
 
 hipError_t hm_launch_plan(const PlanArgs &a, hipStream_t s) {
@@ -811,6 +833,17 @@ hipError_t hm_launch_read_regs_h(uint32_t n, const uint32_t *handles, const uint
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(hms::read_regs_h_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, handles, regs, dm, n_handles, rr,
                        surv, out_regs, out_surv, cap, counter, bad);
+    return hipGetLastError();
+}
+
+hipError_t hm_launch_read_hist(uint32_t n, const uint32_t *handles, const uint32_t *from, const uint32_t *to,
+                               const uint32_t *out_off, const DevDoc *dm, uint32_t n_handles, const int32_t *hist,
+                               const uint32_t *all_deps, uint32_t S, uint32_t *out_log, uint32_t *out_ad, uint32_t *bad,
+                               hipStream_t s) {
+    if (!n) return hipSuccess;
+    const uint32_t grid = n < 65535u ? n : 65535u;
+    hipLaunchKernelGGL(hms::read_hist_kernel, dim3(grid), dim3(64), 0, s, n, handles, from, to, out_off, dm, n_handles, hist,
+                       all_deps, S, out_log, out_ad, bad);
     return hipGetLastError();
 }
 

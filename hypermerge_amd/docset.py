@@ -16,6 +16,7 @@ from .decode import pack_offsets
 from .engine import Engine, lib
 
 NO_PATCHES = 1          # HM_DOCSET_NO_PATCHES
+NET_DIFFS = 4           # HM_DOCSET_NET_DIFFS
 
 
 class _Cfg(ctypes.Structure):
@@ -41,10 +42,10 @@ def _text(L, t) -> Tuple[str, np.ndarray]:
 
 
 class DocSet:
-    def __init__(self, engine: Engine, threads: int = 0, patches: bool = True):
+    def __init__(self, engine: Engine, threads: int = 0, patches: bool = True, net_diffs: bool = False):
         self._L, self.engine = lib(), engine
         h = ctypes.c_void_p()
-        cfg = _Cfg(threads, 0 if patches else NO_PATCHES)
+        cfg = _Cfg(threads, (0 if patches else NO_PATCHES) | (NET_DIFFS if net_diffs else 0))
         engine._check(self._L.hm_docset_create(engine._h, ctypes.byref(cfg), ctypes.byref(h)), "hm_docset_create")
         self._h = h
 
@@ -107,7 +108,7 @@ class DocSet:
         out = np.zeros(8, np.uint64)
         self.engine._check(self._L.hm_docset_stats(self._h, out.ctypes.data), "hm_docset_stats")
         return {"calls": int(out[0]), "docs": int(out[1]), "moves": int(out[2]), "hit_patches": int(out[3]),
-                "full_patches": int(out[4])}
+                "full_patches": int(out[4]), "op_patches": int(out[5]), "replay_mismatch": int(out[6])}
 
 
 # ---- test helpers: the frontend's view of a document rebuilt from patches ----
@@ -135,7 +136,7 @@ def apply_diffs(objects: Dict[str, Dict[str, Any]], diffs: Sequence[Dict[str, An
         elif d["action"] == "set":
             o["keys"][d["key"]] = e
         elif d["action"] == "remove":
-            del o["keys"][d["key"]]
+            o["keys"].pop(d["key"], None)          # a per-op remove may name an absent key
         else:
             raise ValueError(d)
 

@@ -222,7 +222,11 @@ class GpuEngine {
     this.devices = o.devices || [o.device || 0]
     this.mode = o.mode || 'batched'
     this.patches = o.patches !== false
-    this.docsets = this.devices.map((d) => addon.docsetCreate(d, o.threads || 0, this.patches, o.binary !== false))
+    // diffs: 'ops' (Automerge's per-op sequence in application order) or 'net' (the diffs that
+    // take the previous patch's document to this one)
+    this.diffs = o.diffs || 'ops'
+    this.docsets = this.devices.map((d) => addon.docsetCreate(d, o.threads || 0, this.patches, o.binary !== false,
+      this.diffs === 'net'))
     this.queues = new Map()          // state -> FIFO of jobs
     this.flushing = false
     this.scheduled = false
@@ -237,7 +241,7 @@ class GpuEngine {
   init(docId) { return new GpuBackendState(this, docId) }
 
   stats() {
-    const t = { calls: 0, docs: 0, moves: 0, hitPatches: 0, fullPatches: 0 }
+    const t = { calls: 0, docs: 0, moves: 0, hitPatches: 0, fullPatches: 0, opPatches: 0, replayMismatch: 0 }
     for (const ds of this.docsets) { const s = addon.docsetStats(ds); for (const k in t) t[k] += s[k] }
     return t
   }

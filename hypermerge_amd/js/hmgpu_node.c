@@ -627,20 +627,22 @@ static Docset *get_docset(napi_env env, napi_value v) {
 /* docsetCreate(device, threads, patches[, binary]) -> docset (binary: results in the HMP1 form) */
 static napi_value DocsetCreate(napi_env env, napi_callback_info info) {
     napi_value argv[4];
-    size_t argc = 4;
+    size_t argc = 5;
     if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < 3) {
         napi_throw_type_error(env, NULL, "missing arguments");
         return NULL;
     }
-    bool binary = false;
+    bool binary = false, net = false;
     if (argc >= 4) napi_get_value_bool(env, argv[3], &binary);
+    if (argc >= 5) napi_get_value_bool(env, argv[4], &net);
     Docset *d = (Docset *)calloc(1, sizeof(Docset));
     hm_config cfg = {(int)get_u32(env, argv[0]), 0};
     int st = hm_engine_create(&cfg, &d->engine);
     if (st) { free(d); return throw_status(env, NULL, st, "hm_engine_create"); }
     bool patches = true;
     napi_get_value_bool(env, argv[2], &patches);
-    hm_docset_config dc = {get_u32(env, argv[1]), (patches ? 0u : HM_DOCSET_NO_PATCHES) | (binary ? HM_DOCSET_BINARY : 0u)};
+    hm_docset_config dc = {get_u32(env, argv[1]), (patches ? 0u : HM_DOCSET_NO_PATCHES) | (binary ? HM_DOCSET_BINARY : 0u) |
+                                              (net ? HM_DOCSET_NET_DIFFS : 0u)};
     st = hm_docset_create(d->engine, &dc, &d->ds);
     if (st) { napi_value r = throw_status(env, d->engine, st, "hm_docset_create"); hm_engine_destroy(d->engine); free(d); return r; }
     napi_value out;
@@ -750,7 +752,7 @@ static void ds_call_js(napi_env env, napi_value cb, void *context, void *data) {
  * docset call except docsetOpen throws until every queued round has called back */
 static napi_value DocsetApply(napi_env env, napi_callback_info info) {
     napi_value argv[4];
-    size_t argc = 4;
+    size_t argc = 5;
     if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < 3) {
         napi_throw_type_error(env, NULL, "missing arguments");
         return NULL;
@@ -876,7 +878,7 @@ static napi_value DocsetInfo(napi_env env, napi_callback_info info) {
     return o;
 }
 
-/* docsetStats(docset) -> {calls, docs, moves, hitPatches, fullPatches} */
+/* docsetStats(docset) -> {calls, docs, moves, hitPatches, fullPatches, opPatches, replayMismatch} */
 static napi_value DocsetStats(napi_env env, napi_callback_info info) {
     napi_value argv[1];
     if (!get_args(env, info, 1, argv)) return NULL;
@@ -886,8 +888,8 @@ static napi_value DocsetStats(napi_env env, napi_callback_info info) {
     hm_docset_stats(d->ds, x);
     napi_value o;
     napi_create_object(env, &o);
-    const char *names[5] = {"calls", "docs", "moves", "hitPatches", "fullPatches"};
-    for (int i = 0; i < 5; i++) { napi_value v; napi_create_double(env, (double)x[i], &v); set(env, o, names[i], v); }
+    const char *names[7] = {"calls", "docs", "moves", "hitPatches", "fullPatches", "opPatches", "replayMismatch"};
+    for (int i = 0; i < 7; i++) { napi_value v; napi_create_double(env, (double)x[i], &v); set(env, o, names[i], v); }
     return o;
 }
 

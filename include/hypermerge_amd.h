@@ -352,6 +352,14 @@ int hm_doc_log(hm_store *s, uint32_t doc, hm_change_row *changes, hm_dep_row *de
  * order (src/RepoBackend.ts:572-576).  Returns the count written (<= n). */
 int hm_doc_history_prefix(hm_store *s, uint32_t doc, uint32_t n, uint32_t *out_log_index);
 
+/* history.slice(from[i], to[i]) of many documents at once (the changes one applyChanges round
+ * applied, in application order; patch rendering): request i writes
+ * rows out_off[i] .. out_off[i+1]-1 (out_off[i+1] - out_off[i] = to[i] - from[i]): the log index
+ * of each change and (out_all_deps optional, [rows * a_stride]) its allDeps row.
+ * HM_ERR_INVALID if a slice runs past the document's history. */
+int hm_store_read_history(hm_store *s, uint32_t n, const uint32_t *doc_handles, const uint32_t *from, const uint32_t *to,
+                          const uint32_t *out_off, uint32_t *out_log_index, uint32_t *out_all_deps);
+
 /* minimumClock row of a document (rank-indexed, 0 = absent); used for the
  * min_cmp of the next merges (Clock.cmp(DocBackend.clock, minimumClock)). */
 int hm_doc_set_min_clock(hm_store *s, uint32_t doc, const uint32_t *clock);
@@ -480,6 +488,8 @@ typedef struct {
 } hm_docset_config;
 #define HM_DOCSET_NO_PATCHES 1u   /* patches carry clock / deps only (no diffs, no register reads) */
 #define HM_DOCSET_BINARY 2u       /* hm_docset_apply's text is the binary form below instead of JSON */
+#define HM_DOCSET_NET_DIFFS 4u    /* diffs take the previous patch's document to the new one (one per changed
+                                     register) instead of Automerge's per-op sequence (the default) */
 /* Binary results ('HMP1', for a host that builds the patch objects itself instead of parsing
  * JSON; a call whose strings hold a lone surrogate falls back to the JSON form, first byte '{'):
  *   u32 header[8] = {0x31504D48, n_docs, n_strings, n_words, n_nums, blob_bytes, ascii, 0}
@@ -519,7 +529,9 @@ int hm_docset_clock_update(hm_docset *ds, uint32_t n, const uint32_t *docs, uint
                            hm_text **out_stored);
 /* the merged document: {uuid: {"type", "keys": [[key, entry]], "elems": [[elemId, entry]]}} */
 int hm_docset_view(hm_docset *ds, uint32_t doc, hm_text **out);
-/* counters: calls, documents, class moves, patches from the hit registers, patches from every register */
+/* counters: calls, documents, class moves, net patches from the hit registers, net patches from every
+ * register, per-op patches, per-op replays whose registers differ from the device's merged state
+ * (always 0 unless the renderer and the kernels disagree) */
 int hm_docset_stats(const hm_docset *ds, uint64_t *out8);
 
 /* ------------------------------------------------------------------ */

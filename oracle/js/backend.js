@@ -89,12 +89,25 @@ function getPrevious(obj, elemId) {
   }
 }
 
+// a diff's value fields: the winner's value (link / datatype), the other survivors as conflicts
+function valueFields(o) {
+  const r = { value: o.value }
+  if (o.action === 'link') r.link = true
+  if (o.datatype) r.datatype = o.datatype
+  return r
+}
+function entryFields(ops) {
+  const r = valueFields(ops[0])
+  if (ops.length > 1) r.conflicts = ops.slice(1).map((o) => Object.assign({ actor: o.actor }, valueFields(o)))
+  return r
+}
+
 function updateListElement(s, obj, elemId, diffs, objId) {
   const ops = obj.keys.get(elemId) || []
   let index = obj.elemIds.indexOf(elemId)
   if (index >= 0) {
     if (!ops.length) { obj.elemIds.splice(index, 1); diffs.push({ action: 'remove', type: obj.type, obj: objId, index }) }
-    else diffs.push({ action: 'set', type: obj.type, obj: objId, index, value: ops[0].value })
+    else diffs.push(Object.assign({ action: 'set', type: obj.type, obj: objId, index }, entryFields(ops)))
     return
   }
   if (!ops.length) return
@@ -107,7 +120,7 @@ function updateListElement(s, obj, elemId, diffs, objId) {
     if (index >= 0) break
   }
   obj.elemIds.splice(index + 1, 0, elemId)
-  diffs.push({ action: 'insert', type: obj.type, obj: objId, index: index + 1, elemId, value: ops[0].value })
+  diffs.push(Object.assign({ action: 'insert', type: obj.type, obj: objId, index: index + 1, elemId }, entryFields(ops)))
 }
 
 function applyAssign(s, op, diffs) {
@@ -127,7 +140,7 @@ function applyAssign(s, op, diffs) {
     .map((x) => x[0]).reverse()
   obj.keys.set(op.key, remaining)
   if (obj.type === 'list' || obj.type === 'text') updateListElement(s, obj, op.key, diffs, op.obj)
-  else if (remaining.length) diffs.push({ action: 'set', type: obj.type, obj: op.obj, key: op.key, value: remaining[0].value })
+  else if (remaining.length) diffs.push(Object.assign({ action: 'set', type: obj.type, obj: op.obj, key: op.key }, entryFields(remaining)))
   else diffs.push({ action: 'remove', type: obj.type, obj: op.obj, key: op.key })
 }
 

@@ -65,7 +65,7 @@ const tick = () => new Promise((r) => setImmediate(r))
     let nDiffs = 0
     for (const m of ready.concat(remote)) { applyDiffs(objects, m.patch.diffs); nDiffs += m.patch.diffs.length }
     return { state: render(objects, ROOT, 0), nDiffs, nonEmpty: x.msgs.filter((m) => m.patch && m.patch.diffs.length > 0).length,
-      incremental: engine.stats().hitPatches }
+      incremental: engine.stats().hitPatches + engine.stats().opPatches }
   })
   process.stdout.write(JSON.stringify({ docs: out }) + '\n')
 })().catch((e) => { console.error(e); process.exit(1) })

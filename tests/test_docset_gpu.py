@@ -59,8 +59,11 @@ def _run(ds, chunked, check_each_round=True):
     return ids, objects, logs, last
 
 
-@pytest.mark.parametrize("name,n", [("C2", 60), ("C4", 80), ("C5", 60), ("C3", 6)])
-def test_docset_rounds_equal_oracle(name, n):
+@pytest.mark.parametrize("name,n,net", [("C2", 60, False), ("C4", 80, False), ("C5", 60, False), ("C3", 6, False),
+                                        ("C5", 60, True), ("C3", 6, True)])
+def test_docset_rounds_equal_oracle(name, n, net):
+    """Per-op diffs (default) and net diffs (HM_DOCSET_NET_DIFFS) both rebuild the oracle's
+    document round after round; the per-op replay ends on the device's merged registers."""
     from hypermerge_amd import synth
     from hypermerge_amd.columnar import decode_doc
     from hypermerge_amd.docset import DocSet, render_objects, view_objects
@@ -68,7 +71,7 @@ def test_docset_rounds_equal_oracle(name, n):
     over = {"changes_per_actor": 30} if name == "C3" else {}
     b = synth.generate(synth.config(name, n_docs=n, **over))
     docs = [decode_doc(b, i) for i in range(b.n_docs)]
-    ds = DocSet(Engine(0))
+    ds = DocSet(Engine(0), net_diffs=net)
     ids, objects, logs, last = _run(ds, _chunks(docs, np.random.default_rng(7)), check_each_round=name != "C3")
     for i, d in enumerate(ids):
         s = _oracle(logs[i])
@@ -79,7 +82,11 @@ def test_docset_rounds_equal_oracle(name, n):
         assert [[logs[i][k]["actor"], logs[i][k]["seq"]] for k in order] == s["history"], i
         assert last[i][1]["clock"] == s["clock"] and last[i][2] == s["backend_clock"]
     st = ds.stats()
-    assert st["hit_patches"] > 0 and st["calls"] == 4
+    assert st["calls"] == 4
+    if net:
+        assert st["hit_patches"] > 0 and st["op_patches"] == 0
+    else:
+        assert st["op_patches"] > 0 and st["replay_mismatch"] == 0 and st["hit_patches"] == 0
 
 
 def test_docset_errors_roll_back():
@@ -137,7 +144,7 @@ def test_docset_moves_documents_to_wider_stores():
         assert render_objects(objects[i]) == json.loads(json.dumps(s["state"])), i
         assert render_objects(view_objects(ds.view(d))) == json.loads(json.dumps(s["state"])), i
         assert ds.info(d)["a_stride"] >= len(s["backend_clock"])
-    assert ds.stats()["moves"] > 0
+    assert ds.stats()["moves"] > 0 and ds.stats()["replay_mismatch"] == 0
 
 
 def test_docset_clock_update_matches_reference_sql():

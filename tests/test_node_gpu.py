@@ -107,6 +107,49 @@ def test_patch_diffs_rebuild_the_merged_document(name, n, mode, binary):
         assert sum(g["incremental"] for g in got) > 0
 
 
+@pytest.mark.parametrize("name,n,mode,binary,order", [("C5", 150, "batched", True, "arrival"),
+                                                      ("C5", 150, "async", False, "shuffled"),
+                                                      ("C2", 80, "batched", True, "arrival"),
+                                                      ("C3", 10, "batched", True, "arrival"),
+                                                      ("C3", 10, "async", True, "shuffled"),
+                                                      ("C4", 200, "async", True, "shuffled")])
+def test_patch_diff_sequence_equals_js_restatement(name, n, mode, binary, order):
+    """f2 / a12: every RemotePatchMsg / ReadyMsg patch of the GPU
+    drop-in — clock, deps and the diffs, one per applied op in application order (create,
+    map set/remove with conflicts, list insert/set/remove at the index of that moment) — equals
+    the JS restatement's patch for the same documents fed in the same chunks, including rounds
+    where queued changes apply later (shuffled arrival).  The device's merged registers equal
+    the per-op replay's end state (replayMismatch 0).  Automerge's own diff format is unpinned
+    (not vendored); the sequence rule is Appendix A.4's."""
+    import numpy as np
+    from hypermerge_amd import synth
+    from hypermerge_amd.columnar import decode_doc
+    over = {"changes_per_actor": 30} if name == "C3" else {}
+    b = synth.generate(synth.config(name, n_docs=n, **over))
+    docs = [decode_doc(b, i) for i in range(b.n_docs)]
+    rng = np.random.default_rng(29)
+    chunked = []
+    for chs in docs:
+        chs = list(chs)
+        if order == "shuffled":
+            rng.shuffle(chs)
+        cuts = sorted(rng.integers(1, len(chs) + 1, size=3))
+        chunked.append([chs[:cuts[0]], chs[cuts[0]:cuts[1]], chs[cuts[1]:cuts[2]], chs[cuts[2]:]])
+    p = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "run_patch_seq.js")],
+                       input=json.dumps({"docs": chunked, "mode": mode, "binary": binary}),
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    got = json.loads(p.stdout)
+    assert got["stats"]["replayMismatch"] == 0 and got["stats"]["opPatches"] > 0
+    n_diffs = 0
+    for i, d in enumerate(got["docs"]):
+        assert len(d["gpu"]) == len(d["cpu"]), i
+        for k, (g, c) in enumerate(zip(d["gpu"], d["cpu"])):
+            assert g == c, (i, k)
+            n_diffs += len(c.get("patch", {}).get("diffs", []))
+    assert n_diffs > 0
+
+
 def test_materialize_history_prefix():
     """MaterializeMsg (src/RepoBackend.ts:570-579): history.slice(0, n) replayed through
     Backend.applyChanges(Backend.init(), ...) — the reference's tests/repo.test.ts:129-164
