@@ -305,8 +305,9 @@ def _node_e2e(args):
     16.  `cpu` is the JS restatement (oracle/js/backend.js, BASELINE.md's second baseline) handed
     parsed Change objects, `cpu_blocks` the same with Actor.parseBlock (JSON.parse per block) in
     the timed region; `gpu` / `gpu_async` are the drop-in (GpuDocBackend over the docset, batched /
-    async mode, patch diffs on) handed the raw blocks, `gpu_objects` the drop-in handed Change
-    objects."""
+    async mode, patch diffs on: Automerge's per-op diff sequence, the same diffs as the JS
+    restatement) handed the raw blocks, `gpu_objects` the drop-in handed Change objects,
+    `gpu_async_net` the async drop-in with net diffs (one per changed register)."""
     import shutil
     import subprocess
     import tempfile
@@ -318,7 +319,7 @@ def _node_e2e(args):
     b = synth.generate(synth.config("C2", n_docs=args.node_docs), threads=min(16, os.cpu_count() or 1))
     docs = [decode_doc(b, i) for i in range(b.n_docs)]
     here = os.path.dirname(os.path.abspath(__file__))
-    legs = ["cpu", "cpu_blocks", "gpu", "gpu_async", "gpu_objects"]
+    legs = ["cpu", "cpu_blocks", "gpu", "gpu_async", "gpu_objects", "gpu_async_net"]
     with tempfile.TemporaryDirectory() as td:
         fn = os.path.join(td, "c2.json")
         with open(fn, "w") as f:
@@ -331,6 +332,7 @@ def _node_e2e(args):
     out = json.loads(p.stdout.strip().splitlines()[-1])
     out["same_clocks"] = len({out[k]["digest"] for k in legs}) == 1
     out["same_state"] = len({out[k]["state_digest"] for k in legs}) == 1
+    out["same_diff_count"] = len({out[k]["diffs"] for k in legs if k != "gpu_async_net"}) == 1
     out["sample"] = (f"C2: {b.n_docs} docs x 4 actors x 64 changes, 4 rounds of 16 changes per document "
                      f"(init + 3 applyRemoteChanges), one Node thread; blocks = JSON Change texts")
     out["gpu_async_vs_js"] = out["gpu_async"]["changes_per_s"] / out["cpu"]["changes_per_s"]

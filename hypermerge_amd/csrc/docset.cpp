@@ -983,8 +983,16 @@ struct Replay {
             y.op = k; y.vtag = o.vtag; y.value = o.value;
             sv.push_back(y);
         }
-        std::stable_sort(sv.begin(), sv.end(), [&](const hm_surv_result &a, const hm_surv_result &b) { return rank(a.op) < rank(b.op); });
+        // sortBy(actor).reverse() = reversed, then a stable sort by actor descending (insertion
+        // sort: a register holds a handful of survivors)
         std::reverse(sv.begin(), sv.end());
+        for (size_t i = 1; i < sv.size(); i++) {
+            const hm_surv_result x = sv[i];
+            const uint32_t rx = rank(x.op);
+            size_t j = i;
+            for (; j > 0 && rank(sv[j - 1].op) < rx; j--) sv[j] = sv[j - 1];
+            sv[j] = x;
+        }
         const uint8_t t = o.obj < d.obj_type.size() && d.obj_type[o.obj] != NO_TYPE ? d.obj_type[o.obj] : (uint8_t)HM_MAKE_MAP;
         if (t != HM_MAKE_LIST && t != HM_MAKE_TEXT) {
             if (sv.empty()) w.map_remove(t, o.obj, o.reg);
@@ -1430,6 +1438,7 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
             }
         });
     }
+    mark("diffs");
     if (ds->patches && ds->op_diffs) {
         // the replay's registers against the device's merged registers
         for (uint32_t c = 0; c < N_CLASS; c++) {
@@ -1447,20 +1456,28 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
             rc = hm_store_read_regs(ds->stores[c], (uint32_t)vr.size(), vd.data(), vr.data(), gr.data(), gs.data(),
                                     (uint32_t)gs.size(), &got);
             if (rc) return rc;
-            uint32_t bad_doc = HM_NONE;
-            for (size_t q = 0; q < vr.size(); q++) {
-                DocSt &d = ds->doc(R[vx[q]].doc);
-                bool ok = same_register(d, vr[q], gr[q], gs.data());
-                const uint32_t ob = gr[q].obj;
-                if (ok && !d.rs[vr[q]].empty() && ob < d.obj_type.size() &&
-                    (d.obj_type[ob] == HM_MAKE_LIST || d.obj_type[ob] == HM_MAKE_TEXT)) {
-                    Replay rp{d, STRIDES[c]};
-                    ok = gr[q].list_index == (int32_t)rp.visible_before(ob, vr[q]);
+            std::atomic<uint64_t> bad{0};
+            const uint32_t nq = (uint32_t)vr.size();
+            par_for(nq, std::min<uint32_t>(ds->threads, std::max<uint32_t>(1, nq / 4096)), [&](uint32_t lo, uint32_t hi, uint32_t) {
+                uint32_t bad_doc = HM_NONE;
+                uint64_t nb = 0;
+                for (uint32_t q = lo; q < hi; q++) {
+                    DocSt &d = ds->doc(R[vx[q]].doc);
+                    bool ok = same_register(d, vr[q], gr[q], gs.data());
+                    const uint32_t ob = gr[q].obj;
+                    if (ok && !d.rs[vr[q]].empty() && ob < d.obj_type.size() &&
+                        (d.obj_type[ob] == HM_MAKE_LIST || d.obj_type[ob] == HM_MAKE_TEXT)) {
+                        Replay rp{d, STRIDES[c]};
+                        ok = gr[q].list_index == (int32_t)rp.visible_before(ob, vr[q]);
+                    }
+                    if (!ok && bad_doc != vx[q]) { nb++; bad_doc = vx[q]; }
                 }
-                if (!ok && bad_doc != vx[q]) { ds->stat[6]++; bad_doc = vx[q]; }
-            }
+                bad += nb;
+            });
+            ds->stat[6] += bad.load();
         }
         for (uint32_t c = 0; c < N_CLASS; c++) ds->stat[5] += hreq[c].size();
+        mark("verify");
     }
     std::string &s = out->s;
     s.clear();

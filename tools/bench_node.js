@@ -104,9 +104,9 @@ function profStop() {
   }))
 }
 
-async function runGpu(mode, objects) {
+async function runGpu(mode, objects, diffsForm) {
   const G = require(path.join(__dirname, '..', 'hypermerge_amd', 'js', 'GpuDocBackend.js'))
-  const engine = new G.GpuEngine({ mode, patches: patchesOn })
+  const engine = new G.GpuEngine({ mode, patches: patchesOn, diffs: diffsForm || 'ops' })
   const settle = async () => { if (mode === 'async') await engine.idle(); else { await tick(); await tick() } }
   // warm the device (engine, stores, kernels) outside the timed region
   const w = new G.DocBackend('warm', () => {}, undefined, engine)
@@ -132,7 +132,9 @@ async function runGpu(mode, objects) {
   await profStop()
   const st = engine.stats()
   return { changes: nChanges, seconds: s, changes_per_s: nChanges / s, patches, diffs, submits: engine.submits,
-    patch_diffs: patchesOn, hit_register_patches: st.hitPatches - st0.hitPatches, full_patches: st.fullPatches - st0.fullPatches,
+    patch_diffs: patchesOn, diffs_form: engine.diffs, op_patches: st.opPatches - st0.opPatches,
+    replay_mismatch: st.replayMismatch - st0.replayMismatch,
+    hit_register_patches: st.hitPatches - st0.hitPatches, full_patches: st.fullPatches - st0.fullPatches,
     mode, input: objects ? 'Change objects' : 'raw blocks',
     digest: digest(docs.map((d) => ({ id: d.id, clock: d.clock, hist: d.back.histLen }))),
     state_digest: stateDigest(docs.map((d) => plain(G.materialize(d.back), '00000000-0000-0000-0000-000000000000'))) }
@@ -146,6 +148,7 @@ async function runGpu(mode, objects) {
     else if (m === 'gpu') out[m] = await runGpu('batched', false)
     else if (m === 'gpu_async') out[m] = await runGpu('async', false)
     else if (m === 'gpu_objects') out[m] = await runGpu('async', true)
+    else if (m === 'gpu_async_net') out[m] = await runGpu('async', false, 'net')
     else throw new Error(`unknown leg ${m}`)
   }
   process.stdout.write(JSON.stringify(out) + '\n')
