@@ -44,7 +44,7 @@
 #ifndef HM_STAMPS
 #define HM_STAMPS 0     // diagnostic builds only: per-phase s_memtime shares (tools/stamps.py); never timed
 #endif
-#define HM_NSTAMP 12
+#define HM_NSTAMP 13
 #ifndef HM_PREFETCH_EARLY
 #define HM_PREFETCH_EARLY 0 // 1: the next document's rows are loaded before this document's merge
 #endif
@@ -73,6 +73,16 @@
 #endif
 #ifndef HM_PRIO_K1
 #define HM_PRIO_K1 3        // through validation and the dependency pre-pass: C4 2.41 -> 2.37 ms
+#endif
+#ifndef HM_FENCE_MCMP
+#define HM_FENCE_MCMP 1     // pin Clock.cmp(DocBackend.clock, minimumClock) ahead of the next document's row loads
+#endif
+#ifndef HM_STAGE_FIRST
+#define HM_STAGE_FIRST 0    // 1: stage the next document's rows before this document's stores (A/B: C4 2.38 -> 2.44 ms, the
+                            // store outputs then waited in write_outputs on reused registers)
+#endif
+#ifndef HM_OPAQUE_LANE
+#define HM_OPAQUE_LANE 1    // per-document lane index the compiler cannot hoist out of the document loop
 #endif
 #ifndef HM_WAVES_PER_EU
 #define HM_WAVES_PER_EU 4   // register-allocator target: LDS already caps C4-class launches at ~4.25 waves/SIMD
@@ -140,6 +150,20 @@ __device__ __forceinline__ uint32_t bytesum64(u64 x) {
 // value of the previous lane (lane 0 reads 0)
 __device__ __forceinline__ uint32_t prev_lane(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_WAVE_SHR1, 0xF, 0xF, false);
+}
+// The lane index as a value computed inside the document loop: lane-based LDS addresses built
+// from threadIdx.x are loop-invariant, so the compiler hoists them out of the persistent loop and
+// keeps them live across the whole merge — at 128 VGPRs one of them was spilled to scratch, and
+// its reload (a global-latency round trip, s_waitcnt vmcnt(0)) sat in the survivor-offset scan
+// of every document.  An address built from this value is recomputed where it is used.
+__device__ __forceinline__ uint32_t fresh_lane() {
+#if HM_OPAQUE_LANE
+    uint32_t l;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(l) : "v"((uint32_t)threadIdx.x));
+    return l;
+#else
+    return threadIdx.x;
+#endif
 }
 // One-wave workgroups: a wave's LDS instructions execute in issue order, so an exchange
 // through LDS between lanes needs only a compiler ordering point — no s_waitcnt, no barrier
@@ -482,7 +506,11 @@ __device__ __noinline__ bool fold_differs(FoldView L, uint32_t dep0, uint32_t nd
 // by the stores) and written to LDS after those stores, so nothing stays live across
 // documents.  Named members only (no arrays): the struct is scalarised into VGPRs.
 struct Rows {
-    uint2 c0, c1, c2;                        // change row, lane < n_changes
+    uint4 c01;                               // change row (lane < n_changes): words 0-3 ...
+    uint2 c2;                                // ... and 4-5, held as the two loads fill them (a
+                                             // row split over three 8-byte members needed register
+                                             // moves inside the predicated load, i.e. a wait
+                                             // for the load right after its issue)
     uint4 a0, b0, a1, b1, a2, b2, a3, b3;    // op rows lane + 64 t (first / second 16 B)
     uint2 d0, d1;                            // dep rows lane, lane + 64
 };
@@ -505,10 +533,12 @@ template <int OPL>
 __device__ __forceinline__ Rows load_rows(const SmallParams &p, const hm_doc_row &doc) {
     const uint32_t lane = threadIdx.x;
     Rows r;
-    r.c0 = r.c1 = r.c2 = r.d0 = r.d1 = make_uint2(0, 0);
+    r.c01 = make_uint4(0, 0, 0, 0);
+    r.c2 = r.d0 = r.d1 = make_uint2(0, 0);
     if (lane < doc.n_changes) {
         const uint2 *cs = reinterpret_cast<const uint2 *>(p.changes + doc.change_off + lane);
-        r.c0 = cs[0]; r.c1 = cs[1]; r.c2 = cs[2];
+        const uint2 x0 = cs[0], x1 = cs[1];
+        r.c01 = make_uint4(x0.x, x0.y, x1.x, x1.y); r.c2 = cs[2];
     }
     load_op(p, doc, lane, r.a0, r.b0);
     if (OPL > 1) load_op(p, doc, lane + WAVE, r.a1, r.b1);
@@ -1174,8 +1204,9 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     if (HM_ABLATE & 4) return OUT_UNSUPPORTED;
     // survivor offsets: exclusive scan over register ids (a register's count = its byte sum)
     uint32_t total = 0;
+    const uint32_t lane_s = LISTS ? lane : fresh_lane();     // (list launches: no spill there; A/B C5 +2 % with it)
     for (uint32_t r0 = 0; r0 < R; r0 += WAVE) {
-        const uint32_t r = r0 + lane;
+        const uint32_t r = r0 + lane_s;
         uint32_t tot;
         const uint32_t cnt = r < R ? bytesum64(L.survpk[r]) : 0u;
         const uint32_t ex = wave_excl_scan(cnt, &tot);
@@ -1328,9 +1359,30 @@ __device__ __forceinline__ uint32_t min_cmp_of(const SmallParams &p, const Small
     return p.min_clock ? ((aGTE && bGTE) ? 0u : (aGTE ? 1u : (bGTE ? 2u : 3u))) : 0u;
 }
 
+// A merged document's survivor rows, read out of LDS into registers (lane + WAVE t): the next
+// document's rows overwrite the op tables they come from before these are stored.
+template <int OPL> struct SurvRows { hm_surv_result r[OPL]; };
+template <int OPL>
+__device__ __forceinline__ SurvRows<OPL> surv_rows(const SmallParams &p, const SmallLds &L, const DocState &st) {
+    const uint32_t lane = threadIdx.x;
+    SurvRows<OPL> o;
+#pragma unroll
+    for (int t = 0; t < OPL; t++) {
+        const uint32_t q = lane + WAVE * t;
+        const uint32_t k = q < st.total ? (L.survop[q] & 0xFFu) : 0u, mt = L.opmeta[k];
+        hm_surv_result sr;
+        sr.op = k; sr.vtag = (mt >> 16) & 0xFF; sr.value = op_value(L, k);
+        if (p.counters && q < st.total && (mt & 0xFF) == HM_SET && ((mt >> 8) & 0xFF) == HM_DT_COUNTER && sr.vtag == HM_V_INT)
+            sr.value = (u64)((int64_t)sr.value + L.survsum[q]);
+        o.r[t] = sr;
+    }
+    return o;
+}
+
 template <int OPL, bool LISTS>
 __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallLds &L, uint32_t d, uint32_t ds,
-                                              const hm_doc_row &doc, Outcome oc, const DocState &st, uint32_t mcmp) {
+                                              const hm_doc_row &doc, Outcome oc, const DocState &st, uint32_t mcmp,
+                                              const SurvRows<OPL> &sv) {
     const uint32_t lane = threadIdx.x;
     const uint32_t S = p.a_stride;
     const uint32_t n = doc.n_changes, A = doc.n_actors, R = doc.n_regs;
@@ -1417,15 +1469,7 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
 #pragma unroll
     for (int t = 0; t < OPL; t++) {
         const uint32_t q = lane + WAVE * t;
-        if (q >= st.total) continue;
-        const uint32_t k = L.survop[q] & 0xFFu, mt = L.opmeta[k];
-        const u64 v = op_value(L, k);
-        hm_surv_result sr;
-        sr.op = k; sr.vtag = (mt >> 16) & 0xFF; sr.value = v;
-        const uint32_t smt_t = mt;
-        if (p.counters && (smt_t & 0xFF) == HM_SET && ((smt_t >> 8) & 0xFF) == HM_DT_COUNTER && sr.vtag == HM_V_INT)
-            sr.value = (u64)((int64_t)sr.value + L.survsum[q]);
-        p.res_surv[doc.op_off + q] = sr;
+        if (q < st.total) p.res_surv[doc.op_off + q] = sv.r[t];
     }
 }
 
@@ -1452,7 +1496,7 @@ void merge_small_kernel(SmallParams p) {
     {
         const Rows r = load_rows<OPL>(p, doc);
         stage_rows<OPL, LISTS>(p, L, doc, r);
-        w0 = r.c0; w1 = r.c1; w2 = r.c2;
+        w0 = make_uint2(r.c01.x, r.c01.y); w1 = make_uint2(r.c01.z, r.c01.w); w2 = r.c2;
     }
     wave_sync();
     for (;;) {
@@ -1496,21 +1540,43 @@ void merge_small_kernel(SmallParams p) {
             if (__ballot(extra != 0) && threadIdx.x == NA_MAX) mc |= 1u;
         }
         const Outcome oc = !dok ? OUT_INVALID : in_env ? merge_doc_small<OPL, LISTS>(p, L, doc, w0, w1, w2, st) : OUT_UNSUPPORTED;
-        const uint32_t mcmp = oc == OUT_OK ? min_cmp_of(p, L, doc, mc) : 0u;
+        STAMP(L, 9);
+        uint32_t mcmp = oc == OUT_OK ? min_cmp_of(p, L, doc, mc) : 0u;
+#if HM_FENCE_MCMP
+        // computed here, not sunk to its use in write_outputs: there its wait for the minimumClock
+        // row (s_waitcnt vmcnt(0)) would also wait for the next document's row loads issued below
+        asm volatile("" : "+s"(mcmp) :: "memory");
+#endif
 #if !HM_PREFETCH_EARLY
         if (more) { take_docn(); dokn = check_doc(p, docn); next = load_rows<OPL>(p, docn); }
 #endif
-        STAMP(L, 9);
+        STAMP(L, 12);
         if (HM_PRIO_IO) __builtin_amdgcn_s_setprio(HM_PRIO_IO);
-        write_outputs<OPL, LISTS>(p, L, d, ds, doc, oc, st, mcmp);
+        const SurvRows<OPL> sv = surv_rows<OPL>(p, L, st);
+#if HM_STAGE_FIRST
+        // the next document's rows go to LDS before this document's stores are issued: a wait
+        // for a load also waits for every older store (vmcnt counts both in issue order), so
+        // staging after the stores waited for all of them; now nothing waits for the stores
+        // until the next document's merge has run
+        wave_sync();
+        if (more) stage_rows<OPL, LISTS>(p, L, docn, next);
+        STAMP(L, 11);
+        write_outputs<OPL, LISTS>(p, L, d, ds, doc, oc, st, mcmp, sv);
+        if (HM_PRIO_IO) __builtin_amdgcn_s_setprio(0);
+        wave_sync();
+        STAMP(L, 10);
+        if (!more) break;
+#else
+        write_outputs<OPL, LISTS>(p, L, d, ds, doc, oc, st, mcmp, sv);
         wave_sync();
         STAMP(L, 10);
         if (!more) break;
         stage_rows<OPL, LISTS>(p, L, docn, next);
         if (HM_PRIO_IO) __builtin_amdgcn_s_setprio(0);
-        w0 = next.c0; w1 = next.c1; w2 = next.c2;
         wave_sync();
         STAMP(L, 11);
+#endif
+        w0 = make_uint2(next.c01.x, next.c01.y); w1 = make_uint2(next.c01.z, next.c01.w); w2 = next.c2;
         d = dn;
         doc = docn;
         dok = dokn;
