@@ -70,6 +70,41 @@ function toChange(c) {
 // the parse (the round's strings decoded once, numbers read from a Float64Array).
 const TYPES = ['map', 'table', 'list', 'text']
 const ACTIONS = ['create', 'set', 'remove', 'insert']
+// One round's decoder state (module level: no closures per document — the per-op diff form
+// makes millions of small objects per round, and the garbage collector is the JS thread's
+// largest cost)
+const R = { w: null, nums: null, strs: null, p: 0, sb: 0, nb: 0 }
+function rdClock() {
+  const w = R.w, strs = R.strs, sb = R.sb
+  const c = {}
+  let p = R.p
+  for (let k = w[p++]; k > 0; k--) { c[strs[sb + w[p]]] = w[p + 1]; p += 2 }
+  R.p = p
+  return c
+}
+function rdValue(e) {
+  const v = R.w[R.p++], tag = v & 7, dt = (v >>> 3) & 3, pay = v >>> 5
+  switch (tag) {
+    case 0: e.value = null; break
+    case 1: e.value = false; break
+    case 2: e.value = true; break
+    case 3: case 4: e.value = R.nums[R.nb + pay]; break
+    case 5: e.value = R.strs[R.sb + pay]; break
+    case 6: e.value = R.strs[R.sb + pay]; e.link = true; break
+    default: e.value = null
+  }
+  if (dt === 1) e.datatype = 'counter'
+  else if (dt === 2) e.datatype = 'timestamp'
+}
+function rdEntry(e) {
+  const k = R.w[R.p++]
+  rdValue(e)
+  if (k > 1) {
+    const cs = new Array(k - 1)
+    for (let i = 1; i < k; i++) { const c = { actor: R.strs[R.sb + R.w[R.p++]], value: null }; rdValue(c); cs[i - 1] = c }
+    e.conflicts = cs
+  }
+}
 function decodeRound(buf, n) {
   if (buf.length === 0 || buf[0] === 0x7b) return JSON.parse(buf.toString())
   if (buf.byteOffset % 8) buf = Buffer.from(buf)           // a fresh, aligned copy
@@ -92,65 +127,39 @@ function decodeRound(buf, n) {
   } else {
     for (let i = 0; i < ns; i++) strs[i] = buf.toString('utf8', blobAt + soff[i], blobAt + soff[i + 1])
   }
+  R.w = w; R.nums = nums; R.strs = strs
   const P = new Array(n), B = new Array(n), C = new Array(n)
   for (let d = 0; d < n; d++) {
-    let p = woff[d]
-    if (p === woff[d + 1]) { P[d] = B[d] = C[d] = null; continue }
-    const sb = sbase[d], nb = nbase[d]
-    const clock = () => {
-      const c = {}
-      for (let k = w[p++]; k > 0; k--) { c[strs[sb + w[p]]] = w[p + 1]; p += 2 }
-      return c
-    }
-    const value = (e) => {
-      const v = w[p++], tag = v & 7, dt = (v >>> 3) & 3, pay = v >>> 5
-      switch (tag) {
-        case 0: e.value = null; break
-        case 1: e.value = false; break
-        case 2: e.value = true; break
-        case 3: case 4: e.value = nums[nb + pay]; break
-        case 5: e.value = strs[sb + pay]; break
-        case 6: e.value = strs[sb + pay]; e.link = true; break
-        default: e.value = null
-      }
-      if (dt === 1) e.datatype = 'counter'
-      else if (dt === 2) e.datatype = 'timestamp'
-    }
-    const entry = (e) => {
-      const k = w[p++]
-      value(e)
-      if (k > 1) {
-        const cs = new Array(k - 1)
-        for (let i = 1; i < k; i++) { const c = { actor: strs[sb + w[p++]] }; value(c); cs[i - 1] = c }
-        e.conflicts = cs
-      }
-    }
-    const patch = { clock: clock(), deps: clock(), canUndo: false, canRedo: false, diffs: null }
-    B[d] = clock()
-    C[d] = clock()
-    const nd = w[p++]
+    if (woff[d] === woff[d + 1]) { P[d] = B[d] = C[d] = null; continue }
+    R.p = woff[d]; R.sb = sbase[d]; R.nb = nbase[d]
+    const sb = R.sb
+    const patch = { clock: rdClock(), deps: rdClock(), canUndo: false, canRedo: false, diffs: null }
+    B[d] = rdClock()
+    C[d] = rdClock()
+    const nd = w[R.p++]
     const diffs = new Array(nd)
     for (let k = 0; k < nd; k++) {
-      const h = w[p++], action = h & 7, t = (h >>> 3) & 3
-      const obj = strs[sb + w[p++]]
+      const h = w[R.p++], action = h & 7, t = (h >>> 3) & 3
+      const obj = strs[sb + w[R.p++]]
       let e
       if (action === 0) e = { action: 'create', obj, type: TYPES[t] }
       else if (t < 2) {
-        e = { action: ACTIONS[action], type: TYPES[t], obj, key: strs[sb + w[p++]] }
-        if (action === 1) entry(e)
+        if (action === 1) { e = { action: 'set', type: TYPES[t], obj, key: strs[sb + w[R.p++]], value: null }; rdEntry(e) }
+        else e = { action: ACTIONS[action], type: TYPES[t], obj, key: strs[sb + w[R.p++]] }
       } else if (action === 3) {
-        e = { action: 'insert', type: TYPES[t], obj, index: w[p++], elemId: null }
-        e.elemId = strs[sb + w[p++]]
-        entry(e)
-      } else {
-        e = { action: ACTIONS[action], type: TYPES[t], obj, index: w[p++] }
-        if (action === 1) entry(e)
-      }
+        e = { action: 'insert', type: TYPES[t], obj, index: w[R.p++], elemId: null, value: null }
+        e.elemId = strs[sb + w[R.p++]]
+        rdEntry(e)
+      } else if (action === 1) {
+        e = { action: 'set', type: TYPES[t], obj, index: w[R.p++], value: null }
+        rdEntry(e)
+      } else e = { action: ACTIONS[action], type: TYPES[t], obj, index: w[R.p++] }
       diffs[k] = e
     }
     patch.diffs = diffs
     P[d] = patch
   }
+  R.w = R.nums = R.strs = null
   return { p: P, b: B, c: C }
 }
 
@@ -328,13 +337,26 @@ class GpuEngine {
     return out
   }
 
+  // the call's blocks packed into one Buffer (block end offsets, first block per document):
+  // the addon copies it once instead of visiting every block through N-API
   static prepare(g) {
+    const n = g.items.length
     g.ids = Uint32Array.from(g.items, (it) => it.state.id)
-    g.blocks = g.items.map((it) => {
-      const e = it.job.entries
-      for (let i = 0; i < e.length; i++) if (!Buffer.isBuffer(e[i]) && typeof e[i] !== 'string') return e.map(toBlock)
-      return e                          // raw blocks / JSON texts go over as they are
-    })
+    const bufs = []
+    g.docBlock = new Uint32Array(n + 1)
+    for (let i = 0; i < n; i++) {
+      const e = g.items[i].job.entries
+      for (let k = 0; k < e.length; k++) {
+        const c = e[k]
+        bufs.push(Buffer.isBuffer(c) ? c : Buffer.from(typeof c === 'string' ? c : JSON.stringify(c), 'utf8'))
+      }
+      g.docBlock[i + 1] = bufs.length
+    }
+    g.ends = new Uint32Array(bufs.length)
+    let at = 0
+    for (let b = 0; b < bufs.length; b++) { at += bufs[b].length; g.ends[b] = at }
+    if (at >= 2 ** 32) throw new RangeError('docset call over 4 GB of blocks')
+    g.data = Buffer.concat(bufs, at)
     return g
   }
 
@@ -343,7 +365,7 @@ class GpuEngine {
     const errors = []
     for (const g of this.groups(round, 0)) {
       GpuEngine.prepare(g)
-      this.finish(g, addon.docsetApply(g.ds, g.ids, g.blocks), errors)
+      this.finish(g, addon.docsetApplyPacked(g.ds, g.ids, g.data, g.ends, g.docBlock), errors)
     }
     this.raise(errors)
   }
@@ -361,7 +383,7 @@ class GpuEngine {
     const finish = () => { try { this.raise(errors) } finally { done() } }
     for (const g of gs) {
       GpuEngine.prepare(g)
-      addon.docsetApply(g.ds, g.ids, g.blocks, (err, r) => {
+      addon.docsetApplyPacked(g.ds, g.ids, g.data, g.ends, g.docBlock, (err, r) => {
         try {
           if (err) g.items.forEach(({ job }) => errors.push([job, err]))
           else this.finish(g, r, errors)

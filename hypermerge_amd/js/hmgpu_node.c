@@ -626,7 +626,7 @@ static Docset *get_docset(napi_env env, napi_value v) {
 
 /* docsetCreate(device, threads, patches[, binary]) -> docset (binary: results in the HMP1 form) */
 static napi_value DocsetCreate(napi_env env, napi_callback_info info) {
-    napi_value argv[4];
+    napi_value argv[5];
     size_t argc = 5;
     if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < 3) {
         napi_throw_type_error(env, NULL, "missing arguments");
@@ -712,6 +712,38 @@ static int gather_blocks(napi_env env, napi_value ids_v, napi_value blocks_v, Ds
     return 1;
 }
 
+/* the packed form: ids (Uint32Array n), data (one Buffer of every block back to back),
+ * ends (Uint32Array: end offset of each block), docBlock (Uint32Array n + 1: first block of each
+ * document) — one copy, no per-block N-API calls (1.3M blocks per 20k-document round cost the
+ * main thread ~1 s through napi_get_element / typeof / buffer info) */
+static int gather_packed(napi_env env, napi_value ids_v, napi_value data_v, napi_value ends_v, napi_value db_v, DsJob *j) {
+    void *ip, *dp, *ep, *bp; size_t il, dl, el, bl;
+    if (!get_bytes(env, ids_v, &ip, &il) || !get_bytes(env, data_v, &dp, &dl) || !get_bytes(env, ends_v, &ep, &el) ||
+        !get_bytes(env, db_v, &bp, &bl))
+        return 0;
+    const uint32_t n = (uint32_t)(il / 4), nb = (uint32_t)(el / 4);
+    const uint32_t *ends = (const uint32_t *)ep, *db = (const uint32_t *)bp;
+    if (bl / 4 != (size_t)n + 1 || db[0] != 0 || db[n] != nb) {
+        napi_throw_range_error(env, NULL, "docBlock must hold n + 1 ascending block indices ending at the block count");
+        return 0;
+    }
+    for (uint32_t i = 0; i < n; i++)
+        if (db[i] > db[i + 1]) { napi_throw_range_error(env, NULL, "docBlock not ascending"); return 0; }
+    for (uint32_t b = 0; b < nb; b++)
+        if (ends[b] > dl || (b && ends[b] < ends[b - 1])) { napi_throw_range_error(env, NULL, "block ends outside the data"); return 0; }
+    j->n = n;
+    j->ids = (uint32_t *)malloc((size_t)n * 4 + 4);
+    j->db = (uint32_t *)malloc(((size_t)n + 1) * 4);
+    j->bo = (uint64_t *)malloc(((size_t)nb + 1) * 8);
+    j->data = (uint8_t *)malloc(dl + 1);
+    memcpy(j->ids, ip, (size_t)n * 4);
+    memcpy(j->db, db, ((size_t)n + 1) * 4);
+    j->bo[0] = 0;
+    for (uint32_t b = 0; b < nb; b++) j->bo[b + 1] = ends[b];
+    if (dl) memcpy(j->data, dp, dl);
+    return 1;
+}
+
 static napi_value text_object(napi_env env, hm_text *t) {
     size_t len = 0;
     const char *p = hm_text_data(t, &len);
@@ -750,21 +782,26 @@ static void ds_call_js(napi_env env, napi_value cb, void *context, void *data) {
  * round runs on the docset's host thread and callback(err, {results, data}) runs on the main
  * thread when it is done; further async calls queue behind it (run in call order), any other
  * docset call except docsetOpen throws until every queued round has called back */
-static napi_value DocsetApply(napi_env env, napi_callback_info info) {
-    napi_value argv[4];
-    size_t argc = 5;
-    if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < 3) {
+static napi_value docset_apply(napi_env env, napi_callback_info info, int packed) {
+    napi_value argv[6];
+    size_t argc = 6;
+    const size_t need = packed ? 5 : 3;
+    if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < need) {
         napi_throw_type_error(env, NULL, "missing arguments");
         return NULL;
     }
+    napi_value cbv = argv[need];
     napi_valuetype cbt = napi_undefined;
-    if (argc >= 4) napi_typeof(env, argv[3], &cbt);
+    if (argc > need) napi_typeof(env, cbv, &cbt);
     /* async calls queue behind the ones in flight (the host thread runs them in order); a
      * synchronous call needs the docset idle */
     Docset *d = cbt == napi_function ? get_docset_any(env, argv[0]) : get_docset(env, argv[0]);
     if (!d) return NULL;
     DsJob *j = (DsJob *)calloc(1, sizeof(DsJob));
-    if (!gather_blocks(env, argv[1], argv[2], j)) { ds_job_free(j); return NULL; }
+    if (!(packed ? gather_packed(env, argv[1], argv[2], argv[3], argv[4], j) : gather_blocks(env, argv[1], argv[2], j))) {
+        ds_job_free(j);
+        return NULL;
+    }
     if (cbt != napi_function) {
         int st = hm_docset_apply(d->ds, j->data, j->bo, j->db, j->ids, j->n, &j->out);
         if (st) { ds_job_free(j); return throw_status(env, d->engine, st, "hm_docset_apply"); }
@@ -774,7 +811,7 @@ static napi_value DocsetApply(napi_env env, napi_callback_info info) {
     }
     napi_value name;
     napi_create_string_utf8(env, "hmgpu.docsetApply", NAPI_AUTO_LENGTH, &name);
-    if (napi_create_threadsafe_function(env, argv[3], NULL, name, 0, 1, NULL, NULL, d, ds_call_js, &j->tsfn) != napi_ok) {
+    if (napi_create_threadsafe_function(env, cbv, NULL, name, 0, 1, NULL, NULL, d, ds_call_js, &j->tsfn) != napi_ok) {
         ds_job_free(j);
         napi_throw_error(env, NULL, "napi_create_threadsafe_function failed");
         return NULL;
@@ -798,6 +835,11 @@ static napi_value DocsetApply(napi_env env, napi_callback_info info) {
     pthread_mutex_unlock(&d->mu);
     return NULL;
 }
+
+static napi_value DocsetApply(napi_env env, napi_callback_info info) { return docset_apply(env, info, 0); }
+/* docsetApplyPacked(docset, ids, data, blockEnds, docBlock, callback?): docsetApply with the
+ * blocks packed by the caller (gather_packed) */
+static napi_value DocsetApplyPacked(napi_env env, napi_callback_info info) { return docset_apply(env, info, 1); }
 
 /* docsetHistoryPrefix(docset, doc, n) -> Buffer of u32 log indices (history order) */
 static napi_value DocsetHistoryPrefix(napi_env env, napi_callback_info info) {
@@ -1113,7 +1155,7 @@ static napi_value Init(napi_env env, napi_value exports) {
         {"clockUpdate", ClockUpdate}, {"statusMessage", StatusMessage},
         {"commCreateLocal", CommCreateLocal}, {"clockExchange", ClockExchange}, {"clockMin", ClockMin},
         {"waitAsync", WaitAsync}, {"readRegs", ReadRegs},
-        {"docsetCreate", DocsetCreate}, {"docsetOpen", DocsetOpen}, {"docsetApply", DocsetApply},
+        {"docsetCreate", DocsetCreate}, {"docsetOpen", DocsetOpen}, {"docsetApply", DocsetApply}, {"docsetApplyPacked", DocsetApplyPacked},
         {"docsetHistoryPrefix", DocsetHistoryPrefix}, {"docsetClockUpdate", DocsetClockUpdate},
         {"docsetView", DocsetView}, {"docsetInfo", DocsetInfo}, {"docsetStats", DocsetStats},
         {"cursorsCreate", CursorsCreate}, {"cursorsReserve", CursorsReserve}, {"cursorsUpdate", CursorsUpdate},
