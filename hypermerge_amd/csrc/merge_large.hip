@@ -123,14 +123,45 @@ template <typename T> __device__ __forceinline__ T g_or(GLB T *p, T v) { return 
 template <typename T> __device__ __forceinline__ T g_min(GLB T *p, T v) { return __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 template <typename T> __device__ __forceinline__ T g_max(GLB T *p, T v) { return __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
+// The thread index as a value computed where it is used: the per-lane constants of the scans
+// (lane, wave, shuffle addresses) were hoisted out of the document loop by the compiler and
+// spilled to scratch at 128 VGPRs, so every scan of every document reloaded them through the
+// vector memory path (and its s_waitcnt also waited for every older load and store).
+__device__ __forceinline__ uint32_t fresh_tid() {
+    uint32_t t;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((uint32_t)threadIdx.x));
+    return t;
+}
+// DPP lane moves (gfx9 encodings; lanes without a source read 0): inclusive sum / max over the
+// wave with row shifts and the row broadcasts — VALU only, no address, no LDS crossbar
+#define DPP_ROW_SHR(n) (0x110 + (n))
+#define DPP_WAVE_SHR1 0x138
+#define DPP_ROW_BCAST15 0x142
+#define DPP_ROW_BCAST31 0x143
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_SHR(1), 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_SHR(2), 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_SHR(4), 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_SHR(8), 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_BCAST15, 0xA, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_BCAST31, 0xC, 0xF, false);
+    return x;
+}
+__device__ __forceinline__ uint32_t umax32(uint32_t a, uint32_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+    x = umax32(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_SHR(1), 0xF, 0xF, false));
+    x = umax32(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_SHR(2), 0xF, 0xF, false));
+    x = umax32(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_SHR(4), 0xF, 0xF, false));
+    x = umax32(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_SHR(8), 0xF, 0xF, false));
+    x = umax32(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_BCAST15, 0xA, 0xF, false));
+    x = umax32(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_ROW_BCAST31, 0xC, 0xF, false));
+    return x;
+}
+
 // exclusive scan of v over the block; returns the prefix, *total = block sum
 __device__ __forceinline__ uint32_t block_excl_scan(Shared &sh, uint32_t v, uint32_t *total) {
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t x = v;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane >= (uint32_t)o ? lane - o : lane) << 2), (int)x);
-        if (lane >= (uint32_t)o) x += y;
-    }
+    const uint32_t t = fresh_tid(), lane = t & 63, w = t >> 6;
+    const uint32_t x = wave_incl_sum(v);
     if (lane == 63) sh.scan[w] = x;
     bsync();
     uint32_t off = 0, tot = 0;
@@ -146,17 +177,13 @@ __device__ __forceinline__ uint32_t block_excl_scan(Shared &sh, uint32_t v, uint
 // (P, Q: pool or LDS pointers)
 template <typename P, typename Q>
 __device__ __forceinline__ uint32_t scan_into(Shared &sh, P src, Q dst, uint32_t N) {
-    const uint32_t per = (N + LWG - 1) / LWG;
-    const uint32_t b0 = threadIdx.x * per < N ? threadIdx.x * per : N;
+    const uint32_t per = (N + LWG - 1) / LWG, tb = fresh_tid();
+    const uint32_t b0 = tb * per < N ? tb * per : N;
     const uint32_t b1 = b0 + per < N ? b0 + per : N;
     uint32_t sum = 0;
     for (uint32_t i = b0; i < b1; i++) sum += src[i];
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t x = sum;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane >= (uint32_t)o ? lane - o : lane) << 2), (int)x);
-        if (lane >= (uint32_t)o) x += y;
-    }
+    const uint32_t t = fresh_tid(), lane = t & 63, w = t >> 6;
+    const uint32_t x = wave_incl_sum(sum);
     if (lane == 63) sh.scan[w] = x;
     bsync();
     uint32_t off = 0, tot = 0;
@@ -171,13 +198,9 @@ __device__ __forceinline__ uint32_t scan_array(Shared &sh, P arr, uint32_t N) { 
 // exclusive scan of f(0..N) into dst, for N <= LWG (one value per thread; the same two barriers)
 template <typename F, typename Q>
 __device__ __forceinline__ uint32_t scan_fn_small(Shared &sh, F f, Q dst, uint32_t N) {
-    const uint32_t i = threadIdx.x, lane = i & 63, w = i >> 6;
+    const uint32_t i = fresh_tid(), lane = i & 63, w = i >> 6;
     const uint32_t v = i < N ? f(i) : 0u;
-    uint32_t x = v;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane >= (uint32_t)o ? lane - o : lane) << 2), (int)x);
-        if (lane >= (uint32_t)o) x += y;
-    }
+    const uint32_t x = wave_incl_sum(v);
     if (lane == 63) sh.scan[w] = x;
     bsync();
     uint32_t off = 0, tot = 0;
@@ -235,13 +258,9 @@ __device__ __forceinline__ uint32_t *ad_row(const SmallParams &p, const hm_doc_r
 
 // exclusive max-scan of v over the block (identity 0): the max over lower-numbered threads
 __device__ __forceinline__ uint32_t block_excl_max(Shared &sh, uint32_t v) {
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t x = v;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane >= (uint32_t)o ? lane - o : lane) << 2), (int)x);
-        if (lane >= (uint32_t)o) x = x > y ? x : y;
-    }
-    const uint32_t ex = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane ? lane - 1 : 0) << 2), (int)x);
+    const uint32_t t = fresh_tid(), lane = t & 63, w = t >> 6;
+    const uint32_t x = wave_incl_max(v);
+    const uint32_t ex = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, DPP_WAVE_SHR1, 0xF, 0xF, false);
     if (lane == 63) sh.scan[w] = x;
     bsync();
     uint32_t off = 0;
@@ -435,7 +454,7 @@ __device__ PH_ATTR bool parallel_history(const hm_change_row *CH, const hm_dep_r
 __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uint32_t *ar, const hm_doc_row &doc,
                                        const LDS hm_change_row *sCH, const LDS int32_t *lh, const LDS uint32_t *lh2a,
                                        uint32_t H, uint32_t ad_off, uint32_t limit) {
-    const uint32_t tid = threadIdx.x;
+    const uint32_t tid = fresh_tid();           // (per document: see fresh_tid)
     const uint32_t n = doc.n_changes, A = doc.n_actors, m = doc.n_ops, R = doc.n_regs, O = doc.n_objs;
     const hm_op_row *OP = p.ops + doc.op_off;
     const uint32_t NP = R + O;
@@ -749,11 +768,7 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
             const uint32_t t = tid < O ? sh.otype[tid] : 0xFFu;
             const bool isl = t == HM_MAKE_LIST || t == HM_MAKE_TEXT;
             const uint32_t len = isl ? tsum(2 * (N + sh.listid[tid])) : 0u;
-            uint32_t x = len;          // inclusive scan over lanes in object order = list-id order
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((tid >= (uint32_t)o ? tid - o : tid) << 2), (int)x);
-                if (tid >= (uint32_t)o) x += y;
-            }
+            const uint32_t x = wave_incl_sum(len);   // inclusive scan over lanes in object order = list-id order
             if (isl) sh.listbase[sh.listid[tid]] = x - len;
         }
         bsync();
@@ -802,7 +817,7 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
 // and recomputes it from the start.  Results equal the general path's (same rules, same order).
 __device__ __forceinline__ int merge_doc_res(const SmallParams &p, Shared &sh, LDS uint32_t *ar, const hm_doc_row &doc,
                                              int32_t &H_out) {
-    const uint32_t tid = threadIdx.x;
+    const uint32_t tid = fresh_tid();           // (per document: see fresh_tid)
     const uint32_t n = doc.n_changes, A = doc.n_actors, m = doc.n_ops, nd = doc.n_deps;
     const uint32_t S = p.a_stride;
     const hm_change_row *CH = p.changes + doc.change_off;

@@ -595,9 +595,20 @@ __device__ __forceinline__ uint32_t pow2c(uint32_t x) {
     return x <= 1u ? 1u : 1u << (32 - __builtin_clz(x - 1));
 }
 
-__global__ void plan_kernel(PlanArgs a) {
+// the submit's reductions go through LDS to one atomic per workgroup and value: same-address
+// atomics from every wave of a million-document submit queue at one L2 channel (~10 ns each:
+// ~1.2 ms of a 1M-document incremental plan, the same in doc_rows_kernel)
+#define PLAN_WG 1024
+__global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
+    __shared__ unsigned long long s_need[4][PLAN_WG / 64];
+    __shared__ uint32_t s_inc[PLAN_WG / 64], s_mx[6][PLAN_WG / 64];
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    if (ln == 0) {
+        for (int k = 0; k < 4; k++) s_need[k][wv] = 0;
+        for (int k = 0; k < 6; k++) s_mx[k][wv] = 0;
+        s_inc[wv] = 0;
+    }
     const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
-    if (__ballot(i0 < a.n) == 0) return;                          // whole waves stay (reductions below)
     const bool live = i0 < a.n;
     const uint32_t i = live ? i0 : 0u;
     uint32_t err = 0;
@@ -632,21 +643,19 @@ __global__ void plan_kernel(PlanArgs a) {
             remapped |= y != x;
         }
     }
-    if (__ballot(err != 0)) {                                     // (rare) one atomic per failing lane
-        if (err) atomicOr(&a.st->err, err);
-        return;
-    }
+    const bool wave_ok = __ballot(err != 0) == 0;
+    if (err) atomicOr(&a.st->err, err);                            // (rare) one atomic per failing lane
+    if (wave_ok) {
     PlanRow p;
     p.n_c = m.n_c; p.n_d = m.n_d; p.n_o = m.n_o; p.n_r = m.n_r; p.n_objs = m.n_objs; p.n_actors = m.n_actors; p.flags = m.flags;
     p.g[0] = live && m.n_c + r.n_changes > m.c_cap ? pow2c(m.n_c + r.n_changes) : 0u;
     p.g[1] = live && m.n_d + r.n_deps > m.d_cap ? pow2c(m.n_d + r.n_deps) : 0u;
     p.g[2] = live && m.n_o + r.n_ops > m.o_cap ? pow2c(m.n_o + r.n_ops) : 0u;
     p.g[3] = live && r.n_regs > m.r_cap ? pow2c(r.n_regs) : 0u;
-    // the submit's reductions: one atomic per wave (a million lanes on one address would queue at the L2)
     for (int k = 0; k < 4; k++) {
         unsigned long long g = p.g[k];
         for (int o = 32; o > 0; o >>= 1) g += (unsigned long long)__shfl_xor((long long)g, o);
-        if ((threadIdx.x & 63) == 0 && g) atomicAdd(&a.st->need[k], g);
+        if (ln == 0) s_need[k][wv] = g;
     }
     // route: a clean resident state (last merge ok, nothing queued, no re-rank) and new rows that
     // fit the incremental tiles -> inc_apply_kernel; the rest re-merge their whole log
@@ -660,14 +669,32 @@ __global__ void plan_kernel(PlanArgs a) {
     p.remapped = remapped ? 1u : 0u;
     if (live) a.plan[i] = p;
     const unsigned long long im = __ballot(inc);
-    if ((threadIdx.x & 63) == 0 && im) atomicAdd(&a.st->n_inc, (uint32_t)__popcll(im));
+    if (ln == 0) s_inc[wv] = (uint32_t)__popcll(im);
     if (im) {
         uint32_t v[6] = {inc ? r.n_changes : 0u, inc ? tgt : 0u,
                          inc ? (m.n_c < HM_INC_MAX_STAGE ? m.n_c : (uint32_t)HM_INC_MAX_STAGE) : 0u, inc ? r.n_regs : 0u,
                          inc ? last.n_surv : 0u, inc ? (r.n_ops < HM_INC_SLOTS ? r.n_ops : (uint32_t)HM_INC_SLOTS) : 0u};
         for (int k = 0; k < 6; k++) {
             for (int o = 32; o > 0; o >>= 1) { const uint32_t y = (uint32_t)__shfl_xor((int)v[k], o); v[k] = v[k] > y ? v[k] : y; }
-            if ((threadIdx.x & 63) == 0) atomicMax(&a.st->mx[k], v[k]);
+            if (ln == 0) s_mx[k][wv] = v[k];
+        }
+    }
+    }
+    __syncthreads();
+    if (threadIdx.x < 11) {                                        // one lane per reduced value
+        const uint32_t k = threadIdx.x, nw = PLAN_WG / 64;
+        if (k < 4) {
+            unsigned long long g = 0;
+            for (uint32_t w = 0; w < nw; w++) g += s_need[k][w];
+            if (g) atomicAdd(&a.st->need[k], g);
+        } else if (k == 4) {
+            uint32_t c = 0;
+            for (uint32_t w = 0; w < nw; w++) c += s_inc[w];
+            if (c) atomicAdd(&a.st->n_inc, c);
+        } else {
+            uint32_t x = 0;
+            for (uint32_t w = 0; w < nw; w++) x = x > s_mx[k - 5][w] ? x : s_mx[k - 5][w];
+            if (x) atomicMax(&a.st->mx[k - 5], x);
         }
     }
 }
@@ -702,19 +729,41 @@ __global__ void alloc_kernel(PlanArgs a) {
     if (!p.inc) a.list[atomicAdd(&a.st->n_cold, 1u)] = h;
 }
 
-__global__ void doc_rows_kernel(const uint32_t *list, uint32_t n, const DevDoc *dm, hm_doc_row *rows, PlanStats *st) {
+__global__ __launch_bounds__(PLAN_WG) void doc_rows_kernel(const uint32_t *list, uint32_t n, const DevDoc *dm, hm_doc_row *rows,
+                                                          PlanStats *st) {
+    // per workgroup: 5 maxima, the flags OR, 4 sums -> LDS, then one atomic each
+    __shared__ uint32_t s_mx[6];
+    __shared__ unsigned long long s_tot[4];
+    if (threadIdx.x < 6) s_mx[threadIdx.x] = 0;
+    if (threadIdx.x < 4) s_tot[threadIdx.x] = 0;
+    __syncthreads();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const DevDoc m = dm[list[i]];
-    hm_doc_row r;
-    r.change_off = m.c_off; r.n_changes = m.n_c; r.dep_off = m.d_off; r.n_deps = m.n_d;
-    r.op_off = m.o_off; r.n_ops = m.n_o; r.reg_off = m.r_off; r.n_regs = m.n_r;
-    r.n_objs = m.n_objs; r.n_actors = m.n_actors; r.flags = m.flags; r.reserved[0] = r.reserved[1] = 0;
-    rows[i] = r;
-    atomicMax(&st->max_c, m.n_c); atomicMax(&st->max_o, m.n_o); atomicMax(&st->max_r, m.n_r);
-    atomicMax(&st->max_objs, m.n_objs); atomicMax(&st->max_d, m.n_d); atomicOr(&st->flags, (uint32_t)m.flags);
-    atomicAdd(&st->tot_c, (unsigned long long)m.n_c); atomicAdd(&st->tot_d, (unsigned long long)m.n_d);
-    atomicAdd(&st->tot_o, (unsigned long long)m.n_o); atomicAdd(&st->tot_r, (unsigned long long)m.n_r);
+    if (i < n) {
+        const DevDoc m = dm[list[i]];
+        hm_doc_row r;
+        r.change_off = m.c_off; r.n_changes = m.n_c; r.dep_off = m.d_off; r.n_deps = m.n_d;
+        r.op_off = m.o_off; r.n_ops = m.n_o; r.reg_off = m.r_off; r.n_regs = m.n_r;
+        r.n_objs = m.n_objs; r.n_actors = m.n_actors; r.flags = m.flags; r.reserved[0] = r.reserved[1] = 0;
+        rows[i] = r;
+        atomicMax(&s_mx[0], m.n_c); atomicMax(&s_mx[1], m.n_o); atomicMax(&s_mx[2], m.n_r);
+        atomicMax(&s_mx[3], m.n_objs); atomicMax(&s_mx[4], m.n_d); atomicOr(&s_mx[5], (uint32_t)m.flags);
+        atomicAdd(&s_tot[0], (unsigned long long)m.n_c); atomicAdd(&s_tot[1], (unsigned long long)m.n_d);
+        atomicAdd(&s_tot[2], (unsigned long long)m.n_o); atomicAdd(&s_tot[3], (unsigned long long)m.n_r);
+    }
+    __syncthreads();
+    switch (threadIdx.x) {
+    case 0: atomicMax(&st->max_c, s_mx[0]); break;
+    case 1: atomicMax(&st->max_o, s_mx[1]); break;
+    case 2: atomicMax(&st->max_r, s_mx[2]); break;
+    case 3: atomicMax(&st->max_objs, s_mx[3]); break;
+    case 4: atomicMax(&st->max_d, s_mx[4]); break;
+    case 5: if (s_mx[5]) atomicOr(&st->flags, s_mx[5]); break;
+    case 6: atomicAdd(&st->tot_c, s_tot[0]); break;
+    case 7: atomicAdd(&st->tot_d, s_tot[1]); break;
+    case 8: atomicAdd(&st->tot_o, s_tot[2]); break;
+    case 9: atomicAdd(&st->tot_r, s_tot[3]); break;
+    default: break;
+    }
 }
 
 __global__ void rollback_kernel(const uint32_t *handles, uint32_t n, const hm_doc_result *res_docs, const PlanRow *plan,
@@ -799,7 +848,7 @@ __global__ void read_hist_kernel(uint32_t n, const uint32_t *handles, const uint
 
 hipError_t hm_launch_plan(const PlanArgs &a, hipStream_t s) {
     if (!a.n) return hipSuccess;
-    hipLaunchKernelGGL(hms::plan_kernel, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(hms::plan_kernel, dim3((a.n + PLAN_WG - 1) / PLAN_WG), dim3(PLAN_WG), 0, s, a);
     return hipGetLastError();
 }
 hipError_t hm_launch_alloc(const PlanArgs &a, hipStream_t s) {
@@ -810,7 +859,7 @@ hipError_t hm_launch_alloc(const PlanArgs &a, hipStream_t s) {
 hipError_t hm_launch_doc_rows(const uint32_t *list, uint32_t n, const DevDoc *dm, hm_doc_row *rows, PlanStats *st,
                               hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(hms::doc_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, s, list, n, dm, rows, st);
+    hipLaunchKernelGGL(hms::doc_rows_kernel, dim3((n + PLAN_WG - 1) / PLAN_WG), dim3(PLAN_WG), 0, s, list, n, dm, rows, st);
     return hipGetLastError();
 }
 hipError_t hm_launch_rollback(const uint32_t *handles, uint32_t n, const hm_doc_result *res_docs, const PlanRow *plan,

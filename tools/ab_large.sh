@@ -1,16 +1,13 @@
 #!/bin/bash
-# A/B of merge_large_kernel builds on C3 (and C1 actor-major): stamps shares + bench lines per library.
-# Usage: tools/ab_large.sh name...   (libraries hypermerge_amd/_lib/ablate/lib_<name>.so; "base" = default build)
+# general-kernel A/B: its parity tests on the default build, then the variants on C3 (x2) and C1
 set -o pipefail
-mkdir -p gpurun_out
-for nm in "$@"; do
-  so=hypermerge_amd/_lib/ablate/lib_$nm.so; [ "$nm" = base ] && so=hypermerge_amd/_lib/libhmgpu.so
-  if [ -f hypermerge_amd/_lib/ablate/lib_stamps_$nm.so ]; then
-    HMGPU_LIB=hypermerge_amd/_lib/ablate/lib_stamps_$nm.so timeout -k 10 200 python tools/lstamps.py C3 10000 > gpurun_out/lstamps_$nm.log 2>&1 || exit 2
-    echo "== stamps $nm"; cat gpurun_out/lstamps_$nm.log | grep -v amdgpu.ids
-  fi
-  for cfg in "C3 --docs 10000" "C1 --docs 1 --arrival 1"; do
-    HMGPU_LIB=$so timeout -k 10 300 python bench.py --config $cfg --check-docs 200 --steps 5 --warmup 2 --no-cpu --no-traffic > gpurun_out/ab_$nm.log 2>&1 || { tail -5 gpurun_out/ab_$nm.log; exit 3; }
-    tail -1 gpurun_out/ab_$nm.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$nm', '$cfg'.split()[0], 'value %.3e ms %.3f kernel_ms %.3f parity %s unsup %s' % (d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d['parity_sample_ok'], d['unsupported_docs']))"
-  done
+mkdir -p gpurun_out/ab
+timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_general_resident.py tests/test_wide_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/ab/tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/ab/tests.log; exit 1; }
+tail -1 gpurun_out/ab/tests.log
+LIBS=$(ls hypermerge_amd/_lib/ablate/lib_*.so | grep -v stamps)
+for rep in 1 2; do
+ABL_CONFIG=C3 ABL_DOCS=10000 timeout -k 10 300 python tools/ablate.py $LIBS > gpurun_out/ab/c3_$rep.log 2>&1 || exit 5
+echo "C3 rep $rep"; cat gpurun_out/ab/c3_$rep.log
 done
+ABL_CONFIG=C1 ABL_DOCS=1 ABL_ARGS="--arrival 1" timeout -k 10 300 python tools/ablate.py $LIBS > gpurun_out/ab/c1.log 2>&1 || exit 6
+echo "C1am"; cat gpurun_out/ab/c1.log

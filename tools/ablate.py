@@ -9,4 +9,9 @@ for so in sys.argv[1:]:
                           "--config", os.environ.get("ABL_CONFIG", "C4"), "--no-traffic", "--no-e2e", "--no-orders", "--no-node", "--no-incremental"] + os.environ.get("ABL_ARGS", "").split(), env=env, capture_output=True, text=True,
                          timeout=600)
     line = [l for l in out.stdout.splitlines() if l.startswith("{")]
-    print(os.path.basename(so), (json.loads(line[-1])["roofline"]["kernels"][0]["ms"], json.loads(line[-1])["ms_per_step"], json.loads(line[-1])["parity_sample_ok"]) if line else out.stderr[-800:], flush=True)
+    if line:
+        d = json.loads(line[-1])
+        print(os.path.basename(so), [(k["kernel"][6:11], round(k["ms"], 4)) for k in d["roofline"]["kernels"]],
+              round(d["ms_per_step"], 4), d["parity_sample_ok"], flush=True)
+    else:
+        print(os.path.basename(so), out.stderr[-800:], flush=True)
