@@ -516,14 +516,24 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
     LSTAMP(11);
     // ---- op scan: rows read once from HBM, four per thread in flight ----
     for (uint32_t k0 = 0; k0 < m; k0 += 4 * LWG) {
-        hm_op_row orow[4];
+        // whole 32-byte rows, loaded unconditionally (a clamped index): a predicated load of only
+        // the fields used was compiled as a wait for everything before each of the four loads and
+        // a wait for the load itself inside its predicated block (one row in flight, not four)
+        uint4 ra[4], rb[4];
 #pragma unroll
-        for (int u = 0; u < 4; u++) { const uint32_t k = k0 + tid + u * LWG; if (k < m) orow[u] = OP[k]; }
+        for (int u = 0; u < 4; u++) {
+            const uint32_t k = k0 + tid + u * LWG;
+            const uint4 *src = reinterpret_cast<const uint4 *>(OP + (k < m ? k : m - 1));
+            ra[u] = src[0]; rb[u] = src[1];
+        }
+        asm volatile("" ::: "memory");          // all four issued here (not sunk into their uses)
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const uint32_t k = k0 + tid + u * LWG;
             if (k >= m) continue;
-            const hm_op_row &o = orow[u];
+            struct { uint4 a, b; } raw = {ra[u], rb[u]};
+            hm_op_row o;
+            __builtin_memcpy(&o, &raw, sizeof o);
             const uint32_t ci = o_chg[k];
             const int32_t h = (int32_t)c_hist[ci];
             if (o.action == HM_INC || o.datatype == HM_DT_COUNTER) sh.ctrs = 1;
