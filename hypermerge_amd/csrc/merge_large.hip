@@ -840,13 +840,29 @@ __device__ __forceinline__ int merge_doc_res(const SmallParams &p, Shared &sh, L
     LDS hm_dep_row *sDP = (LDS hm_dep_row *)(ar + stage_base + 6 * n);
     LDS int32_t *lh = (LDS int32_t *)(ar + stage_base + 6 * n + 2 * nd);
     LDS uint32_t *lh2a = ar + stage_base + 7 * n + 2 * nd;
-    for (uint32_t j = tid; j < nd; j += LWG) sDP[j] = p.deps[doc.dep_off + j];
+    // staging: a thread's dep row and change row loads are issued together (one round trip per
+    // 1024 rows, where the deps, then the change rows, then their predecessors were three)
+    {
+        const uint32_t top = n > nd ? n : nd;
+        for (uint32_t j0 = 0; j0 < top; j0 += LWG) {
+            const uint32_t j = j0 + tid;
+            const bool hd = j < nd, hc = j < n;
+            const uint2 dv = hd ? *reinterpret_cast<const uint2 *>(p.deps + doc.dep_off + j) : make_uint2(0, 0);
+            const uint2 *cs = reinterpret_cast<const uint2 *>(CH + (hc ? j : 0u));
+            const uint2 c0 = hc ? cs[0] : make_uint2(0, 0), c1 = hc ? cs[1] : make_uint2(0, 0), c2 = hc ? cs[2] : make_uint2(0, 0);
+            asm volatile("" ::: "memory");
+            if (hd) *reinterpret_cast<LDS uint2 *>(sDP + j) = dv;
+            if (hc) {
+                LDS uint2 *d = reinterpret_cast<LDS uint2 *>(sCH + j);
+                d[0] = c0; d[1] = c1; d[2] = c2;
+            }
+        }
+    }
     bsync();
     for (uint32_t i = tid; i < n; i += LWG) {
-        const hm_change_row c = CH[i];
-        sCH[i] = c;
-        const uint32_t op0 = i ? CH[i - 1].op_first + CH[i - 1].n_ops : doc.op_off;
-        const uint32_t dp0 = i ? CH[i - 1].dep_off + CH[i - 1].n_deps : doc.dep_off;
+        const hm_change_row c = sCH[i];
+        const uint32_t op0 = i ? sCH[i - 1].op_first + sCH[i - 1].n_ops : doc.op_off;
+        const uint32_t dp0 = i ? sCH[i - 1].dep_off + sCH[i - 1].n_deps : doc.dep_off;
         const bool last_bad = i == n - 1 && (c.op_first + c.n_ops != doc.op_off + m || c.dep_off + c.n_deps != doc.dep_off + nd);
         if (c.actor >= A || c.seq == 0 || c.op_first < doc.op_off || c.op_first - doc.op_off + c.n_ops > m ||
             c.dep_off < doc.dep_off || c.dep_off - doc.dep_off + c.n_deps > nd ||
