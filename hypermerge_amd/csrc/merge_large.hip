@@ -453,7 +453,7 @@ __device__ PH_ATTR bool parallel_history(const hm_change_row *CH, const hm_dep_r
 #define RES_FALLBACK 3
 __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uint32_t *ar, const hm_doc_row &doc,
                                        const LDS hm_change_row *sCH, const LDS int32_t *lh, const LDS uint32_t *lh2a,
-                                       uint32_t H, uint32_t ad_off, uint32_t limit) {
+                                       uint32_t H, uint32_t ad_off, uint32_t limit, uint32_t AS) {
     const uint32_t tid = fresh_tid();           // (per document: see fresh_tid)
     const uint32_t n = doc.n_changes, A = doc.n_actors, m = doc.n_ops, R = doc.n_regs, O = doc.n_objs;
     const hm_op_row *OP = p.ops + doc.op_off;
@@ -464,7 +464,7 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
     auto w32 = [&](uint32_t cnt) -> LDS uint32_t * { LDS uint32_t *q = ar + off; off += cnt; return q; };
     auto w16 = [&](uint32_t cnt) -> LDS uint16_t * { LDS uint16_t *q = (LDS uint16_t *)(ar + off); off += (cnt + 1) / 2; return q; };
     auto w8 = [&](uint32_t cnt) -> LDS uint8_t * { LDS uint8_t *q = (LDS uint8_t *)(ar + off); off += (cnt + 3) / 4; return q; };
-    LDS uint32_t *c_ad = w32(n * A);            // L2's closure rows (= allDeps), already in place
+    LDS uint32_t *c_ad = w32(n * AS);           // L2's closure rows (= allDeps, row stride AS), already in place
     LDS uint32_t *c_tmp = w32(n), *c_hist = w32(n), *c_act = w32(n), *c_seq = w32(n), *c_op0 = w32(n), *c_kb = w32(n);
     LDS uint32_t *o_w = w32(m);                 // reg (16) | action (4) << 16 | obj (7, 127 unknown) << 20
     LDS uint16_t *o_chg = w16(m);               // op -> arrival index of its change
@@ -643,7 +643,7 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
             bool surv = true;
             for (uint32_t q = 0; q < cnt; q++) {
                 const uint32_t e = a_k[e0 + q];
-                if (dec_act(o_w[e]) != HM_INC && c_ad[o_chg[e] * A + ao] >= so) surv = false;
+                if (dec_act(o_w[e]) != HM_INC && c_ad[o_chg[e] * AS + ao] >= so) surv = false;
             }
             if (surv) {
                 atomicAdd(&r_scnt[reg], 1u);
@@ -876,7 +876,10 @@ __device__ __forceinline__ int merge_doc_res(const SmallParams &p, Shared &sh, L
     uint32_t T = 0;
     for (uint32_t a = 0; a < A; a++) { if (tid == 0) sh.tabo[a] = T; if (sh.maxs[a]) T += sh.maxs[a] - sh.base[a] + 1; }
     if (tid == 0) sh.tabo[A] = T;
-    if (T > 4 * n + 64 || n * A + T > stage_base) return RES_FALLBACK;
+    // closure rows at an odd stride: the groups of a wave read rows of different changes, and
+    // at stride 8 those rows met in the same banks four apart
+    const uint32_t AS = A | 1u;
+    if (T > 4 * n + 64 || n * AS + T > stage_base) return RES_FALLBACK;
     LDS uint32_t *lt = ar, *lc = ar + T;            // L1 table, L2 closure rows (stride A)
     for (uint32_t i = tid; i < T; i += LWG) lt[i] = 0xFFFFFFFFu;
     bsync();                                        // (also publishes sh.tabo)
@@ -936,7 +939,7 @@ __device__ __forceinline__ int merge_doc_res(const SmallParams &p, Shared &sh, L
     LSTAMP(1);
     // ---- L2: closure rows by pointer jumping per (row, actor), then the literal-fold check ----
     for (uint32_t i = tid; i < n; i += LWG) {
-        LDS uint32_t *row = lc + i * A;
+        LDS uint32_t *row = lc + i * AS;
         for (uint32_t a = 0; a < A; a++) row[a] = 0;
         if (lh[i] < 0) continue;
         const hm_change_row c = sCH[i];
@@ -972,11 +975,11 @@ __device__ __forceinline__ int merge_doc_res(const SmallParams &p, Shared &sh, L
         for (uint32_t w0 = 0; w0 < n * 8; w0 += LWG) {     // whole lane groups: DPP needs them active
             const uint32_t w = w0 + tid, i = w >> 3;
             const bool live = w < n * 8 && a_ok && lh[i < n ? i : 0] >= 0;
-            LDS uint32_t *row = lc + (live ? i : 0u) * A;
+            LDS uint32_t *row = lc + (live ? i : 0u) * AS;
             const uint32_t sq = live ? row[my_a] : 0u;
             const uint32_t ti = (sq && sq >= a_base && sq <= a_max) ? lt[a_off + (sq - a_base)] : 0xFFFFFFFFu;
             const bool src = ti < n;
-            const LDS uint32_t *r2 = lc + (src ? ti : 0u) * A;
+            const LDS uint32_t *r2 = lc + (src ? ti : 0u) * AS;
             uint32_t v[8];
 #pragma unroll
             for (uint32_t b = 0; b < 8; b++) v[b] = (src && b < A) ? r2[b] : 0u;
@@ -1001,7 +1004,7 @@ __device__ __forceinline__ int merge_doc_res(const SmallParams &p, Shared &sh, L
     uint32_t *cur = p.res_all_deps + (size_t)doc.change_off * S;
     for (uint32_t i = tid; i < n; i += LWG) {
         uint32_t *grow_ = cur + (size_t)i * S;
-        const LDS uint32_t *row = lc + i * A;
+        const LDS uint32_t *row = lc + i * AS;
         for (uint32_t a = 0; a < S; a++) grow_[a] = a < A ? row[a] : 0u;
         if (lh[i] < 0) continue;
         const hm_change_row c = sCH[i];
@@ -1013,7 +1016,7 @@ __device__ __forceinline__ int merge_doc_res(const SmallParams &p, Shared &sh, L
             if (sq == 0) return;
             const uint32_t ti = lslot(a, sq);
             if (ti >= n) { same = false; return; }
-            const LDS uint32_t *r2 = lc + ti * A;
+            const LDS uint32_t *r2 = lc + ti * AS;
 #pragma unroll
             for (uint32_t b = 0; b < 8; b++)
                 if (b < A) { const uint32_t x = r2[b]; acc[b] = b == a ? sq : (acc[b] > x ? acc[b] : x); }
@@ -1034,7 +1037,7 @@ __device__ __forceinline__ int merge_doc_res(const SmallParams &p, Shared &sh, L
     LSTAMP(3);
     for (uint32_t h = tid; h < H; h += LWG) {
         const uint32_t ci = lh2a[h];
-        const LDS uint32_t *row = lc + ci * A;
+        const LDS uint32_t *row = lc + ci * AS;
         for (uint32_t a = 0; a < A; a++) atomicMax(&sh.maxad[a], row[a]);
         const hm_change_row c = sCH[ci];
         atomicMax(&sh.clock[c.actor], c.seq);
@@ -1042,7 +1045,7 @@ __device__ __forceinline__ int merge_doc_res(const SmallParams &p, Shared &sh, L
     bsync();
     if (tid < A && sh.clock[tid] && sh.maxad[tid] < sh.clock[tid]) sh.headv[tid] = sh.clock[tid];
     H_out = (int32_t)H;
-    return l34_res(p, sh, ar, doc, sCH, lh, lh2a, H, T, stage_base);
+    return l34_res(p, sh, ar, doc, sCH, lh, lh2a, H, T, stage_base, AS);
 }
 
 __device__ HML_DOC_ATTR Outcome merge_doc_large(const SmallParams &p, Shared &sh, LDS uint32_t *ar, const hm_doc_row &doc, uint32_t d,
