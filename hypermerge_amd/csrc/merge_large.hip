@@ -2096,7 +2096,13 @@ __global__ __launch_bounds__(LWG) __attribute__((amdgpu_waves_per_eu(HML_WPE))) 
         const bool via_res = rc != RES_FALLBACK;   // (every change ready on arrival: nothing queued)
         if (!via_res) {
             bsync();
-            rc = merge_doc_large(psh, sh, arena, doc, d, pool, pool_bytes, pool_used, H);
+            // the general path (not inlined) takes its row by reference: hand it a copy, so the
+            // address that escapes is the copy's and `doc` itself stays in registers (its fields
+            // were read from the stack through every phase of the all-LDS path)
+            hm_doc_row doc_c;
+            __builtin_memcpy(&doc_c, &doc, sizeof doc_c);
+            asm volatile("" ::: "memory");
+            rc = merge_doc_large(psh, sh, arena, doc_c, d, pool, pool_bytes, pool_used, H);
         }
         const Outcome oc = (Outcome)rc;
         bsync();
