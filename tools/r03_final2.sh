@@ -1,11 +1,11 @@
 #!/bin/bash
 # Round-3 re-measurement after the general-kernel changes: C3 profile (stats + PMC) and the per-config table
 set -o pipefail
-O=gpurun_out/r03/final2
+O=gpurun_out/r03/${FINAL_TAG:-final2}
 mkdir -p $O
-bash tools/profile.sh r03c3b --config C3 --docs 10000 > $O/profile_c3.log 2>&1 || { tail $O/profile_c3.log; exit 4; }
-python tools/pmc_summary.py gpurun_out/r03c3b merge_large_kernel > $O/c3_pmc_summary.json || exit 5
-find gpurun_out/r03c3b/trace -name "*kernel_stats.csv" -exec cp {} $O/c3_kernel_stats.csv \;
+bash tools/profile.sh r03c3${FINAL_TAG:-b} --config C3 --docs 10000 > $O/profile_c3.log 2>&1 || { tail $O/profile_c3.log; exit 4; }
+python tools/pmc_summary.py gpurun_out/r03c3${FINAL_TAG:-b} merge_large_kernel > $O/c3_pmc_summary.json || exit 5
+find gpurun_out/r03c3${FINAL_TAG:-b}/trace -name "*kernel_stats.csv" -exec cp {} $O/c3_kernel_stats.csv \;
 timeout -k 10 1000 python tools/perf_table.py > $O/perf_table.md 2>&1 || { tail -20 $O/perf_table.md; exit 1; }
 grep -v '^<!--' $O/perf_table.md
 python3 -c "
