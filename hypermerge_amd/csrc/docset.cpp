@@ -465,7 +465,8 @@ void decode_round(DocSt &d, Round &R, const uint8_t *data, const uint64_t *bo, S
                 r.elem = (uint32_t)(int64_t)o.elem;
                 el.assign(d.actors.ptr(aid), d.actors.len(aid));
                 el += ':';
-                el += js_num_text(o.elem);
+                char nb[40];
+                el.append(nb, js_num_text(o.elem, nb));
                 r.reg = d.regs.get(el.data(), (uint32_t)el.size(), r.obj, f);
                 r.parent = Scan::is(o.key, "_head") ? HM_HEAD : d.regs.get(o.key.p, o.key.n, r.obj, f);
             } else if (a >= HM_SET) {

@@ -267,20 +267,23 @@ std::u16string u16(const std::string &s) {
 
 const char *ROOT_ID = "00000000-0000-0000-0000-000000000000";
 
-int action_of(const std::string &a) {
-    static const char *names[] = {"makeMap", "makeTable", "makeList", "makeText", "ins", "set", "del", "link", "inc"};
-    for (int i = 0; i < 9; i++) if (a == names[i]) return i;
-    return -1;
-}
-
 // JS Number.isInteger(v) && |v| < 2^53
 bool js_int(double v) { return std::isfinite(v) && std::floor(v) == v && std::fabs(v) < 9007199254740992.0; }
-// `${n}` of an integral JS number (the element counter of an elemId)
-std::string js_num_text(double v) {
-    char b[40];
-    if (js_int(v)) snprintf(b, sizeof b, "%lld", (long long)v);
-    else snprintf(b, sizeof b, "%.17g", v);
-    return b;
+// `${n}` of an integral JS number (the element counter of an elemId), written into b
+// (>= 40 bytes); returns its length
+uint32_t js_num_text(double v, char *b) {
+    if (!js_int(v)) return (uint32_t)snprintf(b, 40, "%.17g", v);
+    long long x = (long long)v;
+    char t[24];
+    int n = 0;
+    const bool neg = x < 0;
+    unsigned long long u = neg ? 0ull - (unsigned long long)x : (unsigned long long)x;
+    do { t[n++] = (char)('0' + u % 10); u /= 10; } while (u);
+    uint32_t k = 0;
+    if (neg) b[k++] = '-';
+    while (n) b[k++] = t[--n];
+    b[k] = 0;
+    return k;
 }
 
 
@@ -332,12 +335,14 @@ struct Intern {
             slot[i] = id + 1;
         }
     }
-    uint32_t get(const SV &s, uint32_t tag, bool &fresh) {
-        const uint64_t h = hash_bytes(s.p, s.n, tag);
+    uint32_t get(const SV &s, uint32_t tag, bool &fresh) { return get_h(s, tag, hash_bytes(s.p, s.n, tag), fresh); }
+    // with the name's hash_bytes(s, tag) already known (the batch pool re-interns names that a
+    // document's table hashed before)
+    uint32_t get_h(const SV &s, uint32_t tag, uint64_t h, bool &fresh) {
         for (uint32_t i = (uint32_t)h & mask;; i = (i + 1) & mask) {
             const uint32_t v = slot[i];
             if (!v) {
-                if ((keys.size() + 1) * 2 > slot.size()) { grow(); return get(s, tag, fresh); }
+                if ((keys.size() + 1) * 2 > slot.size()) { grow(); return get_h(s, tag, h, fresh); }
                 slot[i] = (uint32_t)keys.size() + 1;
                 keys.push_back({s, tag, h});
                 fresh = true;
@@ -477,6 +482,11 @@ struct Scan {
         return num(v);
     }
     static bool is(const SV &k, const char *lit) { const size_t n = strlen(lit); return k.n == n && !memcmp(k.p, lit, n); }
+    static int action_of(const SV &a) {
+        static const char *names[] = {"makeMap", "makeTable", "makeList", "makeText", "ins", "set", "del", "link", "inc"};
+        for (int i = 0; i < 9; i++) if (is(a, names[i])) return i;
+        return -1;
+    }
     // value of an op field into the scan op (anything a field can hold)
     bool anyval(ScanOp &o) {
         ws();
@@ -548,7 +558,7 @@ struct Scan {
                             SV a;
                             if (p < e && *p != '"') { o.action = -1; return skip(); }
                             if (!str(a)) return false;
-                            o.action = (int8_t)action_of(std::string(a.p, a.n));
+                            o.action = (int8_t)action_of(a);
                             return true;
                         }
                         if (is(f, "obj")) { if (p < e && *p == '"') return str(o.obj); o.obj = SV(); return skip(); }
