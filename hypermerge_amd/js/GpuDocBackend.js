@@ -105,37 +105,52 @@ function rdEntry(e) {
     e.conflicts = cs
   }
 }
-function decodeRound(buf, n) {
-  if (buf.length === 0 || buf[0] === 0x7b) return JSON.parse(buf.toString())
-  if (buf.byteOffset % 8) buf = Buffer.from(buf)           // a fresh, aligned copy
-  const u = new Uint32Array(buf.buffer, buf.byteOffset, buf.length >>> 2)
-  if (u[0] !== 0x31504d48 || u[1] !== n) throw new Error('docset results: bad HMP1 header')
-  const ns = u[2], nw = u[3], nn = u[4], blobBytes = u[5], ascii = u[6]
-  let at = 8
-  const woff = u.subarray(at, at + n + 1); at += n + 1
-  const sbase = u.subarray(at, at + n + 1); at += n + 1
-  const nbase = u.subarray(at, at + n + 1); at += n + 1
-  const soff = u.subarray(at, at + ns + 1); at += ns + 1
-  const w = u.subarray(at, at + nw); at += nw
-  const numsAt = ((4 * at + 7) >> 3) << 3
-  const nums = new Float64Array(buf.buffer, buf.byteOffset + numsAt, nn)
-  const blobAt = numsAt + 8 * nn
-  const strs = new Array(ns)
-  if (ascii) {
-    const text = buf.toString('latin1', blobAt, blobAt + blobBytes)
-    for (let i = 0; i < ns; i++) strs[i] = text.substring(soff[i], soff[i + 1])
-  } else {
-    for (let i = 0; i < ns; i++) strs[i] = buf.toString('utf8', blobAt + soff[i], blobAt + soff[i + 1])
+// One docset call's HMP1 results, read document by document: decodeRound(buf, n).head(d) gives
+// the patch shell (clock, deps; diffs null), back clock and round clock; .diffs(d) fills the
+// patch's diffs.  finish() reads every head first and each document's diffs only when its
+// patch is delivered, so a round's diff objects die young instead of all being live at once
+// (and promoted by the collector) across the whole delivery loop.
+class RoundReader {
+  constructor(buf, n) {
+    if (buf.byteOffset % 8) buf = Buffer.from(buf)           // a fresh, aligned copy
+    const u = new Uint32Array(buf.buffer, buf.byteOffset, buf.length >>> 2)
+    if (u[0] !== 0x31504d48 || u[1] !== n) throw new Error('docset results: bad HMP1 header')
+    const ns = u[2], nw = u[3], nn = u[4], blobBytes = u[5], ascii = u[6]
+    let at = 8
+    this.woff = u.subarray(at, at + n + 1); at += n + 1
+    this.sbase = u.subarray(at, at + n + 1); at += n + 1
+    this.nbase = u.subarray(at, at + n + 1); at += n + 1
+    const soff = u.subarray(at, at + ns + 1); at += ns + 1
+    this.w = u.subarray(at, at + nw); at += nw
+    const numsAt = ((4 * at + 7) >> 3) << 3
+    this.nums = new Float64Array(buf.buffer, buf.byteOffset + numsAt, nn)
+    const blobAt = numsAt + 8 * nn
+    const strs = this.strs = new Array(ns)
+    if (ascii) {
+      const text = buf.toString('latin1', blobAt, blobAt + blobBytes)
+      for (let i = 0; i < ns; i++) strs[i] = text.substring(soff[i], soff[i + 1])
+    } else {
+      for (let i = 0; i < ns; i++) strs[i] = buf.toString('utf8', blobAt + soff[i], blobAt + soff[i + 1])
+    }
+    this.at = new Uint32Array(n)                             // each document's first diff word
   }
-  R.w = w; R.nums = nums; R.strs = strs
-  const P = new Array(n), B = new Array(n), C = new Array(n)
-  for (let d = 0; d < n; d++) {
-    if (woff[d] === woff[d + 1]) { P[d] = B[d] = C[d] = null; continue }
-    R.p = woff[d]; R.sb = sbase[d]; R.nb = nbase[d]
-    const sb = R.sb
+
+  enter(d, p) { R.w = this.w; R.nums = this.nums; R.strs = this.strs; R.p = p; R.sb = this.sbase[d]; R.nb = this.nbase[d] }
+  leave() { R.w = R.nums = R.strs = null }
+
+  head(d) {
+    if (this.woff[d] === this.woff[d + 1]) return null
+    this.enter(d, this.woff[d])
     const patch = { clock: rdClock(), deps: rdClock(), canUndo: false, canRedo: false, diffs: null }
-    B[d] = rdClock()
-    C[d] = rdClock()
+    const b = rdClock(), c = rdClock()
+    this.at[d] = R.p
+    this.leave()
+    return { patch, b, c }
+  }
+
+  diffs(d) {
+    this.enter(d, this.at[d])
+    const w = R.w, strs = R.strs, sb = R.sb
     const nd = w[R.p++]
     const diffs = new Array(nd)
     for (let k = 0; k < nd; k++) {
@@ -156,11 +171,21 @@ function decodeRound(buf, n) {
       } else e = { action: ACTIONS[action], type: TYPES[t], obj, index: w[R.p++] }
       diffs[k] = e
     }
-    patch.diffs = diffs
-    P[d] = patch
+    this.leave()
+    return diffs
   }
-  R.w = R.nums = R.strs = null
-  return { p: P, b: B, c: C }
+}
+
+// a JSON results buffer (the docset's debug form) read through the same interface
+class JsonRoundReader {
+  constructor(j) { this.j = j }
+  head(d) { const p = this.j.p[d]; return p ? { patch: Object.assign({}, p, { diffs: null }), b: this.j.b[d], c: this.j.c[d] } : null }
+  diffs(d) { return this.j.p[d].diffs }
+}
+
+function decodeRound(buf, n) {
+  if (buf.length === 0 || buf[0] === 0x7b) return new JsonRoundReader(JSON.parse(buf.toString()))
+  return new RoundReader(buf, n)
 }
 
 class History {
@@ -201,7 +226,6 @@ class GpuBackendState {
     this.clock = {}
     this.deps = {}
     this.backClock = {}              // max seq per actor over the whole log (queued included)
-    this.patch = null                // the last round's patch
   }
 
   change(i) {
@@ -408,14 +432,20 @@ class GpuEngine {
       for (const c of job.entries) state.log.push(c)
       state.histLen = res[RESULT_U32 * i + 3]
       state.nQueued = res[RESULT_U32 * i + 4]
-      const patch = j.p[i]
-      state.patch = patch
-      state.clock = patch.clock
-      state.deps = patch.deps
-      state.backClock = j.b[i]
-      ok.push([job, { patch, roundClock: j.c[i], backClock: j.b[i], minCmp: null }])
+      const h = j.head(i)
+      state.clock = h.patch.clock
+      state.deps = h.patch.deps
+      state.backClock = h.b
+      ok.push(i, { patch: h.patch, roundClock: h.c, backClock: h.b, minCmp: null })
     })
-    for (const [job, payload] of ok) job.done(payload)
+    // every state of the call is advanced before the first delivery; each patch's diffs are
+    // read just before it is delivered
+    for (let k = 0; k < ok.length; k += 2) {
+      const i = ok[k], payload = ok[k + 1]
+      payload.patch.diffs = j.diffs(i)
+      ok[k + 1] = null
+      items[i].job.done(payload)
+    }
   }
 
   raise(errors) {

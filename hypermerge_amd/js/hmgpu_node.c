@@ -744,15 +744,22 @@ static int gather_packed(napi_env env, napi_value ids_v, napi_value data_v, napi
     return 1;
 }
 
-static napi_value text_object(napi_env env, hm_text *t) {
+static void text_finalize(napi_env env, void *data, void *hint) { (void)env; (void)data; hm_text_free((hm_text *)hint); }
+
+/* {results, data}: results copied, data handed over without a copy (an external Buffer over the
+ * hm_text, freed when the Buffer is collected; *tp is then NULL) */
+static napi_value text_object(napi_env env, hm_text **tp) {
+    hm_text *t = *tp;
     size_t len = 0;
     const char *p = hm_text_data(t, &len);
     uint32_t n = 0;
     const hm_doc_result *r = hm_text_results(t, &n);
-    napi_value o;
+    napi_value o, dv;
     napi_create_object(env, &o);
     set(env, o, "results", buf_copy(env, r, (size_t)n * sizeof(hm_doc_result)));
-    set(env, o, "data", buf_copy(env, p, len));
+    if (len && napi_create_external_buffer(env, len, (void *)p, text_finalize, t, &dv) == napi_ok) *tp = NULL;
+    else dv = buf_copy(env, p, len);
+    set(env, o, "data", dv);
     return o;
 }
 
@@ -769,7 +776,7 @@ static void ds_call_js(napi_env env, napi_value cb, void *context, void *data) {
             argv[1] = undef;
         } else {
             napi_get_null(env, &argv[0]);
-            argv[1] = text_object(env, j->out);
+            argv[1] = text_object(env, &j->out);
         }
         napi_call_function(env, undef, cb, 2, argv, &ret);
     }
@@ -805,7 +812,7 @@ static napi_value docset_apply(napi_env env, napi_callback_info info, int packed
     if (cbt != napi_function) {
         int st = hm_docset_apply(d->ds, j->data, j->bo, j->db, j->ids, j->n, &j->out);
         if (st) { ds_job_free(j); return throw_status(env, d->engine, st, "hm_docset_apply"); }
-        napi_value o = text_object(env, j->out);
+        napi_value o = text_object(env, &j->out);
         ds_job_free(j);
         return o;
     }

@@ -105,7 +105,7 @@ function profStop() {
 }
 
 async function runGpu(mode, objects, diffsForm) {
-  const G = require(path.join(__dirname, '..', 'hypermerge_amd', 'js', 'GpuDocBackend.js'))
+  const G = require(process.env.HM_GPU_JS || path.join(__dirname, '..', 'hypermerge_amd', 'js', 'GpuDocBackend.js'))
   const engine = new G.GpuEngine({ mode, patches: patchesOn, diffs: diffsForm || 'ops' })
   const settle = async () => { if (mode === 'async') await engine.idle(); else { await tick(); await tick() } }
   // warm the device (engine, stores, kernels) outside the timed region
