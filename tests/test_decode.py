@@ -144,3 +144,53 @@ def test_synth_blocks_decode_to_the_generated_rows(name, kw):
     np.testing.assert_array_equal(ro.docs, rd.docs)
     np.testing.assert_array_equal(ro.clock, rd.clock)
     np.testing.assert_array_equal(ro.hist, rd.hist)
+
+
+def test_tables_independent_of_thread_count_with_failed_documents():
+    """Each decoder thread appends its document range into its own tables and a failed document
+    rolls its rows and names back: every table is the same at any thread count (more threads
+    than documents included), a failed document keeps only the root object, and elemIds of a
+    very long actor id (longer than the per-thread name arena's chunk) are intact."""
+    root = "00000000-0000-0000-0000-000000000000"
+    long_actor = "L" * 70000
+
+    def change(actor, seq, ops, deps=None):
+        return json.dumps({"actor": actor, "seq": seq, "deps": deps or {}, "ops": ops}).encode()
+
+    def text_doc(actor, n):
+        obj = "11111111-0000-0000-0000-00000000000%d" % (n % 10)
+        ops = [{"action": "makeText", "obj": obj},
+               {"action": "link", "obj": root, "key": "t", "value": obj}]
+        prev = "_head"
+        for i in range(1, n + 1):
+            ops.append({"action": "ins", "obj": obj, "key": prev, "elem": i})
+            ops.append({"action": "set", "obj": obj, "key": f"{actor}:{i}", "value": f"c{i}"})
+            prev = f"{actor}:{i}"
+        return [change(actor, 1, ops)]
+
+    docs = []
+    for d in range(23):
+        if d % 5 == 3:                                    # rows appended, then a bad op in the last change
+            docs.append(text_doc(f"a{d}", 4) + [change(f"a{d}", 2, [{"action": "bogus", "obj": root}], {f"a{d}": 1})])
+        elif d % 7 == 2:
+            docs.append([b'{"actor": "x", "seq": 1,'])   # JSON.parse throws
+        elif d == 11:
+            docs.append(text_doc(long_actor, 3))
+        else:
+            docs.append(text_doc(f"a{d}", 1 + d % 4) + [change(f"b{d}", 1, [
+                {"action": "set", "obj": root, "key": f"k{d}", "value": f"v{d % 3}"}])])
+    ref, st = decode_blocks(docs, threads=1)
+    bad = [d for d in range(23) if d % 5 == 3 or d % 7 == 2]
+    assert [d for d in range(23) if st[d]] == bad
+    for d in bad:
+        assert int(ref.docs[d]["n_changes"]) == 0 and int(ref.docs[d]["n_regs"]) == 0
+        assert ref.doc_objs[d] == [root] and ref.doc_actors[d] == [] and ref.doc_regs[d] == []
+    assert ref.doc_actors[11] == [long_actor]
+    assert [t for _, t in ref.doc_regs[11]][:3] == ["t", f"{long_actor}:1", f"{long_actor}:2"]
+    for threads in (2, 3, 7, 64):
+        b, s = decode_blocks(docs, threads=threads)
+        np.testing.assert_array_equal(s, st)
+        for f in ("docs", "changes", "deps", "ops"):
+            np.testing.assert_array_equal(getattr(b, f), getattr(ref, f), err_msg=f"{f} threads={threads}")
+        assert b.strings == ref.strings
+        assert b.doc_actors == ref.doc_actors and b.doc_objs == ref.doc_objs and b.doc_regs == ref.doc_regs
