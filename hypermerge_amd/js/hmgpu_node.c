@@ -553,6 +553,7 @@ static napi_value StatusMessage(napi_env env, napi_callback_info info) {
 typedef struct DsJob {
     struct DsJob *next;
     uint8_t *data;
+    napi_ref data_ref;                  /* packed calls: data is the caller's Buffer, held by this reference */
     uint64_t *bo;
     uint32_t *db, *ids, n;
     int st;
@@ -571,9 +572,12 @@ typedef struct {
     int started, stop, busy;
 } Docset;
 
-static void ds_job_free(DsJob *j) {
+/* env NULL (the environment is going away): a held Buffer reference is left to it */
+static void ds_job_free(napi_env env, DsJob *j) {
     if (!j) return;
-    free(j->data); free(j->bo); free(j->db); free(j->ids);
+    if (j->data_ref) { if (env) napi_delete_reference(env, j->data_ref); }
+    else free(j->data);
+    free(j->bo); free(j->db); free(j->ids);
     if (j->out) hm_text_free(j->out);
     free(j);
 }
@@ -735,12 +739,18 @@ static int gather_packed(napi_env env, napi_value ids_v, napi_value data_v, napi
     j->ids = (uint32_t *)malloc((size_t)n * 4 + 4);
     j->db = (uint32_t *)malloc(((size_t)n + 1) * 4);
     j->bo = (uint64_t *)malloc(((size_t)nb + 1) * 8);
-    j->data = (uint8_t *)malloc(dl + 1);
     memcpy(j->ids, ip, (size_t)n * 4);
     memcpy(j->db, db, ((size_t)n + 1) * 4);
     j->bo[0] = 0;
     for (uint32_t b = 0; b < nb; b++) j->bo[b + 1] = ends[b];
-    if (dl) memcpy(j->data, dp, dl);
+    /* the blocks are read where they lie: the Buffer is held until the call has called back
+     * (GpuEngine.prepare builds it for this call and never writes it again) */
+    if (dl && napi_create_reference(env, data_v, 1, &j->data_ref) == napi_ok) j->data = (uint8_t *)dp;
+    else {
+        j->data_ref = NULL;
+        j->data = (uint8_t *)malloc(dl + 1);
+        if (dl) memcpy(j->data, dp, dl);
+    }
     return 1;
 }
 
@@ -780,7 +790,7 @@ static void ds_call_js(napi_env env, napi_value cb, void *context, void *data) {
         }
         napi_call_function(env, undef, cb, 2, argv, &ret);
     }
-    ds_job_free(j);
+    ds_job_free(env, j);
 }
 
 /* docsetApply(docset, ids Uint32Array, blocks[][], callback?) -> {results, data} | undefined
@@ -806,20 +816,20 @@ static napi_value docset_apply(napi_env env, napi_callback_info info, int packed
     if (!d) return NULL;
     DsJob *j = (DsJob *)calloc(1, sizeof(DsJob));
     if (!(packed ? gather_packed(env, argv[1], argv[2], argv[3], argv[4], j) : gather_blocks(env, argv[1], argv[2], j))) {
-        ds_job_free(j);
+        ds_job_free(env, j);
         return NULL;
     }
     if (cbt != napi_function) {
         int st = hm_docset_apply(d->ds, j->data, j->bo, j->db, j->ids, j->n, &j->out);
-        if (st) { ds_job_free(j); return throw_status(env, d->engine, st, "hm_docset_apply"); }
+        if (st) { ds_job_free(env, j); return throw_status(env, d->engine, st, "hm_docset_apply"); }
         napi_value o = text_object(env, &j->out);
-        ds_job_free(j);
+        ds_job_free(env, j);
         return o;
     }
     napi_value name;
     napi_create_string_utf8(env, "hmgpu.docsetApply", NAPI_AUTO_LENGTH, &name);
     if (napi_create_threadsafe_function(env, cbv, NULL, name, 0, 1, NULL, NULL, d, ds_call_js, &j->tsfn) != napi_ok) {
-        ds_job_free(j);
+        ds_job_free(env, j);
         napi_throw_error(env, NULL, "napi_create_threadsafe_function failed");
         return NULL;
     }
@@ -828,7 +838,7 @@ static napi_value docset_apply(napi_env env, napi_callback_info info, int packed
         pthread_cond_init(&d->cv, NULL);
         if (pthread_create(&d->thread, NULL, docset_thread, d) != 0) {
             napi_release_threadsafe_function(j->tsfn, napi_tsfn_abort);
-            ds_job_free(j);
+            ds_job_free(env, j);
             napi_throw_error(env, NULL, "pthread_create failed");
             return NULL;
         }
@@ -1136,10 +1146,10 @@ static napi_value DecodeBlocks(napi_env env, napi_callback_info info) {
     napi_create_buffer_copy(env, (size_t)n * 4, ids, &idp, &idv);
     free(ids);
     DsJob *j = (DsJob *)calloc(1, sizeof(DsJob));
-    if (!gather_blocks(env, idv, argv[0], j)) { ds_job_free(j); return NULL; }
+    if (!gather_blocks(env, idv, argv[0], j)) { ds_job_free(env, j); return NULL; }
     hm_decoded *dd = NULL;
     int st = hm_decode_blocks(j->data, j->bo, j->db, n, get_u32(env, argv[1]), (int)get_u32(env, argv[2]), &dd);
-    ds_job_free(j);
+    ds_job_free(env, j);
     if (st) return throw_status(env, NULL, st, "hm_decode_blocks");
     hm_batch b;
     hm_decoded_batch(dd, &b);
