@@ -855,7 +855,8 @@ static napi_value docset_apply(napi_env env, napi_callback_info info, int packed
 
 static napi_value DocsetApply(napi_env env, napi_callback_info info) { return docset_apply(env, info, 0); }
 /* docsetApplyPacked(docset, ids, data, blockEnds, docBlock, callback?): docsetApply with the
- * blocks packed by the caller (gather_packed) */
+ * blocks packed by the caller (gather_packed).  `data` is read in place: with a callback the
+ * caller must not write it until the callback has run */
 static napi_value DocsetApplyPacked(napi_env env, napi_callback_info info) { return docset_apply(env, info, 1); }
 
 /* docsetHistoryPrefix(docset, doc, n) -> Buffer of u32 log indices (history order) */
