@@ -16,6 +16,7 @@
 // an undecodable block.  An undecodable block (the reference's Block.unpack / JSON.parse
 // throw) marks its document HM_ERR_INVALID with no rows; other documents are unaffected.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <memory>
@@ -62,6 +63,8 @@ template <typename T> struct Buf {
         p = (T *)q;
         cap = nb / sizeof(T);
     }
+    // capacity hint: a mapping the system refuses is left to growth on demand
+    void try_reserve(size_t k) { try { reserve(k); } catch (const std::bad_alloc &) {} }
     void push_back(const T &v) { if (n == cap) reserve(n + 1); p[n++] = v; }
     void append(const T *v, size_t k) { reserve(n + k); if (k) memcpy(p + n, v, k * sizeof(T)); n += k; }
     void resize(size_t k) { reserve(k); n = k; }           // new rows are not initialised
@@ -354,11 +357,17 @@ int hm_decode_blocks(const uint8_t *data, const uint64_t *block_off, const uint3
         std::vector<Part> parts(T);
         std::vector<uint32_t> lo(T + 1);
         for (int t = 0; t <= T; t++) lo[t] = (uint32_t)((uint64_t)n_docs * t / T);
+        // an exception inside a worker (out of memory) fails the call, not the process
         auto par = [&](auto &&f) {
             if (T == 1) { f(0); return; }
+            std::atomic<bool> failed{false};
             std::vector<std::thread> th;
-            for (int t = 0; t < T; t++) th.emplace_back(f, t);
+            auto run = [&](int t) { try { f(t); } catch (...) { failed = true; } };
+            for (int t = 0; t < T; t++) {
+                try { th.emplace_back(run, t); } catch (...) { run(t); }   // no thread to be had: this one
+            }
             for (auto &x : th) x.join();
+            if (failed) throw std::bad_alloc();
         };
         par([&](int t) {
             Ctx cx;
@@ -368,8 +377,8 @@ int hm_decode_blocks(const uint8_t *data, const uint64_t *block_off, const uint3
             // capacity for the range up front (untouched capacity is free): one change per block,
             // and no op or name row takes fewer than 16 bytes of JSON
             const uint64_t nb = block_off[doc_block[lo[t + 1]]] - block_off[doc_block[lo[t]]];
-            P.ch.reserve(doc_block[lo[t + 1]] - doc_block[lo[t]]);
-            P.op.reserve(nb / 16 + 16); P.op_str.reserve(nb / 16 + 16);
+            P.ch.try_reserve(doc_block[lo[t + 1]] - doc_block[lo[t]]);
+            P.op.try_reserve(nb / 16 + 16); P.op_str.try_reserve(nb / 16 + 16);
             for (uint32_t d = lo[t]; d < lo[t + 1]; d++) {
                 Part::Doc &doc = P.docs[d - lo[t]];
                 const Part::Mark m = P.mark();
