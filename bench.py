@@ -344,66 +344,109 @@ def _node_e2e(args):
 def _incremental(eng, batch, args, tail=4):
     """The north-star event on resident state: every document of the shard is resident in a
     hm_store with all but its last `tail` changes; then rounds in which each document receives
-    its next 1-2 changes (hm_batch_submit + hm_batch_wait, H2D of the new rows and D2H of the
-    per-document results included).  The same rounds run on a second store with the
-    incremental path off (whole-log re-merge) for the comparison and an equality check."""
-    from hypermerge_amd.store import RowStore, slice_changes
-    n = batch.n_docs
+    its next 1-2 changes (DocBackend.ts:169-185).  `value`: the rounds' new rows already in HBM
+    (hm_batch_submit_device + hm_batch_wait_device: plan, append, the incremental kernels, the
+    gathered per-document results), the same convention as the headline.  The same rounds run on
+    a second store with the incremental path off (whole-log re-merge) for the comparison and an
+    equality check of every round's results, and on a third through the host entry points
+    (hm_batch_submit / hm_batch_wait from page-locked buffers: PCIe included, never `value`)."""
+    import torch
+    from hypermerge_amd.store import RowStore, slice_changes, BatchResult
+    from hypermerge_amd.columnar import DOC_RESULT_DT
+    dev = torch.device("cuda", torch.cuda.current_device())
+    n, S = batch.n_docs, batch.a_stride
     nch = batch.docs["n_changes"].astype(np.int64)
     start = np.maximum(nch - tail, 0)
-    rng = np.random.default_rng(5)
-    stores = []
-    for inc in (True, False):
-        st = RowStore(eng, a_stride=batch.a_stride)
-        st.set_incremental(inc)
-        h0 = st.open_n(n)
-        st.submit_batch(slice_changes(batch, np.zeros(n, np.int64), start), np.arange(h0, h0 + n))
-        st.wait()
-        stores.append((st, h0))
-    from hypermerge_amd.store import BatchResult
-    from hypermerge_amd.columnar import DOC_RESULT_DT
-    S = batch.a_stride
-    # result arrays kept between rounds, as a long-running RepoBackend keeps its buffers (page-locked,
-    # so the per-round D2H runs at DMA speed)
-    import torch
+
+    def to_dev(b, hs):
+        t = [torch.from_numpy(np.ascontiguousarray(x).view(np.uint8).reshape(-1)).to(dev) for x in
+             (b.docs, b.changes, b.deps, b.ops, np.ascontiguousarray(hs, np.uint32))]
+        return (len(b.changes), len(b.deps), len(b.ops)), t
 
     def pinned(shape, dt):
         nb = int(np.prod(shape)) * np.dtype(dt).itemsize
         return torch.zeros(max(nb, 1), dtype=torch.uint8, pin_memory=True).numpy()[:nb].view(dt).reshape(shape)
-    outs = [BatchResult(pinned((n,), DOC_RESULT_DT), pinned((n, S), np.uint32), pinned((n, S), np.uint32),
-                        pinned((n, S), np.uint32)) for _ in stores]
+
+    first = slice_changes(batch, np.zeros(n, np.int64), start)
+    fc, ft = to_dev(first, np.arange(n))
+    stores = []
+    for inc in (True, False, True):
+        st = RowStore(eng, a_stride=S)
+        st.set_incremental(inc)
+        h0 = st.open_n(n)
+        assert h0 == 0
+        st.submit_device(n, fc, *ft)
+        st.wait_device(torch.empty(n * (32 + 12 * S), dtype=torch.uint8, device=dev))
+        stores.append(st)
+    del ft
+    # the rounds, staged in HBM (and page-locked host copies for the PCIe leg) before any timing
+    rng = np.random.default_rng(5)
     pos = start.copy()
-    rounds = []
-    same = True
+    rounds_in = []
     while (pos < nch).any():
         k = rng.integers(1, 3, n)
         hi = np.minimum(pos + k, nch)
         sel = np.nonzero(hi > pos)[0]
         sub = slice_changes(batch, pos, hi, sel)
-        r = {"docs": int(len(sel)), "changes": int(len(sub.changes))}
-        res = []
-        for (st, h0), tag, keep in zip(stores, ("incremental", "remerge"), outs):
-            hs = (sel + h0).astype(np.uint32)
-            t = time.perf_counter()
-            st.submit_batch(sub, hs)
-            out = st.wait(keep)
-            dt = time.perf_counter() - t
-            res.append(out)
-            r[tag] = {"ms": dt * 1e3, "changes_per_s": len(sub.changes) / dt, "routing": st.last_routing()}
-        same &= bool(np.array_equal(res[0].docs, res[1].docs) and np.array_equal(res[0].clock, res[1].clock)
-                     and np.array_equal(res[0].heads, res[1].heads))
-        rounds.append(r)
+        cnt, t = to_dev(sub, sel)
+        rounds_in.append((sub, sel.astype(np.uint32), cnt, t))
         pos = np.maximum(pos, hi)
+    out = [torch.empty(n * (32 + 12 * S), dtype=torch.uint8, device=dev) for _ in range(2)]
+    keep = BatchResult(pinned((n,), DOC_RESULT_DT), pinned((n, S), np.uint32), pinned((n, S), np.uint32),
+                       pinned((n, S), np.uint32))
+    rounds, same, routing_ok = [], True, True
+    for sub, sel, cnt, t in rounds_in:
+        r = {"docs": int(len(sel)), "changes": int(len(sub.changes)), "ops": int(len(sub.ops))}
+        nb = len(sel) * (32 + 12 * S)
+        for st, tag, o in zip(stores[:2], ("incremental", "remerge"), out):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            st.submit_device(len(sel), cnt, *t)
+            nf = st.wait_device(o)
+            torch.cuda.synchronize(dev)
+            dt = time.perf_counter() - t0
+            r[tag] = {"ms": dt * 1e3, "changes_per_s": len(sub.changes) / dt, "routing": st.last_routing(), "failed": nf}
+        same &= bool(torch.equal(out[0][:nb], out[1][:nb]))
+        routing_ok &= r["incremental"]["routing"]["incremental"] == len(sel)
+        # PCIe leg: host tables in page-locked memory, results into kept page-locked arrays
+        pb = _pinned_rows(sub)
+        t0 = time.perf_counter()
+        stores[2].submit_batch(pb[0], sel)
+        res = stores[2].wait(keep)
+        dt = time.perf_counter() - t0
+        r["pcie_incremental"] = {"ms": dt * 1e3, "changes_per_s": len(sub.changes) / dt}
+        got = out[0][:nb].cpu().numpy()
+        same &= bool(np.array_equal(got[:len(sel) * 32].view(DOC_RESULT_DT), res.docs)
+                     and np.array_equal(got[len(sel) * 32:len(sel) * (32 + 4 * S)].view(np.uint32).reshape(-1, S), res.clock))
+        rounds.append(r)
     tot_c = sum(r["changes"] for r in rounds)
     t_inc = sum(r["incremental"]["ms"] for r in rounds) / 1e3
     t_rem = sum(r["remerge"]["ms"] for r in rounds) / 1e3
-    for st, _ in stores:
+    t_pci = sum(r["pcie_incremental"]["ms"] for r in rounds) / 1e3
+    for st in stores:
         st.close()
     return {"value": tot_c / t_inc, "unit": "changes/s", "resident_docs": n,
             "us_per_round": t_inc * 1e6 / len(rounds), "remerge_value": tot_c / t_rem,
-            "speedup_vs_remerge": t_rem / t_inc, "same_as_remerge": same, "rounds": rounds,
-            "path": "RowStore (hm_store): hm_batch_submit + hm_batch_wait per round, new rows H2D and "
-                    "per-document results D2H included; incremental = inc_apply_kernel"}
+            "speedup_vs_remerge": t_rem / t_inc, "same_as_remerge": same, "all_incremental": routing_ok,
+            "pcie_value": tot_c / t_pci, "rounds": rounds,
+            "path": "RowStore (hm_store): hm_batch_submit_device + hm_batch_wait_device per round (new rows in HBM, "
+                    "per-document results gathered in HBM); incremental = inc_group_kernel; pcie_* = hm_batch_submit / "
+                    "hm_batch_wait from page-locked host buffers"}
+
+
+def _pinned_rows(b):
+    """Batch `b` with its tables copied into page-locked host memory (returned with the keep-alive list)."""
+    import dataclasses
+    import torch
+    keep = []
+
+    def pin(a):
+        t = torch.zeros(max(a.nbytes, 1), dtype=torch.uint8, pin_memory=True)
+        keep.append(t)
+        v = t.numpy()[:a.nbytes].view(a.dtype).reshape(a.shape)
+        v[...] = a
+        return v
+    return dataclasses.replace(b, docs=pin(b.docs), changes=pin(b.changes), deps=pin(b.deps), ops=pin(b.ops)), keep
 
 
 def _clock_exchange(eng, batch, run, dev, rank, ws, cfg):

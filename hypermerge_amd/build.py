@@ -13,7 +13,7 @@ CSRC = os.path.join(HERE, "csrc")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("HM_OFFLOAD_ARCH", "gfx950")
 
-GPU_SRCS = ["merge_kernels.hip", "merge_large.hip", "store_kernels.hip", "exchange.hip", "cursors.hip", "engine.cpp", "store.cpp",
+GPU_SRCS = ["merge_kernels.hip", "merge_large.hip", "store_kernels.hip", "inc_kernels.hip", "exchange.hip", "cursors.hip", "engine.cpp", "store.cpp",
             "decode.cpp", "docset.cpp"]
 GPU_DEPS = GPU_SRCS + ["scan.h", "merge_kernels.h", "store_kernels.h", "engine_internal.h", "../../include/hypermerge_amd.h"]
 

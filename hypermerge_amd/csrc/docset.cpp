@@ -25,6 +25,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -313,6 +314,7 @@ struct Round {
     // snapshot for the rollback
     uint32_t s_actors = 0, s_objs = 0, s_regs = 0, s_strs = 0, s_cents = 0, s_content = 0, s_ops = 0;
     std::vector<uint16_t> s_rank_of, s_by_rank;
+    bool started = false;                                    // its decode took the snapshot above
     // placement in this call
     uint8_t cls = NO_CLASS;
     uint32_t handle = 0, row = 0;
@@ -335,14 +337,24 @@ struct Scratch {
     std::vector<uint32_t> t2n;
 };
 
+// f(lo, hi, t) over T ranges of [0, n) on host threads.  A worker's exception (out of memory: block
+// data comes from peers, brotli output is unbounded) is caught in the worker, every started
+// thread is joined, a range whose thread cannot be created runs on this one, and the failure is
+// rethrown here as std::bad_alloc (the call returns HM_ERR_NOMEM instead of terminating the process).
 template <typename F> void par_for(uint32_t n, uint32_t T, F &&f) {
     T = std::max(1u, std::min(T, n));
     if (T <= 1) { f(0u, n, 0u); return; }
+    std::atomic<bool> failed{false};
+    auto run = [&f, &failed, n, T](uint32_t t) {
+        try { f((uint32_t)((uint64_t)n * t / T), (uint32_t)((uint64_t)n * (t + 1) / T), t); } catch (...) { failed = true; }
+    };
     std::vector<std::thread> th;
-    th.reserve(T);
-    for (uint32_t t = 0; t < T; t++)
-        th.emplace_back([&f, n, t, T] { f((uint32_t)((uint64_t)n * t / T), (uint32_t)((uint64_t)n * (t + 1) / T), t); });
+    try { th.reserve(T); } catch (...) {}
+    for (uint32_t t = 0; t < T; t++) {
+        try { th.emplace_back(run, t); } catch (...) { run(t); }
+    }
     for (auto &x : th) x.join();
+    if (failed) throw std::bad_alloc();
 }
 
 void rollback(DocSt &d, Round &R) {
@@ -377,6 +389,7 @@ void decode_round(DocSt &d, Round &R, const uint8_t *data, const uint64_t *bo, S
     if (!d.ready) d.setup();
     R.s_actors = d.actors.size(); R.s_objs = d.objs.size(); R.s_regs = d.regs.size(); R.s_strs = d.strs.size();
     R.s_cents = (uint32_t)d.cents.size(); R.s_content = d.n_content; R.s_ops = (uint32_t)d.op_actor.size();
+    R.started = true;
     Ctx &cx = X.cx;
     const uint32_t n = R.b1 - R.b0;
     cx.arena.clear();
@@ -1101,7 +1114,7 @@ struct hm_docset {
     std::mutex open_mu;
     std::atomic<bool> busy{false};
     uint64_t stat[8] = {0, 0, 0, 0, 0, 0, 0, 0};           // rounds, docs, restrides, hit-register patches, full patches,
-                                                             // per-op patches, replay mismatches
+                                                             // per-op patches, replay mismatches, replay checks skipped
     DocSt &doc(uint32_t i) { return chunks[i / CHUNK][i % CHUNK]; }
 };
 
@@ -1156,14 +1169,20 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
     std::vector<Round> R(n);
     for (uint32_t i = 0; i < n; i++) { R[i].doc = docs[i]; R[i].b0 = doc_block[i]; R[i].b1 = doc_block[i + 1]; }
     const uint32_t T = std::min<uint32_t>(ds->threads, std::max<uint32_t>(1, n / 64));
-    par_for(n, T, [&](uint32_t lo, uint32_t hi, uint32_t) {
-        Scratch X;
-        for (uint32_t i = lo; i < hi; i++) {
-            DocSt &d = ds->doc(R[i].doc);
-            decode_round(d, R[i], data, bo, X);
-            if (R[i].status != HM_OK) rollback(d, R[i]);
-        }
-    });
+    try {
+        par_for(n, T, [&](uint32_t lo, uint32_t hi, uint32_t) {
+            Scratch X;
+            for (uint32_t i = lo; i < hi; i++) {
+                DocSt &d = ds->doc(R[i].doc);
+                decode_round(d, R[i], data, bo, X);
+                if (R[i].status != HM_OK) { rollback(d, R[i]); R[i].started = false; }
+            }
+        });
+    } catch (...) {
+        // a decode ran out of memory: every document whose decode started goes back
+        for (uint32_t i = 0; i < n; i++) if (R[i].started) rollback(ds->doc(R[i].doc), R[i]);
+        throw;
+    }
     mark("decode");
     // placement: a document lives in the narrowest class that holds its actors
     std::vector<std::vector<uint32_t>> by_cls(N_CLASS);
@@ -1179,9 +1198,20 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
         x.handle = d.handle;
         by_cls[c].push_back(i);
     }
-    struct ClsOut { std::vector<hm_doc_result> res; std::vector<uint32_t> clock, back, heads; uint64_t id = 0; bool sub = false; };
+    struct ClsOut {
+        std::vector<hm_doc_result> res;
+        std::vector<uint32_t> clock, back, heads;
+        uint64_t id = 0;
+        bool sub = false, done = false;                      // submitted / waited (applied on the device)
+    };
     std::vector<ClsOut> co(N_CLASS);
     int rc = HM_OK;
+    // fault injection for the tests (HM_DOCSET_INJECT_FAIL=wait:<k> fails the call after the k-th
+    // class's batch is applied, =read after every class's; the call must then be undone everywhere)
+    const char *inj = getenv("HM_DOCSET_INJECT_FAIL");
+    const int inj_wait = inj && !strncmp(inj, "wait:", 5) ? atoi(inj + 5) : -1;
+    const bool inj_read = inj && !strcmp(inj, "read");
+    int n_waited = 0;
     for (uint32_t c = 0; c < N_CLASS && rc == HM_OK; c++) {
         auto &rows = by_cls[c];
         if (rows.empty()) continue;
@@ -1258,25 +1288,33 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
         O.heads.resize(rows.size() * (size_t)S);
         if ((rc = hm_batch_wait(st, O.id, O.res.data(), O.clock.data(), O.back.data(), O.heads.data()))) break;
         O.sub = false;
+        O.done = true;
+        if (n_waited++ == inj_wait) { rc = hm_engine_fail(ds->e, HM_ERR_DEVICE, "injected failure (HM_DOCSET_INJECT_FAIL)"); break; }
         for (uint32_t k = 0; k < rows.size(); k++) {
             Round &x = R[rows[k]];
             x.res = O.res[k];
             x.clock = O.clock.data() + (size_t)k * S; x.back = O.back.data() + (size_t)k * S; x.heads = O.heads.data() + (size_t)k * S;
         }
     }
-    if (rc) {
-        // a call-level failure: every document of the call rolls back on the host (a store
-        // whose batch is in flight is waited for first)
-        for (uint32_t c = 0; c < N_CLASS; c++)
+    // a call-level failure: the call is applied to no store — a store whose batch is in flight is
+    // waited for, the batches already applied are undone (hm_batch_undo) — and every document of
+    // the call rolls back on the host
+    auto fail_call = [&](int why) {
+        for (uint32_t c = 0; c < N_CLASS; c++) {
             if (co[c].sub) {
                 std::vector<hm_doc_result> tmp(by_cls[c].size());
-                (void)hm_batch_wait(ds->stores[c], co[c].id, tmp.data(), nullptr, nullptr, nullptr);
+                if (hm_batch_wait(ds->stores[c], co[c].id, tmp.data(), nullptr, nullptr, nullptr) == HM_OK) co[c].done = true;
+                co[c].sub = false;
             }
+            if (co[c].done) { (void)hm_batch_undo(ds->stores[c], co[c].id); co[c].done = false; }
+        }
         for (uint32_t i = 0; i < n; i++) if (R[i].status == HM_OK) rollback(ds->doc(R[i].doc), R[i]);
-        return rc;
-    }
+        return why;
+    };
+    if (rc) return fail_call(rc);
     mark("merge");
-    // commit or roll back each document; the registers each patch reads
+    // failed documents roll back; the registers and history slices each patch reads are requested
+    // before any document's host state advances (a failed read then fails the call on every store)
     std::vector<std::vector<uint32_t>> qdocs(N_CLASS), qregs(N_CLASS), hreq(N_CLASS);
     std::vector<uint32_t> cap(N_CLASS, 0);
     for (uint32_t i = 0; i < n; i++) {
@@ -1288,33 +1326,10 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
             if (x.placed) { d.cls = x.cls; d.handle = x.handle; }          // an empty document in its store
             continue;
         }
-        const uint32_t prev_hist = d.hist_len, prev_q = d.n_queued, old_n_ops = d.n_ops;
-        x.prev_hist = prev_hist;
-        d.cls = x.cls; d.handle = x.handle;
-        d.flags |= x.flags;
-        d.n_changes += (uint32_t)x.ch.size();
-        d.n_ops += (uint32_t)x.op.size();
-        d.hist_len = x.res.hist_len; d.n_queued = x.res.n_queued;
-        d.obj_type.resize(x.n_objs, NO_TYPE);
-        d.obj_emitted.resize(x.n_objs, 0);
-        d.sig.resize(x.n_regs, 0);
-        for (const hm_op_row &o : x.op)
-            if (o.action <= HM_MAKE_TEXT && o.obj < d.obj_type.size() && d.obj_type[o.obj] == NO_TYPE) d.obj_type[o.obj] = o.action;
+        x.prev_hist = d.hist_len;
         if (!ds->patches) continue;
-        if (ds->op_diffs) {
-            // the replay's view of the log (op indices are the store's: appended in order)
-            for (const hm_change_row &c : x.ch) {
-                d.ch_op0.push_back(old_n_ops + c.op_first);
-                d.op_seq.insert(d.op_seq.end(), c.n_ops, c.seq);
-            }
-            d.oplog.insert(d.oplog.end(), x.op.begin(), x.op.end());
-            d.rs.resize(x.n_regs);
-            d.el_op.resize(x.n_regs, HM_NONE);
-            d.el_in.resize(x.n_regs, 0);
-            hreq[x.cls].push_back(i);
-            continue;
-        }
-        x.full = !(prev_q == 0 && x.res.n_queued == 0 && x.res.hist_len - prev_hist == x.ch.size());
+        if (ds->op_diffs) { hreq[x.cls].push_back(i); continue; }
+        x.full = !(d.n_queued == 0 && x.res.n_queued == 0 && x.res.hist_len - d.hist_len == x.ch.size());
         x.q0 = (uint32_t)qregs[x.cls].size();
         if (x.full) {
             for (uint32_t g = 0; g < x.n_regs; g++) { qdocs[x.cls].push_back(x.handle); qregs[x.cls].push_back(g); }
@@ -1337,6 +1352,7 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
     }
     std::vector<std::vector<hm_reg_result>> rrows(N_CLASS);
     std::vector<std::vector<hm_surv_result>> rsurv(N_CLASS);
+    if (inj_read) return fail_call(hm_engine_fail(ds->e, HM_ERR_DEVICE, "injected failure (HM_DOCSET_INJECT_FAIL)"));
     for (uint32_t c = 0; c < N_CLASS; c++) {
         if (qregs[c].empty()) continue;
         rrows[c].resize(qregs[c].size());
@@ -1344,7 +1360,7 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
         uint32_t got = 0;
         rc = hm_store_read_regs(ds->stores[c], (uint32_t)qregs[c].size(), qdocs[c].data(), qregs[c].data(), rrows[c].data(),
                                 rsurv[c].data(), (uint32_t)rsurv[c].size(), &got);
-        if (rc) return rc;
+        if (rc) return fail_call(rc);
     }
     // op diffs: each document's history slice of this round (the changes the GPU applied, in
     // application order) with their allDeps rows
@@ -1355,18 +1371,44 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
         std::vector<uint32_t> hh(m), from(m), to(m), off(m + 1, 0);
         for (uint32_t k = 0; k < m; k++) {
             Round &x = R[hreq[c][k]];
-            const DocSt &d = ds->doc(x.doc);
             hh[k] = x.handle;
             to[k] = x.res.hist_len;
             from[k] = x.prev_hist;
             off[k + 1] = off[k] + (to[k] - from[k]);
             x.h0 = off[k]; x.h1 = off[k + 1];
-            (void)d;
         }
         hlog[c].resize(std::max(1u, off[m]));                 // (rounds that applied nothing: no rows)
         had[c].resize(std::max<size_t>(1, (size_t)off[m] * STRIDES[c]));
         rc = hm_store_read_history(ds->stores[c], m, hh.data(), from.data(), to.data(), off.data(), hlog[c].data(), had[c].data());
-        if (rc) return rc;
+        if (rc) return fail_call(rc);
+    }
+    // commit: every successful document's host state advances with the device's
+    for (uint32_t i = 0; i < n; i++) {
+        Round &x = R[i];
+        if (x.status != HM_OK) continue;
+        DocSt &d = ds->doc(x.doc);
+        const uint32_t old_n_ops = d.n_ops;
+        d.cls = x.cls; d.handle = x.handle;
+        d.flags |= x.flags;
+        d.n_changes += (uint32_t)x.ch.size();
+        d.n_ops += (uint32_t)x.op.size();
+        d.hist_len = x.res.hist_len; d.n_queued = x.res.n_queued;
+        d.obj_type.resize(x.n_objs, NO_TYPE);
+        d.obj_emitted.resize(x.n_objs, 0);
+        d.sig.resize(x.n_regs, 0);
+        for (const hm_op_row &o : x.op)
+            if (o.action <= HM_MAKE_TEXT && o.obj < d.obj_type.size() && d.obj_type[o.obj] == NO_TYPE) d.obj_type[o.obj] = o.action;
+        if (ds->patches && ds->op_diffs) {
+            // the replay's view of the log (op indices are the store's: appended in order)
+            for (const hm_change_row &c : x.ch) {
+                d.ch_op0.push_back(old_n_ops + c.op_first);
+                d.op_seq.insert(d.op_seq.end(), c.n_ops, c.seq);
+            }
+            d.oplog.insert(d.oplog.end(), x.op.begin(), x.op.end());
+            d.rs.resize(x.n_regs);
+            d.el_op.resize(x.n_regs, HM_NONE);
+            d.el_in.resize(x.n_regs, 0);
+        }
     }
     mark("read regs");
     // render every document's patch and DocBackend.clock
@@ -1454,9 +1496,9 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
             std::vector<hm_reg_result> gr(vr.size());
             std::vector<hm_surv_result> gs(std::max<uint32_t>(vcap, 1));
             uint32_t got = 0;
-            rc = hm_store_read_regs(ds->stores[c], (uint32_t)vr.size(), vd.data(), vr.data(), gr.data(), gs.data(),
-                                    (uint32_t)gs.size(), &got);
-            if (rc) return rc;
+            // (a self-check of the committed round: a read that fails skips it, stat[7])
+            if (hm_store_read_regs(ds->stores[c], (uint32_t)vr.size(), vd.data(), vr.data(), gr.data(), gs.data(),
+                                   (uint32_t)gs.size(), &got) != HM_OK) { ds->stat[7]++; continue; }
             std::atomic<uint64_t> bad{0};
             const uint32_t nq = (uint32_t)vr.size();
             par_for(nq, std::min<uint32_t>(ds->threads, std::max<uint32_t>(1, nq / 4096)), [&](uint32_t lo, uint32_t hi, uint32_t) {

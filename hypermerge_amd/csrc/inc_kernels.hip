@@ -1,0 +1,527 @@
+// inc_kernels.hip — incremental applyRemoteChanges on the resident store (store.cpp).
+//
+// The reference applies only the new changes to the live opSet (src/DocBackend.ts:169-185 ->
+// Automerge Backend.applyChanges): a change that is causallyReady against
+// opSet.clock is applied at once (the first applyQueuedOps pass), its allDeps is the
+// transitiveDeps fold over its deps' allDeps rows, and each of its ops runs applyAssign on one
+// register: the survivors not causally before the op stay, the op is pushed (set / link), and
+// the list is sorted by actor descending (sortBy(actor).reverse(), stable).  A document whose new
+// changes all apply in arrival order on its resident state is advanced here; its cost is the new
+// rows plus the registers they hit — the rest of the document is not read.
+//
+//   inc_group_kernel<G>  G lanes per document (G >= the store's actor stride: lane = actor for
+//                        clock / allDeps rows, lane = survivor for a register's list), 256 / G
+//                        documents per workgroup.  Loads are issued in four dependent levels:
+//                        the descriptor; the document's clock rows, new change / dep / op rows and
+//                        the log's last rows (the fold sources are found there by (actor, seq));
+//                        the fold sources' allDeps rows and the hit registers' rows; their
+//                        survivors with their (actor, seq) metadata (IncState / smeta: no log
+//                        search).  A document outside the group's limits is handed to the
+//                        G = 64 instantiation (defer), anything outside the incremental envelope
+//                        to the re-merge (bail) — both before the first store.
+//   inc_meta_kernel      after a re-merge: the survivors' (actor, seq, counter-set) metadata, the
+//                        objects created as maps and the counter bound of each document.
+// All of it is integer row work, HBM / latency bound.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/hypermerge_amd.h"
+#include "store_kernels.h"
+
+namespace hmi {
+
+enum { INC_DONE = 0, INC_DEFER = 1, INC_BAIL = 2 };
+constexpr uint32_t NC = HM_INC_MAX_NEW_C;     // new changes per document and submit (allDeps rows in registers)
+constexpr uint32_t TB = 8;                    // fold sources whose allDeps rows are loaded together
+
+// lanes [base, base + G) of the wave hold one document; every group-level branch is uniform
+// within the group (shuffles and ballots are then well defined for it)
+template <int G>
+struct Grp {
+    uint32_t lane, gl, base;
+    __device__ Grp() {
+        lane = __lane_id();
+        gl = lane & (G - 1);
+        base = lane & ~(uint32_t)(G - 1);
+    }
+    __device__ __forceinline__ uint64_t bits(bool p) const {
+        const uint64_t b = __ballot(p);
+        if constexpr (G == 64) return b;
+        else return (b >> base) & ((1ull << G) - 1);
+    }
+    __device__ __forceinline__ uint32_t below(uint64_t m) const { return (uint32_t)__popcll(m & ((1ull << gl) - 1)); }
+    __device__ __forceinline__ uint32_t sh(uint32_t x, uint32_t l) const { return (uint32_t)__shfl((int)x, (int)l, G); }
+    __device__ __forceinline__ uint32_t up(uint32_t x, uint32_t d) const { return (uint32_t)__shfl_up((int)x, d, G); }
+    // lane l of the group receives x from the lane that names it (dst must be a permutation of the group)
+    __device__ __forceinline__ uint32_t to(uint32_t x, uint32_t dst) const {
+        return (uint32_t)__builtin_amdgcn_ds_permute((int)((base + dst) << 2), (int)x);
+    }
+};
+
+__device__ __forceinline__ uint32_t sel_nc(const uint32_t (&v)[NC], uint32_t j) {
+    uint32_t r = v[0];
+#pragma unroll
+    for (uint32_t x = 1; x < NC; x++) r = j == x ? v[x] : r;
+    return r;
+}
+__device__ __forceinline__ void set_nc(uint32_t (&v)[NC], uint32_t j, uint32_t y) {
+#pragma unroll
+    for (uint32_t x = 0; x < NC; x++) v[x] = j == x ? y : v[x];
+}
+__device__ __forceinline__ uint64_t abs64(int64_t v) { return v < 0 ? (uint64_t)(-v) : (uint64_t)v; }
+
+constexpr unsigned long long TWO53 = 1ull << 53;
+
+template <int G>
+__device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 *smt) {
+    const Grp<G> g;
+    const uint32_t gl = g.gl;
+    const uint32_t S = A.S, h = D.handle, NA = D.n_actors, nnc = D.n_new_c, nno = D.n_new_o, nnd = D.n_new_d;
+    constexpr int FAILG = G < 64 ? INC_DEFER : INC_BAIL;     // a limit of this group size only
+    constexpr uint32_t KT = G >= 32 ? 1u : 32u / G;           // the log's last KT * G rows are searched first
+    if (nnc == 0 || nnc > NC || NA > S || S > G || D.n_old_r > D.n_r) return INC_BAIL;
+    if (nno > G || nnd > G) return FAILG;
+
+    // ---- level 2: everything that depends only on the descriptor ----
+    const IncState I = A.ist[h];
+    const hm_doc_result R0 = A.res_docs[h];
+    uint32_t ck = 0, hd = 0, mc = 0;
+    if (gl < S) {
+        ck = A.clock[(size_t)h * S + gl];
+        hd = A.heads[(size_t)h * S + gl];
+        mc = A.min_clock ? A.min_clock[(size_t)h * S + gl] : 0u;
+    }
+    uint32_t ca = 0, cq = 0, cnd = 0, cdo = 0, cno = 0, coo = 0;
+    if (gl < nnc) {
+        const hm_change_row c = A.changes[D.dst_c + D.n_old_c + gl];
+        ca = c.actor; cq = c.seq; cnd = c.n_deps; cdo = c.dep_off - D.dst_d; cno = c.n_ops; coo = c.op_first - D.dst_o;
+    }
+    uint32_t o_act = 0, o_dt = 0, o_obj = 0, o_reg = 0xFFFFFFFFu, o_vt = 0, o_vlo = 0, o_vhi = 0;
+    if (gl < nno) {
+        const hm_op_row op = A.ops[D.dst_o + D.n_old_o + gl];
+        o_act = op.action; o_dt = op.datatype; o_obj = op.obj; o_reg = op.reg; o_vt = op.vtag;
+        o_vlo = (uint32_t)op.value; o_vhi = (uint32_t)(op.value >> 32);
+    }
+    uint32_t dpa = 0, dpq = 0;
+    if (gl < nnd) {
+        const hm_dep_row d = A.deps[D.dst_d + D.n_old_d + gl];
+        dpa = d.actor; dpq = d.seq;
+    }
+    // the log's last rows, newest first: (actor, seq) and the history position (an applied
+    // change has one; duplicates and queued copies do not)
+    uint32_t tka[KT], tkq[KT];
+    int32_t tkh[KT];
+#pragma unroll
+    for (uint32_t k = 0; k < KT; k++) {
+        const int idx = (int)D.n_old_c - 1 - (int)(k * G + gl);
+        tka[k] = 0xFFFFFFFFu; tkq[k] = 0; tkh[k] = -1;
+        if (idx >= 0) {
+            const uint2 w = *reinterpret_cast<const uint2 *>(A.changes + D.dst_c + idx);
+            tka[k] = w.x & 0xFFFFu; tkq[k] = w.y;
+            tkh[k] = A.hist[D.src_c + idx];
+        }
+    }
+    if (!(I.flags & HM_IST_VALID)) return INC_BAIL;
+
+    // ---- the new rows: grouped by change, in order, after the old rows; supported ops ----
+    uint32_t sd = gl < nnc ? cnd : 0u, so = gl < nnc ? cno : 0u;
+#pragma unroll
+    for (uint32_t d = 1; d < (uint32_t)G; d <<= 1) {
+        const uint32_t yd = g.up(sd, d), yo = g.up(so, d);
+        if (gl >= d) { sd += yd; so += yo; }
+    }
+    const uint32_t xd = sd - (gl < nnc ? cnd : 0u), xo = so - (gl < nnc ? cno : 0u);
+    const uint32_t total_d = g.sh(sd, nnc - 1), total_o = g.sh(so, nnc - 1);
+    const bool bad_c = gl < nnc && (ca >= NA || cq == 0 || cdo != D.n_old_d + xd || coo != D.n_old_o + xo);
+    const int64_t oval = (int64_t)(((uint64_t)o_vhi << 32) | o_vlo);
+    const bool bad_o = gl < nno && ((o_act != HM_SET && o_act != HM_DEL && o_act != HM_LINK && o_act != HM_INC) ||
+                                    (o_act == HM_INC && o_vt != HM_V_INT && o_vt != HM_V_FLOAT) ||
+                                    o_obj >= D.n_objs || o_reg >= D.n_r ||
+                                    (o_vt == HM_V_INT && abs64(oval) > TWO53) ||
+                                    // an object other than ROOT must be a map / table the log created
+                                    (o_obj != 0 && (o_obj >= 64 || !((I.mapmask >> o_obj) & 1ull))));
+    if (g.bits(bad_c || bad_o) || total_o != nno || total_d != nnd) return INC_BAIL;
+    // integer counters: |base| + sum|inc| of every counter stays <= 2^53 (the re-merge's exact rule)
+    unsigned long long cadd = (gl < nno && o_vt == HM_V_INT &&
+                               (o_act == HM_INC || (o_act == HM_SET && o_dt == HM_DT_COUNTER))) ? abs64(oval) : 0ull;
+#pragma unroll
+    for (uint32_t d = 1; d < (uint32_t)G; d <<= 1) cadd += (unsigned long long)__shfl_xor((long long)cadd, d, G);
+    const unsigned long long cabs = I.cabs + cadd;
+    if (cabs > TWO53) return INC_BAIL;
+
+    // ---- level 3a: the hit registers' rows (lane = op) ----
+    hm_reg_result rr = {0u, 0u, -1, HM_NONE};
+    if (gl < nno && o_reg < D.n_old_r) rr = A.regs[D.src_r + o_reg];
+
+    // ---- causallyReady in arrival order; the transitiveDeps fold steps (A.1) ----
+    // target t lives in lane t % G, slot t / G: actor | (new source + 1) << 8 | change << 16, seq, log index
+    uint32_t tA0 = 0, tA1 = 0, tQ0 = 0, tQ1 = 0, tI0 = 0, tI1 = 0;
+    uint32_t jt0 = 0, jtn = 0;                                 // lane j: change j's fold steps
+    uint32_t ckr = ck, nt = 0;
+    for (uint32_t j = 0; j < nnc; j++) {
+        const uint32_t a = g.sh(ca, j), q = g.sh(cq, j), nd = g.sh(cnd, j), d0 = g.sh(xd, j);
+        if (g.sh(ckr, a) + 1u != q) return INC_BAIL;           // a duplicate, or not ready: the queue decides
+        const uint32_t t0 = nt;
+        bool own = false;
+        for (uint32_t t = 0; t <= nd; t++) {
+            uint32_t da, dq;
+            if (t < nd) {
+                da = g.sh(dpa, d0 + t); dq = g.sh(dpq, d0 + t);
+                if (da >= NA) return INC_BAIL;
+                if (da == a) { dq = q - 1; own = true; }       // deps ∪ {actor: seq - 1}: the key keeps its place
+            } else {
+                if (own) break;
+                da = a; dq = q - 1;
+            }
+            if (g.sh(ckr, da) < dq) return INC_BAIL;
+            if (dq == 0) continue;
+            const uint64_t m = g.bits(gl < j && ca == da && cq == dq);
+            const uint32_t src1 = m ? (uint32_t)__builtin_ctzll(m) + 1u : 0u;
+            if (nt >= 2u * G) return FAILG;
+            const uint32_t w = da | (src1 << 8) | (j << 16);
+            if (gl == (nt & (G - 1))) {
+                if (nt < (uint32_t)G) { tA0 = w; tQ0 = dq; } else { tA1 = w; tQ1 = dq; }
+            }
+            nt++;
+        }
+        if (gl == j) { jt0 = t0; jtn = nt - t0; }
+        if (gl == a) ckr = q;
+    }
+
+    // ---- fold sources in the old log: its applied row of (actor, seq), newest rows first ----
+    for (uint32_t t = 0; t < nt; t++) {
+        const uint32_t tl = t & (G - 1);
+        const uint32_t w = g.sh(t < (uint32_t)G ? tA0 : tA1, tl);
+        if ((w >> 8) & 0xFFu) continue;                        // a change of this submit
+        const uint32_t da = w & 0xFFu, dq = g.sh(t < (uint32_t)G ? tQ0 : tQ1, tl);
+        int found = -1;
+#pragma unroll
+        for (uint32_t k = 0; k < KT; k++) {
+            const uint64_t m = g.bits(tka[k] == da && tkq[k] == dq && tkh[k] >= 0);
+            if (m && found < 0) found = (int)D.n_old_c - 1 - (int)(k * G + (uint32_t)__builtin_ctzll(m));
+        }
+        for (int top = (int)D.n_old_c - 1 - (int)(KT * G); found < 0 && top >= 0; top -= G) {
+            const int idx = top - (int)gl;
+            bool hit = false;
+            if (idx >= 0) {
+                const uint2 kw = *reinterpret_cast<const uint2 *>(A.changes + D.dst_c + idx);
+                hit = (kw.x & 0xFFFFu) == da && kw.y == dq && A.hist[D.src_c + idx] >= 0;
+            }
+            const uint64_t m = g.bits(hit);
+            if (m) found = top - (int)__builtin_ctzll(m);
+        }
+        if (found < 0) return INC_BAIL;
+        if (gl == tl) { if (t < (uint32_t)G) tI0 = (uint32_t)found; else tI1 = (uint32_t)found; }
+    }
+
+    // ---- first-touch registers (lane = op): pushes, staging offsets, space ----
+    bool first = gl < nno;
+    uint32_t push = 0, oj = 0;
+    for (uint32_t k = 0; k < nno; k++) {
+        const uint32_t r = g.sh(o_reg, k), ak = g.sh(o_act, k);
+        if (k < gl && r == o_reg) first = false;
+        if (k >= gl && r == o_reg && (ak == HM_SET || ak == HM_LINK)) push++;
+    }
+    for (uint32_t j = 0; j < nnc; j++)
+        if (g.sh(xo + cno, j) <= gl) oj++;                    // the op's change: ops are grouped by change
+    const uint32_t n_old = first ? rr.n_surv : 0u;
+    const uint32_t n_up = first ? n_old + push : 0u;           // the list's length after the submit, at most
+    if (g.bits(first && n_up > (uint32_t)G)) return FAILG;
+    uint32_t s_incl = n_old, g_incl = n_up;
+#pragma unroll
+    for (uint32_t d = 1; d < (uint32_t)G; d <<= 1) {
+        const uint32_t y = g.up(s_incl, d), z = g.up(g_incl, d);
+        if (gl >= d) { s_incl += y; g_incl += z; }
+    }
+    const uint32_t stage_off = s_incl - n_old, tot_old = g.sh(s_incl, G - 1), grow = g.sh(g_incl, G - 1);
+    if (tot_old > 2u * G) return FAILG;
+    if ((unsigned long long)I.s_used + grow > D.o_cap) return INC_BAIL;   // no room: the re-merge repacks
+
+    // ---- level 3b: the fold sources' allDeps rows, TB at a time; allDeps / heads / clock of
+    //      each new change (applyChange) ----
+    uint32_t adn[NC];
+#pragma unroll
+    for (uint32_t x = 0; x < NC; x++) adn[x] = 0;
+    uint32_t hdr = hd, ckf = ck;
+    for (uint32_t j = 0; j < nnc; j++) {
+        const uint32_t t0 = g.sh(jt0, j), tn = g.sh(jtn, j), a = g.sh(ca, j), q = g.sh(cq, j);
+        uint32_t adv = 0;
+        for (uint32_t tb = t0; tb < t0 + tn; tb += TB) {
+            uint32_t row[TB], wv[TB], qv[TB];
+#pragma unroll
+            for (uint32_t u = 0; u < TB; u++) {
+                const uint32_t t = tb + u < 2u * G ? tb + u : 0u, tl = t & (G - 1);
+                wv[u] = g.sh(t < (uint32_t)G ? tA0 : tA1, tl);
+                qv[u] = g.sh(t < (uint32_t)G ? tQ0 : tQ1, tl);
+                const uint32_t ix = g.sh(t < (uint32_t)G ? tI0 : tI1, tl);
+                row[u] = 0;
+                if (tb + u < t0 + tn && !((wv[u] >> 8) & 0xFFu) && gl < S)
+                    row[u] = A.all_deps[(size_t)(D.src_c + ix) * S + gl];
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < TB; u++) {
+                if (tb + u >= t0 + tn) break;
+                const uint32_t src1 = (wv[u] >> 8) & 0xFFu;
+                const uint32_t r = src1 ? sel_nc(adn, src1 - 1) : row[u];
+                if (gl < NA && r > adv) adv = r;
+                if (gl == (wv[u] & 0xFFu)) adv = qv[u];         // then `a: s` (the literal fold)
+            }
+        }
+        if (gl >= NA) adv = 0;
+        set_nc(adn, j, adv);
+        if (hdr && hdr <= adv) hdr = 0;
+        if (gl == a) { hdr = q; ckf = q; }
+    }
+
+    // ---- level 4: the hit registers' survivors and their metadata, staged per group ----
+    {
+        // slot p of the staging area (two per lane) <- survivor src of the register that owns p
+        const uint32_t roff = first ? rr.surv_off : 0u, p0 = gl, p1 = gl + G;
+        uint32_t s0 = 0xFFFFFFFFu, s1 = 0xFFFFFFFFu;
+        for (uint32_t k = 0; k < nno; k++) {
+            const uint32_t b = g.sh(stage_off, k), c = g.sh(n_old, k), o = g.sh(roff, k);
+            if (p0 >= b && p0 < b + c) s0 = o + (p0 - b);
+            if (p1 >= b && p1 < b + c) s1 = o + (p1 - b);
+        }
+        uint4 x0 = {}, x1 = {};
+        uint2 m0 = {}, m1 = {};
+        const bool v0 = p0 < tot_old && s0 != 0xFFFFFFFFu, v1 = p1 < tot_old && s1 != 0xFFFFFFFFu;
+        if (v0) { x0 = *reinterpret_cast<const uint4 *>(A.surv + D.src_o + s0); m0 = A.smeta[D.src_o + s0]; }
+        if (v1) { x1 = *reinterpret_cast<const uint4 *>(A.surv + D.src_o + s1); m1 = A.smeta[D.src_o + s1]; }
+        if (v0) { ssv[p0] = x0; smt[p0] = m0; }
+        if (v1) { ssv[p1] = x1; smt[p1] = m1; }
+    }
+    // segments the append moved: the per-change / survivor / register rows follow (rare: a
+    // segment doubles)
+    const bool mv = D.src_c != D.dst_c || D.src_o != D.dst_o || D.src_r != D.dst_r;
+    if (D.src_c != D.dst_c) {
+        for (uint32_t i = gl; i < D.n_old_c; i += G) A.hist[D.dst_c + i] = A.hist[D.src_c + i];
+        for (size_t w = gl; w < (size_t)D.n_old_c * S; w += G) A.all_deps[(size_t)D.dst_c * S + w] = A.all_deps[(size_t)D.src_c * S + w];
+    }
+    if (D.src_o != D.dst_o)
+        for (uint32_t i = gl; i < I.s_used; i += G) {
+            const uint4 x = *reinterpret_cast<const uint4 *>(A.surv + D.src_o + i);
+            const uint2 xm = A.smeta[D.src_o + i];
+            *reinterpret_cast<uint4 *>(A.surv + D.dst_o + i) = x;
+            A.smeta[D.dst_o + i] = xm;
+        }
+    if (D.src_r != D.dst_r)
+        for (uint32_t i = gl; i < D.n_old_r; i += G) A.regs[D.dst_r + i] = A.regs[D.src_r + i];
+    if (mv) __threadfence_block();                            // the copies land before the writes below
+    __builtin_amdgcn_wave_barrier();
+
+    // ---- the new ops, register by register in first-touch order (applyAssign, A.2) ----
+    uint64_t fm = g.bits(first);
+    uint32_t acc = 0;
+    int32_t dsurv = 0;
+    while (fm) {
+        const uint32_t k0 = (uint32_t)__builtin_ctzll(fm);
+        fm &= fm - 1;
+        const uint32_t greg = g.sh(o_reg, k0), cnt0 = g.sh(n_old, k0), sb = g.sh(stage_off, k0);
+        const uint32_t off_old = g.sh(first ? rr.surv_off : 0u, k0), obj = g.sh(o_obj, k0);
+        uint4 x = {0u, 0u, 0u, 0u};
+        uint2 xm = {0u, 0u};
+        if (gl < cnt0) { x = ssv[sb + gl]; xm = smt[sb + gl]; }
+        uint32_t cnt = cnt0;
+        for (uint32_t k = k0; k < nno; k++) {
+            if (g.sh(o_reg, k) != greg) continue;
+            const uint32_t act = g.sh(o_act, k), vt = g.sh(o_vt, k), dtk = g.sh(o_dt, k);
+            const uint32_t vlo = g.sh(o_vlo, k), vhi = g.sh(o_vhi, k), j = g.sh(oj, k);
+            const uint32_t a = g.sh(ca, j), q = g.sh(cq, j);
+            // allDeps(new)[x.actor]: x is causally before the op iff that is >= x.seq
+            const uint32_t anc = g.sh(sel_nc(adn, j), xm.y & 0xFFu);
+            const bool live = gl < cnt;
+            if (act == HM_INC && live && (xm.y & 0x100u) && (x.y == HM_V_INT || x.y == HM_V_FLOAT) && anc >= xm.x) {
+                // every surviving counter set causally before the inc adds it: integer + integer
+                // exactly (cabs bounds the sums), anything else in f64 in application order
+                const uint64_t cur = ((uint64_t)x.w << 32) | x.z, inc = ((uint64_t)vhi << 32) | vlo;
+                if (x.y == HM_V_INT && vt == HM_V_INT) {
+                    const uint64_t s = (uint64_t)((int64_t)cur + (int64_t)inc);
+                    x.z = (uint32_t)s; x.w = (uint32_t)(s >> 32);
+                } else {
+                    double xv, iv;
+                    if (x.y == HM_V_INT) xv = (double)(int64_t)cur; else __builtin_memcpy(&xv, &cur, 8);
+                    if (vt == HM_V_INT) iv = (double)(int64_t)inc; else __builtin_memcpy(&iv, &inc, 8);
+                    const double r = xv + iv;
+                    uint64_t rb;
+                    __builtin_memcpy(&rb, &r, 8);
+                    x.z = (uint32_t)rb; x.w = (uint32_t)(rb >> 32); x.y = HM_V_FLOAT;
+                }
+            }
+            // the survivors concurrent with the op stay (an inc removes nothing)
+            const bool keep = live && (act == HM_INC || anc < xm.x);
+            const uint64_t km = g.bits(keep);
+            const uint32_t nk = (uint32_t)__popcll(km), pos = g.below(km);
+            const uint32_t dst = keep ? pos : nk + (gl - pos);  // a permutation of the group
+            x.x = g.to(x.x, dst); x.y = g.to(x.y, dst); x.z = g.to(x.z, dst); x.w = g.to(x.w, dst);
+            xm.x = g.to(xm.x, dst); xm.y = g.to(xm.y, dst);
+            const bool pushes = act == HM_SET || act == HM_LINK;
+            if (pushes && gl == nk) {
+                x = make_uint4(D.n_old_o + k, vt, vlo, vhi);
+                xm = make_uint2(q, a | ((act == HM_SET && dtk == HM_DT_COUNTER) ? 0x100u : 0u));
+            }
+            cnt = nk + (pushes ? 1u : 0u);
+            // sortBy(actor) (stable) then reverse
+            const uint32_t my = xm.y & 0xFFu;
+            uint32_t rank = 0;
+            for (uint32_t e = 0; e < cnt; e++) {
+                const uint32_t ae = g.sh(my, e);
+                rank += (ae < my || (ae == my && e < gl)) ? 1u : 0u;
+            }
+            const uint32_t d2 = gl < cnt ? cnt - 1 - rank : gl;
+            x.x = g.to(x.x, d2); x.y = g.to(x.y, d2); x.z = g.to(x.z, d2); x.w = g.to(x.w, d2);
+            xm.x = g.to(xm.x, d2); xm.y = g.to(xm.y, d2);
+        }
+        // a list that is no longer than before stays in its slots, a longer one moves to the end
+        const uint32_t off = cnt <= cnt0 ? off_old : I.s_used + acc;
+        if (cnt > cnt0) acc += cnt;
+        dsurv += (int32_t)cnt - (int32_t)cnt0;
+        if (gl < cnt) {
+            *reinterpret_cast<uint4 *>(A.surv + D.dst_o + off + gl) = x;
+            A.smeta[D.dst_o + off + gl] = xm;
+        }
+        if (gl == 0) {
+            hm_reg_result r;
+            r.n_surv = cnt; r.surv_off = off; r.list_index = -1; r.obj = obj;
+            A.regs[D.dst_r + greg] = r;
+        }
+    }
+    // registers new to the document and not hit (none for map ops; kept for the row contract)
+    for (uint32_t r0 = D.n_old_r; r0 < D.n_r; r0 += G) {
+        const uint32_t r = r0 + gl;
+        bool hit = false;
+        for (uint32_t k = 0; k < nno; k++) hit |= g.sh(o_reg, k) == r;
+        if (r < D.n_r && !hit) {
+            hm_reg_result z;
+            z.n_surv = 0; z.surv_off = 0; z.list_index = -1; z.obj = HM_NONE;
+            A.regs[D.dst_r + r] = z;
+        }
+    }
+
+    // ---- history, allDeps, clocks, the document's result row and IncState ----
+    if (gl < nnc) A.hist[D.dst_c + D.n_old_c + gl] = (int32_t)(R0.hist_len + gl);
+    if (gl < S) {
+#pragma unroll
+        for (uint32_t j = 0; j < NC; j++)
+            if (j < nnc) A.all_deps[(size_t)(D.dst_c + D.n_old_c + j) * S + gl] = adn[j];
+        A.clock[(size_t)h * S + gl] = ckf;
+        A.back_clock[(size_t)h * S + gl] = ckf;                // queue empty: every handed change applied
+        A.heads[(size_t)h * S + gl] = hdr;
+    }
+    const bool ag = g.bits(gl < S && ckf < mc) == 0, bg = g.bits(gl < S && mc < ckf) == 0;
+    if (gl == 0) {
+        hm_doc_result r = {};
+        r.status = HM_OK; r.err_change = HM_NONE; r.err_op = HM_NONE;
+        r.hist_len = R0.hist_len + nnc; r.n_queued = 0; r.n_surv = (uint32_t)((int32_t)R0.n_surv + dsurv);
+        r.min_cmp = (ag && bg) ? 0u : (ag ? 1u : (bg ? 2u : 3u));
+        A.res_docs[h] = r;
+        IncState s = I;
+        s.s_used = I.s_used + acc; s.cabs = cabs;
+        A.ist[h] = s;
+    }
+    return INC_DONE;
+}
+
+template <int G>
+__global__ __launch_bounds__(256) void inc_group_kernel(IncArgs A) {
+    constexpr uint32_t NG = 256 / G;
+    __shared__ uint4 s_sv[NG][2 * G];
+    __shared__ uint2 s_mt[NG][2 * G];
+    const uint32_t grp = threadIdx.x / G, gl = threadIdx.x & (G - 1);
+    const uint32_t n = A.list ? A.list[0] : A.n;
+    for (uint32_t q = blockIdx.x * NG + grp; q < n; q += gridDim.x * NG) {
+        const uint32_t di = A.list ? A.list[1 + q] : q;
+        const AppendDesc D = A.descs[di];
+        if (!D.inc) continue;
+        const int rc = inc_doc<G>(D, A, s_sv[grp], s_mt[grp]);
+        if (rc != INC_DONE && gl == 0) {
+            if (rc == INC_DEFER && A.defer) A.defer[1 + atomicAdd(&A.defer[0], 1u)] = di;
+            else A.bail[1 + atomicAdd(&A.bail[0], 1u)] = D.handle;
+        }
+    }
+}
+
+// After a re-merge (one wave per listed document): survivor metadata (the survivor's change by
+// a binary search over the change rows' first ops — ops are grouped by change in log order),
+// the objects created as maps / tables, the counter bound.  Documents that are not clean
+// (an error, queued changes) get flags = 0: their next submit re-merges.
+__global__ __launch_bounds__(256) void inc_meta_kernel(const uint32_t *list, uint32_t n, const DevDoc *dm,
+                                                       const hm_doc_result *res_docs, const hm_change_row *changes,
+                                                       const hm_op_row *ops, const hm_surv_result *surv, uint2 *smeta,
+                                                       IncState *ist) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6); q < n; q += gridDim.x * 4) {
+        const uint32_t h = list[q];
+        const DevDoc m = dm[h];
+        const hm_doc_result r = res_docs[h];
+        if (r.status != HM_OK || r.n_queued != 0 || r.n_surv > m.o_cap) {
+            if (lane == 0) { IncState z = {}; ist[h] = z; }
+            continue;
+        }
+        for (uint32_t i = lane; i < r.n_surv; i += 64) {
+            const uint32_t op = surv[m.o_off + i].op;
+            uint32_t lo = 0, hi = m.n_c;
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (changes[m.c_off + mid].op_first - m.o_off <= op) lo = mid; else hi = mid;
+            }
+            const uint2 kw = *reinterpret_cast<const uint2 *>(changes + m.c_off + lo);
+            const hm_op_row &o = ops[m.o_off + op];
+            const uint32_t cset = (o.action == HM_SET && o.datatype == HM_DT_COUNTER) ? 0x100u : 0u;
+            smeta[m.o_off + i] = make_uint2(kw.y, (kw.x & 0xFFu) | cset);
+        }
+        unsigned long long mask = 1ull, cabs = 0;
+        for (uint32_t i = lane; i < m.n_o; i += 64) {
+            const hm_op_row o = ops[m.o_off + i];
+            if ((o.action == HM_MAKE_MAP || o.action == HM_MAKE_TABLE) && o.obj < 64) mask |= 1ull << o.obj;
+            if (o.vtag == HM_V_INT && (o.action == HM_INC || (o.action == HM_SET && o.datatype == HM_DT_COUNTER))) {
+                const unsigned long long v = abs64((int64_t)o.value);
+                cabs = cabs + v < cabs || cabs + v > (1ull << 62) ? (1ull << 62) : cabs + v;
+            }
+        }
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            mask |= (unsigned long long)__shfl_xor((long long)mask, d);
+            const unsigned long long y = (unsigned long long)__shfl_xor((long long)cabs, d);
+            cabs = cabs + y > (1ull << 62) ? (1ull << 62) : cabs + y;
+        }
+        if (lane == 0) {
+            IncState s = {};
+            s.s_used = r.n_surv; s.flags = HM_IST_VALID; s.cabs = cabs; s.mapmask = mask;
+            ist[h] = s;
+        }
+    }
+}
+
+}  // namespace hmi
+
+hipError_t hm_launch_inc_apply(const IncArgs &A, hipStream_t s) {
+    if (!A.n) return hipSuccess;
+    const uint32_t S = A.S;
+    if (S > 64) return hipErrorInvalidValue;
+    hipError_t z = hipMemsetAsync(A.bail, 0, 4, s);
+    if (z == hipSuccess && A.defer) z = hipMemsetAsync(A.defer, 0, 4, s);
+    if (z != hipSuccess) return z;
+    auto grid = [](uint32_t n, uint32_t per) { const uint32_t g = (n + per - 1) / per; return g < 65535u ? g : 65535u; };
+    if (S <= 8) hipLaunchKernelGGL(hmi::inc_group_kernel<8>, dim3(grid(A.n, 32)), dim3(256), 0, s, A);
+    else if (S <= 16) hipLaunchKernelGGL(hmi::inc_group_kernel<16>, dim3(grid(A.n, 16)), dim3(256), 0, s, A);
+    if (S <= 16 && A.defer) {
+        // the documents handed over, one per wave (their count is read on the device)
+        IncArgs B = A;
+        B.list = A.defer;
+        B.defer = nullptr;
+        hipLaunchKernelGGL(hmi::inc_group_kernel<64>, dim3(grid(A.n, 4) < 1024u ? grid(A.n, 4) : 1024u), dim3(256), 0, s, B);
+    } else if (S > 16) {
+        IncArgs B = A;
+        B.defer = nullptr;
+        hipLaunchKernelGGL(hmi::inc_group_kernel<64>, dim3(grid(A.n, 4)), dim3(256), 0, s, B);
+    }
+    return hipGetLastError();
+}
+
+hipError_t hm_launch_inc_meta(const uint32_t *list, uint32_t n, const DevDoc *dm, const hm_doc_result *res_docs,
+                              const hm_change_row *changes, const hm_op_row *ops, const hm_surv_result *surv,
+                              uint2 *smeta, IncState *ist, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const uint32_t grid = (n + 3) / 4 < 65535u ? (n + 3) / 4 : 65535u;
+    hipLaunchKernelGGL(hmi::inc_meta_kernel, dim3(grid), dim3(256), 0, s, list, n, dm, res_docs, changes, ops, surv, smeta, ist);
+    return hipGetLastError();
+}

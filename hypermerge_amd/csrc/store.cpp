@@ -64,11 +64,12 @@ struct hm_store {
     size_t cap_c = 0, cap_d = 0, cap_o = 0, cap_r = 0;
     hm_change_row *changes = nullptr; int32_t *hist = nullptr; uint32_t *all_deps = nullptr;
     hm_dep_row *deps = nullptr;
-    hm_op_row *ops = nullptr; hm_surv_result *surv = nullptr;
+    hm_op_row *ops = nullptr; hm_surv_result *surv = nullptr; uint2 *smeta = nullptr;
     hm_reg_result *regs = nullptr;
     // per handle
     size_t cap_h = 0;
     DevDoc *dm = nullptr;                         // segments and totals
+    IncState *ist = nullptr;                      // survivor slots / metadata state of the incremental path
     uint32_t *seen = nullptr;                     // submit stamps (repeated-handle check)
     hm_doc_result *res_docs = nullptr;
     uint32_t *clock = nullptr, *back_clock = nullptr, *heads = nullptr, *min_clock = nullptr, *stored = nullptr;
@@ -86,10 +87,15 @@ struct hm_store {
     // in-flight batch
     std::atomic<bool> pending{false};             // a submitted batch not yet waited for (other threads may read it)
     uint64_t next_id = 1, pending_id = 0;
-    std::vector<uint32_t> p_handles;              // batch rows -> handles
-    uint32_t *p_handles_dev = nullptr;            // (staged)
+    uint32_t p_n = 0;                             // batch rows
+    uint32_t *p_handles_dev = nullptr;            // batch rows -> handles (staged, or the caller's device array)
     bool p_remap = false;
     uint8_t *p_gather_dev = nullptr;
+    uint32_t *p_fail_dev = nullptr;               // rows whose status is not OK (gather_kernel)
+    // the last waited batch, for hm_batch_undo (until the next submit)
+    uint64_t undo_id = 0;
+    uint32_t undo_n = 0;
+    DBuf<uint32_t> undo_handles;
     // incremental applyRemoteChanges (inc_apply_kernel) and the last submit's routing
     bool incremental = true;
     uint32_t st_inc = 0, st_cold = 0, st_bail = 0;
@@ -158,15 +164,19 @@ int ensure_handles(hm_store *s, size_t need) {
     const size_t cap = std::max<size_t>(need, std::max<size_t>(1024, s->cap_h * 2));
     hipStream_t st = hm_engine_stream(s->e);
     const uint32_t S = s->S;
-    hm_doc_result *rd; DevDoc *dm; uint32_t *seen; int r;
-    if ((r = dev_alloc(s, &rd, cap)) || (r = dev_alloc(s, &dm, cap)) || (r = dev_alloc(s, &seen, cap))) return r;
+    hm_doc_result *rd; DevDoc *dm; uint32_t *seen; IncState *ist; int r;
+    if ((r = dev_alloc(s, &rd, cap)) || (r = dev_alloc(s, &dm, cap)) || (r = dev_alloc(s, &seen, cap)) ||
+        (r = dev_alloc(s, &ist, cap)))
+        return r;
     SCHK(s, hipMemsetAsync(rd, 0, cap * sizeof(hm_doc_result), st));
     SCHK(s, hipMemsetAsync(dm, 0, cap * sizeof(DevDoc), st));
     SCHK(s, hipMemsetAsync(seen, 0, cap * 4, st));
+    SCHK(s, hipMemsetAsync(ist, 0, cap * sizeof(IncState), st));
     if (s->cap_h) {
         SCHK(s, hipMemcpyAsync(rd, s->res_docs, s->cap_h * sizeof(hm_doc_result), hipMemcpyDeviceToDevice, st));
         SCHK(s, hipMemcpyAsync(dm, s->dm, s->cap_h * sizeof(DevDoc), hipMemcpyDeviceToDevice, st));
         SCHK(s, hipMemcpyAsync(seen, s->seen, s->cap_h * 4, hipMemcpyDeviceToDevice, st));
+        SCHK(s, hipMemcpyAsync(ist, s->ist, s->cap_h * sizeof(IncState), hipMemcpyDeviceToDevice, st));
     }
     uint32_t **tabs[5] = {&s->clock, &s->back_clock, &s->heads, &s->min_clock, &s->stored};
     uint32_t *nt[5];
@@ -179,7 +189,8 @@ int ensure_handles(hm_store *s, size_t need) {
     if (s->res_docs) (void)hipFree(s->res_docs);
     if (s->dm) (void)hipFree(s->dm);
     if (s->seen) (void)hipFree(s->seen);
-    s->res_docs = rd; s->dm = dm; s->seen = seen;
+    if (s->ist) (void)hipFree(s->ist);
+    s->res_docs = rd; s->dm = dm; s->seen = seen; s->ist = ist;
     for (int i = 0; i < 5; i++) { if (*tabs[i]) (void)hipFree(*tabs[i]); *tabs[i] = nt[i]; }
     s->cap_h = cap;
     return HM_OK;
@@ -203,7 +214,7 @@ struct PhaseTimer {
 
 // Staged batch layout on the device: [changes][deps][ops][docs][handles][remap][gather][bail]
 struct StageLayout {
-    size_t o_ch, o_dp, o_op, o_docs, o_hand, o_remap, o_gather, o_bail, total;
+    size_t o_ch, o_dp, o_op, o_docs, o_hand, o_remap, o_gather, o_bail, o_defer, o_fail, total;
 };
 StageLayout layout(size_t nc, size_t nd, size_t no, size_t n, size_t nremap, uint32_t S) {
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -217,6 +228,8 @@ StageLayout layout(size_t nc, size_t nd, size_t no, size_t n, size_t nremap, uin
     L.o_remap = o; o += al(nremap + 1);
     L.o_gather = o; o += al(n * (sizeof(hm_doc_result) + 3 * 4 * (size_t)S) + 1);
     L.o_bail = o; o += al(4 * (n + 1));
+    L.o_defer = o; o += al(4 * (n + 1));
+    L.o_fail = o; o += 256;
     L.total = o;
     return L;
 }
@@ -250,6 +263,9 @@ int launch_list_merge(hm_store *s, const uint32_t *dev_list, uint32_t n) {
     o.hist = s->hist; o.all_deps = s->all_deps; o.regs = s->regs; o.surv = s->surv;
     const hm_extents ext = {(uint32_t)s->cap_c, (uint32_t)s->cap_d, (uint32_t)s->cap_o, (uint32_t)s->cap_r};
     rc = hm_engine_launch_merge(s->e, &b, &o, dev_list, &ext);
+    // the incremental path's survivor metadata of the re-merged documents (packed survivors)
+    if (rc == HM_OK && s->incremental)
+        SCHK(s, hm_launch_inc_meta(dev_list, n, s->dm, s->res_docs, s->changes, s->ops, s->surv, s->smeta, s->ist, st));
     SCHK(s, hipStreamSynchronize(st));
     return rc;
 }
@@ -273,10 +289,11 @@ int compact(hm_store *s, size_t extra_c, size_t extra_d, size_t extra_o, size_t 
     const size_t nc = std::max<size_t>(2 * live_c, 1 << 16), nd = std::max<size_t>(2 * live_d, 1 << 16);
     const size_t no = std::max<size_t>(2 * live_o, 1 << 16), nr = std::max<size_t>(2 * live_r, 1 << 16);
     hm_change_row *ch; int32_t *hi; uint32_t *ad; hm_dep_row *dp; hm_op_row *op; hm_surv_result *sv; hm_reg_result *rg;
+    uint2 *sm;
     int r;
     if ((r = dev_alloc(s, &ch, nc)) || (r = dev_alloc(s, &hi, nc)) || (r = dev_alloc(s, &ad, nc * S)) ||
         (r = dev_alloc(s, &dp, nd)) || (r = dev_alloc(s, &op, no)) || (r = dev_alloc(s, &sv, no)) ||
-        (r = dev_alloc(s, &rg, nr)))
+        (r = dev_alloc(s, &sm, no)) || (r = dev_alloc(s, &rg, nr)))
         return r;
     // relocate every document (old rows only; no new rows, no remap)
     std::vector<AppendDesc> descs(n);
@@ -312,8 +329,8 @@ int compact(hm_store *s, size_t extra_c, size_t extra_d, size_t extra_o, size_t 
         SCHK(s, hipStreamSynchronize(st));
     }
     (void)hipFree(s->changes); (void)hipFree(s->hist); (void)hipFree(s->all_deps); (void)hipFree(s->deps);
-    (void)hipFree(s->ops); (void)hipFree(s->surv); (void)hipFree(s->regs);
-    s->changes = ch; s->hist = hi; s->all_deps = ad; s->deps = dp; s->ops = op; s->surv = sv; s->regs = rg;
+    (void)hipFree(s->ops); (void)hipFree(s->surv); (void)hipFree(s->smeta); (void)hipFree(s->regs);
+    s->changes = ch; s->hist = hi; s->all_deps = ad; s->deps = dp; s->ops = op; s->surv = sv; s->smeta = sm; s->regs = rg;
     s->cap_c = nc; s->cap_d = nd; s->cap_o = no; s->cap_r = nr;
     const unsigned long long bump[4] = {uc, ud, uo, ur};
     SCHK(s, hipMemcpyAsync(s->st->bump, bump, sizeof bump, hipMemcpyHostToDevice, st));
@@ -348,9 +365,9 @@ int hm_store_create(hm_engine *e, const hm_store_config *cfg, hm_store **out) {
 void hm_store_destroy(hm_store *s) {
     if (!s) return;
     (void)hipStreamSynchronize(hm_engine_stream(s->e));
-    void *bufs[] = {s->changes, s->hist, s->all_deps, s->deps, s->ops, s->surv, s->regs, s->res_docs, s->clock,
+    void *bufs[] = {s->changes, s->hist, s->all_deps, s->deps, s->ops, s->surv, s->smeta, s->ist, s->regs, s->res_docs, s->clock,
                     s->back_clock, s->heads, s->min_clock, s->stored, s->stage.p, s->dm, s->seen, s->plan.p, s->descs.p,
-                    s->bdescs.p, s->list.p, s->blist.p, s->remap.p, s->inv.p, s->rows.p, s->st};
+                    s->bdescs.p, s->list.p, s->blist.p, s->remap.p, s->inv.p, s->rows.p, s->undo_handles.p, s->st};
     for (void *b : bufs) if (b) (void)hipFree(b);
     delete s;
 }
@@ -383,12 +400,15 @@ int hm_doc_open_n(hm_store *s, uint32_t n, uint32_t *out_first) {
     }
 }
 
-int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles, const uint8_t *actor_remap,
-                    uint64_t *out_batch_id) {
+// hm_batch_submit / hm_batch_submit_device: `dev` = the batch's tables, handles and remap are
+// device pointers (no host staging of the rows)
+static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handles, const uint8_t *actor_remap,
+                       uint64_t *out_batch_id, bool dev) {
     if (!s || !b || (b->n_docs && (!doc_handles || !b->docs))) return HM_ERR_INVALID;
     try {
         if (s->pending) return hm_engine_fail(s->e, HM_ERR_INVALID, "a batch is already in flight (call hm_batch_wait)");
         const uint32_t S = s->S, n = b->n_docs;
+        s->undo_id = 0;                                  // the plan rows hm_batch_undo reads are replaced
         if (b->a_stride != S) return hm_engine_fail(s->e, HM_ERR_INVALID, "batch a_stride must equal the store's");
         SCHK(s, hipSetDevice(hm_engine_device(s->e)));
         hipStream_t st = hm_engine_stream(s->e);
@@ -396,25 +416,36 @@ int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
         int rc;
         // stage the batch (its tables, rows, handles and remap) on the device
         const size_t nremap = actor_remap ? (size_t)n * S : 0;
-        const StageLayout L = layout(b->n_changes, b->n_deps, b->n_ops, n, nremap, S);
+        const StageLayout L = dev ? layout(0, 0, 0, n, 0, S) : layout(b->n_changes, b->n_deps, b->n_ops, n, nremap, S);
         if ((rc = ensure_stage(s, L.total)) || (rc = ensure_buf(s, s->plan, n)) || (rc = ensure_buf(s, s->descs, n)) ||
             (rc = ensure_buf(s, s->list, n)))
             return rc;
         uint8_t *sp = s->stage.p;
-        if (b->n_changes) SCHK(s, hipMemcpyAsync(sp + L.o_ch, b->changes, b->n_changes * sizeof(hm_change_row), hipMemcpyHostToDevice, st));
-        if (b->n_deps) SCHK(s, hipMemcpyAsync(sp + L.o_dp, b->deps, b->n_deps * sizeof(hm_dep_row), hipMemcpyHostToDevice, st));
-        if (b->n_ops) SCHK(s, hipMemcpyAsync(sp + L.o_op, b->ops, b->n_ops * sizeof(hm_op_row), hipMemcpyHostToDevice, st));
-        if (n) {
-            SCHK(s, hipMemcpyAsync(sp + L.o_docs, b->docs, (size_t)n * sizeof(hm_doc_row), hipMemcpyHostToDevice, st));
-            SCHK(s, hipMemcpyAsync(sp + L.o_hand, doc_handles, (size_t)n * 4, hipMemcpyHostToDevice, st));
+        const hm_doc_row *t_docs = b->docs;
+        const hm_change_row *t_ch = b->changes;
+        const hm_dep_row *t_dp = b->deps;
+        const hm_op_row *t_op = b->ops;
+        const uint32_t *t_hand = doc_handles;
+        const uint8_t *t_remap = actor_remap;
+        if (!dev) {
+            if (b->n_changes) SCHK(s, hipMemcpyAsync(sp + L.o_ch, b->changes, b->n_changes * sizeof(hm_change_row), hipMemcpyHostToDevice, st));
+            if (b->n_deps) SCHK(s, hipMemcpyAsync(sp + L.o_dp, b->deps, b->n_deps * sizeof(hm_dep_row), hipMemcpyHostToDevice, st));
+            if (b->n_ops) SCHK(s, hipMemcpyAsync(sp + L.o_op, b->ops, b->n_ops * sizeof(hm_op_row), hipMemcpyHostToDevice, st));
+            if (n) {
+                SCHK(s, hipMemcpyAsync(sp + L.o_docs, b->docs, (size_t)n * sizeof(hm_doc_row), hipMemcpyHostToDevice, st));
+                SCHK(s, hipMemcpyAsync(sp + L.o_hand, doc_handles, (size_t)n * 4, hipMemcpyHostToDevice, st));
+            }
+            if (nremap) SCHK(s, hipMemcpyAsync(sp + L.o_remap, actor_remap, nremap, hipMemcpyHostToDevice, st));
+            t_docs = (const hm_doc_row *)(sp + L.o_docs); t_ch = (const hm_change_row *)(sp + L.o_ch);
+            t_dp = (const hm_dep_row *)(sp + L.o_dp); t_op = (const hm_op_row *)(sp + L.o_op);
+            t_hand = (const uint32_t *)(sp + L.o_hand); t_remap = nremap ? sp + L.o_remap : nullptr;
         }
-        if (nremap) SCHK(s, hipMemcpyAsync(sp + L.o_remap, actor_remap, nremap, hipMemcpyHostToDevice, st));
         T.mark("stage: h2d");
         PlanArgs A;
-        A.docs = (const hm_doc_row *)(sp + L.o_docs); A.changes = (const hm_change_row *)(sp + L.o_ch);
-        A.handles = (const uint32_t *)(sp + L.o_hand); A.remap = nremap ? sp + L.o_remap : nullptr;
+        A.docs = t_docs; A.changes = t_ch;
+        A.handles = t_hand; A.remap = nremap ? t_remap : nullptr;
         A.n = n; A.n_changes = b->n_changes; A.n_deps = b->n_deps; A.n_ops = b->n_ops; A.n_handles = s->n_handles;
-        A.S = S; A.stamp = ++s->stamp ? s->stamp : ++s->stamp; A.incremental = s->incremental ? 1u : 0u;
+        A.S = S; A.stamp = ++s->stamp ? s->stamp : ++s->stamp; A.incremental = s->incremental && S <= 64 ? 1u : 0u;
         A.dm = s->dm; A.res_docs = s->res_docs; A.seen = s->seen; A.plan = s->plan.p; A.descs = s->descs.p;
         A.list = s->list.p; A.st = s->st;
         // plan: checks, growth, routes (nothing in the store changes)
@@ -448,16 +479,18 @@ int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
         // segments, descriptors, totals, re-merge list; append; incremental apply
         SCHK(s, hm_launch_alloc(A, st));
         StoreArenas ar = {s->changes, s->deps, s->ops, s->min_clock, s->stored};
-        SCHK(s, hm_launch_append(s->descs.p, n, ar, ar, A.changes, (const hm_dep_row *)(sp + L.o_dp),
-                                 (const hm_op_row *)(sp + L.o_op), A.remap, S, st));
+        SCHK(s, hm_launch_append(s->descs.p, n, ar, ar, A.changes, t_dp, t_op, A.remap, S, st));
         T.mark("alloc+append");
         uint32_t *bail = (uint32_t *)(sp + L.o_bail);
         SCHK(s, hipMemsetAsync(bail, 0, 4, st));
         if (P.n_inc) {
-            const IncDims M = hm_inc_dims(S, P.mx[0], P.mx[1], P.mx[2], P.mx[3], P.mx[4], P.mx[5]);
-            IncArenas IA = {s->changes, s->deps, s->ops, s->hist, s->all_deps, s->regs, s->surv,
-                            s->res_docs, s->clock, s->back_clock, s->heads, s->min_clock};
-            SCHK(s, hm_launch_inc_apply(s->descs.p, n, IA, M, bail, st));
+            IncArgs IA;
+            IA.descs = s->descs.p; IA.n = n; IA.list = nullptr; IA.S = S;
+            IA.changes = s->changes; IA.deps = s->deps; IA.ops = s->ops; IA.hist = s->hist; IA.all_deps = s->all_deps;
+            IA.regs = s->regs; IA.surv = s->surv; IA.smeta = s->smeta; IA.res_docs = s->res_docs;
+            IA.clock = s->clock; IA.back_clock = s->back_clock; IA.heads = s->heads; IA.min_clock = s->min_clock;
+            IA.ist = s->ist; IA.bail = bail; IA.defer = (uint32_t *)(sp + L.o_defer);
+            SCHK(s, hm_launch_inc_apply(IA, st));
         }
         T.mark("incremental");
         // the re-merge list: cold documents, then those the incremental kernel handed back
@@ -469,15 +502,18 @@ int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
         if ((rc = launch_list_merge(s, s->list.p, counts[0] + counts[1]))) return rc;
         T.mark("remerge");
         s->st_inc = P.n_inc - counts[1]; s->st_cold = counts[0]; s->st_bail = counts[1];
-        SCHK(s, hm_launch_gather(A.handles, n, S, s->res_docs, s->clock, s->back_clock, s->heads, sp + L.o_gather, st));
+        uint32_t *fail = (uint32_t *)(sp + L.o_fail);
+        SCHK(s, hipMemsetAsync(fail, 0, 4, st));
+        SCHK(s, hm_launch_gather(A.handles, n, S, s->res_docs, s->clock, s->back_clock, s->heads, sp + L.o_gather, fail, st));
         s->p_gather_dev = sp + L.o_gather;
-        s->p_handles_dev = (uint32_t *)(sp + L.o_hand);
-        s->p_handles.assign(doc_handles, doc_handles + n);
+        s->p_fail_dev = fail;
+        s->p_handles_dev = const_cast<uint32_t *>(A.handles);
+        s->p_n = n;
         s->p_remap = nremap != 0;
         if (nremap) {
             // the rollback needs the remap rows after the staging area is reused
             if ((rc = ensure_buf(s, s->remap, nremap))) return rc;
-            SCHK(s, hipMemcpyAsync(s->remap.p, sp + L.o_remap, nremap, hipMemcpyDeviceToDevice, st));
+            SCHK(s, hipMemcpyAsync(s->remap.p, A.remap, nremap, hipMemcpyDeviceToDevice, st));
         }
         T.mark("gather");
         s->pending = true;
@@ -489,8 +525,41 @@ int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
     }
 }
 
-int hm_batch_wait(hm_store *s, uint64_t batch_id, hm_doc_result *out_docs, uint32_t *out_clock,
-                  uint32_t *out_back_clock, uint32_t *out_heads) {
+int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles, const uint8_t *actor_remap,
+                    uint64_t *out_batch_id) {
+    return submit_impl(s, b, doc_handles, actor_remap, out_batch_id, false);
+}
+
+int hm_batch_submit_device(hm_store *s, const hm_batch *b, const uint32_t *doc_handles, const uint8_t *actor_remap,
+                           uint64_t *out_batch_id) {
+    return submit_impl(s, b, doc_handles, actor_remap, out_batch_id, true);
+}
+
+// Roll documents of the last submit back to their logs before it (every = false: those whose merge
+// failed; true: all of them not rolled back yet): totals restored, ranks re-mapped back, the log
+// truncated, the previous state re-merged.
+static int roll_back(hm_store *s, const uint32_t *handles_dev, uint32_t n, bool every) {
+    hipStream_t st = hm_engine_stream(s->e);
+    const uint32_t S = s->S;
+    int rc;
+    if ((rc = ensure_buf(s, s->bdescs, n)) || (rc = ensure_buf(s, s->blist, n)) ||
+        (s->p_remap && (rc = ensure_buf(s, s->inv, (size_t)n * S))))
+        return rc;
+    if ((rc = reset_stats(s))) return rc;
+    SCHK(s, hm_launch_rollback(handles_dev, n, s->res_docs, s->plan.p, s->p_remap ? s->remap.p : nullptr, S, s->dm,
+                               s->bdescs.p, s->p_remap ? s->inv.p : nullptr, s->blist.p, s->st, every ? 1u : 0u, st));
+    uint32_t nb = 0;
+    SCHK(s, hipMemcpyAsync(&nb, &s->st->n_back, 4, hipMemcpyDeviceToHost, st));
+    SCHK(s, hipStreamSynchronize(st));
+    StoreArenas ar = {s->changes, s->deps, s->ops, s->min_clock, s->stored};
+    SCHK(s, hm_launch_append(s->bdescs.p, nb, ar, ar, nullptr, nullptr, nullptr, s->p_remap ? s->inv.p : nullptr, S, st));
+    return launch_list_merge(s, s->blist.p, nb);
+}
+
+// hm_batch_wait / hm_batch_wait_device: the gathered rows to the host arrays, or (out_dev) as one
+// device-to-device copy with only the failure count read back
+static int wait_impl(hm_store *s, uint64_t batch_id, hm_doc_result *out_docs, uint32_t *out_clock,
+                     uint32_t *out_back_clock, uint32_t *out_heads, void *out_dev, uint32_t *out_n_failed) {
     if (!s) return HM_ERR_INVALID;
     try {
         if (!s->pending || batch_id != s->pending_id) return hm_engine_fail(s->e, HM_ERR_INVALID, "no such batch in flight");
@@ -500,12 +569,18 @@ int hm_batch_wait(hm_store *s, uint64_t batch_id, hm_doc_result *out_docs, uint3
         // the batch stays in flight (pending) until this returns: copy-out and rollback below
         // still read and re-merge the store's documents
         struct Clear { std::atomic<bool> &p; ~Clear() { p.store(false); } } clear_pending{s->pending};
-        const uint32_t n = (uint32_t)s->p_handles.size(), S = s->S;
+        const uint32_t n = s->p_n, S = s->S;
         // results straight from the gathered device rows into the caller's arrays
         std::vector<hm_doc_result> tmp;
         hm_doc_result *res = out_docs;
-        if (!res) { tmp.resize(n); res = tmp.data(); }
-        if (n) {
+        if (!res && !out_dev) { tmp.resize(n); res = tmp.data(); }
+        uint32_t n_fail = 0;
+        if (n && out_dev) {
+            const size_t bytes = (size_t)n * (sizeof(hm_doc_result) + 3 * 4 * (size_t)S);
+            SCHK(s, hipMemcpyAsync(out_dev, s->p_gather_dev, bytes, hipMemcpyDeviceToDevice, st));
+            SCHK(s, hipMemcpyAsync(&n_fail, s->p_fail_dev, 4, hipMemcpyDeviceToHost, st));
+            SCHK(s, hipStreamSynchronize(st));
+        } else if (n) {
             const uint8_t *g = s->p_gather_dev;
             const size_t rb = (size_t)n * S * 4;
             SCHK(s, hipMemcpyAsync(res, g, (size_t)n * sizeof(hm_doc_result), hipMemcpyDeviceToHost, st));
@@ -519,33 +594,63 @@ int hm_batch_wait(hm_store *s, uint64_t batch_id, hm_doc_result *out_docs, uint3
         // roll back documents whose merge threw (or left the envelope): the log returns to its
         // previous length (rows stay where they are), ranks are re-ranked back, and the previous
         // state is re-merged
-        bool any = false;
-        for (uint32_t i = 0; i < n && !any; i++) any = res[i].status != HM_OK;
+        bool any = n_fail != 0;
+        for (uint32_t i = 0; res && i < n && !any; i++) any = res[i].status != HM_OK;
+        if (out_n_failed) {
+            uint32_t k = n_fail;
+            if (!out_dev) for (uint32_t i = 0; i < n; i++) k += res[i].status != HM_OK;
+            *out_n_failed = k;
+        }
         if (any) {
-            int rc;
-            if ((rc = ensure_buf(s, s->bdescs, n)) || (rc = ensure_buf(s, s->blist, n)) ||
-                (s->p_remap && (rc = ensure_buf(s, s->inv, (size_t)n * S))))
-                return rc;
-            if ((rc = reset_stats(s))) return rc;
-            SCHK(s, hm_launch_rollback(s->p_handles_dev, n, s->res_docs, s->plan.p, s->p_remap ? s->remap.p : nullptr, S, s->dm,
-                                       s->bdescs.p, s->p_remap ? s->inv.p : nullptr, s->blist.p, s->st, st));
-            uint32_t nb = 0;
-            SCHK(s, hipMemcpyAsync(&nb, &s->st->n_back, 4, hipMemcpyDeviceToHost, st));
-            SCHK(s, hipStreamSynchronize(st));
-            StoreArenas ar = {s->changes, s->deps, s->ops, s->min_clock, s->stored};
-            SCHK(s, hm_launch_append(s->bdescs.p, nb, ar, ar, nullptr, nullptr, nullptr, s->p_remap ? s->inv.p : nullptr, S, st));
-            if ((rc = launch_list_merge(s, s->blist.p, nb))) return rc;
+            const int rc = roll_back(s, s->p_handles_dev, n, false);
+            if (rc) return rc;
             T.mark("rollback");
         }
+        // hm_batch_undo keeps the batch's handles (the staging area is reused by other calls)
+        if (n) {
+            int rc = ensure_buf(s, s->undo_handles, n);
+            if (rc) return rc;
+            SCHK(s, hipMemcpyAsync(s->undo_handles.p, s->p_handles_dev, (size_t)n * 4, hipMemcpyDeviceToDevice, st));
+        }
+        s->undo_id = batch_id;
+        s->undo_n = n;
         return HM_OK;
     } catch (...) {
         return hm_engine_fail(s->e, HM_ERR_NOMEM, "exception in hm_batch_wait");
     }
 }
 
+int hm_batch_wait(hm_store *s, uint64_t batch_id, hm_doc_result *out_docs, uint32_t *out_clock,
+                  uint32_t *out_back_clock, uint32_t *out_heads) {
+    return wait_impl(s, batch_id, out_docs, out_clock, out_back_clock, out_heads, nullptr, nullptr);
+}
+
+int hm_batch_wait_device(hm_store *s, uint64_t batch_id, void *out_dev, uint32_t *out_n_failed) {
+    if (!out_dev) return HM_ERR_INVALID;
+    return wait_impl(s, batch_id, nullptr, nullptr, nullptr, nullptr, out_dev, out_n_failed);
+}
+
+int hm_batch_undo(hm_store *s, uint64_t batch_id) {
+    if (!s) return HM_ERR_INVALID;
+    try {
+        if (s->pending || !batch_id || batch_id != s->undo_id)
+            return hm_engine_fail(s->e, HM_ERR_INVALID, "hm_batch_undo: not the last waited batch (or a submit since)");
+        SCHK(s, hipSetDevice(hm_engine_device(s->e)));
+        const int rc = roll_back(s, s->undo_handles.p, s->undo_n, true);
+        s->undo_id = 0;
+        return rc;
+    } catch (...) {
+        return hm_engine_fail(s->e, HM_ERR_NOMEM, "exception in hm_batch_undo");
+    }
+}
+
 int hm_store_set_incremental(hm_store *s, int on) {
     if (!s) return HM_ERR_INVALID;
     if (s->pending) return hm_engine_fail(s->e, HM_ERR_INVALID, "batch in flight");
+    // re-merges while the path was off kept no survivor metadata: every document's next submit
+    // re-merges (and rebuilds it)
+    if (on && !s->incremental && s->cap_h)
+        SCHK(s, hipMemsetAsync(s->ist, 0, s->cap_h * sizeof(IncState), hm_engine_stream(s->e)));
     s->incremental = on != 0;
     return HM_OK;
 }
@@ -580,8 +685,24 @@ int hm_doc_read(hm_store *s, uint32_t doc, int32_t *hist, uint32_t *all_deps, hm
     const uint32_t S = s->S;
     if (hist && m.n_c) SCHK(s, hipMemcpy(hist, s->hist + m.c_off, m.n_c * 4, hipMemcpyDeviceToHost));
     if (all_deps && m.n_c) SCHK(s, hipMemcpy(all_deps, s->all_deps + (size_t)m.c_off * S, (size_t)m.n_c * S * 4, hipMemcpyDeviceToHost));
-    if (regs && m.n_r) SCHK(s, hipMemcpy(regs, s->regs + m.r_off, m.n_r * sizeof(hm_reg_result), hipMemcpyDeviceToHost));
-    if (surv && m.n_o) SCHK(s, hipMemcpy(surv, s->surv + m.o_off, m.n_o * sizeof(hm_surv_result), hipMemcpyDeviceToHost));
+    if ((regs || surv) && m.n_r) {
+        // survivor lists may sit anywhere in the op segment's slots (the incremental path moves a
+        // list that grows to the end): handed out packed in register order, as a merge writes them
+        std::vector<hm_reg_result> rg(m.n_r);
+        std::vector<hm_surv_result> sv(m.o_cap ? m.o_cap : 1);
+        SCHK(s, hipMemcpy(rg.data(), s->regs + m.r_off, m.n_r * sizeof(hm_reg_result), hipMemcpyDeviceToHost));
+        if (m.o_cap) SCHK(s, hipMemcpy(sv.data(), s->surv + m.o_off, m.o_cap * sizeof(hm_surv_result), hipMemcpyDeviceToHost));
+        uint32_t off = 0;
+        for (uint32_t g = 0; g < m.n_r; g++) {
+            hm_reg_result &r = rg[g];
+            if ((uint64_t)r.surv_off + r.n_surv > m.o_cap || (uint64_t)off + r.n_surv > m.n_o)
+                return hm_engine_fail(s->e, HM_ERR_DEVICE, "register survivors outside the document's slots");
+            if (surv) for (uint32_t i = 0; i < r.n_surv; i++) surv[off + i] = sv[r.surv_off + i];
+            r.surv_off = off;
+            off += r.n_surv;
+        }
+        if (regs) memcpy(regs, rg.data(), m.n_r * sizeof(hm_reg_result));
+    }
     if (clock) SCHK(s, hipMemcpy(clock, s->clock + (size_t)doc * S, S * 4, hipMemcpyDeviceToHost));
     if (back_clock) SCHK(s, hipMemcpy(back_clock, s->back_clock + (size_t)doc * S, S * 4, hipMemcpyDeviceToHost));
     if (heads) SCHK(s, hipMemcpy(heads, s->heads + (size_t)doc * S, S * 4, hipMemcpyDeviceToHost));

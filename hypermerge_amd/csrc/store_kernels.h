@@ -17,6 +17,7 @@ struct AppendDesc {
     uint32_t src_r, dst_r, n_old_r, n_r;
     uint16_t n_actors, inc;
     uint32_t n_objs;
+    uint32_t o_cap;       // the op segment's capacity after the append (survivor slots, incremental path)
 };
 
 // A document's log segments and totals, resident on the device (the store plans submits there:
@@ -63,7 +64,27 @@ struct StoreArenas {
     uint32_t *stored_clock;   // per handle, rank-indexed
 };
 
-struct IncArenas {
+// Per handle, beside the log: what the incremental path needs to touch only the registers the
+// new ops hit (32 B).  Survivor lists of a document live in its op segment's survivor slots
+// [0, s_used): a list that shrinks or keeps its length is rewritten in place, a list that grows
+// moves to the end (s_used grows); the re-merge repacks.  smeta[slot] = (seq, actor | cset << 8)
+// of the survivor's change (cset: a counter set), so isConcurrent and sortBy(actor) need no log
+// search.  cabs bounds every integer counter's |base| + sum|inc| (the exact-integer rule of
+// the re-merge: an integer counter is exact while that sum is <= 2^53), mapmask marks objects
+// created as maps / tables (bit 0 = ROOT).  flags = 0: not built (the next submit re-merges).
+struct IncState {
+    uint32_t s_used, flags;
+    unsigned long long cabs, mapmask;
+    uint32_t pad[2];
+};
+static_assert(sizeof(IncState) == 32, "IncState is 32 B");
+#define HM_IST_VALID 1u
+
+struct IncArgs {
+    const AppendDesc *descs;
+    uint32_t n;                                // batch rows (descs)
+    const uint32_t *list;                      // NULL: every desc; else list[0] = count, list[1..] desc indices
+    uint32_t S;
     const hm_change_row *changes;
     const hm_dep_row *deps;
     const hm_op_row *ops;
@@ -71,28 +92,19 @@ struct IncArenas {
     uint32_t *all_deps;
     hm_reg_result *regs;
     hm_surv_result *surv;
+    uint2 *smeta;
     hm_doc_result *res_docs;
     uint32_t *clock, *back_clock, *heads;
     const uint32_t *min_clock;
+    IncState *ist;
+    uint32_t *bail;                            // [0] count, [1..] handles re-merged
+    uint32_t *defer;                           // [0] count, [1..] desc indices for the wave kernel (NULL: bail)
 };
 
 // envelope of the incremental path (larger submits take the full re-merge)
 #define HM_INC_MAX_NEW_C 8
 #define HM_INC_MAX_NEW_O 64
-#define HM_INC_MAX_TGT 64        // allDeps fold steps of a submit's new changes
-#define HM_INC_MAX_REGS 256
-#define HM_INC_MAX_SURV 256
-#define HM_INC_MAX_STAGE 512     // old change rows staged in LDS (longer logs are searched in HBM)
-#define HM_INC_SLOTS 8
-#define HM_INC_SLOT_CAP 32
-
-// per-launch LDS tiles, sized to the launch's largest document (dynamic LDS)
-struct IncDims {
-    uint32_t S, new_c, tgt, stage, regs, surv, slots;
-    uint32_t o_nc, o_dep, o_tkey, o_tsrc, o_tad, o_adn, o_skey, o_sof, o_reg, o_sold, o_wl, o_wls, o_wla, o_scnt, bytes;
-};
-IncDims hm_inc_dims(uint32_t S, uint32_t new_c, uint32_t tgt, uint32_t stage, uint32_t regs, uint32_t surv,
-                    uint32_t slots);
+#define HM_INC_MAX_TGT 128       // transitiveDeps fold steps of a submit's new changes (2 per lane, wave kernel)
 
 struct PlanArgs {
     const hm_doc_row *docs;
@@ -113,10 +125,11 @@ hipError_t hm_launch_alloc(const PlanArgs &a, hipStream_t s);
 // hm_doc_row of each listed handle from its device meta (+ the launch hints in st)
 hipError_t hm_launch_doc_rows(const uint32_t *list, uint32_t n, const DevDoc *dm, hm_doc_row *rows, PlanStats *st,
                               hipStream_t s);
-// documents of a batch whose merge failed: totals restored, rows re-ranked back, listed for re-merge
-hipError_t hm_launch_rollback(const uint32_t *handles, uint32_t n, const hm_doc_result *res_docs, const PlanRow *plan,
+// documents of a batch whose merge failed (every = all of the batch's documents): totals restored,
+// rows re-ranked back, listed for re-merge
+hipError_t hm_launch_rollback(const uint32_t *handles, uint32_t n, const hm_doc_result *res_docs, PlanRow *plan,
                               const uint8_t *remap, uint32_t S, DevDoc *dm, AppendDesc *descs, uint8_t *inv,
-                              uint32_t *list, PlanStats *st, hipStream_t s);
+                              uint32_t *list, PlanStats *st, uint32_t every, hipStream_t s);
 hipError_t hm_launch_init_docs(DevDoc *dm, uint32_t h0, uint32_t n, hipStream_t s);
 // chosen registers of resident documents by (handle, register): validated on the device
 hipError_t hm_launch_read_hist(uint32_t n, const uint32_t *handles, const uint32_t *from, const uint32_t *to,
@@ -128,8 +141,13 @@ hipError_t hm_launch_read_regs_h(uint32_t n, const uint32_t *handles, const uint
                                  hm_reg_result *out_regs, hm_surv_result *out_surv, uint32_t cap, uint32_t *counter,
                                  uint32_t *bad, hipStream_t s);
 
-hipError_t hm_launch_inc_apply(const AppendDesc *descs, uint32_t n, const IncArenas &A, const IncDims &M,
-                               uint32_t *bail, hipStream_t s);
+// incremental applyRemoteChanges: a group of G = (S <= 8 ? 8 : S <= 16 ? 16 : 64) lanes per document,
+// then the documents it handed over (defer list) one per wave; the rest listed in bail
+hipError_t hm_launch_inc_apply(const IncArgs &A, hipStream_t s);
+// survivor metadata / IncState of re-merged documents (so the next submit can go incremental)
+hipError_t hm_launch_inc_meta(const uint32_t *list, uint32_t n, const DevDoc *dm, const hm_doc_result *res_docs,
+                              const hm_change_row *changes, const hm_op_row *ops, const hm_surv_result *surv,
+                              uint2 *smeta, IncState *ist, hipStream_t s);
 hipError_t hm_launch_append(const AppendDesc *descs, uint32_t n_desc, const StoreArenas &src, const StoreArenas &dst,
                             const hm_change_row *st_changes, const hm_dep_row *st_deps, const hm_op_row *st_ops,
                             const uint8_t *remap, uint32_t S, hipStream_t s);
@@ -138,7 +156,7 @@ hipError_t hm_launch_read_regs(uint32_t n, const uint32_t *abs_reg, const uint32
                                uint32_t *counter, hipStream_t s);
 hipError_t hm_launch_gather(const uint32_t *handles, uint32_t n, uint32_t S, const hm_doc_result *res_docs,
                             const uint32_t *clock, const uint32_t *back_clock, const uint32_t *heads, uint8_t *out,
-                            hipStream_t s);
+                            uint32_t *n_fail, hipStream_t s);
 hipError_t hm_launch_clock_update(const uint32_t *docs, uint32_t n, uint32_t S, const uint32_t *back_clock,
                                   uint32_t *stored, uint8_t *written, uint8_t *differs, uint32_t *out_stored,
                                   hipStream_t s);

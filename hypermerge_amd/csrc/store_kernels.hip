@@ -6,8 +6,7 @@
 //                       the rank-indexed per-document rows (minimumClock, stored clock),
 //                       and appends the new change/dep/op rows with their offsets rebased
 //                       from batch-local to arena positions.
-//  inc_apply_kernel     incremental applyRemoteChanges: new changes applied on the resident
-//                       state of documents whose submit is causally ready (see below).
+//  (inc_kernels.hip)    incremental applyRemoteChanges on the resident state.
 //  gather_kernel        per-document result rows of a batch (by handle) into one
 //                       contiguous buffer, so hm_batch_wait is a single D2H copy.
 //  clock_update_kernel  ClockStore.update (src/ClockStore.ts:78-91) over many documents:
@@ -97,19 +96,29 @@ __global__ __launch_bounds__(SWG) void append_kernel(const AppendDesc *descs, ui
     }
 }
 
-// out = [n x hm_doc_result][n x S clock][n x S back_clock][n x S heads]
+// out = [n x hm_doc_result][n x S clock][n x S back_clock][n x S heads], one 4-byte word per lane
+// (consecutive lanes write consecutive words); n_fail (optional) counts rows whose status is not OK
 __global__ void gather_kernel(const uint32_t *handles, uint32_t n, uint32_t S, const hm_doc_result *res_docs,
                               const uint32_t *clock, const uint32_t *back_clock, const uint32_t *heads,
-                              uint8_t *out) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t h = handles[i];
-    reinterpret_cast<hm_doc_result *>(out)[i] = res_docs[h];
-    uint32_t *oc = reinterpret_cast<uint32_t *>(out + (size_t)n * sizeof(hm_doc_result));
-    for (uint32_t a = 0; a < S; a++) {
-        oc[(size_t)i * S + a] = clock[(size_t)h * S + a];
-        oc[(size_t)n * S + (size_t)i * S + a] = back_clock[(size_t)h * S + a];
-        oc[(size_t)2 * n * S + (size_t)i * S + a] = heads[(size_t)h * S + a];
+                              uint8_t *out, uint32_t *n_fail) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t nr = (size_t)n * 8, ns = (size_t)n * S;
+    uint32_t *o = reinterpret_cast<uint32_t *>(out);
+    bool fail = false;
+    if (t < nr) {
+        const uint32_t i = (uint32_t)(t >> 3), w = (uint32_t)(t & 7);
+        const uint32_t v = reinterpret_cast<const uint32_t *>(res_docs + handles[i])[w];
+        o[t] = v;
+        fail = w == 0 && v != (uint32_t)HM_OK;
+    } else if (t < nr + 3 * ns) {
+        const size_t u = t - nr, k = u / ns, e = u - k * ns;
+        const uint32_t i = (uint32_t)(e / S), a = (uint32_t)(e - (size_t)i * S);
+        const uint32_t *src = k == 0 ? clock : (k == 1 ? back_clock : heads);
+        o[t] = src[(size_t)handles[i] * S + a];
+    }
+    if (n_fail) {
+        const unsigned long long b = __ballot(fail);
+        if (b && (threadIdx.x & 63) == 0) atomicAdd(n_fail, (uint32_t)__popcll(b));
     }
 }
 
@@ -157,416 +166,6 @@ __global__ void sync_ranges_kernel(const uint64_t *present, const uint64_t *word
     out_end[i] = lo[i] >= h ? lo[i] : (j < h ? j : h);
 }
 
-// ---------------- incremental applyRemoteChanges ----------------
-// inc_apply_kernel: one wave per document whose new changes all apply in arrival order on
-// the resident state (Automerge's applyQueuedOps applies them in its first pass when each is
-// causally ready after the previous ones; DocBackend.ts:169-185 -> Backend.applyChanges).
-// For each new change: causallyReady against the resident opSet.clock, allDeps by the
-// transitiveDeps fold over the resident allDeps rows (each old fold source found by
-// (actor, seq) in one scan of the log), history position, heads and clock.  For each new map
-// op (set / del / link): the register's survivors filtered to the concurrent ones, the op
-// pushed, sortBy(actor).reverse() — only the registers the new ops hit are recomputed; the
-// rest of the register table is repacked as it was.  Anything outside that (a duplicate or
-// not-yet-ready change, inc / counter / list / object-creation ops, an unknown object, tiles
-// too small) lists the document in bail before any merged state is written, and the host re-merges that
-// document's whole log with the batch kernels.  The loads that depend only on the
-// descriptor (new rows, clock / heads, the old log's (actor, seq) keys, the register table,
-// the survivors) are issued together; the remaining dependent steps are one scan of the log
-// and one gather of allDeps rows.
-__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
-__device__ __forceinline__ uint32_t lane_bcast(uint32_t x, uint32_t l) { return __builtin_amdgcn_readlane(x, l); }
-__device__ __forceinline__ uint64_t wave_ballot(bool p) { return __ballot(p); }
-__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-__device__ __forceinline__ uint64_t key_of(const hm_change_row *r) {
-    const uint2 w = *reinterpret_cast<const uint2 *>(r);          // actor | n_deps << 16, seq
-    return ((uint64_t)(w.x & 0xFFFFu) << 32) | w.y;
-}
-
-// was object `o` created as a map/table by an op of the old log?
-__device__ bool inc_obj_is_map(const AppendDesc &D, const IncArenas &A, uint32_t o, uint32_t lane) {
-    for (uint32_t base = 0; base < D.n_old_o; base += 64) {
-        const uint32_t i = base + lane;
-        bool m = false;
-        uint32_t act = 0;
-        if (i < D.n_old_o) {
-            const hm_op_row &r = A.ops[D.dst_o + i];
-            act = r.action;
-            m = act <= HM_MAKE_TEXT && r.obj == o;
-        }
-        const uint64_t b = wave_ballot(m);
-        if (b) {
-            const uint32_t first = lane_bcast(act, (uint32_t)__builtin_ctzll(b));
-            return first == HM_MAKE_MAP || first == HM_MAKE_TABLE;
-        }
-    }
-    return false;
-}
-
-__device__ bool inc_doc(const AppendDesc &D, const IncArenas &A, const IncDims &M, uint32_t lane, uint8_t *lds) {
-    const uint32_t S = M.S, h = D.handle, NA = D.n_actors, nnc = D.n_new_c, nno = D.n_new_o;
-    uint32_t *nc = reinterpret_cast<uint32_t *>(lds + M.o_nc);          // per new change: 8 words
-    uint32_t *dep = reinterpret_cast<uint32_t *>(lds + M.o_dep);        // new deps: actor, seq
-    uint64_t *tkey = reinterpret_cast<uint64_t *>(lds + M.o_tkey);      // fold steps: (actor, seq)
-    int32_t *tsrc = reinterpret_cast<int32_t *>(lds + M.o_tsrc);        // new change index, or -1 (old)
-    uint32_t *tidx = reinterpret_cast<uint32_t *>(tsrc + M.tgt), *tcnt = tidx + M.tgt;
-    uint32_t *tad = reinterpret_cast<uint32_t *>(lds + M.o_tad);        // allDeps rows of old sources
-    uint32_t *adn = reinterpret_cast<uint32_t *>(lds + M.o_adn);        // allDeps rows of the new changes
-    uint64_t *skey = reinterpret_cast<uint64_t *>(lds + M.o_skey);      // staged old log: (actor, seq)
-    uint32_t *sof = reinterpret_cast<uint32_t *>(lds + M.o_sof);        //                 first op
-    uint32_t *r_cnt = reinterpret_cast<uint32_t *>(lds + M.o_reg), *r_off = r_cnt + M.regs, *r_obj = r_off + M.regs;
-    uint8_t *r_slot = reinterpret_cast<uint8_t *>(r_obj + M.regs);
-    hm_surv_result *sold = reinterpret_cast<hm_surv_result *>(lds + M.o_sold);
-    hm_surv_result *wl = reinterpret_cast<hm_surv_result *>(lds + M.o_wl);
-    uint32_t *wls = reinterpret_cast<uint32_t *>(lds + M.o_wls), *scnt = reinterpret_cast<uint32_t *>(lds + M.o_scnt);
-    uint8_t *wla = lds + M.o_wla;
-
-    const uint32_t hist_len = uni(A.res_docs[h].hist_len), n_old_surv = uni(A.res_docs[h].n_surv);
-    // (lane-per-actor rows: wide strides re-merge; survivor actor bytes keep 7 bits)
-    if (S > 64 || NA > S || nnc == 0 || nnc > M.new_c || nno > 64 || D.n_r > M.regs || n_old_surv > M.surv || D.n_old_r > D.n_r)
-        return false;
-    const bool staged = D.n_old_c <= M.stage;
-
-    // ---- loads that depend only on the descriptor ----
-    uint32_t clk = 0, hd = 0, mc = 0;
-    if (lane < S) {
-        clk = A.clock[(size_t)h * S + lane];
-        hd = A.heads[(size_t)h * S + lane];
-        mc = A.min_clock ? A.min_clock[(size_t)h * S + lane] : 0u;
-    }
-    uint32_t ca = 0, cq = 0, cnd = 0, cdo = 0, cno = 0, coo = 0;
-    if (lane < nnc) {
-        const hm_change_row c = A.changes[D.dst_c + D.n_old_c + lane];
-        ca = c.actor; cq = c.seq; cnd = c.n_deps; cdo = c.dep_off - D.dst_d; cno = c.n_ops; coo = c.op_first - D.dst_o;
-    }
-    uint32_t o_act = 0, o_dt = 0, o_obj = 0, o_reg = 0, o_vt = 0, o_vlo = 0, o_vhi = 0;
-    if (lane < nno) {
-        const hm_op_row op = A.ops[D.dst_o + D.n_old_o + lane];
-        o_act = op.action; o_dt = op.datatype; o_obj = op.obj; o_reg = op.reg; o_vt = op.vtag;
-        o_vlo = (uint32_t)op.value; o_vhi = (uint32_t)(op.value >> 32);
-    }
-    if (staged)
-        for (uint32_t i = lane; i < D.n_old_c; i += 64) {
-            const hm_change_row *r = A.changes + D.dst_c + i;
-            skey[i] = key_of(r);
-            sof[i] = r->op_first - D.dst_o;
-        }
-    for (uint32_t g = lane; g < D.n_r; g += 64) {
-        uint32_t c = 0, o = 0, ob = HM_NONE;
-        if (g < D.n_old_r) {
-            const hm_reg_result r = A.regs[D.src_r + g];
-            c = r.n_surv; o = r.surv_off; ob = r.obj;
-        }
-        r_cnt[g] = c; r_off[g] = o; r_obj[g] = ob; r_slot[g] = 0xFF;
-    }
-    for (uint32_t i = lane; i < n_old_surv; i += 64) sold[i] = A.surv[D.src_o + i];
-
-    // ---- the new rows: layout (grouped by change, in order, after the old rows) and values ----
-    uint32_t sd = lane < nnc ? cnd : 0u, so = lane < nnc ? cno : 0u;
-    for (uint32_t d = 1; d < 8; d <<= 1) {
-        const uint32_t yd = __shfl_up(sd, d, 64), yo = __shfl_up(so, d, 64);
-        if (lane >= d) { sd += yd; so += yo; }
-    }
-    const uint32_t xd = sd - (lane < nnc ? cnd : 0u), xo = so - (lane < nnc ? cno : 0u);
-    const uint32_t total_d = lane_bcast(sd, nnc - 1), total_o = lane_bcast(so, nnc - 1);
-    const bool bad_c = lane < nnc && (ca >= NA || cq == 0 || cdo != D.n_old_d + xd || coo != D.n_old_o + xo);
-    // set / del / link, counter sets, and incs by a number (an inc of anything else is left to
-    // the re-merge); an inc must stay inside the exact-integer envelope checked below
-    const bool bad_o = lane < nno && ((o_act != HM_SET && o_act != HM_DEL && o_act != HM_LINK && o_act != HM_INC) ||
-                                      (o_act == HM_INC && o_vt != HM_V_INT && o_vt != HM_V_FLOAT) ||
-                                      (o_act == HM_INC && o_vt == HM_V_INT &&
-                                       ((int64_t)(((uint64_t)o_vhi << 32) | o_vlo) >= (1ll << 43) ||
-                                        (int64_t)(((uint64_t)o_vhi << 32) | o_vlo) <= -(1ll << 43))) ||
-                                      (o_act == HM_INC && D.n_old_o + nno > 256) ||
-                                      o_obj >= D.n_objs || o_reg >= D.n_r ||
-                                      (o_vt == HM_V_INT && ((int64_t)(((uint64_t)o_vhi << 32) | o_vlo) > 9007199254740992ll ||
-                                                            (int64_t)(((uint64_t)o_vhi << 32) | o_vlo) < -9007199254740992ll)));
-    if (wave_ballot(bad_c || bad_o) || total_o != nno || total_d != D.n_new_d || total_d + nnc > M.tgt) return false;
-    if (wave_ballot(lane < nno && o_act == HM_INC)) {
-        // the exact-integer envelope over the whole log (the oracle's |partial sums| <= 2^53 rule):
-        // every integer counter base |v| < 2^50 and inc |v| < 2^43 in <= 256 ops bound any sum
-        bool big = false;
-        for (uint32_t i = lane; i < D.n_old_o; i += 64) {
-            const hm_op_row &r = A.ops[D.dst_o + i];
-            const int64_t v = (int64_t)r.value;
-            if (r.vtag == HM_V_INT && r.action == HM_INC) big |= v >= (1ll << 43) || v <= -(1ll << 43);
-            if (r.vtag == HM_V_INT && r.action == HM_SET && r.datatype == HM_DT_COUNTER) big |= v >= (1ll << 50) || v <= -(1ll << 50);
-        }
-        if (lane < nno && o_act == HM_SET && o_dt == HM_DT_COUNTER && o_vt == HM_V_INT) {
-            const int64_t v = (int64_t)(((uint64_t)o_vhi << 32) | o_vlo);
-            big |= v >= (1ll << 50) || v <= -(1ll << 50);
-        }
-        if (wave_ballot(big)) return false;
-    }
-    if (lane < nnc) {
-        uint32_t *w = nc + lane * 8;
-        w[0] = ca; w[1] = cq; w[2] = cnd; w[3] = xd; w[4] = cno; w[5] = xo;
-    }
-    for (uint32_t t = lane; t < total_d; t += 64) {
-        const hm_dep_row d = A.deps[D.dst_d + D.n_old_d + t];
-        dep[2 * t] = d.actor; dep[2 * t + 1] = d.seq;
-    }
-    __syncthreads();
-
-    // ---- causallyReady in arrival order; the transitiveDeps fold steps (A.1) ----
-    uint32_t ck = clk, nt = 0;
-    for (uint32_t j = 0; j < nnc; j++) {
-        const uint32_t a = uni(nc[j * 8]), q = uni(nc[j * 8 + 1]), nd = uni(nc[j * 8 + 2]), d0 = uni(nc[j * 8 + 3]);
-        if (lane_bcast(ck, a) + 1u != q) return false;          // a duplicate, or not ready: queue semantics
-        const uint32_t t0 = nt;
-        bool own = false;
-        for (uint32_t t = 0; t <= nd; t++) {
-            uint32_t da, dq;
-            if (t < nd) {
-                da = uni(dep[2 * (d0 + t)]); dq = uni(dep[2 * (d0 + t) + 1]);
-                if (da >= NA) return false;
-                if (da == a) { dq = q - 1; own = true; }
-            } else {
-                if (own) break;
-                da = a; dq = q - 1;
-            }
-            if (lane_bcast(ck, da) < dq) return false;
-            if (dq == 0) continue;
-            int src = -1;
-            for (uint32_t k = 0; k < j; k++)
-                if (uni(nc[k * 8]) == da && uni(nc[k * 8 + 1]) == dq) src = (int)k;
-            if (lane == 0) { tkey[nt] = ((uint64_t)da << 32) | dq; tsrc[nt] = src; tcnt[nt] = 0; tidx[nt] = 0; }
-            nt++;
-        }
-        if (lane == 0) { nc[j * 8 + 6] = t0; nc[j * 8 + 7] = nt - t0; }
-        if (lane == a) ck = q;
-    }
-    __syncthreads();
-
-    // ---- old fold sources: exactly one applied row of the log per (actor, seq) ----
-    bool any_old = false;
-    for (uint32_t t = 0; t < nt; t++) any_old |= tsrc[t] < 0;
-    if (any_old) {
-        for (uint32_t base = 0; base < D.n_old_c; base += 64) {
-            const uint32_t i = base + lane;
-            uint64_t key = ~0ull;
-            if (i < D.n_old_c) key = staged ? skey[i] : key_of(A.changes + D.dst_c + i);
-            for (uint32_t t = 0; t < nt; t++) {
-                if (tsrc[t] >= 0) continue;
-                const uint64_t m = wave_ballot(key == tkey[t]);
-                if (m && lane == 0) { tcnt[t] += (uint32_t)__builtin_popcountll(m); tidx[t] = base + (uint32_t)__builtin_ctzll(m); }
-            }
-        }
-        __syncthreads();
-        for (uint32_t t = 0; t < nt; t++)
-            if (tsrc[t] < 0 && uni(tcnt[t]) != 1u) return false;       // duplicates in the log: re-merge
-        for (uint32_t w = lane; w < nt * S; w += 64) {
-            const uint32_t t = w / S, x = w - t * S;
-            tad[w] = tsrc[t] < 0 ? A.all_deps[(size_t)(D.src_c + tidx[t]) * S + x] : 0u;
-        }
-        __syncthreads();
-    }
-
-    // ---- per new change: allDeps, heads, clock (applyChange) ----
-    for (uint32_t j = 0; j < nnc; j++) {
-        const uint32_t a = uni(nc[j * 8]), q = uni(nc[j * 8 + 1]), t0 = uni(nc[j * 8 + 6]), tn = uni(nc[j * 8 + 7]);
-        uint32_t adv = 0;
-        for (uint32_t t = t0; t < t0 + tn; t++) {
-            const uint64_t key = tkey[t];
-            const uint32_t da = uni((uint32_t)(key >> 32)), dq = uni((uint32_t)key);
-            const int src = (int)uni((uint32_t)tsrc[t]);
-            const uint32_t row = lane < S ? (src >= 0 ? adn[src * S + lane] : tad[t * S + lane]) : 0u;
-            if (lane < NA && row > adv) adv = row;
-            if (lane == da) adv = dq;
-        }
-        if (lane >= NA) adv = 0;
-        if (lane < S) adn[j * S + lane] = adv;
-        if (hd && hd <= adv) hd = 0;
-        if (lane == a) { hd = q; clk = q; }
-        __syncthreads();
-    }
-
-    // ---- objects other than the root must be maps created by the old log ----
-    {
-        uint64_t om = wave_ballot(lane < nno && o_obj != 0);
-        uint32_t checked = 0;
-        while (om) {
-            const uint32_t l = (uint32_t)__builtin_ctzll(om);
-            om &= om - 1;
-            const uint32_t o = lane_bcast(o_obj, l);
-            if (o == checked) continue;
-            if (!inc_obj_is_map(D, A, o, lane)) return false;
-            checked = o;
-        }
-    }
-
-    // ---- the new ops in order (applyAssign, A.2) on the registers they hit ----
-    uint32_t nslots = 0, j = 0, jend = uni(nc[4]);
-    for (uint32_t k = 0; k < nno; k++) {
-        while (k >= jend) { j++; jend += uni(nc[j * 8 + 4]); }
-        const uint32_t a = uni(nc[j * 8]), q = uni(nc[j * 8 + 1]);
-        const uint32_t act = lane_bcast(o_act, k), obj = lane_bcast(o_obj, k), g = lane_bcast(o_reg, k);
-        const uint32_t vtag = lane_bcast(o_vt, k);
-        const uint64_t val = ((uint64_t)lane_bcast(o_vhi, k) << 32) | lane_bcast(o_vlo, k);
-        uint32_t slot = uni(r_slot[g]);
-        if (slot == 0xFF) {
-            if (nslots == M.slots) return false;
-            slot = nslots++;
-            const uint32_t c0 = uni(r_cnt[g]), o0 = uni(r_off[g]);
-            if (c0 > HM_INC_SLOT_CAP || o0 + c0 > n_old_surv) return false;
-            if (lane < c0) {
-                const hm_surv_result x = sold[o0 + lane];
-                // the old change owning op x.op: the last change whose first op is <= x.op
-                uint32_t lo = 0, hi = D.n_old_c;
-                while (hi - lo > 1) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    const uint32_t f = staged ? sof[mid] : A.changes[D.dst_c + mid].op_first - D.dst_o;
-                    if (f <= x.op) lo = mid; else hi = mid;
-                }
-                const uint64_t kk = staged ? skey[lo] : key_of(A.changes + D.dst_c + lo);
-                const hm_op_row &xo = A.ops[D.dst_o + x.op];
-                const uint32_t cset = (xo.action == HM_SET && xo.datatype == HM_DT_COUNTER) ? 0x80u : 0u;
-                wl[slot * HM_INC_SLOT_CAP + lane] = x;
-                wla[slot * HM_INC_SLOT_CAP + lane] = (uint8_t)((kk >> 32) | cset);
-                wls[slot * HM_INC_SLOT_CAP + lane] = (uint32_t)kk;
-            }
-            if (lane == 0) { scnt[slot] = c0; r_slot[g] = (uint8_t)slot; }
-            __syncthreads();
-        }
-        const uint32_t base = slot * HM_INC_SLOT_CAP, cnt = uni(scnt[slot]);
-        if (act == HM_INC) {
-            // applyAssign for inc (A.2): every surviving counter set that is causally before the
-            // inc (its change an ancestor of the inc's: allDeps(inc)[x.actor] >= x.seq) adds the
-            // inc, integer + integer exactly, anything else in f64 (the application order); nothing
-            // is removed or reordered.  Integer sums stay inside the exact range: |value| < 2^50,
-            // |inc| < 2^43, at most 256 ops in the log (else the re-merge decides)
-            bool out = false;
-            if (lane < cnt) {
-                hm_surv_result x = wl[base + lane];
-                const uint32_t xa = wla[base + lane], xs = wls[base + lane];
-                const bool numeric = x.vtag == HM_V_INT || x.vtag == HM_V_FLOAT;
-                if ((xa & 0x80u) && numeric && adn[j * S + (xa & 0x7Fu)] >= xs) {
-                    if (x.vtag == HM_V_INT && vtag == HM_V_INT) {
-                        const int64_t cur = (int64_t)x.value;
-                        out = cur >= (1ll << 50) || cur <= -(1ll << 50);
-                        x.value = (uint64_t)(cur + (int64_t)val);
-                    } else {
-                        double xv, iv;
-                        if (x.vtag == HM_V_INT) xv = (double)(int64_t)x.value; else __builtin_memcpy(&xv, &x.value, 8);
-                        if (vtag == HM_V_INT) iv = (double)(int64_t)val; else __builtin_memcpy(&iv, &val, 8);
-                        const double r = xv + iv;
-                        __builtin_memcpy(&x.value, &r, 8);
-                        x.vtag = HM_V_FLOAT;
-                    }
-                    wl[base + lane] = x;
-                }
-            }
-            if (wave_ballot(out)) return false;
-            __syncthreads();
-            // (then, like every assign, the stable sortBy(actor).reverse() below: an inc flips
-            // the order of a change's equal-actor survivors too)
-        }
-        // survivors concurrent with the new op stay (isConcurrent reduces to
-        // allDeps(new)[x.actor] < x.seq: no resident change can depend on the new one)
-        hm_surv_result x = {};
-        uint32_t xa = 0, xs = 0;
-        bool keep = false;
-        if (lane < cnt) {
-            x = wl[base + lane]; xa = wla[base + lane]; xs = wls[base + lane];
-            keep = act == HM_INC || adn[j * S + (xa & 0x7Fu)] < xs;      // an inc removes nothing
-        }
-        const uint64_t km = wave_ballot(keep);
-        const uint32_t nk = (uint32_t)__builtin_popcountll(km), pos = lanes_below(km);
-        const bool push = act != HM_DEL && act != HM_INC;
-        const uint32_t ncnt = nk + (push ? 1u : 0u);
-        if (ncnt > HM_INC_SLOT_CAP) return false;
-        __syncthreads();
-        if (keep) { wl[base + pos] = x; wla[base + pos] = (uint8_t)xa; wls[base + pos] = xs; }
-        if (push && lane == 0) {
-            hm_surv_result y;
-            y.op = D.n_old_o + k; y.vtag = vtag; y.value = val;
-            const uint32_t cset = (act == HM_SET && lane_bcast(o_dt, k) == HM_DT_COUNTER) ? 0x80u : 0u;
-            wl[base + nk] = y; wla[base + nk] = (uint8_t)(a | cset); wls[base + nk] = q;
-        }
-        __syncthreads();
-        // sortBy(actor) (stable) then reverse
-        if (lane < ncnt) { x = wl[base + lane]; xa = wla[base + lane]; xs = wls[base + lane]; }
-        uint32_t rank = 0;
-        for (uint32_t e = 0; e < ncnt; e++) {
-            const uint32_t ea = wla[base + e] & 0x7Fu, xr = xa & 0x7Fu;
-            rank += (ea < xr || (ea == xr && e < lane)) ? 1u : 0u;
-        }
-        __syncthreads();
-        if (lane < ncnt) {
-            const uint32_t d = ncnt - 1 - rank;
-            wl[base + d] = x; wla[base + d] = (uint8_t)xa; wls[base + d] = xs;
-        }
-        if (lane == 0) { scnt[slot] = ncnt; r_obj[g] = obj; }
-        __syncthreads();
-    }
-
-    // ---- write back: registers (repacked in register order), survivors ----
-    const bool same_o = D.src_o == D.dst_o, same_r = D.src_r == D.dst_r;
-    uint32_t carry = 0;
-    for (uint32_t g0 = 0; g0 < D.n_r; g0 += 64) {
-        const uint32_t g = g0 + lane;
-        const bool valid = g < D.n_r;
-        const uint32_t slot = valid ? r_slot[g] : 0xFFu;
-        const uint32_t cnt = !valid ? 0u : (slot != 0xFF ? scnt[slot] : r_cnt[g]);
-        uint32_t incl = cnt;
-        for (uint32_t d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += y;
-        }
-        const uint32_t off = carry + incl - cnt;
-        carry += lane_bcast(incl, 63);
-        if (valid) {
-            const bool unchanged = slot == 0xFF && g < D.n_old_r && off == r_off[g];
-            if (!(unchanged && same_r)) {
-                hm_reg_result r;
-                r.n_surv = cnt; r.surv_off = off; r.list_index = -1; r.obj = r_obj[g];
-                A.regs[D.dst_r + g] = r;
-            }
-            if (!(unchanged && same_o))
-                for (uint32_t i = 0; i < cnt; i++)
-                    A.surv[D.dst_o + off + i] = slot != 0xFF ? wl[slot * HM_INC_SLOT_CAP + i] : sold[r_off[g] + i];
-        }
-    }
-
-    // ---- history, allDeps, clocks, the document's result row ----
-    if (D.src_c != D.dst_c) {
-        for (uint32_t i = lane; i < D.n_old_c; i += 64) A.hist[D.dst_c + i] = A.hist[D.src_c + i];
-        for (size_t w = lane; w < (size_t)D.n_old_c * S; w += 64)
-            A.all_deps[(size_t)D.dst_c * S + w] = A.all_deps[(size_t)D.src_c * S + w];
-    }
-    if (lane < nnc) A.hist[D.dst_c + D.n_old_c + lane] = (int32_t)(hist_len + lane);
-    for (uint32_t w = lane; w < nnc * S; w += 64) A.all_deps[(size_t)(D.dst_c + D.n_old_c) * S + w] = adn[w];
-    if (lane < S) {
-        A.clock[(size_t)h * S + lane] = clk;
-        A.back_clock[(size_t)h * S + lane] = clk;                 // queue empty: every handed change applied
-        A.heads[(size_t)h * S + lane] = hd;
-    }
-    const bool ag = wave_ballot(lane < S && clk < mc) == 0, bg = wave_ballot(lane < S && mc < clk) == 0;
-    if (lane == 0) {
-        hm_doc_result r = {};
-        r.status = HM_OK; r.err_change = HM_NONE; r.err_op = HM_NONE;
-        r.hist_len = hist_len + nnc; r.n_queued = 0; r.n_surv = carry;
-        r.min_cmp = (ag && bg) ? 0u : (ag ? 1u : (bg ? 2u : 3u));
-        A.res_docs[h] = r;
-    }
-    return true;
-}
-
-// bail[0] = count, bail[1 ..] = the handles handed back (any order)
-__global__ __launch_bounds__(64, 8) void inc_apply_kernel(const AppendDesc *descs, uint32_t n, IncArenas A, IncDims M,
-                                                       uint32_t *bail) {
-    extern __shared__ __align__(16) uint8_t inc_lds[];
-    const uint32_t lane = threadIdx.x;
-    for (uint32_t di = blockIdx.x; di < n; di += gridDim.x) {
-        if (!descs[di].inc) continue;
-        const AppendDesc D = descs[di];
-        const bool ok = inc_doc(D, A, M, lane, inc_lds);
-        if (lane == 0 && !ok) bail[1 + atomicAdd(&bail[0], 1u)] = D.handle;
-        __syncthreads();
-    }
-}
-
 // Rows of chosen registers (incremental patches): request i reads register abs_reg[i] and its
 // survivors (doc op-segment base surv_base[i] + surv_off) into out_surv at an offset taken
 // from a bump counter; its row's surv_off is rewritten to that offset.
@@ -601,11 +200,10 @@ __device__ __forceinline__ uint32_t pow2c(uint32_t x) {
 #define PLAN_WG 1024
 __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
     __shared__ unsigned long long s_need[4][PLAN_WG / 64];
-    __shared__ uint32_t s_inc[PLAN_WG / 64], s_mx[6][PLAN_WG / 64];
+    __shared__ uint32_t s_inc[PLAN_WG / 64];
     const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
     if (ln == 0) {
         for (int k = 0; k < 4; k++) s_need[k][wv] = 0;
-        for (int k = 0; k < 6; k++) s_mx[k][wv] = 0;
         s_inc[wv] = 0;
     }
     const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
@@ -657,44 +255,31 @@ __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
         for (int o = 32; o > 0; o >>= 1) g += (unsigned long long)__shfl_xor((long long)g, o);
         if (ln == 0) s_need[k][wv] = g;
     }
-    // route: a clean resident state (last merge ok, nothing queued, no re-rank) and new rows that
-    // fit the incremental tiles -> inc_apply_kernel; the rest re-merge their whole log
+    // route: a clean resident state (last merge ok, nothing queued, no re-rank) and new rows inside
+    // the incremental envelope -> the incremental kernels (which touch only the registers the new
+    // ops hit); the rest re-merge their whole log
     const hm_doc_result last = a.res_docs[live ? h : 0u];
     const uint32_t tgt = r.n_deps + r.n_changes;
     const bool inc = live && a.incremental && last.status == HM_OK && last.n_queued == 0 && !remapped && r.n_changes > 0 &&
                      r.n_changes <= HM_INC_MAX_NEW_C && r.n_ops <= HM_INC_MAX_NEW_O && tgt <= HM_INC_MAX_TGT &&
-                     r.n_regs <= HM_INC_MAX_REGS && last.n_surv <= HM_INC_MAX_SURV && m.n_r <= r.n_regs &&
-                     r.n_actors <= a.S && !((m.flags | r.flags) & HM_DOC_HAS_LISTS);
+                     m.n_r <= r.n_regs && r.n_actors <= a.S && !((m.flags | r.flags) & HM_DOC_HAS_LISTS);
     p.inc = inc ? 1u : 0u;
     p.remapped = remapped ? 1u : 0u;
     if (live) a.plan[i] = p;
     const unsigned long long im = __ballot(inc);
     if (ln == 0) s_inc[wv] = (uint32_t)__popcll(im);
-    if (im) {
-        uint32_t v[6] = {inc ? r.n_changes : 0u, inc ? tgt : 0u,
-                         inc ? (m.n_c < HM_INC_MAX_STAGE ? m.n_c : (uint32_t)HM_INC_MAX_STAGE) : 0u, inc ? r.n_regs : 0u,
-                         inc ? last.n_surv : 0u, inc ? (r.n_ops < HM_INC_SLOTS ? r.n_ops : (uint32_t)HM_INC_SLOTS) : 0u};
-        for (int k = 0; k < 6; k++) {
-            for (int o = 32; o > 0; o >>= 1) { const uint32_t y = (uint32_t)__shfl_xor((int)v[k], o); v[k] = v[k] > y ? v[k] : y; }
-            if (ln == 0) s_mx[k][wv] = v[k];
-        }
-    }
     }
     __syncthreads();
-    if (threadIdx.x < 11) {                                        // one lane per reduced value
+    if (threadIdx.x < 5) {                                         // one lane per reduced value
         const uint32_t k = threadIdx.x, nw = PLAN_WG / 64;
         if (k < 4) {
             unsigned long long g = 0;
             for (uint32_t w = 0; w < nw; w++) g += s_need[k][w];
             if (g) atomicAdd(&a.st->need[k], g);
-        } else if (k == 4) {
+        } else {
             uint32_t c = 0;
             for (uint32_t w = 0; w < nw; w++) c += s_inc[w];
             if (c) atomicAdd(&a.st->n_inc, c);
-        } else {
-            uint32_t x = 0;
-            for (uint32_t w = 0; w < nw; w++) x = x > s_mx[k - 5][w] ? x : s_mx[k - 5][w];
-            if (x) atomicMax(&a.st->mx[k - 5], x);
         }
     }
 }
@@ -722,7 +307,7 @@ __global__ void alloc_kernel(PlanArgs a) {
     D.remap_row = p.remapped ? i : 0xFFFFFFFFu;
     m.n_c += r.n_changes; m.n_d += r.n_deps; m.n_o += r.n_ops;
     m.n_r = r.n_regs; m.n_objs = r.n_objs; m.n_actors = r.n_actors; m.flags |= r.flags;
-    D.n_r = m.n_r; D.n_actors = m.n_actors; D.n_objs = m.n_objs;
+    D.n_r = m.n_r; D.n_actors = m.n_actors; D.n_objs = m.n_objs; D.o_cap = m.o_cap;
     D.inc = (uint16_t)p.inc;
     a.descs[i] = D;
     a.dm[h] = m;
@@ -766,14 +351,17 @@ __global__ __launch_bounds__(PLAN_WG) void doc_rows_kernel(const uint32_t *list,
     }
 }
 
-__global__ void rollback_kernel(const uint32_t *handles, uint32_t n, const hm_doc_result *res_docs, const PlanRow *plan,
+// every = 0: the documents whose merge failed (marked in their plan row: rolled back once);
+// every = 1: all documents of the batch not rolled back yet (hm_batch_undo)
+__global__ void rollback_kernel(const uint32_t *handles, uint32_t n, const hm_doc_result *res_docs, PlanRow *plan,
                                 const uint8_t *remap, uint32_t S, DevDoc *dm, AppendDesc *descs, uint8_t *inv,
-                                uint32_t *list, PlanStats *st) {
+                                uint32_t *list, PlanStats *st, uint32_t every) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t h = handles[i];
-    if (res_docs[h].status == HM_OK) return;
+    if (plan[i].inc == 0xFFFFFFFFu || (!every && res_docs[h].status == HM_OK)) return;
     const PlanRow p = plan[i];
+    plan[i].inc = 0xFFFFFFFFu;
     DevDoc m = dm[h];
     const uint32_t k = atomicAdd(&st->n_back, 1u);
     AppendDesc D = {};
@@ -862,12 +450,12 @@ hipError_t hm_launch_doc_rows(const uint32_t *list, uint32_t n, const DevDoc *dm
     hipLaunchKernelGGL(hms::doc_rows_kernel, dim3((n + PLAN_WG - 1) / PLAN_WG), dim3(PLAN_WG), 0, s, list, n, dm, rows, st);
     return hipGetLastError();
 }
-hipError_t hm_launch_rollback(const uint32_t *handles, uint32_t n, const hm_doc_result *res_docs, const PlanRow *plan,
+hipError_t hm_launch_rollback(const uint32_t *handles, uint32_t n, const hm_doc_result *res_docs, PlanRow *plan,
                               const uint8_t *remap, uint32_t S, DevDoc *dm, AppendDesc *descs, uint8_t *inv,
-                              uint32_t *list, PlanStats *st, hipStream_t s) {
+                              uint32_t *list, PlanStats *st, uint32_t every, hipStream_t s) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(hms::rollback_kernel, dim3((n + 255) / 256), dim3(256), 0, s, handles, n, res_docs, plan, remap, S, dm,
-                       descs, inv, list, st);
+                       descs, inv, list, st, every);
     return hipGetLastError();
 }
 hipError_t hm_launch_init_docs(DevDoc *dm, uint32_t h0, uint32_t n, hipStream_t s) {
@@ -906,48 +494,6 @@ hipError_t hm_launch_append(const AppendDesc *descs, uint32_t n_desc, const Stor
     return hipGetLastError();
 }
 
-IncDims hm_inc_dims(uint32_t S, uint32_t new_c, uint32_t tgt, uint32_t stage, uint32_t regs, uint32_t surv,
-                    uint32_t slots) {
-    IncDims M = {};
-    M.S = S; M.new_c = new_c ? new_c : 1; M.tgt = tgt ? tgt : 1; M.stage = stage; M.regs = regs ? regs : 1;
-    M.surv = surv ? surv : 1; M.slots = slots ? slots : 1;
-    uint32_t o = 0;
-    auto take = [&](size_t bytes) { const uint32_t r = o; o += (uint32_t)((bytes + 15) & ~(size_t)15); return r; };
-    M.o_nc = take((size_t)M.new_c * 32);
-    M.o_dep = take((size_t)M.tgt * 8);
-    M.o_tkey = take((size_t)M.tgt * 8);
-    M.o_tsrc = take((size_t)M.tgt * 12);
-    M.o_tad = take((size_t)M.tgt * S * 4);
-    M.o_adn = take((size_t)M.new_c * S * 4);
-    M.o_skey = take((size_t)M.stage * 8);
-    M.o_sof = take((size_t)M.stage * 4);
-    M.o_reg = take((size_t)M.regs * 13);
-    M.o_sold = take((size_t)M.surv * 16);
-    M.o_wl = take((size_t)M.slots * HM_INC_SLOT_CAP * 16);
-    M.o_wls = take((size_t)M.slots * HM_INC_SLOT_CAP * 4);
-    M.o_wla = take((size_t)M.slots * HM_INC_SLOT_CAP);
-    M.o_scnt = take((size_t)M.slots * 4);
-    M.bytes = o;
-    return M;
-}
-
-hipError_t hm_launch_inc_apply(const AppendDesc *descs, uint32_t n, const IncArenas &A, const IncDims &M,
-                               uint32_t *bail, hipStream_t s) {
-    if (!n) return hipSuccess;
-    hipError_t z = hipMemsetAsync(bail, 0, 4, s);
-    if (z != hipSuccess) return z;
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&hms::inc_apply_kernel),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
-    const uint32_t grid = n < (1u << 20) ? n : (1u << 20);
-    hipLaunchKernelGGL(hms::inc_apply_kernel, dim3(grid), dim3(64), M.bytes, s, descs, n, A, M, bail);
-    return hipGetLastError();
-}
-
 hipError_t hm_launch_read_regs(uint32_t n, const uint32_t *abs_reg, const uint32_t *surv_base, const hm_reg_result *regs,
                                const hm_surv_result *surv, hm_reg_result *out_regs, hm_surv_result *out_surv, uint32_t cap,
                                uint32_t *counter, hipStream_t s) {
@@ -959,10 +505,11 @@ hipError_t hm_launch_read_regs(uint32_t n, const uint32_t *abs_reg, const uint32
 
 hipError_t hm_launch_gather(const uint32_t *handles, uint32_t n, uint32_t S, const hm_doc_result *res_docs,
                             const uint32_t *clock, const uint32_t *back_clock, const uint32_t *heads, uint8_t *out,
-                            hipStream_t s) {
+                            uint32_t *n_fail, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(hms::gather_kernel, dim3((n + 255) / 256), dim3(256), 0, s, handles, n, S, res_docs, clock,
-                       back_clock, heads, out);
+    const size_t words = (size_t)n * (8 + 3 * (size_t)S);
+    hipLaunchKernelGGL(hms::gather_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, handles, n, S, res_docs,
+                       clock, back_clock, heads, out, n_fail);
     return hipGetLastError();
 }
 

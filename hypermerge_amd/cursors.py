@@ -15,7 +15,7 @@ from typing import Dict, List, Mapping, Optional, Sequence, Tuple
 import numpy as np
 
 from .engine import Engine, lib
-from .exchange import fnv1a64
+from .exchange import KeyTable
 
 INFINITY_SEQ = 9007199254740991            # Number.MAX_SAFE_INTEGER (src/CursorStore.ts:17)
 Cursor = Dict[str, float]
@@ -57,10 +57,11 @@ class _Table:
 
 
 class CursorStore:
-    def __init__(self, engine: Engine, max_actors_per_doc: int = 64):
+    def __init__(self, engine: Engine, max_actors_per_doc: int = 64, hash_fn=None):
         self.engine, self.K = engine, max_actors_per_doc
         self.tables: Dict[str, _Table] = {}
-        self.actor_ids: Dict[int, str] = {}
+        self.keys = KeyTable(hash_fn)             # a key two actor ids share raises, never merges them
+        self.actor_ids: Dict[int, str] = self.keys.ids
         self.updateQ: List[Descriptor] = []
 
     def close(self):
@@ -80,9 +81,7 @@ class CursorStore:
         return t
 
     def _key(self, actor: str) -> int:
-        k = fnv1a64(actor)
-        self.actor_ids[k] = actor
-        return k
+        return self.keys.key(actor)
 
     # -- the reference API --------------------------------------------------------------------
     def get(self, repo_id: str, doc_id: str) -> Cursor:

@@ -34,7 +34,8 @@ EXPORTS = ("hm_abi_version", "hm_status_message", "hm_engine_create", "hm_engine
            "hm_cursors_entry", "hm_cursors_docs_with_actors", "hm_docset_create", "hm_docset_destroy",
            "hm_docset_engine", "hm_docset_open", "hm_docset_apply", "hm_text_data", "hm_text_results", "hm_text_free",
            "hm_docset_doc_info", "hm_docset_history_prefix", "hm_docset_clock_update", "hm_docset_view",
-           "hm_docset_stats", "hm_sync_ranges_host")
+           "hm_docset_stats", "hm_sync_ranges_host", "hm_batch_submit_device", "hm_batch_wait_device",
+           "hm_batch_undo")
 
 _lib = None
 
@@ -76,6 +77,8 @@ def lib():
         sig = {
             "hm_store_create": [vp, vp, vp], "hm_store_destroy": [vp], "hm_doc_open": [vp, vp],
             "hm_batch_submit": [vp, vp, vp, vp, vp], "hm_batch_wait": [vp, ctypes.c_uint64, vp, vp, vp, vp],
+            "hm_batch_submit_device": [vp, vp, vp, vp, vp], "hm_batch_wait_device": [vp, ctypes.c_uint64, vp, vp],
+            "hm_batch_undo": [vp, ctypes.c_uint64],
             "hm_doc_info": [vp, u32, vp], "hm_doc_read": [vp, u32] + [vp] * 7, "hm_doc_log": [vp, u32, vp, vp, vp],
             "hm_doc_history_prefix": [vp, u32, u32, vp], "hm_doc_set_min_clock": [vp, u32, vp],
             "hm_store_clock_update": [vp, u32, vp, vp, vp, vp],

@@ -55,11 +55,12 @@ class KeyTable:
     """key -> id string for the documents and actors a host has seen (a 64-bit key that two
     different ids share is an error, never a silent merge of two actors)."""
 
-    def __init__(self) -> None:
+    def __init__(self, hash_fn=None) -> None:
         self.ids: Dict[int, str] = {}
+        self.hash = hash_fn or fnv1a64
 
     def key(self, s: str) -> int:
-        k = fnv1a64(s)
+        k = self.hash(s)
         old = self.ids.setdefault(k, s)
         if old != s:
             raise ValueError(f"FNV-1a64 key collision: {old!r} / {s!r}")

@@ -213,6 +213,21 @@ function fnv1a64(s) {
 // The per-document BackendState: a document of its shard's docset plus the log entries as
 // they were handed over (history slices).  States are linear: applyChanges advances the
 // document in place and returns the same state object.
+// key -> id string of every id a host has keyed: a 64-bit key that two different ids share is
+// an error, never a silent merge of two actors' cursors or clocks (the reference keys its
+// Cursors / Clocks rows by the id strings themselves, src/CursorStore.ts, src/ClockStore.ts)
+class KeyTable {
+  constructor(hash) { this.hash = hash || fnv1a64; this.ids = new Map() }
+  key(s) {
+    const k = this.hash(s)
+    const old = this.ids.get(k)
+    if (old === undefined) this.ids.set(k, s)
+    else if (old !== s) throw new Error(`FNV-1a64 key collision: ${JSON.stringify(old)} and ${JSON.stringify(s)} (key ${k})`)
+    return k
+  }
+  id(k) { return this.ids.get(k) }
+}
+
 class GpuBackendState {
   constructor(engine, docId) {
     this.engine = engine
@@ -249,7 +264,7 @@ class GpuBackendState {
 class GpuEngine {
   // opts: devices (HIP ordinals; documents shard over them by FNV-1a64(docId) % devices.length),
   // mode 'sync' | 'batched' | 'async', patches (diffs on), threads (host threads per docset),
-  // onError
+  // onError, hash (tests: a key function to force collisions)
   constructor(opts) {
     const o = opts || {}
     this.devices = o.devices || [o.device || 0]
@@ -267,6 +282,7 @@ class GpuEngine {
     this.submits = 0
     this.comm = null
     this.slice = o.slice || 4096     // documents per docset call in async mode (pipelined)
+    this.hash = o.hash || null       // the id -> 64-bit key function of the clock exchange (default FNV-1a64)
   }
 
   shardOf(docId) { return Number(fnv1a64(docId) % BigInt(this.docsets.length)) }
@@ -509,15 +525,10 @@ class GpuEngine {
   // {docId: {actorId: seq}} with the host's id tables.
   exchangeClocks(states) {
     const perShard = this.docsets.map(() => [])
-    const ids = new Map()
+    const ids = this.keys || (this.keys = new KeyTable(this.hash))
     for (const st of states) {
-      const dk = fnv1a64(st.docId)
-      ids.set(dk, st.docId)
-      for (const [a, s] of Object.entries(st.backClock)) {
-        const ak = fnv1a64(a)
-        ids.set(ak, a)
-        perShard[st.shard].push([dk, ak, s])
-      }
+      const dk = ids.key(st.docId)
+      for (const [a, s] of Object.entries(st.backClock)) perShard[st.shard].push([dk, ids.key(a), s])
     }
     const bufs = perShard.map((rows) => {
       const b = Buffer.alloc(rows.length * 24)
@@ -532,7 +543,7 @@ class GpuEngine {
     } else all = Buffer.concat(bufs)           // shards sharing one device: the host holds them all
     const out = {}
     for (let i = 0; i < all.length / 24; i++) {
-      const doc = ids.get(all.readBigUInt64LE(24 * i)), actor = ids.get(all.readBigUInt64LE(24 * i + 8))
+      const doc = ids.id(all.readBigUInt64LE(24 * i)), actor = ids.id(all.readBigUInt64LE(24 * i + 8))
       const c = out[doc] || (out[doc] = {})
       const s = all.readUInt32LE(24 * i + 16)
       if (!(actor in c) || s > c[actor]) c[actor] = s
@@ -708,6 +719,17 @@ class ClockStore {
     this.engine = engine || null
     this.rows = new Map()            // repoId \0 docId -> Map(actorId -> seq)
     this.updateQ = new Channel('clockstore:updateQ')
+    this.writes = []                 // rows written since the last takeBatch (the persistence batch)
+  }
+
+  // The Clocks rows this store wrote since the last call, in order, for one SQL transaction
+  // (INTEGRATION.md §3): ['upsert', repoId, docId, actorId, seq] for every row an upsert-max
+  // changed or inserted, ['delete', repoId, docId] for set()'s clear.  Replayed through the
+  // reference's statements (src/ClockStore.ts:37-48) they give the table this store holds.
+  takeBatch() { const b = this.writes; this.writes = []; return b }
+
+  upsert(m, repoId, docId, a, s) {
+    if (!m.has(a) || s > m.get(a)) { m.set(a, s); this.writes.push(['upsert', repoId, docId, a, s]) }
   }
 
   key(repoId, docId) { return repoId + '\u0000' + docId }
@@ -727,9 +749,7 @@ class ClockStore {
     const k = this.key(repoId, docId)
     let m = this.rows.get(k)
     if (!m) { m = new Map(); this.rows.set(k, m) }
-    for (const [a, s] of Object.entries(clock)) {
-      if (!m.has(a) || s > m.get(a)) m.set(a, s)
-    }
+    for (const [a, s] of Object.entries(clock)) this.upsert(m, repoId, docId, a, s)
     const stored = this.get(repoId, docId)
     const d = [repoId, docId, stored]
     if (!Clock.equal(clock, stored)) this.updateQ.push(d)
@@ -737,7 +757,7 @@ class ClockStore {
   }
 
   set(repoId, docId, clock) {
-    this.rows.delete(this.key(repoId, docId))
+    if (this.rows.delete(this.key(repoId, docId))) this.writes.push(['delete', repoId, docId])
     return this.update(repoId, docId, clock)
   }
 
@@ -771,7 +791,7 @@ class ClockStore {
         if (r.written[j]) {
           let m = this.rows.get(k)
           if (!m) { m = new Map(); this.rows.set(k, m) }
-          for (const [a, s] of Object.entries(stored[j])) if (!m.has(a) || s > m.get(a)) m.set(a, s)
+          for (const [a, s] of Object.entries(stored[j])) this.upsert(m, repoId, doc.id, a, s)
         }
         const d = [repoId, doc.id, this.get(repoId, doc.id)]
         if (r.differs[j]) this.updateQ.push(d)
@@ -789,13 +809,19 @@ function byteOrder(a, b) { return Buffer.compare(Buffer.from(a, 'utf8'), Buffer.
 // rows, actors as FNV-1a64 keys (the clock exchange's); every batched form is one launch.
 const INFINITY_SEQ = Number.MAX_SAFE_INTEGER
 class CursorStore {
-  constructor(engine, maxActorsPerDoc) {
+  constructor(engine, maxActorsPerDoc, opts) {
     this.engine = engine
     this.K = maxActorsPerDoc || 64
     this.tables = new Map()          // repoId -> {c, rows: Map(docId -> row), docs: []}
-    this.actors = new Map()          // key -> actorId
+    this.actors = new KeyTable(opts && opts.hash)
     this.updateQ = new Channel('cursorstore:updateQ')
+    this.writes = []
   }
+
+  // The Cursors upserts since the last call, for one SQL transaction (INTEGRATION.md §3):
+  // ['upsert', repoId, docId, actorId, boundedSeq] per entry handed to update, in order — the
+  // statements src/CursorStore.ts:51-64 runs, batched across calls.
+  takeBatch() { const b = this.writes; this.writes = []; return b }
 
   table(repoId) {
     let t = this.tables.get(repoId)
@@ -809,7 +835,7 @@ class CursorStore {
     return r
   }
 
-  key(actorId) { const k = fnv1a64(actorId); this.actors.set(k, actorId); return k }
+  key(actorId) { return this.actors.key(actorId) }
 
   getMany(repoId, docIds) {
     const t = this.table(repoId)
@@ -822,7 +848,7 @@ class CursorStore {
         const ent = []
         for (let e = 0; e < n; e++) {
           const o = 8 * (i * this.K + e)
-          ent.push([this.actors.get(g.actors.readBigUInt64LE(o)), Number(g.seqs.readBigUInt64LE(o))])
+          ent.push([this.actors.id(g.actors.readBigUInt64LE(o)), Number(g.seqs.readBigUInt64LE(o))])
         }
         ent.sort((a, b) => byteOrder(a[0], b[0]))            // SELECT * in primary-key order
         out.set(d, Object.fromEntries(ent))
@@ -842,6 +868,10 @@ class CursorStore {
     docs.forEach((d, i) => {
       for (const [a, s] of Object.entries(cursors[d])) { keys.push(this.key(a)); seqs.push(s) }
       off[i + 1] = keys.length
+    })
+    docs.forEach((d) => {
+      for (const [a, s] of Object.entries(cursors[d]))
+        this.writes.push(['upsert', repoId, d, a, Math.max(0, Math.min(s, INFINITY_SEQ))])
     })
     const rows = Uint32Array.from(docs, (d) => this.row(t, d))
     const differs = addon.cursorsUpdate(t.c, rows, off, BigUint64Array.from(keys), Float64Array.from(seqs))
@@ -917,5 +947,5 @@ function syncPlan(engine, cursors, repoId, actors, docs, present) {
   return hits.map(([d, a], i) => [d, a, lo[i], end.readUInt32LE(4 * i)]).sort((x, y) => byteOrder(x[0] + '\0' + x[1], y[0] + '\0' + y[1]))
 }
 
-module.exports = { GpuEngine, GpuBackendState, DocBackend, ClockStore, CursorStore, syncPlan, makeBackend, materialize,
-  fnv1a64, addon, toChange, decodeRound }
+module.exports = { GpuEngine, GpuBackendState, DocBackend, ClockStore, CursorStore, KeyTable, syncPlan, makeBackend,
+  materialize, fnv1a64, addon, toChange, decodeRound }

@@ -428,6 +428,28 @@ class RowStore(DocStore):
         self._pending = (bid.value, len(hs), None, keep)
         return bid.value
 
+    def submit_device(self, n_docs: int, counts, docs, changes, deps, ops, handles) -> int:
+        """hm_batch_submit_device: the batch's tables and handles already in HBM (torch tensors or
+        device pointers, read in place until wait_device returns); counts = (n_changes, n_deps, n_ops)."""
+        ptr = [int(getattr(t, "data_ptr", lambda: t)()) for t in (docs, changes, deps, ops, handles)]
+        cb = CBatch(n_docs, int(counts[0]), int(counts[1]), int(counts[2]), 0, self.S, 0, 0, 0, 0, 0, 0,
+                    ptr[0], ptr[1], ptr[2], ptr[3], None)
+        bid = ctypes.c_uint64()
+        self._check(self._L.hm_batch_submit_device(self._h, ctypes.byref(cb), ctypes.c_void_p(ptr[4]), None,
+                                                   ctypes.byref(bid)), "hm_batch_submit_device")
+        self._pending = (bid.value, n_docs, None, (docs, changes, deps, ops, handles))
+        return bid.value
+
+    def wait_device(self, out) -> int:
+        """hm_batch_wait_device: the gathered result rows into device memory `out` (a torch tensor of at
+        least n * (32 + 12 * a_stride) bytes); returns the number of rows whose status is not OK."""
+        bid, n, _, _ = self._pending
+        self._pending = None
+        nf = ctypes.c_uint32()
+        self._check(self._L.hm_batch_wait_device(self._h, ctypes.c_uint64(bid), ctypes.c_void_p(int(out.data_ptr())),
+                                                 ctypes.byref(nf)), "hm_batch_wait_device")
+        return nf.value
+
     def wait(self, out: Optional[BatchResult] = None) -> BatchResult:
         """Results of the submitted batch; `out` (arrays of at least the batch's size, e.g. kept
         between rounds by a long-running host) is filled instead of fresh arrays."""

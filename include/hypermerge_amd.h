@@ -311,11 +311,34 @@ int hm_batch_submit(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
 int hm_batch_wait(hm_store *s, uint64_t batch_id, hm_doc_result *out_docs,
                   uint32_t *out_clock, uint32_t *out_back_clock, uint32_t *out_heads);
 
+/* hm_batch_submit with the batch already in HBM: b->docs / changes / deps / ops, doc_handles
+ * and actor_remap are device pointers on the store's device (counts in b as usual), read
+ * in place — they must stay unchanged until the batch's wait returns.  (A host that decodes
+ * blocks into device buffers on a copy stream, or a GPU producer, hands rows over without a
+ * host round trip.) */
+int hm_batch_submit_device(hm_store *s, const hm_batch *b, const uint32_t *doc_handles,
+                           const uint8_t *actor_remap, uint64_t *out_batch_id);
+
+/* Wait for a batch and leave its results on the device: out_dev (device memory) receives
+ * [n_docs hm_doc_result][n_docs*a_stride clock][n_docs*a_stride back_clock][n_docs*a_stride heads]
+ * by one device-to-device copy; out_n_failed (optional, host) = rows whose status is not OK
+ * (those documents are rolled back before this returns, as in hm_batch_wait). */
+int hm_batch_wait_device(hm_store *s, uint64_t batch_id, void *out_dev, uint32_t *out_n_failed);
+
+/* Undo the last waited batch: every document of it back to its log and state before the
+ * submit (its new rows dropped, actor ranks mapped back, the previous state re-merged), as if
+ * the batch had thrown for all of them.  Only the last batch waited for, and only until the
+ * store's next submit.  (The docset undoes the batches of a call whose later step failed, so a
+ * call is applied to every store or to none.) */
+int hm_batch_undo(hm_store *s, uint64_t batch_id);
+
 /* Incremental applyRemoteChanges (on by default): a document whose new changes are each
  * causally ready in arrival order on its resident state (nothing queued, no actor re-rank,
- * map set/del/link ops, small submits) is advanced in place — history, allDeps, heads and
- * clock appended, only the registers its new ops hit recomputed — instead of re-merging
- * its whole log.  Results are identical either way; off = always re-merge. */
+ * map set/del/link/inc ops, small submits) is advanced in place — history, allDeps, heads and
+ * clock appended, only the registers its new ops hit read and rewritten — instead of
+ * re-merging its whole log.  Results are identical either way; off = always re-merge.
+ * (A register's survivors may then sit anywhere in its document's op segment; hm_doc_read
+ * hands them out packed, as a merge writes them.) */
 int hm_store_set_incremental(hm_store *s, int on);
 /* Routing of the last submit: out3 = {incremental, re-merged, incremental handed back to
  * the re-merge}. */

@@ -118,6 +118,39 @@ def test_docset_errors_roll_back():
     assert ds.view(d) == ds.view(d + 1)
 
 
+@pytest.mark.parametrize("where", ["wait:1", "read"])
+def test_docset_failed_call_is_undone_everywhere(where, monkeypatch):
+    """A call whose documents live in two store classes fails after the first class's batch was
+    applied (wait:1: after the second class's; read: after both, before the patch reads): the
+    batches already applied are undone (hm_batch_undo) and every document's host state rolls back,
+    so the store and the host agree and the same round applies cleanly afterwards."""
+    from hypermerge_amd.columnar import ROOT_ID as R
+    from hypermerge_amd.docset import DocSet, render_objects, view_objects
+    from hypermerge_amd.engine import Engine, EngineError
+    ds = DocSet(Engine(0))
+    d = ds.open(2)
+    narrow = [{"actor": f"n{i}", "seq": 1, "deps": {}, "ops": [{"action": "set", "obj": R, "key": "k", "value": i}]}
+              for i in range(3)]
+    wide = [{"actor": f"w{i:02d}", "seq": 1, "deps": {}, "ops": [{"action": "set", "obj": R, "key": f"k{i % 3}", "value": i}]}
+            for i in range(12)]                                  # 12 actors: the 16-wide class
+    ds.apply([d, d + 1], [_blocks(narrow[:2]), _blocks(wide[:10])])
+    info0, view0 = [ds.info(x) for x in (d, d + 1)], [ds.view(x) for x in (d, d + 1)]
+    r2 = [narrow[2:] + [{"actor": "n0", "seq": 2, "deps": {"n1": 1, "n2": 1}, "ops": [{"action": "del", "obj": R, "key": "k"}]}],
+          wide[10:] + [{"actor": "w00", "seq": 2, "deps": {"w05": 1}, "ops": [{"action": "set", "obj": R, "key": "k1", "value": 7}]}]]
+    monkeypatch.setenv("HM_DOCSET_INJECT_FAIL", where)
+    with pytest.raises(EngineError):
+        ds.apply([d, d + 1], [_blocks(r2[0]), _blocks(r2[1])])
+    monkeypatch.delenv("HM_DOCSET_INJECT_FAIL")
+    assert [ds.info(x) for x in (d, d + 1)] == info0
+    assert [ds.view(x) for x in (d, d + 1)] == view0
+    res, js = ds.apply([d, d + 1], [_blocks(r2[0]), _blocks(r2[1])])
+    assert (res["status"] == 0).all()
+    for k, (x, log) in enumerate(((d, narrow + r2[0][1:]), (d + 1, wide + r2[1][2:]))):
+        s = _oracle(log)
+        assert js["p"][k]["clock"] == s["clock"] and js["b"][k] == s["backend_clock"]
+        assert render_objects(view_objects(ds.view(x))) == json.loads(json.dumps(s["state"]))
+
+
 def test_docset_moves_documents_to_wider_stores():
     """Documents whose actors outgrow 8 / 16 / 32 move to the wider store class with their
     whole log; the merged state equals the oracle's, patches included."""

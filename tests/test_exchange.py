@@ -214,3 +214,28 @@ def test_align_counts_held_documents_without_records():
     own2 = allr[:1].copy()
     _, mine = align(allr, own2, held=np.array([1, 7], np.uint64))
     assert list(mine) == [3, 0]
+
+
+def test_key_collisions_fail_loudly():
+    """The 64-bit keys stand for id strings; two ids on one key (forced here with a key
+    function that collides) raise instead of merging two actors' clocks or cursors — in a
+    rank's own table, when tables meet across ranks, and in the dense rows of an exchange."""
+    import pytest
+    from hypermerge_amd import exchange as X
+    weak = lambda s: len(s)                                  # noqa: E731  every id of one length collides
+    t = X.KeyTable(weak)
+    assert t.key("actorA") == t.key("actorA")
+    with pytest.raises(ValueError, match="collision"):
+        t.key("actorB")
+    other = X.KeyTable(weak)
+    other.key("docXY")
+    mine = X.KeyTable(weak)
+    mine.key("docZW")
+    with pytest.raises(ValueError, match="collision"):
+        mine.update(other.ids)
+    with pytest.raises(ValueError, match="collision"):
+        X.dense_rows([("docA", {"ab": 1, "cd": 2})], 4, X.KeyTable(weak))
+    # the real key function keeps distinct ids apart
+    real = X.KeyTable()
+    ids = [f"actor{i}" for i in range(2000)]
+    assert len({real.key(a) for a in ids}) == len(ids)

@@ -125,3 +125,51 @@ console.log(JSON.stringify({ same: hex(first) === hex(again), t0, t1, t2, remap:
     assert json.loads(got["t0"]) == [["mm"], [ROOT_ID], [[0, "x"]], 1]
     assert got["remap"] == [1]
     assert got["cids"] == [1, 2, 0]          # aa:1 new, mm:1 with new content new, mm:1 as before = class 0
+
+
+# the persistence side's own statements (a restatement: one table keyed like the reference's
+# Clocks, the upsert-max it runs per entry); the expected tables come from the reference SQL
+_CLOCKS = ("CREATE TABLE Clocks (repoId TEXT NOT NULL, documentId TEXT NOT NULL, actorId TEXT NOT NULL, "
+           "seq INTEGER NOT NULL, PRIMARY KEY (repoId, documentId, actorId)) WITHOUT ROWID")
+_UPSERT = ("INSERT INTO Clocks (repoId, documentId, actorId, seq) VALUES (?, ?, ?, ?) ON CONFLICT (repoId, documentId, "
+           "actorId) DO UPDATE SET seq = excluded.seq WHERE excluded.seq > seq")
+_DELETE = "DELETE FROM Clocks WHERE repoId = ? AND documentId = ?"
+
+
+def apply_batch(db, batch):
+    """One round's ClockStore.takeBatch() rows in one transaction."""
+    with db:
+        for row in batch:
+            if row[0] == "upsert":
+                db.execute(_UPSERT, tuple(row[1:]))
+            else:
+                db.execute(_DELETE, tuple(row[1:]))
+
+
+def test_clockstore_batches_replay_to_reference_tables():
+    """Row f3: every round's ClockStore writes leave as ONE batch (takeBatch), replayed in one
+    sqlite3 transaction; after each round the table equals the reference SQL's after the same
+    update / set calls (tests/golden/clockstore_batches.json).  A colliding 64-bit key throws."""
+    import sqlite3
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "clockstore_batches.json")))
+    p = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "run_persist.js")],
+                       input=json.dumps({"rounds": gold["rounds"], "docs": gold["docs"]}),
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    got = json.loads(p.stdout)
+    db = sqlite3.connect(":memory:")
+    db.execute(_CLOCKS)
+    n_rows = 0
+    for r, (batch, want) in enumerate(zip(got["batches"], gold["tables"])):
+        apply_batch(db, batch)
+        n_rows += len(batch)
+        table = [list(x) for x in db.execute(
+            "SELECT repoId, documentId, actorId, seq FROM Clocks ORDER BY repoId, documentId, actorId").fetchall()]
+        assert table == want, r
+    assert n_rows < sum(len(c[3]) for rd in gold["rounds"] for c in rd)      # only the rows that changed
+    last = {(a, b): [] for a, b in gold["docs"]}
+    for rp, d, a, s in gold["tables"][-1]:
+        last[(rp, d)].append([a, s])
+    for (rp, d), g in zip(gold["docs"], got["get"]):
+        assert sorted(g) == sorted(last[(rp, d)]), (rp, d)
+    assert got["collision"] and "collision" in got["collision"] and '"actorA"' in got["collision"]

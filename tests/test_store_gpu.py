@@ -196,17 +196,20 @@ def test_bad_remap_leaves_store_unchanged(engine):
     assert_doc_matches_oracle(store, hs[0])
 
 
-@pytest.mark.parametrize("name,n,extra,hi,expect_inc", [
-    ("C4", 300, {}, 2, 0.9),                               # generation order: every arrival applies at once
-    ("C4", 300, {"arrival": 1}, 3, True),                  # actor-major: some arrivals wait -> re-merge
-    ("C2", 200, {}, 2, 0.9),                               # counter sets and incs applied incrementally
-    ("C5", 150, {}, 2, False),                             # lists / nested objects / duplicates: re-merge
-    ("C1", 1, {"changes_per_actor": 300}, 4, True),        # one long two-actor document
-    ("FC", 60, {}, 2, True),                               # integral and f64 counters, shuffled (queued) arrivals
+@pytest.mark.parametrize("name,n,extra,hi,expect_inc,S", [
+    ("C4", 300, {}, 2, 0.9, 8),                            # generation order: every arrival applies at once
+    ("C4", 300, {"arrival": 1}, 3, True, 8),               # actor-major: some arrivals wait -> re-merge
+    ("C2", 200, {}, 2, 0.9, 8),                            # counter sets and incs applied incrementally
+    ("C5", 150, {}, 2, False, 8),                          # lists / nested objects / duplicates: re-merge
+    ("C1", 1, {"changes_per_actor": 300}, 4, True, 8),     # one long two-actor document
+    ("FC", 60, {}, 2, True, 8),                            # integral and f64 counters, shuffled (queued) arrivals
+    ("C4", 200, {}, 6, 0.9, 16),                           # 16 lanes per document (inc_group_kernel<16>)
+    ("C2", 120, {}, 8, 0.9, 64),                           # one document per wave (inc_group_kernel<64>)
+    ("C4", 200, {}, 8, 0.9, 8),                            # up to 8 changes per call: some documents handed to the wave kernel
 ])
-def test_incremental_apply_equals_full_remerge(engine, name, n, extra, hi, expect_inc):
+def test_incremental_apply_equals_full_remerge(engine, name, n, extra, hi, expect_inc, S):
     """applyRemoteChanges with 1..hi new changes per document per call
-    (src/DocBackend.ts:169-185): the incremental path (inc_apply_kernel) and the whole-log
+    (src/DocBackend.ts:169-185): the incremental path (inc_group_kernel) and the whole-log
     re-merge give identical per-call results and device state, and sampled documents are
     bit-exact with the oracle's cold merge of their log after every call."""
     if name == "FC":
@@ -216,7 +219,7 @@ def test_incremental_apply_equals_full_remerge(engine, name, n, extra, hi, expec
         b = synth.generate(synth.config(name, n_docs=n, **extra))
         docs = [decode_doc(b, i) for i in range(b.n_docs)]
     rng = np.random.default_rng(11)
-    A, B = DocStore(engine, a_stride=8), DocStore(engine, a_stride=8)
+    A, B = DocStore(engine, a_stride=S), DocStore(engine, a_stride=S)
     B.set_incremental(False)
     ha = [A.open() for _ in docs]
     hb = [B.open() for _ in docs]
@@ -258,3 +261,116 @@ def test_incremental_apply_equals_full_remerge(engine, name, n, extra, hi, expec
     if isinstance(expect_inc, float):           # the share of calls applied incrementally
         assert routed["incremental"] >= expect_inc * sum(routed.values()), routed
     print(name, extra, routed)
+
+
+def _growing_conflicts(n_cycles, actors=("a1", "a2", "a3", "a4", "a5", "a6", "a7", "a8")):
+    """One register that repeatedly goes from one survivor to eight: each cycle starts with a
+    set that has seen everything (the list shrinks to one, in place), then the other actors set
+    it concurrently one after another, each having seen only its own chain (the list grows by
+    one per set: every growth moves the list to the end of the document's survivor slots)."""
+    seq = {a: 0 for a in actors}
+    out = []
+    for c in range(n_cycles):
+        lead = actors[c % len(actors)]
+        seq[lead] += 1
+        out.append(ch(lead, seq[lead], {a: q for a, q in seq.items() if a != lead and q}, s("k", c * 100)))
+        for a in actors:
+            if a == lead:
+                continue
+            seq[a] += 1
+            deps = {lead: seq[lead]} if a != lead else {}
+            out.append(ch(a, seq[a], deps, s("k", c * 100 + len(out) % 97), s(f"x{len(out)}", a)))
+    return out
+
+
+def test_survivor_slots_run_out_and_repack(engine):
+    """Lists that grow faster than the op log fill a document's survivor slots: the incremental
+    path then hands the document to the re-merge (which packs its survivors again) and goes on
+    incrementally; every call equals the re-merge store and the oracle."""
+    log = _growing_conflicts(12)
+    A, B = DocStore(engine, a_stride=8), DocStore(engine, a_stride=8)
+    B.set_incremental(False)
+    ha, hb = A.open(), B.open()
+    routed = {"incremental": 0, "remerged": 0, "handed_back": 0}
+    for i in range(0, len(log), 1):
+        ra, rb = A.apply([(ha, log[i:i + 1])]), B.apply([(hb, log[i:i + 1])])
+        for k, v in A.last_routing().items():
+            routed[k] += v
+        for f in ("docs", "clock", "back_clock", "heads"):
+            np.testing.assert_array_equal(getattr(ra, f), getattr(rb, f), err_msg=f"{f} call {i}")
+        if i % 9 == 0:
+            assert_doc_matches_oracle(A, ha)
+    assert_doc_matches_oracle(A, ha)
+    assert routed["incremental"] > len(log) // 2 and routed["handed_back"] > 0, routed
+
+
+def test_batch_undo_restores_previous_state(engine):
+    """hm_batch_undo: every document of the last waited batch back to its state before it
+    (incremental and re-merged documents alike); the next batch merges on top of that."""
+    b = synth.generate(synth.config("C4", n_docs=60))
+    docs = [decode_doc(b, i) for i in range(b.n_docs)]
+    store = DocStore(engine, a_stride=8)
+    hs = [store.open() for _ in docs]
+    store.apply([(h, docs[i][:40]) for i, h in enumerate(hs)])
+    before = [canonical_json(*store.read(h), 0) for h in hs]
+    snaps = [store.enc[h].snapshot() for h in hs]
+    store.submit([(h, docs[i][40:43]) for i, h in enumerate(hs)])
+    bid = store._pending[0]
+    r = store.wait()
+    assert (r.docs["status"] == 0).all()
+    store._check(store._L.hm_batch_undo(store._h, bid), "hm_batch_undo")
+    for i, h in enumerate(hs):
+        store.enc[h].restore(snaps[i])
+        assert canonical_json(*store.read(h), 0) == before[i], i
+    assert store._L.hm_batch_undo(store._h, bid) != 0                      # once only
+    store.apply([(h, docs[i][40:]) for i, h in enumerate(hs)])
+    cold = encode(docs, 8)
+    co = O.merge(cold)
+    for i in range(0, len(hs), 7):
+        bb, g = assert_doc_matches_oracle(store, hs[i])
+        assert canonical_json(bb, g, 0) == canonical_json(cold, co, i)
+
+
+def test_device_submit_equals_host_submit(engine):
+    """hm_batch_submit_device / hm_batch_wait_device (rows already in HBM) give the host entry
+    points' results and state."""
+    import torch
+    from hypermerge_amd.store import RowStore, slice_changes
+    b = synth.generate(synth.config("C4", n_docs=500))
+    n, S = b.n_docs, b.a_stride
+    nch = b.docs["n_changes"].astype(np.int64)
+    dev = torch.device("cuda", 0)
+    A, B = RowStore(engine, a_stride=S), RowStore(engine, a_stride=S)
+    ha, hb = A.open_n(n), B.open_n(n)
+
+    def on_dev(x, hs):
+        return (len(x.changes), len(x.deps), len(x.ops)), [
+            torch.from_numpy(np.ascontiguousarray(y).view(np.uint8).reshape(-1)).to(dev)
+            for y in (x.docs, x.changes, x.deps, x.ops, np.ascontiguousarray(hs, np.uint32))]
+    pos = np.zeros(n, np.int64)
+    rng = np.random.default_rng(3)
+    out = torch.empty(n * (32 + 12 * S), dtype=torch.uint8, device=dev)
+    first = True
+    while (pos < nch).any():
+        hi = np.minimum(pos + (40 if first else rng.integers(1, 4, n)), nch)
+        first = False
+        sel = np.nonzero(hi > pos)[0]
+        sub = slice_changes(b, pos, hi, sel)
+        A.submit_batch(sub, sel + ha)
+        ra = A.wait()
+        cnt, t = on_dev(sub, sel + hb)
+        assert B.submit_device(len(sel), cnt, *t) > 0
+        assert B.wait_device(out) == 0
+        got = out[:len(sel) * (32 + 12 * S)].cpu().numpy()
+        k = len(sel)
+        np.testing.assert_array_equal(got[:k * 32].view(ra.docs.dtype), ra.docs)
+        rows = got[k * 32:].view(np.uint32).reshape(3, k, S)
+        np.testing.assert_array_equal(rows[0], ra.clock)
+        np.testing.assert_array_equal(rows[1], ra.back_clock)
+        np.testing.assert_array_equal(rows[2], ra.heads)
+        pos = np.maximum(pos, hi)
+    for i in range(0, n, 37):
+        _, ga = A.read(ha + i)
+        _, gb = B.read(hb + i)
+        for f in ("hist", "all_deps", "regs", "surv", "clock", "heads"):
+            np.testing.assert_array_equal(getattr(ga, f), getattr(gb, f), err_msg=f)
