@@ -10,6 +10,7 @@ one launch each."""
 from __future__ import annotations
 
 import ctypes
+import sys
 from typing import Dict, List, Mapping, Optional, Sequence, Tuple
 
 import numpy as np
@@ -69,6 +70,10 @@ class CursorStore:
             t.close()
 
     def __del__(self):
+        # (at interpreter exit finalizers run in any order: the engine may be gone, and the
+        # process releases the device anyway)
+        if sys.is_finalizing():
+            return
         try:
             self.close()
         except Exception:

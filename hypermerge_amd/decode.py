@@ -4,6 +4,7 @@ src/Actor.ts:137-141) and the host encoder's rows, multi-threaded over documents
 from __future__ import annotations
 
 import ctypes
+import sys
 from typing import List, Sequence, Tuple
 
 import numpy as np
@@ -77,7 +78,7 @@ class _Decoded:
         self.L, self.h = L, h
 
     def __del__(self):
-        if self.h:
+        if self.h and not sys.is_finalizing():
             self.L.hm_decoded_free(self.h)
             self.h = None
 

@@ -6,6 +6,7 @@ Used by the Python tests; the production caller is the N-API addon (js/hmgpu_nod
 from __future__ import annotations
 
 import ctypes
+import sys
 import json
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -55,6 +56,10 @@ class DocSet:
             self._h = None
 
     def __del__(self):
+        # (at interpreter exit finalizers run in any order: the engine may be gone, and the
+        # process releases the device anyway)
+        if sys.is_finalizing():
+            return
         try:
             self.close()
         except Exception:

@@ -7,6 +7,7 @@ This is the Python face of the boundary; the Node face is hypermerge_amd/js
 from __future__ import annotations
 
 import ctypes
+import sys
 import os
 from typing import Optional, Sequence
 
@@ -157,6 +158,10 @@ class Engine:
             self._h = None
 
     def __del__(self):
+        # (at interpreter exit finalizers run in any order: the engine may be gone, and the
+        # process releases the device anyway)
+        if sys.is_finalizing():
+            return
         try:
             self.close()
         except Exception:

@@ -13,6 +13,7 @@ ids they were first given.
 from __future__ import annotations
 
 import ctypes
+import sys
 from dataclasses import dataclass
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -213,10 +214,15 @@ class DocStore:
 
     def close(self) -> None:
         if getattr(self, "_h", None):
-            self._L.hm_store_destroy(self._h)
+            if getattr(self.engine, "_h", None):               # (the store lives on its engine's stream)
+                self._L.hm_store_destroy(self._h)
             self._h = None
 
     def __del__(self):
+        # (at interpreter exit finalizers run in any order: the engine may be gone, and the
+        # process releases the device anyway)
+        if sys.is_finalizing():
+            return
         try:
             self.close()
         except Exception:
@@ -318,10 +324,11 @@ class DocStore:
         return {f: getattr(i, f) for f, _ in _DocInfo._fields_}
 
     def read(self, h: int) -> Tuple[Batch, Results]:
-        """The document's log and merged state as a one-document (Batch, Results)."""
+        """The document's log and merged state as a one-document (Batch, Results); the Batch is
+        None for a store fed prebuilt rows (RowStore: no host encoder keeps the log)."""
         inf = self.info(h)
         S = self.S
-        b = self.enc[h].log_batch(S)
+        b = self.enc[h].log_batch(S) if h < len(self.enc) else None
         r = Results(np.zeros(1, DOC_RESULT_DT), np.zeros(S, np.uint32), np.zeros(S, np.uint32),
                     np.zeros(S, np.uint32), np.zeros(inf["n_changes"], np.int32),
                     np.zeros(inf["n_changes"] * S, np.uint32), np.zeros(inf["n_regs"], REG_RESULT_DT),
