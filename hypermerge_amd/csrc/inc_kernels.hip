@@ -78,6 +78,22 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
     const uint32_t S = A.S, h = D.handle, NA = D.n_actors, nnc = D.n_new_c, nno = D.n_new_o, nnd = D.n_new_d;
     constexpr int FAILG = G < 64 ? INC_DEFER : INC_BAIL;     // a limit of this group size only
     constexpr uint32_t KT = G >= 32 ? 1u : 32u / G;           // the log's last KT * G rows are searched first
+    // the new rows, from the submit's staged tables (batch-local offsets): a document whose
+    // segments did not move gets them appended here (append_kernel skips it), rebased — before
+    // anything can hand the document over, since the re-merge reads them from the log
+    const bool moved = D.src_c != D.dst_c || D.src_d != D.dst_d || D.src_o != D.dst_o;
+    if (!moved) {
+        for (uint32_t i = gl; i < nnc; i += G) {
+            hm_change_row c = A.st_changes[D.new_c + i];
+            c.dep_off = D.dst_d + D.n_old_d + (c.dep_off - D.new_d);
+            c.op_first = D.dst_o + D.n_old_o + (c.op_first - D.new_o);
+            A.changes[D.dst_c + D.n_old_c + i] = c;
+        }
+        for (uint32_t i = gl; i < nnd; i += G) A.deps[D.dst_d + D.n_old_d + i] = A.st_deps[D.new_d + i];
+        const uint4 *so4 = reinterpret_cast<const uint4 *>(A.st_ops + D.new_o);
+        uint4 *do4 = reinterpret_cast<uint4 *>(A.ops + D.dst_o + D.n_old_o);
+        for (uint32_t i = gl; i < 2 * nno; i += G) do4[i] = so4[i];
+    }
     if (nnc == 0 || nnc > NC || NA > S || S > G || D.n_old_r > D.n_r) return INC_BAIL;
     if (nno > G || nnd > G) return FAILG;
 
@@ -92,35 +108,32 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
     }
     uint32_t ca = 0, cq = 0, cnd = 0, cdo = 0, cno = 0, coo = 0;
     if (gl < nnc) {
-        const hm_change_row c = A.changes[D.dst_c + D.n_old_c + gl];
-        ca = c.actor; cq = c.seq; cnd = c.n_deps; cdo = c.dep_off - D.dst_d; cno = c.n_ops; coo = c.op_first - D.dst_o;
+        const hm_change_row c = A.st_changes[D.new_c + gl];
+        ca = c.actor; cq = c.seq; cnd = c.n_deps; cdo = c.dep_off - D.new_d; cno = c.n_ops; coo = c.op_first - D.new_o;
     }
     uint32_t o_act = 0, o_dt = 0, o_obj = 0, o_reg = 0xFFFFFFFFu, o_vt = 0, o_vlo = 0, o_vhi = 0;
     if (gl < nno) {
-        const hm_op_row op = A.ops[D.dst_o + D.n_old_o + gl];
-        o_act = op.action; o_dt = op.datatype; o_obj = op.obj; o_reg = op.reg; o_vt = op.vtag;
-        o_vlo = (uint32_t)op.value; o_vhi = (uint32_t)(op.value >> 32);
+        const uint4 *src = reinterpret_cast<const uint4 *>(A.st_ops + D.new_o + gl);
+        const uint4 w0 = src[0], w1 = src[1];
+        // hm_op_row: obj, reg, parent, elem | action, datatype, vtag, pad, key, value lo, value hi
+        o_obj = w0.x; o_reg = w0.y;
+        o_act = w1.x & 0xFFu; o_dt = (w1.x >> 8) & 0xFFu; o_vt = (w1.x >> 16) & 0xFFu;
+        o_vlo = w1.z; o_vhi = w1.w;
     }
     uint32_t dpa = 0, dpq = 0;
     if (gl < nnd) {
-        const hm_dep_row d = A.deps[D.dst_d + D.n_old_d + gl];
+        const hm_dep_row d = A.st_deps[D.new_d + gl];
         dpa = d.actor; dpq = d.seq;
     }
-    // the log's last rows, newest first: (actor, seq) and the history position (an applied
-    // change has one; duplicates and queued copies do not)
-    uint32_t tka[KT], tkq[KT];
-    int32_t tkh[KT];
+    // the log's last rows, newest first, as packed (actor, seq, applied) keys: the applied copy of a
+    // change is the one a fold finds (duplicates and queued copies are not applied)
+    uint32_t tk[KT];
 #pragma unroll
     for (uint32_t k = 0; k < KT; k++) {
         const int idx = (int)D.n_old_c - 1 - (int)(k * G + gl);
-        tka[k] = 0xFFFFFFFFu; tkq[k] = 0; tkh[k] = -1;
-        if (idx >= 0) {
-            const uint2 w = *reinterpret_cast<const uint2 *>(A.changes + D.dst_c + idx);
-            tka[k] = w.x & 0xFFFFu; tkq[k] = w.y;
-            tkh[k] = A.hist[D.src_c + idx];
-        }
+        tk[k] = idx >= 0 ? A.ckey[D.src_c + idx] : 0u;
     }
-    if (!(I.flags & HM_IST_VALID)) return INC_BAIL;
+    if ((I.flags & (HM_IST_VALID | HM_IST_NOCKEY)) != HM_IST_VALID) return INC_BAIL;
 
     // ---- the new rows: grouped by change, in order, after the old rows; supported ops ----
     uint32_t sd = gl < nnc ? cnd : 0u, so = gl < nnc ? cno : 0u;
@@ -131,7 +144,7 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
     }
     const uint32_t xd = sd - (gl < nnc ? cnd : 0u), xo = so - (gl < nnc ? cno : 0u);
     const uint32_t total_d = g.sh(sd, nnc - 1), total_o = g.sh(so, nnc - 1);
-    const bool bad_c = gl < nnc && (ca >= NA || cq == 0 || cdo != D.n_old_d + xd || coo != D.n_old_o + xo);
+    const bool bad_c = gl < nnc && (ca >= NA || cq == 0 || cq >= (1u << 24) || cdo != xd || coo != xo);
     const int64_t oval = (int64_t)(((uint64_t)o_vhi << 32) | o_vlo);
     const bool bad_o = gl < nno && ((o_act != HM_SET && o_act != HM_DEL && o_act != HM_LINK && o_act != HM_INC) ||
                                     (o_act == HM_INC && o_vt != HM_V_INT && o_vt != HM_V_FLOAT) ||
@@ -193,20 +206,16 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
         const uint32_t w = g.sh(t < (uint32_t)G ? tA0 : tA1, tl);
         if ((w >> 8) & 0xFFu) continue;                        // a change of this submit
         const uint32_t da = w & 0xFFu, dq = g.sh(t < (uint32_t)G ? tQ0 : tQ1, tl);
+        const uint32_t want = hm_ckey(da, dq, true);
         int found = -1;
 #pragma unroll
         for (uint32_t k = 0; k < KT; k++) {
-            const uint64_t m = g.bits(tka[k] == da && tkq[k] == dq && tkh[k] >= 0);
+            const uint64_t m = g.bits(tk[k] == want);
             if (m && found < 0) found = (int)D.n_old_c - 1 - (int)(k * G + (uint32_t)__builtin_ctzll(m));
         }
         for (int top = (int)D.n_old_c - 1 - (int)(KT * G); found < 0 && top >= 0; top -= G) {
             const int idx = top - (int)gl;
-            bool hit = false;
-            if (idx >= 0) {
-                const uint2 kw = *reinterpret_cast<const uint2 *>(A.changes + D.dst_c + idx);
-                hit = (kw.x & 0xFFFFu) == da && kw.y == dq && A.hist[D.src_c + idx] >= 0;
-            }
-            const uint64_t m = g.bits(hit);
+            const uint64_t m = g.bits(idx >= 0 && A.ckey[D.src_c + idx] == want);
             if (m) found = top - (int)__builtin_ctzll(m);
         }
         if (found < 0) return INC_BAIL;
@@ -294,7 +303,7 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
     // segment doubles)
     const bool mv = D.src_c != D.dst_c || D.src_o != D.dst_o || D.src_r != D.dst_r;
     if (D.src_c != D.dst_c) {
-        for (uint32_t i = gl; i < D.n_old_c; i += G) A.hist[D.dst_c + i] = A.hist[D.src_c + i];
+        for (uint32_t i = gl; i < D.n_old_c; i += G) { A.hist[D.dst_c + i] = A.hist[D.src_c + i]; A.ckey[D.dst_c + i] = A.ckey[D.src_c + i]; }
         for (size_t w = gl; w < (size_t)D.n_old_c * S; w += G) A.all_deps[(size_t)D.dst_c * S + w] = A.all_deps[(size_t)D.src_c * S + w];
     }
     if (D.src_o != D.dst_o)
@@ -398,7 +407,10 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
     }
 
     // ---- history, allDeps, clocks, the document's result row and IncState ----
-    if (gl < nnc) A.hist[D.dst_c + D.n_old_c + gl] = (int32_t)(R0.hist_len + gl);
+    if (gl < nnc) {
+        A.hist[D.dst_c + D.n_old_c + gl] = (int32_t)(R0.hist_len + gl);
+        A.ckey[D.dst_c + D.n_old_c + gl] = hm_ckey(ca, cq, true);
+    }
     if (gl < S) {
 #pragma unroll
         for (uint32_t j = 0; j < NC; j++)
@@ -446,8 +458,8 @@ __global__ __launch_bounds__(256) void inc_group_kernel(IncArgs A) {
 // (an error, queued changes) get flags = 0: their next submit re-merges.
 __global__ __launch_bounds__(256) void inc_meta_kernel(const uint32_t *list, uint32_t n, const DevDoc *dm,
                                                        const hm_doc_result *res_docs, const hm_change_row *changes,
-                                                       const hm_op_row *ops, const hm_surv_result *surv, uint2 *smeta,
-                                                       IncState *ist) {
+                                                       const int32_t *hist, uint32_t *ckey, const hm_op_row *ops,
+                                                       const hm_surv_result *surv, uint2 *smeta, IncState *ist) {
     const uint32_t lane = threadIdx.x & 63;
     for (uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6); q < n; q += gridDim.x * 4) {
         const uint32_t h = list[q];
@@ -469,6 +481,13 @@ __global__ __launch_bounds__(256) void inc_meta_kernel(const uint32_t *list, uin
             const uint32_t cset = (o.action == HM_SET && o.datatype == HM_DT_COUNTER) ? 0x100u : 0u;
             smeta[m.o_off + i] = make_uint2(kw.y, (kw.x & 0xFFu) | cset);
         }
+        bool wide = false;                                   // a seq the packed keys cannot hold
+        for (uint32_t i = lane; i < m.n_c; i += 64) {
+            const uint2 kw = *reinterpret_cast<const uint2 *>(changes + m.c_off + i);
+            wide |= kw.y >= (1u << 24);
+            ckey[m.c_off + i] = hm_ckey(kw.x & 0xFFFFu, kw.y, hist[m.c_off + i] >= 0);
+        }
+        wide = __ballot(wide) != 0;
         unsigned long long mask = 1ull, cabs = 0;
         for (uint32_t i = lane; i < m.n_o; i += 64) {
             const hm_op_row o = ops[m.o_off + i];
@@ -485,7 +504,7 @@ __global__ __launch_bounds__(256) void inc_meta_kernel(const uint32_t *list, uin
         }
         if (lane == 0) {
             IncState s = {};
-            s.s_used = r.n_surv; s.flags = HM_IST_VALID; s.cabs = cabs; s.mapmask = mask;
+            s.s_used = r.n_surv; s.flags = HM_IST_VALID | (wide ? HM_IST_NOCKEY : 0u); s.cabs = cabs; s.mapmask = mask;
             ist[h] = s;
         }
     }
@@ -518,10 +537,11 @@ hipError_t hm_launch_inc_apply(const IncArgs &A, hipStream_t s) {
 }
 
 hipError_t hm_launch_inc_meta(const uint32_t *list, uint32_t n, const DevDoc *dm, const hm_doc_result *res_docs,
-                              const hm_change_row *changes, const hm_op_row *ops, const hm_surv_result *surv,
-                              uint2 *smeta, IncState *ist, hipStream_t s) {
+                              const hm_change_row *changes, const int32_t *hist, uint32_t *ckey, const hm_op_row *ops,
+                              const hm_surv_result *surv, uint2 *smeta, IncState *ist, hipStream_t s) {
     if (!n) return hipSuccess;
     const uint32_t grid = (n + 3) / 4 < 65535u ? (n + 3) / 4 : 65535u;
-    hipLaunchKernelGGL(hmi::inc_meta_kernel, dim3(grid), dim3(256), 0, s, list, n, dm, res_docs, changes, ops, surv, smeta, ist);
+    hipLaunchKernelGGL(hmi::inc_meta_kernel, dim3(grid), dim3(256), 0, s, list, n, dm, res_docs, changes, hist, ckey, ops,
+                       surv, smeta, ist);
     return hipGetLastError();
 }

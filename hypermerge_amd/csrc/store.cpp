@@ -62,7 +62,7 @@ struct hm_store {
     uint32_t n_handles = 0;
     // arenas (capacity in rows); the bump pointers live in the device PlanStats
     size_t cap_c = 0, cap_d = 0, cap_o = 0, cap_r = 0;
-    hm_change_row *changes = nullptr; int32_t *hist = nullptr; uint32_t *all_deps = nullptr;
+    hm_change_row *changes = nullptr; int32_t *hist = nullptr; uint32_t *all_deps = nullptr; uint32_t *ckey = nullptr;
     hm_dep_row *deps = nullptr;
     hm_op_row *ops = nullptr; hm_surv_result *surv = nullptr; uint2 *smeta = nullptr;
     hm_reg_result *regs = nullptr;
@@ -265,7 +265,8 @@ int launch_list_merge(hm_store *s, const uint32_t *dev_list, uint32_t n) {
     rc = hm_engine_launch_merge(s->e, &b, &o, dev_list, &ext);
     // the incremental path's survivor metadata of the re-merged documents (packed survivors)
     if (rc == HM_OK && s->incremental)
-        SCHK(s, hm_launch_inc_meta(dev_list, n, s->dm, s->res_docs, s->changes, s->ops, s->surv, s->smeta, s->ist, st));
+        SCHK(s, hm_launch_inc_meta(dev_list, n, s->dm, s->res_docs, s->changes, s->hist, s->ckey, s->ops, s->surv, s->smeta,
+                                   s->ist, st));
     SCHK(s, hipStreamSynchronize(st));
     return rc;
 }
@@ -290,8 +291,9 @@ int compact(hm_store *s, size_t extra_c, size_t extra_d, size_t extra_o, size_t 
     const size_t no = std::max<size_t>(2 * live_o, 1 << 16), nr = std::max<size_t>(2 * live_r, 1 << 16);
     hm_change_row *ch; int32_t *hi; uint32_t *ad; hm_dep_row *dp; hm_op_row *op; hm_surv_result *sv; hm_reg_result *rg;
     uint2 *sm;
+    uint32_t *ck;
     int r;
-    if ((r = dev_alloc(s, &ch, nc)) || (r = dev_alloc(s, &hi, nc)) || (r = dev_alloc(s, &ad, nc * S)) ||
+    if ((r = dev_alloc(s, &ch, nc)) || (r = dev_alloc(s, &hi, nc)) || (r = dev_alloc(s, &ck, nc)) || (r = dev_alloc(s, &ad, nc * S)) ||
         (r = dev_alloc(s, &dp, nd)) || (r = dev_alloc(s, &op, no)) || (r = dev_alloc(s, &sv, no)) ||
         (r = dev_alloc(s, &sm, no)) || (r = dev_alloc(s, &rg, nr)))
         return r;
@@ -328,9 +330,9 @@ int compact(hm_store *s, size_t extra_c, size_t extra_d, size_t extra_o, size_t 
         SCHK(s, hipMemcpyAsync(s->dm, nm.data(), (size_t)n * sizeof(DevDoc), hipMemcpyHostToDevice, st));
         SCHK(s, hipStreamSynchronize(st));
     }
-    (void)hipFree(s->changes); (void)hipFree(s->hist); (void)hipFree(s->all_deps); (void)hipFree(s->deps);
+    (void)hipFree(s->changes); (void)hipFree(s->hist); (void)hipFree(s->ckey); (void)hipFree(s->all_deps); (void)hipFree(s->deps);
     (void)hipFree(s->ops); (void)hipFree(s->surv); (void)hipFree(s->smeta); (void)hipFree(s->regs);
-    s->changes = ch; s->hist = hi; s->all_deps = ad; s->deps = dp; s->ops = op; s->surv = sv; s->smeta = sm; s->regs = rg;
+    s->changes = ch; s->hist = hi; s->ckey = ck; s->all_deps = ad; s->deps = dp; s->ops = op; s->surv = sv; s->smeta = sm; s->regs = rg;
     s->cap_c = nc; s->cap_d = nd; s->cap_o = no; s->cap_r = nr;
     const unsigned long long bump[4] = {uc, ud, uo, ur};
     SCHK(s, hipMemcpyAsync(s->st->bump, bump, sizeof bump, hipMemcpyHostToDevice, st));
@@ -365,7 +367,7 @@ int hm_store_create(hm_engine *e, const hm_store_config *cfg, hm_store **out) {
 void hm_store_destroy(hm_store *s) {
     if (!s) return;
     (void)hipStreamSynchronize(hm_engine_stream(s->e));
-    void *bufs[] = {s->changes, s->hist, s->all_deps, s->deps, s->ops, s->surv, s->smeta, s->ist, s->regs, s->res_docs, s->clock,
+    void *bufs[] = {s->changes, s->hist, s->ckey, s->all_deps, s->deps, s->ops, s->surv, s->smeta, s->ist, s->regs, s->res_docs, s->clock,
                     s->back_clock, s->heads, s->min_clock, s->stored, s->stage.p, s->dm, s->seen, s->plan.p, s->descs.p,
                     s->bdescs.p, s->list.p, s->blist.p, s->remap.p, s->inv.p, s->rows.p, s->undo_handles.p, s->st};
     for (void *b : bufs) if (b) (void)hipFree(b);
@@ -486,7 +488,8 @@ static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handl
         if (P.n_inc) {
             IncArgs IA;
             IA.descs = s->descs.p; IA.n = n; IA.list = nullptr; IA.S = S;
-            IA.changes = s->changes; IA.deps = s->deps; IA.ops = s->ops; IA.hist = s->hist; IA.all_deps = s->all_deps;
+            IA.st_changes = A.changes; IA.st_deps = t_dp; IA.st_ops = t_op;
+            IA.changes = s->changes; IA.deps = s->deps; IA.ops = s->ops; IA.hist = s->hist; IA.ckey = s->ckey; IA.all_deps = s->all_deps;
             IA.regs = s->regs; IA.surv = s->surv; IA.smeta = s->smeta; IA.res_docs = s->res_docs;
             IA.clock = s->clock; IA.back_clock = s->back_clock; IA.heads = s->heads; IA.min_clock = s->min_clock;
             IA.ist = s->ist; IA.bail = bail; IA.defer = (uint32_t *)(sp + L.o_defer);

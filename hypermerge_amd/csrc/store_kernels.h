@@ -79,16 +79,27 @@ struct IncState {
 };
 static_assert(sizeof(IncState) == 32, "IncState is 32 B");
 #define HM_IST_VALID 1u
+// ckey[change slot] = seq | actor << 24 | applied << 31: the log's (actor, seq) keys packed, so the
+// incremental path finds a fold source in a few 64-byte lines instead of the 24-byte change rows
+// (documents with a seq >= 2^24 are not packed: HM_IST_NOCKEY, they re-merge)
+#define HM_IST_NOCKEY 2u
+__host__ __device__ inline uint32_t hm_ckey(uint32_t actor, uint32_t seq, bool applied) {
+    return (seq & 0xFFFFFFu) | ((actor & 0x7Fu) << 24) | (applied ? 0x80000000u : 0u);
+}
 
 struct IncArgs {
     const AppendDesc *descs;
+    const hm_change_row *st_changes;           // the submit's staged rows (batch-local offsets): the
+    const hm_dep_row *st_deps;                 // kernel appends the new rows of its documents whose
+    const hm_op_row *st_ops;                   // segments did not move (append_kernel skips those)
     uint32_t n;                                // batch rows (descs)
     const uint32_t *list;                      // NULL: every desc; else list[0] = count, list[1..] desc indices
     uint32_t S;
-    const hm_change_row *changes;
-    const hm_dep_row *deps;
-    const hm_op_row *ops;
+    hm_change_row *changes;
+    hm_dep_row *deps;
+    hm_op_row *ops;
     int32_t *hist;
+    uint32_t *ckey;
     uint32_t *all_deps;
     hm_reg_result *regs;
     hm_surv_result *surv;
@@ -146,8 +157,8 @@ hipError_t hm_launch_read_regs_h(uint32_t n, const uint32_t *handles, const uint
 hipError_t hm_launch_inc_apply(const IncArgs &A, hipStream_t s);
 // survivor metadata / IncState of re-merged documents (so the next submit can go incremental)
 hipError_t hm_launch_inc_meta(const uint32_t *list, uint32_t n, const DevDoc *dm, const hm_doc_result *res_docs,
-                              const hm_change_row *changes, const hm_op_row *ops, const hm_surv_result *surv,
-                              uint2 *smeta, IncState *ist, hipStream_t s);
+                              const hm_change_row *changes, const int32_t *hist, uint32_t *ckey, const hm_op_row *ops,
+                              const hm_surv_result *surv, uint2 *smeta, IncState *ist, hipStream_t s);
 hipError_t hm_launch_append(const AppendDesc *descs, uint32_t n_desc, const StoreArenas &src, const StoreArenas &dst,
                             const hm_change_row *st_changes, const hm_dep_row *st_deps, const hm_op_row *st_ops,
                             const uint8_t *remap, uint32_t S, hipStream_t s);

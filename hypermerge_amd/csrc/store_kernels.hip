@@ -1,6 +1,6 @@
 // store_kernels.hip — device side of the resident document store (store.cpp).
 //
-//  append_kernel        one workgroup per document of a submit: moves the document's
+//  append_kernel        one wave per document of a submit: moves the document's
 //                       log segments when they outgrow their capacity (or on arena
 //                       compaction), applies an actor-rank remap to the old rows and to
 //                       the rank-indexed per-document rows (minimumClock, stored clock),
@@ -35,6 +35,7 @@ __global__ __launch_bounds__(SWG) void append_kernel(const AppendDesc *descs, ui
     for (uint32_t di = blockIdx.x * 4 + (threadIdx.x >> 6); di < n_desc; di += gridDim.x * 4) {
         const AppendDesc D = descs[di];
         const bool moved = D.src_c != D.dst_c || D.src_d != D.dst_d || D.src_o != D.dst_o || src.changes != dst.changes;
+        if (D.inc && !moved) continue;                  // the incremental kernel appends its rows itself
         const bool rm = D.remap_row != 0xFFFFFFFFu;
         const uint8_t *mp = rm ? remap + (size_t)D.remap_row * S : nullptr;
         // old rows: moved (rebased) and/or re-ranked
