@@ -64,6 +64,7 @@ def main() -> int:
     ap.add_argument("--no-node", action="store_true",
                     help="skip the Node DocBackend leg (C2 sample: JS restatement vs the GPU drop-in)")
     ap.add_argument("--node-docs", type=int, default=20000)
+    ap.add_argument("--text-docs", type=int, default=10000, help="C3 documents in the resident text leg")
     ap.add_argument("--arrival", type=int, default=None,
                     help="override the config's arrival order (0 generation, 1 actor-major as RepoBackend.loadDocument "
                          "concatenates, 2 shuffled)")
@@ -207,8 +208,14 @@ def main() -> int:
     # applyRemoteChanges on resident documents: every document of the shard resident in the
     # store, then rounds in which each receives its next 1-2 changes (DocBackend.ts:169-185)
     incremental = None
+    incremental_text = None
     if rank == 0 and ws == 1 and not args.no_incremental and args.config == "C4" and args.arrival is None:
         incremental = _incremental(eng, batch, args)
+        # the same event on text documents (C3: RGA inserts / deletes on the resident element order)
+        c3 = synth.generate(synth.config("C3", n_docs=args.text_docs), threads=min(16, os.cpu_count() or 1))
+        incremental_text = _incremental(eng, c3, args, tail=8, oracle_docs=200)
+        incremental_text["workload"] = f"C3: {c3.n_docs} text docs x 8 actors, the last 8 changes of each in rounds of 1-2"
+        del c3
     # the Node host path end to end through the DocBackend message API (C2 sample)
     node = None
     if rank == 0 and ws == 1 and not args.no_node:
@@ -258,7 +265,7 @@ def main() -> int:
                          "kernel": kern["kernel"], "kernel_ms": kern["kernel_ms"], "alg_bytes": kern["alg_bytes"],
                          "kernels": kern["kernels"], "traffic_detail": traffic},
             "cpu_baseline": cpu, "cpu_parallel": cpu_mt, "end_to_end": e2e, "from_blocks": from_blocks,
-            "resident_incremental": incremental, "node_docbackend": node,
+            "resident_incremental": incremental, "resident_incremental_text": incremental_text, "node_docbackend": node,
             "arrival_orders": orders,
             "host": _host_info(),
             "parity_sample_ok": parity, "unsupported_docs": unsupported, "error_docs": errors,
@@ -341,7 +348,7 @@ def _node_e2e(args):
     return out
 
 
-def _incremental(eng, batch, args, tail=4):
+def _incremental(eng, batch, args, tail=4, oracle_docs=0):
     """The north-star event on resident state: every document of the shard is resident in a
     hm_store with all but its last `tail` changes; then rounds in which each document receives
     its next 1-2 changes (DocBackend.ts:169-185).  `value`: the rounds' new rows already in HBM
@@ -423,9 +430,29 @@ def _incremental(eng, batch, args, tail=4):
     t_inc = sum(r["incremental"]["ms"] for r in rounds) / 1e3
     t_rem = sum(r["remerge"]["ms"] for r in rounds) / 1e3
     t_pci = sum(r["pcie_incremental"]["ms"] for r in rounds) / 1e3
+    oracle_ok = None
+    if oracle_docs:
+        # the incremental store's documents against the oracle's cold merge of their whole logs
+        import oracle.oracle as O
+        k = min(oracle_docs, n)
+        sub = _subbatch(batch, k)
+        o = O.merge(sub, threads=min(16, os.cpu_count() or 1))
+        oracle_ok = True
+        for i in range(k):
+            _, g = stores[0].read(i)
+            d = sub.docs[i]
+            c0, nc, r0, nr, s0 = int(d["change_off"]), int(d["n_changes"]), int(d["reg_off"]), int(d["n_regs"]), int(d["op_off"])
+            ns = int(o.docs["n_surv"][i])
+            oracle_ok &= bool(np.array_equal(g.hist, o.hist[c0:c0 + nc])
+                              and np.array_equal(g.all_deps, o.all_deps[c0 * S:(c0 + nc) * S])
+                              and np.array_equal(g.regs, o.regs[r0:r0 + nr]) and np.array_equal(g.surv[:ns], o.surv[s0:s0 + ns])
+                              and np.array_equal(g.clock, o.clock[i * S:(i + 1) * S])
+                              and np.array_equal(g.heads, o.heads[i * S:(i + 1) * S]))
+    routed = [r["incremental"]["routing"] for r in rounds]
     for st in stores:
         st.close()
-    return {"value": tot_c / t_inc, "unit": "changes/s", "resident_docs": n,
+    return {"value": tot_c / t_inc, "unit": "changes/s", "resident_docs": n, "oracle_docs_equal": oracle_ok,
+            "incremental_share": sum(x["incremental"] for x in routed) / max(1, sum(sum(x.values()) for x in routed)),
             "us_per_round": t_inc * 1e6 / len(rounds), "remerge_value": tot_c / t_rem,
             "speedup_vs_remerge": t_rem / t_inc, "same_as_remerge": same, "all_incremental": routing_ok,
             "pcie_value": tot_c / t_pci, "rounds": rounds,

@@ -189,6 +189,73 @@ struct CHash {
     }
 };
 
+// A list's placed elements in document order, in blocks: a position, an insertion or a visible
+// index costs O(blocks + block size) instead of O(elements) (a text document holds thousands of
+// elements, and the per-op replay asks for one of these per list op).  Blocks have stable ids;
+// `where` (per register, the document's) names each placed element's block; a block keeps its
+// count of visible elements (a non-empty survivor set).
+struct ListOrder {
+    static constexpr uint32_t SPLIT = 256;
+    struct Blk { std::vector<uint32_t> el; uint32_t vis = 0; };
+    std::vector<Blk> pool;                                   // by block id
+    std::vector<uint32_t> seq;                               // block ids in document order
+    uint32_t n = 0;
+    uint32_t size() const { return n; }
+    uint32_t pos_of(uint32_t e, const std::vector<uint32_t> &where) const {
+        const uint32_t b = where[e];
+        uint32_t at = 0;
+        for (uint32_t id : seq) {
+            if (id == b) break;
+            at += (uint32_t)pool[id].el.size();
+        }
+        const auto &v = pool[b].el;
+        return at + (uint32_t)(std::find(v.begin(), v.end(), e) - v.begin());
+    }
+    template <typename Vis>
+    uint32_t vis_before(uint32_t e, const std::vector<uint32_t> &where, Vis &&vis) const {
+        if (e >= where.size() || where[e] == HM_NONE) return 0;
+        const uint32_t b = where[e];
+        uint32_t c = 0;
+        for (uint32_t id : seq) {
+            if (id == b) break;
+            c += pool[id].vis;
+        }
+        for (uint32_t x : pool[b].el) {
+            if (x == e) break;
+            c += vis(x) ? 1u : 0u;
+        }
+        return c;
+    }
+    // the elements `sub` (in order) at position pos
+    template <typename Vis>
+    void insert_at(uint32_t pos, const std::vector<uint32_t> &sub, std::vector<uint32_t> &where, Vis &&vis) {
+        if (sub.empty()) return;
+        if (seq.empty()) { pool.emplace_back(); seq.push_back(0); }
+        uint32_t k = 0, at = 0;
+        while (k + 1 < seq.size() && at + pool[seq[k]].el.size() < pos) at += (uint32_t)pool[seq[k++]].el.size();
+        const uint32_t b = seq[k];
+        Blk &B = pool[b];
+        B.el.insert(B.el.begin() + (pos - at), sub.begin(), sub.end());
+        for (uint32_t x : sub) { where[x] = b; B.vis += vis(x) ? 1u : 0u; }
+        n += (uint32_t)sub.size();
+        if (pool[b].el.size() > SPLIT) {                     // split off the second half
+            const uint32_t nb = (uint32_t)pool.size();
+            pool.emplace_back();
+            Blk &L = pool[b], &R = pool[nb];
+            const size_t half = L.el.size() / 2;
+            R.el.assign(L.el.begin() + half, L.el.end());
+            L.el.resize(half);
+            R.vis = 0;
+            for (uint32_t x : R.el) { where[x] = nb; R.vis += vis(x) ? 1u : 0u; }
+            L.vis -= R.vis;
+            seq.insert(seq.begin() + k + 1, nb);
+        }
+    }
+    void vis_change(uint32_t e, const std::vector<uint32_t> &where, bool now) {
+        if (e < where.size() && where[e] != HM_NONE) { Blk &B = pool[where[e]]; B.vis = now ? B.vis + 1 : B.vis - 1; }
+    }
+};
+
 // ---------------- one document ----------------
 struct DocSt {
     bool ready = false;
@@ -222,8 +289,9 @@ struct DocSt {
     std::vector<std::vector<hm_surv_result>> rs;             // per register
     std::vector<uint32_t> el_op;                             // per register: its ins op, or HM_NONE
     std::vector<uint8_t> el_in;                              // per register: placed in its list's order
+    std::vector<uint32_t> el_blk;                            // per register: its ListOrder block (HM_NONE = not placed)
     std::unordered_map<uint32_t, std::vector<uint32_t>> kids;      // parent key -> children, (elem, actor) descending
-    std::vector<std::pair<uint32_t, std::vector<uint32_t>>> ord;    // list object -> placed elements in document order
+    std::vector<std::pair<uint32_t, ListOrder>> ord;         // list object -> placed elements in document order
     void setup() {
         bool f;
         objs.get(ROOT_ID, 36, 0, f);
@@ -265,10 +333,10 @@ struct DocSt {
         lists.emplace_back(obj, std::vector<uint32_t>());
         return &lists.back().second;
     }
-    static std::vector<uint32_t> &keyed(std::vector<std::pair<uint32_t, std::vector<uint32_t>>> &v, uint32_t k) {
-        for (auto &x : v) if (x.first == k) return x.second;
-        v.emplace_back(k, std::vector<uint32_t>());
-        return v.back().second;
+    ListOrder &order_of(uint32_t obj) {
+        for (auto &x : ord) if (x.first == obj) return x.second;
+        ord.emplace_back(obj, ListOrder());
+        return ord.back().second;
     }
 };
 
@@ -927,17 +995,17 @@ struct Replay {
         while (i < sib.size() && sib_before(sib[i], e)) i++;
         sib.insert(sib.begin() + i, e);
         if (o.parent != HM_HEAD && !(o.parent < d.el_in.size() && d.el_in[o.parent])) return;
-        std::vector<uint32_t> &ov = DocSt::keyed(d.ord, o.obj);
+        ListOrder &ov = d.order_of(o.obj);
         uint32_t pos;
-        if (i == 0) pos = o.parent == HM_HEAD ? 0u : find(ov, o.parent) + 1;
-        else if (i + 1 < sib.size()) pos = find(ov, sib[i + 1]);
+        if (i == 0) pos = o.parent == HM_HEAD ? 0u : ov.pos_of(o.parent, d.el_blk) + 1;
+        else if (i + 1 < sib.size()) pos = ov.pos_of(sib[i + 1], d.el_blk);
         else {                                               // after the parent's subtree
-            pos = (uint32_t)ov.size();
+            pos = ov.size();
             for (uint32_t x = o.parent; x != HM_HEAD;) {
                 const hm_op_row &xo = d.oplog[d.el_op[x]];
                 const std::vector<uint32_t> &xs = d.kids[pkey(xo)];
                 const uint32_t j = find(xs, x);
-                if (j + 1 < xs.size()) { pos = find(ov, xs[j + 1]); break; }
+                if (j + 1 < xs.size()) { pos = ov.pos_of(xs[j + 1], d.el_blk); break; }
                 x = xo.parent;
             }
         }
@@ -951,16 +1019,10 @@ struct Replay {
             if (it != d.kids.end())
                 for (size_t c = it->second.size(); c-- > 0;) stk.push_back(it->second[c]);
         }
-        ov.insert(ov.begin() + pos, sub.begin(), sub.end());
+        ov.insert_at(pos, sub, d.el_blk, [&](uint32_t x) { return !d.rs[x].empty(); });
     }
     uint32_t visible_before(uint32_t obj, uint32_t e) {
-        const std::vector<uint32_t> &ov = DocSt::keyed(d.ord, obj);
-        uint32_t n = 0;
-        for (uint32_t x : ov) {
-            if (x == e) break;
-            n += !d.rs[x].empty();
-        }
-        return n;
+        return d.order_of(obj).vis_before(e, d.el_blk, [&](uint32_t x) { return !d.rs[x].empty(); });
     }
     static bool numeric(uint32_t vt) { return vt == HM_V_INT || vt == HM_V_FLOAT; }
     static double num(uint32_t vt, uint64_t v) {
@@ -1008,6 +1070,8 @@ struct Replay {
             sv[j] = x;
         }
         const uint8_t t = o.obj < d.obj_type.size() && d.obj_type[o.obj] != NO_TYPE ? d.obj_type[o.obj] : (uint8_t)HM_MAKE_MAP;
+        if (was != !sv.empty() && o.reg < d.el_in.size() && d.el_in[o.reg])   // a placed element's visibility
+            d.order_of(o.obj).vis_change(o.reg, d.el_blk, !sv.empty());
         if (t != HM_MAKE_LIST && t != HM_MAKE_TEXT) {
             if (sv.empty()) w.map_remove(t, o.obj, o.reg);
             else w.map_set(t, o.obj, o.reg, sv.data(), (uint32_t)sv.size());
@@ -1408,6 +1472,7 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
             d.rs.resize(x.n_regs);
             d.el_op.resize(x.n_regs, HM_NONE);
             d.el_in.resize(x.n_regs, 0);
+            d.el_blk.resize(x.n_regs, HM_NONE);
         }
     }
     mark("read regs");

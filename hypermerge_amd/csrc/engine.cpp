@@ -69,9 +69,10 @@ Caps launch_caps(const hm_batch *b) {
 // must be serialised: one stream at a time, which the engine enforces by synchronising the
 // device before the pool is resized).
 int launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, hipStream_t s, const uint32_t *doc_slot,
-                 const hm_extents *ext, void *scratch) {
+                 const hm_extents *ext, void *scratch, uint32_t *epos = nullptr) {
     Caps c = launch_caps(b);
     SmallParams p;
+    p.res_epos = epos;
     p.docs = b->docs; p.changes = b->changes; p.deps = b->deps; p.ops = b->ops; p.min_clock = b->min_clock;
     p.res_docs = o->docs; p.res_clock = o->clock; p.res_back_clock = o->back_clock; p.res_heads = o->heads;
     p.res_hist = o->hist; p.res_all_deps = o->all_deps; p.res_regs = o->regs; p.res_surv = o->surv;
@@ -161,8 +162,8 @@ int check_batch(hm_engine *e, const hm_batch *b) {
 
 // ---- internal interface for store.cpp (engine_internal.h) ----
 int hm_engine_launch_merge(hm_engine *e, const hm_batch *b, const hm_results *o, const uint32_t *doc_slot,
-                           const hm_extents *ext) {
-    return launch_merge(e, b, o, e->stream, doc_slot, ext, nullptr);
+                           const hm_extents *ext, uint32_t *epos) {
+    return launch_merge(e, b, o, e->stream, doc_slot, ext, nullptr, epos);
 }
 hipStream_t hm_engine_stream(hm_engine *e) { return e->stream; }
 int hm_engine_device(hm_engine *e) { return e->device; }

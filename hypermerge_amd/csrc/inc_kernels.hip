@@ -71,8 +71,200 @@ __device__ __forceinline__ uint64_t abs64(int64_t v) { return v < 0 ? (uint64_t)
 
 constexpr unsigned long long TWO53 = 1ull << 53;
 
+// ---------------- list / text ops (G = 64: one document per wave) ----------------
+// The document's list order is resident (lorder / epos / epar / ekey, HM_IST_LIST).  A round's
+// `ins` ops take the fast path of applyInsert when every new element hangs off an element that
+// exists (or one this round inserted earlier) and, under an old parent, sorts before that
+// parent's current first child (lamportCompare (elem, actor) DESCENDING: the typing case, a new
+// element with the largest elem counter): the new elements then form blocks, one per old anchor,
+// in pre-order of their own forest, placed right after the anchor; every old element after an
+// anchor shifts by the blocks before it.  Anything else (concurrent inserts under one parent that
+// sort after an existing child, an insert after an element not inserted yet, a duplicate elemId)
+// goes to the re-merge.  Sets / deletes on elements are applyAssign as for map keys; the visible
+// indices are then rewritten from the first position that changed.
+constexpr uint32_t LSCR = 192;                 // per document: anchors (64), cumulative block sizes (64), subtree sizes (64)
+
+struct ListPlan {
+    uint32_t n_el0, n_el;                      // elements before / after the submit (uniform)
+    uint32_t na, pmin, q0;                     // anchors, first old position that moves, first index that changes
+    uint32_t npos, key;                        // ins lanes: the new element's position and lamport key
+};
+
+__device__ __forceinline__ uint32_t list_shift(const uint32_t *lscr, uint32_t na, uint32_t i) {
+    uint32_t s = 0;
+    for (uint32_t k = 0; k < na; k++)
+        if ((int)lscr[k] - 1 < (int)i) s = lscr[64 + k];     // blocks of the anchors before position i
+    return s;
+}
+
+__device__ int list_plan(const Grp<64> &g, const AppendDesc &D, const IncArgs &A, const IncState &I, uint32_t nno,
+                         uint32_t o_act, uint32_t o_reg, uint32_t o_par, uint32_t o_elem, bool lst, uint32_t opactor,
+                         uint32_t *lscr, ListPlan &lp) {
+    const uint32_t gl = g.gl, n_el = I.pad[0];
+    const bool ins = lst && o_act == HM_INS, eop = lst && o_act != HM_INS;
+    const uint64_t insm = g.bits(ins);
+    const uint32_t nins = (uint32_t)__popcll(insm);
+    const uint32_t key = (o_elem << 8) | (opactor & 0xFFu);
+    // a new element's register is fresh; its parent exists: an old element, '_head', or an
+    // element inserted earlier in this round; an assign hits an element that exists
+    bool bad = ins && o_reg < D.n_old_r;
+    uint32_t pnew = HM_NONE, ecr = HM_NONE;
+    for (uint32_t k = 0; k < nno; k++) {
+        if (!((insm >> k) & 1ull)) continue;
+        const uint32_t rk = g.sh(o_reg, k);
+        if (k < gl && ins && rk == o_reg) bad = true;
+        if (k < gl && ins && rk == o_par) pnew = k;
+        if (k < gl && eop && rk == o_reg) ecr = k;
+    }
+    const bool root = ins && pnew == HM_NONE;
+    uint32_t pold = HM_NONE, eold = HM_NONE;
+    if (root && o_par != HM_HEAD) pold = o_par < D.n_old_r ? A.epos[D.src_r + o_par] : HM_NONE;
+    if (eop && ecr == HM_NONE) eold = o_reg < D.n_old_r ? A.epos[D.src_r + o_reg] : HM_NONE;
+    bad |= (root && o_par != HM_HEAD && pold >= n_el) || (eop && ecr == HM_NONE && eold >= n_el);
+    if (g.bits(bad)) return INC_BAIL;
+    // the positions read back name the registers (a register that is no element has a stale slot)
+    const int pa = root ? (o_par == HM_HEAD ? -1 : (int)pold) : 0;
+    uint32_t at_p = HM_NONE, at_e = HM_NONE, nxt = HM_NONE;
+    if (root && pa >= 0) at_p = A.lorder[D.src_r + pa];
+    if (root && (uint32_t)(pa + 1) < n_el) nxt = A.lorder[D.src_r + pa + 1];
+    if (eop && ecr == HM_NONE) at_e = A.lorder[D.src_r + eold];
+    bad = (root && pa >= 0 && at_p != o_par) || (eop && ecr == HM_NONE && at_e != o_reg);
+    // under an old parent the new element must sort before the parent's first child
+    if (root && nxt != HM_NONE && A.epar[D.src_r + nxt] == o_par && !(key > A.ekey[D.src_r + nxt])) bad = true;
+    if (g.bits(bad)) return INC_BAIL;
+
+    // subtree sizes in the round's forest: every element counts itself at each of its ancestors
+    uint32_t *sz = lscr + 128;
+    sz[gl] = 0;
+    __builtin_amdgcn_wave_barrier();
+    {
+        uint32_t a = ins ? gl : HM_NONE;
+        for (uint32_t st = 0; st < nins; st++) {
+            if (a != HM_NONE) atomicAdd(&sz[a], 1u);
+            const uint32_t up = g.sh(pnew, a == HM_NONE ? 0u : a);
+            a = a == HM_NONE ? HM_NONE : up;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t size = ins ? sz[gl] : 0u;
+    // rank in the anchor's block: siblings (same new parent, or the same anchor for roots) with a
+    // larger key come first with their subtrees; a child follows its parent
+    uint32_t r0 = ins && !root ? 1u : 0u;
+    for (uint32_t k = 0; k < nno; k++) {
+        if (!((insm >> k) & 1ull)) continue;
+        const uint32_t pk = g.sh(pnew, k), ak = g.sh((uint32_t)pa, k), kk = g.sh(key, k), sk = g.sh(size, k);
+        const bool same = pnew != HM_NONE ? pk == pnew : (pk == HM_NONE && (int)ak == pa);
+        if (ins && k != gl && same && kk > key) r0 += sk;
+    }
+    uint32_t rank = r0, ranc = (uint32_t)pa;
+    {
+        uint32_t a = ins ? pnew : HM_NONE;
+        for (uint32_t st = 0; st < nins; st++) {
+            const uint32_t src = a == HM_NONE ? 0u : a;
+            const uint32_t ra = g.sh(r0, src), pp = g.sh(pnew, src), an = g.sh((uint32_t)pa, src);
+            if (a != HM_NONE) { rank += ra; ranc = an; a = pp; }
+        }
+    }
+    // anchors (distinct root anchors) in position order with their cumulative block sizes
+    bool leader = root;
+    uint32_t bsize = 0, before = 0;
+    for (uint32_t k = 0; k < nno; k++) {
+        if (!((insm >> k) & 1ull)) continue;
+        const uint32_t pk = g.sh(pnew, k), ak = g.sh((uint32_t)pa, k), sk = g.sh(size, k);
+        if (pk != HM_NONE) continue;
+        if (root && k < gl && (int)ak == pa) leader = false;
+        if (root && (int)ak == pa) bsize += sk;
+        if (ins && (int)ak < (int)ranc) before += sk;      // blocks of the anchors before this element's
+    }
+    const uint64_t lm = g.bits(leader);
+    const uint32_t na = (uint32_t)__popcll(lm);
+    uint32_t idx = 0, cum = 0;
+    for (uint32_t k = 0; k < nno; k++) {
+        if (!((lm >> k) & 1ull)) continue;
+        const uint32_t ak = g.sh((uint32_t)pa, k), bk = g.sh(bsize, k);
+        if (leader && (int)ak < pa) idx++;
+        if (leader && (int)ak <= pa) cum += bk;
+    }
+    if (leader) { lscr[idx] = (uint32_t)(pa + 1); lscr[64 + idx] = cum; }
+    __builtin_amdgcn_wave_barrier();
+    uint32_t pmin = ins ? (uint32_t)((int)ranc + 1) : HM_NONE;
+    for (uint32_t d = 1; d < 64; d <<= 1) { const uint32_t y = g.sh(pmin, gl ^ d); pmin = y < pmin ? y : pmin; }
+    lp.n_el0 = n_el; lp.n_el = n_el + nins; lp.na = na; lp.pmin = nins ? pmin : n_el;
+    lp.key = key;
+    lp.npos = ins ? (uint32_t)((int)ranc + 1) + before + rank : HM_NONE;
+    // the first position whose visible index may change: the first moved one, or an element an
+    // assign hits (at its new position)
+    uint32_t qe = HM_NONE;
+    {
+        const uint32_t cn = g.sh(lp.npos, ecr == HM_NONE ? 0u : ecr);
+        if (eop) qe = ecr != HM_NONE ? cn : eold + list_shift(lscr, na, eold);
+    }
+    uint32_t q0 = qe < lp.pmin ? qe : lp.pmin;
+    for (uint32_t d = 1; d < 64; d <<= 1) { const uint32_t y = g.sh(q0, gl ^ d); q0 = y < q0 ? y : q0; }
+    lp.q0 = q0;
+    return INC_DONE;
+}
+
+// the order rewritten: old elements from pmin on shift right (from the end, 64 at a time: every
+// move goes up, so nothing is overwritten before it is read), then the new elements land
+__device__ void list_insert(const Grp<64> &g, const AppendDesc &D, const IncArgs &A, const IncState &I, uint32_t o_act,
+                            uint32_t o_reg, uint32_t o_par, const uint32_t *lscr, const ListPlan &lp) {
+    const uint32_t gl = g.gl;
+    if (lp.n_el > lp.n_el0)
+        for (int top = (int)lp.n_el0 - 1; top >= (int)lp.pmin; top -= 64) {
+            const int i = top - (int)gl;
+            const bool v = i >= (int)lp.pmin;
+            const uint32_t e = v ? A.lorder[D.dst_r + i] : 0u;
+            if (v) {
+                const uint32_t np = (uint32_t)i + list_shift(lscr, lp.na, (uint32_t)i);
+                A.lorder[D.dst_r + np] = e;
+                A.epos[D.dst_r + e] = np;
+            }
+        }
+    if (lp.npos != HM_NONE && o_act == HM_INS) {
+        A.lorder[D.dst_r + lp.npos] = o_reg;
+        A.epos[D.dst_r + o_reg] = lp.npos;
+        A.epar[D.dst_r + o_reg] = o_par;
+        A.ekey[D.dst_r + o_reg] = lp.key;
+    }
+}
+
+// visible indices (hm_reg_result.list_index) from the first position that changed to the end
+__device__ void list_indices(const Grp<64> &g, const AppendDesc &D, const IncArgs &A, const ListPlan &lp) {
+    const uint32_t gl = g.gl;
+    if (lp.q0 >= lp.n_el) return;
+    uint32_t c = 0;                                           // visible elements before q0
+    for (int top = (int)lp.q0 - 1; top >= 0; top -= 64) {
+        const int i = top - (int)gl;
+        bool v = false;
+        int32_t li = -1;
+        if (i >= 0) {
+            const hm_reg_result &r = A.regs[D.dst_r + A.lorder[D.dst_r + i]];
+            v = r.n_surv > 0;
+            li = r.list_index;
+        }
+        const uint64_t m = g.bits(v);
+        if (m) { c = (uint32_t)g.sh((uint32_t)li, (uint32_t)__builtin_ctzll(m)) + 1u; break; }
+    }
+    for (uint32_t q = lp.q0; q < lp.n_el; q += 64) {
+        const uint32_t i = q + gl;
+        hm_reg_result *r = nullptr;
+        bool v = false;
+        int32_t old = -1;
+        if (i < lp.n_el) {
+            r = A.regs + D.dst_r + A.lorder[D.dst_r + i];
+            v = r->n_surv > 0;
+            old = r->list_index;
+        }
+        const uint64_t m = g.bits(v);
+        const int32_t li = v ? (int32_t)(c + g.below(m)) : -1;
+        if (r && li != old) r->list_index = li;
+        c += (uint32_t)__popcll(m);
+    }
+}
+
 template <int G>
-__device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 *smt) {
+__device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 *smt, uint32_t *lscr) {
     const Grp<G> g;
     const uint32_t gl = g.gl;
     const uint32_t S = A.S, h = D.handle, NA = D.n_actors, nnc = D.n_new_c, nno = D.n_new_o, nnd = D.n_new_d;
@@ -111,12 +303,12 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
         const hm_change_row c = A.st_changes[D.new_c + gl];
         ca = c.actor; cq = c.seq; cnd = c.n_deps; cdo = c.dep_off - D.new_d; cno = c.n_ops; coo = c.op_first - D.new_o;
     }
-    uint32_t o_act = 0, o_dt = 0, o_obj = 0, o_reg = 0xFFFFFFFFu, o_vt = 0, o_vlo = 0, o_vhi = 0;
+    uint32_t o_act = 0, o_dt = 0, o_obj = 0, o_reg = 0xFFFFFFFFu, o_vt = 0, o_vlo = 0, o_vhi = 0, o_par = 0, o_elem = 0;
     if (gl < nno) {
         const uint4 *src = reinterpret_cast<const uint4 *>(A.st_ops + D.new_o + gl);
         const uint4 w0 = src[0], w1 = src[1];
         // hm_op_row: obj, reg, parent, elem | action, datatype, vtag, pad, key, value lo, value hi
-        o_obj = w0.x; o_reg = w0.y;
+        o_obj = w0.x; o_reg = w0.y; o_par = w0.z; o_elem = w0.w;
         o_act = w1.x & 0xFFu; o_dt = (w1.x >> 8) & 0xFFu; o_vt = (w1.x >> 16) & 0xFFu;
         o_vlo = w1.z; o_vhi = w1.w;
     }
@@ -146,13 +338,19 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
     const uint32_t total_d = g.sh(sd, nnc - 1), total_o = g.sh(so, nnc - 1);
     const bool bad_c = gl < nnc && (ca >= NA || cq == 0 || cq >= (1u << 24) || cdo != xd || coo != xo);
     const int64_t oval = (int64_t)(((uint64_t)o_vhi << 32) | o_vlo);
-    const bool bad_o = gl < nno && ((o_act != HM_SET && o_act != HM_DEL && o_act != HM_LINK && o_act != HM_INC) ||
+    // an op on the document's list / text object (its order is resident: HM_IST_LIST)
+    const bool lst = gl < nno && (I.flags & HM_IST_LIST) && o_obj == I.pad[1];
+    const bool bad_o = gl < nno && ((o_act != HM_SET && o_act != HM_DEL && o_act != HM_LINK && o_act != HM_INC &&
+                                     !(lst && o_act == HM_INS)) ||
                                     (o_act == HM_INC && o_vt != HM_V_INT && o_vt != HM_V_FLOAT) ||
                                     o_obj >= D.n_objs || o_reg >= D.n_r ||
                                     (o_vt == HM_V_INT && abs64(oval) > TWO53) ||
+                                    (o_act == HM_INS && (o_elem >= (1u << 24) || (o_par != HM_HEAD && o_par >= D.n_r))) ||
                                     // an object other than ROOT must be a map / table the log created
-                                    (o_obj != 0 && (o_obj >= 64 || !((I.mapmask >> o_obj) & 1ull))));
+                                    (!lst && o_obj != 0 && (o_obj >= 64 || !((I.mapmask >> o_obj) & 1ull))));
     if (g.bits(bad_c || bad_o) || total_o != nno || total_d != nnd) return INC_BAIL;
+    const bool any_list = g.bits(lst) != 0;
+    if (G < 64 && any_list) return INC_DEFER;                 // list / text ops: one document per wave
     // integer counters: |base| + sum|inc| of every counter stays <= 2^53 (the re-merge's exact rule)
     unsigned long long cadd = (gl < nno && o_vt == HM_V_INT &&
                                (o_act == HM_INC || (o_act == HM_SET && o_dt == HM_DT_COUNTER))) ? abs64(oval) : 0ull;
@@ -223,11 +421,11 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
     }
 
     // ---- first-touch registers (lane = op): pushes, staging offsets, space ----
-    bool first = gl < nno;
+    bool first = gl < nno && o_act != HM_INS;                 // (an ins creates its register; the assigns fill it)
     uint32_t push = 0, oj = 0;
     for (uint32_t k = 0; k < nno; k++) {
         const uint32_t r = g.sh(o_reg, k), ak = g.sh(o_act, k);
-        if (k < gl && r == o_reg) first = false;
+        if (k < gl && r == o_reg && ak != HM_INS) first = false;
         if (k >= gl && r == o_reg && (ak == HM_SET || ak == HM_LINK)) push++;
     }
     for (uint32_t j = 0; j < nnc; j++)
@@ -281,6 +479,15 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
         if (gl == a) { hdr = q; ckf = q; }
     }
 
+    // ---- list / text ops (applyInsert, A.3): the new elements' places in the resident order ----
+    ListPlan lp;
+    if constexpr (G == 64) {
+        if (any_list) {
+            const int rc = list_plan(g, D, A, I, nno, o_act, o_reg, o_par, o_elem, lst, g.sh(ca, oj), lscr, lp);
+            if (rc != INC_DONE) return rc;
+        }
+    }
+
     // ---- level 4: the hit registers' survivors and their metadata, staged per group ----
     {
         // slot p of the staging area (two per lane) <- survivor src of the register that owns p
@@ -313,10 +520,22 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
             *reinterpret_cast<uint4 *>(A.surv + D.dst_o + i) = x;
             A.smeta[D.dst_o + i] = xm;
         }
-    if (D.src_r != D.dst_r)
+    if (D.src_r != D.dst_r) {
         for (uint32_t i = gl; i < D.n_old_r; i += G) A.regs[D.dst_r + i] = A.regs[D.src_r + i];
+        if (I.flags & HM_IST_LIST) {
+            for (uint32_t i = gl; i < D.n_old_r; i += G) {
+                A.epos[D.dst_r + i] = A.epos[D.src_r + i];
+                A.epar[D.dst_r + i] = A.epar[D.src_r + i];
+                A.ekey[D.dst_r + i] = A.ekey[D.src_r + i];
+            }
+            for (uint32_t i = gl; i < I.pad[0]; i += G) A.lorder[D.dst_r + i] = A.lorder[D.src_r + i];
+        }
+    }
     if (mv) __threadfence_block();                            // the copies land before the writes below
     __builtin_amdgcn_wave_barrier();
+    if constexpr (G == 64) {
+        if (any_list) list_insert(g, D, A, I, o_act, o_reg, o_par, lscr, lp);
+    }
 
     // ---- the new ops, register by register in first-touch order (applyAssign, A.2) ----
     uint64_t fm = g.bits(first);
@@ -332,7 +551,7 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
         if (gl < cnt0) { x = ssv[sb + gl]; xm = smt[sb + gl]; }
         uint32_t cnt = cnt0;
         for (uint32_t k = k0; k < nno; k++) {
-            if (g.sh(o_reg, k) != greg) continue;
+            if (g.sh(o_reg, k) != greg || g.sh(o_act, k) == HM_INS) continue;
             const uint32_t act = g.sh(o_act, k), vt = g.sh(o_vt, k), dtk = g.sh(o_dt, k);
             const uint32_t vlo = g.sh(o_vlo, k), vhi = g.sh(o_vhi, k), j = g.sh(oj, k);
             const uint32_t a = g.sh(ca, j), q = g.sh(cq, j);
@@ -398,11 +617,19 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
     for (uint32_t r0 = D.n_old_r; r0 < D.n_r; r0 += G) {
         const uint32_t r = r0 + gl;
         bool hit = false;
-        for (uint32_t k = 0; k < nno; k++) hit |= g.sh(o_reg, k) == r;
+        for (uint32_t k = 0; k < nno; k++) hit |= g.sh(o_reg, k) == r && g.sh(o_act, k) != HM_INS;
         if (r < D.n_r && !hit) {
             hm_reg_result z;
             z.n_surv = 0; z.surv_off = 0; z.list_index = -1; z.obj = HM_NONE;
             A.regs[D.dst_r + r] = z;
+        }
+    }
+
+    if constexpr (G == 64) {
+        if (any_list) {
+            __threadfence_block();                            // the register rows above, then the visible indices
+            __builtin_amdgcn_wave_barrier();
+            list_indices(g, D, A, lp);
         }
     }
 
@@ -428,6 +655,7 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
         A.res_docs[h] = r;
         IncState s = I;
         s.s_used = I.s_used + acc; s.cabs = cabs;
+        if (G == 64 && any_list) s.pad[0] = lp.n_el;
         A.ist[h] = s;
     }
     return INC_DONE;
@@ -438,13 +666,14 @@ __global__ __launch_bounds__(256) void inc_group_kernel(IncArgs A) {
     constexpr uint32_t NG = 256 / G;
     __shared__ uint4 s_sv[NG][2 * G];
     __shared__ uint2 s_mt[NG][2 * G];
+    __shared__ uint32_t s_ls[G == 64 ? NG : 1][G == 64 ? LSCR : 1];   // the list phase's anchors
     const uint32_t grp = threadIdx.x / G, gl = threadIdx.x & (G - 1);
     const uint32_t n = A.list ? A.list[0] : A.n;
     for (uint32_t q = blockIdx.x * NG + grp; q < n; q += gridDim.x * NG) {
         const uint32_t di = A.list ? A.list[1 + q] : q;
         const AppendDesc D = A.descs[di];
         if (!D.inc) continue;
-        const int rc = inc_doc<G>(D, A, s_sv[grp], s_mt[grp]);
+        const int rc = inc_doc<G>(D, A, s_sv[grp], s_mt[grp], s_ls[G == 64 ? grp : 0]);
         if (rc != INC_DONE && gl == 0) {
             if (rc == INC_DEFER && A.defer) A.defer[1 + atomicAdd(&A.defer[0], 1u)] = di;
             else A.bail[1 + atomicAdd(&A.bail[0], 1u)] = D.handle;
@@ -452,46 +681,58 @@ __global__ __launch_bounds__(256) void inc_group_kernel(IncArgs A) {
     }
 }
 
+// the change that owns doc-local op k: the last change whose first op is <= k (ops are grouped
+// by change in log order; a change without ops shares its first op with the next)
+__device__ __forceinline__ uint32_t change_of_op(const hm_change_row *ch, uint32_t n_c, uint32_t o_off, uint32_t k) {
+    uint32_t lo = 0, hi = n_c;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (ch[mid].op_first - o_off <= k) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
 // After a re-merge (one wave per listed document): survivor metadata (the survivor's change by
-// a binary search over the change rows' first ops — ops are grouped by change in log order),
-// the objects created as maps / tables, the counter bound.  Documents that are not clean
-// (an error, queued changes) get flags = 0: their next submit re-merges.
-__global__ __launch_bounds__(256) void inc_meta_kernel(const uint32_t *list, uint32_t n, const DevDoc *dm,
-                                                       const hm_doc_result *res_docs, const hm_change_row *changes,
-                                                       const int32_t *hist, uint32_t *ckey, const hm_op_row *ops,
-                                                       const hm_surv_result *surv, uint2 *smeta, IncState *ist) {
+// a binary search over the change rows' first ops), the packed change keys, the objects created
+// as maps / tables, the counter bound, and — for a document with one list / text object — the
+// resident list order (lorder, epos, epar, ekey) from the element positions the merge wrote.
+// Documents that are not clean (an error, queued changes) get flags = 0: their next submit
+// re-merges.
+__global__ __launch_bounds__(256) void inc_meta_kernel(MetaArgs a) {
     const uint32_t lane = threadIdx.x & 63;
-    for (uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6); q < n; q += gridDim.x * 4) {
-        const uint32_t h = list[q];
-        const DevDoc m = dm[h];
-        const hm_doc_result r = res_docs[h];
+    for (uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6); q < a.n; q += gridDim.x * 4) {
+        const uint32_t h = a.list[q];
+        const DevDoc m = a.dm[h];
+        const hm_doc_result r = a.res_docs[h];
         if (r.status != HM_OK || r.n_queued != 0 || r.n_surv > m.o_cap) {
-            if (lane == 0) { IncState z = {}; ist[h] = z; }
+            if (lane == 0) { IncState z = {}; a.ist[h] = z; }
             continue;
         }
+        const hm_change_row *ch = a.changes + m.c_off;
         for (uint32_t i = lane; i < r.n_surv; i += 64) {
-            const uint32_t op = surv[m.o_off + i].op;
-            uint32_t lo = 0, hi = m.n_c;
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (changes[m.c_off + mid].op_first - m.o_off <= op) lo = mid; else hi = mid;
-            }
-            const uint2 kw = *reinterpret_cast<const uint2 *>(changes + m.c_off + lo);
-            const hm_op_row &o = ops[m.o_off + op];
+            const uint32_t op = a.surv[m.o_off + i].op;
+            const uint32_t c = change_of_op(ch, m.n_c, m.o_off, op);
+            const uint2 kw = *reinterpret_cast<const uint2 *>(ch + c);
+            const hm_op_row &o = a.ops[m.o_off + op];
             const uint32_t cset = (o.action == HM_SET && o.datatype == HM_DT_COUNTER) ? 0x100u : 0u;
-            smeta[m.o_off + i] = make_uint2(kw.y, (kw.x & 0xFFu) | cset);
+            a.smeta[m.o_off + i] = make_uint2(kw.y, (kw.x & 0xFFu) | cset);
         }
         bool wide = false;                                   // a seq the packed keys cannot hold
         for (uint32_t i = lane; i < m.n_c; i += 64) {
-            const uint2 kw = *reinterpret_cast<const uint2 *>(changes + m.c_off + i);
+            const uint2 kw = *reinterpret_cast<const uint2 *>(ch + i);
             wide |= kw.y >= (1u << 24);
-            ckey[m.c_off + i] = hm_ckey(kw.x & 0xFFFFu, kw.y, hist[m.c_off + i] >= 0);
+            a.ckey[m.c_off + i] = hm_ckey(kw.x & 0xFFFFu, kw.y, a.hist[m.c_off + i] >= 0);
         }
         wide = __ballot(wide) != 0;
         unsigned long long mask = 1ull, cabs = 0;
+        uint32_t lmin = HM_NONE, lmax = 0;                   // the list / text objects created
         for (uint32_t i = lane; i < m.n_o; i += 64) {
-            const hm_op_row o = ops[m.o_off + i];
+            const hm_op_row o = a.ops[m.o_off + i];
             if ((o.action == HM_MAKE_MAP || o.action == HM_MAKE_TABLE) && o.obj < 64) mask |= 1ull << o.obj;
+            if (o.action == HM_MAKE_LIST || o.action == HM_MAKE_TEXT) {
+                lmin = o.obj < lmin ? o.obj : lmin;
+                lmax = o.obj > lmax ? o.obj : lmax;
+            }
             if (o.vtag == HM_V_INT && (o.action == HM_INC || (o.action == HM_SET && o.datatype == HM_DT_COUNTER))) {
                 const unsigned long long v = abs64((int64_t)o.value);
                 cabs = cabs + v < cabs || cabs + v > (1ull << 62) ? (1ull << 62) : cabs + v;
@@ -501,12 +742,63 @@ __global__ __launch_bounds__(256) void inc_meta_kernel(const uint32_t *list, uin
             mask |= (unsigned long long)__shfl_xor((long long)mask, d);
             const unsigned long long y = (unsigned long long)__shfl_xor((long long)cabs, d);
             cabs = cabs + y > (1ull << 62) ? (1ull << 62) : cabs + y;
+            const uint32_t a0 = (uint32_t)__shfl_xor((int)lmin, d), a1 = (uint32_t)__shfl_xor((int)lmax, d);
+            lmin = a0 < lmin ? a0 : lmin;
+            lmax = a1 > lmax ? a1 : lmax;
+        }
+        // (a duplicate of the creating change repeats its make op: the same object)
+        const uint32_t n_lists = lmin == HM_NONE ? 0u : (lmin == lmax ? 1u : 2u), lobj = lmin;
+        // one list / text object: its order from the element positions of the merge
+        uint32_t flags = HM_IST_VALID | (wide ? HM_IST_NOCKEY : 0u), n_el = 0;
+        if (n_lists == 1 && lobj < 64 && a.lorder) {
+            bool ok = true;
+            uint32_t cnt = 0;
+            for (uint32_t i = lane; i < m.n_o; i += 64) {
+                const hm_op_row o = a.ops[m.o_off + i];
+                bool applied_ins = false;
+                if (o.action == HM_INS) {
+                    const uint32_t c = change_of_op(ch, m.n_c, m.o_off, i);
+                    applied_ins = a.hist[m.c_off + c] >= 0;          // (a duplicate's copy: its twin counts)
+                    if (applied_ins) {
+                        const uint32_t pos = o.reg < m.n_r ? a.epos[m.r_off + o.reg] : HM_NONE;
+                        ok &= o.obj == lobj && o.elem < (1u << 24) && pos < m.n_r;
+                        if (pos < m.n_r) {
+                            a.lorder[m.r_off + pos] = o.reg;
+                            a.epar[m.r_off + o.reg] = o.parent;
+                            a.ekey[m.r_off + o.reg] = (o.elem << 8) | (ch[c].actor & 0xFFu);
+                        }
+                    }
+                }
+                cnt += (uint32_t)__popcll(__ballot(applied_ins));
+            }
+            n_el = __shfl((int)cnt, 0);
+            ok = __ballot(!ok) == 0;
+            // every element placed, at positions 0 .. n_el - 1 (detached elements have none)
+            if (ok) {
+                bool hole = false;
+                for (uint32_t i = lane; i < m.n_o; i += 64) {
+                    const hm_op_row o = a.ops[m.o_off + i];
+                    if (o.action == HM_INS && o.reg < m.n_r) hole |= a.epos[m.r_off + o.reg] >= n_el;
+                }
+                ok = __ballot(hole) == 0;
+            }
+            if (ok) flags |= HM_IST_LIST;
         }
         if (lane == 0) {
             IncState s = {};
-            s.s_used = r.n_surv; s.flags = HM_IST_VALID | (wide ? HM_IST_NOCKEY : 0u); s.cabs = cabs; s.mapmask = mask;
-            ist[h] = s;
+            s.s_used = r.n_surv; s.flags = flags; s.cabs = cabs; s.mapmask = mask;
+            s.pad[0] = n_el; s.pad[1] = (flags & HM_IST_LIST) ? lobj : HM_NONE;
+            a.ist[h] = s;
         }
+    }
+}
+
+__global__ __launch_bounds__(256) void epos_clear_kernel(const uint32_t *list, uint32_t n, const DevDoc *dm, uint32_t *epos) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6); q < n; q += gridDim.x * 4) {
+        const DevDoc m = dm[list[q]];
+        if (!(m.flags & HM_DOC_HAS_LISTS)) continue;
+        for (uint32_t g = lane; g < m.n_r; g += 64) epos[m.r_off + g] = HM_NONE;
     }
 }
 
@@ -536,12 +828,16 @@ hipError_t hm_launch_inc_apply(const IncArgs &A, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t hm_launch_inc_meta(const uint32_t *list, uint32_t n, const DevDoc *dm, const hm_doc_result *res_docs,
-                              const hm_change_row *changes, const int32_t *hist, uint32_t *ckey, const hm_op_row *ops,
-                              const hm_surv_result *surv, uint2 *smeta, IncState *ist, hipStream_t s) {
+hipError_t hm_launch_inc_meta(const MetaArgs &a, hipStream_t s) {
+    if (!a.n) return hipSuccess;
+    const uint32_t grid = (a.n + 3) / 4 < 65535u ? (a.n + 3) / 4 : 65535u;
+    hipLaunchKernelGGL(hmi::inc_meta_kernel, dim3(grid), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t hm_launch_epos_clear(const uint32_t *list, uint32_t n, const DevDoc *dm, uint32_t *epos, hipStream_t s) {
     if (!n) return hipSuccess;
     const uint32_t grid = (n + 3) / 4 < 65535u ? (n + 3) / 4 : 65535u;
-    hipLaunchKernelGGL(hmi::inc_meta_kernel, dim3(grid), dim3(256), 0, s, list, n, dm, res_docs, changes, hist, ckey, ops,
-                       surv, smeta, ist);
+    hipLaunchKernelGGL(hmi::epos_clear_kernel, dim3(grid), dim3(256), 0, s, list, n, dm, epos);
     return hipGetLastError();
 }

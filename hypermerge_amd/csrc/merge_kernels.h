@@ -29,6 +29,10 @@ struct SmallParams {
     // extents of the row tables: a document row whose ranges leave them (or whose n_actors
     // exceeds a_stride) is reported HM_ERR_INVALID and never read through
     uint32_t lim_changes, lim_deps, lim_ops, lim_regs;
+    // optional (the resident store): per list element register, its position in its list's
+    // document order (every inserted element, visible or not) — the order the incremental path
+    // keeps resident; rows of other registers are not written
+    uint32_t *res_epos;
 };
 #ifdef __HIPCC__
 __device__ __forceinline__ bool hm_doc_row_ok(const SmallParams &p, const hm_doc_row &d) {

@@ -317,7 +317,7 @@ __device__ __forceinline__ void rga_order(const SmallLds &L, uint32_t R, uint32_
                                           const uint32_t (&oreg)[OPL], const uint32_t (&oobj)[OPL],
                                           const uint32_t (&opar)[OPL], const uint32_t (&oact)[OPL],
                                           const uint32_t (&oelem)[OPL], const uint32_t (&oarr)[OPL],
-                                          const int32_t (&oh)[OPL]) {
+                                          const int32_t (&oh)[OPL], uint32_t *epos) {
     const uint32_t lane = threadIdx.x;
     const uint32_t NP = R + O;
     constexpr uint32_t END = 0xFFFFu;
@@ -436,6 +436,7 @@ __device__ __forceinline__ void rga_order(const SmallLds &L, uint32_t R, uint32_
         const uint32_t pos = L.listbase[l] + total - (cur[2 * i] & 0xFFFFu);
         L.seglist[pos] = L.survcnt[reg] > 0 ? 1u : 0u;       // visible = non-empty survivor set
         L.nodekey[i] = pos;
+        if (epos) epos[reg] = pos - L.listbase[l];
         L.insmin[reg] = 0xFFFFFFFFu;                          // -> list index (or -1)
     }
     wave_sync();
@@ -1296,7 +1297,8 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     STAMP(L, 8);
     if (HM_ABLATE & 256) return OUT_UNSUPPORTED;
     if constexpr (LISTS) {
-        if (doc_lists) rga_order<OPL>(L, R, O, oreg, oobj, opar, oact, oelem, oarr, oh);
+        if (doc_lists) rga_order<OPL>(L, R, O, oreg, oobj, opar, oact, oelem, oarr, oh,
+                                      p.res_epos ? p.res_epos + doc.reg_off : nullptr);
     }
     // counters: an inc adds to every surviving counter set that is its ancestor.
     // JS numbers: an integer counter is exact only while |base| + sum|inc| <= 2^53; with at

@@ -790,6 +790,7 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
         for (uint32_t i = tid; i < N; i += LWG) {
             const uint32_t l = n_list[i], rg = n_reg[i];
             r_ins[rg] = r_scnt[rg] > 0 ? vis[pos_of(i, l)] - vis[sh.listbase[l]] : 0xFFFFFFFFu;
+            if (p.res_epos) p.res_epos[doc.reg_off + rg] = pos_of(i, l) - sh.listbase[l];
         }
         bsync();
     }
@@ -2023,6 +2024,7 @@ __device__ HML_DOC_ATTR Outcome merge_doc_large(const SmallParams &p, Shared &sh
             const uint32_t l = X.nlist[i], rg = X.nreg[i];
             // list elements carry their visible index (or -1) in insmin from here on
             X.insmin[rg] = X.survcnt[rg] > 0 ? X.vis[pos_of(i, l)] - X.vis[X.listbase[l]] : 0xFFFFFFFFu;
+            if (p.res_epos) p.res_epos[doc.reg_off + rg] = pos_of(i, l) - X.listbase[l];
         }
         bsync();
     }

@@ -66,6 +66,7 @@ struct hm_store {
     hm_dep_row *deps = nullptr;
     hm_op_row *ops = nullptr; hm_surv_result *surv = nullptr; uint2 *smeta = nullptr;
     hm_reg_result *regs = nullptr;
+    uint32_t *epos = nullptr, *epar = nullptr, *ekey = nullptr, *lorder = nullptr;   // reg space: resident list order
     // per handle
     size_t cap_h = 0;
     DevDoc *dm = nullptr;                         // segments and totals
@@ -262,11 +263,17 @@ int launch_list_merge(hm_store *s, const uint32_t *dev_list, uint32_t n) {
     o.docs = s->res_docs; o.clock = s->clock; o.back_clock = s->back_clock; o.heads = s->heads;
     o.hist = s->hist; o.all_deps = s->all_deps; o.regs = s->regs; o.surv = s->surv;
     const hm_extents ext = {(uint32_t)s->cap_c, (uint32_t)s->cap_d, (uint32_t)s->cap_o, (uint32_t)s->cap_r};
-    rc = hm_engine_launch_merge(s->e, &b, &o, dev_list, &ext);
+    // the incremental path keeps list documents' element order: positions written by the merge
+    if (s->incremental && (P.flags & HM_DOC_HAS_LISTS)) SCHK(s, hm_launch_epos_clear(dev_list, n, s->dm, s->epos, st));
+    rc = hm_engine_launch_merge(s->e, &b, &o, dev_list, &ext, s->incremental ? s->epos : nullptr);
     // the incremental path's survivor metadata of the re-merged documents (packed survivors)
-    if (rc == HM_OK && s->incremental)
-        SCHK(s, hm_launch_inc_meta(dev_list, n, s->dm, s->res_docs, s->changes, s->hist, s->ckey, s->ops, s->surv, s->smeta,
-                                   s->ist, st));
+    if (rc == HM_OK && s->incremental) {
+        MetaArgs M;
+        M.list = dev_list; M.n = n; M.dm = s->dm; M.res_docs = s->res_docs; M.changes = s->changes; M.hist = s->hist;
+        M.ckey = s->ckey; M.ops = s->ops; M.surv = s->surv; M.smeta = s->smeta; M.ist = s->ist;
+        M.epos = s->epos; M.epar = s->epar; M.ekey = s->ekey; M.lorder = s->lorder;
+        SCHK(s, hm_launch_inc_meta(M, st));
+    }
     SCHK(s, hipStreamSynchronize(st));
     return rc;
 }
@@ -291,11 +298,12 @@ int compact(hm_store *s, size_t extra_c, size_t extra_d, size_t extra_o, size_t 
     const size_t no = std::max<size_t>(2 * live_o, 1 << 16), nr = std::max<size_t>(2 * live_r, 1 << 16);
     hm_change_row *ch; int32_t *hi; uint32_t *ad; hm_dep_row *dp; hm_op_row *op; hm_surv_result *sv; hm_reg_result *rg;
     uint2 *sm;
-    uint32_t *ck;
+    uint32_t *ck, *ep, *epr, *ek, *lo;
     int r;
     if ((r = dev_alloc(s, &ch, nc)) || (r = dev_alloc(s, &hi, nc)) || (r = dev_alloc(s, &ck, nc)) || (r = dev_alloc(s, &ad, nc * S)) ||
         (r = dev_alloc(s, &dp, nd)) || (r = dev_alloc(s, &op, no)) || (r = dev_alloc(s, &sv, no)) ||
-        (r = dev_alloc(s, &sm, no)) || (r = dev_alloc(s, &rg, nr)))
+        (r = dev_alloc(s, &sm, no)) || (r = dev_alloc(s, &rg, nr)) || (r = dev_alloc(s, &ep, nr)) ||
+        (r = dev_alloc(s, &epr, nr)) || (r = dev_alloc(s, &ek, nr)) || (r = dev_alloc(s, &lo, nr)))
         return r;
     // relocate every document (old rows only; no new rows, no remap)
     std::vector<AppendDesc> descs(n);
@@ -332,6 +340,8 @@ int compact(hm_store *s, size_t extra_c, size_t extra_d, size_t extra_o, size_t 
     }
     (void)hipFree(s->changes); (void)hipFree(s->hist); (void)hipFree(s->ckey); (void)hipFree(s->all_deps); (void)hipFree(s->deps);
     (void)hipFree(s->ops); (void)hipFree(s->surv); (void)hipFree(s->smeta); (void)hipFree(s->regs);
+    (void)hipFree(s->epos); (void)hipFree(s->epar); (void)hipFree(s->ekey); (void)hipFree(s->lorder);
+    s->epos = ep; s->epar = epr; s->ekey = ek; s->lorder = lo;
     s->changes = ch; s->hist = hi; s->ckey = ck; s->all_deps = ad; s->deps = dp; s->ops = op; s->surv = sv; s->smeta = sm; s->regs = rg;
     s->cap_c = nc; s->cap_d = nd; s->cap_o = no; s->cap_r = nr;
     const unsigned long long bump[4] = {uc, ud, uo, ur};
@@ -367,7 +377,8 @@ int hm_store_create(hm_engine *e, const hm_store_config *cfg, hm_store **out) {
 void hm_store_destroy(hm_store *s) {
     if (!s) return;
     (void)hipStreamSynchronize(hm_engine_stream(s->e));
-    void *bufs[] = {s->changes, s->hist, s->ckey, s->all_deps, s->deps, s->ops, s->surv, s->smeta, s->ist, s->regs, s->res_docs, s->clock,
+    void *bufs[] = {s->changes, s->hist, s->ckey, s->all_deps, s->deps, s->ops, s->surv, s->smeta, s->ist, s->regs, s->epos,
+                    s->epar, s->ekey, s->lorder, s->res_docs, s->clock,
                     s->back_clock, s->heads, s->min_clock, s->stored, s->stage.p, s->dm, s->seen, s->plan.p, s->descs.p,
                     s->bdescs.p, s->list.p, s->blist.p, s->remap.p, s->inv.p, s->rows.p, s->undo_handles.p, s->st};
     for (void *b : bufs) if (b) (void)hipFree(b);
@@ -491,6 +502,7 @@ static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handl
             IA.st_changes = A.changes; IA.st_deps = t_dp; IA.st_ops = t_op;
             IA.changes = s->changes; IA.deps = s->deps; IA.ops = s->ops; IA.hist = s->hist; IA.ckey = s->ckey; IA.all_deps = s->all_deps;
             IA.regs = s->regs; IA.surv = s->surv; IA.smeta = s->smeta; IA.res_docs = s->res_docs;
+            IA.epos = s->epos; IA.epar = s->epar; IA.ekey = s->ekey; IA.lorder = s->lorder;
             IA.clock = s->clock; IA.back_clock = s->back_clock; IA.heads = s->heads; IA.min_clock = s->min_clock;
             IA.ist = s->ist; IA.bail = bail; IA.defer = (uint32_t *)(sp + L.o_defer);
             SCHK(s, hm_launch_inc_apply(IA, st));

@@ -83,6 +83,11 @@ static_assert(sizeof(IncState) == 32, "IncState is 32 B");
 // incremental path finds a fold source in a few 64-byte lines instead of the 24-byte change rows
 // (documents with a seq >= 2^24 are not packed: HM_IST_NOCKEY, they re-merge)
 #define HM_IST_NOCKEY 2u
+// the document has exactly one list / text object and its order is resident: lorder[reg slot k]
+// = the element register at position k (every inserted element, visible or not), per element
+// register epos (its position), epar (parent element register | HM_HEAD) and ekey (elem << 8 |
+// actor: lamportCompare's key); IncState.pad[0] = elements, pad[1] = the list's object id
+#define HM_IST_LIST 4u
 __host__ __device__ inline uint32_t hm_ckey(uint32_t actor, uint32_t seq, bool applied) {
     return (seq & 0xFFFFFFu) | ((actor & 0x7Fu) << 24) | (applied ? 0x80000000u : 0u);
 }
@@ -104,6 +109,7 @@ struct IncArgs {
     hm_reg_result *regs;
     hm_surv_result *surv;
     uint2 *smeta;
+    uint32_t *epos, *epar, *ekey, *lorder;     // list order (reg space), HM_IST_LIST documents
     hm_doc_result *res_docs;
     uint32_t *clock, *back_clock, *heads;
     const uint32_t *min_clock;
@@ -156,9 +162,23 @@ hipError_t hm_launch_read_regs_h(uint32_t n, const uint32_t *handles, const uint
 // then the documents it handed over (defer list) one per wave; the rest listed in bail
 hipError_t hm_launch_inc_apply(const IncArgs &A, hipStream_t s);
 // survivor metadata / IncState of re-merged documents (so the next submit can go incremental)
-hipError_t hm_launch_inc_meta(const uint32_t *list, uint32_t n, const DevDoc *dm, const hm_doc_result *res_docs,
-                              const hm_change_row *changes, const int32_t *hist, uint32_t *ckey, const hm_op_row *ops,
-                              const hm_surv_result *surv, uint2 *smeta, IncState *ist, hipStream_t s);
+struct MetaArgs {
+    const uint32_t *list;
+    uint32_t n;
+    const DevDoc *dm;
+    const hm_doc_result *res_docs;
+    const hm_change_row *changes;
+    const int32_t *hist;
+    uint32_t *ckey;
+    const hm_op_row *ops;
+    const hm_surv_result *surv;
+    uint2 *smeta;
+    IncState *ist;
+    uint32_t *epos, *epar, *ekey, *lorder;
+};
+hipError_t hm_launch_inc_meta(const MetaArgs &a, hipStream_t s);
+// element positions of the listed list documents reset (HM_NONE) before their re-merge writes them
+hipError_t hm_launch_epos_clear(const uint32_t *list, uint32_t n, const DevDoc *dm, uint32_t *epos, hipStream_t s);
 hipError_t hm_launch_append(const AppendDesc *descs, uint32_t n_desc, const StoreArenas &src, const StoreArenas &dst,
                             const hm_change_row *st_changes, const hm_dep_row *st_deps, const hm_op_row *st_ops,
                             const uint8_t *remap, uint32_t S, hipStream_t s);

@@ -263,7 +263,7 @@ __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
     const uint32_t tgt = r.n_deps + r.n_changes;
     const bool inc = live && a.incremental && last.status == HM_OK && last.n_queued == 0 && !remapped && r.n_changes > 0 &&
                      r.n_changes <= HM_INC_MAX_NEW_C && r.n_ops <= HM_INC_MAX_NEW_O && tgt <= HM_INC_MAX_TGT &&
-                     m.n_r <= r.n_regs && r.n_actors <= a.S && !((m.flags | r.flags) & HM_DOC_HAS_LISTS);
+                     m.n_r <= r.n_regs && r.n_actors <= a.S;
     p.inc = inc ? 1u : 0u;
     p.remapped = remapped ? 1u : 0u;
     if (live) a.plan[i] = p;

@@ -206,6 +206,8 @@ def test_bad_remap_leaves_store_unchanged(engine):
     ("C4", 200, {}, 6, 0.9, 16),                           # 16 lanes per document (inc_group_kernel<16>)
     ("C2", 120, {}, 8, 0.9, 64),                           # one document per wave (inc_group_kernel<64>)
     ("C4", 200, {}, 8, 0.9, 8),                            # up to 8 changes per call: some documents handed to the wave kernel
+    ("C3", 40, {"changes_per_actor": 240}, 2, 0.9, 8),     # text: inserts / deletes on the resident element order
+    ("C3", 20, {"changes_per_actor": 30, "arrival": 2, "shuffle_pct": 20}, 3, True, 8),   # text, shuffled arrivals
 ])
 def test_incremental_apply_equals_full_remerge(engine, name, n, extra, hi, expect_inc, S):
     """applyRemoteChanges with 1..hi new changes per document per call
@@ -374,3 +376,45 @@ def test_device_submit_equals_host_submit(engine):
         _, gb = B.read(hb + i)
         for f in ("hist", "all_deps", "regs", "surv", "clock", "heads"):
             np.testing.assert_array_equal(getattr(ga, f), getattr(gb, f), err_msg=f)
+
+
+def _text_rounds():
+    """A text object edited round by round: typing at the end, at the head, in the middle after an
+    element that already has children (a larger elem counter: first child), a concurrent insert
+    that sorts after an existing child (the re-merge's case), deletes, an insert after a deleted
+    element, a value overwrite, a run of inserts in one change, and a map key beside the text."""
+    T = "text-1"
+    A, B = "aaaa", "bbbb"
+    rounds = [[ch(A, 1, {}, mk("makeText", T), link("t", T), ins(T, "_head", 1), s(f"{A}:1", "h", T),
+                  ins(T, f"{A}:1", 2), s(f"{A}:2", "e", T))]]
+    rounds.append([ch(A, 2, {}, ins(T, f"{A}:2", 3), s(f"{A}:3", "y", T))])                    # typing at the end
+    rounds.append([ch(B, 1, {A: 2}, ins(T, "_head", 4), s(f"{B}:4", "<", T))])                 # at the head
+    rounds.append([ch(B, 2, {A: 2}, ins(T, f"{A}:1", 5), s(f"{B}:5", "+", T))])                # after h: first child
+    rounds.append([ch(A, 3, {A: 2}, ins(T, f"{A}:1", 4), s(f"{A}:4", "x", T))])                # concurrent, sorts later
+    rounds.append([ch(A, 4, {B: 2}, d(f"{A}:2", T)), ch(B, 3, {A: 3}, s(f"{A}:3", "Y", T))])    # delete, overwrite
+    rounds.append([ch(B, 4, {A: 4, B: 3}, ins(T, f"{A}:2", 9), s(f"{B}:9", "!", T),             # after a deleted one
+                      ins(T, f"{B}:9", 10), s(f"{B}:10", "?", T), ins(T, f"{B}:10", 11), s(f"{B}:11", ".", T),
+                      s("title", "doc"))])
+    rounds.append([ch(A, 5, {B: 4}, d(f"{B}:10", T), ins(T, f"{B}:11", 12), s(f"{A}:12", "z", T)),
+                   ch(A, 6, {}, ins(T, f"{A}:12", 13), s(f"{A}:13", "w", T))])
+    return rounds
+
+
+def test_incremental_text_edits_equal_remerge_and_oracle(engine):
+    """Row a11 on the incremental path: list / text ops applied on the resident element order
+    (lorder / epos), each call equal to the whole-log re-merge and to the oracle's cold merge."""
+    rounds = _text_rounds()
+    A, B = DocStore(engine, a_stride=8), DocStore(engine, a_stride=8)
+    B.set_incremental(False)
+    ha, hb = A.open(), B.open()
+    routed = []
+    for i, r in enumerate(rounds):
+        ra, rb = A.apply([(ha, r)]), B.apply([(hb, r)])
+        routed.append(A.last_routing()["incremental"])
+        for f in ("docs", "clock", "back_clock", "heads"):
+            np.testing.assert_array_equal(getattr(ra, f), getattr(rb, f), err_msg=f"{f} round {i}")
+        assert int(ra.docs["status"][0]) == 0, (i, ra.docs)
+        bb, g = assert_doc_matches_oracle(A, ha)
+        _, gb = B.read(hb)
+        np.testing.assert_array_equal(g.regs, gb.regs, err_msg=f"round {i}")
+    assert sum(routed[1:]) >= len(rounds) - 3, routed          # the sorts-later insert re-merges
