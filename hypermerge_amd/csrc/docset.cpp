@@ -386,7 +386,7 @@ struct Round {
     // placement in this call
     uint8_t cls = NO_CLASS;
     uint32_t handle = 0, row = 0;
-    bool moved = false, placed = false;
+    bool moved = false, placed = false, fresh = false;       // fresh: handle taken for it in this call
     hm_doc_result res = {};
     const uint32_t *clock = nullptr, *back = nullptr, *heads = nullptr;
     bool full = false;                                       // patch from every register (else the hit ones)
@@ -1171,6 +1171,8 @@ struct hm_docset {
     bool binary = false;                                     // HM_DOCSET_BINARY results
     bool op_diffs = true;                                    // Automerge's per-op diff sequence (else HM_DOCSET_NET_DIFFS)
     hm_store *stores[N_CLASS] = {};
+    std::vector<uint32_t> free_h[N_CLASS];                   // released handles (empty documents), reused first
+    uint32_t opened[N_CLASS] = {};                           // handles opened per store
     // documents: fixed chunks, so hm_docset_open may run while a call works on earlier documents
     static constexpr uint32_t CHUNK = 4096;
     std::vector<std::unique_ptr<DocSt[]>> chunks;
@@ -1282,11 +1284,21 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
         hm_store *st;
         if ((rc = store_of(ds, c, &st))) break;
         const uint32_t S = STRIDES[c];
-        // fresh handles for placed and moved documents
+        // fresh handles for placed and moved documents: released ones first, then new ones
         uint32_t fresh = 0;
         for (uint32_t i : rows) fresh += R[i].placed || R[i].moved;
-        uint32_t h0 = 0;
-        if (fresh && (rc = hm_doc_open_n(st, fresh, &h0))) break;
+        std::vector<uint32_t> fh;
+        size_t next_fh = 0;
+        {
+            std::vector<uint32_t> &fl = ds->free_h[c];
+            const size_t k = std::min<size_t>(fresh, fl.size());
+            fh.assign(fl.end() - k, fl.end());
+            fl.resize(fl.size() - k);
+            uint32_t h0 = 0;
+            if (fresh > k && (rc = hm_doc_open_n(st, fresh - (uint32_t)k, &h0))) { fl.insert(fl.end(), fh.begin(), fh.end()); break; }
+            ds->opened[c] += fresh - (uint32_t)k;
+            for (uint32_t j = 0; j < fresh - k; j++) fh.push_back(h0 + j);
+        }
         std::vector<hm_doc_row> drows(rows.size());
         std::vector<hm_change_row> ch;
         std::vector<hm_dep_row> dp;
@@ -1310,7 +1322,7 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
             r = hm_doc_row{};
             r.change_off = (uint32_t)ch.size(); r.dep_off = (uint32_t)dp.size(); r.op_off = (uint32_t)op.size();
             const uint32_t c0 = (uint32_t)ch.size(), d0 = (uint32_t)dp.size(), o0 = (uint32_t)op.size();
-            if (x.placed || x.moved) x.handle = h0++;
+            if (x.placed || x.moved) { x.handle = fh[next_fh++]; x.fresh = true; }
             hand[k] = x.handle;
             if (x.moved) {
                 // the whole log moves: its rows from the old store, ranks re-mapped to this round's
@@ -1340,6 +1352,8 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
             r.n_regs = x.n_regs; r.n_objs = x.n_objs; r.n_actors = x.n_actors;
             r.flags = (uint16_t)(x.flags | (x.moved ? d.flags : 0));
         }
+        // handles taken but not handed to a document (a failed log read) are still empty
+        ds->free_h[c].insert(ds->free_h[c].end(), fh.begin() + next_fh, fh.end());
         if (rc) break;
         hm_batch b = {};
         b.n_docs = (uint32_t)rows.size(); b.n_changes = (uint32_t)ch.size(); b.n_deps = (uint32_t)dp.size(); b.n_ops = (uint32_t)op.size();
@@ -1360,10 +1374,23 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
             x.clock = O.clock.data() + (size_t)k * S; x.back = O.back.data() + (size_t)k * S; x.heads = O.heads.data() + (size_t)k * S;
         }
     }
+    // released handles (a moved document's old one, a fresh one its document does not keep) go
+    // back to their store as empty documents (hm_doc_reset) and are reused by later calls; their
+    // rows are reclaimed when the store compacts
+    std::vector<std::vector<uint32_t>> rel(N_CLASS);
+    auto release = [&]() {
+        for (uint32_t c = 0; c < N_CLASS; c++) {
+            if (rel[c].empty()) continue;
+            if (hm_doc_reset(ds->stores[c], rel[c].data(), (uint32_t)rel[c].size()) == HM_OK)
+                ds->free_h[c].insert(ds->free_h[c].end(), rel[c].begin(), rel[c].end());
+            rel[c].clear();
+        }
+    };
     // a call-level failure: the call is applied to no store — a store whose batch is in flight is
     // waited for, the batches already applied are undone (hm_batch_undo) — and every document of
     // the call rolls back on the host
     auto fail_call = [&](int why) {
+        for (auto &v : rel) v.clear();                       // (every fresh handle is listed below)
         for (uint32_t c = 0; c < N_CLASS; c++) {
             if (co[c].sub) {
                 std::vector<hm_doc_result> tmp(by_cls[c].size());
@@ -1372,7 +1399,11 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
             }
             if (co[c].done) { (void)hm_batch_undo(ds->stores[c], co[c].id); co[c].done = false; }
         }
-        for (uint32_t i = 0; i < n; i++) if (R[i].status == HM_OK) rollback(ds->doc(R[i].doc), R[i]);
+        for (uint32_t i = 0; i < n; i++) {
+            if (R[i].status == HM_OK) rollback(ds->doc(R[i].doc), R[i]);
+            if (R[i].fresh) rel[R[i].cls].push_back(R[i].handle);
+        }
+        release();
         return why;
     };
     if (rc) return fail_call(rc);
@@ -1388,6 +1419,7 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
         if (x.status != HM_OK) {
             if (x.cls != NO_CLASS) rollback(d, x);
             if (x.placed) { d.cls = x.cls; d.handle = x.handle; }          // an empty document in its store
+            else if (x.moved) rel[x.cls].push_back(x.handle);               // it stays where it was
             continue;
         }
         x.prev_hist = d.hist_len;
@@ -1452,6 +1484,7 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
         if (x.status != HM_OK) continue;
         DocSt &d = ds->doc(x.doc);
         const uint32_t old_n_ops = d.n_ops;
+        if (x.moved) rel[d.cls].push_back(d.handle);
         d.cls = x.cls; d.handle = x.handle;
         d.flags |= x.flags;
         d.n_changes += (uint32_t)x.ch.size();
@@ -1475,6 +1508,7 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
             d.el_blk.resize(x.n_regs, HM_NONE);
         }
     }
+    release();
     mark("read regs");
     // render every document's patch and DocBackend.clock
     auto round_clock = [](const Round &x, uint32_t *rc) {      // this call's changes alone (updateClock(changes))
@@ -1828,6 +1862,13 @@ int hm_docset_view(hm_docset *ds, uint32_t doc, hm_text **out) {
     } catch (...) {
         return hm_engine_fail(ds->e, HM_ERR_NOMEM, "exception in hm_docset_view");
     }
+}
+
+int hm_docset_handles(const hm_docset *ds, uint32_t a_stride, uint32_t *out_opened, uint32_t *out_free) {
+    if (!ds || !out_opened || !out_free) return HM_ERR_INVALID;
+    for (uint32_t c = 0; c < N_CLASS; c++)
+        if (STRIDES[c] == a_stride) { *out_opened = ds->opened[c]; *out_free = (uint32_t)ds->free_h[c].size(); return HM_OK; }
+    return HM_ERR_INVALID;
 }
 
 int hm_docset_stats(const hm_docset *ds, uint64_t *out8) {

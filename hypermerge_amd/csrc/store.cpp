@@ -413,6 +413,30 @@ int hm_doc_open_n(hm_store *s, uint32_t n, uint32_t *out_first) {
     }
 }
 
+int hm_doc_reset(hm_store *s, const uint32_t *doc_handles, uint32_t n) {
+    if (!s || (n && !doc_handles)) return HM_ERR_INVALID;
+    try {
+        if (s->pending) return hm_engine_fail(s->e, HM_ERR_INVALID, "hm_doc_reset while a batch is in flight");
+        if (!n) return HM_OK;
+        std::vector<uint32_t> hs(doc_handles, doc_handles + n);
+        std::sort(hs.begin(), hs.end());
+        if (hs.back() >= s->n_handles) return hm_engine_fail(s->e, HM_ERR_INVALID, "hm_doc_reset: bad handle");
+        if (std::adjacent_find(hs.begin(), hs.end()) != hs.end())
+            return hm_engine_fail(s->e, HM_ERR_INVALID, "hm_doc_reset: repeated handle");
+        int r;
+        if ((r = ensure_buf(s, s->blist, n))) return r;
+        hipStream_t st = hm_engine_stream(s->e);
+        SCHK(s, hipMemcpyAsync(s->blist.p, hs.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
+        SCHK(s, hm_launch_reset_docs(s->blist.p, n, s->dm, s->res_docs, s->ist, s->clock, s->back_clock, s->heads, s->min_clock,
+                                     s->stored, s->S, st));
+        SCHK(s, hipStreamSynchronize(st));
+        s->undo_id = 0;                               // the last batch's undo no longer applies
+        return HM_OK;
+    } catch (...) {
+        return HM_ERR_NOMEM;
+    }
+}
+
 // hm_batch_submit / hm_batch_submit_device: `dev` = the batch's tables, handles and remap are
 // device pointers (no host staging of the rows)
 static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handles, const uint8_t *actor_remap,

@@ -148,6 +148,9 @@ hipError_t hm_launch_rollback(const uint32_t *handles, uint32_t n, const hm_doc_
                               const uint8_t *remap, uint32_t S, DevDoc *dm, AppendDesc *descs, uint8_t *inv,
                               uint32_t *list, PlanStats *st, uint32_t every, hipStream_t s);
 hipError_t hm_launch_init_docs(DevDoc *dm, uint32_t h0, uint32_t n, hipStream_t s);
+hipError_t hm_launch_reset_docs(const uint32_t *handles, uint32_t n, DevDoc *dm, hm_doc_result *res, IncState *ist,
+                                uint32_t *clock, uint32_t *back, uint32_t *heads, uint32_t *minc, uint32_t *stored,
+                                uint32_t S, hipStream_t s);
 // chosen registers of resident documents by (handle, register): validated on the device
 hipError_t hm_launch_read_hist(uint32_t n, const uint32_t *handles, const uint32_t *from, const uint32_t *to,
                                const uint32_t *out_off, const DevDoc *dm, uint32_t n_handles, const int32_t *hist,

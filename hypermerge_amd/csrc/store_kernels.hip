@@ -393,6 +393,27 @@ __global__ void init_docs_kernel(DevDoc *dm, uint32_t h0, uint32_t n) {
     dm[h0 + i] = m;
 }
 
+// hm_doc_reset: the listed handles back to the empty document (init_docs_kernel's row, the
+// Backend.init() result row, zero clocks and incremental state); one thread per handle
+__global__ void reset_docs_kernel(const uint32_t *handles, uint32_t n, DevDoc *dm, hm_doc_result *res, IncState *ist,
+                                  uint32_t *clock, uint32_t *back, uint32_t *heads, uint32_t *minc, uint32_t *stored,
+                                  uint32_t S) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t h = handles[i];
+    DevDoc m = {};
+    m.n_objs = 1;
+    dm[h] = m;
+    hm_doc_result r = {};
+    r.err_change = HM_NONE; r.err_op = HM_NONE;
+    res[h] = r;
+    ist[h] = IncState{};
+    for (uint32_t a = 0; a < S; a++) {
+        const size_t k = (size_t)h * S + a;
+        clock[k] = 0; back[k] = 0; heads[k] = 0; minc[k] = 0; stored[k] = 0;
+    }
+}
+
 __global__ void read_regs_h_kernel(uint32_t n, const uint32_t *handles, const uint32_t *regs, const DevDoc *dm,
                                    uint32_t n_handles, const hm_reg_result *rr, const hm_surv_result *surv,
                                    hm_reg_result *out_regs, hm_surv_result *out_surv, uint32_t cap, uint32_t *counter,
@@ -462,6 +483,14 @@ hipError_t hm_launch_rollback(const uint32_t *handles, uint32_t n, const hm_doc_
 hipError_t hm_launch_init_docs(DevDoc *dm, uint32_t h0, uint32_t n, hipStream_t s) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(hms::init_docs_kernel, dim3((n + 255) / 256), dim3(256), 0, s, dm, h0, n);
+    return hipGetLastError();
+}
+hipError_t hm_launch_reset_docs(const uint32_t *handles, uint32_t n, DevDoc *dm, hm_doc_result *res, IncState *ist,
+                                uint32_t *clock, uint32_t *back, uint32_t *heads, uint32_t *minc, uint32_t *stored,
+                                uint32_t S, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(hms::reset_docs_kernel, dim3((n + 255) / 256), dim3(256), 0, s, handles, n, dm, res, ist, clock, back,
+                       heads, minc, stored, S);
     return hipGetLastError();
 }
 hipError_t hm_launch_read_regs_h(uint32_t n, const uint32_t *handles, const uint32_t *regs, const DevDoc *dm,

@@ -109,6 +109,13 @@ class DocSet:
         s, _ = _text(self._L, t)
         return json.loads(s)
 
+    def handles(self, a_stride: int) -> Dict[str, int]:
+        """hm_docset_handles: handles opened in the a_stride store and released ones awaiting reuse."""
+        o, f = ctypes.c_uint32(), ctypes.c_uint32()
+        self.engine._check(self._L.hm_docset_handles(self._h, a_stride, ctypes.byref(o), ctypes.byref(f)),
+                           "hm_docset_handles")
+        return {"opened": o.value, "free": f.value}
+
     def stats(self) -> Dict[str, int]:
         out = np.zeros(8, np.uint64)
         self.engine._check(self._L.hm_docset_stats(self._h, out.ctypes.data), "hm_docset_stats")

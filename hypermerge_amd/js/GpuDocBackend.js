@@ -423,6 +423,7 @@ class GpuEngine {
     const finish = () => { try { this.raise(errors) } finally { done() } }
     for (const g of gs) {
       GpuEngine.prepare(g)
+      // in place: prepare() built g.data for this call alone and nothing touches it again
       addon.docsetApplyPacked(g.ds, g.ids, g.data, g.ends, g.docBlock, (err, r) => {
         try {
           if (err) g.items.forEach(({ job }) => errors.push([job, err]))
@@ -430,7 +431,7 @@ class GpuEngine {
         } finally {
           if (--left === 0) finish()
         }
-      })
+      }, true)
     }
   }
 

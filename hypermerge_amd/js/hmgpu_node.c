@@ -554,6 +554,7 @@ typedef struct DsJob {
     struct DsJob *next;
     uint8_t *data;
     napi_ref data_ref;                  /* packed calls: data is the caller's Buffer, held by this reference */
+    int borrowed;                       /* synchronous packed calls: data is the caller's Buffer, read before returning */
     uint64_t *bo;
     uint32_t *db, *ids, n;
     int st;
@@ -576,7 +577,7 @@ typedef struct {
 static void ds_job_free(napi_env env, DsJob *j) {
     if (!j) return;
     if (j->data_ref) { if (env) napi_delete_reference(env, j->data_ref); }
-    else free(j->data);
+    else if (!j->borrowed) free(j->data);
     free(j->bo); free(j->db); free(j->ids);
     if (j->out) hm_text_free(j->out);
     free(j);
@@ -720,7 +721,10 @@ static int gather_blocks(napi_env env, napi_value ids_v, napi_value blocks_v, Ds
  * ends (Uint32Array: end offset of each block), docBlock (Uint32Array n + 1: first block of each
  * document) — one copy, no per-block N-API calls (1.3M blocks per 20k-document round cost the
  * main thread ~1 s through napi_get_element / typeof / buffer info) */
-static int gather_packed(napi_env env, napi_value ids_v, napi_value data_v, napi_value ends_v, napi_value db_v, DsJob *j) {
+/* mode 0: copy `data`; 1: hold it by a reference and read it in place (async); 2: read it in
+ * place (synchronous: the call is done before JS runs again) */
+static int gather_packed(napi_env env, napi_value ids_v, napi_value data_v, napi_value ends_v, napi_value db_v, int mode,
+                         DsJob *j) {
     void *ip, *dp, *ep, *bp; size_t il, dl, el, bl;
     if (!get_bytes(env, ids_v, &ip, &il) || !get_bytes(env, data_v, &dp, &dl) || !get_bytes(env, ends_v, &ep, &el) ||
         !get_bytes(env, db_v, &bp, &bl))
@@ -743,9 +747,11 @@ static int gather_packed(napi_env env, napi_value ids_v, napi_value data_v, napi
     memcpy(j->db, db, ((size_t)n + 1) * 4);
     j->bo[0] = 0;
     for (uint32_t b = 0; b < nb; b++) j->bo[b + 1] = ends[b];
-    /* the blocks are read where they lie: the Buffer is held until the call has called back
-     * (GpuEngine.prepare builds it for this call and never writes it again) */
-    if (dl && napi_create_reference(env, data_v, 1, &j->data_ref) == napi_ok) j->data = (uint8_t *)dp;
+    /* copied by default; in place only when the caller promises the Buffer is its own and is
+     * neither written nor transferred until the call has called back (GpuEngine.prepare builds
+     * it for this call and never touches it again) — the Buffer is then held by a reference */
+    if (mode == 2) { j->borrowed = 1; j->data = (uint8_t *)dp; }
+    else if (mode == 1 && dl && napi_create_reference(env, data_v, 1, &j->data_ref) == napi_ok) j->data = (uint8_t *)dp;
     else {
         j->data_ref = NULL;
         j->data = (uint8_t *)malloc(dl + 1);
@@ -800,8 +806,8 @@ static void ds_call_js(napi_env env, napi_value cb, void *context, void *data) {
  * thread when it is done; further async calls queue behind it (run in call order), any other
  * docset call except docsetOpen throws until every queued round has called back */
 static napi_value docset_apply(napi_env env, napi_callback_info info, int packed) {
-    napi_value argv[6];
-    size_t argc = 6;
+    napi_value argv[7];
+    size_t argc = 7;
     const size_t need = packed ? 5 : 3;
     if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < need) {
         napi_throw_type_error(env, NULL, "missing arguments");
@@ -815,7 +821,10 @@ static napi_value docset_apply(napi_env env, napi_callback_info info, int packed
     Docset *d = cbt == napi_function ? get_docset_any(env, argv[0]) : get_docset(env, argv[0]);
     if (!d) return NULL;
     DsJob *j = (DsJob *)calloc(1, sizeof(DsJob));
-    if (!(packed ? gather_packed(env, argv[1], argv[2], argv[3], argv[4], j) : gather_blocks(env, argv[1], argv[2], j))) {
+    bool in_place = false;
+    if (packed && argc > need + 1) napi_get_value_bool(env, argv[need + 1], &in_place);
+    if (!(packed ? gather_packed(env, argv[1], argv[2], argv[3], argv[4], cbt != napi_function ? 2 : in_place ? 1 : 0, j)
+                 : gather_blocks(env, argv[1], argv[2], j))) {
         ds_job_free(env, j);
         return NULL;
     }
@@ -854,9 +863,10 @@ static napi_value docset_apply(napi_env env, napi_callback_info info, int packed
 }
 
 static napi_value DocsetApply(napi_env env, napi_callback_info info) { return docset_apply(env, info, 0); }
-/* docsetApplyPacked(docset, ids, data, blockEnds, docBlock, callback?): docsetApply with the
- * blocks packed by the caller (gather_packed).  `data` is read in place: with a callback the
- * caller must not write it until the callback has run */
+/* docsetApplyPacked(docset, ids, data, blockEnds, docBlock, callback?, inPlace?): docsetApply
+ * with the blocks packed by the caller (gather_packed).  A synchronous call reads `data` in
+ * place; an async call copies it unless inPlace is true: then the caller must neither write nor
+ * transfer it until the callback has run */
 static napi_value DocsetApplyPacked(napi_env env, napi_callback_info info) { return docset_apply(env, info, 1); }
 
 /* docsetHistoryPrefix(docset, doc, n) -> Buffer of u32 log indices (history order) */

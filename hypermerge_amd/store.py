@@ -249,6 +249,15 @@ class DocStore:
         self.enc.append(DocEncoder(self.pool))
         return h.value
 
+    def reset(self, handles) -> None:
+        """hm_doc_reset: the handles become empty documents again (their rows are dead space
+        until the store compacts)."""
+        hs = np.ascontiguousarray(handles, np.uint32)
+        self._check(self._L.hm_doc_reset(self._h, _p(hs), len(hs)), "hm_doc_reset")
+        for h in hs:
+            if h < len(self.enc):
+                self.enc[h] = DocEncoder(self.pool)
+
     # -- applyChanges over many documents -----------------------------------------------------
     def submit(self, items: Sequence[Tuple[int, Sequence[Dict[str, Any]]]],
                extra_actors: Optional[Dict[int, Sequence[str]]] = None) -> int:

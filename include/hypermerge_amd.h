@@ -291,6 +291,13 @@ int hm_doc_open(hm_store *s, uint32_t *out_doc);
 /* n new, empty documents with consecutive handles starting at *out_first. */
 int hm_doc_open_n(hm_store *s, uint32_t n, uint32_t *out_first);
 
+/* Release n documents: each handle becomes an empty document again (as hm_doc_open made it,
+ * ready for reuse) and its old rows are dead space that the next compaction reclaims.
+ * Not while a batch is in flight; the handles must be distinct.  (No reference counterpart:
+ * the docset's restride (a document moving to a wider actor class) releases its old handle
+ * with it instead of leaking its rows.) */
+int hm_doc_reset(hm_store *s, const uint32_t *doc_handles, uint32_t n);
+
 /* Append new changes to documents and re-merge them.  `b` is a batch in the
  * hm_batch layout whose rows are only the NEW changes (offsets local to `b`);
  * for each row i, docs[i].n_actors / n_regs / n_objs are document totals
@@ -556,6 +563,9 @@ int hm_docset_view(hm_docset *ds, uint32_t doc, hm_text **out);
  * register, per-op patches, per-op replays whose registers differ from the device's merged state
  * (always 0 unless the renderer and the kernels disagree) */
 int hm_docset_stats(const hm_docset *ds, uint64_t *out8);
+/* The store of class a_stride (8, 16, 32, 64, 128, 256): handles opened in it and handles
+ * released (a document moved to a wider class; empty, reused before new ones are opened) */
+int hm_docset_handles(const hm_docset *ds, uint32_t a_stride, uint32_t *out_opened, uint32_t *out_free);
 
 /* ------------------------------------------------------------------ */
 /* Clock exchange across the node's GPUs (RCCL over xGMI)              */

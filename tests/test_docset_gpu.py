@@ -180,6 +180,46 @@ def test_docset_moves_documents_to_wider_stores():
     assert ds.stats()["moves"] > 0 and ds.stats()["replay_mismatch"] == 0
 
 
+def test_docset_moved_documents_release_their_handles():
+    """A document that moves to a wider store releases its old handle (hm_doc_reset): the
+    handle is an empty document again and the next documents placed in that store take it
+    instead of opening new ones; their rounds (incremental ones included) equal the oracle."""
+    from hypermerge_amd.columnar import ROOT_ID as R
+    from hypermerge_amd.docset import DocSet, render_objects, view_objects
+    from hypermerge_amd.engine import Engine
+
+    def chg(actor, seq, deps, key, value):
+        return {"actor": actor, "seq": seq, "deps": deps, "ops": [{"action": "set", "obj": R, "key": key, "value": value}]}
+    ds = DocSet(Engine(0))
+    a = ds.open(6)
+    logs = {}
+    first = {a + i: [chg(f"a{i}{j}", 1, {}, f"k{j % 3}", j) for j in range(5)] for i in range(6)}
+    ds.apply(list(first), [_blocks(v) for v in first.values()])
+    logs.update(first)
+    assert ds.handles(8) == {"opened": 6, "free": 0}
+    wide = {a + i: [chg(f"w{i}{j:02d}", 1, {}, f"k{j % 4}", 100 + j) for j in range(9)] for i in range(4)}
+    res, _ = ds.apply(list(wide), [_blocks(v) for v in wide.values()])
+    assert (res["status"] == 0).all()
+    for d, v in wide.items():
+        logs[d] = logs[d] + v
+        assert ds.info(d)["a_stride"] == 16
+    assert ds.handles(8) == {"opened": 6, "free": 4} and ds.handles(16)["opened"] == 4
+    b = ds.open(3)
+    for r in range(3):                                              # placed, then two incremental rounds
+        new = {b + i: [chg(f"b{i}", r + 1, {f"b{i}": r} if r else {}, f"k{r}", 10 * i + r)] for i in range(3)}
+        res, js = ds.apply(list(new), [_blocks(v) for v in new.values()])
+        assert (res["status"] == 0).all()
+        for k, (d, v) in enumerate(new.items()):
+            logs[d] = logs.get(d, []) + v
+            s = _oracle(logs[d])
+            assert js["p"][k]["clock"] == s["clock"] and js["b"][k] == s["backend_clock"]
+    assert ds.handles(8) == {"opened": 6, "free": 1}
+    for d, log in logs.items():
+        s = _oracle(log)
+        assert render_objects(view_objects(ds.view(d))) == json.loads(json.dumps(s["state"])), d
+        assert ds.info(d)["n_changes"] == len(log)
+
+
 def test_docset_clock_update_matches_reference_sql():
     """ClockStore.update(self, doc, doc.clock) after a round (src/ClockStore.ts:78-91): the
     first update writes, a repeat does not, and the stored clocks are the DocBackend clocks."""
