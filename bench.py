@@ -332,7 +332,7 @@ def _node_e2e(args):
         with open(fn, "w") as f:
             json.dump({"docs": [[d[k:k + 16] for k in range(0, len(d), 16)] for d in docs]}, f)
         del docs
-        p = subprocess.run([node, "--max-old-space-size=16384", os.path.join(here, "tools", "bench_node.js"), fn,
+        p = subprocess.run([node, "--max-old-space-size=16384", "--max-semi-space-size=64", os.path.join(here, "tools", "bench_node.js"), fn,
                             ",".join(legs)], capture_output=True, text=True, timeout=900)
     if p.returncode != 0:
         return {"error": p.stderr[-800:]}

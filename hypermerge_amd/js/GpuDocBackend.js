@@ -203,11 +203,32 @@ class History {
 
 // FNV-1a 64 over the UTF-8 bytes of an id string: the shard key (and the clock exchange's
 // record key) of hypermerge_amd/exchange.py and include/hypermerge_amd.h.
-const FNV_OFFSET = 0xcbf29ce484222325n, FNV_PRIME = 0x100000001b3n, M64 = (1n << 64n) - 1n
+// Computed on two 32-bit halves in plain Numbers (h * prime = h * 0x1b3 + h << 40; every partial
+// product stays below 2^53), the BigInt only built at the end.
+const TWO32 = 4294967296
+function fnvHalves(s) {
+  let lo = 0x84222325, hi = 0xcbf29ce4
+  const step = (b) => {
+    lo = (lo ^ b) >>> 0
+    const pl = lo * 0x1b3
+    const nlo = pl >>> 0
+    hi = (hi * 0x1b3 + Math.floor(pl / TWO32) + (lo & 0xffffff) * 256) >>> 0
+    lo = nlo
+  }
+  let ascii = true
+  for (let i = 0; i < s.length && ascii; i++) ascii = s.charCodeAt(i) < 0x80
+  if (ascii) for (let i = 0; i < s.length; i++) step(s.charCodeAt(i))
+  else for (const b of Buffer.from(s, 'utf8')) step(b)
+  return [hi, lo]
+}
 function fnv1a64(s) {
-  let h = FNV_OFFSET
-  for (const b of Buffer.from(s, 'utf8')) h = ((h ^ BigInt(b)) * FNV_PRIME) & M64
-  return h
+  const [hi, lo] = fnvHalves(s)
+  return (BigInt(hi) << 32n) | BigInt(lo)
+}
+// fnv1a64(s) % n without the BigInt ((hi * 2^32 + lo) mod n, n < 2^21)
+function fnvMod(s, n) {
+  const [hi, lo] = fnvHalves(s)
+  return ((hi % n) * (TWO32 % n) + (lo % n)) % n
 }
 
 // The per-document BackendState: a document of its shard's docset plus the log entries as
@@ -285,7 +306,7 @@ class GpuEngine {
     this.hash = o.hash || null       // the id -> 64-bit key function of the clock exchange (default FNV-1a64)
   }
 
-  shardOf(docId) { return Number(fnv1a64(docId) % BigInt(this.docsets.length)) }
+  shardOf(docId) { return fnvMod(docId, this.docsets.length) }
 
   init(docId) { return new GpuBackendState(this, docId) }
 
