@@ -64,6 +64,8 @@ def main() -> int:
     ap.add_argument("--no-node", action="store_true",
                     help="skip the Node DocBackend leg (C2 sample: JS restatement vs the GPU drop-in)")
     ap.add_argument("--node-docs", type=int, default=20000)
+    ap.add_argument("--node-text-docs", type=int, default=40, help="C3 documents of the Node leg (0: skip)")
+    ap.add_argument("--node-c5-docs", type=int, default=5000, help="C5 documents of the Node leg (0: skip)")
     ap.add_argument("--text-docs", type=int, default=10000, help="C3 documents in the resident text leg")
     ap.add_argument("--arrival", type=int, default=None,
                     help="override the config's arrival order (0 generation, 1 actor-major as RepoBackend.loadDocument "
@@ -306,6 +308,26 @@ def _from_blocks(eng, batch, cfg, args):
             "path": "JSON blocks -> hm_decode_blocks (native, multi-threaded) -> hm_merge_host (PCIe included)"}
 
 
+def _node_run(node, docs, legs, chunk=16, timeout=900):
+    """tools/bench_node.js over `docs` (each document's changes, fed in chunks of `chunk`)."""
+    import subprocess
+    import tempfile
+    here = os.path.dirname(os.path.abspath(__file__))
+    with tempfile.TemporaryDirectory() as td:
+        fn = os.path.join(td, "docs.json")
+        with open(fn, "w") as f:
+            json.dump({"docs": [[d[k:k + chunk] for k in range(0, len(d), chunk)] for d in docs]}, f)
+        p = subprocess.run([node, "--max-old-space-size=16384", "--max-semi-space-size=64",
+                            os.path.join(here, "tools", "bench_node.js"), fn, ",".join(legs)],
+                           capture_output=True, text=True, timeout=timeout)
+    if p.returncode != 0:
+        return {"error": p.stderr[-800:]}
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    out["same_clocks"] = len({out[k]["digest"] for k in legs}) == 1
+    out["same_state"] = len({out[k]["state_digest"] for k in legs}) == 1
+    return out
+
+
 def _node_e2e(args):
     """C2 documents fed through the DocBackend message API on one Node thread (tools/bench_node.js):
     init() with each document's first 16 changes, then one applyRemoteChanges round per further
@@ -314,37 +336,41 @@ def _node_e2e(args):
     the timed region; `gpu` / `gpu_async` are the drop-in (GpuDocBackend over the docset, batched /
     async mode, patch diffs on: Automerge's per-op diff sequence, the same diffs as the JS
     restatement) handed the raw blocks, `gpu_objects` the drop-in handed Change objects,
-    `gpu_async_net` the async drop-in with net diffs (one per changed register)."""
+    `gpu_async_net` the async drop-in with net diffs (one per changed register).  `C3` / `C5`:
+    text documents and nested maps / lists with out-of-order and duplicate delivery through the
+    same API (legs cpu and gpu_async, the same state required)."""
     import shutil
-    import subprocess
-    import tempfile
     node = shutil.which("node")
     if node is None:
         return {"skipped": "node not installed"}
     from hypermerge_amd import synth
     from hypermerge_amd.columnar import decode_doc
-    b = synth.generate(synth.config("C2", n_docs=args.node_docs), threads=min(16, os.cpu_count() or 1))
+    th = min(16, os.cpu_count() or 1)
+    b = synth.generate(synth.config("C2", n_docs=args.node_docs), threads=th)
     docs = [decode_doc(b, i) for i in range(b.n_docs)]
-    here = os.path.dirname(os.path.abspath(__file__))
     legs = ["cpu", "cpu_blocks", "gpu", "gpu_async", "gpu_objects", "gpu_async_net"]
-    with tempfile.TemporaryDirectory() as td:
-        fn = os.path.join(td, "c2.json")
-        with open(fn, "w") as f:
-            json.dump({"docs": [[d[k:k + 16] for k in range(0, len(d), 16)] for d in docs]}, f)
-        del docs
-        p = subprocess.run([node, "--max-old-space-size=16384", "--max-semi-space-size=64", os.path.join(here, "tools", "bench_node.js"), fn,
-                            ",".join(legs)], capture_output=True, text=True, timeout=900)
-    if p.returncode != 0:
-        return {"error": p.stderr[-800:]}
-    out = json.loads(p.stdout.strip().splitlines()[-1])
-    out["same_clocks"] = len({out[k]["digest"] for k in legs}) == 1
-    out["same_state"] = len({out[k]["state_digest"] for k in legs}) == 1
+    out = _node_run(node, docs, legs)
+    del docs
+    if "error" in out:
+        return out
     out["same_diff_count"] = len({out[k]["diffs"] for k in legs if k != "gpu_async_net"}) == 1
     out["sample"] = (f"C2: {b.n_docs} docs x 4 actors x 64 changes, 4 rounds of 16 changes per document "
                      f"(init + 3 applyRemoteChanges), one Node thread; blocks = JSON Change texts")
     out["gpu_async_vs_js"] = out["gpu_async"]["changes_per_s"] / out["cpu"]["changes_per_s"]
     out["gpu_async_vs_js_blocks"] = out["gpu_async"]["changes_per_s"] / out["cpu_blocks"]["changes_per_s"]
     out["gpu_vs_js"] = out["gpu"]["changes_per_s"] / out["cpu"]["changes_per_s"]
+    for name, n, over, desc in (("C3", args.node_text_docs, {},
+                                 "text documents x 8 actors, ~240 typing changes of ~15 ops each (80% insert / 20% delete)"),
+                                ("C5", args.node_c5_docs, {},
+                                 "nested maps / lists x 4 actors x 8 changes, 20% delivered before their deps, 3% duplicates")):
+        if n <= 0:
+            continue
+        bx = synth.generate(synth.config(name, n_docs=n, **over), threads=th)
+        r = _node_run(node, [decode_doc(bx, i) for i in range(bx.n_docs)], ["cpu", "gpu_async"])
+        if "error" not in r:
+            r["gpu_async_vs_js"] = r["gpu_async"]["changes_per_s"] / r["cpu"]["changes_per_s"]
+            r["sample"] = f"{name}: {bx.n_docs} {desc}; rounds of 16 changes per document"
+        out[name] = r
     return out
 
 

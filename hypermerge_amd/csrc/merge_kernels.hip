@@ -292,7 +292,12 @@ __device__ __forceinline__ void need_set(uint32_t &lo, uint32_t &hi, uint32_t a,
 }
 
 
-// the (actor, seq) table: NA_MAX x 64 words of all ones, two 16-byte stores per lane
+// the (actor, seq) table: NA_MAX x 64 words, slot-major (word s * NA_MAX + a for actor a's
+// s-th seq of the batch window): the lanes of a 32-lane half look up (actor, slot) pairs of
+// nearby arrivals — every actor at the same few slots — which an actor-major table (stride 64
+// words, bank = slot mod 32) put on a handful of banks (4-way conflicts on C4's 8 x 8 logs)
+__device__ __forceinline__ uint32_t fidx(uint32_t a, uint32_t s) { return (s & 63) * NA_MAX + (a & (NA_MAX - 1)); }
+// all ones, two 16-byte stores per lane
 __device__ __forceinline__ void clear_first(LDS uint32_t *first) {
     static_assert(NA_MAX * 64 == 2 * WAVE * 4, "first-table size");
     LDS uint4 *f4 = (LDS uint4 *)first;
@@ -475,7 +480,7 @@ __device__ __forceinline__ uint32_t fc_of(FoldView L, uint32_t h, uint32_t x) {
 }
 // history position of the applied change (a, s) (s >= 1, in this batch)
 __device__ __forceinline__ uint32_t hpos_of(FoldView L, uint32_t a, uint32_t s) {
-    return (uint32_t)L.hist_of[L.first[a * 64 + (s - L.base[a])]];
+    return (uint32_t)L.hist_of[L.first[fidx(a, (s - L.base[a]))]];
 }
 // Does the literal transitiveDeps fold differ from the closure for this change?
 __device__ __noinline__ bool fold_differs(FoldView L, uint32_t dep0, uint32_t nd, uint32_t actor, uint32_t seq) {
@@ -673,7 +678,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     const uint32_t mybase = act ? L.base[a8] : 0;
     const uint32_t slot = seq - mybase;
     if (__ballot(act && slot >= 64)) return OUT_UNSUPPORTED;
-    lds_min(&L.first[a8 * 64 + (slot & 63)], act ? lane : 0xFFFFFFFFu);
+    lds_min(&L.first[fidx(a8, (slot & 63))], act ? lane : 0xFFFFFFFFu);
     {
         const uint32_t o0 = c.op_first - doc.op_off;       // ops -> arrival index of their change
         if (act) for (uint32_t j = 0; j < c.n_ops; j++) L.opchg[o0 + j] = (uint16_t)(lane | (a8 << 8));
@@ -695,13 +700,13 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
             const uint32_t ad = a & (NA_MAX - 1);
             const uint32_t b = L.base[ad];
             const bool inwin = b != 0xFFFFFFFFu && s >= b && s - b < 64;
-            const uint32_t f = L.first[ad * 64 + ((s - b) & 63)];
+            const uint32_t f = L.first[fidx(ad, ((s - b) & 63))];
             const uint32_t rel = s == 0 ? 0u : (inwin ? s - b + 1 : 0x7Fu);
             L.depinfo[i] = (inwin && f < 64 ? f : 0x7Fu) | (rel << 8) | (ad << 16);
         }
         if (__ballot(bad_dep)) return OUT_UNSUPPORTED;
     }
-    const uint32_t first_me = act ? L.first[actor * 64 + slot] : lane;
+    const uint32_t first_me = act ? L.first[fidx(actor, slot)] : lane;
     const bool dup = act && first_me != lane;
     const uint32_t cid_first = shfl32(c.content_id, (int)(first_me & 63));
     u64 dmask = 0;                       // direct deps in arrival-index space (fast path)
@@ -731,7 +736,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         }
         const uint32_t ps = seq - 1;
         const bool hp = act && ps != 0, inb = ps >= mybase;
-        const uint32_t f = L.first[a8 * 64 + ((ps - mybase) & 63)];
+        const uint32_t f = L.first[fidx(a8, ((ps - mybase) & 63))];
         ok = ok && !(hp && (!inb || f >= lane));
         const bool pv = hp && inb && f < lane;
         dmask |= pv ? (1ull << (f & 63)) : 0ull;
@@ -780,7 +785,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
             }
             const uint32_t ps = seq - 1;
             const bool hp = act && ps != 0, inb = ps >= mybase;
-            const uint32_t f = L.first[a8 * 64 + ((ps - mybase) & 63)];
+            const uint32_t f = L.first[fidx(a8, ((ps - mybase) & 63))];
             never |= hp && (!inb || f >= 64);
             dall |= (hp && inb && f < 64) ? (1ull << f) : 0ull;
             pred_any = (hp && inb && f < 64) ? f : 0xFFu;
@@ -870,7 +875,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
                 for (uint32_t j = 0; j < n; j++) rank += (uint32_t)__builtin_amdgcn_readlane((int)hk, (int)j) < hk ? 1u : 0u;
                 hist = apl ? (int32_t)rank : (act && tk != INF ? -2 : -1);
                 H = (uint32_t)__popcll(__ballot(apl));
-                if (apl && dup) L.first[a8 * 64 + (slot & 63)] = lane;   // (actor, seq) -> applied copy
+                if (apl && dup) L.first[fidx(a8, (slot & 63))] = lane;   // (actor, seq) -> applied copy
                 copy_applied = __ballot(apl && dup) != 0;
                 solved = true;
             }
@@ -886,7 +891,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
                     const uint32_t kd = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)d);
                     if (!((applied | keys) >> kd & 1)) {
                         ap |= 1ull << d; keys |= 1ull << kd; copy_applied = true;
-                        if (lane == d) L.first[a8 * 64 + (slot & 63)] = lane;   // (actor, seq) -> applied lane
+                        if (lane == d) L.first[fidx(a8, (slot & 63))] = lane;   // (actor, seq) -> applied lane
                     }
                 }
                 if ((P >> lane) & 1) hist = ((ap >> lane) & 1) ? (int32_t)(H + (uint32_t)__popcll(ap & below)) : -2;
@@ -922,9 +927,9 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
                     const uint32_t pk = L.deps[my_dep0 + j];
                     const uint32_t a = pk >> 24, s = pk & 0xFFFFFF;
                     if (a == actor || s == 0) continue;
-                    dmask |= 1ull << L.first[a * 64 + (s - L.base[a])];
+                    dmask |= 1ull << L.first[fidx(a, (s - L.base[a]))];
                 }
-                if (seq - 1 != 0) { pred_arr = L.first[actor * 64 + (seq - 1 - mybase)]; dmask |= 1ull << pred_arr; }
+                if (seq - 1 != 0) { pred_arr = L.first[fidx(actor, (seq - 1 - mybase))]; dmask |= 1ull << pred_arr; }
             }
         }
     } else {
@@ -967,7 +972,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
                     progress = true;
                     above = (j >= 63) ? 0 : (~0ull << (j + 1));
                     if (sj + 1 <= cur) {                         // seq <= clock: already applied
-                        const uint32_t k = L.first[aj * 64 + sj];
+                        const uint32_t k = L.first[fidx(aj, sj)];
                         const uint32_t ck = (uint32_t)__builtin_amdgcn_readlane((int)c.content_id, (int)k);
                         const uint32_t cj = (uint32_t)__builtin_amdgcn_readlane((int)c.content_id, (int)j);
                         if (lane == j) hist = -2;
@@ -981,7 +986,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
                     }
                     if (aj < 4) crel_lo = (crel_lo & ~(0xFFu << sh)) | ((sj + 1) << sh);
                     else        crel_hi = (crel_hi & ~(0xFFu << sh)) | ((sj + 1) << sh);
-                    if (lane == 0) L.first[aj * 64 + sj] = j;
+                    if (lane == 0) L.first[fidx(aj, sj)] = j;
                     if (lane == j) hist = (int32_t)H;
                     H++;
                     if (first_pass) break;
@@ -999,9 +1004,9 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
                 const uint32_t pk = L.deps[my_dep0 + j];
                 const uint32_t a = pk >> 24, s = pk & 0xFFFFFF;
                 if (a == actor || s == 0) continue;
-                dmask |= 1ull << L.first[a * 64 + (s - L.base[a])];
+                dmask |= 1ull << L.first[fidx(a, (s - L.base[a]))];
             }
-            if (seq - 1 != 0) { pred_arr = L.first[actor * 64 + (seq - 1 - mybase)]; dmask |= 1ull << pred_arr; }
+            if (seq - 1 != 0) { pred_arr = L.first[fidx(actor, (seq - 1 - mybase))]; dmask |= 1ull << pred_arr; }
         }
     }
 
