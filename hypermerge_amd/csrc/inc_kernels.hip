@@ -105,9 +105,10 @@ __device__ int list_plan(const Grp<64> &g, const AppendDesc &D, const IncArgs &A
     const uint64_t insm = g.bits(ins);
     const uint32_t nins = (uint32_t)__popcll(insm);
     const uint32_t key = (o_elem << 8) | (opactor & 0xFFu);
-    // a new element's register is fresh; its parent exists: an old element, '_head', or an
-    // element inserted earlier in this round; an assign hits an element that exists
-    bool bad = ins && o_reg < D.n_old_r;
+    // a new element's register is fresh (checked by the caller: no op touched it before); its
+    // parent exists: an old element, '_head', or an element inserted earlier in this round; an
+    // assign hits an element that exists
+    bool bad = false;
     uint32_t pnew = HM_NONE, ecr = HM_NONE;
     for (uint32_t k = 0; k < nno; k++) {
         if (!((insm >> k) & 1ull)) continue;
@@ -483,6 +484,9 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
     ListPlan lp;
     if constexpr (G == 64) {
         if (any_list) {
+            // an inserted element's register was never touched: a fresh id, or one the document's
+            // declared register count reserved (untouched registers have no object)
+            if (g.bits(lst && o_act == HM_INS && o_reg < D.n_old_r && (rr.obj != HM_NONE || rr.n_surv != 0))) return INC_BAIL;
             const int rc = list_plan(g, D, A, I, nno, o_act, o_reg, o_par, o_elem, lst, g.sh(ca, oj), lscr, lp);
             if (rc != INC_DONE) return rc;
         }
@@ -617,11 +621,25 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
     for (uint32_t r0 = D.n_old_r; r0 < D.n_r; r0 += G) {
         const uint32_t r = r0 + gl;
         bool hit = false;
-        for (uint32_t k = 0; k < nno; k++) hit |= g.sh(o_reg, k) == r && g.sh(o_act, k) != HM_INS;
+        for (uint32_t k = 0; k < nno; k++) hit |= g.sh(o_reg, k) == r;
         if (r < D.n_r && !hit) {
             hm_reg_result z;
             z.n_surv = 0; z.surv_off = 0; z.list_index = -1; z.obj = HM_NONE;
             A.regs[D.dst_r + r] = z;
+        }
+    }
+    // elements inserted and not assigned: no survivors, the list object (as the merge's op scan
+    // records every op's object on its register)
+    if (any_list) {
+        bool asg = false;
+        for (uint32_t k = 0; k < nno; k++) {
+            const uint32_t rk = g.sh(o_reg, k), ak = g.sh(o_act, k);
+            asg |= rk == o_reg && ak != HM_INS;
+        }
+        if (gl < nno && o_act == HM_INS && !asg) {
+            hm_reg_result z;
+            z.n_surv = 0; z.surv_off = 0; z.list_index = -1; z.obj = o_obj;
+            A.regs[D.dst_r + o_reg] = z;
         }
     }
 

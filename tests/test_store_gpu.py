@@ -400,6 +400,45 @@ def _text_rounds():
     return rounds
 
 
+def test_rowstore_text_rounds_with_declared_registers(engine):
+    """Resident text documents fed prebuilt rows whose document totals are declared up front
+    (RowStore + slice_changes: n_regs is the whole log's, so a new element's register id was
+    reserved but never touched): typing rounds of 1-2 changes go incremental, and every round's
+    results and the final device state equal the whole-log re-merge's."""
+    from hypermerge_amd.store import RowStore, slice_changes
+    b = synth.generate(synth.config("C3", n_docs=24))
+    n = b.n_docs
+    nch = b.docs["n_changes"].astype(np.int64)
+    pos = np.maximum(nch - 10, 0)
+    A, B = RowStore(engine, a_stride=b.a_stride), RowStore(engine, a_stride=b.a_stride)
+    B.set_incremental(False)
+    ha, hb = A.open_n(n), B.open_n(n)
+    for st, h0 in ((A, ha), (B, hb)):
+        st.submit_batch(slice_changes(b, np.zeros(n, np.int64), pos), np.arange(h0, h0 + n))
+        st.wait()
+    rng = np.random.default_rng(3)
+    routed = {"incremental": 0, "remerged": 0, "handed_back": 0}
+    while (pos < nch).any():
+        hi = np.minimum(pos + rng.integers(1, 3, n), nch)
+        sel = np.nonzero(hi > pos)[0]
+        sub = slice_changes(b, pos, hi, sel)
+        A.submit_batch(sub, sel + ha)
+        ra = A.wait()
+        for k, v in A.last_routing().items():
+            routed[k] += v
+        B.submit_batch(sub, sel + hb)
+        rb = B.wait()
+        for f in ("docs", "clock", "back_clock", "heads"):
+            np.testing.assert_array_equal(getattr(ra, f), getattr(rb, f), err_msg=f)
+        pos = np.maximum(pos, hi)
+    for i in range(n):
+        _, ga = A.read(ha + i)
+        _, gb = B.read(hb + i)
+        for f in ("docs", "clock", "back_clock", "heads", "hist", "all_deps", "regs", "surv"):
+            np.testing.assert_array_equal(getattr(ga, f), getattr(gb, f), err_msg=f"{f} doc {i}")
+    assert routed["incremental"] >= 0.9 * sum(routed.values()), routed
+
+
 def test_incremental_text_edits_equal_remerge_and_oracle(engine):
     """Row a11 on the incremental path: list / text ops applied on the resident element order
     (lorder / epos), each call equal to the whole-log re-merge and to the oracle's cold merge."""
