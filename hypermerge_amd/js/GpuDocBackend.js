@@ -73,7 +73,7 @@ const ACTIONS = ['create', 'set', 'remove', 'insert']
 // One round's decoder state (module level: no closures per document — the per-op diff form
 // makes millions of small objects per round, and the garbage collector is the JS thread's
 // largest cost)
-const R = { w: null, nums: null, strs: null, p: 0, sb: 0, nb: 0 }
+const R = { w: null, nums: null, strs: null, p: 0, sb: 0, nb: 0, tag: 0, dt: 0 }
 function rdClock() {
   const w = R.w, strs = R.strs, sb = R.sb
   const c = {}
@@ -81,29 +81,6 @@ function rdClock() {
   for (let k = w[p++]; k > 0; k--) { c[strs[sb + w[p]]] = w[p + 1]; p += 2 }
   R.p = p
   return c
-}
-function rdValue(e) {
-  const v = R.w[R.p++], tag = v & 7, dt = (v >>> 3) & 3, pay = v >>> 5
-  switch (tag) {
-    case 0: e.value = null; break
-    case 1: e.value = false; break
-    case 2: e.value = true; break
-    case 3: case 4: e.value = R.nums[R.nb + pay]; break
-    case 5: e.value = R.strs[R.sb + pay]; break
-    case 6: e.value = R.strs[R.sb + pay]; e.link = true; break
-    default: e.value = null
-  }
-  if (dt === 1) e.datatype = 'counter'
-  else if (dt === 2) e.datatype = 'timestamp'
-}
-function rdEntry(e) {
-  const k = R.w[R.p++]
-  rdValue(e)
-  if (k > 1) {
-    const cs = new Array(k - 1)
-    for (let i = 1; i < k; i++) { const c = { actor: R.strs[R.sb + R.w[R.p++]], value: null }; rdValue(c); cs[i - 1] = c }
-    e.conflicts = cs
-  }
 }
 // One docset call's HMP1 results, read document by document: decodeRound(buf, n).head(d) gives
 // the patch shell (clock, deps; diffs null), back clock and round clock; .diffs(d) fills the
@@ -159,21 +136,77 @@ class RoundReader {
       let e
       if (action === 0) e = { action: 'create', obj, type: TYPES[t] }
       else if (t < 2) {
-        if (action === 1) { e = { action: 'set', type: TYPES[t], obj, key: strs[sb + w[R.p++]], value: null }; rdEntry(e) }
+        if (action === 1) e = setDiff(TYPES[t], obj, strs[sb + w[R.p++]])
         else e = { action: ACTIONS[action], type: TYPES[t], obj, key: strs[sb + w[R.p++]] }
       } else if (action === 3) {
-        e = { action: 'insert', type: TYPES[t], obj, index: w[R.p++], elemId: null, value: null }
-        e.elemId = strs[sb + w[R.p++]]
-        rdEntry(e)
+        const index = w[R.p++]
+        e = insertDiff(TYPES[t], obj, index, strs[sb + w[R.p++]])
       } else if (action === 1) {
-        e = { action: 'set', type: TYPES[t], obj, index: w[R.p++], value: null }
-        rdEntry(e)
+        e = setIndexDiff(TYPES[t], obj, w[R.p++])
       } else e = { action: ACTIONS[action], type: TYPES[t], obj, index: w[R.p++] }
       diffs[k] = e
     }
     this.leave()
     return diffs
   }
+}
+
+// The value-carrying diffs, built whole: the entry (value, datatype, link, conflicts) is read
+// first and the object created with exactly its fields, so no property is added after the
+// literal (an added property costs an out-of-object backing store per diff).
+function rdVal() {
+  const v = R.w[R.p++]
+  const dt = (v >>> 3) & 3
+  R.tag = v & 7; R.dt = dt === 3 ? 0 : dt
+  const pay = v >>> 5
+  switch (R.tag) {
+    case 1: return false
+    case 2: return true
+    case 3: case 4: return R.nums[R.nb + pay]
+    case 5: case 6: return R.strs[R.sb + pay]
+    default: return null
+  }
+}
+function rdConflicts(k) {
+  const cs = new Array(k - 1)
+  for (let i = 1; i < k; i++) {
+    const actor = R.strs[R.sb + R.w[R.p++]]
+    const value = rdVal()
+    let c
+    if (R.tag === 6) c = R.dt ? { actor, value, link: true, datatype: DTS[R.dt] } : { actor, value, link: true }
+    else c = R.dt ? { actor, value, datatype: DTS[R.dt] } : { actor, value }
+    cs[i - 1] = c
+  }
+  return cs
+}
+const DTS = [undefined, 'counter', 'timestamp', undefined]
+function setDiff(type, obj, key) {
+  const k = R.w[R.p++]
+  const value = rdVal(), tag = R.tag, dt = R.dt
+  const conflicts = k > 1 ? rdConflicts(k) : null
+  if (conflicts === null) {
+    if (tag === 6) return { action: 'set', type, obj, key, value, link: true }
+    return dt ? { action: 'set', type, obj, key, value, datatype: DTS[dt] } : { action: 'set', type, obj, key, value }
+  }
+  if (tag === 6) return { action: 'set', type, obj, key, value, link: true, conflicts }
+  return dt ? { action: 'set', type, obj, key, value, datatype: DTS[dt], conflicts } : { action: 'set', type, obj, key, value, conflicts }
+}
+function setIndexDiff(type, obj, index) {
+  const k = R.w[R.p++]
+  const value = rdVal(), tag = R.tag, dt = R.dt
+  const conflicts = k > 1 ? rdConflicts(k) : null
+  const e = tag === 6 ? { action: 'set', type, obj, index, value, link: true }
+    : dt ? { action: 'set', type, obj, index, value, datatype: DTS[dt] } : { action: 'set', type, obj, index, value }
+  if (conflicts !== null) e.conflicts = conflicts
+  return e
+}
+function insertDiff(type, obj, index, elemId) {
+  const k = R.w[R.p++]
+  const value = rdVal(), tag = R.tag, dt = R.dt
+  const e = tag === 6 ? { action: 'insert', type, obj, index, elemId, value, link: true }
+    : dt ? { action: 'insert', type, obj, index, elemId, value, datatype: DTS[dt] } : { action: 'insert', type, obj, index, elemId, value }
+  if (k > 1) e.conflicts = rdConflicts(k)
+  return e
 }
 
 // a JSON results buffer (the docset's debug form) read through the same interface

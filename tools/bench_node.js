@@ -143,12 +143,14 @@ async function runGpu(mode, objects, diffsForm) {
 ;(async () => {
   const out = {}
   for (const m of legs) {
-    if (m === 'cpu') out[m] = await runCpu(false)
-    else if (m === 'cpu_blocks') out[m] = await runCpu(true)
-    else if (m === 'gpu') out[m] = await runGpu('batched', false)
-    else if (m === 'gpu_async') out[m] = await runGpu('async', false)
-    else if (m === 'gpu_objects') out[m] = await runGpu('async', true)
-    else if (m === 'gpu_async_net') out[m] = await runGpu('async', false, 'net')
+    let key = m
+    for (let i = 2; key in out; i++) key = `${m}#${i}`           // a repeated leg: m#2, m#3, ...
+    if (m === 'cpu') out[key] = await runCpu(false)
+    else if (m === 'cpu_blocks') out[key] = await runCpu(true)
+    else if (m === 'gpu') out[key] = await runGpu('batched', false)
+    else if (m === 'gpu_async') out[key] = await runGpu('async', false)
+    else if (m === 'gpu_objects') out[key] = await runGpu('async', true)
+    else if (m === 'gpu_async_net') out[key] = await runGpu('async', false, 'net')
     else throw new Error(`unknown leg ${m}`)
   }
   process.stdout.write(JSON.stringify(out) + '\n')
