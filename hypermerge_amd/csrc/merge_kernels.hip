@@ -52,6 +52,10 @@
 #define HM_WAVES_PER_EU_OPL4 3  // 256 ops per document: the op arrays need a larger register budget (measured:
                                 // C2 0.87 -> 0.65 ms at 3 waves/SIMD; list launches (C5) best at 2: 3.99 -> 3.25 ms)
 #endif
+#ifndef HM_WAVES_PER_EU_LIST3
+#define HM_WAVES_PER_EU_LIST3 3 // list launches of <= 192 ops per document: 168 VGPRs, no spill; K3's tables
+                                // overlay the dead K1/K2 tables, so LDS holds 10 such waves per CU
+#endif
 // Wave priority (s_setprio) for the phases other waves should not hold up: the ancestor push
 // (64 dependent readlane steps: a lower-priority wave's VALU issue fills its hazard gaps) and a
 // wave's store / next-row staging (its memory requests go out sooner).  C4 A/B over priorities
@@ -212,45 +216,54 @@ template <> struct SizeClass<2> { static constexpr uint32_t NR = 128, NO = 32, N
 // resident waves per CU, so nothing is carved that the launch's documents cannot use.
 // The kernel instantiates it with compile-time sizes (a size class), so every LDS address
 // folds into a ds_* immediate offset instead of occupying an SGPR.
-// Aliases: seglist/survp live in `first` (dead after K1b).
+// Two parts: the tables live until the outputs, then the tables no phase reads after K2
+// (validation, readiness, history, ancestors, the op scan, survivor tests, ranks).  K3's
+// tables (RGA order, list launches) overlay that second part, so a list launch costs the
+// larger of the two, not their sum.
 template <typename L_t, typename P>
 __host__ __device__ inline size_t small_carve(P base, uint32_t NOp, uint32_t NR, uint32_t NO, uint32_t ND,
                                               bool lists, bool counters, L_t *L) {
     size_t o = 0;
 #define TAKE(f, T, cnt) do { L->f = (decltype(L->f))(base + o); o = (o + (size_t)(cnt) * sizeof(T) + 15) & ~(size_t)15; } while (0)
-    TAKE(anc, u64, 64);          TAKE(chain, u64, NA_MAX);     TAKE(segor, u64, NR);
-    TAKE(opval, u64, NOp);       TAKE(survpk, u64, NR);
-    TAKE(errkey, u64, 1);        TAKE(cov, u64, 1);
-    TAKE(first, uint32_t, NA_MAX * 64 > 2 * NOp ? NA_MAX * 64 : 2 * NOp);
-    L->seglist = L->first; L->survp = L->first + NOp;
-    TAKE(base, uint32_t, NA_MAX * 3);
-    TAKE(objslot, uint32_t, NO); TAKE(segcnt, uint32_t, NR);   TAKE(survcnt, uint32_t, NR);
-    TAKE(regoff, uint32_t, NR);  TAKE(regobj, uint32_t, NR);   TAKE(insmin, uint32_t, NR);
-    TAKE(flags, uint32_t, 2);
-    const size_t deps_at = o;                                      // deps + depinfo: dead after K1b's fold check
-    TAKE(deps, uint32_t, ND > NOp ? ND : NOp);                     // flags[1]: max n_deps
-    TAKE(depinfo, uint32_t, ND);
-    const size_t deps_bytes = o - deps_at;
+    // ---- live through the outputs (and the counters pass) ----
+    TAKE(anc, u64, 64);          TAKE(chain, u64, NA_MAX);     TAKE(opval, u64, NOp);
+    TAKE(errkey, u64, 1);        TAKE(base, uint32_t, NA_MAX * 3);
+    TAKE(survcnt, uint32_t, NR); TAKE(regoff, uint32_t, NR);   TAKE(regobj, uint32_t, NR);
+    TAKE(insmin, uint32_t, NR);  TAKE(flags, uint32_t, 2);
     TAKE(opmeta, uint32_t, NOp); TAKE(opro, uint32_t, NOp);
-    TAKE(hist_of, int32_t, 64);
-    TAKE(survop, uint16_t, NOp); TAKE(opbase, uint16_t, 64);   TAKE(oppar, uint16_t, NOp);
-    TAKE(h2a, uint8_t, 64);      TAKE(chactor, uint8_t, 64);   TAKE(opchg, uint16_t, NOp);
-    TAKE(objtype, uint8_t, NO);
+    TAKE(survop, uint16_t, NOp); TAKE(chactor, uint8_t, 64);   TAKE(objtype, uint8_t, NO);
     if (lists) {
-        const uint32_t NP = NR + NO, NE = 2 * (NOp + NO);
         TAKE(opelem, uint32_t, NOp);
         L->nodekey = L->opelem;                                    // opelem is dead after K2's op scan (K3 runs later)
-        TAKE(nins, uint32_t, 1);      TAKE(pcount, uint32_t, NP);  TAKE(poff, uint32_t, NP);
-        TAKE(pfill, uint32_t, NP);
-        if ((size_t)NE * sizeof(uint32_t) <= deps_bytes) L->tour0 = (decltype(L->tour0))(base + deps_at);   // K3's tour in the dep tables
-        else TAKE(tour0, uint32_t, NE);
-        TAKE(listbase, uint32_t, NO + 1);
-        TAKE(nodeop, uint16_t, NOp);  TAKE(nodepi, uint16_t, NOp); TAKE(regnode, uint16_t, NR);
-        TAKE(plist, uint16_t, NOp);   TAKE(fc, uint16_t, NP);      TAKE(ns, uint16_t, NOp);
-        TAKE(listid, uint16_t, NO);
+        TAKE(nins, uint32_t, 1);
     }
     TAKE(stamps, u64, HM_STAMPS ? HM_NSTAMP + 1 : 0);
-    TAKE(survsum, int64_t, counters ? NOp : 0);       // last: the rest of the carve ignores `counters`
+    // ---- dead once K2 has ranked the survivors (the next document's staging refills deps / oppar
+    //      after this document's outputs) ----
+    const size_t dead_at = o;
+    TAKE(first, uint32_t, NA_MAX * 64);
+    TAKE(deps, uint32_t, ND > NOp ? ND : NOp);                     // flags[1]: max n_deps
+    TAKE(depinfo, uint32_t, ND);
+    TAKE(segor, u64, NR);        TAKE(survpk, u64, NR);        TAKE(cov, u64, 1);
+    TAKE(objslot, uint32_t, NO); TAKE(segcnt, uint32_t, NR);   TAKE(hist_of, int32_t, 64);
+    TAKE(opbase, uint16_t, 64);  TAKE(oppar, uint16_t, NOp);   TAKE(h2a, uint8_t, 64);
+    TAKE(opchg, uint16_t, NOp);
+    L->seglist = L->first; L->survp = L->first;                    // (K3's; list launches carve them below)
+    if (lists) {
+        const uint32_t NP = NR + NO, NE = 2 * (NOp + NO);
+        size_t q = dead_at;
+#define TAKEK(f, T, cnt) do { L->f = (decltype(L->f))(base + q); q = (q + (size_t)(cnt) * sizeof(T) + 15) & ~(size_t)15; } while (0)
+        TAKEK(seglist, uint32_t, NOp); TAKEK(survp, uint32_t, NOp); TAKEK(tour0, uint32_t, NE);
+        TAKEK(pcount, uint32_t, NP);   TAKEK(poff, uint32_t, NP);   TAKEK(pfill, uint32_t, NP);
+        TAKEK(listbase, uint32_t, NO + 1);
+        TAKEK(nodeop, uint16_t, NOp);  TAKEK(nodepi, uint16_t, NOp); TAKEK(regnode, uint16_t, NR);
+        TAKEK(plist, uint16_t, NOp);   TAKEK(fc, uint16_t, NP);      TAKEK(ns, uint16_t, NOp);
+        TAKEK(listid, uint16_t, NO);
+#undef TAKEK
+        if (q > o) o = q;
+    }
+    // last: the kernel carves with counters on, the host sizes the launch with the batch's flag
+    TAKE(survsum, int64_t, counters ? NOp : 0);
 #undef TAKE
     L->bclock = L->base + NA_MAX;
     L->headv = L->base + 2 * NA_MAX;
@@ -1481,7 +1494,7 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
 }
 
 template <int OPL, bool LISTS, int CLS>
-__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(OPL >= 3 ? (LISTS ? HM_WAVES_PER_EU_OPL4 - 1 : HM_WAVES_PER_EU_OPL4) : HM_WAVES_PER_EU)))
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(OPL >= 3 ? (LISTS ? (OPL == 3 ? HM_WAVES_PER_EU_LIST3 : HM_WAVES_PER_EU_OPL4 - 1) : HM_WAVES_PER_EU_OPL4) : HM_WAVES_PER_EU)))
 void merge_small_kernel(SmallParams p) {
     extern __shared__ __align__(16) uint8_t lds_raw[];
     typedef SizeClass<CLS> C;
