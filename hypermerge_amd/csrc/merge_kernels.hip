@@ -188,7 +188,9 @@ struct SmallLds {
     LDS u64 *survpk;                // per register: survivor count per actor rank, one byte each
     LDS int64_t *survsum;           // counter launches only
     LDS uint32_t *first, *base, *bclock, *headv, *objslot, *segcnt, *survcnt, *regoff, *regobj, *insmin;
-    LDS uint32_t *flags, *deps, *depinfo, *seglist, *survp;
+    LDS uint32_t *flags, *deps, *depinfo;
+    LDS uint8_t *seglist;           // K3: visible flag per list position
+    LDS uint16_t *survp;            // K3: visible elements before a position
     LDS uint32_t *opmeta;           // action | datatype << 8 | vtag << 16
     LDS uint32_t *opro;             // reg | obj << 16 (clamped to 0xFFFF: >= any carve)
     LDS uint32_t *opelem;           // ins element counter (list launches)
@@ -197,7 +199,8 @@ struct SmallLds {
     LDS uint8_t *h2a, *chactor, *objtype;
     LDS uint16_t *opchg;            // op -> arrival index of its change | actor rank << 8
     // K3 (RGA lists); carved only for launches with list documents
-    LDS uint32_t *nins, *pcount, *poff, *pfill, *nodekey, *tour0, *listbase;   // tour ranked in place
+    LDS uint32_t *nins, *pcount, *pfill, *nodekey, *tour0, *listbase;   // tour ranked in place
+    LDS uint16_t *poff;
     LDS uint16_t *nodeop, *nodepi, *regnode, *plist, *fc, *ns, *listid;
     LDS u64 *stamps;                // HM_STAMPS builds: [HM_NSTAMP] cycle sums + last stamp
 };
@@ -238,27 +241,33 @@ __host__ __device__ inline size_t small_carve(P base, uint32_t NOp, uint32_t NR,
         TAKE(nins, uint32_t, 1);
     }
     TAKE(stamps, u64, HM_STAMPS ? HM_NSTAMP + 1 : 0);
-    // ---- dead once K2 has ranked the survivors (the next document's staging refills deps / oppar
-    //      after this document's outputs) ----
+    // ---- tables no phase reads after K2 (the next document's staging refills deps / oppar only
+    //      after this document's outputs).  K1's (first-arrival table, deps, dep lookups: dead
+    //      after the fold check) and K2's (survivor tests and ranks: initialised after the fold
+    //      check) share one region; K3's tables overlay the whole part ----
     const size_t dead_at = o;
+    TAKE(hist_of, int32_t, 64);  TAKE(cov, u64, 1);            TAKE(opbase, uint16_t, 64);
+    TAKE(oppar, uint16_t, NOp);  TAKE(h2a, uint8_t, 64);       TAKE(opchg, uint16_t, NOp);
+    const size_t k1_at = o;
     TAKE(first, uint32_t, NA_MAX * 64);
     TAKE(deps, uint32_t, ND > NOp ? ND : NOp);                     // flags[1]: max n_deps
     TAKE(depinfo, uint32_t, ND);
-    TAKE(segor, u64, NR);        TAKE(survpk, u64, NR);        TAKE(cov, u64, 1);
-    TAKE(objslot, uint32_t, NO); TAKE(segcnt, uint32_t, NR);   TAKE(hist_of, int32_t, 64);
-    TAKE(opbase, uint16_t, 64);  TAKE(oppar, uint16_t, NOp);   TAKE(h2a, uint8_t, 64);
-    TAKE(opchg, uint16_t, NOp);
-    L->seglist = L->first; L->survp = L->first;                    // (K3's; list launches carve them below)
+    const size_t k1_end = o;
+    o = k1_at;
+    TAKE(segor, u64, NR);        TAKE(survpk, u64, NR);        TAKE(segcnt, uint32_t, NR);
+    TAKE(objslot, uint32_t, NO);
+    if (o < k1_end) o = k1_end;
+    L->seglist = (decltype(L->seglist))L->first; L->survp = (decltype(L->survp))L->first;   // (K3's: below)
     if (lists) {
         const uint32_t NP = NR + NO, NE = 2 * (NOp + NO);
         size_t q = dead_at;
 #define TAKEK(f, T, cnt) do { L->f = (decltype(L->f))(base + q); q = (q + (size_t)(cnt) * sizeof(T) + 15) & ~(size_t)15; } while (0)
-        TAKEK(seglist, uint32_t, NOp); TAKEK(survp, uint32_t, NOp); TAKEK(tour0, uint32_t, NE);
-        TAKEK(pcount, uint32_t, NP);   TAKEK(poff, uint32_t, NP);   TAKEK(pfill, uint32_t, NP);
+        TAKEK(tour0, uint32_t, NE);     TAKEK(pcount, uint32_t, NP);  TAKEK(pfill, uint32_t, NP);
         TAKEK(listbase, uint32_t, NO + 1);
-        TAKEK(nodeop, uint16_t, NOp);  TAKEK(nodepi, uint16_t, NOp); TAKEK(regnode, uint16_t, NR);
-        TAKEK(plist, uint16_t, NOp);   TAKEK(fc, uint16_t, NP);      TAKEK(ns, uint16_t, NOp);
-        TAKEK(listid, uint16_t, NO);
+        TAKEK(poff, uint16_t, NP);      TAKEK(survp, uint16_t, NOp);
+        TAKEK(nodeop, uint16_t, NOp);   TAKEK(nodepi, uint16_t, NOp); TAKEK(regnode, uint16_t, NR);
+        TAKEK(plist, uint16_t, NOp);    TAKEK(fc, uint16_t, NP);      TAKEK(ns, uint16_t, NOp);
+        TAKEK(listid, uint16_t, NO);    TAKEK(seglist, uint8_t, NOp);
 #undef TAKEK
         if (q > o) o = q;
     }
