@@ -67,6 +67,7 @@ def main() -> int:
     ap.add_argument("--node-text-docs", type=int, default=40, help="C3 documents of the Node leg (0: skip)")
     ap.add_argument("--node-c5-docs", type=int, default=5000, help="C5 documents of the Node leg (0: skip)")
     ap.add_argument("--text-docs", type=int, default=10000, help="C3 documents in the resident text leg")
+    ap.add_argument("--c5-docs", type=int, default=100000, help="C5 documents in the resident nested-document leg (0: skip)")
     ap.add_argument("--arrival", type=int, default=None,
                     help="override the config's arrival order (0 generation, 1 actor-major as RepoBackend.loadDocument "
                          "concatenates, 2 shuffled)")
@@ -211,6 +212,7 @@ def main() -> int:
     # store, then rounds in which each receives its next 1-2 changes (DocBackend.ts:169-185)
     incremental = None
     incremental_text = None
+    incremental_c5 = None
     if rank == 0 and ws == 1 and not args.no_incremental and args.config == "C4" and args.arrival is None:
         incremental = _incremental(eng, batch, args)
         # the same event on text documents (C3: RGA inserts / deletes on the resident element order)
@@ -218,6 +220,16 @@ def main() -> int:
         incremental_text = _incremental(eng, c3, args, tail=8, oracle_docs=200)
         incremental_text["workload"] = f"C3: {c3.n_docs} text docs x 8 actors, the last 8 changes of each in rounds of 1-2"
         del c3
+        # nested maps / lists with out-of-order and duplicate delivery (C5): the share the
+        # incremental path takes and the share it hands to the re-merge (queued or duplicate
+        # changes, object creation, a second list per document)
+        if args.c5_docs > 0:
+            c5 = synth.generate(synth.config("C5", n_docs=args.c5_docs), threads=min(16, os.cpu_count() or 1))
+            incremental_c5 = _incremental(eng, c5, args, tail=4, oracle_docs=200)
+            incremental_c5["workload"] = (f"C5: {c5.n_docs} nested map / list docs x 4 actors, 20% delivered before "
+                                          f"their deps, 3% duplicates; the last 4 changes of each in rounds of 1-2")
+            incremental_c5["bail_share"] = 1.0 - incremental_c5["incremental_share"]
+            del c5
     # the Node host path end to end through the DocBackend message API (C2 sample)
     node = None
     if rank == 0 and ws == 1 and not args.no_node:
@@ -267,7 +279,8 @@ def main() -> int:
                          "kernel": kern["kernel"], "kernel_ms": kern["kernel_ms"], "alg_bytes": kern["alg_bytes"],
                          "kernels": kern["kernels"], "traffic_detail": traffic},
             "cpu_baseline": cpu, "cpu_parallel": cpu_mt, "end_to_end": e2e, "from_blocks": from_blocks,
-            "resident_incremental": incremental, "resident_incremental_text": incremental_text, "node_docbackend": node,
+            "resident_incremental": incremental, "resident_incremental_text": incremental_text,
+            "resident_incremental_c5": incremental_c5, "node_docbackend": node,
             "arrival_orders": orders,
             "host": _host_info(),
             "parity_sample_ok": parity, "unsupported_docs": unsupported, "error_docs": errors,

@@ -199,7 +199,7 @@ struct SmallLds {
     LDS uint8_t *h2a, *chactor, *objtype;
     LDS uint16_t *opchg;            // op -> arrival index of its change | actor rank << 8
     // K3 (RGA lists); carved only for launches with list documents
-    LDS uint32_t *nins, *pcount, *pfill, *nodekey, *tour0, *listbase;   // tour ranked in place
+    LDS uint32_t *nins, *pcount, *nodekey, *tour0, *listbase;   // tour ranked in place
     LDS uint16_t *poff;
     LDS uint16_t *nodeop, *nodepi, *regnode, *plist, *fc, *ns, *listid;
     LDS u64 *stamps;                // HM_STAMPS builds: [HM_NSTAMP] cycle sums + last stamp
@@ -262,9 +262,8 @@ __host__ __device__ inline size_t small_carve(P base, uint32_t NOp, uint32_t NR,
         const uint32_t NP = NR + NO, NE = 2 * (NOp + NO);
         size_t q = dead_at;
 #define TAKEK(f, T, cnt) do { L->f = (decltype(L->f))(base + q); q = (q + (size_t)(cnt) * sizeof(T) + 15) & ~(size_t)15; } while (0)
-        TAKEK(tour0, uint32_t, NE);     TAKEK(pcount, uint32_t, NP);  TAKEK(pfill, uint32_t, NP);
-        TAKEK(listbase, uint32_t, NO + 1);
-        TAKEK(poff, uint16_t, NP);      TAKEK(survp, uint16_t, NOp);
+        TAKEK(tour0, uint32_t, NE);     TAKEK(pcount, uint32_t, NP);  TAKEK(listbase, uint32_t, NO + 1);
+        TAKEK(poff, uint16_t, NP + 1);  TAKEK(survp, uint16_t, NOp);
         TAKEK(nodeop, uint16_t, NOp);   TAKEK(nodepi, uint16_t, NOp); TAKEK(regnode, uint16_t, NR);
         TAKEK(plist, uint16_t, NOp);    TAKEK(fc, uint16_t, NP);      TAKEK(ns, uint16_t, NOp);
         TAKEK(listid, uint16_t, NO);    TAKEK(seglist, uint8_t, NOp);
@@ -348,7 +347,7 @@ __device__ __forceinline__ void rga_order(const SmallLds &L, uint32_t R, uint32_
     const uint32_t lane = threadIdx.x;
     const uint32_t NP = R + O;
     constexpr uint32_t END = 0xFFFFu;
-    for (uint32_t i = lane; i < NP; i += WAVE) { L.pcount[i] = 0; L.pfill[i] = 0; L.fc[i] = 0xFFFFu; }
+    for (uint32_t i = lane; i < NP; i += WAVE) { L.pcount[i] = 0; L.fc[i] = 0xFFFFu; }
     for (uint32_t i = lane; i < R; i += WAVE) L.regnode[i] = 0xFFFFu;
     if (lane == 0) *L.nins = 0;
     // compact ids of the list/text objects
@@ -385,16 +384,17 @@ __device__ __forceinline__ void rga_order(const SmallLds &L, uint32_t R, uint32_
         if (r < NP) L.poff[r] = tot + ex;
         tot += tt;
     }
+    if (lane == 0) L.poff[NP] = tot;
     wave_sync();
     for (uint32_t i = lane; i < N; i += WAVE) {
         const uint32_t pi = L.nodepi[i];
-        L.plist[L.poff[pi] + lds_add(&L.pfill[pi], 1u)] = (uint16_t)i;
+        L.plist[L.poff[pi] + lds_add(&L.pcount[pi], 0xFFFFFFFFu) - 1u] = (uint16_t)i;   // counts down to 0
     }
     wave_sync();
     // sibling order: next sibling = the largest smaller key; the largest key is the first child
     for (uint32_t i = lane; i < N; i += WAVE) {
         const uint32_t pi = L.nodepi[i], key = L.nodekey[i];
-        const uint32_t q0 = L.poff[pi], qn = L.pcount[pi];
+        const uint32_t q0 = L.poff[pi], qn = L.poff[pi + 1] - q0;
         uint32_t best = 0xFFFFu, bkey = 0;
         bool firstc = true;
         for (uint32_t q = 0; q < qn; q++) {
@@ -1678,6 +1678,10 @@ size_t hm_small_lds_bytes(uint32_t opl, uint32_t cls, bool lists, bool counters)
 uint32_t hm_small_occupancy(uint32_t opl, uint32_t cls, bool lists, bool counters) {
     const size_t lds = hm_small_lds_bytes(opl, cls, lists, counters);
     int n = 0;
+    // the persistent grid must be resident at once (a wave that starts after the others drain
+    // runs its documents serially at the end): also bound by the LDS with the allocation rounded
+    // to 512 bytes (a 13,376-byte carve reported 12 workgroups per CU and ran as if 11 fit)
+    const int by_lds = (int)(160u * 1024u / ((lds + 511) & ~(size_t)511));
 #define HM_OCC(O_, L_, C_) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, hm::merge_small_kernel<O_, L_, C_>, WAVE, lds)
 #define HM_OCC_OPL(L_, C_) switch (opl) { case 1: HM_OCC(1, L_, C_); break; case 2: HM_OCC(2, L_, C_); break; case 3: HM_OCC(3, L_, C_); break; default: HM_OCC(4, L_, C_); }
     if (cls == 0)      { if (lists) { HM_OCC_OPL(true, 0) } else { HM_OCC_OPL(false, 0) } }
@@ -1685,6 +1689,7 @@ uint32_t hm_small_occupancy(uint32_t opl, uint32_t cls, bool lists, bool counter
     else               { if (lists) { HM_OCC_OPL(true, 1) } else { HM_OCC_OPL(false, 1) } }
 #undef HM_OCC_OPL
 #undef HM_OCC
+    if (n > by_lds) n = by_lds;
     return n > 0 ? (uint32_t)n : 1u;
 }
 

@@ -17,5 +17,7 @@ nd=d.get('node_docbackend') or {}
 rt=d.get('resident_incremental_text') or {}
 print('text', {k: rt.get(k) for k in ('value','remerge_value','speedup_vs_remerge','same_as_remerge','all_incremental','incremental_share','oracle_docs_equal','us_per_round')})
 for r in rt.get('rounds', []): print(r['docs'], r['incremental']['ms'], r['remerge']['ms'])
+r5=d.get('resident_incremental_c5') or {}
+print('c5', {k: r5.get(k) for k in ('value','remerge_value','speedup_vs_remerge','same_as_remerge','incremental_share','bail_share','oracle_docs_equal')})
 print('node', {k: nd.get(k) for k in ('gpu_async_vs_js','gpu_async_vs_js_blocks','same_state','same_clocks')}, {c: {k: (nd.get(c) or {}).get(k) for k in ('gpu_async_vs_js','same_state','same_clocks','error')} for c in ('C3','C5')})
 "
