@@ -485,6 +485,7 @@ static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handl
         A.S = S; A.stamp = ++s->stamp ? s->stamp : ++s->stamp; A.incremental = s->incremental && S <= 64 ? 1u : 0u;
         A.dm = s->dm; A.res_docs = s->res_docs; A.seen = s->seen; A.plan = s->plan.p; A.descs = s->descs.p;
         A.list = s->list.p; A.st = s->st;
+        A.ist = A.incremental ? s->ist : nullptr; A.ops = t_op;
         // plan: checks, growth, routes (nothing in the store changes)
         if ((rc = reset_stats(s))) return rc;
         SCHK(s, hm_launch_plan(A, st));

@@ -136,6 +136,8 @@ struct PlanArgs {
     AppendDesc *descs;
     uint32_t *list;                            // cold handles
     PlanStats *st;
+    const IncState *ist;                       // incremental stores: documents the incremental kernel
+    const hm_op_row *ops;                      //   would hand back are routed to the re-merge at once
 };
 hipError_t hm_launch_plan(const PlanArgs &a, hipStream_t s);
 hipError_t hm_launch_alloc(const PlanArgs &a, hipStream_t s);

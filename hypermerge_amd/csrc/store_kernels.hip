@@ -261,9 +261,23 @@ __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
     // ops hit); the rest re-merge their whole log
     const hm_doc_result last = a.res_docs[live ? h : 0u];
     const uint32_t tgt = r.n_deps + r.n_changes;
-    const bool inc = live && a.incremental && last.status == HM_OK && last.n_queued == 0 && !remapped && r.n_changes > 0 &&
-                     r.n_changes <= HM_INC_MAX_NEW_C && r.n_ops <= HM_INC_MAX_NEW_O && tgt <= HM_INC_MAX_TGT &&
-                     m.n_r <= r.n_regs && r.n_actors <= a.S;
+    bool inc = live && a.incremental && last.status == HM_OK && last.n_queued == 0 && !remapped && r.n_changes > 0 &&
+               r.n_changes <= HM_INC_MAX_NEW_C && r.n_ops <= HM_INC_MAX_NEW_O && tgt <= HM_INC_MAX_TGT &&
+               m.n_r <= r.n_regs && r.n_actors <= a.S;
+    if (inc && a.ist) {
+        // what inc_group_kernel would hand straight back (its state checks, and for documents with
+        // lists its op checks): no metadata, or an op it does not take — object creation, an op on
+        // an object that is neither a map of the log nor the document's one resident list
+        const IncState I = a.ist[h];
+        if ((I.flags & (HM_IST_VALID | HM_IST_NOCKEY)) != HM_IST_VALID) inc = false;
+        else if ((r.flags | m.flags) & HM_DOC_HAS_LISTS)
+            for (uint32_t k = r.op_off; k < r.op_off + r.n_ops && inc; k++) {
+                const uint4 w = reinterpret_cast<const uint4 *>(a.ops + k)[0];
+                const uint32_t act = reinterpret_cast<const uint4 *>(a.ops + k)[1].x & 0xFFu, obj = w.x;
+                const bool lst = (I.flags & HM_IST_LIST) && obj == I.pad[1];
+                if (act <= HM_MAKE_TEXT || (!lst && obj != 0 && (obj >= 64 || !((I.mapmask >> obj) & 1ull)))) inc = false;
+            }
+    }
     p.inc = inc ? 1u : 0u;
     p.remapped = remapped ? 1u : 0u;
     if (live) a.plan[i] = p;
