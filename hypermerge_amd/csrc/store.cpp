@@ -79,6 +79,7 @@ struct hm_store {
     DBuf<AppendDesc> descs, bdescs;
     DBuf<uint32_t> list;                          // re-merge list (cold, then handed back)
     DBuf<uint32_t> blist;                         // rollback list
+    DBuf<uint32_t> alist;                         // append list (batch rows with append work)
     DBuf<uint8_t> remap, inv;
     DBuf<hm_doc_row> rows;
     PlanStats *st = nullptr;
@@ -380,7 +381,7 @@ void hm_store_destroy(hm_store *s) {
     void *bufs[] = {s->changes, s->hist, s->ckey, s->all_deps, s->deps, s->ops, s->surv, s->smeta, s->ist, s->regs, s->epos,
                     s->epar, s->ekey, s->lorder, s->res_docs, s->clock,
                     s->back_clock, s->heads, s->min_clock, s->stored, s->stage.p, s->dm, s->seen, s->plan.p, s->descs.p,
-                    s->bdescs.p, s->list.p, s->blist.p, s->remap.p, s->inv.p, s->rows.p, s->undo_handles.p, s->st};
+                    s->bdescs.p, s->list.p, s->blist.p, s->alist.p, s->remap.p, s->inv.p, s->rows.p, s->undo_handles.p, s->st};
     for (void *b : bufs) if (b) (void)hipFree(b);
     delete s;
 }
@@ -486,6 +487,8 @@ static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handl
         A.dm = s->dm; A.res_docs = s->res_docs; A.seen = s->seen; A.plan = s->plan.p; A.descs = s->descs.p;
         A.list = s->list.p; A.st = s->st;
         A.ist = A.incremental ? s->ist : nullptr; A.ops = t_op;
+        if ((rc = ensure_buf(s, s->alist, n))) return rc;
+        A.alist = s->alist.p;
         // plan: checks, growth, routes (nothing in the store changes)
         if ((rc = reset_stats(s))) return rc;
         SCHK(s, hm_launch_plan(A, st));
@@ -517,7 +520,7 @@ static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handl
         // segments, descriptors, totals, re-merge list; append; incremental apply
         SCHK(s, hm_launch_alloc(A, st));
         StoreArenas ar = {s->changes, s->deps, s->ops, s->min_clock, s->stored};
-        SCHK(s, hm_launch_append(s->descs.p, n, ar, ar, A.changes, t_dp, t_op, A.remap, S, st));
+        SCHK(s, hm_launch_append(s->descs.p, n, ar, ar, A.changes, t_dp, t_op, A.remap, S, st, s->alist.p, &s->st->n_app));
         T.mark("alloc+append");
         uint32_t *bail = (uint32_t *)(sp + L.o_bail);
         SCHK(s, hipMemsetAsync(bail, 0, 4, st));

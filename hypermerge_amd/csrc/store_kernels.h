@@ -42,7 +42,7 @@ struct PlanRow {
 // What the host reads back of a submit's device-side plan (one small copy per phase).
 struct PlanStats {
     uint32_t err;                              // HM_PLAN_* bits of the failed checks
-    uint32_t n_inc, n_cold, n_back;
+    uint32_t n_inc, n_cold, n_back, n_app;       // (n_app: batch rows append_kernel has work for)
     uint32_t mx[6];                            // incremental tile maxima (hm_inc_dims)
     uint32_t max_c, max_o, max_r, max_objs, max_d, flags;   // launch hints of a merge list
     unsigned long long need[4];                // rows the submit's growing segments take, per space
@@ -135,6 +135,7 @@ struct PlanArgs {
     PlanRow *plan;
     AppendDesc *descs;
     uint32_t *list;                            // cold handles
+    uint32_t *alist;                           // batch rows to append (cold, moved or re-ranked)
     PlanStats *st;
     const IncState *ist;                       // incremental stores: documents the incremental kernel
     const hm_op_row *ops;                      //   would hand back are routed to the re-merge at once
@@ -186,7 +187,8 @@ hipError_t hm_launch_inc_meta(const MetaArgs &a, hipStream_t s);
 hipError_t hm_launch_epos_clear(const uint32_t *list, uint32_t n, const DevDoc *dm, uint32_t *epos, hipStream_t s);
 hipError_t hm_launch_append(const AppendDesc *descs, uint32_t n_desc, const StoreArenas &src, const StoreArenas &dst,
                             const hm_change_row *st_changes, const hm_dep_row *st_deps, const hm_op_row *st_ops,
-                            const uint8_t *remap, uint32_t S, hipStream_t s);
+                            const uint8_t *remap, uint32_t S, hipStream_t s,
+                            const uint32_t *list = nullptr, const uint32_t *count = nullptr);
 hipError_t hm_launch_read_regs(uint32_t n, const uint32_t *abs_reg, const uint32_t *surv_base, const hm_reg_result *regs,
                                const hm_surv_result *surv, hm_reg_result *out_regs, hm_surv_result *out_surv, uint32_t cap,
                                uint32_t *counter, hipStream_t s);

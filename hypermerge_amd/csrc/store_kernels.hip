@@ -28,11 +28,16 @@ namespace hms {
 __global__ __launch_bounds__(SWG) void append_kernel(const AppendDesc *descs, uint32_t n_desc, StoreArenas src,
                                                      StoreArenas dst, const hm_change_row *st_changes,
                                                      const hm_dep_row *st_deps, const hm_op_row *st_ops,
-                                                     const uint8_t *remap, uint32_t S) {
+                                                     const uint8_t *remap, uint32_t S, const uint32_t *list,
+                                                     const uint32_t *count) {
     // one wave per document (a submit's appends are a few rows each; a 256-lane group per
-    // document would idle most of its lanes), four documents per workgroup
+    // document would idle most of its lanes), four documents per workgroup; with a list, only
+    // the listed batch rows (alloc_kernel lists the documents with work here: a round of
+    // incremental documents whose segments did not move has none)
     const uint32_t t = threadIdx.x & 63, W = 64;
-    for (uint32_t di = blockIdx.x * 4 + (threadIdx.x >> 6); di < n_desc; di += gridDim.x * 4) {
+    const uint32_t nd = list ? *count : n_desc;
+    for (uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 6); k < nd; k += gridDim.x * 4) {
+        const uint32_t di = list ? list[k] : k;
         const AppendDesc D = descs[di];
         const bool moved = D.src_c != D.dst_c || D.src_d != D.dst_d || D.src_o != D.dst_o || src.changes != dst.changes;
         if (D.inc && !moved) continue;                  // the incremental kernel appends its rows itself
@@ -327,6 +332,14 @@ __global__ void alloc_kernel(PlanArgs a) {
     a.descs[i] = D;
     a.dm[h] = m;
     if (!p.inc) a.list[atomicAdd(&a.st->n_cold, 1u)] = h;
+    // the rows append_kernel must visit, one counter atomic per wave
+    const bool app = !p.inc || p.g[0] || p.g[1] || p.g[2] || p.remapped;
+    const unsigned long long am = __ballot(app);
+    const uint32_t ln = threadIdx.x & 63, lead = am ? (uint32_t)__builtin_ctzll(am) : 0u;
+    uint32_t base = 0;
+    if (am && ln == lead) base = atomicAdd(&a.st->n_app, (uint32_t)__popcll(am));
+    base = (uint32_t)__shfl((int)base, (int)lead);
+    if (app) a.alist[base + (uint32_t)__popcll(am & ((1ull << ln) - 1))] = i;
 }
 
 __global__ __launch_bounds__(PLAN_WG) void doc_rows_kernel(const uint32_t *list, uint32_t n, const DevDoc *dm, hm_doc_row *rows,
@@ -530,11 +543,12 @@ hipError_t hm_launch_read_hist(uint32_t n, const uint32_t *handles, const uint32
 
 hipError_t hm_launch_append(const AppendDesc *descs, uint32_t n_desc, const StoreArenas &src, const StoreArenas &dst,
                             const hm_change_row *st_changes, const hm_dep_row *st_deps, const hm_op_row *st_ops,
-                            const uint8_t *remap, uint32_t S, hipStream_t s) {
+                            const uint8_t *remap, uint32_t S, hipStream_t s, const uint32_t *list, const uint32_t *count) {
     if (!n_desc) return hipSuccess;
-    const uint32_t grid = (n_desc + 3) / 4 < 65535u ? (n_desc + 3) / 4 : 65535u;
+    const uint32_t cap = list ? 2048u : 65535u;                 // (a listed launch: the count is on the device)
+    const uint32_t grid = (n_desc + 3) / 4 < cap ? (n_desc + 3) / 4 : cap;
     hipLaunchKernelGGL(hms::append_kernel, dim3(grid), dim3(SWG), 0, s, descs, n_desc, src, dst, st_changes, st_deps,
-                       st_ops, remap, S);
+                       st_ops, remap, S, list, count);
     return hipGetLastError();
 }
 
