@@ -72,65 +72,94 @@ __device__ __forceinline__ uint64_t abs64(int64_t v) { return v < 0 ? (uint64_t)
 constexpr unsigned long long TWO53 = 1ull << 53;
 
 // ---------------- list / text ops (G = 64: one document per wave) ----------------
-// The document's list order is resident (lorder / epos / epar / ekey, HM_IST_LIST).  A round's
-// `ins` ops take the fast path of applyInsert when every new element hangs off an element that
-// exists (or one this round inserted earlier) and, under an old parent, sorts before that
-// parent's current first child (lamportCompare (elem, actor) DESCENDING: the typing case, a new
-// element with the largest elem counter): the new elements then form blocks, one per old anchor,
-// in pre-order of their own forest, placed right after the anchor; every old element after an
-// anchor shifts by the blocks before it.  Anything else (concurrent inserts under one parent that
-// sort after an existing child, an insert after an element not inserted yet, a duplicate elemId)
-// goes to the re-merge.  Sets / deletes on elements are applyAssign as for map keys; the visible
-// indices are then rewritten from the first position that changed.
+// The document's lists have their order resident (lorder / epos / epar / ekey and the list
+// directory, HM_IST_LIST): the lists end to end in object-id order, so an element's position is
+// global and list k occupies [base_k, base_k + count_k).  A round's `ins` ops take the fast path
+// of applyInsert when every new element hangs off an element of its own list that exists (or
+// one this round inserted earlier) or off the list's '_head', and, under an old parent, sorts
+// before that parent's current first child (lamportCompare (elem, actor) DESCENDING: the typing
+// case, a new element with the largest elem counter): the new elements then form blocks, one per
+// old anchor, in pre-order of their own forest, placed at the anchor's insertion point; every
+// old element after an insertion point (later lists' included) shifts by the blocks before it.
+// Anything else (concurrent inserts under one parent that sort after an existing child, an
+// insert after an element not inserted yet, a duplicate elemId) goes to the re-merge.  Sets /
+// deletes on elements are applyAssign as for map keys; the visible indices (per list) are then
+// rewritten from the first position that changed.
 constexpr uint32_t LSCR = 192;                 // per document: anchors (64), cumulative block sizes (64), subtree sizes (64)
+constexpr uint32_t LMAX = HM_INC_LISTS;
 
 struct ListPlan {
-    uint32_t n_el0, n_el;                      // elements before / after the submit (uniform)
-    uint32_t na, pmin, q0;                     // anchors, first old position that moves, first index that changes
+    uint32_t n_el0, n_el;                      // elements before / after the submit, all lists (uniform)
+    uint32_t na, pmin, q0;                     // anchors, first old position that moves, first position that changes
     uint32_t npos, key;                        // ins lanes: the new element's position and lamport key
+    uint32_t nl;                               // lists (uniform)
+    uint32_t bnew, cnew;                       // lane k < nl: list k's base and elements after the submit
 };
 
 __device__ __forceinline__ uint32_t list_shift(const uint32_t *lscr, uint32_t na, uint32_t i) {
     uint32_t s = 0;
     for (uint32_t k = 0; k < na; k++)
-        if ((int)lscr[k] - 1 < (int)i) s = lscr[64 + k];     // blocks of the anchors before position i
+        if ((int)lscr[k] - 1 < (int)i) s = lscr[64 + k];     // blocks of the anchors at or before position i
     return s;
 }
 
+// the list (directory index) holding global position i, from the lanes' (base, count)
+__device__ __forceinline__ uint32_t list_at(const Grp<64> &g, uint32_t nl, uint32_t b, uint32_t c, uint32_t i) {
+    uint32_t l = HM_NONE;
+    for (uint32_t k = 0; k < nl; k++) {
+        const uint32_t bk = g.sh(b, k), ck = g.sh(c, k);
+        if (i >= bk && i < bk + ck) l = k;
+    }
+    return l;
+}
+
+// li: the op's list (directory index; HM_NONE for other ops); dir: lane k < nl holds list k's
+// directory entry (object, elements)
 __device__ int list_plan(const Grp<64> &g, const AppendDesc &D, const IncArgs &A, const IncState &I, uint32_t nno,
-                         uint32_t o_act, uint32_t o_reg, uint32_t o_par, uint32_t o_elem, bool lst, uint32_t opactor,
-                         uint32_t *lscr, ListPlan &lp) {
-    const uint32_t gl = g.gl, n_el = I.pad[0];
+                         uint32_t o_act, uint32_t o_reg, uint32_t o_par, uint32_t o_elem, bool lst, uint32_t li,
+                         uint32_t opactor, uint2 dir, uint32_t *lscr, ListPlan &lp) {
+    const uint32_t gl = g.gl, n_el = I.pad[0], nl = I.pad[1];
+    // the lists' bases (lane k): the counts before list k
+    const uint32_t ck = gl < nl ? dir.y : 0u;
+    uint32_t bk = 0;
+    for (uint32_t k = 0; k < nl; k++) { const uint32_t x = g.sh(ck, k); bk += k < gl ? x : 0u; }   // (every lane shuffles)
+    const uint32_t lix = li < nl ? li : 0u;
+    const uint32_t lb = g.sh(bk, lix), lc = g.sh(ck, lix);            // this op's list
     const bool ins = lst && o_act == HM_INS, eop = lst && o_act != HM_INS;
     const uint64_t insm = g.bits(ins);
     const uint32_t nins = (uint32_t)__popcll(insm);
     const uint32_t key = (o_elem << 8) | (opactor & 0xFFu);
     // a new element's register is fresh (checked by the caller: no op touched it before); its
-    // parent exists: an old element, '_head', or an element inserted earlier in this round; an
-    // assign hits an element that exists
+    // parent exists in its own list: an old element, '_head', or an element inserted earlier in
+    // this round; an assign hits an element that exists
     bool bad = false;
     uint32_t pnew = HM_NONE, ecr = HM_NONE;
     for (uint32_t k = 0; k < nno; k++) {
         if (!((insm >> k) & 1ull)) continue;
-        const uint32_t rk = g.sh(o_reg, k);
+        const uint32_t rk = g.sh(o_reg, k), lk = g.sh(li, k);
         if (k < gl && ins && rk == o_reg) bad = true;
-        if (k < gl && ins && rk == o_par) pnew = k;
-        if (k < gl && eop && rk == o_reg) ecr = k;
+        if (k < gl && ins && rk == o_par) { pnew = k; bad |= lk != li; }
+        if (k < gl && eop && rk == o_reg) { ecr = k; bad |= lk != li; }
     }
     const bool root = ins && pnew == HM_NONE;
     uint32_t pold = HM_NONE, eold = HM_NONE;
     if (root && o_par != HM_HEAD) pold = o_par < D.n_old_r ? A.epos[D.src_r + o_par] : HM_NONE;
     if (eop && ecr == HM_NONE) eold = o_reg < D.n_old_r ? A.epos[D.src_r + o_reg] : HM_NONE;
-    bad |= (root && o_par != HM_HEAD && pold >= n_el) || (eop && ecr == HM_NONE && eold >= n_el);
+    bad |= (root && o_par != HM_HEAD && (pold < lb || pold >= lb + lc)) || (eop && ecr == HM_NONE && (eold < lb || eold >= lb + lc));
     if (g.bits(bad)) return INC_BAIL;
+    // the anchor: its insertion point (after the old parent, or the list's start for '_head') and a
+    // key that orders anchors by insertion point, then an element's before the '_head's at the same
+    // point (the end of one list is the start of the next), then '_head's by list (empty lists
+    // share their base with the next list): insertion point << 4 | head << 3 | list
+    const uint32_t ins_at = root ? (o_par == HM_HEAD ? lb : pold + 1u) : 0u;
+    const uint32_t akey = root ? (ins_at << 4) | (o_par == HM_HEAD ? 8u | lix : 0u) : 0u;
     // the positions read back name the registers (a register that is no element has a stale slot)
-    const int pa = root ? (o_par == HM_HEAD ? -1 : (int)pold) : 0;
     uint32_t at_p = HM_NONE, at_e = HM_NONE, nxt = HM_NONE;
-    if (root && pa >= 0) at_p = A.lorder[D.src_r + pa];
-    if (root && (uint32_t)(pa + 1) < n_el) nxt = A.lorder[D.src_r + pa + 1];
+    if (root && o_par != HM_HEAD) at_p = A.lorder[D.src_r + pold];
+    if (root && ins_at < lb + lc) nxt = A.lorder[D.src_r + ins_at];
     if (eop && ecr == HM_NONE) at_e = A.lorder[D.src_r + eold];
-    bad = (root && pa >= 0 && at_p != o_par) || (eop && ecr == HM_NONE && at_e != o_reg);
-    // under an old parent the new element must sort before the parent's first child
+    bad = (root && o_par != HM_HEAD && at_p != o_par) || (eop && ecr == HM_NONE && at_e != o_reg);
+    // under an old parent (or '_head') the new element must sort before the parent's first child
     if (root && nxt != HM_NONE && A.epar[D.src_r + nxt] == o_par && !(key > A.ekey[D.src_r + nxt])) bad = true;
     if (g.bits(bad)) return INC_BAIL;
 
@@ -153,52 +182,63 @@ __device__ int list_plan(const Grp<64> &g, const AppendDesc &D, const IncArgs &A
     uint32_t r0 = ins && !root ? 1u : 0u;
     for (uint32_t k = 0; k < nno; k++) {
         if (!((insm >> k) & 1ull)) continue;
-        const uint32_t pk = g.sh(pnew, k), ak = g.sh((uint32_t)pa, k), kk = g.sh(key, k), sk = g.sh(size, k);
-        const bool same = pnew != HM_NONE ? pk == pnew : (pk == HM_NONE && (int)ak == pa);
+        const uint32_t pk = g.sh(pnew, k), ak = g.sh(akey, k), kk = g.sh(key, k), sk = g.sh(size, k);
+        const bool same = pnew != HM_NONE ? pk == pnew : (pk == HM_NONE && ak == akey);
         if (ins && k != gl && same && kk > key) r0 += sk;
     }
-    uint32_t rank = r0, ranc = (uint32_t)pa;
+    uint32_t rank = r0, ranc = akey;
     {
         uint32_t a = ins ? pnew : HM_NONE;
         for (uint32_t st = 0; st < nins; st++) {
             const uint32_t src = a == HM_NONE ? 0u : a;
-            const uint32_t ra = g.sh(r0, src), pp = g.sh(pnew, src), an = g.sh((uint32_t)pa, src);
+            const uint32_t ra = g.sh(r0, src), pp = g.sh(pnew, src), an = g.sh(akey, src);
             if (a != HM_NONE) { rank += ra; ranc = an; a = pp; }
         }
     }
-    // anchors (distinct root anchors) in position order with their cumulative block sizes
+    // anchors (distinct root anchors) in anchor-key order with their cumulative block sizes
     bool leader = root;
     uint32_t bsize = 0, before = 0;
     for (uint32_t k = 0; k < nno; k++) {
         if (!((insm >> k) & 1ull)) continue;
-        const uint32_t pk = g.sh(pnew, k), ak = g.sh((uint32_t)pa, k), sk = g.sh(size, k);
+        const uint32_t pk = g.sh(pnew, k), ak = g.sh(akey, k), sk = g.sh(size, k);
         if (pk != HM_NONE) continue;
-        if (root && k < gl && (int)ak == pa) leader = false;
-        if (root && (int)ak == pa) bsize += sk;
-        if (ins && (int)ak < (int)ranc) before += sk;      // blocks of the anchors before this element's
+        if (root && k < gl && ak == akey) leader = false;
+        if (root && ak == akey) bsize += sk;
+        if (ins && ak < ranc) before += sk;                   // blocks of the anchors before this element's
     }
     const uint64_t lm = g.bits(leader);
     const uint32_t na = (uint32_t)__popcll(lm);
     uint32_t idx = 0, cum = 0;
     for (uint32_t k = 0; k < nno; k++) {
         if (!((lm >> k) & 1ull)) continue;
-        const uint32_t ak = g.sh((uint32_t)pa, k), bk = g.sh(bsize, k);
-        if (leader && (int)ak < pa) idx++;
-        if (leader && (int)ak <= pa) cum += bk;
+        const uint32_t ak = g.sh(akey, k), bk2 = g.sh(bsize, k);
+        if (leader && ak < akey) idx++;
+        if (leader && ak <= akey) cum += bk2;
     }
-    if (leader) { lscr[idx] = (uint32_t)(pa + 1); lscr[64 + idx] = cum; }
+    if (leader) { lscr[idx] = ins_at; lscr[64 + idx] = cum; }
     __builtin_amdgcn_wave_barrier();
-    uint32_t pmin = ins ? (uint32_t)((int)ranc + 1) : HM_NONE;
+    uint32_t pmin = ins ? (ranc >> 4) : HM_NONE;
     for (uint32_t d = 1; d < 64; d <<= 1) { const uint32_t y = g.sh(pmin, gl ^ d); pmin = y < pmin ? y : pmin; }
     lp.n_el0 = n_el; lp.n_el = n_el + nins; lp.na = na; lp.pmin = nins ? pmin : n_el;
     lp.key = key;
-    lp.npos = ins ? (uint32_t)((int)ranc + 1) + before + rank : HM_NONE;
+    lp.npos = ins ? (ranc >> 4) + before + rank : HM_NONE;
+    lp.nl = nl;
+    // the lists after the submit: counts grow by their inserts, bases follow
+    uint32_t cn = ck;
+    for (uint32_t k = 0; k < nl; k++) {
+        const uint32_t m = (uint32_t)__popcll(g.bits(ins && li == k));
+        if (gl == k) cn += m;
+    }
+    uint32_t bn = 0;
+    for (uint32_t k = 0; k < nl; k++) { const uint32_t x = g.sh(cn, k); bn += k < gl ? x : 0u; }
+    lp.cnew = cn; lp.bnew = bn;
     // the first position whose visible index may change: the first moved one, or an element an
     // assign hits (at its new position)
     uint32_t qe = HM_NONE;
     {
-        const uint32_t cn = g.sh(lp.npos, ecr == HM_NONE ? 0u : ecr);
-        if (eop) qe = ecr != HM_NONE ? cn : eold + list_shift(lscr, na, eold);
+        const uint32_t cnp = g.sh(lp.npos, ecr == HM_NONE ? 0u : ecr);
+        const uint32_t sh = list_shift(lscr, na, eold == HM_NONE ? 0u : eold);
+        if (eop) qe = ecr != HM_NONE ? cnp : eold + sh;
     }
     uint32_t q0 = qe < lp.pmin ? qe : lp.pmin;
     for (uint32_t d = 1; d < 64; d <<= 1) { const uint32_t y = g.sh(q0, gl ^ d); q0 = y < q0 ? y : q0; }
@@ -230,16 +270,20 @@ __device__ void list_insert(const Grp<64> &g, const AppendDesc &D, const IncArgs
     }
 }
 
-// visible indices (hm_reg_result.list_index) from the first position that changed to the end
+// visible indices (hm_reg_result.list_index, counted per list) from the first position that
+// changed to the end of the last list
 __device__ void list_indices(const Grp<64> &g, const AppendDesc &D, const IncArgs &A, const ListPlan &lp) {
-    const uint32_t gl = g.gl;
+    const uint32_t gl = g.gl, nl = lp.nl, bn = lp.bnew, cn = lp.cnew;
     if (lp.q0 >= lp.n_el) return;
-    uint32_t c = 0;                                           // visible elements before q0
-    for (int top = (int)lp.q0 - 1; top >= 0; top -= 64) {
+    const uint32_t l0 = list_at(g, nl, bn, cn, lp.q0);
+    const uint32_t b0 = g.sh(bn, l0 < nl ? l0 : 0u);
+    const uint32_t start = l0 < nl ? b0 : lp.q0;
+    uint32_t c = 0;                                           // visible elements of q0's list before q0
+    for (int top = (int)lp.q0 - 1; top >= (int)start; top -= 64) {
         const int i = top - (int)gl;
         bool v = false;
         int32_t li = -1;
-        if (i >= 0) {
+        if (i >= (int)start) {
             const hm_reg_result &r = A.regs[D.dst_r + A.lorder[D.dst_r + i]];
             v = r.n_surv > 0;
             li = r.list_index;
@@ -252,15 +296,30 @@ __device__ void list_indices(const Grp<64> &g, const AppendDesc &D, const IncArg
         hm_reg_result *r = nullptr;
         bool v = false;
         int32_t old = -1;
+        uint32_t s = 0;                                       // the first lane of this lane's list in the chunk
+        bool cont = true;                                     // this lane's list began before the chunk
         if (i < lp.n_el) {
             r = A.regs + D.dst_r + A.lorder[D.dst_r + i];
             v = r->n_surv > 0;
             old = r->list_index;
         }
+        {
+            const uint32_t l = list_at(g, nl, bn, cn, i < lp.n_el ? i : lp.n_el - 1u);
+            const uint32_t bl = g.sh(bn, l < nl ? l : 0u);        // (every lane shuffles)
+            const uint32_t b = l < nl ? bl : q;
+            cont = b < q;
+            s = cont ? 0u : b - q;
+        }
         const uint64_t m = g.bits(v);
-        const int32_t li = v ? (int32_t)(c + g.below(m)) : -1;
+        const uint64_t mine = m & ((1ull << gl) - 1) & ~((1ull << s) - 1);     // (gl, s < 64)
+        const int32_t li = v ? (int32_t)((cont ? c : 0u) + (uint32_t)__popcll(mine)) : -1;
         if (r && li != old) r->list_index = li;
-        c += (uint32_t)__popcll(m);
+        // the carry: the visible elements of the chunk's last list, this chunk's included
+        const uint32_t last = lp.n_el - 1u - q < 63u ? lp.n_el - 1u - q : 63u;
+        const uint32_t sl = g.sh(s, last);
+        const bool cl = g.sh(cont ? 1u : 0u, last) != 0u;
+        const uint64_t tail = m & (last >= 63 ? ~0ull : ((1ull << (last + 1)) - 1)) & ~((1ull << sl) - 1);
+        c = (cl ? c : 0u) + (uint32_t)__popcll(tail);
     }
 }
 
@@ -293,6 +352,9 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
     // ---- level 2: everything that depends only on the descriptor ----
     const IncState I = A.ist[h];
     const hm_doc_result R0 = A.res_docs[h];
+    // the list directory (one document per wave only: lane k < HM_INC_LISTS holds entry k)
+    uint2 dir = make_uint2(HM_NONE, 0u);
+    if constexpr (G == 64) { if (A.ldir && gl < LMAX) dir = A.ldir[(size_t)h * LMAX + gl]; }
     uint32_t ck = 0, hd = 0, mc = 0;
     if (gl < S) {
         ck = A.clock[(size_t)h * S + gl];
@@ -339,8 +401,17 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
     const uint32_t total_d = g.sh(sd, nnc - 1), total_o = g.sh(so, nnc - 1);
     const bool bad_c = gl < nnc && (ca >= NA || cq == 0 || cq >= (1u << 24) || cdo != xd || coo != xo);
     const int64_t oval = (int64_t)(((uint64_t)o_vhi << 32) | o_vlo);
-    // an op on the document's list / text object (its order is resident: HM_IST_LIST)
-    const bool lst = gl < nno && (I.flags & HM_IST_LIST) && o_obj == I.pad[1];
+    // an op on one of the document's list / text objects (their order is resident: HM_IST_LIST);
+    // li = its list in the directory.  A group of 8 / 16 lanes has no directory: an op on an
+    // object that is not a map of the log marks the document for the one-document-per-wave pass
+    const uint32_t nl = (I.flags & HM_IST_LIST) ? (I.pad[1] < LMAX ? I.pad[1] : LMAX) : 0u;
+    uint32_t li = HM_NONE;
+    if constexpr (G == 64) {
+        for (uint32_t k = 0; k < nl; k++) li = g.sh(dir.x, k) == o_obj ? k : li;
+    } else {
+        li = nl && o_obj != 0 && (o_obj >= 64 || !((I.mapmask >> o_obj) & 1ull)) ? 0u : HM_NONE;
+    }
+    const bool lst = gl < nno && li != HM_NONE;
     const bool bad_o = gl < nno && ((o_act != HM_SET && o_act != HM_DEL && o_act != HM_LINK && o_act != HM_INC &&
                                      !(lst && o_act == HM_INS)) ||
                                     (o_act == HM_INC && o_vt != HM_V_INT && o_vt != HM_V_FLOAT) ||
@@ -487,7 +558,7 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
             // an inserted element's register was never touched: a fresh id, or one the document's
             // declared register count reserved (untouched registers have no object)
             if (g.bits(lst && o_act == HM_INS && o_reg < D.n_old_r && (rr.obj != HM_NONE || rr.n_surv != 0))) return INC_BAIL;
-            const int rc = list_plan(g, D, A, I, nno, o_act, o_reg, o_par, o_elem, lst, g.sh(ca, oj), lscr, lp);
+            const int rc = list_plan(g, D, A, I, nno, o_act, o_reg, o_par, o_elem, lst, li, g.sh(ca, oj), dir, lscr, lp);
             if (rc != INC_DONE) return rc;
         }
     }
@@ -676,6 +747,9 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
         if (G == 64 && any_list) s.pad[0] = lp.n_el;
         A.ist[h] = s;
     }
+    if constexpr (G == 64) {
+        if (any_list && gl < lp.nl) A.ldir[(size_t)h * LMAX + gl] = make_uint2(dir.x, lp.cnew);   // the lists' new lengths
+    }
     return INC_DONE;
 }
 
@@ -743,55 +817,87 @@ __global__ __launch_bounds__(256) void inc_meta_kernel(MetaArgs a) {
         }
         wide = __ballot(wide) != 0;
         unsigned long long mask = 1ull, cabs = 0;
-        uint32_t lmin = HM_NONE, lmax = 0;                   // the list / text objects created
-        for (uint32_t i = lane; i < m.n_o; i += 64) {
-            const hm_op_row o = a.ops[m.o_off + i];
+        // the list / text objects created: distinct, ascending, at most LMAX (lane k holds list k)
+        uint32_t lobj = HM_NONE, nlst = 0;
+        bool over = false;
+        for (uint32_t i0 = 0; i0 < m.n_o; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            hm_op_row o = {};
+            o.action = 0xFF;
+            if (i < m.n_o) o = a.ops[m.o_off + i];
             if ((o.action == HM_MAKE_MAP || o.action == HM_MAKE_TABLE) && o.obj < 64) mask |= 1ull << o.obj;
-            if (o.action == HM_MAKE_LIST || o.action == HM_MAKE_TEXT) {
-                lmin = o.obj < lmin ? o.obj : lmin;
-                lmax = o.obj > lmax ? o.obj : lmax;
-            }
             if (o.vtag == HM_V_INT && (o.action == HM_INC || (o.action == HM_SET && o.datatype == HM_DT_COUNTER))) {
                 const unsigned long long v = abs64((int64_t)o.value);
                 cabs = cabs + v < cabs || cabs + v > (1ull << 62) ? (1ull << 62) : cabs + v;
+            }
+            // (a duplicate of the creating change repeats its make op: the same object)
+            for (unsigned long long mk = __ballot(o.action == HM_MAKE_LIST || o.action == HM_MAKE_TEXT); mk; mk &= mk - 1) {
+                const uint32_t ob = (uint32_t)__shfl((int)o.obj, (int)__builtin_ctzll(mk));
+                if (__ballot(lane < nlst && lobj == ob)) continue;
+                if (nlst == LMAX) { over = true; continue; }
+                const uint32_t at = (uint32_t)__popcll(__ballot(lane < nlst && lobj < ob));
+                const uint32_t prev = (uint32_t)__shfl((int)lobj, (int)(lane ? lane - 1 : 0));
+                if (lane == at) lobj = ob;
+                else if (lane > at && lane <= nlst) lobj = prev;
+                nlst++;
             }
         }
         for (uint32_t d = 1; d < 64; d <<= 1) {
             mask |= (unsigned long long)__shfl_xor((long long)mask, d);
             const unsigned long long y = (unsigned long long)__shfl_xor((long long)cabs, d);
             cabs = cabs + y > (1ull << 62) ? (1ull << 62) : cabs + y;
-            const uint32_t a0 = (uint32_t)__shfl_xor((int)lmin, d), a1 = (uint32_t)__shfl_xor((int)lmax, d);
-            lmin = a0 < lmin ? a0 : lmin;
-            lmax = a1 > lmax ? a1 : lmax;
         }
-        // (a duplicate of the creating change repeats its make op: the same object)
-        const uint32_t n_lists = lmin == HM_NONE ? 0u : (lmin == lmax ? 1u : 2u), lobj = lmin;
-        // one list / text object: its order from the element positions of the merge
+        // the lists' order from the element positions of the merge (within each list), laid end
+        // to end: every applied insert counted per list, then placed at its list's base
         uint32_t flags = HM_IST_VALID | (wide ? HM_IST_NOCKEY : 0u), n_el = 0;
-        if (n_lists == 1 && lobj < 64 && a.lorder) {
+        if (nlst && !over && a.lorder && a.ldir) {
             bool ok = true;
-            uint32_t cnt = 0;
-            for (uint32_t i = lane; i < m.n_o; i += 64) {
-                const hm_op_row o = a.ops[m.o_off + i];
-                bool applied_ins = false;
-                if (o.action == HM_INS) {
-                    const uint32_t c = change_of_op(ch, m.n_c, m.o_off, i);
-                    applied_ins = a.hist[m.c_off + c] >= 0;          // (a duplicate's copy: its twin counts)
-                    if (applied_ins) {
+            uint32_t cnt = 0;                                  // lane k < nlst: list k's elements
+            for (uint32_t pass = 0; pass < 2 && ok; pass++) {
+                uint32_t bk = 0;                               // pass 1: lane k holds list k's base
+                if (pass)
+                    for (uint32_t k = 0; k < nlst; k++) {
+                        const uint32_t x = (uint32_t)__shfl((int)cnt, (int)k);     // (every lane shuffles)
+                        bk += k < lane ? x : 0u;
+                    }
+                for (uint32_t i0 = 0; i0 < m.n_o; i0 += 64) {
+                    const uint32_t i = i0 + lane;
+                    hm_op_row o = {};
+                    o.action = 0xFF;
+                    if (i < m.n_o) o = a.ops[m.o_off + i];
+                    bool applied_ins = false;
+                    uint32_t c = 0, lk = HM_NONE;
+                    if (o.action == HM_INS) {
+                        c = change_of_op(ch, m.n_c, m.o_off, i);
+                        applied_ins = a.hist[m.c_off + c] >= 0;          // (a duplicate's copy: its twin counts)
+                    }
+                    for (uint32_t k = 0; k < nlst; k++) lk = (uint32_t)__shfl((int)lobj, (int)k) == o.obj ? k : lk;
+                    // (every lane shuffles: a lane that places nothing still serves as a source)
+                    const uint32_t lkc = lk < nlst ? lk : 0u;
+                    const uint32_t lb = (uint32_t)__shfl((int)bk, (int)lkc), lc = (uint32_t)__shfl((int)cnt, (int)lkc);
+                    if (!pass) {
+                        ok &= !applied_ins || (lk != HM_NONE && o.elem < (1u << 24));
+                        for (uint32_t k = 0; k < nlst; k++) {
+                            const uint32_t nk = (uint32_t)__popcll(__ballot(applied_ins && lk == k));
+                            if (lane == k) cnt += nk;
+                        }
+                    } else if (applied_ins) {
                         const uint32_t pos = o.reg < m.n_r ? a.epos[m.r_off + o.reg] : HM_NONE;
-                        ok &= o.obj == lobj && o.elem < (1u << 24) && pos < m.n_r;
-                        if (pos < m.n_r) {
-                            a.lorder[m.r_off + pos] = o.reg;
+                        ok &= pos < lc;
+                        if (pos < lc) {
+                            a.lorder[m.r_off + lb + pos] = o.reg;
+                            a.epos[m.r_off + o.reg] = lb + pos;           // global from here on
                             a.epar[m.r_off + o.reg] = o.parent;
                             a.ekey[m.r_off + o.reg] = (o.elem << 8) | (ch[c].actor & 0xFFu);
                         }
                     }
                 }
-                cnt += (uint32_t)__popcll(__ballot(applied_ins));
+                ok = __ballot(!ok) == 0;
             }
-            n_el = __shfl((int)cnt, 0);
-            ok = __ballot(!ok) == 0;
+            for (uint32_t k = 0; k < nlst; k++) n_el += (uint32_t)__shfl((int)cnt, (int)k);
             // every element placed, at positions 0 .. n_el - 1 (detached elements have none)
+            __threadfence_block();
+            __builtin_amdgcn_wave_barrier();
             if (ok) {
                 bool hole = false;
                 for (uint32_t i = lane; i < m.n_o; i += 64) {
@@ -800,13 +906,16 @@ __global__ __launch_bounds__(256) void inc_meta_kernel(MetaArgs a) {
                 }
                 ok = __ballot(hole) == 0;
             }
-            if (ok) flags |= HM_IST_LIST;
+            if (ok) {
+                flags |= HM_IST_LIST;
+                if (lane < nlst) a.ldir[(size_t)h * LMAX + lane] = make_uint2(lobj, cnt);
+            }
         }
         if (lane == 0) {
-            IncState s = {};
-            s.s_used = r.n_surv; s.flags = flags; s.cabs = cabs; s.mapmask = mask;
-            s.pad[0] = n_el; s.pad[1] = (flags & HM_IST_LIST) ? lobj : HM_NONE;
-            a.ist[h] = s;
+            IncState st = {};
+            st.s_used = r.n_surv; st.flags = flags; st.cabs = cabs; st.mapmask = mask;
+            st.pad[0] = (flags & HM_IST_LIST) ? n_el : 0u; st.pad[1] = (flags & HM_IST_LIST) ? nlst : 0u;
+            a.ist[h] = st;
         }
     }
 }

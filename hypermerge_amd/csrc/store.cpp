@@ -71,6 +71,7 @@ struct hm_store {
     size_t cap_h = 0;
     DevDoc *dm = nullptr;                         // segments and totals
     IncState *ist = nullptr;                      // survivor slots / metadata state of the incremental path
+    uint2 *ldir = nullptr;                        // list directory (HM_INC_LISTS per handle)
     uint32_t *seen = nullptr;                     // submit stamps (repeated-handle check)
     hm_doc_result *res_docs = nullptr;
     uint32_t *clock = nullptr, *back_clock = nullptr, *heads = nullptr, *min_clock = nullptr, *stored = nullptr;
@@ -166,19 +167,21 @@ int ensure_handles(hm_store *s, size_t need) {
     const size_t cap = std::max<size_t>(need, std::max<size_t>(1024, s->cap_h * 2));
     hipStream_t st = hm_engine_stream(s->e);
     const uint32_t S = s->S;
-    hm_doc_result *rd; DevDoc *dm; uint32_t *seen; IncState *ist; int r;
+    hm_doc_result *rd; DevDoc *dm; uint32_t *seen; IncState *ist; uint2 *ldir; int r;
     if ((r = dev_alloc(s, &rd, cap)) || (r = dev_alloc(s, &dm, cap)) || (r = dev_alloc(s, &seen, cap)) ||
-        (r = dev_alloc(s, &ist, cap)))
+        (r = dev_alloc(s, &ist, cap)) || (r = dev_alloc(s, &ldir, cap * HM_INC_LISTS)))
         return r;
     SCHK(s, hipMemsetAsync(rd, 0, cap * sizeof(hm_doc_result), st));
     SCHK(s, hipMemsetAsync(dm, 0, cap * sizeof(DevDoc), st));
     SCHK(s, hipMemsetAsync(seen, 0, cap * 4, st));
     SCHK(s, hipMemsetAsync(ist, 0, cap * sizeof(IncState), st));
+    SCHK(s, hipMemsetAsync(ldir, 0, cap * HM_INC_LISTS * sizeof(uint2), st));
     if (s->cap_h) {
         SCHK(s, hipMemcpyAsync(rd, s->res_docs, s->cap_h * sizeof(hm_doc_result), hipMemcpyDeviceToDevice, st));
         SCHK(s, hipMemcpyAsync(dm, s->dm, s->cap_h * sizeof(DevDoc), hipMemcpyDeviceToDevice, st));
         SCHK(s, hipMemcpyAsync(seen, s->seen, s->cap_h * 4, hipMemcpyDeviceToDevice, st));
         SCHK(s, hipMemcpyAsync(ist, s->ist, s->cap_h * sizeof(IncState), hipMemcpyDeviceToDevice, st));
+        SCHK(s, hipMemcpyAsync(ldir, s->ldir, s->cap_h * HM_INC_LISTS * sizeof(uint2), hipMemcpyDeviceToDevice, st));
     }
     uint32_t **tabs[5] = {&s->clock, &s->back_clock, &s->heads, &s->min_clock, &s->stored};
     uint32_t *nt[5];
@@ -192,7 +195,8 @@ int ensure_handles(hm_store *s, size_t need) {
     if (s->dm) (void)hipFree(s->dm);
     if (s->seen) (void)hipFree(s->seen);
     if (s->ist) (void)hipFree(s->ist);
-    s->res_docs = rd; s->dm = dm; s->seen = seen; s->ist = ist;
+    if (s->ldir) (void)hipFree(s->ldir);
+    s->res_docs = rd; s->dm = dm; s->seen = seen; s->ist = ist; s->ldir = ldir;
     for (int i = 0; i < 5; i++) { if (*tabs[i]) (void)hipFree(*tabs[i]); *tabs[i] = nt[i]; }
     s->cap_h = cap;
     return HM_OK;
@@ -236,6 +240,35 @@ StageLayout layout(size_t nc, size_t nd, size_t no, size_t n, size_t nremap, uin
     return L;
 }
 
+// HM_INC_DEBUG_HANDLE=h (dev diagnostics): the incremental list state of handle h on stderr
+void dbg_list_state(hm_store *s, const char *when) {
+    const char *e = getenv("HM_INC_DEBUG_HANDLE");
+    if (!e) return;
+    const uint32_t h = (uint32_t)atoi(e);
+    if (h >= s->n_handles) return;
+    hipStream_t st = hm_engine_stream(s->e);
+    DevDoc m; IncState I; uint2 dir[HM_INC_LISTS];
+    (void)hipMemcpyAsync(&m, s->dm + h, sizeof m, hipMemcpyDeviceToHost, st);
+    (void)hipMemcpyAsync(&I, s->ist + h, sizeof I, hipMemcpyDeviceToHost, st);
+    (void)hipMemcpyAsync(dir, s->ldir + (size_t)h * HM_INC_LISTS, sizeof dir, hipMemcpyDeviceToHost, st);
+    (void)hipStreamSynchronize(st);
+    std::vector<uint32_t> lo(m.n_r + 1), ep(m.n_r + 1), pa(m.n_r + 1), ek(m.n_r + 1);
+    if (m.n_r) {
+        (void)hipMemcpyAsync(lo.data(), s->lorder + m.r_off, m.n_r * 4, hipMemcpyDeviceToHost, st);
+        (void)hipMemcpyAsync(ep.data(), s->epos + m.r_off, m.n_r * 4, hipMemcpyDeviceToHost, st);
+        (void)hipMemcpyAsync(pa.data(), s->epar + m.r_off, m.n_r * 4, hipMemcpyDeviceToHost, st);
+        (void)hipMemcpyAsync(ek.data(), s->ekey + m.r_off, m.n_r * 4, hipMemcpyDeviceToHost, st);
+        (void)hipStreamSynchronize(st);
+    }
+    fprintf(stderr, "[inc dbg %s] h=%u n_r=%u r_off=%u flags=%u n_el=%u nl=%u dir=", when, h, m.n_r, m.r_off, I.flags, I.pad[0], I.pad[1]);
+    for (uint32_t k = 0; k < HM_INC_LISTS && k < I.pad[1]; k++) fprintf(stderr, "(%u,%u)", dir[k].x, dir[k].y);
+    fprintf(stderr, "\n  lorder:");
+    for (uint32_t i = 0; i < I.pad[0] && i < m.n_r; i++) fprintf(stderr, " %u", lo[i]);
+    fprintf(stderr, "\n  epos/epar/ekey:");
+    for (uint32_t r = 0; r < m.n_r; r++) fprintf(stderr, " %u:%d/%d/%x", r, (int)ep[r], (int)pa[r], ek[r]);
+    fprintf(stderr, "\n");
+}
+
 // Re-merge the `n` documents listed (handles, device) on the engine stream: their launch rows
 // built on the device from their metas, the launch hints read back.
 int launch_list_merge(hm_store *s, const uint32_t *dev_list, uint32_t n) {
@@ -272,7 +305,7 @@ int launch_list_merge(hm_store *s, const uint32_t *dev_list, uint32_t n) {
         MetaArgs M;
         M.list = dev_list; M.n = n; M.dm = s->dm; M.res_docs = s->res_docs; M.changes = s->changes; M.hist = s->hist;
         M.ckey = s->ckey; M.ops = s->ops; M.surv = s->surv; M.smeta = s->smeta; M.ist = s->ist;
-        M.epos = s->epos; M.epar = s->epar; M.ekey = s->ekey; M.lorder = s->lorder;
+        M.epos = s->epos; M.epar = s->epar; M.ekey = s->ekey; M.lorder = s->lorder; M.ldir = s->ldir;
         SCHK(s, hm_launch_inc_meta(M, st));
     }
     SCHK(s, hipStreamSynchronize(st));
@@ -378,7 +411,7 @@ int hm_store_create(hm_engine *e, const hm_store_config *cfg, hm_store **out) {
 void hm_store_destroy(hm_store *s) {
     if (!s) return;
     (void)hipStreamSynchronize(hm_engine_stream(s->e));
-    void *bufs[] = {s->changes, s->hist, s->ckey, s->all_deps, s->deps, s->ops, s->surv, s->smeta, s->ist, s->regs, s->epos,
+    void *bufs[] = {s->changes, s->hist, s->ckey, s->all_deps, s->deps, s->ops, s->surv, s->smeta, s->ist, s->ldir, s->regs, s->epos,
                     s->epar, s->ekey, s->lorder, s->res_docs, s->clock,
                     s->back_clock, s->heads, s->min_clock, s->stored, s->stage.p, s->dm, s->seen, s->plan.p, s->descs.p,
                     s->bdescs.p, s->list.p, s->blist.p, s->alist.p, s->remap.p, s->inv.p, s->rows.p, s->undo_handles.p, s->st};
@@ -530,10 +563,12 @@ static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handl
             IA.st_changes = A.changes; IA.st_deps = t_dp; IA.st_ops = t_op;
             IA.changes = s->changes; IA.deps = s->deps; IA.ops = s->ops; IA.hist = s->hist; IA.ckey = s->ckey; IA.all_deps = s->all_deps;
             IA.regs = s->regs; IA.surv = s->surv; IA.smeta = s->smeta; IA.res_docs = s->res_docs;
-            IA.epos = s->epos; IA.epar = s->epar; IA.ekey = s->ekey; IA.lorder = s->lorder;
+            IA.epos = s->epos; IA.epar = s->epar; IA.ekey = s->ekey; IA.lorder = s->lorder; IA.ldir = s->ldir;
             IA.clock = s->clock; IA.back_clock = s->back_clock; IA.heads = s->heads; IA.min_clock = s->min_clock;
             IA.ist = s->ist; IA.bail = bail; IA.defer = (uint32_t *)(sp + L.o_defer);
+            dbg_list_state(s, "before");
             SCHK(s, hm_launch_inc_apply(IA, st));
+            dbg_list_state(s, "after");
         }
         T.mark("incremental");
         // the re-merge list: cold documents, then those the incremental kernel handed back
@@ -543,6 +578,7 @@ static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handl
         SCHK(s, hipStreamSynchronize(st));
         if (counts[1]) SCHK(s, hipMemcpyAsync(s->list.p + counts[0], bail + 1, (size_t)counts[1] * 4, hipMemcpyDeviceToDevice, st));
         if ((rc = launch_list_merge(s, s->list.p, counts[0] + counts[1]))) return rc;
+        dbg_list_state(s, "after merge");
         T.mark("remerge");
         s->st_inc = P.n_inc - counts[1]; s->st_cold = counts[0]; s->st_bail = counts[1];
         uint32_t *fail = (uint32_t *)(sp + L.o_fail);

@@ -83,11 +83,14 @@ static_assert(sizeof(IncState) == 32, "IncState is 32 B");
 // incremental path finds a fold source in a few 64-byte lines instead of the 24-byte change rows
 // (documents with a seq >= 2^24 are not packed: HM_IST_NOCKEY, they re-merge)
 #define HM_IST_NOCKEY 2u
-// the document has exactly one list / text object and its order is resident: lorder[reg slot k]
-// = the element register at position k (every inserted element, visible or not), per element
+// the document's list / text objects (at most HM_INC_LISTS) have their order resident: the
+// lists laid end to end in object-id order, lorder[reg slot k] = the element register at
+// position k of that concatenation (every inserted element, visible or not), per element
 // register epos (its position), epar (parent element register | HM_HEAD) and ekey (elem << 8 |
-// actor: lamportCompare's key); IncState.pad[0] = elements, pad[1] = the list's object id
+// actor: lamportCompare's key); the list directory ldir[handle][k] = (object id, elements) of
+// list k; IncState.pad[0] = elements of all lists, pad[1] = lists
 #define HM_IST_LIST 4u
+#define HM_INC_LISTS 8u
 __host__ __device__ inline uint32_t hm_ckey(uint32_t actor, uint32_t seq, bool applied) {
     return (seq & 0xFFFFFFu) | ((actor & 0x7Fu) << 24) | (applied ? 0x80000000u : 0u);
 }
@@ -110,6 +113,7 @@ struct IncArgs {
     hm_surv_result *surv;
     uint2 *smeta;
     uint32_t *epos, *epar, *ekey, *lorder;     // list order (reg space), HM_IST_LIST documents
+    uint2 *ldir;                               // list directory (HM_INC_LISTS per handle)
     hm_doc_result *res_docs;
     uint32_t *clock, *back_clock, *heads;
     const uint32_t *min_clock;
@@ -181,6 +185,7 @@ struct MetaArgs {
     uint2 *smeta;
     IncState *ist;
     uint32_t *epos, *epar, *ekey, *lorder;
+    uint2 *ldir;
 };
 hipError_t hm_launch_inc_meta(const MetaArgs &a, hipStream_t s);
 // element positions of the listed list documents reset (HM_NONE) before their re-merge writes them

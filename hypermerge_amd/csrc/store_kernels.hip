@@ -279,8 +279,10 @@ __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
             for (uint32_t k = r.op_off; k < r.op_off + r.n_ops && inc; k++) {
                 const uint4 w = reinterpret_cast<const uint4 *>(a.ops + k)[0];
                 const uint32_t act = reinterpret_cast<const uint4 *>(a.ops + k)[1].x & 0xFFu, obj = w.x;
-                const bool lst = (I.flags & HM_IST_LIST) && obj == I.pad[1];
-                if (act <= HM_MAKE_TEXT || (!lst && obj != 0 && (obj >= 64 || !((I.mapmask >> obj) & 1ull)))) inc = false;
+                // (a document whose lists are resident: the incremental kernel checks the object
+                // against its list directory)
+                if (act <= HM_MAKE_TEXT ||
+                    (!(I.flags & HM_IST_LIST) && obj != 0 && (obj >= 64 || !((I.mapmask >> obj) & 1ull)))) inc = false;
             }
     }
     p.inc = inc ? 1u : 0u;

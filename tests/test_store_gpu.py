@@ -200,7 +200,7 @@ def test_bad_remap_leaves_store_unchanged(engine):
     ("C4", 300, {}, 2, 0.9, 8),                            # generation order: every arrival applies at once
     ("C4", 300, {"arrival": 1}, 3, True, 8),               # actor-major: some arrivals wait -> re-merge
     ("C2", 200, {}, 2, 0.9, 8),                            # counter sets and incs applied incrementally
-    ("C5", 150, {}, 2, False, 8),                          # lists / nested objects / duplicates: re-merge
+    ("C5", 150, {}, 2, True, 8),                           # two lists, nested objects, duplicates
     ("C1", 1, {"changes_per_actor": 300}, 4, True, 8),     # one long two-actor document
     ("FC", 60, {}, 2, True, 8),                            # integral and f64 counters, shuffled (queued) arrivals
     ("C4", 200, {}, 6, 0.9, 16),                           # 16 lanes per document (inc_group_kernel<16>)
@@ -398,6 +398,49 @@ def _text_rounds():
     rounds.append([ch(A, 5, {B: 4}, d(f"{B}:10", T), ins(T, f"{B}:11", 12), s(f"{A}:12", "z", T)),
                    ch(A, 6, {}, ins(T, f"{A}:12", 13), s(f"{A}:13", "w", T))])
     return rounds
+
+
+def _lists_rounds():
+    """Four list objects in one document (a list, a text, and two lists that stay empty until a
+    later round, then get their first elements in one change), edited round by round: an append at the end of the first list and an insert
+    at the head of the second in one change (both at the same point of the concatenated order),
+    inserts in the middle, at a head, into the empty list, deletes, an overwrite, a change that
+    touches every list, and a concurrent insert that sorts after an existing child."""
+    L, T, E, F = "list-1", "text-2", "list-3", "list-4"
+    A, B = "aaaa", "bbbb"
+    rounds = [[ch(A, 1, {}, mk("makeList", L), link("l", L), mk("makeText", T), link("t", T), mk("makeList", E),
+                  link("e", E), mk("makeList", F), link("f", F), ins(L, "_head", 1), s(f"{A}:1", 10, L), ins(L, f"{A}:1", 2), s(f"{A}:2", 20, L),
+                  ins(T, "_head", 3), s(f"{A}:3", "x", T))]]
+    rounds.append([ch(A, 2, {}, ins(L, f"{A}:2", 4), s(f"{A}:4", 30, L), ins(T, "_head", 5), s(f"{A}:5", "y", T))])
+    rounds.append([ch(B, 1, {A: 2}, ins(T, f"{A}:3", 6), s(f"{B}:6", "z", T), d(f"{A}:1", L))])
+    rounds.append([ch(B, 2, {A: 2}, ins(L, "_head", 7), s(f"{B}:7", 5, L), ins(F, "_head", 14), s(f"{B}:14", "F", F),
+                      ins(E, "_head", 8), s(f"{B}:8", "e", E))])                               # two empty lists at one point
+    rounds.append([ch(A, 3, {B: 2}, ins(E, f"{B}:8", 9), s(f"{A}:9", "f", E), s(f"{A}:4", 31, L),
+                      ins(T, f"{A}:5", 10), s(f"{A}:10", "w", T), ins(L, f"{B}:7", 11), s(f"{A}:11", 6, L))])
+    rounds.append([ch(B, 3, {A: 3}, ins(L, f"{B}:7", 4), s(f"{B}:4", 7, L))])                  # concurrent, sorts later
+    rounds.append([ch(A, 4, {B: 3}, d(f"{A}:10", T), ins(E, "_head", 12), s(f"{A}:12", "g", E)),
+                   ch(A, 5, {}, ins(L, f"{A}:4", 13), s(f"{A}:13", 40, L), s("title", "lists"))])
+    return rounds
+
+
+def test_incremental_edits_on_several_lists(engine):
+    """The incremental path with a document's lists end to end in one resident order (the list
+    directory): every call equal to the whole-log re-merge and to the oracle's cold merge."""
+    rounds = _lists_rounds()
+    A, B = DocStore(engine, a_stride=8), DocStore(engine, a_stride=8)
+    B.set_incremental(False)
+    ha, hb = A.open(), B.open()
+    routed = []
+    for i, r in enumerate(rounds):
+        ra, rb = A.apply([(ha, r)]), B.apply([(hb, r)])
+        routed.append(A.last_routing()["incremental"])
+        for f in ("docs", "clock", "back_clock", "heads"):
+            np.testing.assert_array_equal(getattr(ra, f), getattr(rb, f), err_msg=f"{f} round {i}")
+        assert int(ra.docs["status"][0]) == 0, (i, ra.docs)
+        bb, g = assert_doc_matches_oracle(A, ha)
+        _, gb = B.read(hb)
+        np.testing.assert_array_equal(g.regs, gb.regs, err_msg=f"round {i}")
+    assert sum(routed[1:]) >= len(rounds) - 2, routed          # the sorts-later insert re-merges
 
 
 def test_rowstore_text_rounds_with_declared_registers(engine):
