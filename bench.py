@@ -229,6 +229,8 @@ def main() -> int:
             incremental_c5["workload"] = (f"C5: {c5.n_docs} nested map / list docs x 4 actors, 20% delivered before "
                                           f"their deps, 3% duplicates; the last 4 changes of each in rounds of 1-2")
             incremental_c5["bail_share"] = 1.0 - incremental_c5["incremental_share"]
+            incremental_c5["policy"] = ("incremental mode 1 (the default): a document with lists and <= 256 ops re-merges "
+                                        "(one small-kernel wave either way) and keeps no incremental state")
             del c5
     # the Node host path end to end through the DocBackend message API (C2 sample)
     node = None

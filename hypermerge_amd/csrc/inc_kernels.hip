@@ -764,7 +764,7 @@ __global__ __launch_bounds__(256) void inc_group_kernel(IncArgs A) {
     for (uint32_t q = blockIdx.x * NG + grp; q < n; q += gridDim.x * NG) {
         const uint32_t di = A.list ? A.list[1 + q] : q;
         const AppendDesc D = A.descs[di];
-        if (!D.inc) continue;
+        if (!D.inc || (G < 64 && D.inc == 2)) continue;            // (inc 2: listed for the wave pass)
         const int rc = inc_doc<G>(D, A, s_sv[grp], s_mt[grp], s_ls[G == 64 ? grp : 0]);
         if (rc != INC_DONE && gl == 0) {
             if (rc == INC_DEFER && A.defer) A.defer[1 + atomicAdd(&A.defer[0], 1u)] = di;
@@ -796,7 +796,10 @@ __global__ __launch_bounds__(256) void inc_meta_kernel(MetaArgs a) {
         const uint32_t h = a.list[q];
         const DevDoc m = a.dm[h];
         const hm_doc_result r = a.res_docs[h];
-        if (r.status != HM_OK || r.n_queued != 0 || r.n_surv > m.o_cap) {
+        // (mode 1: a small document with lists re-merges every round — one small-kernel wave either
+        // way — so it keeps no incremental state at all)
+        if (r.status != HM_OK || r.n_queued != 0 || r.n_surv > m.o_cap ||
+            ((m.flags & HM_DOC_HAS_LISTS) && m.n_o <= a.small_lists)) {
             if (lane == 0) { IncState z = {}; a.ist[h] = z; }
             continue;
         }
@@ -935,8 +938,8 @@ hipError_t hm_launch_inc_apply(const IncArgs &A, hipStream_t s) {
     if (!A.n) return hipSuccess;
     const uint32_t S = A.S;
     if (S > 64) return hipErrorInvalidValue;
+    // (the defer list's count was zeroed before alloc_kernel, which lists the list documents)
     hipError_t z = hipMemsetAsync(A.bail, 0, 4, s);
-    if (z == hipSuccess && A.defer) z = hipMemsetAsync(A.defer, 0, 4, s);
     if (z != hipSuccess) return z;
     auto grid = [](uint32_t n, uint32_t per) { const uint32_t g = (n + per - 1) / per; return g < 65535u ? g : 65535u; };
     if (S <= 8) hipLaunchKernelGGL(hmi::inc_group_kernel<8>, dim3(grid(A.n, 32)), dim3(256), 0, s, A);

@@ -101,6 +101,7 @@ struct hm_store {
     DBuf<uint32_t> undo_handles;
     // incremental applyRemoteChanges (inc_apply_kernel) and the last submit's routing
     bool incremental = true;
+    uint32_t inc_mode = 1;                        // 1: small list documents re-merge (cost policy); 2: every one
     uint32_t st_inc = 0, st_cold = 0, st_bail = 0;
 };
 
@@ -306,6 +307,7 @@ int launch_list_merge(hm_store *s, const uint32_t *dev_list, uint32_t n) {
         M.list = dev_list; M.n = n; M.dm = s->dm; M.res_docs = s->res_docs; M.changes = s->changes; M.hist = s->hist;
         M.ckey = s->ckey; M.ops = s->ops; M.surv = s->surv; M.smeta = s->smeta; M.ist = s->ist;
         M.epos = s->epos; M.epar = s->epar; M.ekey = s->ekey; M.lorder = s->lorder; M.ldir = s->ldir;
+        M.small_lists = s->inc_mode == 1 ? HM_INC_SMALL_LIST_OPS : 0u;
         SCHK(s, hm_launch_inc_meta(M, st));
     }
     SCHK(s, hipStreamSynchronize(st));
@@ -516,10 +518,11 @@ static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handl
         A.docs = t_docs; A.changes = t_ch;
         A.handles = t_hand; A.remap = nremap ? t_remap : nullptr;
         A.n = n; A.n_changes = b->n_changes; A.n_deps = b->n_deps; A.n_ops = b->n_ops; A.n_handles = s->n_handles;
-        A.S = S; A.stamp = ++s->stamp ? s->stamp : ++s->stamp; A.incremental = s->incremental && S <= 64 ? 1u : 0u;
+        A.S = S; A.stamp = ++s->stamp ? s->stamp : ++s->stamp; A.incremental = s->incremental && S <= 64 ? s->inc_mode : 0u;
         A.dm = s->dm; A.res_docs = s->res_docs; A.seen = s->seen; A.plan = s->plan.p; A.descs = s->descs.p;
         A.list = s->list.p; A.st = s->st;
-        A.ist = A.incremental ? s->ist : nullptr; A.ops = t_op;
+        A.ist = A.incremental ? s->ist : nullptr; A.ops = t_op; A.deps = t_dp; A.clock = s->clock;
+        A.defer = (uint32_t *)(sp + L.o_defer);
         if ((rc = ensure_buf(s, s->alist, n))) return rc;
         A.alist = s->alist.p;
         // plan: checks, growth, routes (nothing in the store changes)
@@ -551,6 +554,7 @@ static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handl
             T.mark("compact+plan");
         }
         // segments, descriptors, totals, re-merge list; append; incremental apply
+        SCHK(s, hipMemsetAsync(A.defer, 0, 4, st));
         SCHK(s, hm_launch_alloc(A, st));
         StoreArenas ar = {s->changes, s->deps, s->ops, s->min_clock, s->stored};
         SCHK(s, hm_launch_append(s->descs.p, n, ar, ar, A.changes, t_dp, t_op, A.remap, S, st, s->alist.p, &s->st->n_app));
@@ -731,6 +735,7 @@ int hm_store_set_incremental(hm_store *s, int on) {
     if (on && !s->incremental && s->cap_h)
         SCHK(s, hipMemsetAsync(s->ist, 0, s->cap_h * sizeof(IncState), hm_engine_stream(s->e)));
     s->incremental = on != 0;
+    s->inc_mode = on == 2 ? 2u : 1u;
     return HM_OK;
 }
 

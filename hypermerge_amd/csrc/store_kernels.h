@@ -91,6 +91,9 @@ static_assert(sizeof(IncState) == 32, "IncState is 32 B");
 // list k; IncState.pad[0] = elements of all lists, pad[1] = lists
 #define HM_IST_LIST 4u
 #define HM_INC_LISTS 8u
+// the cost policy of incremental mode 1: a list document of at most this many ops re-merges (one
+// small-kernel wave, all in LDS) rather than taking the one-document-per-wave incremental pass
+#define HM_INC_SMALL_LIST_OPS 256u
 __host__ __device__ inline uint32_t hm_ckey(uint32_t actor, uint32_t seq, bool applied) {
     return (seq & 0xFFFFFFu) | ((actor & 0x7Fu) << 24) | (applied ? 0x80000000u : 0u);
 }
@@ -143,7 +146,10 @@ struct PlanArgs {
     PlanStats *st;
     const IncState *ist;                       // incremental stores: documents the incremental kernel
     const hm_op_row *ops;                      //   would hand back are routed to the re-merge at once
-};
+    const hm_dep_row *deps;                    //   (staged deps, and the resident clocks: changes that
+    const uint32_t *clock;                     //   are not causally ready in arrival order)
+    uint32_t *defer;                           // the one-document-per-wave pass's list ([0] = count):
+};                                             //   documents with list ops go there directly
 hipError_t hm_launch_plan(const PlanArgs &a, hipStream_t s);
 hipError_t hm_launch_alloc(const PlanArgs &a, hipStream_t s);
 // hm_doc_row of each listed handle from its device meta (+ the launch hints in st)
@@ -186,6 +192,7 @@ struct MetaArgs {
     IncState *ist;
     uint32_t *epos, *epar, *ekey, *lorder;
     uint2 *ldir;
+    uint32_t small_lists;                      // list documents of at most this many ops keep no list state
 };
 hipError_t hm_launch_inc_meta(const MetaArgs &a, hipStream_t s);
 // element positions of the listed list documents reset (HM_NONE) before their re-merge writes them

@@ -269,23 +269,50 @@ __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
     bool inc = live && a.incremental && last.status == HM_OK && last.n_queued == 0 && !remapped && r.n_changes > 0 &&
                r.n_changes <= HM_INC_MAX_NEW_C && r.n_ops <= HM_INC_MAX_NEW_O && tgt <= HM_INC_MAX_TGT &&
                m.n_r <= r.n_regs && r.n_actors <= a.S;
+    bool wave = false;                                             // list ops: the one-document-per-wave pass
     if (inc && a.ist) {
         // what inc_group_kernel would hand straight back (its state checks, and for documents with
         // lists its op checks): no metadata, or an op it does not take — object creation, an op on
-        // an object that is neither a map of the log nor the document's one resident list
+        // an object that is neither a map of the log nor one of the document's resident lists
         const IncState I = a.ist[h];
         if ((I.flags & (HM_IST_VALID | HM_IST_NOCKEY)) != HM_IST_VALID) inc = false;
         else if ((r.flags | m.flags) & HM_DOC_HAS_LISTS)
             for (uint32_t k = r.op_off; k < r.op_off + r.n_ops && inc; k++) {
                 const uint4 w = reinterpret_cast<const uint4 *>(a.ops + k)[0];
                 const uint32_t act = reinterpret_cast<const uint4 *>(a.ops + k)[1].x & 0xFFu, obj = w.x;
-                // (a document whose lists are resident: the incremental kernel checks the object
-                // against its list directory)
-                if (act <= HM_MAKE_TEXT ||
-                    (!(I.flags & HM_IST_LIST) && obj != 0 && (obj >= 64 || !((I.mapmask >> obj) & 1ull)))) inc = false;
+                const bool other = obj != 0 && (obj >= 64 || !((I.mapmask >> obj) & 1ull));   // not ROOT / a map
+                if (act <= HM_MAKE_TEXT || (other && !(I.flags & HM_IST_LIST))) inc = false;
+                wave |= other;
             }
+        // causallyReady in arrival order against the resident clock (small strides: the clock in
+        // registers): a change the queue would hold, or a duplicate, goes to the re-merge at once.
+        // Only for documents with lists, whose failed attempt costs a wave each (the map-only
+        // documents' group pass finds it as cheaply as this would)
+        if (inc && a.clock && a.S <= 16 && ((r.flags | m.flags) & HM_DOC_HAS_LISTS)) {
+            uint32_t ck[16];
+#pragma unroll
+            for (uint32_t x = 0; x < 16; x++) ck[x] = x < a.S ? a.clock[(size_t)h * a.S + x] : 0u;
+            for (uint32_t c = r.change_off; c < r.change_off + r.n_changes && inc; c++) {
+                const hm_change_row cr = a.changes[c];
+                uint32_t cur = 0;
+#pragma unroll
+                for (uint32_t x = 0; x < 16; x++) cur = x == cr.actor ? ck[x] : cur;
+                if (cr.actor >= a.S || cr.seq != cur + 1u) { inc = false; break; }
+                for (uint32_t j = 0; j < cr.n_deps && inc; j++) {
+                    const hm_dep_row dr = a.deps[cr.dep_off + j];
+                    uint32_t dv = 0;
+#pragma unroll
+                    for (uint32_t x = 0; x < 16; x++) dv = x == dr.actor ? ck[x] : dv;
+                    if (dr.actor != cr.actor && (dr.actor >= a.S || dr.seq > dv)) inc = false;
+                }
+#pragma unroll
+                for (uint32_t x = 0; x < 16; x++) ck[x] = x == cr.actor ? cr.seq : ck[x];
+            }
+        }
     }
-    p.inc = inc ? 1u : 0u;
+    // cost policy (mode 1): a small list document re-merges in one small-kernel wave
+    if (inc && wave && a.incremental == 1u && m.n_o + r.n_ops <= HM_INC_SMALL_LIST_OPS) inc = false;
+    p.inc = inc ? (wave ? 2u : 1u) : 0u;
     p.remapped = remapped ? 1u : 0u;
     if (live) a.plan[i] = p;
     const unsigned long long im = __ballot(inc);
@@ -334,6 +361,15 @@ __global__ void alloc_kernel(PlanArgs a) {
     a.descs[i] = D;
     a.dm[h] = m;
     if (!p.inc) a.list[atomicAdd(&a.st->n_cold, 1u)] = h;
+    // documents with list ops go to the one-document-per-wave pass directly (one atomic per wave)
+    if (a.defer) {
+        const unsigned long long wm = __ballot(p.inc == 2u);
+        const uint32_t wl = threadIdx.x & 63, wlead = wm ? (uint32_t)__builtin_ctzll(wm) : 0u;
+        uint32_t wb = 0;
+        if (wm && wl == wlead) wb = atomicAdd(&a.defer[0], (uint32_t)__popcll(wm));
+        wb = (uint32_t)__shfl((int)wb, (int)wlead);
+        if (p.inc == 2u) a.defer[1 + wb + (uint32_t)__popcll(wm & ((1ull << wl) - 1))] = i;
+    }
     // the rows append_kernel must visit, one counter atomic per wave
     const bool app = !p.inc || p.g[0] || p.g[1] || p.g[2] || p.remapped;
     const unsigned long long am = __ballot(app);

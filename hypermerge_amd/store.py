@@ -231,10 +231,12 @@ class DocStore:
     def _check(self, st: int, what: str) -> None:
         self.engine._check(st, what)
 
-    def set_incremental(self, on: bool) -> None:
+    def set_incremental(self, on) -> None:
         """Incremental applyRemoteChanges on the resident state (default on); off = every submit
-        re-merges each touched document's whole log.  Results are identical."""
-        self._check(self._L.hm_store_set_incremental(self._h, int(bool(on))), "hm_store_set_incremental")
+        re-merges each touched document's whole log; 2 = also small list documents (no cost
+        policy).  Results are identical."""
+        mode = 2 if on == 2 else int(bool(on))
+        self._check(self._L.hm_store_set_incremental(self._h, mode), "hm_store_set_incremental")
 
     def last_routing(self) -> Dict[str, int]:
         """How the last submit's documents were merged: incremental / re-merged / handed back."""

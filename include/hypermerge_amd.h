@@ -344,6 +344,9 @@ int hm_batch_undo(hm_store *s, uint64_t batch_id);
  * map set/del/link/inc ops, small submits) is advanced in place — history, allDeps, heads and
  * clock appended, only the registers its new ops hit read and rewritten — instead of
  * re-merging its whole log.  Results are identical either way; off = always re-merge.
+ * on = 1: a document with list / text objects whose log fits the small merge kernel (<= 256
+ * ops) re-merges: it is one wave either way, and such a document then keeps no incremental
+ * state to maintain; on = 2: every eligible document takes the incremental path (tests).
  * (A register's survivors may then sit anywhere in its document's op segment; hm_doc_read
  * hands them out packed, as a merge writes them.) */
 int hm_store_set_incremental(hm_store *s, int on);

@@ -222,6 +222,7 @@ def test_incremental_apply_equals_full_remerge(engine, name, n, extra, hi, expec
         docs = [decode_doc(b, i) for i in range(b.n_docs)]
     rng = np.random.default_rng(11)
     A, B = DocStore(engine, a_stride=S), DocStore(engine, a_stride=S)
+    A.set_incremental(2)                                   # (every eligible document, small list ones too)
     B.set_incremental(False)
     ha = [A.open() for _ in docs]
     hb = [B.open() for _ in docs]
@@ -428,6 +429,7 @@ def test_incremental_edits_on_several_lists(engine):
     directory): every call equal to the whole-log re-merge and to the oracle's cold merge."""
     rounds = _lists_rounds()
     A, B = DocStore(engine, a_stride=8), DocStore(engine, a_stride=8)
+    A.set_incremental(2)                                   # (every eligible document, small list ones too)
     B.set_incremental(False)
     ha, hb = A.open(), B.open()
     routed = []
@@ -454,6 +456,7 @@ def test_rowstore_text_rounds_with_declared_registers(engine):
     nch = b.docs["n_changes"].astype(np.int64)
     pos = np.maximum(nch - 10, 0)
     A, B = RowStore(engine, a_stride=b.a_stride), RowStore(engine, a_stride=b.a_stride)
+    A.set_incremental(2)
     B.set_incremental(False)
     ha, hb = A.open_n(n), B.open_n(n)
     for st, h0 in ((A, ha), (B, hb)):
@@ -487,6 +490,7 @@ def test_incremental_text_edits_equal_remerge_and_oracle(engine):
     (lorder / epos), each call equal to the whole-log re-merge and to the oracle's cold merge."""
     rounds = _text_rounds()
     A, B = DocStore(engine, a_stride=8), DocStore(engine, a_stride=8)
+    A.set_incremental(2)                                   # (every eligible document, small list ones too)
     B.set_incremental(False)
     ha, hb = A.open(), B.open()
     routed = []

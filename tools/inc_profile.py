@@ -19,13 +19,14 @@ def main():
     ap.add_argument("--incremental", type=int, default=1)
     ap.add_argument("--tail", type=int, default=4)
     ap.add_argument("--device", type=int, default=0, help="1: new rows already in HBM (submit_device)")
+    ap.add_argument("--config", default="C4")
     a = ap.parse_args()
     import torch
     torch.cuda.init()
     from hypermerge_amd import synth
     from hypermerge_amd.engine import Engine
     from hypermerge_amd.store import RowStore, slice_changes
-    b = synth.generate(synth.config("C4", n_docs=a.docs), threads=16)
+    b = synth.generate(synth.config(a.config, n_docs=a.docs), threads=16)
     eng = Engine(0)
     n = b.n_docs
     nch = b.docs["n_changes"].astype(np.int64)
