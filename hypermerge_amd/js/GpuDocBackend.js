@@ -82,11 +82,19 @@ function rdClock() {
   R.p = p
   return c
 }
-// One docset call's HMP1 results, read document by document: decodeRound(buf, n).head(d) gives
-// the patch shell (clock, deps; diffs null), back clock and round clock; .diffs(d) fills the
-// patch's diffs.  finish() reads every head first and each document's diffs only when its
-// patch is delivered, so a round's diff objects die young instead of all being live at once
-// (and promoted by the collector) across the whole delivery loop.
+// into an existing object (a clock that only grows: every key it had stays)
+function rdClockInto(c) {
+  const w = R.w, strs = R.strs, sb = R.sb
+  let p = R.p
+  for (let k = w[p++]; k > 0; k--) { c[strs[sb + w[p]]] = w[p + 1]; p += 2 }
+  R.p = p
+}
+function skipClock() { R.p += 1 + 2 * R.w[R.p] }
+// One docset call's HMP1 results, read document by document: decodeRound(buf, n).advance(d,
+// state) moves a document's state to the round's end (clocks, deps), .message(d, state) builds
+// its patch (clock, deps, diffs) and the round's clock.  finish() advances every document first
+// and builds each patch only when it is delivered, so a round's patch and diff objects die young
+// instead of all being live at once (and promoted by the collector) across the delivery loop.
 class RoundReader {
   constructor(buf, n) {
     if (buf.byteOffset % 8) buf = Buffer.from(buf)           // a fresh, aligned copy
@@ -115,14 +123,30 @@ class RoundReader {
   enter(d, p) { R.w = this.w; R.nums = this.nums; R.strs = this.strs; R.p = p; R.sb = this.sbase[d]; R.nb = this.nbase[d] }
   leave() { R.w = R.nums = R.strs = null }
 
-  head(d) {
-    if (this.woff[d] === this.woff[d + 1]) return null
+  // pass 1, every document of the call: its state advanced from its head — the opSet clock and
+  // DocBackend.clock updated in place (they only grow), deps a fresh object — so nothing else
+  // is held across the call's deliveries (objects that live through a young-generation
+  // collection are promoted, and the old generation's collections cost the JS thread most)
+  advance(d, state) {
+    if (this.woff[d] === this.woff[d + 1]) return false
     this.enter(d, this.woff[d])
-    const patch = { clock: rdClock(), deps: rdClock(), canUndo: false, canRedo: false, diffs: null }
-    const b = rdClock(), c = rdClock()
+    rdClockInto(state.clock)
+    state.deps = rdClock()
+    rdClockInto(state.backClock)
+    skipClock()
     this.at[d] = R.p
     this.leave()
-    return { patch, b, c }
+    return true
+  }
+
+  // pass 2, just before the document's delivery: its patch and the round's clock
+  message(d, state) {
+    this.enter(d, this.woff[d])
+    const clock = rdClock()
+    skipClock(); skipClock()
+    const c = rdClock()
+    this.leave()
+    return { patch: { clock, deps: state.deps, canUndo: false, canRedo: false, diffs: this.diffs(d) }, c }
   }
 
   diffs(d) {
@@ -212,8 +236,15 @@ function insertDiff(type, obj, index, elemId) {
 // a JSON results buffer (the docset's debug form) read through the same interface
 class JsonRoundReader {
   constructor(j) { this.j = j }
-  head(d) { const p = this.j.p[d]; return p ? { patch: Object.assign({}, p, { diffs: null }), b: this.j.b[d], c: this.j.c[d] } : null }
-  diffs(d) { return this.j.p[d].diffs }
+  advance(d, state) {
+    const p = this.j.p[d]
+    if (!p) return false
+    Object.assign(state.clock, p.clock)
+    state.deps = p.deps
+    Object.assign(state.backClock, this.j.b[d])
+    return true
+  }
+  message(d, state) { return { patch: Object.assign({}, this.j.p[d], { deps: state.deps }), c: this.j.c[d] } }
 }
 
 function decodeRound(buf, n) {
@@ -503,19 +534,14 @@ class GpuEngine {
       for (const c of job.entries) state.log.push(c)
       state.histLen = res[RESULT_U32 * i + 3]
       state.nQueued = res[RESULT_U32 * i + 4]
-      const h = j.head(i)
-      state.clock = h.patch.clock
-      state.deps = h.patch.deps
-      state.backClock = h.b
-      ok.push(i, { patch: h.patch, roundClock: h.c, backClock: h.b, minCmp: null })
+      if (j.advance(i, state)) ok.push(i)
     })
-    // every state of the call is advanced before the first delivery; each patch's diffs are
-    // read just before it is delivered
-    for (let k = 0; k < ok.length; k += 2) {
-      const i = ok[k], payload = ok[k + 1]
-      payload.patch.diffs = j.diffs(i)
-      ok[k + 1] = null
-      items[i].job.done(payload)
+    // every state of the call is advanced before the first delivery; each patch is built just
+    // before it is delivered
+    for (const i of ok) {
+      const { state, job } = items[i]
+      const m = j.message(i, state)
+      job.done({ patch: m.patch, roundClock: m.c, backClock: state.backClock, minCmp: null })
     }
   }
 
