@@ -557,6 +557,21 @@ static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handl
         SCHK(s, hipMemsetAsync(A.defer, 0, 4, st));
         SCHK(s, hm_launch_alloc(A, st));
         StoreArenas ar = {s->changes, s->deps, s->ops, s->min_clock, s->stored};
+        if (T.on) {
+            // what the append has to move: documents whose segments moved, re-ranked ones, old rows
+            std::vector<AppendDesc> dd(n);
+            SCHK(s, hipMemcpyAsync(dd.data(), s->descs.p, (size_t)n * sizeof(AppendDesc), hipMemcpyDeviceToHost, st));
+            SCHK(s, hipStreamSynchronize(st));
+            size_t mv = 0, rmp = 0, inc = 0, old_o = 0, new_o = 0;
+            for (const AppendDesc &D : dd) {
+                const bool m = D.src_c != D.dst_c || D.src_d != D.dst_d || D.src_o != D.dst_o;
+                mv += m; rmp += D.remap_row != 0xFFFFFFFFu; inc += D.inc != 0; new_o += D.n_new_o;
+                if (m) old_o += D.n_old_o;
+            }
+            fprintf(stderr, "[hm_store] append: %zu docs, %zu moved (%zu old op rows), %zu re-ranked, %zu incremental, %zu new op rows\n",
+                    (size_t)n, mv, old_o, rmp, inc, new_o);
+            T.mark("(append census)");
+        }
         SCHK(s, hm_launch_append(s->descs.p, n, ar, ar, A.changes, t_dp, t_op, A.remap, S, st, s->alist.p, &s->st->n_app));
         T.mark("alloc+append");
         uint32_t *bail = (uint32_t *)(sp + L.o_bail);

@@ -1,6 +1,6 @@
 // store_kernels.hip — device side of the resident document store (store.cpp).
 //
-//  append_kernel        one wave per document of a submit: moves the document's
+//  append_kernel<G>     G lanes per document of a submit: moves the document's
 //                       log segments when they outgrow their capacity (or on arena
 //                       compaction), applies an actor-rank remap to the old rows and to
 //                       the rank-indexed per-document rows (minimumClock, stored clock),
@@ -25,78 +25,106 @@ namespace hms {
 
 #define SWG 256
 
+// G lanes per document, 256 / G documents per workgroup.  A submit's appends are a few rows per
+// document (C5: 1-2 changes, ~5 ops), so G = 16 keeps four documents' load -> store chains in
+// flight per wave instead of one (one wave per document ran 100k documents as ~12 dependent
+// chains per wave: 210 us); a compaction or rollback (old rows only, every document moved) takes
+// G = 64.  Within a document every copy reads only rows no earlier store of it writes (a moved
+// segment is a fresh bump allocation; new rows come from the staging tables), so the pointers
+// are restrict-qualified and each loop's loads issue ahead of its stores.
+template <int G>
 __global__ __launch_bounds__(SWG) void append_kernel(const AppendDesc *descs, uint32_t n_desc, StoreArenas src,
                                                      StoreArenas dst, const hm_change_row *st_changes,
                                                      const hm_dep_row *st_deps, const hm_op_row *st_ops,
                                                      const uint8_t *remap, uint32_t S, const uint32_t *list,
                                                      const uint32_t *count) {
-    // one wave per document (a submit's appends are a few rows each; a 256-lane group per
-    // document would idle most of its lanes), four documents per workgroup; with a list, only
-    // the listed batch rows (alloc_kernel lists the documents with work here: a round of
-    // incremental documents whose segments did not move has none)
-    const uint32_t t = threadIdx.x & 63, W = 64;
+    // with a list, only the listed batch rows (alloc_kernel lists the documents with work here: a
+    // round of incremental documents whose segments did not move has none)
+    constexpr uint32_t PER = SWG / G;
+    const uint32_t t = threadIdx.x & (G - 1);
     const uint32_t nd = list ? *count : n_desc;
-    for (uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 6); k < nd; k += gridDim.x * 4) {
+    for (uint32_t k = blockIdx.x * PER + threadIdx.x / G; k < nd; k += gridDim.x * PER) {
         const uint32_t di = list ? list[k] : k;
         const AppendDesc D = descs[di];
         const bool moved = D.src_c != D.dst_c || D.src_d != D.dst_d || D.src_o != D.dst_o || src.changes != dst.changes;
         if (D.inc && !moved) continue;                  // the incremental kernel appends its rows itself
         const bool rm = D.remap_row != 0xFFFFFFFFu;
         const uint8_t *mp = rm ? remap + (size_t)D.remap_row * S : nullptr;
-        // old rows: moved (rebased) and/or re-ranked
+        // old rows: moved (rebased) and/or re-ranked (in place when not moved: row i -> row i)
         if (moved || rm) {
             const int64_t dd = (int64_t)D.dst_d - (int64_t)D.src_d, dop = (int64_t)D.dst_o - (int64_t)D.src_o;
-            for (uint32_t i = t; i < D.n_old_c; i += W) {
+            for (uint32_t i = t; i < D.n_old_c; i += G) {
                 hm_change_row c = src.changes[D.src_c + i];
                 c.dep_off = (uint32_t)((int64_t)c.dep_off + dd);
                 c.op_first = (uint32_t)((int64_t)c.op_first + dop);
                 if (rm && c.actor < S) c.actor = mp[c.actor];
                 dst.changes[D.dst_c + i] = c;
             }
-            for (uint32_t i = t; i < D.n_old_d; i += W) {
+            for (uint32_t i = t; i < D.n_old_d; i += G) {
                 hm_dep_row r = src.deps[D.src_d + i];
                 if (rm && r.actor < S) r.actor = mp[r.actor];
                 dst.deps[D.dst_d + i] = r;
             }
         }
         if (moved) {
-            // 32-byte op rows as two 16-byte words per thread
-            const uint4 *so = reinterpret_cast<const uint4 *>(src.ops + D.src_o);
-            uint4 *dop = reinterpret_cast<uint4 *>(dst.ops + D.dst_o);
-            for (uint32_t i = t; i < 2 * D.n_old_o; i += W) dop[i] = so[i];
+            // 32-byte op rows as two 16-byte words per lane, four in flight
+            const uint4 *__restrict__ so = reinterpret_cast<const uint4 *>(src.ops + D.src_o);
+            uint4 *__restrict__ dop = reinterpret_cast<uint4 *>(dst.ops + D.dst_o);
+            const uint32_t nw = 2 * D.n_old_o;
+            uint32_t i = t;
+            for (; i + 3 * G < nw; i += 4 * G) {
+                const uint4 x0 = so[i], x1 = so[i + G], x2 = so[i + 2 * G], x3 = so[i + 3 * G];
+                dop[i] = x0; dop[i + G] = x1; dop[i + 2 * G] = x2; dop[i + 3 * G] = x3;
+            }
+            for (; i < nw; i += G) dop[i] = so[i];
         }
-        // new rows: batch-local offsets -> arena offsets
+        // new rows: batch-local offsets -> arena offsets; every load of the three tables before
+        // the stores (the common round: one pass of each loop)
         const uint32_t c_at = D.dst_c + D.n_old_c, d_at = D.dst_d + D.n_old_d, o_at = D.dst_o + D.n_old_o;
-        for (uint32_t i = t; i < D.n_new_c; i += W) {
-            hm_change_row c = st_changes[D.new_c + i];
-            c.dep_off = d_at + (c.dep_off - D.new_d);
-            c.op_first = o_at + (c.op_first - D.new_o);
-            dst.changes[c_at + i] = c;
+        const hm_change_row *__restrict__ nc = st_changes + D.new_c;
+        const hm_dep_row *__restrict__ ndp = st_deps + D.new_d;
+        const uint4 *__restrict__ no = reinterpret_cast<const uint4 *>(st_ops + D.new_o);
+        hm_change_row *__restrict__ oc = dst.changes + c_at;
+        hm_dep_row *__restrict__ od = dst.deps + d_at;
+        uint4 *__restrict__ oo = reinterpret_cast<uint4 *>(dst.ops + o_at);
+        const uint32_t nwo = 2 * D.n_new_o;
+        const uint32_t rounds = max(max(D.n_new_c, D.n_new_d), nwo);
+        for (uint32_t i = t; i < rounds; i += G) {
+            hm_change_row c = {};
+            hm_dep_row r = {};
+            uint4 o = {};
+            if (i < D.n_new_c) c = nc[i];
+            if (i < D.n_new_d) r = ndp[i];
+            if (i < nwo) o = no[i];
+            if (i < D.n_new_c) {
+                c.dep_off = d_at + (c.dep_off - D.new_d);
+                c.op_first = o_at + (c.op_first - D.new_o);
+                oc[i] = c;
+            }
+            if (i < D.n_new_d) od[i] = r;
+            if (i < nwo) oo[i] = o;
         }
-        for (uint32_t i = t; i < D.n_new_d; i += W) dst.deps[d_at + i] = st_deps[D.new_d + i];
-        {
-            const uint4 *so = reinterpret_cast<const uint4 *>(st_ops + D.new_o);
-            uint4 *dop = reinterpret_cast<uint4 *>(dst.ops + o_at);
-            for (uint32_t i = t; i < 2 * D.n_new_o; i += W) dop[i] = so[i];
-        }
-        // rank-indexed per-document rows follow the remap: lane t gathers the new ranks t + 64k
-        // (k < 4: S <= HM_MAX_STRIDE) from every old rank, all loads before any store (one wave)
+        // rank-indexed per-document rows follow the remap: lane t gathers the new ranks t + G j
+        // (j < 256 / G: S <= HM_MAX_STRIDE) from every old rank, all loads before any store
         if (rm) {
+            constexpr uint32_t NJ = HM_MAX_STRIDE / G;
             uint32_t *rows[2] = {dst.min_clock + (size_t)D.handle * S, dst.stored_clock + (size_t)D.handle * S};
             for (int w = 0; w < 2; w++) {
-                uint32_t v0 = 0, v1 = 0, v2 = 0, v3 = 0;
+                uint32_t v[NJ];
+#pragma unroll
+                for (uint32_t j = 0; j < NJ; j++) v[j] = 0;
                 for (uint32_t a = 0; a < S; a++) {
                     const uint32_t na = mp[a];
-                    if (na >= S || (na & 63) != t) continue;
+                    if (na >= S || (na & (G - 1)) != t) continue;
                     const uint32_t x = rows[w][a];
-                    const uint32_t k = na >> 6;
-                    v0 = k == 0 ? x : v0; v1 = k == 1 ? x : v1; v2 = k == 2 ? x : v2; v3 = k == 3 ? x : v3;
+                    const uint32_t jj = na / G;
+#pragma unroll
+                    for (uint32_t j = 0; j < NJ; j++) v[j] = jj == j ? x : v[j];
                 }
                 __builtin_amdgcn_wave_barrier();
-                if (t < S) rows[w][t] = v0;
-                if (t + 64 < S) rows[w][t + 64] = v1;
-                if (t + 128 < S) rows[w][t + 128] = v2;
-                if (t + 192 < S) rows[w][t + 192] = v3;
+#pragma unroll
+                for (uint32_t j = 0; j < NJ; j++)
+                    if (t + G * j < S) rows[w][t + G * j] = v[j];
             }
         }
     }
@@ -203,7 +231,7 @@ __device__ __forceinline__ uint32_t pow2c(uint32_t x) {
 // the submit's reductions go through LDS to one atomic per workgroup and value: same-address
 // atomics from every wave of a million-document submit queue at one L2 channel (~10 ns each:
 // ~1.2 ms of a 1M-document incremental plan, the same in doc_rows_kernel)
-#define PLAN_WG 1024
+#define PLAN_WG 256
 __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
     __shared__ unsigned long long s_need[4][PLAN_WG / 64];
     __shared__ uint32_t s_inc[PLAN_WG / 64];
@@ -583,10 +611,17 @@ hipError_t hm_launch_append(const AppendDesc *descs, uint32_t n_desc, const Stor
                             const hm_change_row *st_changes, const hm_dep_row *st_deps, const hm_op_row *st_ops,
                             const uint8_t *remap, uint32_t S, hipStream_t s, const uint32_t *list, const uint32_t *count) {
     if (!n_desc) return hipSuccess;
-    const uint32_t cap = list ? 2048u : 65535u;                 // (a listed launch: the count is on the device)
-    const uint32_t grid = (n_desc + 3) / 4 < cap ? (n_desc + 3) / 4 : cap;
-    hipLaunchKernelGGL(hms::append_kernel, dim3(grid), dim3(SWG), 0, s, descs, n_desc, src, dst, st_changes, st_deps,
-                       st_ops, remap, S, list, count);
+    // new rows: 16 lanes per document; old rows only (compaction, rollback): a wave each
+    const bool small = st_changes != nullptr;
+    const uint32_t per = small ? SWG / 16 : SWG / 64;
+    const uint32_t cap = list ? 4096u : 65535u;                 // (a listed launch: the count is on the device)
+    const uint32_t grid = (n_desc + per - 1) / per < cap ? (n_desc + per - 1) / per : cap;
+    if (small)
+        hipLaunchKernelGGL(hms::append_kernel<16>, dim3(grid), dim3(SWG), 0, s, descs, n_desc, src, dst, st_changes,
+                           st_deps, st_ops, remap, S, list, count);
+    else
+        hipLaunchKernelGGL(hms::append_kernel<64>, dim3(grid), dim3(SWG), 0, s, descs, n_desc, src, dst, st_changes,
+                           st_deps, st_ops, remap, S, list, count);
     return hipGetLastError();
 }
 
