@@ -53,6 +53,12 @@ uint32_t pow2ceil(uint32_t x) {
     while (c < x) c <<= 1;
     return c;
 }
+// a compacted segment: its rows and a quarter as many again, to a power of two (the plan grows
+// segments the same way, store_kernels.hip grow_rows)
+uint32_t seg_cap(uint32_t n) {
+    const uint64_t x = (uint64_t)n + (n >> 2);
+    return pow2ceil((uint32_t)std::max<uint64_t>(std::min<uint64_t>(x, 0x80000000ull), 16));
+}
 
 }  // namespace
 
@@ -327,8 +333,7 @@ int compact(hm_store *s, size_t extra_c, size_t extra_d, size_t extra_o, size_t 
     }
     size_t live_c = extra_c, live_d = extra_d, live_o = extra_o, live_r = extra_r;
     for (auto &m : old) {
-        live_c += pow2ceil(std::max<uint32_t>(m.n_c, 16)); live_d += pow2ceil(std::max<uint32_t>(m.n_d, 16));
-        live_o += pow2ceil(std::max<uint32_t>(m.n_o, 16)); live_r += pow2ceil(std::max<uint32_t>(m.n_r, 16));
+        live_c += seg_cap(m.n_c); live_d += seg_cap(m.n_d); live_o += seg_cap(m.n_o); live_r += seg_cap(m.n_r);
     }
     const size_t nc = std::max<size_t>(2 * live_c, 1 << 16), nd = std::max<size_t>(2 * live_d, 1 << 16);
     const size_t no = std::max<size_t>(2 * live_o, 1 << 16), nr = std::max<size_t>(2 * live_r, 1 << 16);
@@ -347,7 +352,7 @@ int compact(hm_store *s, size_t extra_c, size_t extra_d, size_t extra_o, size_t 
     std::vector<uint32_t> all(n);
     uint64_t uc = 0, ud = 0, uo = 0, ur = 0;
     auto seg = [](uint64_t &used, uint32_t need, uint32_t &off, uint32_t &cap) {
-        cap = pow2ceil(std::max<uint32_t>(need, 16));
+        cap = seg_cap(need);
         off = (uint32_t)used;
         used += cap;
     };

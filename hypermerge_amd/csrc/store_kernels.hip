@@ -223,6 +223,7 @@ __global__ void read_regs_kernel(uint32_t n, const uint32_t *abs_reg, const uint
 // deps / ops, the actor remap a permutation into the new ranks), the segments the append
 // outgrows and the route (incremental or re-merge).  Nothing in the store changes here: a
 // failed check fails the submit with the store as it was.
+__device__ __forceinline__ uint32_t grow_rows(uint32_t x) { return x > 0xC0000000u ? x : x + (x >> 2); }
 __device__ __forceinline__ uint32_t pow2c(uint32_t x) {
     x = x < 16u ? 16u : x;
     return x <= 1u ? 1u : 1u << (32 - __builtin_clz(x - 1));
@@ -280,10 +281,13 @@ __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
     if (wave_ok) {
     PlanRow p;
     p.n_c = m.n_c; p.n_d = m.n_d; p.n_o = m.n_o; p.n_r = m.n_r; p.n_objs = m.n_objs; p.n_actors = m.n_actors; p.flags = m.flags;
-    p.g[0] = live && m.n_c + r.n_changes > m.c_cap ? pow2c(m.n_c + r.n_changes) : 0u;
-    p.g[1] = live && m.n_d + r.n_deps > m.d_cap ? pow2c(m.n_d + r.n_deps) : 0u;
-    p.g[2] = live && m.n_o + r.n_ops > m.o_cap ? pow2c(m.n_o + r.n_ops) : 0u;
-    p.g[3] = live && r.n_regs > m.r_cap ? pow2c(r.n_regs) : 0u;
+    // a segment that outgrows its capacity moves to one with a quarter of its rows again as headroom
+    // (a tight power of two moved a quarter to a half of C5's documents every round: their whole
+    // logs copied by append_kernel)
+    p.g[0] = live && m.n_c + r.n_changes > m.c_cap ? pow2c(grow_rows(m.n_c + r.n_changes)) : 0u;
+    p.g[1] = live && m.n_d + r.n_deps > m.d_cap ? pow2c(grow_rows(m.n_d + r.n_deps)) : 0u;
+    p.g[2] = live && m.n_o + r.n_ops > m.o_cap ? pow2c(grow_rows(m.n_o + r.n_ops)) : 0u;
+    p.g[3] = live && r.n_regs > m.r_cap ? pow2c(grow_rows(r.n_regs)) : 0u;
     for (int k = 0; k < 4; k++) {
         unsigned long long g = p.g[k];
         for (int o = 32; o > 0; o >>= 1) g += (unsigned long long)__shfl_xor((long long)g, o);
@@ -362,50 +366,67 @@ __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
 }
 
 // alloc_kernel: segments for the rows that outgrow theirs (bump allocation at the arenas'
-// ends), the append descriptor, the document's new totals, and the re-merge list
-__global__ void alloc_kernel(PlanArgs a) {
+// ends), the append descriptor, the document's new totals, and the three work lists (re-merge,
+// wave pass, append).  The list slots are taken one atomic per workgroup and list: the same-
+// address atomics of every wave of a submit serialize at one L2 channel (100k documents: ~1.5k
+// waves x 3 lists)
+#define ALLOC_WG 256
+__global__ __launch_bounds__(ALLOC_WG) void alloc_kernel(PlanArgs a) {
+    __shared__ uint32_t s_cnt[3][ALLOC_WG / 64];
+    __shared__ uint32_t s_base[3];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n) return;
-    const uint32_t h = a.handles[i];
-    const hm_doc_row r = a.docs[i];
-    const PlanRow p = a.plan[i];
-    DevDoc m = a.dm[h];
-    AppendDesc D;
-    D.handle = h;
-    D.src_c = m.c_off; D.n_old_c = m.n_c; D.new_c = r.change_off; D.n_new_c = r.n_changes;
-    D.src_d = m.d_off; D.n_old_d = m.n_d; D.new_d = r.dep_off; D.n_new_d = r.n_deps;
-    D.src_o = m.o_off; D.n_old_o = m.n_o; D.new_o = r.op_off; D.n_new_o = r.n_ops;
-    D.src_r = m.r_off; D.n_old_r = m.n_r;
-    if (p.g[0]) { m.c_off = (uint32_t)atomicAdd(&a.st->bump[0], (unsigned long long)p.g[0]); m.c_cap = p.g[0]; }
-    if (p.g[1]) { m.d_off = (uint32_t)atomicAdd(&a.st->bump[1], (unsigned long long)p.g[1]); m.d_cap = p.g[1]; }
-    if (p.g[2]) { m.o_off = (uint32_t)atomicAdd(&a.st->bump[2], (unsigned long long)p.g[2]); m.o_cap = p.g[2]; }
-    if (p.g[3]) { m.r_off = (uint32_t)atomicAdd(&a.st->bump[3], (unsigned long long)p.g[3]); m.r_cap = p.g[3]; }
-    D.dst_c = m.c_off; D.dst_d = m.d_off; D.dst_o = m.o_off; D.dst_r = m.r_off;
-    D.remap_row = p.remapped ? i : 0xFFFFFFFFu;
-    m.n_c += r.n_changes; m.n_d += r.n_deps; m.n_o += r.n_ops;
-    m.n_r = r.n_regs; m.n_objs = r.n_objs; m.n_actors = r.n_actors; m.flags |= r.flags;
-    D.n_r = m.n_r; D.n_actors = m.n_actors; D.n_objs = m.n_objs; D.o_cap = m.o_cap;
-    D.inc = (uint16_t)p.inc;
-    a.descs[i] = D;
-    a.dm[h] = m;
-    if (!p.inc) a.list[atomicAdd(&a.st->n_cold, 1u)] = h;
-    // documents with list ops go to the one-document-per-wave pass directly (one atomic per wave)
-    if (a.defer) {
-        const unsigned long long wm = __ballot(p.inc == 2u);
-        const uint32_t wl = threadIdx.x & 63, wlead = wm ? (uint32_t)__builtin_ctzll(wm) : 0u;
-        uint32_t wb = 0;
-        if (wm && wl == wlead) wb = atomicAdd(&a.defer[0], (uint32_t)__popcll(wm));
-        wb = (uint32_t)__shfl((int)wb, (int)wlead);
-        if (p.inc == 2u) a.defer[1 + wb + (uint32_t)__popcll(wm & ((1ull << wl) - 1))] = i;
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const bool live = i < a.n;
+    bool cold = false, wavep = false, app = false;
+    uint32_t h = 0;
+    if (live) {
+        h = a.handles[i];
+        const hm_doc_row r = a.docs[i];
+        const PlanRow p = a.plan[i];
+        DevDoc m = a.dm[h];
+        AppendDesc D;
+        D.handle = h;
+        D.src_c = m.c_off; D.n_old_c = m.n_c; D.new_c = r.change_off; D.n_new_c = r.n_changes;
+        D.src_d = m.d_off; D.n_old_d = m.n_d; D.new_d = r.dep_off; D.n_new_d = r.n_deps;
+        D.src_o = m.o_off; D.n_old_o = m.n_o; D.new_o = r.op_off; D.n_new_o = r.n_ops;
+        D.src_r = m.r_off; D.n_old_r = m.n_r;
+        if (p.g[0]) { m.c_off = (uint32_t)atomicAdd(&a.st->bump[0], (unsigned long long)p.g[0]); m.c_cap = p.g[0]; }
+        if (p.g[1]) { m.d_off = (uint32_t)atomicAdd(&a.st->bump[1], (unsigned long long)p.g[1]); m.d_cap = p.g[1]; }
+        if (p.g[2]) { m.o_off = (uint32_t)atomicAdd(&a.st->bump[2], (unsigned long long)p.g[2]); m.o_cap = p.g[2]; }
+        if (p.g[3]) { m.r_off = (uint32_t)atomicAdd(&a.st->bump[3], (unsigned long long)p.g[3]); m.r_cap = p.g[3]; }
+        D.dst_c = m.c_off; D.dst_d = m.d_off; D.dst_o = m.o_off; D.dst_r = m.r_off;
+        D.remap_row = p.remapped ? i : 0xFFFFFFFFu;
+        m.n_c += r.n_changes; m.n_d += r.n_deps; m.n_o += r.n_ops;
+        m.n_r = r.n_regs; m.n_objs = r.n_objs; m.n_actors = r.n_actors; m.flags |= r.flags;
+        D.n_r = m.n_r; D.n_actors = m.n_actors; D.n_objs = m.n_objs; D.o_cap = m.o_cap;
+        D.inc = (uint16_t)p.inc;
+        a.descs[i] = D;
+        a.dm[h] = m;
+        cold = !p.inc;                                   // the re-merge list (handles)
+        wavep = a.defer && p.inc == 2u;                  // documents with list ops: the one-document-per-wave pass
+        app = !p.inc || p.g[0] || p.g[1] || p.g[2] || p.remapped;   // the rows append_kernel must visit
     }
-    // the rows append_kernel must visit, one counter atomic per wave
-    const bool app = !p.inc || p.g[0] || p.g[1] || p.g[2] || p.remapped;
-    const unsigned long long am = __ballot(app);
-    const uint32_t ln = threadIdx.x & 63, lead = am ? (uint32_t)__builtin_ctzll(am) : 0u;
-    uint32_t base = 0;
-    if (am && ln == lead) base = atomicAdd(&a.st->n_app, (uint32_t)__popcll(am));
-    base = (uint32_t)__shfl((int)base, (int)lead);
-    if (app) a.alist[base + (uint32_t)__popcll(am & ((1ull << ln) - 1))] = i;
+    const unsigned long long mk[3] = {__ballot(cold), __ballot(wavep), __ballot(app)};
+    if (ln < 3) s_cnt[ln][wv] = (uint32_t)__popcll(ln == 0 ? mk[0] : ln == 1 ? mk[1] : mk[2]);
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const uint32_t k = threadIdx.x;
+        uint32_t t = 0;
+        for (uint32_t w = 0; w < ALLOC_WG / 64; w++) t += s_cnt[k][w];
+        uint32_t *ctr = k == 0 ? &a.st->n_cold : k == 1 ? a.defer : &a.st->n_app;
+        s_base[k] = t ? atomicAdd(ctr, t) : 0u;
+    }
+    __syncthreads();
+    const unsigned long long lt = (1ull << ln) - 1;
+    uint32_t off[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        off[k] = s_base[k] + (uint32_t)__popcll(mk[k] & lt);
+        for (uint32_t w = 0; w < wv; w++) off[k] += s_cnt[k][w];
+    }
+    if (cold) a.list[off[0]] = h;
+    if (wavep) a.defer[1 + off[1]] = i;
+    if (app) a.alist[off[2]] = i;
 }
 
 __global__ __launch_bounds__(PLAN_WG) void doc_rows_kernel(const uint32_t *list, uint32_t n, const DevDoc *dm, hm_doc_row *rows,
@@ -556,7 +577,7 @@ hipError_t hm_launch_plan(const PlanArgs &a, hipStream_t s) {
 }
 hipError_t hm_launch_alloc(const PlanArgs &a, hipStream_t s) {
     if (!a.n) return hipSuccess;
-    hipLaunchKernelGGL(hms::alloc_kernel, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(hms::alloc_kernel, dim3((a.n + ALLOC_WG - 1) / ALLOC_WG), dim3(ALLOC_WG), 0, s, a);
     return hipGetLastError();
 }
 hipError_t hm_launch_doc_rows(const uint32_t *list, uint32_t n, const DevDoc *dm, hm_doc_row *rows, PlanStats *st,

@@ -2,7 +2,7 @@
 # Round-4 measurement at HEAD: the default bench line (all legs), rocprofv3 kernel stats + PMC of the
 # C4, C3 and C5 steps.  Outputs under gpurun_out/r04/final.
 set -o pipefail
-O=gpurun_out/r04/final
+O=gpurun_out/r04/${1:-final}
 mkdir -p $O
 timeout -k 10 700 python bench.py > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
 grep '^{' $O/bench.log | tail -1 > $O/bench_line.json
