@@ -451,10 +451,13 @@ def _incremental(eng, batch, args, tail=4, oracle_docs=0):
     keep = BatchResult(pinned((n,), DOC_RESULT_DT), pinned((n, S), np.uint32), pinned((n, S), np.uint32),
                        pinned((n, S), np.uint32))
     rounds, same, routing_ok = [], True, True
-    for sub, sel, cnt, t in rounds_in:
+    for ri, (sub, sel, cnt, t) in enumerate(rounds_in):
         r = {"docs": int(len(sel)), "changes": int(len(sub.changes)), "ops": int(len(sub.ops))}
         nb = len(sel) * (32 + 12 * S)
-        for st, tag, o in zip(stores[:2], ("incremental", "remerge"), out):
+        legs = list(zip(stores[:2], ("incremental", "remerge"), out))
+        # the two legs take turns going first (the first submit after the host's work between
+        # rounds meets an idle, down-clocked GPU)
+        for st, tag, o in (legs if ri % 2 == 0 else legs[::-1]):
             torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
             st.submit_device(len(sel), cnt, *t)

@@ -305,8 +305,12 @@ int launch_list_merge(hm_store *s, const uint32_t *dev_list, uint32_t n) {
     o.hist = s->hist; o.all_deps = s->all_deps; o.regs = s->regs; o.surv = s->surv;
     const hm_extents ext = {(uint32_t)s->cap_c, (uint32_t)s->cap_d, (uint32_t)s->cap_o, (uint32_t)s->cap_r};
     // the incremental path keeps list documents' element order: positions written by the merge
-    if (s->incremental && (P.flags & HM_DOC_HAS_LISTS)) SCHK(s, hm_launch_epos_clear(dev_list, n, s->dm, s->epos, st));
-    rc = hm_engine_launch_merge(s->e, &b, &o, dev_list, &ext, s->incremental ? s->epos : nullptr);
+    // (mode 1: when every listed document holds <= HM_INC_SMALL_LIST_OPS ops, none with lists keeps
+    // incremental state — inc_meta skips them — so no positions are needed)
+    const bool positions = s->incremental && (P.flags & HM_DOC_HAS_LISTS) &&
+                           !(s->inc_mode == 1 && P.max_o <= HM_INC_SMALL_LIST_OPS);
+    if (positions) SCHK(s, hm_launch_epos_clear(dev_list, n, s->dm, s->epos, st));
+    rc = hm_engine_launch_merge(s->e, &b, &o, dev_list, &ext, positions ? s->epos : nullptr);
     // the incremental path's survivor metadata of the re-merged documents (packed survivors)
     if (rc == HM_OK && s->incremental) {
         MetaArgs M;
