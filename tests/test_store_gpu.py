@@ -132,6 +132,34 @@ def test_arena_compaction_keeps_state(engine):
         assert canonical_json(bb, g, 0) == canonical_json(cold, co, i)
 
 
+@pytest.mark.parametrize("mode", [1, 2])
+def test_one_change_per_call_growth(engine, mode):
+    """Text documents fed one change per call: their log segments outgrow their capacity again
+    and again (a move keeps a quarter of headroom), and under mode 1 they cross the small-list
+    bound (256 ops) mid-way — re-merged without element positions before it, incremental on the
+    resident list order after it; every few calls and at the end the state equals the oracle's."""
+    b = synth.generate(synth.config("C3", n_docs=6, changes_per_actor=320))   # ~40 changes, ~600 ops
+    docs = [decode_doc(b, i) for i in range(b.n_docs)]
+    store = DocStore(engine, a_stride=8)
+    store.set_incremental(mode)
+    hs = [store.open() for _ in docs]
+    inc = 0
+    for k in range(max(len(c) for c in docs)):
+        items = [(h, docs[i][k:k + 1]) for i, h in enumerate(hs) if k < len(docs[i])]
+        r = store.apply(items)
+        assert (r.docs["status"] == 0).all(), (k, r.docs["status"])
+        inc += store.last_routing()["incremental"]
+        if k % 16 == 15:
+            for h in hs[::2]:
+                assert_doc_matches_oracle(store, h)
+    assert inc > 0                                   # (past 256 ops the rounds go incremental)
+    cold = encode(docs, 8)
+    co = O.merge(cold)
+    for i, h in enumerate(hs):
+        bb, g = assert_doc_matches_oracle(store, h)
+        assert canonical_json(bb, g, 0) == canonical_json(cold, co, i), i
+
+
 def test_min_clock_and_clock_store(engine):
     """minimumClock comparison (DocBackend.testMinimumClockSatisfied) and the batched
     ClockStore.update(self, doc, doc.clock) flags against src/Clock.ts semantics."""
