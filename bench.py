@@ -44,9 +44,60 @@ def _dist():
     return ws, rank, local
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def rank_envs(n: int, base: dict, port: int) -> list:
+    """The environment of each of the n ranks of a single-node launch (what torch.distributed.run
+    sets: RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE / MASTER_ADDR / MASTER_PORT)."""
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        envs.append(e)
+    return envs
+
+
+def launch_ranks(n: int, argv: list, visible: int, popen=None, port: int | None = None) -> int:
+    """`bench.py --gpus N` without a launcher: start N child processes of this script, one per GPU
+    of the node, with the ranks' environment; rank 0 prints the JSON line.  Runs before anything
+    touches the GPU (the caller counts devices only).  Returns the exit code: non-zero when the
+    node has fewer than N visible devices (nothing started) or when any rank fails (the others are
+    then terminated)."""
+    import subprocess
+    if n > visible:
+        print(f"bench.py: --gpus {n} needs {n} visible GPUs, this node has {visible}", file=sys.stderr, flush=True)
+        return 2
+    popen = popen or subprocess.Popen
+    envs = rank_envs(n, os.environ, port or _free_port())
+    procs = [popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=e) for e in envs]
+    rc = 0
+    live = list(range(n))
+    while live:
+        for i in list(live):
+            code = procs[i].poll()
+            if code is None:
+                continue
+            live.remove(i)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"bench.py: rank {i} exited with {code}; stopping the other ranks", file=sys.stderr, flush=True)
+                for j in live:
+                    procs[j].terminate()
+        if live:
+            time.sleep(0.05)
+    return rc
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs of this node (ranks); without WORLD_SIZE in the environment, N > 1 starts N ranks")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--docs", type=int, default=1_000_000, help="documents per GPU")
@@ -73,9 +124,20 @@ def main() -> int:
                          "concatenates, 2 shuffled)")
     args = ap.parse_args()
 
-    ws, rank, local = _dist()
     import torch
     import torch.distributed as dist
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        # no launcher: this process starts the ranks and touches no GPU itself (counting devices
+        # does not initialise one on this image)
+        return launch_ranks(args.gpus, sys.argv[1:], torch.cuda.device_count())
+    ws, rank, local = _dist()
+    if args.gpus is not None and args.gpus != ws:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr, flush=True)
+        return 2
+    if ws > torch.cuda.device_count():
+        print(f"bench.py: WORLD_SIZE={ws} needs {ws} visible GPUs, this node has {torch.cuda.device_count()}",
+              file=sys.stderr, flush=True)
+        return 2
     if ws > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -289,6 +351,11 @@ def main() -> int:
             "gen_s": round(gen_s, 2), "event_ms_per_step": ev_ms / args.steps,
             "clock_exchange": xchg,
         }
+        if ws > 1:
+            line["ranks_note"] = (f"{ws} ranks, one per GPU, each merging its own {nd}-document shard (FNV-1a64(docId) % "
+                                  f"{ws}); value = changes of all ranks / max-over-ranks time. cpu_baseline, the side legs "
+                                  "and roofline.traffic (PMC passes) are measured at N=1 only; roofline is rank 0's kernel")
+
         print(json.dumps(line), flush=True)
     if ws > 1:
         dist.destroy_process_group()

@@ -1179,6 +1179,7 @@ struct hm_docset {
     std::atomic<uint32_t> n_docs{0};
     std::mutex open_mu;
     std::atomic<bool> busy{false};
+    bool broken = false;                                     // a failed call could not be undone on a store
     uint64_t stat[8] = {0, 0, 0, 0, 0, 0, 0, 0};           // rounds, docs, restrides, hit-register patches, full patches,
                                                              // per-op patches, replay mismatches, replay checks skipped
     DocSt &doc(uint32_t i) { return chunks[i / CHUNK][i % CHUNK]; }
@@ -1391,19 +1392,34 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
     // the call rolls back on the host
     auto fail_call = [&](int why) {
         for (auto &v : rel) v.clear();                       // (every fresh handle is listed below)
+        // a store whose batch cannot be waited for or undone keeps rows the host no longer
+        // describes: the docset refuses every later call rather than diverge silently
+        bool lost = false;
         for (uint32_t c = 0; c < N_CLASS; c++) {
             if (co[c].sub) {
                 std::vector<hm_doc_result> tmp(by_cls[c].size());
                 if (hm_batch_wait(ds->stores[c], co[c].id, tmp.data(), nullptr, nullptr, nullptr) == HM_OK) co[c].done = true;
+                else lost = true;                              // submitted, neither waited for nor undoable
                 co[c].sub = false;
             }
-            if (co[c].done) { (void)hm_batch_undo(ds->stores[c], co[c].id); co[c].done = false; }
+            if (co[c].done) {
+                if (hm_batch_undo(ds->stores[c], co[c].id) != HM_OK) lost = true;
+                co[c].done = false;
+            }
         }
         for (uint32_t i = 0; i < n; i++) {
-            if (R[i].status == HM_OK) rollback(ds->doc(R[i].doc), R[i]);
-            if (R[i].fresh) rel[R[i].cls].push_back(R[i].handle);
+            Round &x = R[i];
+            DocSt &d = ds->doc(x.doc);
+            if (x.status == HM_OK) rollback(d, x);
+            if (!x.fresh) continue;
+            // a new document whose own merge failed was given its fresh handle above (an empty
+            // document in its store); the handle goes back to the free list, so the document
+            // must not keep it
+            if (x.placed && d.cls == x.cls && d.handle == x.handle) { d.cls = NO_CLASS; d.handle = 0; }
+            rel[x.cls].push_back(x.handle);
         }
         release();
+        if (lost) ds->broken = true;
         return why;
     };
     if (rc) return fail_call(rc);
@@ -1745,6 +1761,8 @@ int hm_docset_apply(hm_docset *ds, const uint8_t *data, const uint64_t *block_of
     *out = nullptr;
     Busy b(ds);
     if (!b.ok) return hm_engine_fail(ds->e, HM_ERR_INVALID, "hm_docset_apply: another call on this docset is running");
+    if (ds->broken)
+        return hm_engine_fail(ds->e, HM_ERR_DEVICE, "hm_docset_apply: an earlier failed call could not be undone on its store");
     try {
         std::unique_ptr<hm_text> t(new hm_text());
         const int rc = apply(ds, data, block_off, doc_block, docs, n_docs, t.get());

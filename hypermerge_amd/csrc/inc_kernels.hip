@@ -786,8 +786,10 @@ __device__ __forceinline__ uint32_t change_of_op(const hm_change_row *ch, uint32
 
 // After a re-merge (one wave per listed document): survivor metadata (the survivor's change by
 // a binary search over the change rows' first ops), the packed change keys, the objects created
-// as maps / tables, the counter bound, and — for a document with one list / text object — the
-// resident list order (lorder, epos, epar, ekey) from the element positions the merge wrote.
+// as maps / tables, the counter bound, and — for a document with up to HM_INC_LISTS list / text
+// objects — the resident list order from the element positions the merge wrote: the lists end to
+// end in object-id order in lorder (epos global, epar, ekey per element), indexed by the per-handle
+// directory ldir = (object, elements) per list.
 // Documents that are not clean (an error, queued changes) get flags = 0: their next submit
 // re-merges.
 __global__ __launch_bounds__(256) void inc_meta_kernel(MetaArgs a) {

@@ -151,6 +151,39 @@ def test_docset_failed_call_is_undone_everywhere(where, monkeypatch):
         assert render_objects(view_objects(ds.view(x))) == json.loads(json.dumps(s["state"]))
 
 
+def test_docset_failed_call_frees_a_failed_new_documents_handle(monkeypatch):
+    """A new document whose own merge throws keeps a fresh (empty) handle; when the call then
+    fails as a whole, that handle goes back to the free list and the document must not keep it —
+    otherwise a later new document is given the same handle and both share store rows."""
+    from hypermerge_amd.columnar import ROOT_ID as R
+    from hypermerge_amd.docset import DocSet, render_objects, view_objects
+    from hypermerge_amd.engine import Engine, EngineError
+    ds = DocSet(Engine(0))
+    a = ds.open(3)
+    good = [{"actor": "g0", "seq": 1, "deps": {}, "ops": [{"action": "set", "obj": R, "key": "k", "value": 1}]}]
+    bad = [{"actor": "b0", "seq": 1, "deps": {}, "ops": [{"action": "set", "obj": "no-such-object", "key": "k", "value": 2}]}]
+    monkeypatch.setenv("HM_DOCSET_INJECT_FAIL", "read")
+    with pytest.raises(EngineError):
+        ds.apply([a, a + 1], [_blocks(good), _blocks(bad)])
+    monkeypatch.delenv("HM_DOCSET_INJECT_FAIL")
+    assert ds.info(a + 1)["a_stride"] == 0                    # not placed: no handle kept
+    h = ds.handles(8)
+    assert h["opened"] == h["free"]                           # both fresh handles are free again
+    # the failed document, then a fresh one: each gets its own handle
+    res, _ = ds.apply([a + 1], [_blocks(bad)])
+    assert res["status"][0] != 0
+    other = [{"actor": "o0", "seq": 1, "deps": {}, "ops": [{"action": "set", "obj": R, "key": "z", "value": 9}]}]
+    res, _ = ds.apply([a, a + 2], [_blocks(good), _blocks(other)])
+    assert (res["status"] == 0).all()
+    fixed = [{"actor": "b0", "seq": 1, "deps": {}, "ops": [{"action": "set", "obj": R, "key": "q", "value": 3}]}]
+    res, _ = ds.apply([a + 1], [_blocks(fixed)])
+    assert (res["status"] == 0).all()
+    for x, log in ((a, good), (a + 1, fixed), (a + 2, other)):
+        assert render_objects(view_objects(ds.view(x))) == json.loads(json.dumps(_oracle(log)["state"])), x
+    h = ds.handles(8)
+    assert h["opened"] - h["free"] == 3                       # one handle per document
+
+
 def test_docset_moves_documents_to_wider_stores():
     """Documents whose actors outgrow 8 / 16 / 32 move to the wider store class with their
     whole log; the merged state equals the oracle's, patches included."""
