@@ -327,6 +327,13 @@ def main() -> int:
     traffic = None
     if rank == 0 and ws == 1 and not args.no_traffic:
         traffic = _pmc_traffic(args, kern["kernel"])
+        if incremental and incremental.get("roofline"):
+            it = _pmc_inc_traffic(args)
+            if it:
+                ro = incremental["roofline"]
+                ro["traffic_detail"] = it
+                ro["traffic"] = it["bytes_per_doc"] * args.docs          # per 1M-document round
+                ro["traffic_vs_alg"] = it["bytes_per_doc"] / ro["alg_bytes_per_doc"]
 
     if rank == 0:
         line = {
@@ -519,7 +526,8 @@ def _incremental(eng, batch, args, tail=4, oracle_docs=0):
                        pinned((n, S), np.uint32))
     rounds, same, routing_ok = [], True, True
     for ri, (sub, sel, cnt, t) in enumerate(rounds_in):
-        r = {"docs": int(len(sel)), "changes": int(len(sub.changes)), "ops": int(len(sub.ops))}
+        r = {"docs": int(len(sel)), "changes": int(len(sub.changes)), "ops": int(len(sub.ops)),
+             "alg_bytes": inc_alg_bytes(sub, S)}
         nb = len(sel) * (32 + 12 * S)
         legs = list(zip(stores[:2], ("incremental", "remerge"), out))
         # the two legs take turns going first (the first submit after the host's work between
@@ -531,7 +539,8 @@ def _incremental(eng, batch, args, tail=4, oracle_docs=0):
             nf = st.wait_device(o)
             torch.cuda.synchronize(dev)
             dt = time.perf_counter() - t0
-            r[tag] = {"ms": dt * 1e3, "changes_per_s": len(sub.changes) / dt, "routing": st.last_routing(), "failed": nf}
+            r[tag] = {"ms": dt * 1e3, "changes_per_s": len(sub.changes) / dt, "routing": st.last_routing(), "failed": nf,
+                      **st.last_kernel_ms()}
         same &= bool(torch.equal(out[0][:nb], out[1][:nb]))
         routing_ok &= r["incremental"]["routing"]["incremental"] == len(sel)
         # PCIe leg: host tables in page-locked memory, results into kept page-locked arrays
@@ -570,7 +579,22 @@ def _incremental(eng, batch, args, tail=4, oracle_docs=0):
     routed = [r["incremental"]["routing"] for r in rounds]
     for st in stores:
         st.close()
+    # the incremental kernels on the roofline: §8(d) bytes of each round (inc_alg_bytes) over the
+    # kernels' HIP-event time, rounds that went fully incremental only (a re-merged document's
+    # bytes are the merge kernels')
+    full = [r for r in rounds if r["incremental"]["routing"]["remerged"] == 0]
+    kb = sum(r["alg_bytes"] for r in full)
+    kms = sum(r["incremental"]["incremental_ms"] for r in full)
+    roof = None
+    if kms > 0:
+        ach = kb / (kms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS,
+                "kernel": "inc_group_kernel (+ inc_lane_kernel / inc_group_kernel<64> passes)", "kernel_ms": kms,
+                "alg_bytes": kb, "alg_bytes_per_doc": kb / max(1, sum(r["docs"] for r in full)),
+                "rounds": len(full), "traffic": None}
+        assert roof["frac"] <= 1.0, roof
     return {"value": tot_c / t_inc, "unit": "changes/s", "resident_docs": n, "oracle_docs_equal": oracle_ok,
+            "roofline": roof,
             "incremental_share": sum(x["incremental"] for x in routed) / max(1, sum(sum(x.values()) for x in routed)),
             "us_per_round": t_inc * 1e6 / len(rounds), "remerge_value": tot_c / t_rem,
             "speedup_vs_remerge": t_rem / t_inc, "same_as_remerge": same, "all_incremental": routing_ok,
@@ -578,6 +602,28 @@ def _incremental(eng, batch, args, tail=4, oracle_docs=0):
             "path": "RowStore (hm_store): hm_batch_submit_device + hm_batch_wait_device per round (new rows in HBM, "
                     "per-document results gathered in HBM); incremental = inc_group_kernel; pcie_* = hm_batch_submit / "
                     "hm_batch_wait from page-locked host buffers"}
+
+
+def inc_alg_bytes(sub, S):
+    """Algorithmic HBM bytes of one incremental applyRemoteChanges round (DESIGN §3
+    inc_group_kernel): the new change / dep / op rows read from the submit and written to the log;
+    per new change its history slot and packed key (8 B), its allDeps row written (4S) and each
+    transitiveDeps fold source's allDeps row read (4S: its deps, plus {actor: seq - 1} unless a dep
+    names the actor); per document its result row and incremental state read and written (2 x 32 B
+    each), its clock and heads rows read (8S) and clock / back-clock / heads written (12S); per
+    register the round's set / del / link / inc ops hit, the register row read and written (2 x 16 B)
+    and one survivor with its metadata read and written (2 x 24 B: a last-writer-wins register)."""
+    ch, dp, op, docs = sub.changes, sub.deps, sub.ops, sub.docs
+    nc, nd, no, n = len(ch), len(dp), len(op), len(docs)
+    chg = np.repeat(np.arange(nc), ch["n_deps"].astype(np.int64))
+    own = np.zeros(nc, bool)
+    if nd:
+        own[chg[dp["actor"] == ch["actor"][chg]]] = True
+    sources = nd + int(((~own) & (ch["seq"] > 1)).sum())
+    doc_of_op = np.repeat(np.arange(n), docs["n_ops"].astype(np.int64))
+    asg = op["action"] >= 5
+    hits = len(np.unique(doc_of_op[asg].astype(np.int64) * (1 << 32) + op["reg"][asg].astype(np.int64))) if asg.any() else 0
+    return int(2 * (24 * nc + 8 * nd + 32 * no) + nc * (8 + 4 * S) + sources * 4 * S + n * (128 + 20 * S) + hits * 80)
 
 
 def _pinned_rows(b):
@@ -771,6 +817,50 @@ def _pmc_traffic(args, kernel="merge_small_kernel"):
     wr = vals["WRITE_SIZE"] * 1024
     return {"bytes": rd + wr, "read_bytes": rd, "write_bytes": wr, "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
             "(separate passes), FETCH_SIZE x2 per MI355X_MICROARCH.md §HBM"}
+
+
+def _pmc_inc_traffic(args):
+    """HBM bytes per document of the incremental kernels (inc_lane_kernel, inc_group_kernel<G>) over
+    the resident leg's rounds: tools/inc_profile.py (the same documents and rounds as
+    _incremental) under two rocprofv3 PMC passes, FETCH_SIZE x2 + WRITE_SIZE as _pmc_traffic."""
+    import csv
+    import glob
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None
+    vals, docs = {}, None
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="hm_pmci_", dir="/tmp")
+        cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "run", "--", sys.executable,
+               os.path.join(HERE, "tools", "inc_profile.py"), "--incremental", "1", "--device", "1", "--docs", str(args.docs)]
+        pr = subprocess.Popen(cmd, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), stdout=subprocess.DEVNULL,
+                              stderr=subprocess.PIPE, start_new_session=True, text=True)
+        try:
+            _, err = pr.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            os.killpg(pr.pid, signal.SIGKILL)
+            pr.wait()
+            shutil.rmtree(d, ignore_errors=True)
+            return None
+        tot = 0.0
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    if row.get("Counter_Name") == ctr and ("inc_group_kernel" in row["Kernel_Name"] or
+                                                           "inc_lane_kernel" in row["Kernel_Name"]):
+                        tot += float(row["Counter_Value"])
+        shutil.rmtree(d, ignore_errors=True)
+        nd = sum(int(l.split()[2]) for l in (err or "").splitlines() if l.startswith("round "))
+        if not tot or not nd:
+            return None
+        vals[ctr], docs = tot, nd
+    rd, wr = vals["FETCH_SIZE"] * 1024 * 2, vals["WRITE_SIZE"] * 1024
+    return {"bytes_per_doc": (rd + wr) / docs, "read_per_doc": rd / docs, "write_per_doc": wr / docs, "docs": docs,
+            "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of tools/inc_profile.py (same rounds), FETCH_SIZE x2"}
 
 
 def _subbatch(b, k):

@@ -359,7 +359,7 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
     if (gl < S) {
         ck = A.clock[(size_t)h * S + gl];
         hd = A.heads[(size_t)h * S + gl];
-        mc = A.min_clock ? A.min_clock[(size_t)h * S + gl] : 0u;
+        mc = (A.min_clock && (D.inc & HM_DINC_MINC)) ? A.min_clock[(size_t)h * S + gl] : 0u;   // (no row: zeros)
     }
     uint32_t ca = 0, cq = 0, cnd = 0, cdo = 0, cno = 0, coo = 0;
     if (gl < nnc) {
@@ -411,15 +411,31 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
     } else {
         li = nl && o_obj != 0 && (o_obj >= 64 || !((I.mapmask >> o_obj) & 1ull)) ? 0u : HM_NONE;
     }
-    const bool lst = gl < nno && li != HM_NONE;
-    const bool bad_o = gl < nno && ((o_act != HM_SET && o_act != HM_DEL && o_act != HM_LINK && o_act != HM_INC &&
+    // makeMap / makeTable (A.0): a fresh object id (a duplicate throws: the re-merge reports it);
+    // documents with lists hand object creation to the re-merge (their list ids are not in mapmask).
+    // `made` = the maps this round created before each op (an exclusive prefix OR over the group)
+    const bool mk = gl < nno && (o_act == HM_MAKE_MAP || o_act == HM_MAKE_TABLE);
+    unsigned long long made = mk && o_obj < 64 ? (1ull << o_obj) : 0ull;
+#pragma unroll
+    for (uint32_t d = 1; d < (uint32_t)G; d <<= 1) {
+        const unsigned long long y = (unsigned long long)__shfl_up((long long)made, d, G);
+        if (gl >= d) made |= y;
+    }
+    const unsigned long long made_all = (unsigned long long)__shfl((long long)made, G - 1, G);
+    made = (unsigned long long)__shfl_up((long long)made, 1, G);
+    if (gl == 0) made = 0;
+    const unsigned long long known = I.mapmask | made;
+    const bool lst = gl < nno && !mk && li != HM_NONE;
+    const bool bad_o = gl < nno && ((o_act != HM_SET && o_act != HM_DEL && o_act != HM_LINK && o_act != HM_INC && !mk &&
                                      !(lst && o_act == HM_INS)) ||
+                                    (mk && ((D.inc & HM_DINC_LISTS) || o_obj == 0 || o_obj >= 64 || ((known >> o_obj) & 1ull))) ||
                                     (o_act == HM_INC && o_vt != HM_V_INT && o_vt != HM_V_FLOAT) ||
-                                    o_obj >= D.n_objs || o_reg >= D.n_r ||
+                                    o_obj >= D.n_objs || (!mk && o_reg >= D.n_r) ||
                                     (o_vt == HM_V_INT && abs64(oval) > TWO53) ||
                                     (o_act == HM_INS && (o_elem >= (1u << 24) || (o_par != HM_HEAD && o_par >= D.n_r))) ||
-                                    // an object other than ROOT must be a map / table the log created
-                                    (!lst && o_obj != 0 && (o_obj >= 64 || !((I.mapmask >> o_obj) & 1ull))));
+                                    // an object other than ROOT must be a map / table the log (or an
+                                    // earlier op of this round) created
+                                    (!mk && !lst && o_obj != 0 && (o_obj >= 64 || !((known >> o_obj) & 1ull))));
     if (g.bits(bad_c || bad_o) || total_o != nno || total_d != nnd) return INC_BAIL;
     const bool any_list = g.bits(lst) != 0;
     if (G < 64 && any_list) return INC_DEFER;                 // list / text ops: one document per wave
@@ -493,11 +509,11 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
     }
 
     // ---- first-touch registers (lane = op): pushes, staging offsets, space ----
-    bool first = gl < nno && o_act != HM_INS;                 // (an ins creates its register; the assigns fill it)
+    bool first = gl < nno && o_act >= HM_SET;                 // (an ins creates its register, a make an object)
     uint32_t push = 0, oj = 0;
     for (uint32_t k = 0; k < nno; k++) {
         const uint32_t r = g.sh(o_reg, k), ak = g.sh(o_act, k);
-        if (k < gl && r == o_reg && ak != HM_INS) first = false;
+        if (k < gl && r == o_reg && ak >= HM_SET) first = false;
         if (k >= gl && r == o_reg && (ak == HM_SET || ak == HM_LINK)) push++;
     }
     for (uint32_t j = 0; j < nnc; j++)
@@ -626,7 +642,7 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
         if (gl < cnt0) { x = ssv[sb + gl]; xm = smt[sb + gl]; }
         uint32_t cnt = cnt0;
         for (uint32_t k = k0; k < nno; k++) {
-            if (g.sh(o_reg, k) != greg || g.sh(o_act, k) == HM_INS) continue;
+            if (g.sh(o_reg, k) != greg || g.sh(o_act, k) < HM_SET) continue;
             const uint32_t act = g.sh(o_act, k), vt = g.sh(o_vt, k), dtk = g.sh(o_dt, k);
             const uint32_t vlo = g.sh(o_vlo, k), vhi = g.sh(o_vhi, k), j = g.sh(oj, k);
             const uint32_t a = g.sh(ca, j), q = g.sh(cq, j);
@@ -743,7 +759,7 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
         r.min_cmp = (ag && bg) ? 0u : (ag ? 1u : (bg ? 2u : 3u));
         A.res_docs[h] = r;
         IncState s = I;
-        s.s_used = I.s_used + acc; s.cabs = cabs;
+        s.s_used = I.s_used + acc; s.cabs = cabs; s.mapmask = I.mapmask | made_all;
         if (G == 64 && any_list) s.pad[0] = lp.n_el;
         A.ist[h] = s;
     }
@@ -764,13 +780,388 @@ __global__ __launch_bounds__(256) void inc_group_kernel(IncArgs A) {
     for (uint32_t q = blockIdx.x * NG + grp; q < n; q += gridDim.x * NG) {
         const uint32_t di = A.list ? A.list[1 + q] : q;
         const AppendDesc D = A.descs[di];
-        if (!D.inc || (G < 64 && D.inc == 2)) continue;            // (inc 2: listed for the wave pass)
+        const uint32_t route = D.inc & HM_DINC_ROUTE;
+        if (!route || route == 3 || (G < 64 && route == 2)) continue;   // (2: listed for the wave pass, 3: the lane pass)
         const int rc = inc_doc<G>(D, A, s_sv[grp], s_mt[grp], s_ls[G == 64 ? grp : 0]);
         if (rc != INC_DONE && gl == 0) {
             if (rc == INC_DEFER && A.defer) A.defer[1 + atomicAdd(&A.defer[0], 1u)] = di;
             else A.bail[1 + atomicAdd(&A.bail[0], 1u)] = D.handle;
         }
     }
+}
+
+// ---------------- one lane per document: map documents of strides <= 16 ----------------
+// The group pass above spends most of its time exchanging values between the lanes of a group
+// (every step of a document's short serial work is a ds_bpermute round trip).  A map document's
+// round — a few new changes, a few ops on a few registers — is serial work over a few hundred
+// bytes, so here ONE lane takes the whole document: its clock / heads / allDeps rows live in
+// registers, the new changes apply one after the other in arrival order (no limit on their
+// number: each change's allDeps row is folded, written and used by its own ops, and a later
+// change finds it in the log like any older one), and each op runs applyAssign on its register's
+// survivor list read from the slot and written back (in place when it does not grow).  Cross-
+// lane work is only the wave-aggregated list appends at the end.
+//   validation (before any store but the log append): every change causally ready in arrival
+//   order against the resident clock, every op a map op on ROOT / a map of the log (or a
+//   makeMap / makeTable of a new object), counters inside the exact-integer bound.  A document
+//   that fails a check with a chance in the group / wave pass (list ops, a moved segment) is
+//   deferred to it untouched; anything else goes to the re-merge (bail).  After the first store
+//   the only exits are a register of more than LSV survivors, a full slot area or a fold source
+//   missing from the log — the document is then re-merged, which rewrites every row the lane
+//   wrote (the new rows are in the log before anything else happens).
+constexpr uint32_t LSV = 4;    // survivors of a register the lane path holds (more: re-merge)
+constexpr uint32_t LKF = 2;    // fold sources resolved and loaded together
+
+// v[i] of a register array by selects (each element made opaque first: a select between two
+// loads of one array is otherwise folded into a load through a selected pointer, which sends the
+// whole array to scratch memory)
+template <int N>
+__device__ __forceinline__ uint32_t lsel(const uint32_t (&v)[N], uint32_t i) {
+    uint32_t r = v[0];
+    asm volatile("" : "+v"(r));
+#pragma unroll
+    for (int x = 1; x < N; x++) {
+        uint32_t t = v[x];
+        asm volatile("" : "+v"(t));
+        r = i == (uint32_t)x ? t : r;
+    }
+    return r;
+}
+template <int N>
+__device__ __forceinline__ void lput(uint32_t (&v)[N], uint32_t i, uint32_t y) {
+#pragma unroll
+    for (int x = 0; x < N; x++) v[x] = i == (uint32_t)x ? y : v[x];
+}
+template <int S>
+__device__ __forceinline__ void lrow_load(const uint32_t *p, uint32_t (&v)[S]) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(p);
+#pragma unroll
+    for (int k = 0; k < S / 4; k++) {
+        const uint4 w = q[k];
+        v[4 * k] = w.x; v[4 * k + 1] = w.y; v[4 * k + 2] = w.z; v[4 * k + 3] = w.w;
+    }
+}
+template <int S>
+__device__ __forceinline__ void lrow_store(uint32_t *p, const uint32_t (&v)[S]) {
+    uint4 *q = reinterpret_cast<uint4 *>(p);
+#pragma unroll
+    for (int k = 0; k < S / 4; k++) q[k] = make_uint4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+}
+
+// applyAssign of one map op on its register (A.2): the register's survivors (at most LSV) read
+// from its slot, filtered against the op's change's allDeps row `ad` (isConcurrent:
+// allDeps(op)[x.actor] < x.seq), an inc added to every surviving counter set that is its ancestor,
+// the op pushed (set / link), sortBy(actor) (stable) then reverse — each element written straight
+// to its place, in the slot when the list does not grow, else at the end of the slot area
+template <int S>
+__device__ __forceinline__ int lane_assign(const AppendDesc &D, const IncArgs &A, const uint32_t (&ad)[S], uint32_t a, uint32_t q,
+                                           uint32_t obj, uint32_t reg, uint32_t act, uint32_t dt, uint32_t vt, uint32_t vlo,
+                                           uint32_t vhi, uint32_t op_local, const hm_reg_result &rr, uint32_t &used,
+                                           int32_t &dsurv) {
+    const uint32_t n = rr.n_surv;
+    if (n > LSV) return INC_BAIL;
+    uint4 x[LSV + 1];
+    uint2 m[LSV + 1];
+#pragma unroll
+    for (uint32_t i = 0; i < LSV; i++) {
+        x[i] = make_uint4(0u, 0u, 0u, 0u); m[i] = make_uint2(0u, 0u);
+        if (i < n) {
+            x[i] = *reinterpret_cast<const uint4 *>(A.surv + D.dst_o + rr.surv_off + i);
+            m[i] = A.smeta[D.dst_o + rr.surv_off + i];
+        }
+    }
+    uint32_t keep = 0, pos[LSV + 1], act8[LSV + 1], cnt = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < LSV; i++) {
+        pos[i] = 0; act8[i] = m[i].y & 0xFFu;
+        if (i >= n) continue;
+        const uint32_t anc = lsel<S>(ad, m[i].y & 0xFFu);
+        if (act == HM_INC && (m[i].y & 0x100u) && (x[i].y == HM_V_INT || x[i].y == HM_V_FLOAT) && anc >= m[i].x) {
+            const uint64_t cur = ((uint64_t)x[i].w << 32) | x[i].z, inc = ((uint64_t)vhi << 32) | vlo;
+            if (x[i].y == HM_V_INT && vt == HM_V_INT) {
+                const uint64_t sum = (uint64_t)((int64_t)cur + (int64_t)inc);
+                x[i].z = (uint32_t)sum; x[i].w = (uint32_t)(sum >> 32);
+            } else {
+                double xv, iv;
+                if (x[i].y == HM_V_INT) xv = (double)(int64_t)cur; else __builtin_memcpy(&xv, &cur, 8);
+                if (vt == HM_V_INT) iv = (double)(int64_t)inc; else __builtin_memcpy(&iv, &inc, 8);
+                const double rs = xv + iv;
+                uint64_t rb;
+                __builtin_memcpy(&rb, &rs, 8);
+                x[i].z = (uint32_t)rb; x[i].w = (uint32_t)(rb >> 32); x[i].y = HM_V_FLOAT;
+            }
+        }
+        if (act == HM_INC || anc < m[i].x) { keep |= 1u << i; pos[i] = cnt++; }
+    }
+    x[LSV] = make_uint4(D.n_old_o + op_local, vt, vlo, vhi);
+    m[LSV] = make_uint2(q, a | ((act == HM_SET && dt == HM_DT_COUNTER) ? 0x100u : 0u));
+    act8[LSV] = a; pos[LSV] = cnt;
+    if (act == HM_SET || act == HM_LINK) { keep |= 1u << LSV; cnt++; }
+    const uint32_t off = cnt <= n ? rr.surv_off : used;
+    if (cnt > n) {
+        if ((unsigned long long)used + cnt > D.o_cap) return INC_BAIL;    // no room: the re-merge repacks
+        used += cnt;
+    }
+#pragma unroll
+    for (uint32_t e = 0; e <= LSV; e++) {
+        if (!((keep >> e) & 1u)) continue;
+        uint32_t rank = 0;
+#pragma unroll
+        for (uint32_t f = 0; f <= LSV; f++)
+            rank += ((keep >> f) & 1u) && (act8[f] < act8[e] || (act8[f] == act8[e] && pos[f] < pos[e])) ? 1u : 0u;
+        const uint32_t dst = off + cnt - 1u - rank;
+        *reinterpret_cast<uint4 *>(A.surv + D.dst_o + dst) = x[e];
+        A.smeta[D.dst_o + dst] = m[e];
+    }
+    dsurv += (int32_t)cnt - (int32_t)n;
+    hm_reg_result nr;
+    nr.n_surv = cnt; nr.surv_off = off; nr.list_index = -1; nr.obj = obj;
+    A.regs[D.dst_r + reg] = nr;
+    return INC_DONE;
+}
+
+// the document's clocks (back_clock = clock: the queue is empty), result row and IncState
+template <int S>
+__device__ __forceinline__ void lane_finish(const AppendDesc &D, const IncArgs &A, const IncState &I, const hm_doc_result &R0,
+                                            const uint32_t (&ck)[S], const uint32_t (&hd)[S], uint32_t used, int32_t dsurv,
+                                            unsigned long long cabs, unsigned long long mm) {
+    const uint32_t h = D.handle;
+    lrow_store<S>(A.clock + (size_t)h * S, ck);
+    lrow_store<S>(A.back_clock + (size_t)h * S, ck);
+    lrow_store<S>(A.heads + (size_t)h * S, hd);
+    uint32_t mc[S];
+#pragma unroll
+    for (int x = 0; x < S; x++) mc[x] = 0;
+    if (D.inc & HM_DINC_MINC) lrow_load<S>(A.min_clock + (size_t)h * S, mc);
+    bool ag = true, bg = true;
+#pragma unroll
+    for (int x = 0; x < S; x++) { ag &= ck[x] >= mc[x]; bg &= mc[x] >= ck[x]; }
+    hm_doc_result r = {};
+    r.status = HM_OK; r.err_change = HM_NONE; r.err_op = HM_NONE;
+    r.hist_len = R0.hist_len + D.n_new_c; r.n_queued = 0; r.n_surv = (uint32_t)((int32_t)R0.n_surv + dsurv);
+    r.min_cmp = (ag && bg) ? 0u : (ag ? 1u : (bg ? 2u : 3u));
+    A.res_docs[h] = r;
+    IncState st = I;
+    st.s_used = used; st.cabs = cabs; st.mapmask = mm;
+    A.ist[h] = st;
+}
+
+template <int S>
+__device__ int inc_lane(const AppendDesc &D, const IncArgs &A) {
+    const uint32_t h = D.handle, NA = D.n_actors, nnc = D.n_new_c, nnd = D.n_new_d, nno = D.n_new_o;
+    const bool rows_moved = D.src_c != D.dst_c || D.src_d != D.dst_d || D.src_o != D.dst_o;
+    if (!rows_moved) {
+        // the new rows into the log first (append_kernel skipped this document): whatever
+        // happens below, the re-merge finds them there
+#pragma unroll 4
+        for (uint32_t i = 0; i < nnc; i++) {
+            hm_change_row c = A.st_changes[D.new_c + i];
+            c.dep_off = D.dst_d + D.n_old_d + (c.dep_off - D.new_d);
+            c.op_first = D.dst_o + D.n_old_o + (c.op_first - D.new_o);
+            A.changes[D.dst_c + D.n_old_c + i] = c;
+        }
+#pragma unroll 4
+        for (uint32_t i = 0; i < nnd; i++) A.deps[D.dst_d + D.n_old_d + i] = A.st_deps[D.new_d + i];
+        const uint4 *so4 = reinterpret_cast<const uint4 *>(A.st_ops + D.new_o);
+        uint4 *do4 = reinterpret_cast<uint4 *>(A.ops + D.dst_o + D.n_old_o);
+#pragma unroll 4
+        for (uint32_t i = 0; i < 2 * nno; i++) do4[i] = so4[i];
+    }
+    // a moved segment: the group pass copies the per-change / survivor / register rows along
+    if (rows_moved || D.src_r != D.dst_r) return INC_DEFER;
+    if (nnc == 0 || NA > (uint32_t)S || D.n_old_r > D.n_r) return INC_BAIL;
+    const IncState I = A.ist[h];
+    if ((I.flags & (HM_IST_VALID | HM_IST_NOCKEY)) != HM_IST_VALID) return INC_BAIL;
+    const bool lists = (D.inc & HM_DINC_LISTS) != 0;
+    const hm_doc_result R0 = A.res_docs[h];
+    uint32_t ck[S], hd[S];
+    lrow_load<S>(A.clock + (size_t)h * S, ck);
+    lrow_load<S>(A.heads + (size_t)h * S, hd);
+    // the log's last 8 change keys, oldest first (the fold sources are almost always there)
+    uint32_t tail[8];
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        const int idx = (int)D.n_old_c - 8 + t;
+        tail[t] = idx >= 0 ? A.ckey[D.dst_c + idx] : 0u;
+    }
+
+    // ---- validation: readiness in arrival order, supported ops, counter bound ----
+    unsigned long long mm = I.mapmask, cadd = 0;
+    {
+        uint32_t cur[S];
+#pragma unroll
+        for (int x = 0; x < S; x++) cur[x] = ck[x];
+        uint32_t xd = 0, xo = 0;
+        int defer = 0;
+        for (uint32_t j = 0; j < nnc; j++) {
+            const hm_change_row c = A.st_changes[D.new_c + j];
+            if (c.actor >= NA || c.seq == 0 || c.seq >= (1u << 24) || c.dep_off - D.new_d != xd || c.op_first - D.new_o != xo ||
+                xd + c.n_deps > nnd || xo + c.n_ops > nno)
+                return INC_BAIL;
+            if (lsel<S>(cur, c.actor) + 1u != c.seq) return INC_BAIL;      // a duplicate, or not ready: the queue decides
+            for (uint32_t t = 0; t < c.n_deps; t++) {
+                const hm_dep_row d = A.st_deps[D.new_d + xd + t];
+                if (d.actor >= NA) return INC_BAIL;
+                if (d.actor != c.actor && lsel<S>(cur, d.actor) < d.seq) return INC_BAIL;
+            }
+            for (uint32_t k = 0; k < c.n_ops; k++) {
+                const uint4 *src = reinterpret_cast<const uint4 *>(A.st_ops + D.new_o + xo + k);
+                const uint4 w0 = src[0], w1 = src[1];
+                const uint32_t obj = w0.x, reg = w0.y, act = w1.x & 0xFFu, dt = (w1.x >> 8) & 0xFFu, vt = (w1.x >> 16) & 0xFFu;
+                const int64_t v = (int64_t)(((uint64_t)w1.w << 32) | w1.z);
+                if (act == HM_MAKE_MAP || act == HM_MAKE_TABLE) {
+                    // a new map: its id must be fresh (a list's id is not in mapmask: documents with
+                    // lists take the group pass, which hands object creation to the re-merge)
+                    if (lists) { defer = 1; continue; }
+                    if (obj == 0 || obj >= 64 || obj >= D.n_objs || ((mm >> obj) & 1ull)) return INC_BAIL;
+                    mm |= 1ull << obj;
+                    continue;
+                }
+                if (act == HM_INS || act == HM_MAKE_LIST || act == HM_MAKE_TEXT) { defer = 1; continue; }
+                if (act != HM_SET && act != HM_DEL && act != HM_LINK && act != HM_INC) return INC_BAIL;
+                if (obj >= D.n_objs || reg >= D.n_r) return INC_BAIL;
+                if (obj != 0 && (obj >= 64 || !((mm >> obj) & 1ull))) {
+                    if (lists) { defer = 1; continue; }              // a list element: the wave pass
+                    return INC_BAIL;
+                }
+                if (act == HM_INC && vt != HM_V_INT && vt != HM_V_FLOAT) return INC_BAIL;
+                if (vt == HM_V_INT && abs64(v) > TWO53) return INC_BAIL;
+                if (vt == HM_V_INT && (act == HM_INC || (act == HM_SET && dt == HM_DT_COUNTER))) cadd += abs64(v);
+            }
+            xd += c.n_deps; xo += c.n_ops;
+            lput<S>(cur, c.actor, c.seq);
+        }
+        if (xd != nnd || xo != nno) return INC_BAIL;
+        if (defer) return INC_DEFER;
+    }
+    const unsigned long long cabs = I.cabs + cadd;
+    if (cabs > TWO53) return INC_BAIL;
+
+    // ---- apply: registers new to the document start empty (the ops below read their rows) ----
+    for (uint32_t r = D.n_old_r; r < D.n_r; r++) {
+        hm_reg_result z;
+        z.n_surv = 0; z.surv_off = 0; z.list_index = -1; z.obj = HM_NONE;
+        A.regs[D.dst_r + r] = z;
+    }
+    uint32_t used = I.s_used;
+    int32_t dsurv = 0;
+    uint32_t xd = 0, xo = 0;
+    for (uint32_t j = 0; j < nnc; j++) {
+        const hm_change_row c = A.st_changes[D.new_c + j];
+        const uint32_t a = c.actor, q = c.seq, nd = c.n_deps, end = D.n_old_c + j;
+        // transitiveDeps: the literal fold over deps in key order, then {actor: seq - 1} unless a
+        // dep names the actor (A.1); each source is the applied row of (actor, seq) in the log
+        uint32_t ad[S];
+#pragma unroll
+        for (int x = 0; x < S; x++) ad[x] = 0;
+        bool own = false;
+        for (uint32_t t0 = 0; t0 <= nd; t0 += LKF) {
+            uint32_t sa[LKF], sq[LKF], si[LKF];
+#pragma unroll
+            for (uint32_t u = 0; u < LKF; u++) {
+                const uint32_t t = t0 + u;
+                sa[u] = 0; sq[u] = 0; si[u] = HM_NONE;
+                if (t < nd) {
+                    const hm_dep_row d = A.st_deps[D.new_d + xd + t];
+                    sa[u] = d.actor; sq[u] = d.seq;
+                    if (d.actor == a) { sq[u] = q - 1u; own = true; }
+                } else if (t == nd && !own) {
+                    sa[u] = a; sq[u] = q - 1u;
+                }
+            }
+            // positions: the last 8 rows in registers, then older rows 8 at a time
+            uint32_t miss = 0;
+#pragma unroll
+            for (uint32_t u = 0; u < LKF; u++) {
+                if (!sq[u]) continue;
+                const uint32_t want = hm_ckey(sa[u], sq[u], true);
+#pragma unroll
+                for (int t = 0; t < 8; t++) if (tail[t] == want && (int)end - 8 + t >= 0) si[u] = end - 8u + (uint32_t)t;
+                if (si[u] == HM_NONE) miss |= 1u << u;
+            }
+            for (int top = (int)end - 9; miss && top >= 0; top -= 8) {
+                uint32_t kk[8];
+#pragma unroll
+                for (int t = 0; t < 8; t++) kk[t] = top - t >= 0 ? A.ckey[D.dst_c + top - t] : 0u;
+#pragma unroll
+                for (uint32_t u = 0; u < LKF; u++) {
+                    if (!((miss >> u) & 1u)) continue;
+                    const uint32_t want = hm_ckey(sa[u], sq[u], true);
+#pragma unroll
+                    for (int t = 7; t >= 0; t--) if (kk[t] == want && top - t >= 0) si[u] = (uint32_t)(top - t);
+                    if (si[u] != HM_NONE) miss &= ~(1u << u);
+                }
+            }
+            if (miss) return INC_BAIL;
+            uint32_t row[LKF][S];
+#pragma unroll
+            for (uint32_t u = 0; u < LKF; u++) {
+                if (sq[u]) lrow_load<S>(A.all_deps + (size_t)(D.dst_c + si[u]) * S, row[u]);
+                else {
+#pragma unroll
+                    for (int x = 0; x < S; x++) row[u][x] = 0;
+                }
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < LKF; u++) {
+                if (!sq[u]) continue;
+#pragma unroll
+                for (int x = 0; x < S; x++) if ((uint32_t)x < NA && row[u][x] > ad[x]) ad[x] = row[u][x];
+                lput<S>(ad, sa[u], sq[u]);
+            }
+        }
+        // the change enters history
+        const uint32_t key = hm_ckey(a, q, true);
+        A.hist[D.dst_c + end] = (int32_t)(R0.hist_len + j);
+        A.ckey[D.dst_c + end] = key;
+        lrow_store<S>(A.all_deps + (size_t)(D.dst_c + end) * S, ad);
+#pragma unroll
+        for (int t = 0; t < 7; t++) tail[t] = tail[t + 1];
+        tail[7] = key;
+#pragma unroll
+        for (int x = 0; x < S; x++) if (hd[x] && hd[x] <= ad[x]) hd[x] = 0;
+        lput<S>(hd, a, q);
+        lput<S>(ck, a, q);
+
+        // its ops: applyAssign on each register (A.2)
+        for (uint32_t k = 0; k < c.n_ops; k++) {
+            const uint4 *src = reinterpret_cast<const uint4 *>(A.st_ops + D.new_o + xo + k);
+            const uint4 w0 = src[0], w1 = src[1];
+            const uint32_t act = w1.x & 0xFFu;
+            if (act == HM_MAKE_MAP || act == HM_MAKE_TABLE) continue;    // (mapmask updated above)
+            const hm_reg_result rr = A.regs[D.dst_r + w0.y];
+            if (lane_assign<S>(D, A, ad, a, q, w0.x, w0.y, act, (w1.x >> 8) & 0xFFu, (w1.x >> 16) & 0xFFu, w1.z, w1.w, xo + k, rr,
+                               used, dsurv) != INC_DONE)
+                return INC_BAIL;
+        }
+        xd += nd; xo += c.n_ops;
+    }
+
+    lane_finish<S>(D, A, I, R0, ck, hd, used, dsurv, cabs, mm);
+    return INC_DONE;
+}
+
+// wave-aggregated append of the lanes' entries to list[1..] (list[0] = count)
+__device__ __forceinline__ void lane_list_push(uint32_t *list, bool p, uint32_t v) {
+    const uint64_t m = __ballot(p);
+    if (!m) return;
+    const uint32_t lane = __lane_id(), lead = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == lead) base = atomicAdd(&list[0], (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, (int)lead);
+    if (p) list[1 + base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = v;
+}
+
+template <int S>
+__global__ __launch_bounds__(256) void inc_lane_kernel(IncArgs A) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    int rc = -1;
+    uint32_t hnd = 0;
+    if (i < A.n) {
+        const AppendDesc D = A.descs[i];
+        if ((D.inc & HM_DINC_ROUTE) == 3u) { hnd = D.handle; rc = inc_lane<S>(D, A); }
+    }
+    // (the group passes hold a round in registers: what the lane pass hands over re-merges)
+    lane_list_push(A.bail, rc == INC_BAIL || rc == INC_DEFER, hnd);
 }
 
 // the change that owns doc-local op k: the last change whose first op is <= k (ops are grouped
@@ -944,6 +1335,12 @@ hipError_t hm_launch_inc_apply(const IncArgs &A, hipStream_t s) {
     hipError_t z = hipMemsetAsync(A.bail, 0, 4, s);
     if (z != hipSuccess) return z;
     auto grid = [](uint32_t n, uint32_t per) { const uint32_t g = (n + per - 1) / per; return g < 65535u ? g : 65535u; };
+    if (S <= 16) {
+        // rounds longer than the group passes hold (route 3): one lane per document, first
+        const uint32_t gl = (A.n + 255) / 256;
+        if (S <= 8) hipLaunchKernelGGL(hmi::inc_lane_kernel<8>, dim3(gl), dim3(256), 0, s, A);
+        else hipLaunchKernelGGL(hmi::inc_lane_kernel<16>, dim3(gl), dim3(256), 0, s, A);
+    }
     if (S <= 8) hipLaunchKernelGGL(hmi::inc_group_kernel<8>, dim3(grid(A.n, 32)), dim3(256), 0, s, A);
     else if (S <= 16) hipLaunchKernelGGL(hmi::inc_group_kernel<16>, dim3(grid(A.n, 16)), dim3(256), 0, s, A);
     if (S <= 16 && A.defer) {

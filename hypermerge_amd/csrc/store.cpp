@@ -109,6 +109,9 @@ struct hm_store {
     bool incremental = true;
     uint32_t inc_mode = 1;                        // 1: small list documents re-merge (cost policy); 2: every one
     uint32_t st_inc = 0, st_cold = 0, st_bail = 0;
+    // HIP events around the last submit's incremental kernels and its re-merge (engine stream)
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    float last_ms[2] = {0.f, 0.f};
 };
 
 namespace {
@@ -427,6 +430,7 @@ void hm_store_destroy(hm_store *s) {
                     s->back_clock, s->heads, s->min_clock, s->stored, s->stage.p, s->dm, s->seen, s->plan.p, s->descs.p,
                     s->bdescs.p, s->list.p, s->blist.p, s->alist.p, s->remap.p, s->inv.p, s->rows.p, s->undo_handles.p, s->st};
     for (void *b : bufs) if (b) (void)hipFree(b);
+    for (hipEvent_t e : s->ev) if (e) (void)hipEventDestroy(e);
     delete s;
 }
 
@@ -574,7 +578,7 @@ static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handl
             size_t mv = 0, rmp = 0, inc = 0, old_o = 0, new_o = 0;
             for (const AppendDesc &D : dd) {
                 const bool m = D.src_c != D.dst_c || D.src_d != D.dst_d || D.src_o != D.dst_o;
-                mv += m; rmp += D.remap_row != 0xFFFFFFFFu; inc += D.inc != 0; new_o += D.n_new_o;
+                mv += m; rmp += D.remap_row != 0xFFFFFFFFu; inc += (D.inc & HM_DINC_ROUTE) != 0; new_o += D.n_new_o;
                 if (m) old_o += D.n_old_o;
             }
             fprintf(stderr, "[hm_store] append: %zu docs, %zu moved (%zu old op rows), %zu re-ranked, %zu incremental, %zu new op rows\n",
@@ -585,6 +589,9 @@ static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handl
         T.mark("alloc+append");
         uint32_t *bail = (uint32_t *)(sp + L.o_bail);
         SCHK(s, hipMemsetAsync(bail, 0, 4, st));
+        if (!s->ev[0])
+            for (auto &e : s->ev) SCHK(s, hipEventCreate(&e));
+        SCHK(s, hipEventRecord(s->ev[0], st));
         if (P.n_inc) {
             IncArgs IA;
             IA.descs = s->descs.p; IA.n = n; IA.list = nullptr; IA.S = S;
@@ -598,6 +605,7 @@ static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handl
             SCHK(s, hm_launch_inc_apply(IA, st));
             dbg_list_state(s, "after");
         }
+        SCHK(s, hipEventRecord(s->ev[1], st));
         T.mark("incremental");
         // the re-merge list: cold documents, then those the incremental kernel handed back
         uint32_t counts[2] = {0, 0};
@@ -605,7 +613,12 @@ static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handl
         SCHK(s, hipMemcpyAsync(&counts[1], bail, 4, hipMemcpyDeviceToHost, st));
         SCHK(s, hipStreamSynchronize(st));
         if (counts[1]) SCHK(s, hipMemcpyAsync(s->list.p + counts[0], bail + 1, (size_t)counts[1] * 4, hipMemcpyDeviceToDevice, st));
+        SCHK(s, hipEventRecord(s->ev[2], st));
         if ((rc = launch_list_merge(s, s->list.p, counts[0] + counts[1]))) return rc;
+        SCHK(s, hipEventRecord(s->ev[3], st));
+        SCHK(s, hipEventSynchronize(s->ev[3]));
+        SCHK(s, hipEventElapsedTime(&s->last_ms[0], s->ev[0], s->ev[1]));
+        SCHK(s, hipEventElapsedTime(&s->last_ms[1], s->ev[2], s->ev[3]));
         dbg_list_state(s, "after merge");
         T.mark("remerge");
         s->st_inc = P.n_inc - counts[1]; s->st_cold = counts[0]; s->st_bail = counts[1];
@@ -766,6 +779,12 @@ int hm_store_set_incremental(hm_store *s, int on) {
 int hm_store_last_routing(const hm_store *s, uint32_t *out3) {
     if (!s || !out3) return HM_ERR_INVALID;
     out3[0] = s->st_inc; out3[1] = s->st_cold; out3[2] = s->st_bail;
+    return HM_OK;
+}
+
+int hm_store_last_kernel_ms(const hm_store *s, float *out2) {
+    if (!s || !out2) return HM_ERR_INVALID;
+    out2[0] = s->last_ms[0]; out2[1] = s->last_ms[1];
     return HM_OK;
 }
 
@@ -930,6 +949,11 @@ int hm_doc_set_min_clock(hm_store *s, uint32_t doc, const uint32_t *clock) {
     if (!s || doc >= s->n_handles || !clock) return HM_ERR_INVALID;
     if (s->pending) return hm_engine_fail(s->e, HM_ERR_INVALID, "batch in flight");
     SCHK(s, hipMemcpy(s->min_clock + (size_t)doc * s->S, clock, s->S * 4, hipMemcpyHostToDevice));
+    // the incremental kernels read the row only for documents that have one
+    DevDoc m;
+    SCHK(s, hipMemcpy(&m, s->dm + doc, sizeof m, hipMemcpyDeviceToHost));
+    m.pad[0] |= HM_DDOC_MINC;
+    SCHK(s, hipMemcpy(s->dm + doc, &m, sizeof m, hipMemcpyHostToDevice));
     return HM_OK;
 }
 

@@ -26,9 +26,10 @@ struct DevDoc {
     uint32_t c_off, c_cap, d_off, d_cap, o_off, o_cap, r_off, r_cap;
     uint32_t n_c, n_d, n_o, n_r, n_objs;
     uint16_t n_actors, flags;
-    uint32_t pad[2];
+    uint32_t pad[2];      // pad[0]: HM_DDOC_* bits
 };
 static_assert(sizeof(DevDoc) == 64, "DevDoc is 64 B");
+#define HM_DDOC_MINC 1u   // hm_doc_set_min_clock wrote the document's minimumClock row
 
 // One batch row's plan: the document's totals before the append (the rollback restores them),
 // the capacities of the segments it outgrows (0 = fits) and its route.
@@ -125,10 +126,18 @@ struct IncArgs {
     uint32_t *defer;                           // [0] count, [1..] desc indices for the wave kernel (NULL: bail)
 };
 
+// AppendDesc.inc: the route (bits 0-1: 0 re-merge, 1 incremental group pass, 2 wave pass, 3 lane pass) and what
+// alloc_kernel adds for the incremental kernels
+#define HM_DINC_ROUTE 3u
+#define HM_DINC_MINC 4u        // the document has a minimumClock row (else it reads as zeros)
+#define HM_DINC_LISTS 8u       // the document has list / text objects
+
 // envelope of the incremental path (larger submits take the full re-merge)
 #define HM_INC_MAX_NEW_C 8
 #define HM_INC_MAX_NEW_O 64
 #define HM_INC_MAX_TGT 128       // transitiveDeps fold steps of a submit's new changes (2 per lane, wave kernel)
+#define HM_INC_LANE_MAX_C 64     // the one-lane pass (map documents, strides <= 16)
+#define HM_INC_LANE_MAX_O 512
 
 struct PlanArgs {
     const hm_doc_row *docs;

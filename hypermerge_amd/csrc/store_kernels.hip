@@ -47,7 +47,7 @@ __global__ __launch_bounds__(SWG) void append_kernel(const AppendDesc *descs, ui
         const uint32_t di = list ? list[k] : k;
         const AppendDesc D = descs[di];
         const bool moved = D.src_c != D.dst_c || D.src_d != D.dst_d || D.src_o != D.dst_o || src.changes != dst.changes;
-        if (D.inc && !moved) continue;                  // the incremental kernel appends its rows itself
+        if ((D.inc & HM_DINC_ROUTE) && !moved) continue;   // the incremental kernel appends its rows itself
         const bool rm = D.remap_row != 0xFFFFFFFFu;
         const uint8_t *mp = rm ? remap + (size_t)D.remap_row * S : nullptr;
         // old rows: moved (rebased) and/or re-ranked (in place when not moved: row i -> row i)
@@ -298,9 +298,15 @@ __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
     // ops hit); the rest re-merge their whole log
     const hm_doc_result last = a.res_docs[live ? h : 0u];
     const uint32_t tgt = r.n_deps + r.n_changes;
+    // the group / wave passes hold a round in registers (HM_INC_MAX_NEW_C changes, _O ops); a longer
+    // round of a map document of stride <= 16 takes the one-lane-per-document pass, which applies
+    // the changes one after the other (up to HM_INC_LANE_MAX_C / _O: longer still keeps one lane
+    // busy for longer than its re-merge)
+    const bool small = r.n_changes <= HM_INC_MAX_NEW_C && r.n_ops <= HM_INC_MAX_NEW_O && tgt <= HM_INC_MAX_TGT;
+    const bool lane = !small && a.S <= 16 && !((r.flags | m.flags) & HM_DOC_HAS_LISTS) && r.n_changes <= HM_INC_LANE_MAX_C &&
+                      r.n_ops <= HM_INC_LANE_MAX_O;
     bool inc = live && a.incremental && last.status == HM_OK && last.n_queued == 0 && !remapped && r.n_changes > 0 &&
-               r.n_changes <= HM_INC_MAX_NEW_C && r.n_ops <= HM_INC_MAX_NEW_O && tgt <= HM_INC_MAX_TGT &&
-               m.n_r <= r.n_regs && r.n_actors <= a.S;
+               (small || lane) && m.n_r <= r.n_regs && r.n_actors <= a.S;
     bool wave = false;                                             // list ops: the one-document-per-wave pass
     if (inc && a.ist) {
         // what inc_group_kernel would hand straight back (its state checks, and for documents with
@@ -344,7 +350,7 @@ __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
     }
     // cost policy (mode 1): a small list document re-merges in one small-kernel wave
     if (inc && wave && a.incremental == 1u && m.n_o + r.n_ops <= HM_INC_SMALL_LIST_OPS) inc = false;
-    p.inc = inc ? (wave ? 2u : 1u) : 0u;
+    p.inc = inc ? (wave ? 2u : (lane ? 3u : 1u)) : 0u;
     p.remapped = remapped ? 1u : 0u;
     if (live) a.plan[i] = p;
     const unsigned long long im = __ballot(inc);
@@ -399,7 +405,8 @@ __global__ __launch_bounds__(ALLOC_WG) void alloc_kernel(PlanArgs a) {
         m.n_c += r.n_changes; m.n_d += r.n_deps; m.n_o += r.n_ops;
         m.n_r = r.n_regs; m.n_objs = r.n_objs; m.n_actors = r.n_actors; m.flags |= r.flags;
         D.n_r = m.n_r; D.n_actors = m.n_actors; D.n_objs = m.n_objs; D.o_cap = m.o_cap;
-        D.inc = (uint16_t)p.inc;
+        D.inc = (uint16_t)(p.inc | (p.inc && (m.pad[0] & HM_DDOC_MINC) ? HM_DINC_MINC : 0u) |
+                           (p.inc && (m.flags & HM_DOC_HAS_LISTS) ? HM_DINC_LISTS : 0u));
         a.descs[i] = D;
         a.dm[h] = m;
         cold = !p.inc;                                   // the re-merge list (handles)

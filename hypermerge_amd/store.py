@@ -244,6 +244,12 @@ class DocStore:
         self._check(self._L.hm_store_last_routing(self._h, _p(out)), "hm_store_last_routing")
         return {"incremental": int(out[0]), "remerged": int(out[1]), "handed_back": int(out[2])}
 
+    def last_kernel_ms(self) -> Dict[str, float]:
+        """Device time of the last submit (HIP events): the incremental kernels and the re-merge."""
+        out = np.zeros(2, np.float32)
+        self._check(self._L.hm_store_last_kernel_ms(self._h, _p(out)), "hm_store_last_kernel_ms")
+        return {"incremental_ms": float(out[0]), "remerge_ms": float(out[1])}
+
     def open(self) -> int:
         h = ctypes.c_uint32()
         self._check(self._L.hm_doc_open(self._h, ctypes.byref(h)), "hm_doc_open")

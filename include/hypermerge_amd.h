@@ -353,6 +353,10 @@ int hm_store_set_incremental(hm_store *s, int on);
 /* Routing of the last submit: out3 = {incremental, re-merged, incremental handed back to
  * the re-merge}. */
 int hm_store_last_routing(const hm_store *s, uint32_t *out3);
+/* Device time of the last submit, from HIP events on the engine stream: out2[0] = the
+ * incremental kernels (lane / group / wave passes), out2[1] = the re-merge of the documents
+ * they did not take (row build, merge kernels, metadata), in ms. */
+int hm_store_last_kernel_ms(const hm_store *s, float *out2);
 
 /* Sizes of a document's log and merged state. */
 typedef struct {

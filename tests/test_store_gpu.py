@@ -15,6 +15,7 @@ from hypermerge_amd.store import DocStore
 import oracle.oracle as O
 
 from kat_cases import ch, s, d, ins, mk, link
+from hypermerge_amd.columnar import ROOT_ID as R
 
 pytestmark = pytest.mark.gpu
 
@@ -236,6 +237,15 @@ def test_bad_remap_leaves_store_unchanged(engine):
     ("C4", 200, {}, 8, 0.9, 8),                            # up to 8 changes per call: some documents handed to the wave kernel
     ("C3", 40, {"changes_per_actor": 240}, 2, 0.9, 8),     # text: inserts / deletes on the resident element order
     ("C3", 20, {"changes_per_actor": 30, "arrival": 2, "shuffle_pct": 20}, 3, True, 8),   # text, shuffled arrivals
+    # rounds longer than the group passes hold (> 8 changes or > 64 ops): the one-lane pass
+    ("C4", 200, {}, 16, 0.9, 8),
+    ("C2", 150, {}, 24, 0.9, 8),                           # counters, up to 24 changes per call
+    ("FC", 60, {}, 16, True, 8),                           # integral / f64 counters, shuffled arrivals
+    ("C4", 120, {}, 16, 0.9, 16),
+    # nested maps created as the documents go (makeMap / makeTable + link): object creation applies
+    # incrementally on both passes
+    ("NM", 120, {}, 2, 0.8, 8),
+    ("NM", 120, {}, 12, 0.8, 8),
 ])
 def test_incremental_apply_equals_full_remerge(engine, name, n, extra, hi, expect_inc, S):
     """applyRemoteChanges with 1..hi new changes per document per call
@@ -245,6 +255,8 @@ def test_incremental_apply_equals_full_remerge(engine, name, n, extra, hi, expec
     if name == "FC":
         from test_gpu_parity import _float_counter_docs
         docs = _float_counter_docs(n, 31)
+    elif name == "NM":
+        docs = _nested_map_docs(n, 5)
     else:
         b = synth.generate(synth.config(name, n_docs=n, **extra))
         docs = [decode_doc(b, i) for i in range(b.n_docs)]
@@ -292,6 +304,47 @@ def test_incremental_apply_equals_full_remerge(engine, name, n, extra, hi, expec
     if isinstance(expect_inc, float):           # the share of calls applied incrementally
         assert routed["incremental"] >= expect_inc * sum(routed.values()), routed
     print(name, extra, routed)
+
+
+def _nested_map_docs(n_docs, seed, n_actors=4):
+    """Documents of maps and tables created as they go (makeMap / makeTable + link into ROOT or into
+    an earlier map) and sets / deletes / counters on them, in generation order: every change is
+    causally ready on arrival, so object creation is the only thing the incremental passes have to
+    take beyond map ops."""
+    import random
+    rng = random.Random(seed)
+    docs = []
+    for di in range(n_docs):
+        actors = [f"nm{di:04d}{i}" for i in range(n_actors)]
+        seqs = {a: 0 for a in actors}
+        heard = {a: {} for a in actors}
+        objs = [R]
+        chs = []
+        for i in range(rng.randint(10, 50)):
+            a = rng.choice(actors)
+            seqs[a] += 1
+            ops = []
+            if rng.random() < 0.3 and len(objs) < 40:
+                o = f"{di:08x}-{len(objs):04x}-4000-8000-{rng.randrange(16 ** 12):012x}"
+                ops.append(mk("makeTable" if rng.random() < 0.2 else "makeMap", o))
+                ops.append(link(f"k{rng.randrange(4)}", o, rng.choice(objs)))
+                objs.append(o)
+            for _ in range(rng.randint(1, 3)):
+                obj = rng.choice(objs)
+                r = rng.random()
+                if r < 0.15:
+                    ops.append(d(f"k{rng.randrange(4)}", obj))
+                elif r < 0.25:
+                    ops.append({"action": "set", "obj": obj, "key": "n", "value": rng.randint(0, 9), "datatype": "counter"})
+                else:
+                    ops.append(s(f"k{rng.randrange(4)}", rng.randrange(100), obj))
+            deps = {b: q for b, q in heard[a].items() if b != a}
+            chs.append(ch(a, seqs[a], deps, *ops))
+            for b in actors:
+                if b == a or rng.random() < 0.6:
+                    heard[b][a] = seqs[a]
+        docs.append(chs)
+    return docs
 
 
 def _growing_conflicts(n_cycles, actors=("a1", "a2", "a3", "a4", "a5", "a6", "a7", "a8")):
