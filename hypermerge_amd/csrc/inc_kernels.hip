@@ -323,31 +323,36 @@ __device__ void list_indices(const Grp<64> &g, const AppendDesc &D, const IncArg
     }
 }
 
+// the new rows of a document whose segments did not move, from the submit's staged tables
+// (batch-local offsets) to the log, rebased (append_kernel skips such documents)
 template <int G>
-__device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 *smt, uint32_t *lscr) {
+__device__ __forceinline__ void inc_append(const Grp<G> &g, const AppendDesc &D, const IncArgs &A) {
+    const uint32_t gl = g.gl, nnc = D.n_new_c, nno = D.n_new_o, nnd = D.n_new_d;
+    for (uint32_t i = gl; i < nnc; i += G) {
+        hm_change_row c = A.st_changes[D.new_c + i];
+        c.dep_off = D.dst_d + D.n_old_d + (c.dep_off - D.new_d);
+        c.op_first = D.dst_o + D.n_old_o + (c.op_first - D.new_o);
+        A.changes[D.dst_c + D.n_old_c + i] = c;
+    }
+    for (uint32_t i = gl; i < nnd; i += G) A.deps[D.dst_d + D.n_old_d + i] = A.st_deps[D.new_d + i];
+    const uint4 *so4 = reinterpret_cast<const uint4 *>(A.st_ops + D.new_o);
+    uint4 *do4 = reinterpret_cast<uint4 *>(A.ops + D.dst_o + D.n_old_o);
+    for (uint32_t i = gl; i < 2 * nno; i += G) do4[i] = so4[i];
+}
+
+template <int G>
+__device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 *smt, uint32_t *lscr, bool appended = false) {
     const Grp<G> g;
     const uint32_t gl = g.gl;
     const uint32_t S = A.S, h = D.handle, NA = D.n_actors, nnc = D.n_new_c, nno = D.n_new_o, nnd = D.n_new_d;
     constexpr int FAILG = G < 64 ? INC_DEFER : INC_BAIL;     // a limit of this group size only
     constexpr uint32_t KT = G >= 32 ? 1u : 32u / G;           // the log's last KT * G rows are searched first
-    // the new rows, from the submit's staged tables (batch-local offsets): a document whose
-    // segments did not move gets them appended here (append_kernel skips it), rebased — before
+    // the new rows: a document whose segments did not move gets them appended here — before
     // anything can hand the document over, since the re-merge reads them from the log
     const bool moved = D.src_c != D.dst_c || D.src_d != D.dst_d || D.src_o != D.dst_o;
-    if (!moved) {
-        for (uint32_t i = gl; i < nnc; i += G) {
-            hm_change_row c = A.st_changes[D.new_c + i];
-            c.dep_off = D.dst_d + D.n_old_d + (c.dep_off - D.new_d);
-            c.op_first = D.dst_o + D.n_old_o + (c.op_first - D.new_o);
-            A.changes[D.dst_c + D.n_old_c + i] = c;
-        }
-        for (uint32_t i = gl; i < nnd; i += G) A.deps[D.dst_d + D.n_old_d + i] = A.st_deps[D.new_d + i];
-        const uint4 *so4 = reinterpret_cast<const uint4 *>(A.st_ops + D.new_o);
-        uint4 *do4 = reinterpret_cast<uint4 *>(A.ops + D.dst_o + D.n_old_o);
-        for (uint32_t i = gl; i < 2 * nno; i += G) do4[i] = so4[i];
-    }
-    if (nnc == 0 || nnc > NC || NA > S || S > G || D.n_old_r > D.n_r) return INC_BAIL;
-    if (nno > G || nnd > G) return FAILG;
+    if (!moved && !appended) inc_append<G>(g, D, A);
+    if (nnc == 0 || NA > S || S > G || D.n_old_r > D.n_r) return INC_BAIL;
+    if (nnc > NC || nno > G || nnd > G) return FAILG;       // (the tiled wave pass takes longer rounds)
 
     // ---- level 2: everything that depends only on the descriptor ----
     const IncState I = A.ist[h];
@@ -769,7 +774,57 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
     return INC_DONE;
 }
 
+// A round longer than a group holds (more than NC changes, G ops or G dep rows) is applied in
+// tiles: every row is appended first, then each tile — the most whole changes that fit — runs as a
+// round of its own on the state the previous tile left (the rows before it are old rows to it).
+// A tile after the first that cannot go incremental sends the document to the re-merge, which
+// rewrites every row the earlier tiles wrote.
 template <int G>
+__device__ int inc_doc_tiled(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 *smt, uint32_t *lscr) {
+    const Grp<G> g;
+    const uint32_t gl = g.gl;
+    // (one call site of inc_doc: a second inlined copy costs the common round its occupancy)
+    const bool tiled = D.n_new_c > NC || D.n_new_o > (uint32_t)G || D.n_new_d > (uint32_t)G;
+    if (tiled && !(D.src_c != D.dst_c || D.src_d != D.dst_d || D.src_o != D.dst_o)) inc_append<G>(g, D, A);
+    AppendDesc T = D;
+    uint32_t c0 = 0, d0 = 0, o0 = 0;
+    for (bool first = true;; first = false) {
+        uint32_t k = D.n_new_c, to = D.n_new_o, td = D.n_new_d;
+        if (tiled) {
+            // the tile: changes c0 .. c0 + k - 1, at most NC of them with at most G ops and G dep rows
+            uint32_t no = 0, nd = 0;
+            if (gl < NC && c0 + gl < D.n_new_c) {
+                const hm_change_row c = A.st_changes[D.new_c + c0 + gl];
+                no = c.n_ops; nd = c.n_deps;
+            }
+            uint32_t so = no, sd = nd;
+#pragma unroll
+            for (uint32_t d = 1; d < NC; d <<= 1) {
+                const uint32_t yo = g.up(so, d), yd = g.up(sd, d);
+                if (gl >= d && gl < NC) { so += yo; sd += yd; }
+            }
+            k = (uint32_t)__popcll(g.bits(gl < NC && c0 + gl < D.n_new_c && so <= (uint32_t)G && sd <= (uint32_t)G));
+            if (k == 0) return INC_BAIL;                      // a change larger than a group: the re-merge
+            to = g.sh(so, k - 1); td = g.sh(sd, k - 1);
+            T.new_c = D.new_c + c0; T.n_new_c = k; T.new_d = D.new_d + d0; T.n_new_d = td; T.new_o = D.new_o + o0; T.n_new_o = to;
+            T.n_old_c = D.n_old_c + c0; T.n_old_d = D.n_old_d + d0; T.n_old_o = D.n_old_o + o0;
+            if (!first) {
+                T.src_c = D.dst_c; T.src_d = D.dst_d; T.src_o = D.dst_o; T.src_r = D.dst_r;
+                T.n_old_r = D.n_r;                            // (the first tile wrote every new register's row)
+            }
+        }
+        const int rc = inc_doc<G>(T, A, ssv, smt, lscr, tiled);
+        if (rc != INC_DONE) return first ? rc : INC_BAIL;
+        c0 += k; d0 += td; o0 += to;
+        if (c0 >= D.n_new_c) return INC_DONE;
+        __threadfence_block();                                // this tile's rows, then the next tile's reads
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// TL: the launch for rounds that need tiles (a separate instantiation: the tile loop around
+// inc_doc costs the common round's register allocation half its occupancy)
+template <int G, bool TL>
 __global__ __launch_bounds__(256) void inc_group_kernel(IncArgs A) {
     constexpr uint32_t NG = 256 / G;
     __shared__ uint4 s_sv[NG][2 * G];
@@ -782,7 +837,11 @@ __global__ __launch_bounds__(256) void inc_group_kernel(IncArgs A) {
         const AppendDesc D = A.descs[di];
         const uint32_t route = D.inc & HM_DINC_ROUTE;
         if (!route || route == 3 || (G < 64 && route == 2)) continue;   // (2: listed for the wave pass, 3: the lane pass)
-        const int rc = inc_doc<G>(D, A, s_sv[grp], s_mt[grp], s_ls[G == 64 ? grp : 0]);
+        const bool tl = D.n_new_c > NC || D.n_new_o > (uint32_t)G || D.n_new_d > (uint32_t)G;
+        if (G == 64 && tl != TL) continue;                             // (the other launch's document)
+        int rc;
+        if constexpr (TL) rc = inc_doc_tiled<G>(D, A, s_sv[grp], s_mt[grp], s_ls[G == 64 ? grp : 0]);
+        else rc = inc_doc<G>(D, A, s_sv[grp], s_mt[grp], s_ls[G == 64 ? grp : 0]);
         if (rc != INC_DONE && gl == 0) {
             if (rc == INC_DEFER && A.defer) A.defer[1 + atomicAdd(&A.defer[0], 1u)] = di;
             else A.bail[1 + atomicAdd(&A.bail[0], 1u)] = D.handle;
@@ -808,7 +867,7 @@ __global__ __launch_bounds__(256) void inc_group_kernel(IncArgs A) {
 //   the only exits are a register of more than LSV survivors, a full slot area or a fold source
 //   missing from the log — the document is then re-merged, which rewrites every row the lane
 //   wrote (the new rows are in the log before anything else happens).
-constexpr uint32_t LSV = 4;    // survivors of a register the lane path holds (more: re-merge)
+constexpr uint32_t LSV = 8;    // survivors of a register the lane path holds (more: re-merge)
 constexpr uint32_t LKF = 2;    // fold sources resolved and loaded together
 
 // v[i] of a register array by selects (each element made opaque first: a select between two
@@ -966,11 +1025,30 @@ __device__ int inc_lane(const AppendDesc &D, const IncArgs &A) {
 #pragma unroll 4
         for (uint32_t i = 0; i < 2 * nno; i++) do4[i] = so4[i];
     }
-    // a moved segment: the group pass copies the per-change / survivor / register rows along
-    if (rows_moved || D.src_r != D.dst_r) return INC_DEFER;
     if (nnc == 0 || NA > (uint32_t)S || D.n_old_r > D.n_r) return INC_BAIL;
     const IncState I = A.ist[h];
-    if ((I.flags & (HM_IST_VALID | HM_IST_NOCKEY)) != HM_IST_VALID) return INC_BAIL;
+    if ((I.flags & (HM_IST_VALID | HM_IST_NOCKEY | HM_IST_LIST)) != HM_IST_VALID) return INC_BAIL;
+    // segments the append moved (append_kernel copied the log rows, the new ones included): the
+    // per-change, survivor and register rows follow
+    if (D.src_c != D.dst_c) {
+#pragma unroll 4
+        for (uint32_t i = 0; i < D.n_old_c; i++) { A.hist[D.dst_c + i] = A.hist[D.src_c + i]; A.ckey[D.dst_c + i] = A.ckey[D.src_c + i]; }
+        const uint4 *sa = reinterpret_cast<const uint4 *>(A.all_deps + (size_t)D.src_c * S);
+        uint4 *da = reinterpret_cast<uint4 *>(A.all_deps + (size_t)D.dst_c * S);
+#pragma unroll 4
+        for (uint32_t w = 0; w < D.n_old_c * (uint32_t)(S / 4); w++) da[w] = sa[w];
+    }
+    if (D.src_o != D.dst_o) {
+#pragma unroll 4
+        for (uint32_t i = 0; i < I.s_used; i++) {
+            *reinterpret_cast<uint4 *>(A.surv + D.dst_o + i) = *reinterpret_cast<const uint4 *>(A.surv + D.src_o + i);
+            A.smeta[D.dst_o + i] = A.smeta[D.src_o + i];
+        }
+    }
+    if (D.src_r != D.dst_r) {
+#pragma unroll 4
+        for (uint32_t i = 0; i < D.n_old_r; i++) A.regs[D.dst_r + i] = A.regs[D.src_r + i];
+    }
     const bool lists = (D.inc & HM_DINC_LISTS) != 0;
     const hm_doc_result R0 = A.res_docs[h];
     uint32_t ck[S], hd[S];
@@ -1335,24 +1413,28 @@ hipError_t hm_launch_inc_apply(const IncArgs &A, hipStream_t s) {
     hipError_t z = hipMemsetAsync(A.bail, 0, 4, s);
     if (z != hipSuccess) return z;
     auto grid = [](uint32_t n, uint32_t per) { const uint32_t g = (n + per - 1) / per; return g < 65535u ? g : 65535u; };
-    if (S <= 16) {
+    if (S <= 16 && A.n_lane) {
         // rounds longer than the group passes hold (route 3): one lane per document, first
         const uint32_t gl = (A.n + 255) / 256;
         if (S <= 8) hipLaunchKernelGGL(hmi::inc_lane_kernel<8>, dim3(gl), dim3(256), 0, s, A);
         else hipLaunchKernelGGL(hmi::inc_lane_kernel<16>, dim3(gl), dim3(256), 0, s, A);
     }
-    if (S <= 8) hipLaunchKernelGGL(hmi::inc_group_kernel<8>, dim3(grid(A.n, 32)), dim3(256), 0, s, A);
-    else if (S <= 16) hipLaunchKernelGGL(hmi::inc_group_kernel<16>, dim3(grid(A.n, 16)), dim3(256), 0, s, A);
+    if (S <= 8) hipLaunchKernelGGL((hmi::inc_group_kernel<8, false>), dim3(grid(A.n, 32)), dim3(256), 0, s, A);
+    else if (S <= 16) hipLaunchKernelGGL((hmi::inc_group_kernel<16, false>), dim3(grid(A.n, 16)), dim3(256), 0, s, A);
     if (S <= 16 && A.defer) {
-        // the documents handed over, one per wave (their count is read on the device)
+        // the documents handed over, one per wave (their count is read on the device); rounds that
+        // need tiles in a launch of their own
         IncArgs B = A;
         B.list = A.defer;
         B.defer = nullptr;
-        hipLaunchKernelGGL(hmi::inc_group_kernel<64>, dim3(grid(A.n, 4) < 1024u ? grid(A.n, 4) : 1024u), dim3(256), 0, s, B);
+        const uint32_t gw = grid(A.n, 4) < 1024u ? grid(A.n, 4) : 1024u;
+        hipLaunchKernelGGL((hmi::inc_group_kernel<64, false>), dim3(gw), dim3(256), 0, s, B);
+        hipLaunchKernelGGL((hmi::inc_group_kernel<64, true>), dim3(gw), dim3(256), 0, s, B);
     } else if (S > 16) {
         IncArgs B = A;
         B.defer = nullptr;
-        hipLaunchKernelGGL(hmi::inc_group_kernel<64>, dim3(grid(A.n, 4)), dim3(256), 0, s, B);
+        hipLaunchKernelGGL((hmi::inc_group_kernel<64, false>), dim3(grid(A.n, 4)), dim3(256), 0, s, B);
+        hipLaunchKernelGGL((hmi::inc_group_kernel<64, true>), dim3(grid(A.n, 4) < 1024u ? grid(A.n, 4) : 1024u), dim3(256), 0, s, B);
     }
     return hipGetLastError();
 }

@@ -600,7 +600,7 @@ static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handl
             IA.regs = s->regs; IA.surv = s->surv; IA.smeta = s->smeta; IA.res_docs = s->res_docs;
             IA.epos = s->epos; IA.epar = s->epar; IA.ekey = s->ekey; IA.lorder = s->lorder; IA.ldir = s->ldir;
             IA.clock = s->clock; IA.back_clock = s->back_clock; IA.heads = s->heads; IA.min_clock = s->min_clock;
-            IA.ist = s->ist; IA.bail = bail; IA.defer = (uint32_t *)(sp + L.o_defer);
+            IA.ist = s->ist; IA.bail = bail; IA.defer = (uint32_t *)(sp + L.o_defer); IA.n_lane = P.mx[0];
             dbg_list_state(s, "before");
             SCHK(s, hm_launch_inc_apply(IA, st));
             dbg_list_state(s, "after");

@@ -44,7 +44,7 @@ struct PlanRow {
 struct PlanStats {
     uint32_t err;                              // HM_PLAN_* bits of the failed checks
     uint32_t n_inc, n_cold, n_back, n_app;       // (n_app: batch rows append_kernel has work for)
-    uint32_t mx[6];                            // incremental tile maxima (hm_inc_dims)
+    uint32_t mx[6];                            // mx[0]: documents routed to the lane pass (the rest unused)
     uint32_t max_c, max_o, max_r, max_objs, max_d, flags;   // launch hints of a merge list
     unsigned long long need[4];                // rows the submit's growing segments take, per space
     unsigned long long bump[4];                // arena bump pointers (device-side segment allocation)
@@ -124,6 +124,7 @@ struct IncArgs {
     IncState *ist;
     uint32_t *bail;                            // [0] count, [1..] handles re-merged
     uint32_t *defer;                           // [0] count, [1..] desc indices for the wave kernel (NULL: bail)
+    uint32_t n_lane;                           // documents routed to the lane pass (0: no launch)
 };
 
 // AppendDesc.inc: the route (bits 0-1: 0 re-merge, 1 incremental group pass, 2 wave pass, 3 lane pass) and what
@@ -138,6 +139,8 @@ struct IncArgs {
 #define HM_INC_MAX_TGT 128       // transitiveDeps fold steps of a submit's new changes (2 per lane, wave kernel)
 #define HM_INC_LANE_MAX_C 64     // the one-lane pass (map documents, strides <= 16)
 #define HM_INC_LANE_MAX_O 512
+#define HM_INC_TILED_MAX_C 256    // tiles of the group / wave passes (list documents, strides over 16)
+#define HM_INC_TILED_MAX_O 4096
 
 struct PlanArgs {
     const hm_doc_row *docs;

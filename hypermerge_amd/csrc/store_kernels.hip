@@ -236,10 +236,12 @@ __device__ __forceinline__ uint32_t pow2c(uint32_t x) {
 __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
     __shared__ unsigned long long s_need[4][PLAN_WG / 64];
     __shared__ uint32_t s_inc[PLAN_WG / 64];
+    __shared__ uint32_t s_lane[PLAN_WG / 64];
     const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
     if (ln == 0) {
         for (int k = 0; k < 4; k++) s_need[k][wv] = 0;
         s_inc[wv] = 0;
+        s_lane[wv] = 0;
     }
     const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
     const bool live = i0 < a.n;
@@ -298,15 +300,18 @@ __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
     // ops hit); the rest re-merge their whole log
     const hm_doc_result last = a.res_docs[live ? h : 0u];
     const uint32_t tgt = r.n_deps + r.n_changes;
-    // the group / wave passes hold a round in registers (HM_INC_MAX_NEW_C changes, _O ops); a longer
-    // round of a map document of stride <= 16 takes the one-lane-per-document pass, which applies
-    // the changes one after the other (up to HM_INC_LANE_MAX_C / _O: longer still keeps one lane
-    // busy for longer than its re-merge)
+    // the group / wave passes hold a round in registers (HM_INC_MAX_NEW_C changes, _O ops) and take
+    // a longer one in tiles of that size; a longer round of a map document of stride <= 16 takes the
+    // one-lane-per-document pass, which applies the changes one after the other (up to
+    // HM_INC_LANE_MAX_C / _O, HM_INC_TILED_MAX_C / _O in tiles: longer still keeps one lane / wave
+    // busy for longer than the document's re-merge)
+    const bool lists = ((r.flags | m.flags) & HM_DOC_HAS_LISTS) != 0;
     const bool small = r.n_changes <= HM_INC_MAX_NEW_C && r.n_ops <= HM_INC_MAX_NEW_O && tgt <= HM_INC_MAX_TGT;
-    const bool lane = !small && a.S <= 16 && !((r.flags | m.flags) & HM_DOC_HAS_LISTS) && r.n_changes <= HM_INC_LANE_MAX_C &&
-                      r.n_ops <= HM_INC_LANE_MAX_O;
+    const bool lane = !small && a.S <= 16 && !lists && r.n_changes <= HM_INC_LANE_MAX_C && r.n_ops <= HM_INC_LANE_MAX_O;
+    const bool longr = lane || (!small && (lists || a.S > 16) && r.n_changes <= HM_INC_TILED_MAX_C &&
+                                r.n_ops <= HM_INC_TILED_MAX_O);     // (tiles of the group / wave passes)
     bool inc = live && a.incremental && last.status == HM_OK && last.n_queued == 0 && !remapped && r.n_changes > 0 &&
-               (small || lane) && m.n_r <= r.n_regs && r.n_actors <= a.S;
+               (small || longr) && m.n_r <= r.n_regs && r.n_actors <= a.S;
     bool wave = false;                                             // list ops: the one-document-per-wave pass
     if (inc && a.ist) {
         // what inc_group_kernel would hand straight back (its state checks, and for documents with
@@ -353,11 +358,11 @@ __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
     p.inc = inc ? (wave ? 2u : (lane ? 3u : 1u)) : 0u;
     p.remapped = remapped ? 1u : 0u;
     if (live) a.plan[i] = p;
-    const unsigned long long im = __ballot(inc);
-    if (ln == 0) s_inc[wv] = (uint32_t)__popcll(im);
+    const unsigned long long im = __ballot(inc), lm = __ballot(inc && p.inc == 3u);
+    if (ln == 0) { s_inc[wv] = (uint32_t)__popcll(im); s_lane[wv] = (uint32_t)__popcll(lm); }
     }
     __syncthreads();
-    if (threadIdx.x < 5) {                                         // one lane per reduced value
+    if (threadIdx.x < 6) {                                         // one lane per reduced value
         const uint32_t k = threadIdx.x, nw = PLAN_WG / 64;
         if (k < 4) {
             unsigned long long g = 0;
@@ -365,8 +370,8 @@ __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
             if (g) atomicAdd(&a.st->need[k], g);
         } else {
             uint32_t c = 0;
-            for (uint32_t w = 0; w < nw; w++) c += s_inc[w];
-            if (c) atomicAdd(&a.st->n_inc, c);
+            for (uint32_t w = 0; w < nw; w++) c += k == 4 ? s_inc[w] : s_lane[w];
+            if (c) atomicAdd(k == 4 ? &a.st->n_inc : &a.st->mx[0], c);
         }
     }
 }

@@ -242,6 +242,10 @@ def test_bad_remap_leaves_store_unchanged(engine):
     ("C2", 150, {}, 24, 0.9, 8),                           # counters, up to 24 changes per call
     ("FC", 60, {}, 16, True, 8),                           # integral / f64 counters, shuffled arrivals
     ("C4", 120, {}, 16, 0.9, 16),
+    # ... and in tiles of the group / wave passes: list and text documents, strides over 16
+    ("C3", 20, {"changes_per_actor": 120}, 20, True, 8),       # (new actors mid-way re-rank: re-merge)
+    ("C5", 100, {}, 12, True, 8),
+    ("C2", 80, {}, 24, 0.9, 64),
     # nested maps created as the documents go (makeMap / makeTable + link): object creation applies
     # incrementally on both passes
     ("NM", 120, {}, 2, 0.8, 8),
