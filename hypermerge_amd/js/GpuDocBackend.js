@@ -639,10 +639,12 @@ class GpuEngine {
 // patch into the current one, in the Automerge 0.12 diff vocabulary (SURVEY.md Appendix A.4):
 // {action:'create', obj, type}, {action:'set'|'remove', type:'map'|'table', obj, key, value,
 // link?, datatype?, conflicts?}, {action:'insert'|'set'|'remove', type:'list'|'text', obj,
-// index, elemId?, value, ...}: one diff per register whose rendered value changed (map keys in
-// the order the round's ops first hit them; per list removals, insertions, value changes).
-// The document a frontend builds from them equals the merged state; the exact per-op
-// sequence of Automerge is unpinned (Automerge 0.12 is not available here).
+// index, elemId?, value, ...}.  By default one diff per applied op, in application order (the
+// sequence Automerge's applyChanges emits, Appendix A.4; the docset replays the round's ops over
+// the patch base, csrc/docset.cpp Replay); with the docset's net-diff option (HM_DOCSET_NET_DIFFS)
+// one diff per register whose rendered value changed instead.  The document a frontend builds
+// from either equals the merged state; Automerge 0.12's own diff field set is unpinned (it is not
+// available here).
 
 // the merged document as {objUuid -> {type, keys: Map(key -> entry), elems: [[elemId, entry]]}}
 function materialize(state) {

@@ -155,3 +155,48 @@ def test_cursor_update_is_all_or_nothing(engine):
     assert cs.get_many("r", ["d1", "d2"]) == before
     cs.update("r", "d1", {"c": 4})
     assert cs.get("r", "d1") == {"a": 1, "b": 2, "c": 4}
+
+
+def test_cursorstore_batches_replay_to_reference_tables(engine):
+    """Row f3: the Node CursorStore's writes leave as one persistence batch per call (takeBatch:
+    ['upsert', repoId, docId, actorId, boundedSeq] per entry handed to update, in order); replayed
+    into sqlite3 with the reference's upsert statement (src/CursorStore.ts:31-36) the table after
+    every round equals the reference SQL's after the same update calls, and the device rows
+    (get) equal it at the end."""
+    import json
+    import os
+    import shutil
+    import subprocess
+    node = shutil.which("node")
+    if node is None:
+        pytest.skip("node not installed")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    rng = np.random.default_rng(9)
+    docs = [f"doc{i:02d}" for i in range(30)]
+    actors = [f"actor-{i}" for i in range(12)] + ["é☃", "00"]
+    vals = [0, 1, 2, 3, 7, 40, -3, "Infinity", INFINITY_SEQ, INFINITY_SEQ + 10]
+    rounds = []
+    for _ in range(8):
+        r = {}
+        for d in rng.choice(docs, size=12, replace=False):
+            r[str(d)] = {str(a): vals[int(rng.integers(len(vals)))] for a in rng.choice(actors, size=int(rng.integers(1, 5)), replace=False)}
+        rounds.append(r)
+    p = subprocess.run([node, os.path.join(root, "tests", "js", "run_cursor_batches.js")],
+                       input=json.dumps({"rounds": rounds, "docs": docs}), capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    got = json.loads(p.stdout)
+    ref, db = SqlCursors(), SqlCursors()
+    table = "SELECT repoId, documentId, actorId, seq FROM Cursors ORDER BY repoId, documentId, actorId"
+    for r, (calls, batch) in enumerate(zip(rounds, got["batches"])):
+        for d, c in calls.items():
+            ref.update("repo", d, {a: (math.inf if s == "Infinity" else s) for a, s in c.items()})
+        assert len(batch) == sum(len(c) for c in calls.values())
+        for kind, repo, d, a, s in batch:                 # one transaction per batch
+            assert kind == "upsert" and repo == "repo" and 0 <= s <= INFINITY_SEQ
+            db.db.execute("INSERT INTO Cursors (repoId, documentId, actorId, seq) VALUES (?, ?, ?, ?) "
+                          "ON CONFLICT (repoId, documentId, actorId) DO UPDATE SET seq = excluded.seq "
+                          "WHERE excluded.seq > seq", (repo, d, a, s))
+        db.db.commit()
+        assert db.db.execute(table).fetchall() == ref.db.execute(table).fetchall(), r
+    for d, g in zip(docs, got["get"]):
+        assert dict(g) == ref.get("repo", d), d

@@ -194,3 +194,27 @@ def test_tables_independent_of_thread_count_with_failed_documents():
             np.testing.assert_array_equal(getattr(b, f), getattr(ref, f), err_msg=f"{f} threads={threads}")
         assert b.strings == ref.strings
         assert b.doc_actors == ref.doc_actors and b.doc_objs == ref.doc_objs and b.doc_regs == ref.doc_regs
+
+
+def test_reference_jsonbuffer_vectors():
+    """Blocks written by the reference's own JsonBuffer.bufferify and their JsonBuffer.parse
+    values (tests/golden/jsonbuffer_vectors.json, tools/golden/gen_jsonbuffer_vectors.js over
+    dist/JsonBuffer.js): the native decoder's rows encode exactly the reference-parsed changes
+    (every value kind: -0, 1e21, 2^53 +- 2, denormals, escapes, surrogate pairs, counters,
+    timestamps, lists); blocks JsonBuffer.parse throws on, and blocks whose first two bytes are
+    neither '{"' nor 'BR' (Block.unpack's switch, src/Block.ts:20-27), fail their document only."""
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "jsonbuffer_vectors.json")))
+    raw = [[base64.b64decode(v["block"]) for v in doc] for doc in gold["valid"]]
+    parsed = [[json.loads(v["parsed"]) for v in doc] for doc in gold["valid"]]
+    b, status = decode_blocks(raw, threads=2)
+    assert (status == 0).all(), status
+    for d, chs in enumerate(parsed):
+        want = decode_doc(encode([chs]), 0)
+        assert decode_doc(b, d) == want, d
+    bad = [[base64.b64decode(m["block"])] for m in gold["malformed"]]
+    bad += [[base64.b64decode(x)] for x in gold["bad_header"]]
+    ok_doc = [base64.b64decode(v["block"]) for v in gold["valid"][1]]
+    b2, st2 = decode_blocks(bad + [ok_doc], threads=2)
+    assert all(m["throws"] for m in gold["malformed"])
+    assert (st2[:-1] != 0).all(), st2
+    assert st2[-1] == 0 and decode_doc(b2, len(bad)) == decode_doc(encode([parsed[1]]), 0)
