@@ -37,6 +37,14 @@ WORKLOAD_KIND = {"C1": "map sets, 2 alternating actors", "C2": "map LWW sets + c
                  "C5": "nested maps/lists, conflicts, deletes, causally blocked + duplicate changes"}
 
 
+_T0 = time.time()
+
+
+def _progress(msg: str) -> None:
+    """A progress line on stderr (the JSON line stays alone on stdout): long runs keep writing."""
+    print(f"[bench {time.time() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def _dist():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -152,6 +160,7 @@ def main() -> int:
     cfg = synth.config(args.config, n_docs=args.docs, shard=rank, n_shards=ws, **over)
     batch = synth.generate(cfg, threads=min(16, os.cpu_count() or 1))
     gen_s = time.time() - t0
+    _progress(f"generated {args.config} shard: {batch.n_docs} docs in {gen_s:.1f}s")
 
     eng = Engine(local)
     stream = torch.cuda.Stream(dev)          # a real stream: the C-ABI treats handle 0 as "engine stream"
@@ -174,6 +183,7 @@ def main() -> int:
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t_start
+    _progress(f"timed steps: {wall * 1e3 / args.steps:.3f} ms/step")
     ev_ms = ev0.elapsed_time(ev1)
     # per-launch kernel durations (both kernels): HIP events on the launch stream, extra launches
     kern = run.kernel_roofline(max(3, min(args.steps, 10)))
@@ -217,6 +227,7 @@ def main() -> int:
         g = eng.merge(sub)
         o = O.merge(sub, threads=min(16, os.cpu_count() or 1))
         parity = bool(_same(sub, g, o))
+        _progress(f"oracle parity sample: {parity}")
     if rank == 0 and ws == 1 and not args.no_cpu:          # CPU legs: rank 0 at N=1 only
         import oracle.oracle as O
         ns = min(args.cpu_sample_docs, nd)
@@ -236,6 +247,7 @@ def main() -> int:
                   "reason": (f"a one-GPU box grants {nth} host threads (its CPU share; os.cpu_count() = "
                                    f"{os.cpu_count()} counts the whole host); per-document merges are independent, "
                                    "so the rate scales with the share")}
+        _progress("cpu baseline legs done")
 
     # end to end: host tables -> device -> merge -> host results (hm_merge_host, PCIe included);
     # reported beside the kernel rate, never as `value`
@@ -265,6 +277,7 @@ def main() -> int:
                          "same_results": ok,
                          "path": "hm_merge_host, page-locked (torch pin_memory) host tables and reused result arrays"}
         del pb, pr, keep
+        _progress("end-to-end legs done")
     # from raw hypercore blocks: JSON blocks (as Block.pack writes them) -> the native
     # multi-threaded decoder (hm_decode_blocks) -> hm_merge_host; reported beside `value`
     from_blocks = None
@@ -277,9 +290,11 @@ def main() -> int:
     incremental_c5 = None
     if rank == 0 and ws == 1 and not args.no_incremental and args.config == "C4" and args.arrival is None:
         incremental = _incremental(eng, batch, args)
+        _progress("resident C4 leg done")
         # the same event on text documents (C3: RGA inserts / deletes on the resident element order)
         c3 = synth.generate(synth.config("C3", n_docs=args.text_docs), threads=min(16, os.cpu_count() or 1))
         incremental_text = _incremental(eng, c3, args, tail=8, oracle_docs=200)
+        _progress("resident C3 leg done")
         incremental_text["workload"] = f"C3: {c3.n_docs} text docs x 8 actors, the last 8 changes of each in rounds of 1-2"
         del c3
         # nested maps / lists with out-of-order and duplicate delivery (C5): the share the
@@ -291,6 +306,7 @@ def main() -> int:
             incremental_c5["workload"] = (f"C5: {c5.n_docs} nested map / list docs x 4 actors, 20% delivered before "
                                           f"their deps, 3% duplicates; the last 4 changes of each in rounds of 1-2")
             incremental_c5["bail_share"] = 1.0 - incremental_c5["incremental_share"]
+            _progress("resident C5 leg done")
             incremental_c5["policy"] = ("incremental mode 1 (the default): a document with lists and <= 256 ops re-merges "
                                         "(one small-kernel wave either way) and keeps no incremental state")
             del c5
@@ -298,6 +314,7 @@ def main() -> int:
     node = None
     if rank == 0 and ws == 1 and not args.no_node:
         node = _node_e2e(args)
+        _progress("node legs done")
     # the same workload in RepoBackend.loadDocument's arrival order (actor-major concatenation,
     # src/RepoBackend.ts:242-248): changes whose deps come later in the array wait in the queue
     orders = None
@@ -318,6 +335,7 @@ def main() -> int:
         dt = (time.perf_counter() - t) / k_am
         kr = r_am.kernel_roofline(3)
         ap = int(r_am.docs_res["hist_len"].astype(np.int64).sum())
+        _progress("actor-major leg done")
         orders = {"actor_major": {"value": ap / dt, "unit": "changes/s", "ms_per_step": dt * 1e3,
                                   "roofline_frac": kr["frac"], "kernel": kr["kernel"],
                                   "unsupported_docs": int((r_am.docs_res["status"] == 16).sum()),
@@ -327,8 +345,10 @@ def main() -> int:
     traffic = None
     if rank == 0 and ws == 1 and not args.no_traffic:
         traffic = _pmc_traffic(args, kern["kernel"])
+        _progress("merge kernel PMC passes done")
         if incremental and incremental.get("roofline"):
             it = _pmc_inc_traffic(args)
+            _progress("incremental kernel PMC passes done")
             if it:
                 ro = incremental["roofline"]
                 ro["traffic_detail"] = it

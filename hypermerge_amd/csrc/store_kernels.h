@@ -95,6 +95,11 @@ static_assert(sizeof(IncState) == 32, "IncState is 32 B");
 // the cost policy of incremental mode 1: a list document of at most this many ops re-merges (one
 // small-kernel wave, all in LDS) rather than taking the one-document-per-wave incremental pass
 #define HM_INC_SMALL_LIST_OPS 256u
+// ... and a round of more than 1 / HM_INC_COST of the log's rows (changes + ops, the new ones
+// included) re-merges: the per-row cost ratio of the incremental passes to the merge kernels,
+// measured on C4 (profiles/r05/inc: inc_lane_kernel 25.5 ms for a 60-change first load of 1M
+// documents, inc_group_kernel 0.79 ms per 1.5M changes; merge_small_kernel 2.4 ms per 64M)
+#define HM_INC_COST 12u
 __host__ __device__ inline uint32_t hm_ckey(uint32_t actor, uint32_t seq, bool applied) {
     return (seq & 0xFFFFFFu) | ((actor & 0x7Fu) << 24) | (applied ? 0x80000000u : 0u);
 }

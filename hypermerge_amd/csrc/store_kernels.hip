@@ -353,8 +353,15 @@ __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
             }
         }
     }
-    // cost policy (mode 1): a small list document re-merges in one small-kernel wave
+    // cost policy (mode 1): a small list document re-merges in one small-kernel wave; and a round
+    // whose new rows are more than 1 / HM_INC_COST of the log after it re-merges — the merge
+    // kernels take a log row ~HM_INC_COST times faster than the incremental passes take a new
+    // one (C4: 37 ps per change merged vs 0.43-0.53 ns per change applied), so that round is
+    // cheaper re-merged (this also sends a first load into a document re-merged empty to the merge)
     if (inc && wave && a.incremental == 1u && m.n_o + r.n_ops <= HM_INC_SMALL_LIST_OPS) inc = false;
+    if (inc && a.incremental == 1u &&
+        (unsigned long long)HM_INC_COST * (r.n_changes + r.n_ops) > (unsigned long long)m.n_c + m.n_o + r.n_changes + r.n_ops)
+        inc = false;
     p.inc = inc ? (wave ? 2u : (lane ? 3u : 1u)) : 0u;
     p.remapped = remapped ? 1u : 0u;
     if (live) a.plan[i] = p;
