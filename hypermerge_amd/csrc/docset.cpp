@@ -1180,6 +1180,7 @@ struct hm_docset {
     std::mutex open_mu;
     std::atomic<bool> busy{false};
     bool broken = false;                                     // a failed call could not be undone on a store
+    uint64_t routing[3] = {0, 0, 0};                         // document rounds: incremental, re-merged, handed back
     uint64_t stat[8] = {0, 0, 0, 0, 0, 0, 0, 0};           // rounds, docs, restrides, hit-register patches, full patches,
                                                              // per-op patches, replay mismatches, replay checks skipped
     DocSt &doc(uint32_t i) { return chunks[i / CHUNK][i % CHUNK]; }
@@ -1368,6 +1369,11 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
         if ((rc = hm_batch_wait(st, O.id, O.res.data(), O.clock.data(), O.back.data(), O.heads.data()))) break;
         O.sub = false;
         O.done = true;
+        {
+            uint32_t r3[3] = {0, 0, 0};
+            if (hm_store_last_routing(st, r3) == HM_OK)
+                for (int k = 0; k < 3; k++) ds->routing[k] += r3[k];
+        }
         if (n_waited++ == inj_wait) { rc = hm_engine_fail(ds->e, HM_ERR_DEVICE, "injected failure (HM_DOCSET_INJECT_FAIL)"); break; }
         for (uint32_t k = 0; k < rows.size(); k++) {
             Round &x = R[rows[k]];
@@ -1887,6 +1893,12 @@ int hm_docset_handles(const hm_docset *ds, uint32_t a_stride, uint32_t *out_open
     for (uint32_t c = 0; c < N_CLASS; c++)
         if (STRIDES[c] == a_stride) { *out_opened = ds->opened[c]; *out_free = (uint32_t)ds->free_h[c].size(); return HM_OK; }
     return HM_ERR_INVALID;
+}
+
+int hm_docset_routing(const hm_docset *ds, uint64_t *out3) {
+    if (!ds || !out3) return HM_ERR_INVALID;
+    for (int k = 0; k < 3; k++) out3[k] = ds->routing[k];
+    return HM_OK;
 }
 
 int hm_docset_stats(const hm_docset *ds, uint64_t *out8) {

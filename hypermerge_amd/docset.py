@@ -116,6 +116,12 @@ class DocSet:
                            "hm_docset_handles")
         return {"opened": o.value, "free": f.value}
 
+    def routing(self) -> Dict[str, int]:
+        """hm_docset_routing: document rounds by store route so far."""
+        out = np.zeros(3, np.uint64)
+        self.engine._check(self._L.hm_docset_routing(self._h, out.ctypes.data), "hm_docset_routing")
+        return {"incremental": int(out[0]), "remerged": int(out[1]), "handed_back": int(out[2])}
+
     def stats(self) -> Dict[str, int]:
         out = np.zeros(8, np.uint64)
         self.engine._check(self._L.hm_docset_stats(self._h, out.ctypes.data), "hm_docset_stats")

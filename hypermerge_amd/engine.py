@@ -35,7 +35,7 @@ EXPORTS = ("hm_abi_version", "hm_status_message", "hm_engine_create", "hm_engine
            "hm_cursors_entry", "hm_cursors_docs_with_actors", "hm_docset_create", "hm_docset_destroy",
            "hm_docset_engine", "hm_docset_open", "hm_docset_apply", "hm_text_data", "hm_text_results", "hm_text_free",
            "hm_docset_doc_info", "hm_docset_history_prefix", "hm_docset_clock_update", "hm_docset_view",
-           "hm_docset_stats", "hm_docset_handles", "hm_sync_ranges_host", "hm_batch_submit_device", "hm_batch_wait_device",
+           "hm_docset_stats", "hm_docset_routing", "hm_docset_handles", "hm_sync_ranges_host", "hm_batch_submit_device", "hm_batch_wait_device",
            "hm_batch_undo")
 
 _lib = None
@@ -109,7 +109,7 @@ def lib():
             "hm_text_data": [vp, vp], "hm_text_results": [vp, vp], "hm_text_free": [vp],
             "hm_docset_doc_info": [vp, u32, vp], "hm_docset_history_prefix": [vp, u32, u32, vp],
             "hm_docset_clock_update": [vp, u32, vp, vp, vp, vp], "hm_docset_view": [vp, u32, vp],
-            "hm_docset_stats": [vp, vp], "hm_docset_handles": [vp, u32, vp, vp], "hm_sync_ranges_host": [vp, vp, vp, vp, vp, vp, u32, u32],
+            "hm_docset_stats": [vp, vp], "hm_docset_routing": [vp, vp], "hm_docset_handles": [vp, u32, vp, vp], "hm_sync_ranges_host": [vp, vp, vp, vp, vp, vp, u32, u32],
         }
         for f, a in sig.items():
             getattr(L, f).argtypes = a

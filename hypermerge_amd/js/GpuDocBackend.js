@@ -375,7 +375,8 @@ class GpuEngine {
   init(docId) { return new GpuBackendState(this, docId) }
 
   stats() {
-    const t = { calls: 0, docs: 0, moves: 0, hitPatches: 0, fullPatches: 0, opPatches: 0, replayMismatch: 0 }
+    const t = { calls: 0, docs: 0, moves: 0, hitPatches: 0, fullPatches: 0, opPatches: 0, replayMismatch: 0,
+      incremental: 0, remerged: 0, handedBack: 0 }
     for (const ds of this.docsets) { const s = addon.docsetStats(ds); for (const k in t) t[k] += s[k] }
     return t
   }

@@ -948,7 +948,8 @@ static napi_value DocsetInfo(napi_env env, napi_callback_info info) {
     return o;
 }
 
-/* docsetStats(docset) -> {calls, docs, moves, hitPatches, fullPatches, opPatches, replayMismatch} */
+/* docsetStats(docset) -> {calls, docs, moves, hitPatches, fullPatches, opPatches, replayMismatch, incremental,
+ * remerged, handedBack} (the last three: document rounds by store route, hm_docset_routing) */
 static napi_value DocsetStats(napi_env env, napi_callback_info info) {
     napi_value argv[1];
     if (!get_args(env, info, 1, argv)) return NULL;
@@ -960,6 +961,10 @@ static napi_value DocsetStats(napi_env env, napi_callback_info info) {
     napi_create_object(env, &o);
     const char *names[7] = {"calls", "docs", "moves", "hitPatches", "fullPatches", "opPatches", "replayMismatch"};
     for (int i = 0; i < 7; i++) { napi_value v; napi_create_double(env, (double)x[i], &v); set(env, o, names[i], v); }
+    uint64_t r3[3] = {0, 0, 0};
+    hm_docset_routing(d->ds, r3);
+    const char *rn[3] = {"incremental", "remerged", "handedBack"};
+    for (int i = 0; i < 3; i++) { napi_value v; napi_create_double(env, (double)r3[i], &v); set(env, o, rn[i], v); }
     return o;
 }
 

@@ -570,6 +570,9 @@ int hm_docset_view(hm_docset *ds, uint32_t doc, hm_text **out);
  * register, per-op patches, per-op replays whose registers differ from the device's merged state
  * (always 0 unless the renderer and the kernels disagree) */
 int hm_docset_stats(const hm_docset *ds, uint64_t *out8);
+/* How the docset's stores merged its document rounds so far (hm_store_last_routing summed over
+ * every submit): out3 = {incremental, re-merged, incremental handed back to the re-merge}. */
+int hm_docset_routing(const hm_docset *ds, uint64_t *out3);
 /* The store of class a_stride (8, 16, 32, 64, 128, 256): handles opened in it and handles
  * released (a document moved to a wider class; empty, reused before new ones are opened) */
 int hm_docset_handles(const hm_docset *ds, uint32_t a_stride, uint32_t *out_opened, uint32_t *out_free);

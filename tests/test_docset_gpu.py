@@ -272,3 +272,31 @@ def test_docset_clock_update_matches_reference_sql():
     assert stored[:-1] == js["b"] and stored[-1] == {}
     w, df, stored = ds.clock_update(ids)
     assert not w.any() and not df.any()
+
+
+def test_docset_rounds_report_their_route():
+    """The docset's stores route arriving rounds by the cost rule (store_kernels.h HM_INC_COST):
+    after a first load, rounds of 1-2 changes per document go incremental — hm_docset_routing
+    counts them — and the patches / state still equal the oracle's; a round as long as the log
+    re-merges."""
+    from hypermerge_amd import synth
+    from hypermerge_amd.columnar import decode_doc
+    from hypermerge_amd.docset import DocSet, render_objects, view_objects
+    from hypermerge_amd.engine import Engine
+    b = synth.generate(synth.config("C4", n_docs=60))
+    docs = [decode_doc(b, i) for i in range(b.n_docs)]
+    chunked = []
+    for chs in docs:
+        parts, k = [chs[:len(chs) - 6]], len(chs) - 6
+        while k < len(chs):
+            parts.append(chs[k:k + 2])
+            k += 2
+        chunked.append(parts)
+    ds = DocSet(Engine(0))
+    ids, objects, logs, last = _run(ds, chunked)
+    r = ds.routing()
+    assert r["incremental"] >= 2 * len(docs), r             # (the three 2-change rounds, most of them)
+    assert r["remerged"] >= len(docs)                        # (the first load)
+    for i, d in enumerate(ids[::7]):
+        s = _oracle(logs[ids.index(d)])
+        assert render_objects(view_objects(ds.view(d))) == json.loads(json.dumps(s["state"]))

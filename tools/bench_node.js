@@ -135,6 +135,8 @@ async function runGpu(mode, objects, diffsForm) {
     patch_diffs: patchesOn, diffs_form: engine.diffs, op_patches: st.opPatches - st0.opPatches,
     replay_mismatch: st.replayMismatch - st0.replayMismatch,
     hit_register_patches: st.hitPatches - st0.hitPatches, full_patches: st.fullPatches - st0.fullPatches,
+    routing: { incremental: st.incremental - st0.incremental, remerged: st.remerged - st0.remerged,
+      handed_back: st.handedBack - st0.handedBack },
     mode, input: objects ? 'Change objects' : 'raw blocks',
     digest: digest(docs.map((d) => ({ id: d.id, clock: d.clock, hist: d.back.histLen }))),
     state_digest: stateDigest(docs.map((d) => plain(G.materialize(d.back), '00000000-0000-0000-0000-000000000000'))) }
