@@ -57,10 +57,17 @@ struct Grp {
     }
 };
 
+// v[j] by selects over opaque elements (a select between two loads of one array is otherwise
+// folded into a load through a selected pointer, which puts the array in scratch memory)
 __device__ __forceinline__ uint32_t sel_nc(const uint32_t (&v)[NC], uint32_t j) {
     uint32_t r = v[0];
+    asm volatile("" : "+v"(r));
 #pragma unroll
-    for (uint32_t x = 1; x < NC; x++) r = j == x ? v[x] : r;
+    for (uint32_t x = 1; x < NC; x++) {
+        uint32_t t = v[x];
+        asm volatile("" : "+v"(t));
+        r = j == x ? t : r;
+    }
     return r;
 }
 __device__ __forceinline__ void set_nc(uint32_t (&v)[NC], uint32_t j, uint32_t y) {
@@ -824,8 +831,11 @@ __device__ int inc_doc_tiled(const AppendDesc &D, const IncArgs &A, uint4 *ssv, 
 
 // TL: the launch for rounds that need tiles (a separate instantiation: the tile loop around
 // inc_doc costs the common round's register allocation half its occupancy)
+#ifndef HM_INC_WAVES
+#define HM_INC_WAVES 1       // dev A/B: waves per SIMD the G = 8 / 16 instantiations are compiled for
+#endif
 template <int G, bool TL>
-__global__ __launch_bounds__(256) void inc_group_kernel(IncArgs A) {
+__global__ __launch_bounds__(256, (G < 64 ? HM_INC_WAVES : 1)) void inc_group_kernel(IncArgs A) {
     constexpr uint32_t NG = 256 / G;
     __shared__ uint4 s_sv[NG][2 * G];
     __shared__ uint2 s_mt[NG][2 * G];

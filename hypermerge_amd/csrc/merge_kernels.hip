@@ -85,6 +85,14 @@
 #define HM_STAGE_FIRST 0    // 1: stage the next document's rows before this document's stores (A/B: C4 2.38 -> 2.44 ms, the
                             // store outputs then waited in write_outputs on reused registers)
 #endif
+#ifndef HM_ASYNC_NEXT
+#define HM_ASYNC_NEXT 1     // the next document's rows by inline-asm loads, waited for by a counted vmcnt that
+                            // leaves this document's stores in flight (a compiler-counted load is waited for
+                            // with vmcnt(0): the stores' count varies by path, so the staging waited for them)
+#endif
+#ifndef HM_ASYNC_STORES
+#define HM_ASYNC_STORES 10  // store instructions an OK document's write_outputs issues at least (padded)
+#endif
 #ifndef HM_OPAQUE_LANE
 #define HM_OPAQUE_LANE 1    // per-document lane index the compiler cannot hoist out of the document loop
 #endif
@@ -577,6 +585,85 @@ __device__ __forceinline__ Rows load_rows(const SmallParams &p, const hm_doc_row
     if (lane + WAVE < doc.n_deps) r.d1 = *reinterpret_cast<const uint2 *>(dp + lane + WAVE);
     return r;
 }
+#if HM_ASYNC_NEXT
+// The next document's rows issued as inline-asm loads: hipcc does not count them, so the staging
+// waits with an explicit vmcnt(N) — N the store instructions write_outputs is certain to issue
+// after them on the path taken — instead of the vmcnt(0) a counted load gets, which also waited
+// for every one of this document's stores.  Lanes past a table's rows re-load its last row (every
+// address stays inside the document's range; a uniform branch skips an empty table) and are zeroed
+// once the data is in.  The destinations are named "+v" by the wait statement, so no consumer is
+// scheduled above it (cdna_hip_programming.md, 'What hipcc does not do' item 1, form ii).
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+struct AsyncRows { u32x2 c0, c1, c2; u32x4 a0, b0, a1, b1; u32x2 d0, d1; };
+__device__ __forceinline__ u32x2 aload2(const void *p) {
+    u32x2 v;
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ u32x4 aload4(const void *p) {
+    u32x4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+template <int OPL>
+__device__ __forceinline__ AsyncRows load_rows_async(const SmallParams &p, const hm_doc_row &doc) {
+    static_assert(OPL <= 2, "async next rows: up to two op rows per lane");
+    const uint32_t lane = threadIdx.x;
+    AsyncRows r;
+    r.c0 = r.c1 = r.c2 = r.d0 = r.d1 = u32x2{0u, 0u};
+    r.a0 = r.b0 = r.a1 = r.b1 = u32x4{0u, 0u, 0u, 0u};
+    if (doc.n_changes) {
+        const uint32_t i = lane < doc.n_changes ? lane : doc.n_changes - 1u;
+        const uint2 *cs = reinterpret_cast<const uint2 *>(p.changes + doc.change_off + i);
+        r.c0 = aload2(cs); r.c1 = aload2(cs + 1); r.c2 = aload2(cs + 2);
+    }
+    if (doc.n_ops) {
+        const uint32_t i0 = lane < doc.n_ops ? lane : doc.n_ops - 1u;
+        const uint4 *o0 = reinterpret_cast<const uint4 *>(p.ops + doc.op_off + i0);
+        r.a0 = aload4(o0); r.b0 = aload4(o0 + 1);
+        if (OPL > 1) {
+            const uint32_t i1 = lane + WAVE < doc.n_ops ? lane + WAVE : doc.n_ops - 1u;
+            const uint4 *o1 = reinterpret_cast<const uint4 *>(p.ops + doc.op_off + i1);
+            r.a1 = aload4(o1); r.b1 = aload4(o1 + 1);
+        }
+    }
+    if (doc.n_deps) {
+        const uint32_t i0 = lane < doc.n_deps ? lane : doc.n_deps - 1u, i1 = lane + WAVE < doc.n_deps ? lane + WAVE : doc.n_deps - 1u;
+        r.d0 = aload2(p.deps + doc.dep_off + i0); r.d1 = aload2(p.deps + doc.dep_off + i1);
+    }
+    return r;
+}
+// the wait (see above) and the rows as load_rows returns them: write_outputs padded an OK
+// document's stores to at least HM_ASYNC_STORES instructions after the loads (pad_stores), so
+// one fixed wait leaves every one of them in flight; other outcomes wait for everything.  (One
+// asm statement: a wait chosen at run time would merge register values after it, and the copies
+// the compiler may then place ahead of the wait read the destinations before the data lands.)
+template <int OPL>
+__device__ __forceinline__ Rows take_rows_async(AsyncRows &r, const hm_doc_row &doc, bool padded) {
+    if (padded)
+        asm volatile("s_waitcnt vmcnt(%9)"
+                     : "+v"(r.c0), "+v"(r.c1), "+v"(r.c2), "+v"(r.a0), "+v"(r.b0), "+v"(r.a1), "+v"(r.b1), "+v"(r.d0), "+v"(r.d1)
+                     : "n"(HM_ASYNC_STORES) : "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(0)"
+                     : "+v"(r.c0), "+v"(r.c1), "+v"(r.c2), "+v"(r.a0), "+v"(r.b0), "+v"(r.a1), "+v"(r.b1), "+v"(r.d0), "+v"(r.d1)
+                     :: "memory");
+    const uint32_t lane = threadIdx.x;
+    Rows o;
+    const bool c = lane < doc.n_changes, k0 = lane < doc.n_ops, k1 = lane + WAVE < doc.n_ops;
+    o.c01 = c ? make_uint4(r.c0.x, r.c0.y, r.c1.x, r.c1.y) : make_uint4(0u, 0u, 0u, 0u);
+    o.c2 = c ? make_uint2(r.c2.x, r.c2.y) : make_uint2(0u, 0u);
+    o.a0 = k0 ? make_uint4(r.a0.x, r.a0.y, r.a0.z, r.a0.w) : make_uint4(0u, 0u, 0u, 0u);
+    o.b0 = k0 ? make_uint4(r.b0.x, r.b0.y, r.b0.z, r.b0.w) : make_uint4(0u, 0u, 0u, 0u);
+    o.a1 = k1 ? make_uint4(r.a1.x, r.a1.y, r.a1.z, r.a1.w) : make_uint4(0u, 0u, 0u, 0u);
+    o.b1 = k1 ? make_uint4(r.b1.x, r.b1.y, r.b1.z, r.b1.w) : make_uint4(0u, 0u, 0u, 0u);
+    o.a2 = o.b2 = o.a3 = o.b3 = make_uint4(0u, 0u, 0u, 0u);
+    o.d0 = lane < doc.n_deps ? make_uint2(r.d0.x, r.d0.y) : make_uint2(0u, 0u);
+    o.d1 = lane + WAVE < doc.n_deps ? make_uint2(r.d1.x, r.d1.y) : make_uint2(0u, 0u);
+    return o;
+}
+#endif
 // an op's 8-byte value, staged in LDS with its row (an L2 re-read would put a global-load
 // round trip on the output phase's critical path)
 __device__ __forceinline__ u64 op_value(const SmallLds &L, uint32_t k) { return L.opval[k]; }
@@ -1502,6 +1589,32 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
     }
 }
 
+#if HM_ASYNC_NEXT
+// A lower bound on the store instructions write_outputs issues for a document merged OK (each
+// term names the stores above it counts): the register rows (one dwordx4 per 64 registers),
+// the allDeps rows (two dwordx4 at S = 8, one at S = 4, at least one otherwise, when there are
+// changes), the clock / heads / back-clock rows (three), the history positions (one, when there
+// are changes), the 32-byte result row (two: no store is wider than 16 bytes), the survivor rows
+// (one dwordx4 per 64).  pad_stores tops it up to HM_ASYNC_STORES with stores of the result row's
+// pad word (zero, as the row itself wrote it), issued by asm so each is exactly one instruction.
+template <int OPL>
+__device__ __forceinline__ uint32_t out_stores_min(const SmallParams &p, const hm_doc_row &doc, const DocState &st) {
+    const uint32_t S = p.a_stride, n = doc.n_changes;
+    uint32_t c = (doc.n_regs + WAVE - 1) / WAVE;
+    if (n) c += (S == 8 ? 2u : 1u) + 1u;
+    c += 3u + 2u;
+    c += (st.total + WAVE - 1) / WAVE < (uint32_t)OPL ? (st.total + WAVE - 1) / WAVE : (uint32_t)OPL;
+    return c;
+}
+template <int OPL>
+__device__ __forceinline__ void pad_stores(const SmallParams &p, const hm_doc_row &doc, const DocState &st, uint32_t ds) {
+    uint32_t *pad = &p.res_docs[ds].pad;
+    const uint32_t zero = 0u;
+    for (uint32_t c = out_stores_min<OPL>(p, doc, st); c < HM_ASYNC_STORES; c++)      // (wave-uniform)
+        asm volatile("global_store_dword %0, %1, off" :: "v"(pad), "v"(zero) : "memory");
+}
+#endif
+
 template <int OPL, bool LISTS, int CLS>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(OPL >= 3 ? (LISTS ? (OPL == 3 ? HM_WAVES_PER_EU_LIST3 : HM_WAVES_PER_EU_OPL4 - 1) : HM_WAVES_PER_EU_OPL4) : HM_WAVES_PER_EU)))
 void merge_small_kernel(SmallParams p) {
@@ -1548,6 +1661,12 @@ void merge_small_kernel(SmallParams p) {
             __builtin_memcpy(&docn, w, sizeof docn);
         };
         Rows next;
+#if HM_ASYNC_NEXT
+        AsyncRows anext;
+        constexpr bool ASY = OPL <= 2 && !HM_PREFETCH_EARLY && !HM_STAGE_FIRST;
+#else
+        constexpr bool ASY = false;
+#endif
 #if HM_PREFETCH_EARLY
         if (more) { take_docn(); dokn = check_doc(p, docn); next = load_rows<OPL>(p, docn); }
 #endif
@@ -1577,7 +1696,15 @@ void merge_small_kernel(SmallParams p) {
         asm volatile("" : "+s"(mcmp) :: "memory");
 #endif
 #if !HM_PREFETCH_EARLY
-        if (more) { take_docn(); dokn = check_doc(p, docn); next = load_rows<OPL>(p, docn); }
+        if (more) {
+            take_docn();
+            dokn = check_doc(p, docn);
+#if HM_ASYNC_NEXT
+            if constexpr (ASY) anext = load_rows_async<OPL>(p, docn);
+            else
+#endif
+            next = load_rows<OPL>(p, docn);
+        }
 #endif
         STAMP(L, 12);
         if (HM_PRIO_IO) __builtin_amdgcn_s_setprio(HM_PRIO_IO);
@@ -1597,9 +1724,15 @@ void merge_small_kernel(SmallParams p) {
         if (!more) break;
 #else
         write_outputs<OPL, LISTS>(p, L, d, ds, doc, oc, st, mcmp, sv);
+#if HM_ASYNC_NEXT
+        if constexpr (ASY) { if (more && oc == OUT_OK) pad_stores<OPL>(p, doc, st, ds); }
+#endif
         wave_sync();
         STAMP(L, 10);
         if (!more) break;
+#if HM_ASYNC_NEXT
+        if constexpr (ASY) next = take_rows_async<OPL>(anext, docn, oc == OUT_OK);
+#endif
         stage_rows<OPL, LISTS>(p, L, docn, next);
         if (HM_PRIO_IO) __builtin_amdgcn_s_setprio(0);
         wave_sync();

@@ -312,6 +312,9 @@ __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
                                 r.n_ops <= HM_INC_TILED_MAX_O);     // (tiles of the group / wave passes)
     bool inc = live && a.incremental && last.status == HM_OK && last.n_queued == 0 && !remapped && r.n_changes > 0 &&
                (small || longr) && m.n_r <= r.n_regs && r.n_actors <= a.S;
+    // mode 1: a small list document keeps no incremental state (inc_meta_kernel), so it re-merges
+    // before any of the reads below
+    if (inc && lists && a.incremental == 1u && m.n_o + r.n_ops <= HM_INC_SMALL_LIST_OPS) inc = false;
     bool wave = false;                                             // list ops: the one-document-per-wave pass
     if (inc && a.ist) {
         // what inc_group_kernel would hand straight back (its state checks, and for documents with
