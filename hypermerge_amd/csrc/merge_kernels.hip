@@ -90,6 +90,9 @@
                             // leaves this document's stores in flight (a compiler-counted load is waited for
                             // with vmcnt(0): the stores' count varies by path, so the staging waited for them)
 #endif
+#ifndef HM_ASYNC_MAX_OPL
+#define HM_ASYNC_MAX_OPL 2  // instantiations (op rows per lane) that load the next document's rows by asm
+#endif
 #ifndef HM_ASYNC_STORES
 #define HM_ASYNC_STORES 10  // store instructions an OK document's write_outputs issues at least (padded)
 #endif
@@ -595,7 +598,7 @@ __device__ __forceinline__ Rows load_rows(const SmallParams &p, const hm_doc_row
 // scheduled above it (cdna_hip_programming.md, 'What hipcc does not do' item 1, form ii).
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-struct AsyncRows { u32x2 c0, c1, c2; u32x4 a0, b0, a1, b1; u32x2 d0, d1; };
+struct AsyncRows { u32x2 c0, c1, c2; u32x4 a0, b0, a1, b1, a2, b2, a3, b3; u32x2 d0, d1; };
 __device__ __forceinline__ u32x2 aload2(const void *p) {
     u32x2 v;
     asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
@@ -608,11 +611,10 @@ __device__ __forceinline__ u32x4 aload4(const void *p) {
 }
 template <int OPL>
 __device__ __forceinline__ AsyncRows load_rows_async(const SmallParams &p, const hm_doc_row &doc) {
-    static_assert(OPL <= 2, "async next rows: up to two op rows per lane");
     const uint32_t lane = threadIdx.x;
     AsyncRows r;
     r.c0 = r.c1 = r.c2 = r.d0 = r.d1 = u32x2{0u, 0u};
-    r.a0 = r.b0 = r.a1 = r.b1 = u32x4{0u, 0u, 0u, 0u};
+    r.a0 = r.b0 = r.a1 = r.b1 = r.a2 = r.b2 = r.a3 = r.b3 = u32x4{0u, 0u, 0u, 0u};
     if (doc.n_changes) {
         const uint32_t i = lane < doc.n_changes ? lane : doc.n_changes - 1u;
         const uint2 *cs = reinterpret_cast<const uint2 *>(p.changes + doc.change_off + i);
@@ -626,6 +628,16 @@ __device__ __forceinline__ AsyncRows load_rows_async(const SmallParams &p, const
             const uint32_t i1 = lane + WAVE < doc.n_ops ? lane + WAVE : doc.n_ops - 1u;
             const uint4 *o1 = reinterpret_cast<const uint4 *>(p.ops + doc.op_off + i1);
             r.a1 = aload4(o1); r.b1 = aload4(o1 + 1);
+        }
+        if (OPL > 2) {
+            const uint32_t i2 = lane + 2 * WAVE < doc.n_ops ? lane + 2 * WAVE : doc.n_ops - 1u;
+            const uint4 *o2 = reinterpret_cast<const uint4 *>(p.ops + doc.op_off + i2);
+            r.a2 = aload4(o2); r.b2 = aload4(o2 + 1);
+        }
+        if (OPL > 3) {
+            const uint32_t i3 = lane + 3 * WAVE < doc.n_ops ? lane + 3 * WAVE : doc.n_ops - 1u;
+            const uint4 *o3 = reinterpret_cast<const uint4 *>(p.ops + doc.op_off + i3);
+            r.a3 = aload4(o3); r.b3 = aload4(o3 + 1);
         }
     }
     if (doc.n_deps) {
@@ -641,14 +653,24 @@ __device__ __forceinline__ AsyncRows load_rows_async(const SmallParams &p, const
 // the compiler may then place ahead of the wait read the destinations before the data lands.)
 template <int OPL>
 __device__ __forceinline__ Rows take_rows_async(AsyncRows &r, const hm_doc_row &doc, bool padded) {
-    if (padded)
-        asm volatile("s_waitcnt vmcnt(%9)"
-                     : "+v"(r.c0), "+v"(r.c1), "+v"(r.c2), "+v"(r.a0), "+v"(r.b0), "+v"(r.a1), "+v"(r.b1), "+v"(r.d0), "+v"(r.d1)
-                     : "n"(HM_ASYNC_STORES) : "memory");
-    else
-        asm volatile("s_waitcnt vmcnt(0)"
-                     : "+v"(r.c0), "+v"(r.c1), "+v"(r.c2), "+v"(r.a0), "+v"(r.b0), "+v"(r.a1), "+v"(r.b1), "+v"(r.d0), "+v"(r.d1)
-                     :: "memory");
+    // (the statement names only the destinations this instantiation loads: a pinned unused one
+    // costs a register across write_outputs)
+#define HM_AW2 "+v"(r.c0), "+v"(r.c1), "+v"(r.c2), "+v"(r.a0), "+v"(r.b0), "+v"(r.a1), "+v"(r.b1), "+v"(r.d0), "+v"(r.d1)
+#define HM_AW3 HM_AW2, "+v"(r.a2), "+v"(r.b2)
+#define HM_AW4 HM_AW3, "+v"(r.a3), "+v"(r.b3)
+    if constexpr (OPL <= 2) {
+        if (padded) asm volatile("s_waitcnt vmcnt(%9)" : HM_AW2 : "n"(HM_ASYNC_STORES) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" : HM_AW2 :: "memory");
+    } else if constexpr (OPL == 3) {
+        if (padded) asm volatile("s_waitcnt vmcnt(%11)" : HM_AW3 : "n"(HM_ASYNC_STORES) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" : HM_AW3 :: "memory");
+    } else {
+        if (padded) asm volatile("s_waitcnt vmcnt(%13)" : HM_AW4 : "n"(HM_ASYNC_STORES) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" : HM_AW4 :: "memory");
+    }
+#undef HM_AW4
+#undef HM_AW3
+#undef HM_AW2
     const uint32_t lane = threadIdx.x;
     Rows o;
     const bool c = lane < doc.n_changes, k0 = lane < doc.n_ops, k1 = lane + WAVE < doc.n_ops;
@@ -658,7 +680,11 @@ __device__ __forceinline__ Rows take_rows_async(AsyncRows &r, const hm_doc_row &
     o.b0 = k0 ? make_uint4(r.b0.x, r.b0.y, r.b0.z, r.b0.w) : make_uint4(0u, 0u, 0u, 0u);
     o.a1 = k1 ? make_uint4(r.a1.x, r.a1.y, r.a1.z, r.a1.w) : make_uint4(0u, 0u, 0u, 0u);
     o.b1 = k1 ? make_uint4(r.b1.x, r.b1.y, r.b1.z, r.b1.w) : make_uint4(0u, 0u, 0u, 0u);
-    o.a2 = o.b2 = o.a3 = o.b3 = make_uint4(0u, 0u, 0u, 0u);
+    const bool k2 = lane + 2 * WAVE < doc.n_ops, k3 = lane + 3 * WAVE < doc.n_ops;
+    o.a2 = k2 ? make_uint4(r.a2.x, r.a2.y, r.a2.z, r.a2.w) : make_uint4(0u, 0u, 0u, 0u);
+    o.b2 = k2 ? make_uint4(r.b2.x, r.b2.y, r.b2.z, r.b2.w) : make_uint4(0u, 0u, 0u, 0u);
+    o.a3 = k3 ? make_uint4(r.a3.x, r.a3.y, r.a3.z, r.a3.w) : make_uint4(0u, 0u, 0u, 0u);
+    o.b3 = k3 ? make_uint4(r.b3.x, r.b3.y, r.b3.z, r.b3.w) : make_uint4(0u, 0u, 0u, 0u);
     o.d0 = lane < doc.n_deps ? make_uint2(r.d0.x, r.d0.y) : make_uint2(0u, 0u);
     o.d1 = lane + WAVE < doc.n_deps ? make_uint2(r.d1.x, r.d1.y) : make_uint2(0u, 0u);
     return o;
@@ -1663,7 +1689,7 @@ void merge_small_kernel(SmallParams p) {
         Rows next;
 #if HM_ASYNC_NEXT
         AsyncRows anext;
-        constexpr bool ASY = OPL <= 2 && !HM_PREFETCH_EARLY && !HM_STAGE_FIRST;
+        constexpr bool ASY = OPL <= HM_ASYNC_MAX_OPL && !HM_PREFETCH_EARLY && !HM_STAGE_FIRST;
 #else
         constexpr bool ASY = false;
 #endif
