@@ -630,7 +630,8 @@ def inc_alg_bytes(sub, S):
     per new change its history slot and packed key (8 B), its allDeps row written (4S) and each
     transitiveDeps fold source's allDeps row read (4S: its deps, plus {actor: seq - 1} unless a dep
     names the actor); per document its result row and incremental state read and written (2 x 32 B
-    each), its clock and heads rows read (8S) and clock / back-clock / heads written (12S); per
+    each), its clock and heads rows read (8S), clock / back-clock / heads written (12S) and the
+    submit's gathered copy of the result and those three rows written (32 B + 12S); per
     register the round's set / del / link / inc ops hit, the register row read and written (2 x 16 B)
     and one survivor with its metadata read and written (2 x 24 B: a last-writer-wins register)."""
     ch, dp, op, docs = sub.changes, sub.deps, sub.ops, sub.docs
@@ -643,7 +644,7 @@ def inc_alg_bytes(sub, S):
     doc_of_op = np.repeat(np.arange(n), docs["n_ops"].astype(np.int64))
     asg = op["action"] >= 5
     hits = len(np.unique(doc_of_op[asg].astype(np.int64) * (1 << 32) + op["reg"][asg].astype(np.int64))) if asg.any() else 0
-    return int(2 * (24 * nc + 8 * nd + 32 * no) + nc * (8 + 4 * S) + sources * 4 * S + n * (128 + 20 * S) + hits * 80)
+    return int(2 * (24 * nc + 8 * nd + 32 * no) + nc * (8 + 4 * S) + sources * 4 * S + n * (160 + 32 * S) + hits * 80)
 
 
 def _pinned_rows(b):

@@ -330,6 +330,21 @@ __device__ void list_indices(const Grp<64> &g, const AppendDesc &D, const IncArg
     }
 }
 
+// The submit's gathered results (what hm_batch_wait hands out: the result rows, then the clock,
+// back-clock and heads rows, by batch row) written straight from the registers of a document
+// finished here; gather_kernel then copies only the rows of the documents the re-merge took
+// (gdone[bi] = 0).
+__device__ __forceinline__ void gather_rows(const IncArgs &A, uint32_t bi, uint32_t a, uint32_t ck, uint32_t bk, uint32_t hd) {
+    if (!A.gout) return;
+    uint32_t *o = reinterpret_cast<uint32_t *>(A.gout) + (size_t)A.n * 8;
+    const size_t ns = (size_t)A.n * A.S, k = (size_t)bi * A.S + a;
+    o[k] = ck; o[ns + k] = bk; o[2 * ns + k] = hd;
+}
+__device__ __forceinline__ void gather_result(const IncArgs &A, uint32_t bi, const hm_doc_result &r) {
+    if (!A.gout) return;
+    reinterpret_cast<hm_doc_result *>(A.gout)[bi] = r;
+}
+
 // the new rows of a document whose segments did not move, from the submit's staged tables
 // (batch-local offsets) to the log, rebased (append_kernel skips such documents)
 template <int G>
@@ -348,7 +363,8 @@ __device__ __forceinline__ void inc_append(const Grp<G> &g, const AppendDesc &D,
 }
 
 template <int G>
-__device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 *smt, uint32_t *lscr, bool appended = false) {
+__device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 *smt, uint32_t *lscr, bool appended = false,
+                        uint32_t bi = HM_NONE) {
     const Grp<G> g;
     const uint32_t gl = g.gl;
     const uint32_t S = A.S, h = D.handle, NA = D.n_actors, nnc = D.n_new_c, nno = D.n_new_o, nnd = D.n_new_d;
@@ -762,6 +778,7 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
         A.clock[(size_t)h * S + gl] = ckf;
         A.back_clock[(size_t)h * S + gl] = ckf;                // queue empty: every handed change applied
         A.heads[(size_t)h * S + gl] = hdr;
+        if (bi != HM_NONE) gather_rows(A, bi, gl, ckf, ckf, hdr);
     }
     const bool ag = g.bits(gl < S && ckf < mc) == 0, bg = g.bits(gl < S && mc < ckf) == 0;
     if (gl == 0) {
@@ -770,6 +787,7 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
         r.hist_len = R0.hist_len + nnc; r.n_queued = 0; r.n_surv = (uint32_t)((int32_t)R0.n_surv + dsurv);
         r.min_cmp = (ag && bg) ? 0u : (ag ? 1u : (bg ? 2u : 3u));
         A.res_docs[h] = r;
+        if (bi != HM_NONE) gather_result(A, bi, r);
         IncState s = I;
         s.s_used = I.s_used + acc; s.cabs = cabs; s.mapmask = I.mapmask | made_all;
         if (G == 64 && any_list) s.pad[0] = lp.n_el;
@@ -787,7 +805,7 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
 // A tile after the first that cannot go incremental sends the document to the re-merge, which
 // rewrites every row the earlier tiles wrote.
 template <int G>
-__device__ int inc_doc_tiled(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 *smt, uint32_t *lscr) {
+__device__ int inc_doc_tiled(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 *smt, uint32_t *lscr, uint32_t bi) {
     const Grp<G> g;
     const uint32_t gl = g.gl;
     // (one call site of inc_doc: a second inlined copy costs the common round its occupancy)
@@ -820,7 +838,7 @@ __device__ int inc_doc_tiled(const AppendDesc &D, const IncArgs &A, uint4 *ssv, 
                 T.n_old_r = D.n_r;                            // (the first tile wrote every new register's row)
             }
         }
-        const int rc = inc_doc<G>(T, A, ssv, smt, lscr, tiled);
+        const int rc = inc_doc<G>(T, A, ssv, smt, lscr, tiled, bi);
         if (rc != INC_DONE) return first ? rc : INC_BAIL;
         c0 += k; d0 += td; o0 += to;
         if (c0 >= D.n_new_c) return INC_DONE;
@@ -850,8 +868,9 @@ __global__ __launch_bounds__(256, (G < 64 ? HM_INC_WAVES : 1)) void inc_group_ke
         const bool tl = D.n_new_c > NC || D.n_new_o > (uint32_t)G || D.n_new_d > (uint32_t)G;
         if (G == 64 && tl != TL) continue;                             // (the other launch's document)
         int rc;
-        if constexpr (TL) rc = inc_doc_tiled<G>(D, A, s_sv[grp], s_mt[grp], s_ls[G == 64 ? grp : 0]);
-        else rc = inc_doc<G>(D, A, s_sv[grp], s_mt[grp], s_ls[G == 64 ? grp : 0]);
+        if constexpr (TL) rc = inc_doc_tiled<G>(D, A, s_sv[grp], s_mt[grp], s_ls[G == 64 ? grp : 0], di);
+        else rc = inc_doc<G>(D, A, s_sv[grp], s_mt[grp], s_ls[G == 64 ? grp : 0], false, di);
+        if (rc == INC_DONE && gl == 0 && A.gdone) A.gdone[di] = 1;
         if (rc != INC_DONE && gl == 0) {
             if (rc == INC_DEFER && A.defer) A.defer[1 + atomicAdd(&A.defer[0], 1u)] = di;
             else A.bail[1 + atomicAdd(&A.bail[0], 1u)] = D.handle;
@@ -992,7 +1011,7 @@ __device__ __forceinline__ int lane_assign(const AppendDesc &D, const IncArgs &A
 template <int S>
 __device__ __forceinline__ void lane_finish(const AppendDesc &D, const IncArgs &A, const IncState &I, const hm_doc_result &R0,
                                             const uint32_t (&ck)[S], const uint32_t (&hd)[S], uint32_t used, int32_t dsurv,
-                                            unsigned long long cabs, unsigned long long mm) {
+                                            unsigned long long cabs, unsigned long long mm, uint32_t bi) {
     const uint32_t h = D.handle;
     lrow_store<S>(A.clock + (size_t)h * S, ck);
     lrow_store<S>(A.back_clock + (size_t)h * S, ck);
@@ -1012,10 +1031,13 @@ __device__ __forceinline__ void lane_finish(const AppendDesc &D, const IncArgs &
     IncState st = I;
     st.s_used = used; st.cabs = cabs; st.mapmask = mm;
     A.ist[h] = st;
+#pragma unroll
+    for (int x = 0; x < S; x++) gather_rows(A, bi, (uint32_t)x, ck[x], ck[x], hd[x]);
+    gather_result(A, bi, r);
 }
 
 template <int S>
-__device__ int inc_lane(const AppendDesc &D, const IncArgs &A) {
+__device__ int inc_lane(const AppendDesc &D, const IncArgs &A, uint32_t bi) {
     const uint32_t h = D.handle, NA = D.n_actors, nnc = D.n_new_c, nnd = D.n_new_d, nno = D.n_new_o;
     const bool rows_moved = D.src_c != D.dst_c || D.src_d != D.dst_d || D.src_o != D.dst_o;
     if (!rows_moved) {
@@ -1224,7 +1246,7 @@ __device__ int inc_lane(const AppendDesc &D, const IncArgs &A) {
         xd += nd; xo += c.n_ops;
     }
 
-    lane_finish<S>(D, A, I, R0, ck, hd, used, dsurv, cabs, mm);
+    lane_finish<S>(D, A, I, R0, ck, hd, used, dsurv, cabs, mm, bi);
     return INC_DONE;
 }
 
@@ -1246,7 +1268,11 @@ __global__ __launch_bounds__(256) void inc_lane_kernel(IncArgs A) {
     uint32_t hnd = 0;
     if (i < A.n) {
         const AppendDesc D = A.descs[i];
-        if ((D.inc & HM_DINC_ROUTE) == 3u) { hnd = D.handle; rc = inc_lane<S>(D, A); }
+        if ((D.inc & HM_DINC_ROUTE) == 3u) {
+            hnd = D.handle;
+            rc = inc_lane<S>(D, A, i);
+            if (rc == INC_DONE && A.gdone) A.gdone[i] = 1;
+        }
     }
     // (the group passes hold a round in registers: what the lane pass hands over re-merges)
     lane_list_push(A.bail, rc == INC_BAIL || rc == INC_DEFER, hnd);

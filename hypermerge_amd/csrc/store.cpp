@@ -230,7 +230,7 @@ struct PhaseTimer {
 
 // Staged batch layout on the device: [changes][deps][ops][docs][handles][remap][gather][bail]
 struct StageLayout {
-    size_t o_ch, o_dp, o_op, o_docs, o_hand, o_remap, o_gather, o_bail, o_defer, o_fail, total;
+    size_t o_ch, o_dp, o_op, o_docs, o_hand, o_remap, o_gather, o_bail, o_defer, o_gdone, o_fail, total;
 };
 StageLayout layout(size_t nc, size_t nd, size_t no, size_t n, size_t nremap, uint32_t S) {
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -245,6 +245,7 @@ StageLayout layout(size_t nc, size_t nd, size_t no, size_t n, size_t nremap, uin
     L.o_gather = o; o += al(n * (sizeof(hm_doc_result) + 3 * 4 * (size_t)S) + 1);
     L.o_bail = o; o += al(4 * (n + 1));
     L.o_defer = o; o += al(4 * (n + 1));
+    L.o_gdone = o; o += al(n);
     L.o_fail = o; o += 256;
     L.total = o;
     return L;
@@ -601,6 +602,9 @@ static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handl
             IA.epos = s->epos; IA.epar = s->epar; IA.ekey = s->ekey; IA.lorder = s->lorder; IA.ldir = s->ldir;
             IA.clock = s->clock; IA.back_clock = s->back_clock; IA.heads = s->heads; IA.min_clock = s->min_clock;
             IA.ist = s->ist; IA.bail = bail; IA.defer = (uint32_t *)(sp + L.o_defer); IA.n_lane = P.mx[0];
+            // the documents the incremental kernels finish write their gathered rows themselves
+            IA.gout = sp + L.o_gather; IA.gdone = sp + L.o_gdone;
+            SCHK(s, hipMemsetAsync(IA.gdone, 0, n, st));
             dbg_list_state(s, "before");
             SCHK(s, hm_launch_inc_apply(IA, st));
             dbg_list_state(s, "after");
@@ -624,7 +628,8 @@ static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handl
         s->st_inc = P.n_inc - counts[1]; s->st_cold = counts[0]; s->st_bail = counts[1];
         uint32_t *fail = (uint32_t *)(sp + L.o_fail);
         SCHK(s, hipMemsetAsync(fail, 0, 4, st));
-        SCHK(s, hm_launch_gather(A.handles, n, S, s->res_docs, s->clock, s->back_clock, s->heads, sp + L.o_gather, fail, st));
+        SCHK(s, hm_launch_gather(A.handles, n, S, s->res_docs, s->clock, s->back_clock, s->heads, sp + L.o_gather, fail, st,
+                                 P.n_inc ? sp + L.o_gdone : nullptr));
         s->p_gather_dev = sp + L.o_gather;
         s->p_fail_dev = fail;
         s->p_handles_dev = const_cast<uint32_t *>(A.handles);

@@ -130,6 +130,8 @@ struct IncArgs {
     uint32_t *bail;                            // [0] count, [1..] handles re-merged
     uint32_t *defer;                           // [0] count, [1..] desc indices for the wave kernel (NULL: bail)
     uint32_t n_lane;                           // documents routed to the lane pass (0: no launch)
+    uint8_t *gout;                             // the submit's gather buffer (gather_kernel's layout), or NULL
+    uint8_t *gdone;                            // [n] 1: the row was gathered by the incremental kernels
 };
 
 // AppendDesc.inc: the route (bits 0-1: 0 re-merge, 1 incremental group pass, 2 wave pass, 3 lane pass) and what
@@ -223,7 +225,7 @@ hipError_t hm_launch_read_regs(uint32_t n, const uint32_t *abs_reg, const uint32
                                uint32_t *counter, hipStream_t s);
 hipError_t hm_launch_gather(const uint32_t *handles, uint32_t n, uint32_t S, const hm_doc_result *res_docs,
                             const uint32_t *clock, const uint32_t *back_clock, const uint32_t *heads, uint8_t *out,
-                            uint32_t *n_fail, hipStream_t s);
+                            uint32_t *n_fail, hipStream_t s, const uint8_t *gdone = nullptr);
 hipError_t hm_launch_clock_update(const uint32_t *docs, uint32_t n, uint32_t S, const uint32_t *back_clock,
                                   uint32_t *stored, uint8_t *written, uint8_t *differs, uint32_t *out_stored,
                                   hipStream_t s);

@@ -156,6 +156,32 @@ __global__ void gather_kernel(const uint32_t *handles, uint32_t n, uint32_t S, c
     }
 }
 
+// The same gather after an incremental round: the documents the incremental kernels finished
+// (gdone[i] = 1) wrote their rows already, so one lane per batch row copies the rest — the
+// re-merged documents, usually few — row by row.
+__global__ void gather_rest_kernel(const uint32_t *handles, uint32_t n, uint32_t S, const hm_doc_result *res_docs,
+                                   const uint32_t *clock, const uint32_t *back_clock, const uint32_t *heads,
+                                   uint8_t *out, uint32_t *n_fail, const uint8_t *gdone) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool fail = false;
+    if (i < n && !gdone[i]) {
+        const size_t ns = (size_t)n * S, h = handles[i];
+        const hm_doc_result r = res_docs[h];
+        reinterpret_cast<hm_doc_result *>(out)[i] = r;
+        fail = r.status != HM_OK;
+        uint32_t *o = reinterpret_cast<uint32_t *>(out) + (size_t)n * 8 + (size_t)i * S;
+        for (uint32_t a = 0; a < S; a++) {
+            o[a] = clock[h * S + a];
+            o[ns + a] = back_clock[h * S + a];
+            o[2 * ns + a] = heads[h * S + a];
+        }
+    }
+    if (n_fail) {
+        const unsigned long long b = __ballot(fail);
+        if (b && (threadIdx.x & 63) == 0) atomicAdd(n_fail, (uint32_t)__popcll(b));
+    }
+}
+
 // One lane per (document, entry).  ClockStore.update writes each input entry with
 // `ON CONFLICT ... DO UPDATE SET seq=excluded.seq WHERE excluded.seq > seq`, then re-reads
 // the stored clock; Clock.equal treats missing and zero entries alike (src/Clock.ts:13-25).
@@ -679,8 +705,13 @@ hipError_t hm_launch_read_regs(uint32_t n, const uint32_t *abs_reg, const uint32
 
 hipError_t hm_launch_gather(const uint32_t *handles, uint32_t n, uint32_t S, const hm_doc_result *res_docs,
                             const uint32_t *clock, const uint32_t *back_clock, const uint32_t *heads, uint8_t *out,
-                            uint32_t *n_fail, hipStream_t s) {
+                            uint32_t *n_fail, hipStream_t s, const uint8_t *gdone) {
     if (!n) return hipSuccess;
+    if (gdone) {
+        hipLaunchKernelGGL(hms::gather_rest_kernel, dim3((n + 255) / 256), dim3(256), 0, s, handles, n, S, res_docs, clock,
+                           back_clock, heads, out, n_fail, gdone);
+        return hipGetLastError();
+    }
     const size_t words = (size_t)n * (8 + 3 * (size_t)S);
     hipLaunchKernelGGL(hms::gather_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, handles, n, S, res_docs,
                        clock, back_clock, heads, out, n_fail);
