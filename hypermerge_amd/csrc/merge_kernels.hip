@@ -44,7 +44,7 @@
 #ifndef HM_STAMPS
 #define HM_STAMPS 0     // diagnostic builds only: per-phase s_memtime shares (tools/stamps.py); never timed
 #endif
-#define HM_NSTAMP 13
+#define HM_NSTAMP 16
 #ifndef HM_PREFETCH_EARLY
 #define HM_PREFETCH_EARLY 0 // 1: the next document's rows are loaded before this document's merge
 #endif
@@ -74,6 +74,12 @@
 #endif
 #ifndef HM_PRIO_K2
 #define HM_PRIO_K2 0        // dev A/B: priority through the K2 op scan and survivor tests
+#endif
+#ifndef HM_HIST_DP
+#define HM_HIST_DP 1        // queued documents: history by the parallel (t, pass, pos) solve before the pass loop
+#endif
+#ifndef HM_HIST_REGS
+#define HM_HIST_REGS 1      // ... iterated in registers (cross-lane reads) when every change has <= 4 dependency lanes
 #endif
 #ifndef HM_PRIO_K1
 #define HM_PRIO_K1 3        // through validation and the dependency pre-pass: C4 2.41 -> 2.37 ms
@@ -931,7 +937,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         u64 applied = 0, queue = 0;                       // applied keys; queued lanes
         bool copy_applied = false;                        // a duplicate copy stands for its key
         bool solved = false;
-        {
+        if (HM_HIST_DP) {
             // Every change's place in history in parallel, per (actor, seq) key (its first
             // arrival's lane; copies of a key have equal content, hence equal deps).  The arrival
             // whose processing applies key K is t(K) = max(first arrival of K, t(deps)) = the
@@ -950,17 +956,42 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
             const bool has_dup = dupm != 0;
             const bool kl = act && !dup;                            // this lane is its key's first arrival
             uint32_t t = (!kl || never) ? INF : lane;
-            for (uint32_t it = 0; it <= n; it++) {
-                tx[lane] = t;
-                wave_sync();
-                uint32_t nt = t;
-                if (kl && t != INF)
-                    for (u64 m = dall; m; m &= m - 1) { const uint32_t x = tx[__builtin_ctzll(m)]; nt = nt > x ? nt : x; }
-                wave_sync();
-                const bool grew = nt != t;
-                t = nt;
-                if (__ballot(grew) == 0) break;
+            // Documents without duplicates whose changes have at most 4 dependency lanes each
+            // (C4 / C5: at most 2 deps and the predecessor) iterate in registers: the lanes a
+            // change reads are fixed, so each round is 4 cross-lane reads (ds_bpermute) and a
+            // ballot, with no LDS round trip or fence.
+            const bool regdp = HM_HIST_REGS && !has_dup && __ballot(act && __popcll(dall) > 4) == 0;
+            uint32_t sl0 = lane, sl1 = lane, sl2 = lane, sl3 = lane;
+            if (regdp) {
+                u64 m = dall;
+                sl0 = m ? (uint32_t)__builtin_ctzll(m) : lane; m &= m - 1;
+                sl1 = m ? (uint32_t)__builtin_ctzll(m) : lane; m &= m - 1;
+                sl2 = m ? (uint32_t)__builtin_ctzll(m) : lane; m &= m - 1;
+                sl3 = m ? (uint32_t)__builtin_ctzll(m) : lane;
+                for (uint32_t it = 0; it <= n; it++) {
+                    const uint32_t x0 = shfl32(t, (int)sl0), x1 = shfl32(t, (int)sl1);
+                    const uint32_t x2 = shfl32(t, (int)sl2), x3 = shfl32(t, (int)sl3);
+                    uint32_t nt = t;
+                    nt = nt > x0 ? nt : x0; nt = nt > x1 ? nt : x1; nt = nt > x2 ? nt : x2; nt = nt > x3 ? nt : x3;
+                    nt = (kl && t != INF) ? nt : t;
+                    const bool grew = nt != t;
+                    t = nt;
+                    if (__ballot(grew) == 0) break;
+                }
+            } else {
+                for (uint32_t it = 0; it <= n; it++) {
+                    tx[lane] = t;
+                    wave_sync();
+                    uint32_t nt = t;
+                    if (kl && t != INF)
+                        for (u64 m = dall; m; m &= m - 1) { const uint32_t x = tx[__builtin_ctzll(m)]; nt = nt > x ? nt : x; }
+                    wave_sync();
+                    const bool grew = nt != t;
+                    t = nt;
+                    if (__ballot(grew) == 0) break;
+                }
             }
+            STAMP(L, 13);
             // every copy learns its key's t; key word = t << 16 | pass << 8 | pos
             tx[lane] = t;
             wave_sync();
@@ -968,7 +999,27 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
             wave_sync();
             uint32_t w = (!kl || t == INF) ? 0xFFFFFFFFu : ((t << 16) | ((t == lane ? 1u : 2u) << 8) | lane);
             bool conv = false;
-            for (uint32_t it = 0; it <= n + 1; it++) {
+            if (regdp) {
+                // (no duplicates: every active lane is its key's first arrival, tk = t)
+                const bool queued_copy = act && tk != INF && tk != key && lane < tk;
+                const uint32_t nsl = (uint32_t)__popcll(dall);
+                for (uint32_t it = 0; it <= n + 1; it++) {
+                    const uint32_t y0 = shfl32(w, (int)sl0), y1 = shfl32(w, (int)sl1);
+                    const uint32_t y2 = shfl32(w, (int)sl2), y3 = shfl32(w, (int)sl3);
+                    uint32_t pc = 2;
+                    auto fold = [&](uint32_t wd, uint32_t k) {
+                        const uint32_t v = ((wd >> 8) & 0xFFu) + ((wd & 0xFFu) > lane ? 1u : 0u);
+                        pc = (k < nsl && (wd >> 16) == tk && v > pc) ? v : pc;
+                    };
+                    fold(y0, 0); fold(y1, 1); fold(y2, 2); fold(y3, 3);
+                    const uint32_t cand = queued_copy ? ((tk << 16) | ((pc > 0xFEu ? 0xFEu : pc) << 8) | lane) : 0xFFFFFFFFu;
+                    const uint32_t nw = (kl && t != INF && t != lane) ? cand : w;
+                    const bool grew = nw != w;
+                    w = nw;
+                    if (__ballot(grew) == 0) { conv = true; break; }
+                }
+            }
+            for (uint32_t it = 0; !regdp && it <= n + 1; it++) {
                 tx[lane] = w;                                       // meaningful on key lanes
                 if (has_dup) tm[lane] = 0xFFFFFFFFu;
                 wave_sync();
@@ -995,6 +1046,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
                 w = nw;
                 if (__ballot(grew) == 0) { conv = true; break; }
             }
+            STAMP(L, 14);
             tx[lane] = w;
             wave_sync();
             const uint32_t wk = act && tk != INF ? tx[key] : 0xFFFFFFFFu;
@@ -1006,14 +1058,30 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
                 for (u64 m = dall; m; m &= m - 1) bad |= tx[__builtin_ctzll(m)] >= hk;
             wave_sync();
             if (conv && __ballot(bad) == 0) {
+                // rank of the key among the applied keys: a radix pass over the bits of t, then of
+                // pass, high to low (one ballot each: the lanes whose key agrees so far with a 0
+                // there are smaller); the low byte is the applying lane itself, so the lanes still
+                // equal after (t, pass) are ordered by lane
+                const u64 A = __ballot(apl);
+                u64 eq = apl ? A : 0ull;
                 uint32_t rank = 0;
-                for (uint32_t j = 0; j < n; j++) rank += (uint32_t)__builtin_amdgcn_readlane((int)hk, (int)j) < hk ? 1u : 0u;
+                const uint32_t tmax = wave_max(apl ? (hk >> 16) : 0u), pmax = wave_max(apl ? ((hk >> 8) & 0xFFu) : 0u);
+                auto rbit = [&](uint32_t b) {
+                    const bool one = (hk >> b) & 1u;
+                    const u64 B = __ballot(apl && one);
+                    rank += one ? (uint32_t)__popcll(eq & ~B) : 0u;
+                    eq &= one ? B : ~B;
+                };
+                for (int b = 16 + (31 - __builtin_clz(tmax | 1u)); b >= 16; b--) rbit((uint32_t)b);
+                for (int b = 8 + (31 - __builtin_clz(pmax | 1u)); b >= 8; b--) rbit((uint32_t)b);
+                rank += (uint32_t)__popcll(eq & below);
                 hist = apl ? (int32_t)rank : (act && tk != INF ? -2 : -1);
                 H = (uint32_t)__popcll(__ballot(apl));
                 if (apl && dup) L.first[fidx(a8, (slot & 63))] = lane;   // (actor, seq) -> applied copy
                 copy_applied = __ballot(apl && dup) != 0;
                 solved = true;
             }
+            STAMP(L, 15);
         }
         for (uint32_t i = 0; i < n && !solved; i++) {
             queue |= 1ull << i;

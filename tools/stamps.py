@@ -6,7 +6,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from hypermerge_amd import synth
 from hypermerge_amd.engine import Engine, lib
 NAMES = ["pre-merge", "validate+first-table", "deps/readiness", "history", "ancestor push", "fold+heads+reg-init",
-         "K2 op scan", "objects+survivors", "offsets+rank+ties", "lists/counters", "outputs", "stage next", "min_cmp+next-row loads"]
+         "K2 op scan", "objects+survivors", "offsets+rank+ties", "lists/counters", "outputs", "stage next", "min_cmp+next-row loads",
+         "history: t solve", "history: (pass, pos) solve", "history: check + rank"]
 cfg = sys.argv[1] if len(sys.argv) > 1 else "C4"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000
 over = {"arrival": int(sys.argv[3])} if len(sys.argv) > 3 else {}
@@ -14,11 +15,11 @@ b = synth.generate(synth.config(cfg, n_docs=n, **over))
 e = Engine(0)
 L = lib()
 L.hm_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
-buf = (ctypes.c_ulonglong * 13)()
+buf = (ctypes.c_ulonglong * 16)()
 e.merge(b)
-L.hm_debug_stamps(buf, 13, 1)
+L.hm_debug_stamps(buf, 16, 1)
 e.merge(b)
-L.hm_debug_stamps(buf, 13, 1)
+L.hm_debug_stamps(buf, 16, 1)
 tot = sum(buf)
 for i, nm in enumerate(NAMES):
     print(f"{i:2d} {nm:24s} {100.0 * buf[i] / tot:6.2f}%  {buf[i] / n:10.1f} cyc/doc")
