@@ -44,7 +44,7 @@
 #ifndef HM_STAMPS
 #define HM_STAMPS 0     // diagnostic builds only: per-phase s_memtime shares (tools/stamps.py); never timed
 #endif
-#define HM_NSTAMP 16
+#define HM_NSTAMP 20
 #ifndef HM_PREFETCH_EARLY
 #define HM_PREFETCH_EARLY 0 // 1: the next document's rows are loaded before this document's merge
 #endif
@@ -391,6 +391,7 @@ __device__ __forceinline__ void rga_order(const SmallLds &L, uint32_t R, uint32_
         lds_add(&L.pcount[pi], 1u);
     }
     wave_sync();
+    STAMP(L, 16);
     const uint32_t N = *L.nins;
     // children of every parent (CSR over parent slots: element registers, then list heads)
     uint32_t tot = 0;
@@ -423,6 +424,7 @@ __device__ __forceinline__ void rga_order(const SmallLds &L, uint32_t R, uint32_
         if (firstc) L.fc[pi] = (uint16_t)i;
     }
     wave_sync();
+    STAMP(L, 17);
     // Euler tour: down(i) = 2i (value 1), up(i) = 2i+1; list head h = N + listid: 2h, 2h+1 (end)
     const uint32_t E = 2 * (N + nl);
     for (uint32_t i = lane; i < N; i += WAVE) {
@@ -463,6 +465,7 @@ __device__ __forceinline__ void rga_order(const SmallLds &L, uint32_t R, uint32_
         }
         wave_sync();
     }
+    STAMP(L, 18);
     // list sizes -> base positions; pre-order position of every node
     uint32_t lb = 0;
     for (uint32_t l0 = 0; l0 < nl; l0 += WAVE) {
@@ -503,6 +506,7 @@ __device__ __forceinline__ void rga_order(const SmallLds &L, uint32_t R, uint32_
         }
     }
     wave_sync();
+    STAMP(L, 19);
 }
 
 
@@ -956,11 +960,11 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
             const bool has_dup = dupm != 0;
             const bool kl = act && !dup;                            // this lane is its key's first arrival
             uint32_t t = (!kl || never) ? INF : lane;
-            // Documents without duplicates whose changes have at most 4 dependency lanes each
-            // (C4 / C5: at most 2 deps and the predecessor) iterate in registers: the lanes a
-            // change reads are fixed, so each round is 4 cross-lane reads (ds_bpermute) and a
-            // ballot, with no LDS round trip or fence.
-            const bool regdp = HM_HIST_REGS && !has_dup && __ballot(act && __popcll(dall) > 4) == 0;
+            // Documents whose changes have at most 4 dependency lanes each (C4 / C5: at most 2
+            // deps and the predecessor) iterate in registers: the lanes a change reads are fixed,
+            // so each round is 4 cross-lane reads (ds_bpermute) and a ballot, with no LDS round
+            // trip (the copies of a duplicated key still meet in LDS for their minimum).
+            const bool regdp = HM_HIST_REGS && __ballot(act && __popcll(dall) > 4) == 0;
             uint32_t sl0 = lane, sl1 = lane, sl2 = lane, sl3 = lane;
             if (regdp) {
                 u64 m = dall;
@@ -1000,7 +1004,6 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
             uint32_t w = (!kl || t == INF) ? 0xFFFFFFFFu : ((t << 16) | ((t == lane ? 1u : 2u) << 8) | lane);
             bool conv = false;
             if (regdp) {
-                // (no duplicates: every active lane is its key's first arrival, tk = t)
                 const bool queued_copy = act && tk != INF && tk != key && lane < tk;
                 const uint32_t nsl = (uint32_t)__popcll(dall);
                 for (uint32_t it = 0; it <= n + 1; it++) {
@@ -1013,7 +1016,14 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
                     };
                     fold(y0, 0); fold(y1, 1); fold(y2, 2); fold(y3, 3);
                     const uint32_t cand = queued_copy ? ((tk << 16) | ((pc > 0xFEu ? 0xFEu : pc) << 8) | lane) : 0xFFFFFFFFu;
-                    const uint32_t nw = (kl && t != INF && t != lane) ? cand : w;
+                    uint32_t nw = w;
+                    if (has_dup) {                                  // the first copy a pass reaches applies
+                        tm[lane] = 0xFFFFFFFFu;
+                        wave_sync();
+                        if (cand != 0xFFFFFFFFu) lds_min(&tm[key], cand);
+                        wave_sync();
+                        if (kl && t != INF && t != lane) nw = tm[lane];
+                    } else if (kl && t != INF && t != lane) nw = cand;
                     const bool grew = nw != w;
                     w = nw;
                     if (__ballot(grew) == 0) { conv = true; break; }
