@@ -311,6 +311,8 @@ __device__ __forceinline__ u64 stamp_now() {
     return t;
 }
 #define STAMP(L_, i) do { const u64 t_ = stamp_now(); if (threadIdx.x == 0) { (L_).stamps[i] += t_ - (L_).stamps[HM_NSTAMP]; (L_).stamps[HM_NSTAMP] = t_; } } while (0)
+#elif defined(HM_MARKS)
+#define STAMP(L_, i) asm volatile(";HMMARK " #i)          // static instruction census by phase (dev tool)
 #else
 #define STAMP(L_, i) do { } while (0)
 #endif
