@@ -32,7 +32,7 @@ def main():
     nch = b.docs["n_changes"].astype(np.int64)
     pos = np.maximum(nch - a.tail, 0)
     st = RowStore(eng, a_stride=b.a_stride)
-    st.set_incremental(bool(a.incremental))
+    st.set_incremental(a.incremental)          # 2: small list documents too (no cost policy)
     h0 = st.open_n(n)
     S = b.a_stride
     dev = torch.device("cuda", 0)
