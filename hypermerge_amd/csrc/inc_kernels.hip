@@ -849,18 +849,28 @@ __device__ int inc_doc_tiled(const AppendDesc &D, const IncArgs &A, uint4 *ssv, 
 
 // TL: the launch for rounds that need tiles (a separate instantiation: the tile loop around
 // inc_doc costs the common round's register allocation half its occupancy)
+#ifndef HM_INC_KARG_RELOAD
+#define HM_INC_KARG_RELOAD 1 // inc_group_kernel: launch parameters re-read per document (see the kernel)
+#endif
 #ifndef HM_INC_WAVES
 #define HM_INC_WAVES 1       // dev A/B: waves per SIMD the G = 8 / 16 instantiations are compiled for
 #endif
 template <int G, bool TL>
-__global__ __launch_bounds__(256, (G < 64 ? HM_INC_WAVES : 1)) void inc_group_kernel(IncArgs A) {
+__global__ __launch_bounds__(256, (G < 64 ? HM_INC_WAVES : 1)) void inc_group_kernel(IncArgs A_in) {
     constexpr uint32_t NG = 256 / G;
     __shared__ uint4 s_sv[NG][2 * G];
     __shared__ uint2 s_mt[NG][2 * G];
     __shared__ uint32_t s_ls[G == 64 ? NG : 1][G == 64 ? LSCR : 1];   // the list phase's anchors
     const uint32_t grp = threadIdx.x / G, gl = threadIdx.x & (G - 1);
-    const uint32_t n = A.list ? A.list[0] : A.n;
+    const uint32_t n = A_in.list ? A_in.list[0] : A_in.n;
+    // the loop reads the launch parameters through an opaque pointer to the kernarg segment: a
+    // document re-loads the fields it uses (scalar loads) rather than holding them in SGPRs
+    // across the loop, where they were spilled to VGPR lanes (readlane / writelane VALU)
+    typedef __attribute__((address_space(4))) const IncArgs KArgs;
+    KArgs *kp = (KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
     for (uint32_t q = blockIdx.x * NG + grp; q < n; q += gridDim.x * NG) {
+        if (HM_INC_KARG_RELOAD) asm volatile("" : "+s"(kp));
+        const IncArgs &A = HM_INC_KARG_RELOAD ? *(const IncArgs *)kp : A_in;
         const uint32_t di = A.list ? A.list[1 + q] : q;
         const AppendDesc D = A.descs[di];
         const uint32_t route = D.inc & HM_DINC_ROUTE;

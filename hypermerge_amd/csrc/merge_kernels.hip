@@ -75,6 +75,9 @@
 #ifndef HM_PRIO_K2
 #define HM_PRIO_K2 0        // dev A/B: priority through the K2 op scan and survivor tests
 #endif
+#ifndef HM_KARG_RELOAD
+#define HM_KARG_RELOAD 1    // merge_small_kernel: launch parameters re-read per document (see the kernel)
+#endif
 #ifndef HM_HIST_DP
 #define HM_HIST_DP 1        // queued documents: history by the parallel (t, pass, pos) solve before the pass loop
 #endif
@@ -722,13 +725,14 @@ __device__ __forceinline__ void stage_op(const SmallLds &L, uint32_t k, uint32_t
     if (LISTS) L.opelem[k] = a.w;
 }
 template <int OPL, bool LISTS>
-__device__ __forceinline__ void stage_rows(const SmallParams &p, const SmallLds &L, const hm_doc_row &doc, const Rows &r) {
+__device__ __forceinline__ void stage_rows(const SmallParams &p, const SmallLds &L, const hm_doc_row &doc, const Rows &r,
+                                           uint32_t cap_deps) {
     const uint32_t lane = threadIdx.x, m = doc.n_ops;
     stage_op<LISTS>(L, lane, m, r.a0, r.b0);
     if (OPL > 1) stage_op<LISTS>(L, lane + WAVE, m, r.a1, r.b1);
     if (OPL > 2) stage_op<LISTS>(L, lane + 2 * WAVE, m, r.a2, r.b2);
     if (OPL > 3) stage_op<LISTS>(L, lane + 3 * WAVE, m, r.a3, r.b3);
-    const uint32_t nd = doc.n_deps < p.cap_deps ? doc.n_deps : p.cap_deps;
+    const uint32_t nd = doc.n_deps < cap_deps ? doc.n_deps : cap_deps;
     if (lane < nd) L.deps[lane] = pack_dep(r.d0);
     if (lane + WAVE < nd) L.deps[lane + WAVE] = pack_dep(r.d1);
     for (uint32_t i = lane + 2 * WAVE; i < nd; i += WAVE)     // long dep tables: read on demand
@@ -1728,7 +1732,14 @@ void merge_small_kernel(SmallParams p) {
     typedef SizeClass<CLS> C;
     SmallLds L;
     small_carve((LDS uint8_t *)lds_raw, WAVE * OPL, C::NR, C::NO, C::ND, LISTS, true, &L);
-    p.cap_regs = C::NR; p.cap_objs = C::NO; p.cap_deps = C::ND;
+    p.cap_regs = C::NR; p.cap_objs = C::NO; p.cap_deps = C::ND;     // (the loop reads the C:: constants)
+#if HM_KARG_RELOAD
+    // the loop reads the launch parameters through an opaque pointer to the kernarg segment:
+    // each document re-loads the fields it uses (scalar loads) instead of holding ~50 SGPRs of
+    // them across the loop, where they were spilled to VGPR lanes (readlane / writelane VALU)
+    typedef __attribute__((address_space(4))) const SmallParams KParams;
+    KParams *kp = (KParams *)__builtin_amdgcn_kernarg_segment_ptr();
+#endif
     // workgroups are dealt round-robin over the 8 XCDs (speed only, MI355X_MICROARCH.md): give
     // the workgroups of one XCD consecutive documents, so the 128 B lines a document boundary
     // splits in every table are read and written through one L2 instead of two
@@ -1743,11 +1754,15 @@ void merge_small_kernel(SmallParams p) {
     uint2 w0, w1, w2;                        // this document's change row (lane = arrival index)
     {
         const Rows r = load_rows<OPL>(p, doc);
-        stage_rows<OPL, LISTS>(p, L, doc, r);
+        stage_rows<OPL, LISTS>(p, L, doc, r, C::ND);
         w0 = make_uint2(r.c01.x, r.c01.y); w1 = make_uint2(r.c01.z, r.c01.w); w2 = r.c2;
     }
     wave_sync();
     for (;;) {
+#if HM_KARG_RELOAD
+        asm volatile("" : "+s"(kp));
+        const SmallParams &p = *(const SmallParams *)kp;
+#endif
         // software pipeline over this wave's documents: the next document's rows are
         // loaded before this document's stores and staged to LDS after them
         const uint32_t dn = d + gridDim.x;
@@ -1777,8 +1792,8 @@ void merge_small_kernel(SmallParams p) {
         if (more) { take_docn(); dokn = check_doc(p, docn); next = load_rows<OPL>(p, docn); }
 #endif
         const bool in_env = doc.n_changes <= 64 && doc.n_actors <= NA_MAX && doc.n_ops <= WAVE * OPL && doc.n_ops < 256 &&
-                            doc.n_regs <= p.cap_regs && doc.n_objs <= p.cap_objs && doc.n_objs >= 1 &&
-                            doc.n_deps <= p.cap_deps && !p.general_only;
+                            doc.n_regs <= C::NR && doc.n_objs <= C::NO && doc.n_objs >= 1 &&
+                            doc.n_deps <= C::ND && !p.general_only;
         DocState st;
         // output row and minimumClock row requested before the merge: consumed before the next
         // document's rows are requested (min_cmp_of), so neither waits behind that prefetch
@@ -1821,7 +1836,7 @@ void merge_small_kernel(SmallParams p) {
         // staging after the stores waited for all of them; now nothing waits for the stores
         // until the next document's merge has run
         wave_sync();
-        if (more) stage_rows<OPL, LISTS>(p, L, docn, next);
+        if (more) stage_rows<OPL, LISTS>(p, L, docn, next, C::ND);
         STAMP(L, 11);
         write_outputs<OPL, LISTS>(p, L, d, ds, doc, oc, st, mcmp, sv);
         if (HM_PRIO_IO) __builtin_amdgcn_s_setprio(0);
@@ -1839,7 +1854,7 @@ void merge_small_kernel(SmallParams p) {
 #if HM_ASYNC_NEXT
         if constexpr (ASY) next = take_rows_async<OPL>(anext, docn, oc == OUT_OK);
 #endif
-        stage_rows<OPL, LISTS>(p, L, docn, next);
+        stage_rows<OPL, LISTS>(p, L, docn, next, C::ND);
         if (HM_PRIO_IO) __builtin_amdgcn_s_setprio(0);
         wave_sync();
         STAMP(L, 11);

@@ -20,6 +20,9 @@
 #include "../../include/hypermerge_amd.h"
 #include "merge_kernels.h"
 
+#ifndef HML_KARG_RELOAD
+#define HML_KARG_RELOAD 1   // merge_large_kernel: launch parameters re-read per document (see the kernel)
+#endif
 #ifndef HML_WGS_PER_CU
 #define HML_WGS_PER_CU 1   // workgroups per CU: 16 waves per CU split into this many documents
 #endif
@@ -2078,7 +2081,18 @@ __global__ __launch_bounds__(LWG) __attribute__((amdgpu_waves_per_eu(HML_WPE))) 
 #if HM_STAMPS
     if (tid <= HML_NSTAMP) hml_st[tid] = 0;
 #endif
+#if HML_KARG_RELOAD
+    // the loop reads the launch parameters through an opaque pointer to the kernarg segment: a
+    // document re-loads the fields it uses (scalar loads) rather than holding them in SGPRs
+    // across the loop, where they were spilled to VGPR lanes (readlane / writelane VALU)
+    typedef __attribute__((address_space(4))) const SmallParams KParams;
+    KParams *kp = (KParams *)__builtin_amdgcn_kernarg_segment_ptr();
+#endif
     for (;;) {
+#if HML_KARG_RELOAD
+        asm volatile("" : "+s"(kp));
+        const SmallParams &p = *(const SmallParams *)kp;
+#endif
         if (tid == 0) claim = atomicAdd(p.large_cursor, 1u);
         bsync();
         const uint32_t ci = claim;
