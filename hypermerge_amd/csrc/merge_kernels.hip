@@ -75,6 +75,9 @@
 #ifndef HM_PRIO_K2
 #define HM_PRIO_K2 0        // dev A/B: priority through the K2 op scan and survivor tests
 #endif
+#ifndef HM_PUSH_BPERM
+#define HM_PUSH_BPERM 0     // K1b's ancestor push broadcasts through ds_bpermute instead of v_readlane
+#endif
 #ifndef HM_KARG_RELOAD
 #define HM_KARG_RELOAD 1    // merge_small_kernel: launch parameters re-read per document (see the kernel)
 #endif
@@ -1272,10 +1275,18 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         const uint32_t Hs = (uint32_t)__builtin_amdgcn_readfirstlane((int)H);
         const uint32_t Dlo = (uint32_t)D, Dhi = (uint32_t)(D >> 32);
         const uint32_t H1 = Hs < 32 ? Hs : 32;
-#define PUSH_LO(k) alo |= (uint32_t)__builtin_amdgcn_readlane((int)alo, (int)(k)) & (uint32_t)__builtin_amdgcn_sbfe((int)Dlo, (k), 1)
+#if HM_PUSH_BPERM
+        // lane k's set broadcast by ds_bpermute (the LDS pipe) instead of v_readlane (a VALU
+        // instruction and an SGPR hazard): the kernel is VALU-issue bound, the push a quarter of
+        // its VALU instructions
+#define PUSH_BC(v, k) ((uint32_t)__builtin_amdgcn_ds_bpermute((k) << 2, (int)(v)))
+#else
+#define PUSH_BC(v, k) ((uint32_t)__builtin_amdgcn_readlane((int)(v), (int)(k)))
+#endif
+#define PUSH_LO(k) alo |= PUSH_BC(alo, (k)) & (uint32_t)__builtin_amdgcn_sbfe((int)Dlo, (k), 1)
 #define PUSH_HI(k) do { const uint32_t m_ = (uint32_t)__builtin_amdgcn_sbfe((int)Dhi, (k) - 32, 1);          \
-                        alo |= (uint32_t)__builtin_amdgcn_readlane((int)alo, (int)(k)) & m_;              \
-                        ahi |= (uint32_t)__builtin_amdgcn_readlane((int)ahi, (int)(k)) & m_; } while (0)
+                        const uint32_t bl_ = PUSH_BC(alo, (k)), bh_ = PUSH_BC(ahi, (k));                   \
+                        alo |= bl_ & m_; ahi |= bh_ & m_; } while (0)
         // Fully unrolled with immediate lane indices (no scalar index arithmetic per step), one
         // wave-uniform check per group of 8.  Steps at positions >= H are no-ops: those lanes
         // hold no ancestors and no lane depends on them.  (A blocked variant — 4 positions per
@@ -1294,6 +1305,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
         }
 #undef PUSH_LO
 #undef PUSH_HI
+#undef PUSH_BC
         if (HM_PRIO_PUSH) __builtin_amdgcn_s_setprio(0);
     }
     const u64 anc = hv ? ((((u64)ahi << 32) | alo) & ~(1ull << lane)) : 0ull;   // strict ancestors
