@@ -335,3 +335,40 @@ def test_float_counters_random(engine, engine_general, wide):
     assert (o.docs["status"] == 0).sum() > 250
     assert_same(b, engine.merge(b), o)
     assert_same(b, engine_general.merge(b), o)
+
+
+def _wide_dep_docs(n_docs, seed):
+    """Random causal documents whose changes list up to 6 deps (plus the implicit predecessor),
+    delivered shuffled with duplicate copies: documents with more than 4 dependency lanes per
+    change take the LDS fixpoint of the queued-history solve, the rest its register form."""
+    from hypermerge_amd.columnar import ROOT_ID as R
+    rng = np.random.default_rng(seed)
+    docs = []
+    for _ in range(n_docs):
+        na = int(rng.integers(2, 8))
+        actors = [f"{a:02x}" * 4 for a in rng.choice(256, na, replace=False)]
+        seq = {a: 0 for a in actors}
+        order = []
+        for _ in range(int(rng.integers(4, 40))):
+            a = actors[int(rng.integers(na))]
+            seq[a] += 1
+            others = [x for x in actors if x != a and seq[x] > 0]
+            k = int(rng.integers(0, len(others) + 1)) if others else 0
+            deps = {x: int(rng.integers(1, seq[x] + 1)) for x in rng.permutation(others)[:k]}
+            order.append(_qc(a, seq[a], deps, f"k{int(rng.integers(4))}"))
+        rng.shuffle(order)
+        for _ in range(int(rng.integers(0, 3))):                  # duplicate copies
+            order.insert(int(rng.integers(len(order) + 1)), order[int(rng.integers(len(order)))])
+        docs.append(order[:64])
+    return docs
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_queued_history_wide_deps(engine, seed):
+    """The queued-change history with 1-7 dependency lanes per change, shuffled, with copies:
+    bit-exact with the oracle whichever form (registers / LDS) the solve takes."""
+    b = encode(_wide_dep_docs(400, seed))
+    g, o = engine.merge(b), O.merge(b)
+    assert_same(b, g, o)
+    arrival = np.concatenate([np.arange(k) for k in b.docs["n_changes"]])
+    assert (o.hist != arrival).sum() > 1000                   # most documents queue changes on the way
