@@ -123,7 +123,7 @@ def main() -> int:
     ap.add_argument("--no-node", action="store_true",
                     help="skip the Node DocBackend leg (C2 sample: JS restatement vs the GPU drop-in)")
     ap.add_argument("--node-docs", type=int, default=20000)
-    ap.add_argument("--node-text-docs", type=int, default=40, help="C3 documents of the Node leg (0: skip)")
+    ap.add_argument("--node-text-docs", type=int, default=1000, help="C3 documents of the Node leg (0: skip)")
     ap.add_argument("--node-c5-docs", type=int, default=5000, help="C5 documents of the Node leg (0: skip)")
     ap.add_argument("--text-docs", type=int, default=10000, help="C3 documents in the resident text leg")
     ap.add_argument("--c5-docs", type=int, default=100000, help="C5 documents in the resident nested-document leg (0: skip)")
