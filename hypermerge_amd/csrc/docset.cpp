@@ -1500,13 +1500,18 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
         rc = hm_store_read_history(ds->stores[c], m, hh.data(), from.data(), to.data(), off.data(), hlog[c].data(), had[c].data());
         if (rc) return fail_call(rc);
     }
-    // commit: every successful document's host state advances with the device's
-    for (uint32_t i = 0; i < n; i++) {
+    mark("read history");
+    // commit: every successful document's host state advances with the device's (a call lists a
+    // document once, so the documents advance in parallel; the released handles of moved documents
+    // go to the shared lists first)
+    for (uint32_t i = 0; i < n; i++)
+        if (R[i].status == HM_OK && R[i].moved) { const DocSt &d = ds->doc(R[i].doc); rel[d.cls].push_back(d.handle); }
+    par_for(n, T, [&](uint32_t lo, uint32_t hi, uint32_t) {
+    for (uint32_t i = lo; i < hi; i++) {
         Round &x = R[i];
         if (x.status != HM_OK) continue;
         DocSt &d = ds->doc(x.doc);
         const uint32_t old_n_ops = d.n_ops;
-        if (x.moved) rel[d.cls].push_back(d.handle);
         d.cls = x.cls; d.handle = x.handle;
         d.flags |= x.flags;
         d.n_changes += (uint32_t)x.ch.size();
@@ -1530,6 +1535,7 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
             d.el_blk.resize(x.n_regs, HM_NONE);
         }
     }
+    });
     release();
     mark("read regs");
     // render every document's patch and DocBackend.clock
@@ -1650,12 +1656,15 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
         // doc_word_off / doc_str_base / doc_num_base u32[n_docs + 1] each, str_off u32[n_strings + 1]
         // (byte offsets into the blob), words u32[n_words], (8-aligned) nums f64[n_nums], blob
         std::vector<uint32_t> wo(n + 1, 0), sb(n + 1, 0), nb(n + 1, 0);
-        uint64_t blob = 0;
+        std::vector<uint64_t> bo(n + 1, 0);                  // each document's first blob byte
         for (uint32_t i = 0; i < n; i++) {
             const BinDoc &x = R[i].bin;
             wo[i + 1] = wo[i] + (uint32_t)x.w.size(); sb[i + 1] = sb[i] + (uint32_t)x.strs.size(); nb[i + 1] = nb[i] + (uint32_t)x.nums.size();
-            for (auto &t : x.strs) blob += t.second;
+            uint64_t b = 0;
+            for (auto &t : x.strs) b += t.second;
+            bo[i + 1] = bo[i] + b;
         }
+        const uint64_t blob = bo[n];
         const uint32_t ns = sb[n], nw = wo[n], nn = nb[n];
         size_t head = 4 * (8 + 3 * ((size_t)n + 1) + (size_t)ns + 1 + nw);
         const size_t pad = (8 - head % 8) % 8;
@@ -1672,20 +1681,26 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
         double *nums = (double *)(&s[0] + head + pad);
         char *bl = &s[0] + head + pad + 8 * (size_t)nn;
         so[0] = 0;
-        uint32_t k = 0;
-        uint64_t at = 0;
-        bool ascii = true;
-        for (uint32_t i = 0; i < n; i++) {
-            const BinDoc &x = R[i].bin;
-            if (!x.w.empty()) memcpy(words + wo[i], x.w.data(), 4 * x.w.size());
-            if (!x.nums.empty()) memcpy(nums + nb[i], x.nums.data(), 8 * x.nums.size());
-            for (auto &t : x.strs) {
-                memcpy(bl + at, t.first, t.second);
-                for (uint32_t c = 0; c < t.second && ascii; c++) ascii = (unsigned char)t.first[c] < 0x80;
-                at += t.second;
-                so[++k] = (uint32_t)at;
+        // documents copied in parallel: every one has its own word / number / string ranges
+        std::atomic<bool> ascii{true};
+        par_for(n, std::min<uint32_t>(ds->threads, std::max<uint32_t>(1, n / 256)), [&](uint32_t lo, uint32_t hi, uint32_t) {
+            bool asc = true;
+            for (uint32_t i = lo; i < hi; i++) {
+                const BinDoc &x = R[i].bin;
+                if (!x.w.empty()) memcpy(words + wo[i], x.w.data(), 4 * x.w.size());
+                if (!x.nums.empty()) memcpy(nums + nb[i], x.nums.data(), 8 * x.nums.size());
+                uint64_t at = bo[i];
+                uint32_t k = sb[i];
+                for (auto &t : x.strs) {
+                    memcpy(bl + at, t.first, t.second);
+                    if (asc)
+                        for (uint32_t c = 0; c < t.second; c++) asc &= (unsigned char)t.first[c] < 0x80;
+                    at += t.second;
+                    so[++k] = (uint32_t)at;
+                }
             }
-        }
+            if (!asc) ascii = false;
+        });
         h[6] = ascii ? 1 : 0;
     } else {
         // {"p": [patch | null per document], "b": [max over the whole log | null], "c": [max over this call's changes | null]}

@@ -589,7 +589,7 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
         else sh.otype[obj] = dec_act(w);
     }
     // ---- assign lists: r_seg = exclusive offsets, advanced to the segment ends by the fill ----
-    const uint32_t tot2 = scan_into(sh, r_segcnt, r_seg, R);
+    (void)scan_into(sh, r_segcnt, r_seg, R);
     for (uint32_t k = tid; k < m; k += LWG) {
         const uint32_t w = o_w[k], a = dec_act(w);
         if (a < HM_SET || a > HM_INC || dec_obj(w) >= O) continue;     // exactly the ops r_segcnt counted
@@ -715,7 +715,7 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
         const uint32_t N = sh.nins;
         bsync();
         const uint32_t nl = sh.total;
-        const uint32_t tp = scan_into(sh, p_cnt, p_off, NP);
+        (void)scan_into(sh, p_cnt, p_off, NP);
         for (uint32_t i = tid; i < N; i += LWG) {
             const uint32_t pi = n_pi[i];
             if (p_cnt[pi] > 1) n_pl[atomicAdd(&p_off[pi], 1u)] = (uint16_t)i;
