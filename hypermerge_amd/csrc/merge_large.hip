@@ -788,8 +788,7 @@ __device__ __forceinline__ int l34_res(const SmallParams &p, Shared &sh, LDS uin
         auto pos_of = [&](uint32_t i, uint32_t l) -> uint32_t { return sh.listbase[l] + tsum(2 * (N + l)) - tsum(2 * i); };
         for (uint32_t i = tid; i < N; i += LWG) vis[pos_of(i, n_list[i])] = r_scnt[n_reg[i]] > 0 ? 1u : 0u;
         bsync();
-        uint32_t tv;
-        tv = scan_array(sh, vis, N);
+        (void)scan_array(sh, vis, N);
         for (uint32_t i = tid; i < N; i += LWG) {
             const uint32_t l = n_list[i], rg = n_reg[i];
             r_ins[rg] = r_scnt[rg] > 0 ? vis[pos_of(i, l)] - vis[sh.listbase[l]] : 0xFFFFFFFFu;
@@ -1664,8 +1663,7 @@ __device__ HML_DOC_ATTR Outcome merge_doc_large(const SmallParams &p, Shared &sh
         if (c > SEG_SHORT) for (uint32_t a = 0; a < A; a++) X.segmax[(size_t)i * A + a] = 0;
     }
     bsync();
-    uint32_t tot2;
-    tot2 = scan_array(sh, X.segoff, R);
+    (void)scan_array(sh, X.segoff, R);
     for (uint32_t k = tid; k < m; k += LWG) {
         const OpC o = op_c(k);
         if (o.action < HM_SET || o.action > HM_INC || o.obj >= O) continue;   // exactly the ops segcnt counted
@@ -1931,8 +1929,7 @@ __device__ HML_DOC_ATTR Outcome merge_doc_large(const SmallParams &p, Shared &sh
         const uint32_t N = sh.nins;
         for (uint32_t i = tid; i < NP; i += LWG) X.poff[i] = X.pcount[i];
         bsync();
-        uint32_t tp;
-        tp = scan_array(sh, X.poff, NP);
+        (void)scan_array(sh, X.poff, NP);
         // sibling lists (an only child needs none: no next sibling, first child of its parent)
         for (uint32_t i = tid; i < N; i += LWG) {
             const uint32_t pi = X.nodepi[i];
@@ -2015,14 +2012,12 @@ __device__ HML_DOC_ATTR Outcome merge_doc_large(const SmallParams &p, Shared &sh
             if (isl) X.listbase[X.listid[o]] = tsum(2 * (N + X.listid[o]));
         }
         bsync();
-        uint32_t tl;
-        tl = scan_array(sh, X.listbase, nl);
+        (void)scan_array(sh, X.listbase, nl);
         // pre-order position of node i: its list's base + (entries of its list) - (entries from i on)
         auto pos_of = [&](uint32_t i, uint32_t l) -> uint32_t { return X.listbase[l] + tsum(2 * (N + l)) - tsum(2 * i); };
         for (uint32_t i = tid; i < N; i += LWG) X.vis[pos_of(i, X.nlist[i])] = X.survcnt[X.nreg[i]] > 0 ? 1u : 0u;
         bsync();
-        uint32_t tv;
-        tv = scan_array(sh, X.vis, N);             // exclusive scan of visibility over pre-order positions
+        (void)scan_array(sh, X.vis, N);            // exclusive scan of visibility over pre-order positions
         for (uint32_t i = tid; i < N; i += LWG) {
             const uint32_t l = X.nlist[i], rg = X.nreg[i];
             // list elements carry their visible index (or -1) in insmin from here on
