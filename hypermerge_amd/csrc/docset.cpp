@@ -1536,6 +1536,7 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
         }
     }
     });
+    mark("commit");
     release();
     mark("read regs");
     // render every document's patch and DocBackend.clock
