@@ -73,7 +73,7 @@
 #define HM_PRIO_RANK 2      // through the survivor offsets, ranks and ties: C4 2.42 -> 2.39 ms
 #endif
 #ifndef HM_PRIO_K2
-#define HM_PRIO_K2 0        // dev A/B: priority through the K2 op scan and survivor tests
+#define HM_PRIO_K2 2        // through the K2 op scan and survivor tests: C4 2.22 -> 2.16 ms, actor-major 3.32 -> 3.28, C5 0.630 -> 0.621 (r05 ab_prio2)
 #endif
 #ifndef HM_PUSH_BPERM
 #define HM_PUSH_BPERM 0     // K1b's ancestor push broadcasts through ds_bpermute instead of v_readlane
