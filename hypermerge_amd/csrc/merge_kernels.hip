@@ -72,6 +72,9 @@
 #ifndef HM_PRIO_RANK
 #define HM_PRIO_RANK 2      // through the survivor offsets, ranks and ties: C4 2.42 -> 2.39 ms
 #endif
+#ifndef HM_PRIO_K3
+#define HM_PRIO_K3 0        // dev A/B: priority through K3 (list order)
+#endif
 #ifndef HM_PRIO_K2
 #define HM_PRIO_K2 2        // through the K2 op scan and survivor tests: C4 2.22 -> 2.16 ms, actor-major 3.32 -> 3.28, C5 0.630 -> 0.621 (r05 ab_prio2)
 #endif
@@ -1533,8 +1536,11 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     STAMP(L, 8);
     if (HM_ABLATE & 256) return OUT_UNSUPPORTED;
     if constexpr (LISTS) {
-        if (doc_lists) rga_order<OPL>(L, R, O, oreg, oobj, opar, oact, oelem, oarr, oh,
-                                      p.res_epos ? p.res_epos + doc.reg_off : nullptr);
+        if (doc_lists) {
+            if (HM_PRIO_K3) __builtin_amdgcn_s_setprio(HM_PRIO_K3);
+            rga_order<OPL>(L, R, O, oreg, oobj, opar, oact, oelem, oarr, oh, p.res_epos ? p.res_epos + doc.reg_off : nullptr);
+            if (HM_PRIO_K3) __builtin_amdgcn_s_setprio(0);
+        }
     }
     // counters: an inc adds to every surviving counter set that is its ancestor.
     // JS numbers: an integer counter is exact only while |base| + sum|inc| <= 2^53; with at
