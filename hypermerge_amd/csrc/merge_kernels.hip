@@ -72,6 +72,9 @@
 #ifndef HM_PRIO_RANK
 #define HM_PRIO_RANK 2      // through the survivor offsets, ranks and ties: C4 2.42 -> 2.39 ms
 #endif
+#ifndef HM_PRIO_FOLD
+#define HM_PRIO_FOLD 0      // dev A/B: the push's priority held through the fold check and table init
+#endif
 #ifndef HM_PRIO_K3
 #define HM_PRIO_K3 0        // dev A/B: priority through K3 (list order)
 #endif
@@ -1309,7 +1312,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
 #undef PUSH_LO
 #undef PUSH_HI
 #undef PUSH_BC
-        if (HM_PRIO_PUSH) __builtin_amdgcn_s_setprio(0);
+        if (HM_PRIO_PUSH && !HM_PRIO_FOLD) __builtin_amdgcn_s_setprio(0);
     }
     const u64 anc = hv ? ((((u64)ahi << 32) | alo) & ~(1ull << lane)) : 0ull;   // strict ancestors
     if (hv) L.anc[lane] = anc;
@@ -1351,6 +1354,7 @@ __device__ __forceinline__ Outcome merge_doc_small(const SmallParams &p, const S
     wave_sync();
 
     STAMP(L, 5);
+    if (HM_PRIO_FOLD && !HM_PRIO_K2) __builtin_amdgcn_s_setprio(0);
     if (HM_PRIO_K2) __builtin_amdgcn_s_setprio(HM_PRIO_K2);
     if (HM_ABLATE & 2) return OUT_UNSUPPORTED;
     // ---------------- K2: ops (lane + 64*t) ----------------
