@@ -1273,6 +1273,7 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
         bool sub = false, done = false;                      // submitted / waited (applied on the device)
     };
     std::vector<ClsOut> co(N_CLASS);
+    uint64_t call_routing[3] = {0, 0, 0};                      // this call's routing (ds->routing once it commits)
     int rc = HM_OK;
     // fault injection for the tests (HM_DOCSET_INJECT_FAIL=wait:<k> fails the call after the k-th
     // class's batch is applied, =read after every class's; the call must then be undone everywhere)
@@ -1372,7 +1373,7 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
         {
             uint32_t r3[3] = {0, 0, 0};
             if (hm_store_last_routing(st, r3) == HM_OK)
-                for (int k = 0; k < 3; k++) ds->routing[k] += r3[k];
+                for (int k = 0; k < 3; k++) call_routing[k] += r3[k];     // (counted once the call commits)
         }
         if (n_waited++ == inj_wait) { rc = hm_engine_fail(ds->e, HM_ERR_DEVICE, "injected failure (HM_DOCSET_INJECT_FAIL)"); break; }
         for (uint32_t k = 0; k < rows.size(); k++) {
@@ -1536,6 +1537,7 @@ int apply(hm_docset *ds, const uint8_t *data, const uint64_t *bo, const uint32_t
         }
     }
     });
+    for (int k = 0; k < 3; k++) ds->routing[k] += call_routing[k];
     mark("commit");
     release();
     mark("read regs");

@@ -111,6 +111,7 @@ struct hm_store {
     uint32_t st_inc = 0, st_cold = 0, st_bail = 0;
     // HIP events around the last submit's incremental kernels and its re-merge (engine stream)
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    bool ev_live = false;                    // ev[] recorded by the pending submit, not read yet
     float last_ms[2] = {0.f, 0.f};
 };
 
@@ -620,9 +621,7 @@ static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handl
         SCHK(s, hipEventRecord(s->ev[2], st));
         if ((rc = launch_list_merge(s, s->list.p, counts[0] + counts[1]))) return rc;
         SCHK(s, hipEventRecord(s->ev[3], st));
-        SCHK(s, hipEventSynchronize(s->ev[3]));
-        SCHK(s, hipEventElapsedTime(&s->last_ms[0], s->ev[0], s->ev[1]));
-        SCHK(s, hipEventElapsedTime(&s->last_ms[1], s->ev[2], s->ev[3]));
+        s->ev_live = true;           // (read by hm_batch_wait after its stream sync: submit stays asynchronous)
         dbg_list_state(s, "after merge");
         T.mark("remerge");
         s->st_inc = P.n_inc - counts[1]; s->st_cold = counts[0]; s->st_bail = counts[1];
@@ -716,6 +715,13 @@ static int wait_impl(hm_store *s, uint64_t batch_id, hm_doc_result *out_docs, ui
             SCHK(s, hipStreamSynchronize(st));
         }
         T.mark("wait copy-out");
+        if (s->ev_live) {
+            // the submit's kernel intervals (hm_store_last_kernel_ms), complete after the sync above
+            SCHK(s, hipEventSynchronize(s->ev[3]));
+            SCHK(s, hipEventElapsedTime(&s->last_ms[0], s->ev[0], s->ev[1]));
+            SCHK(s, hipEventElapsedTime(&s->last_ms[1], s->ev[2], s->ev[3]));
+            s->ev_live = false;
+        }
         // roll back documents whose merge threw (or left the envelope): the log returns to its
         // previous length (rows stay where they are), ranks are re-ranked back, and the previous
         // state is re-merged

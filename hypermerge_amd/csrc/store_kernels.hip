@@ -333,8 +333,11 @@ __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
     // busy for longer than the document's re-merge)
     const bool lists = ((r.flags | m.flags) & HM_DOC_HAS_LISTS) != 0;
     const bool small = r.n_changes <= HM_INC_MAX_NEW_C && r.n_ops <= HM_INC_MAX_NEW_O && tgt <= HM_INC_MAX_TGT;
-    const bool lane = !small && a.S <= 16 && !lists && r.n_changes <= HM_INC_LANE_MAX_C && r.n_ops <= HM_INC_LANE_MAX_O;
-    const bool longr = lane || (!small && (lists || a.S > 16) && r.n_changes <= HM_INC_TILED_MAX_C &&
+    // (the lane pass is instantiated for row strides 8 and 16 only: its template stride addresses the
+    // clock / heads / allDeps rows, so any other stride takes the tiles of the group passes)
+    const bool lane = !small && (a.S == 8 || a.S == 16) && !lists && r.n_changes <= HM_INC_LANE_MAX_C &&
+                      r.n_ops <= HM_INC_LANE_MAX_O;
+    const bool longr = lane || (!small && (lists || (a.S != 8 && a.S != 16)) && r.n_changes <= HM_INC_TILED_MAX_C &&
                                 r.n_ops <= HM_INC_TILED_MAX_O);     // (tiles of the group / wave passes)
     bool inc = live && a.incremental && last.status == HM_OK && last.n_queued == 0 && !remapped && r.n_changes > 0 &&
                (small || longr) && m.n_r <= r.n_regs && r.n_actors <= a.S;

@@ -355,7 +355,8 @@ int hm_store_set_incremental(hm_store *s, int on);
 int hm_store_last_routing(const hm_store *s, uint32_t *out3);
 /* Device time of the last submit, from HIP events on the engine stream: out2[0] = the
  * incremental kernels (lane / group / wave passes), out2[1] = the re-merge of the documents
- * they did not take (row build, merge kernels, metadata), in ms. */
+ * they did not take (row build, merge kernels, metadata), in ms; read once hm_batch_wait(_device)
+ * has returned for that submit (the submit itself does not wait for its kernels). */
 int hm_store_last_kernel_ms(const hm_store *s, float *out2);
 
 /* Sizes of a document's log and merged state. */

@@ -79,3 +79,54 @@ def test_gpus_disagreeing_with_world_size_exits_nonzero():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "1"],
                        capture_output=True, text=True, env=env, timeout=300)
     assert p.returncode != 0 and "WORLD_SIZE" in p.stderr
+
+
+def test_visible_gpus_reads_env_then_kfd_topology(tmp_path):
+    b = _bench()
+    assert b.visible_gpus({"HIP_VISIBLE_DEVICES": "0,3"}, sysfs=str(tmp_path)) == 2
+    assert b.visible_gpus({"ROCR_VISIBLE_DEVICES": ""}, sysfs=str(tmp_path)) == 0
+    for i, simds in enumerate([0, 1024, 1024, 0, 1024]):      # CPU nodes report simd_count 0
+        d = tmp_path / str(i)
+        d.mkdir()
+        (d / "properties").write_text(f"cpu_cores_count 64\nsimd_count {simds}\nmax_waves_per_simd 8\n")
+    assert b.visible_gpus({}, sysfs=str(tmp_path)) == 3
+    assert b.visible_gpus({}, sysfs=str(tmp_path / "missing")) == 0
+
+
+def test_the_launcher_parent_never_imports_torch():
+    """--gpus N without a launcher counts devices from the KFD topology before `import torch`."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    code = ("import runpy, sys; sys.argv = ['bench.py', '--gpus', '2']\n"
+            "try:\n    runpy.run_path(%r, run_name='__main__')\nexcept SystemExit:\n    pass\n"
+            "print('TORCH' if 'torch' in sys.modules else 'NOTORCH')" % os.path.join(ROOT, "bench.py"))
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
+    assert p.stdout.strip().endswith("NOTORCH"), p.stdout + p.stderr
+
+
+def test_compact_line_from_the_round5_record():
+    """The driver parses the last line of the bench's output: the round-5 record (21 KB as one
+    line) must compact below 4 KB with the headline, roofline and CPU baseline intact."""
+    import json
+    b = _bench()
+    full = json.load(open(os.path.join(ROOT, "profiles", "r05", "final4", "bench_line.json")))
+    full["detail_file"] = "gpurun_out/bench_detail.json"
+    s = b.dump_line(full)
+    assert len(s) < 2048 and "\n" not in s
+    line = json.loads(s)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "config", "dtype",
+              "roofline", "cpu_baseline", "cpu_parallel", "parity_sample_ok", "clock_exchange", "legs"):
+        assert k in line, k
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert line["roofline"][k] is not None, k
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert line["cpu_baseline"][k] is not None, k
+    assert abs(line["value"] - full["value"]) / full["value"] < 1e-5
+    assert abs(line["roofline"]["frac"] - full["roofline"]["frac"]) < 1e-5
+    assert set(line["legs"]) >= {"end_to_end", "from_blocks", "resident_c4", "resident_c3", "resident_c5",
+                                 "node", "actor_major"}
+    assert line["legs"]["node"]["C2"]["vs_js"] > 1
+    assert line["legs"]["resident_c4"]["speedup"] > 1
+    # an oversized record still prints a parseable line below the cap
+    full["legs_padding"] = "x" * 10
+    big = dict(full, resident_incremental=dict(full["resident_incremental"], value=1.0))
+    assert len(b.dump_line(big)) < 4096

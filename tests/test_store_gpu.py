@@ -242,6 +242,11 @@ def test_bad_remap_leaves_store_unchanged(engine):
     ("C2", 150, {}, 24, 0.9, 8),                           # counters, up to 24 changes per call
     ("FC", 60, {}, 16, True, 8),                           # integral / f64 counters, shuffled arrivals
     ("C4", 120, {}, 16, 0.9, 16),
+    # strides the lane pass is not instantiated for (it addresses rows with its template stride):
+    # long rounds take the group passes' tiles, short ones the group pass at its own stride
+    ("C2", 100, {}, 16, True, 5),
+    ("C4", 100, {}, 16, True, 12),
+    ("C4", 100, {}, 2, 0.9, 12),
     # ... and in tiles of the group / wave passes: list and text documents, strides over 16
     ("C3", 20, {"changes_per_actor": 120}, 20, True, 8),       # (new actors mid-way re-rank: re-merge)
     ("C5", 100, {}, 12, True, 8),
@@ -589,3 +594,32 @@ def test_incremental_text_edits_equal_remerge_and_oracle(engine):
         _, gb = B.read(hb)
         np.testing.assert_array_equal(g.regs, gb.regs, err_msg=f"round {i}")
     assert sum(routed[1:]) >= len(rounds) - 3, routed          # the sorts-later insert re-merges
+
+
+def test_default_cost_rule_on_long_c4_rounds_matches_oracle(engine):
+    """The default routing (mode 1) sends a round whose new rows exceed 1/HM_INC_COST of the log to
+    the re-merge and shorter ones to the incremental passes: C4 documents fed rounds of 1-24
+    changes (both sides of the rule in one call) stay bit-exact with the oracle's cold merge of
+    their log after every call, and both routes are taken."""
+    b = synth.generate(synth.config("C4", n_docs=300))
+    docs = [decode_doc(b, i) for i in range(b.n_docs)]
+    rng = np.random.default_rng(23)
+    store = DocStore(engine, a_stride=8)            # (incremental mode 1: the default)
+    hs = [store.open() for _ in docs]
+    pos = [24] * len(docs)
+    r = store.apply([(h, docs[i][:24]) for i, h in enumerate(hs)])
+    assert (r.docs["status"] == 0).all()
+    routed = {"incremental": 0, "remerged": 0, "handed_back": 0}
+    while any(p < len(c) for p, c in zip(pos, docs)):
+        take = {i: int(rng.choice([1, 2, 12, 24])) for i in range(len(docs)) if pos[i] < len(docs[i])}
+        r = store.apply([(hs[i], docs[i][pos[i]:pos[i] + k]) for i, k in take.items()])
+        assert (r.docs["status"] == 0).all()
+        for k, v in store.last_routing().items():
+            routed[k] += v
+        for i, k in take.items():
+            pos[i] += k
+        for i in list(take)[::5]:
+            assert_doc_matches_oracle(store, hs[i])
+    assert routed["incremental"] > 0 and routed["remerged"] > 0, routed
+    for h in hs:
+        assert_doc_matches_oracle(store, h)
