@@ -862,6 +862,7 @@ __global__ __launch_bounds__(256, (G < 64 ? HM_INC_WAVES : 1)) void inc_group_ke
     __shared__ uint2 s_mt[NG][2 * G];
     __shared__ uint32_t s_ls[G == 64 ? NG : 1][G == 64 ? LSCR : 1];   // the list phase's anchors
     const uint32_t grp = threadIdx.x / G, gl = threadIdx.x & (G - 1);
+    if (!A_in.list && A_in.pst && A_in.pst->n_inc == 0) return;     // (a submit with nothing incremental)
     const uint32_t n = A_in.list ? A_in.list[0] : A_in.n;
     // the loop reads the launch parameters through an opaque pointer to the kernarg segment: a
     // document re-loads the fields it uses (scalar loads) rather than holding them in SGPRs
@@ -1273,6 +1274,7 @@ __device__ __forceinline__ void lane_list_push(uint32_t *list, bool p, uint32_t 
 
 template <int S>
 __global__ __launch_bounds__(256) void inc_lane_kernel(IncArgs A) {
+    if (A.pst && A.pst->mx[0] == 0) return;                   // (no document routed to this pass)
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     int rc = -1;
     uint32_t hnd = 0;
@@ -1307,19 +1309,32 @@ __device__ __forceinline__ uint32_t change_of_op(const hm_change_row *ch, uint32
 // directory ldir = (object, elements) per list.
 // Documents that are not clean (an error, queued changes) get flags = 0: their next submit
 // re-merges.
+__device__ __forceinline__ bool meta_skip(const MetaArgs &a, const DevDoc &m, const hm_doc_result &r) {
+    // (mode 1: a small document with lists re-merges every round — one small-kernel wave either
+    // way — so it keeps no incremental state at all)
+    return r.status != HM_OK || r.n_queued != 0 || r.n_surv > m.o_cap ||
+           ((m.flags & HM_DOC_HAS_LISTS) && m.n_o <= a.small_lists);
+}
+
 __global__ __launch_bounds__(256) void inc_meta_kernel(MetaArgs a) {
     const uint32_t lane = threadIdx.x & 63;
-    for (uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6); q < a.n; q += gridDim.x * 4) {
-        const uint32_t h = a.list[q];
+    // a wave takes 64 listed documents: one lane each decides whether the document keeps state
+    // (the documents that keep none — errors, queued changes, mode 1's small list documents,
+    // often every document of a C5 round — cost one lane, not a wave), then the wave builds the
+    // state of the others one after the other
+    for (uint32_t q0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 64; q0 < a.n; q0 += gridDim.x * 4 * 64) {
+        const uint32_t qi = q0 + lane;
+        bool keep = false;
+        uint32_t hl = 0;
+        if (qi < a.n) {
+            hl = a.list[qi];
+            keep = !meta_skip(a, a.dm[hl], a.res_docs[hl]);
+            if (!keep) { IncState z = {}; a.ist[hl] = z; }
+        }
+        for (unsigned long long km = __ballot(keep); km; km &= km - 1) {
+        const uint32_t h = (uint32_t)__shfl((int)hl, (int)__builtin_ctzll(km));
         const DevDoc m = a.dm[h];
         const hm_doc_result r = a.res_docs[h];
-        // (mode 1: a small document with lists re-merges every round — one small-kernel wave either
-        // way — so it keeps no incremental state at all)
-        if (r.status != HM_OK || r.n_queued != 0 || r.n_surv > m.o_cap ||
-            ((m.flags & HM_DOC_HAS_LISTS) && m.n_o <= a.small_lists)) {
-            if (lane == 0) { IncState z = {}; a.ist[h] = z; }
-            continue;
-        }
         const hm_change_row *ch = a.changes + m.c_off;
         for (uint32_t i = lane; i < r.n_surv; i += 64) {
             const uint32_t op = a.surv[m.o_off + i].op;
@@ -1437,6 +1452,7 @@ __global__ __launch_bounds__(256) void inc_meta_kernel(MetaArgs a) {
             st.pad[0] = (flags & HM_IST_LIST) ? n_el : 0u; st.pad[1] = (flags & HM_IST_LIST) ? nlst : 0u;
             a.ist[h] = st;
         }
+        }
     }
 }
 
@@ -1455,11 +1471,10 @@ hipError_t hm_launch_inc_apply(const IncArgs &A, hipStream_t s) {
     if (!A.n) return hipSuccess;
     const uint32_t S = A.S;
     if (S > 64) return hipErrorInvalidValue;
-    // (the defer list's count was zeroed before alloc_kernel, which lists the list documents)
-    hipError_t z = hipMemsetAsync(A.bail, 0, 4, s);
-    if (z != hipSuccess) return z;
+    // (the defer and bail lists' counts were zeroed by plan_kernel: alloc_kernel lists the list
+    // documents in defer)
     auto grid = [](uint32_t n, uint32_t per) { const uint32_t g = (n + per - 1) / per; return g < 65535u ? g : 65535u; };
-    if (S <= 16 && A.n_lane) {
+    if (S <= 16 && A.n_lane) {                                // (n_lane: the pass may have work; it checks on the device)
         // rounds longer than the group passes hold (route 3): one lane per document, first
         const uint32_t gl = (A.n + 255) / 256;
         if (S <= 8) hipLaunchKernelGGL(hmi::inc_lane_kernel<8>, dim3(gl), dim3(256), 0, s, A);
@@ -1487,7 +1502,7 @@ hipError_t hm_launch_inc_apply(const IncArgs &A, hipStream_t s) {
 
 hipError_t hm_launch_inc_meta(const MetaArgs &a, hipStream_t s) {
     if (!a.n) return hipSuccess;
-    const uint32_t grid = (a.n + 3) / 4 < 65535u ? (a.n + 3) / 4 : 65535u;
+    const uint32_t waves = (a.n + 63) / 64, grid = (waves + 3) / 4 < 65535u ? (waves + 3) / 4 : 65535u;
     hipLaunchKernelGGL(hmi::inc_meta_kernel, dim3(grid), dim3(256), 0, s, a);
     return hipGetLastError();
 }

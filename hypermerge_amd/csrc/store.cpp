@@ -111,6 +111,10 @@ struct hm_store {
     uint32_t st_inc = 0, st_cold = 0, st_bail = 0;
     // HIP events around the last submit's incremental kernels and its re-merge (engine stream)
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // page-locked host words the submit's small read-backs land in (a pageable destination makes
+    // each copy a staged, synchronous one): the plan stats, then the re-merge counts
+    PlanStats *h_st = nullptr;
+    uint32_t *h_cnt = nullptr;
     bool ev_live = false;                    // ev[] recorded by the pending submit, not read yet
     float last_ms[2] = {0.f, 0.f};
 };
@@ -151,15 +155,16 @@ PlanStats read_stats(hm_store *s, int *rc) {
     PlanStats st;
     memset(&st, 0, sizeof st);
     hipStream_t q = hm_engine_stream(s->e);
-    if (hipMemcpyAsync(&st, s->st, sizeof st, hipMemcpyDeviceToHost, q) != hipSuccess || hipStreamSynchronize(q) != hipSuccess)
+    if (hipMemcpyAsync(s->h_st, s->st, sizeof st, hipMemcpyDeviceToHost, q) != hipSuccess || hipStreamSynchronize(q) != hipSuccess)
         *rc = hm_engine_fail(s->e, HM_ERR_DEVICE, "reading the submit plan");
+    else
+        st = *s->h_st;
     return st;
 }
 
 // zero the per-phase fields of the device stats, keeping the bump pointers
 int reset_stats(hm_store *s) {
     SCHK(s, hipMemsetAsync(s->st, 0, offsetof(PlanStats, bump), hm_engine_stream(s->e)));
-    SCHK(s, hipMemsetAsync(&s->st->tot_c, 0, 4 * sizeof(unsigned long long), hm_engine_stream(s->e)));
     return HM_OK;
 }
 
@@ -417,6 +422,9 @@ int hm_store_create(hm_engine *e, const hm_store_config *cfg, hm_store **out) {
     if (hipSetDevice(hm_engine_device(e)) != hipSuccess) { delete s; return HM_ERR_DEVICE; }
     int r = dev_alloc(s, &s->st, 1);
     if (r == HM_OK && hipMemset(s->st, 0, sizeof(PlanStats)) != hipSuccess) r = HM_ERR_DEVICE;
+    if (r == HM_OK && (hipHostMalloc((void **)&s->h_st, sizeof(PlanStats), hipHostMallocDefault) != hipSuccess ||
+                       hipHostMalloc((void **)&s->h_cnt, 64, hipHostMallocDefault) != hipSuccess))
+        r = HM_ERR_NOMEM;
     if (r == HM_OK) r = compact(s, 0, 0, 0, 0);
     if (r == HM_OK) r = ensure_handles(s, 1024);
     if (r != HM_OK) { hm_store_destroy(s); return r; }
@@ -433,6 +441,8 @@ void hm_store_destroy(hm_store *s) {
                     s->bdescs.p, s->list.p, s->blist.p, s->alist.p, s->remap.p, s->inv.p, s->rows.p, s->undo_handles.p, s->st};
     for (void *b : bufs) if (b) (void)hipFree(b);
     for (hipEvent_t e : s->ev) if (e) (void)hipEventDestroy(e);
+    if (s->h_st) (void)hipHostFree(s->h_st);
+    if (s->h_cnt) (void)hipHostFree(s->h_cnt);
     delete s;
 }
 
@@ -538,85 +548,90 @@ static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handl
         A.list = s->list.p; A.st = s->st;
         A.ist = A.incremental ? s->ist : nullptr; A.ops = t_op; A.deps = t_dp; A.clock = s->clock;
         A.defer = (uint32_t *)(sp + L.o_defer);
+        // the submit's work-list counts and gathered-row flags, zeroed by plan_kernel (no memsets)
+        A.bail = (uint32_t *)(sp + L.o_bail); A.fail = (uint32_t *)(sp + L.o_fail); A.gdone = sp + L.o_gdone;
         if ((rc = ensure_buf(s, s->alist, n))) return rc;
         A.alist = s->alist.p;
-        // plan: checks, growth, routes (nothing in the store changes)
-        if ((rc = reset_stats(s))) return rc;
-        SCHK(s, hm_launch_plan(A, st));
-        rc = HM_OK;
-        PlanStats P = read_stats(s, &rc);
-        if (rc) return rc;
-        T.mark("plan");
-        if (P.err) {
-            const char *why = (P.err & HM_PLAN_BAD_HANDLE) || (P.err & HM_PLAN_REPEATED) ? "bad or repeated document handle"
-                            : (P.err & HM_PLAN_ROWS) ? "document rows outside the batch tables"
-                            : (P.err & HM_PLAN_TOTALS) ? "document totals must cover the existing log (and n_actors <= a_stride)"
-                            : (P.err & HM_PLAN_CHANGE_ROWS) ? "change rows outside their document's deps/ops"
-                            : "actor remap is not a permutation into the new ranks";
-            return hm_engine_fail(s->e, HM_ERR_INVALID, why);
-        }
-        if (P.bump[0] + P.need[0] > s->cap_c || P.bump[1] + P.need[1] > s->cap_d || P.bump[2] + P.need[2] > s->cap_o ||
-            P.bump[3] + P.need[3] > s->cap_r) {
-            // the arenas cannot take the growth: compact (every document re-merged), then plan again
+        A.cap[0] = s->cap_c; A.cap[1] = s->cap_d; A.cap[2] = s->cap_o; A.cap[3] = s->cap_r;
+        uint32_t *bail = (uint32_t *)(sp + L.o_bail);            // (count zeroed by the plan)
+        if (!s->ev[0])
+            for (auto &e : s->ev) SCHK(s, hipEventCreate(&e));
+        // plan (checks, growth, routes), alloc, append and the incremental kernels go out back to
+        // back: alloc_kernel itself does nothing when the plan failed a check or the arenas cannot
+        // take the growth (every later kernel then finds no work), and the host reads the plan's
+        // stats once, with the re-merge counts.  A failed check fails the submit with the store
+        // as it was; no room compacts the store (every document re-merged) and runs the plan again.
+        PlanStats P;
+        uint32_t counts[2] = {0, 0};
+        for (int attempt = 0;; attempt++) {
+            if ((rc = reset_stats(s))) return rc;
+            SCHK(s, hm_launch_plan(A, st));
+            T.mark("plan");
+            SCHK(s, hm_launch_alloc(A, st));
+            StoreArenas ar = {s->changes, s->deps, s->ops, s->min_clock, s->stored};
+            if (T.on) {
+                // what the append has to move: documents whose segments moved, re-ranked ones, old rows
+                std::vector<AppendDesc> dd(n);
+                SCHK(s, hipMemcpyAsync(dd.data(), s->descs.p, (size_t)n * sizeof(AppendDesc), hipMemcpyDeviceToHost, st));
+                SCHK(s, hipStreamSynchronize(st));
+                size_t mv = 0, rmp = 0, inc = 0, old_o = 0, new_o = 0;
+                for (const AppendDesc &D : dd) {
+                    const bool m = D.src_c != D.dst_c || D.src_d != D.dst_d || D.src_o != D.dst_o;
+                    mv += m; rmp += D.remap_row != 0xFFFFFFFFu; inc += (D.inc & HM_DINC_ROUTE) != 0; new_o += D.n_new_o;
+                    if (m) old_o += D.n_old_o;
+                }
+                fprintf(stderr, "[hm_store] append: %zu docs, %zu moved (%zu old op rows), %zu re-ranked, %zu incremental, %zu new op rows\n",
+                        (size_t)n, mv, old_o, rmp, inc, new_o);
+                T.mark("(append census)");
+            }
+            SCHK(s, hm_launch_append(s->descs.p, n, ar, ar, A.changes, t_dp, t_op, A.remap, S, st, s->alist.p, &s->st->n_app));
+            T.mark("alloc+append");
+            SCHK(s, hipEventRecord(s->ev[0], st));
+            if (A.incremental) {
+                IncArgs IA;
+                IA.descs = s->descs.p; IA.n = n; IA.list = nullptr; IA.S = S;
+                IA.st_changes = A.changes; IA.st_deps = t_dp; IA.st_ops = t_op;
+                IA.changes = s->changes; IA.deps = s->deps; IA.ops = s->ops; IA.hist = s->hist; IA.ckey = s->ckey; IA.all_deps = s->all_deps;
+                IA.regs = s->regs; IA.surv = s->surv; IA.smeta = s->smeta; IA.res_docs = s->res_docs;
+                IA.epos = s->epos; IA.epar = s->epar; IA.ekey = s->ekey; IA.lorder = s->lorder; IA.ldir = s->ldir;
+                IA.clock = s->clock; IA.back_clock = s->back_clock; IA.heads = s->heads; IA.min_clock = s->min_clock;
+                IA.ist = s->ist; IA.bail = bail; IA.defer = (uint32_t *)(sp + L.o_defer);
+                IA.n_lane = S == 8 || S == 16 ? 1u : 0u;                 // (the lane pass reads its count on the device)
+                IA.pst = s->st;
+                // the documents the incremental kernels finish write their gathered rows themselves
+                IA.gout = sp + L.o_gather; IA.gdone = sp + L.o_gdone;      // (gdone zeroed by the plan)
+                dbg_list_state(s, "before");
+                SCHK(s, hm_launch_inc_apply(IA, st));
+                dbg_list_state(s, "after");
+            }
+            SCHK(s, hipEventRecord(s->ev[1], st));
+            T.mark("incremental");
+            // the plan's stats and the re-merge counts (cold documents, then those the incremental
+            // kernels handed back), one read
+            SCHK(s, hipMemcpyAsync(s->h_st, s->st, sizeof(PlanStats), hipMemcpyDeviceToHost, st));
+            SCHK(s, hipMemcpyAsync(&s->h_cnt[1], bail, 4, hipMemcpyDeviceToHost, st));
+            SCHK(s, hipStreamSynchronize(st));
+            P = *s->h_st;
+            counts[0] = P.n_cold; counts[1] = s->h_cnt[1];
+            if (P.err) {
+                const char *why = (P.err & HM_PLAN_BAD_HANDLE) || (P.err & HM_PLAN_REPEATED) ? "bad or repeated document handle"
+                                : (P.err & HM_PLAN_ROWS) ? "document rows outside the batch tables"
+                                : (P.err & HM_PLAN_TOTALS) ? "document totals must cover the existing log (and n_actors <= a_stride)"
+                                : (P.err & HM_PLAN_CHANGE_ROWS) ? "change rows outside their document's deps/ops"
+                                : "actor remap is not a permutation into the new ranks";
+                if (attempt) return hm_engine_fail(s->e, HM_ERR_INVALID, "submit plan failed after compaction");
+                return hm_engine_fail(s->e, HM_ERR_INVALID, why);
+            }
+            // (P.bump already counts this submit's segments when alloc_kernel ran: its own verdict decides)
+            if (!P.mx[1]) break;
+            // the arenas cannot take the growth (alloc_kernel did nothing): compact, then plan again
+            if (attempt) return hm_engine_fail(s->e, HM_ERR_NOMEM, "the store's arenas cannot take the submit after compaction");
             if ((rc = compact(s, P.need[0], P.need[1], P.need[2], P.need[3]))) return rc;
             A.stamp = ++s->stamp ? s->stamp : ++s->stamp;
             A.dm = s->dm; A.descs = s->descs.p; A.list = s->list.p;     // (compaction may have regrown them)
-            if ((rc = reset_stats(s))) return rc;
-            SCHK(s, hm_launch_plan(A, st));
-            P = read_stats(s, &rc);
-            if (rc) return rc;
-            if (P.err) return hm_engine_fail(s->e, HM_ERR_INVALID, "submit plan failed after compaction");
-            T.mark("compact+plan");
+            A.cap[0] = s->cap_c; A.cap[1] = s->cap_d; A.cap[2] = s->cap_o; A.cap[3] = s->cap_r;
+            T.mark("compact");
         }
-        // segments, descriptors, totals, re-merge list; append; incremental apply
-        SCHK(s, hipMemsetAsync(A.defer, 0, 4, st));
-        SCHK(s, hm_launch_alloc(A, st));
-        StoreArenas ar = {s->changes, s->deps, s->ops, s->min_clock, s->stored};
-        if (T.on) {
-            // what the append has to move: documents whose segments moved, re-ranked ones, old rows
-            std::vector<AppendDesc> dd(n);
-            SCHK(s, hipMemcpyAsync(dd.data(), s->descs.p, (size_t)n * sizeof(AppendDesc), hipMemcpyDeviceToHost, st));
-            SCHK(s, hipStreamSynchronize(st));
-            size_t mv = 0, rmp = 0, inc = 0, old_o = 0, new_o = 0;
-            for (const AppendDesc &D : dd) {
-                const bool m = D.src_c != D.dst_c || D.src_d != D.dst_d || D.src_o != D.dst_o;
-                mv += m; rmp += D.remap_row != 0xFFFFFFFFu; inc += (D.inc & HM_DINC_ROUTE) != 0; new_o += D.n_new_o;
-                if (m) old_o += D.n_old_o;
-            }
-            fprintf(stderr, "[hm_store] append: %zu docs, %zu moved (%zu old op rows), %zu re-ranked, %zu incremental, %zu new op rows\n",
-                    (size_t)n, mv, old_o, rmp, inc, new_o);
-            T.mark("(append census)");
-        }
-        SCHK(s, hm_launch_append(s->descs.p, n, ar, ar, A.changes, t_dp, t_op, A.remap, S, st, s->alist.p, &s->st->n_app));
-        T.mark("alloc+append");
-        uint32_t *bail = (uint32_t *)(sp + L.o_bail);
-        SCHK(s, hipMemsetAsync(bail, 0, 4, st));
-        if (!s->ev[0])
-            for (auto &e : s->ev) SCHK(s, hipEventCreate(&e));
-        SCHK(s, hipEventRecord(s->ev[0], st));
-        if (P.n_inc) {
-            IncArgs IA;
-            IA.descs = s->descs.p; IA.n = n; IA.list = nullptr; IA.S = S;
-            IA.st_changes = A.changes; IA.st_deps = t_dp; IA.st_ops = t_op;
-            IA.changes = s->changes; IA.deps = s->deps; IA.ops = s->ops; IA.hist = s->hist; IA.ckey = s->ckey; IA.all_deps = s->all_deps;
-            IA.regs = s->regs; IA.surv = s->surv; IA.smeta = s->smeta; IA.res_docs = s->res_docs;
-            IA.epos = s->epos; IA.epar = s->epar; IA.ekey = s->ekey; IA.lorder = s->lorder; IA.ldir = s->ldir;
-            IA.clock = s->clock; IA.back_clock = s->back_clock; IA.heads = s->heads; IA.min_clock = s->min_clock;
-            IA.ist = s->ist; IA.bail = bail; IA.defer = (uint32_t *)(sp + L.o_defer); IA.n_lane = P.mx[0];
-            // the documents the incremental kernels finish write their gathered rows themselves
-            IA.gout = sp + L.o_gather; IA.gdone = sp + L.o_gdone;
-            SCHK(s, hipMemsetAsync(IA.gdone, 0, n, st));
-            dbg_list_state(s, "before");
-            SCHK(s, hm_launch_inc_apply(IA, st));
-            dbg_list_state(s, "after");
-        }
-        SCHK(s, hipEventRecord(s->ev[1], st));
-        T.mark("incremental");
-        // the re-merge list: cold documents, then those the incremental kernel handed back
-        uint32_t counts[2] = {0, 0};
-        SCHK(s, hipMemcpyAsync(&counts[0], &s->st->n_cold, 4, hipMemcpyDeviceToHost, st));
-        SCHK(s, hipMemcpyAsync(&counts[1], bail, 4, hipMemcpyDeviceToHost, st));
-        SCHK(s, hipStreamSynchronize(st));
         if (counts[1]) SCHK(s, hipMemcpyAsync(s->list.p + counts[0], bail + 1, (size_t)counts[1] * 4, hipMemcpyDeviceToDevice, st));
         SCHK(s, hipEventRecord(s->ev[2], st));
         if ((rc = launch_list_merge(s, s->list.p, counts[0] + counts[1]))) return rc;
@@ -625,8 +640,7 @@ static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handl
         dbg_list_state(s, "after merge");
         T.mark("remerge");
         s->st_inc = P.n_inc - counts[1]; s->st_cold = counts[0]; s->st_bail = counts[1];
-        uint32_t *fail = (uint32_t *)(sp + L.o_fail);
-        SCHK(s, hipMemsetAsync(fail, 0, 4, st));
+        uint32_t *fail = (uint32_t *)(sp + L.o_fail);            // (count zeroed by the plan)
         SCHK(s, hm_launch_gather(A.handles, n, S, s->res_docs, s->clock, s->back_clock, s->heads, sp + L.o_gather, fail, st,
                                  P.n_inc ? sp + L.o_gdone : nullptr));
         s->p_gather_dev = sp + L.o_gather;

@@ -44,12 +44,13 @@ struct PlanRow {
 struct PlanStats {
     uint32_t err;                              // HM_PLAN_* bits of the failed checks
     uint32_t n_inc, n_cold, n_back, n_app;       // (n_app: batch rows append_kernel has work for)
-    uint32_t mx[6];                            // mx[0]: documents routed to the lane pass (the rest unused)
+    uint32_t mx[6];                            // mx[0]: documents routed to the lane pass; mx[1] = 1: alloc_kernel
+                                               //   found no room for the growth and moved nothing (the rest unused)
     uint32_t max_c, max_o, max_r, max_objs, max_d, flags;   // launch hints of a merge list
     unsigned long long need[4];                // rows the submit's growing segments take, per space
-    unsigned long long bump[4];                // arena bump pointers (device-side segment allocation)
     unsigned long long tot_c, tot_d, tot_o, tot_r;
-};
+    unsigned long long bump[4];                // arena bump pointers (device-side segment allocation;
+};                                             //   last: one memset clears every per-phase field)
 #define HM_PLAN_BAD_HANDLE 1u
 #define HM_PLAN_REPEATED 2u
 #define HM_PLAN_ROWS 4u
@@ -132,6 +133,7 @@ struct IncArgs {
     uint32_t n_lane;                           // documents routed to the lane pass (0: no launch)
     uint8_t *gout;                             // the submit's gather buffer (gather_kernel's layout), or NULL
     uint8_t *gdone;                            // [n] 1: the row was gathered by the incremental kernels
+    const PlanStats *pst;                      // the submit's plan stats (n_inc, mx[0]: work for the passes), or NULL
 };
 
 // AppendDesc.inc: the route (bits 0-1: 0 re-merge, 1 incremental group pass, 2 wave pass, 3 lane pass) and what
@@ -168,7 +170,11 @@ struct PlanArgs {
     const hm_dep_row *deps;                    //   (staged deps, and the resident clocks: changes that
     const uint32_t *clock;                     //   are not causally ready in arrival order)
     uint32_t *defer;                           // the one-document-per-wave pass's list ([0] = count):
-};                                             //   documents with list ops go there directly
+                                               //   documents with list ops go there directly
+    uint32_t *bail, *fail;                     // counts the plan zeroes for the later kernels (NULL: none)
+    unsigned long long cap[4];                 // arena capacities: alloc_kernel does nothing past them
+    uint8_t *gdone;                            // [n] the incremental kernels' gathered-row flags (zeroed)
+};
 hipError_t hm_launch_plan(const PlanArgs &a, hipStream_t s);
 hipError_t hm_launch_alloc(const PlanArgs &a, hipStream_t s);
 // hm_doc_row of each listed handle from its device meta (+ the launch hints in st)

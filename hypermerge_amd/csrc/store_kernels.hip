@@ -272,6 +272,13 @@ __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
     const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
     const bool live = i0 < a.n;
     const uint32_t i = live ? i0 : 0u;
+    // the submit's later work lists start empty (in place of a memset launch each)
+    if (live && a.gdone) a.gdone[i] = 0;
+    if (i0 == 0) {
+        if (a.defer) a.defer[0] = 0;
+        if (a.bail) a.bail[0] = 0;
+        if (a.fail) a.fail[0] = 0;
+    }
     uint32_t err = 0;
     const uint32_t h = live ? a.handles[i] : 0u;
     if (live && h >= a.n_handles) err |= HM_PLAN_BAD_HANDLE;
@@ -427,6 +434,18 @@ __global__ __launch_bounds__(ALLOC_WG) void alloc_kernel(PlanArgs a) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
     const bool live = i < a.n;
+    // the plan failed a check, or the arenas cannot take the growth: nothing moves (the host finds
+    // out from the stats; every later kernel of the submit sees route 0 and empty lists)
+    {
+        const PlanStats *st = a.st;
+        const bool stop = st->err != 0 || st->bump[0] + st->need[0] > a.cap[0] || st->bump[1] + st->need[1] > a.cap[1] ||
+                          st->bump[2] + st->need[2] > a.cap[2] || st->bump[3] + st->need[3] > a.cap[3];
+        if (stop) {
+            if (live) a.descs[i].inc = 0;
+            if (i == 0 && st->err == 0) a.st->mx[1] = 1u;         // no room: the host compacts and plans again
+            return;
+        }
+    }
     bool cold = false, wavep = false, app = false;
     uint32_t h = 0;
     if (live) {
