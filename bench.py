@@ -154,7 +154,7 @@ def compact_line(full: dict) -> dict:
                         "gpu_async": _r((nd.get("gpu_async") or {}).get("changes_per_s"), 3),
                         "inc_remerged": _routing((nd.get("gpu_async") or {}).get("routing")),
                         "same_state": nd.get("same_state")}}
-            for c in ("C3", "C5"):
+            for c in ("C3", "C5", "C2_arrivals"):
                 x = nd.get(c)
                 if isinstance(x, dict):
                     n[c] = ({"error": str(x["error"])[:120]} if "error" in x else
@@ -265,6 +265,8 @@ def main() -> int:
     ap.add_argument("--node-docs", type=int, default=20000)
     ap.add_argument("--node-text-docs", type=int, default=1000, help="C3 documents of the Node leg (0: skip)")
     ap.add_argument("--node-c5-docs", type=int, default=5000, help="C5 documents of the Node leg (0: skip)")
+    ap.add_argument("--node-arrival-docs", type=int, default=10000,
+                    help="C2 documents of the Node live-arrival leg (init 48 changes, then rounds of 2; 0: skip)")
     ap.add_argument("--text-docs", type=int, default=10000, help="C3 documents in the resident text leg")
     ap.add_argument("--c5-docs", type=int, default=100000, help="C5 documents in the resident nested-document leg (0: skip)")
     ap.add_argument("--arrival", type=int, default=None,
@@ -572,15 +574,17 @@ def _from_blocks(eng, batch, cfg, args):
             "path": "JSON blocks -> hm_decode_blocks (native, multi-threaded) -> hm_merge_host (PCIe included)"}
 
 
-def _node_run(node, docs, legs, chunk=16, timeout=900):
-    """tools/bench_node.js over `docs` (each document's changes, fed in chunks of `chunk`)."""
+def _node_run(node, docs, legs, chunk=16, timeout=900, first=None):
+    """tools/bench_node.js over `docs` (each document's changes, fed in chunks of `chunk`; with
+    `first`, the first chunk — DocBackend.init — holds that many changes)."""
     import subprocess
     import tempfile
     here = os.path.dirname(os.path.abspath(__file__))
+    f0 = chunk if first is None else first
     with tempfile.TemporaryDirectory() as td:
         fn = os.path.join(td, "docs.json")
         with open(fn, "w") as f:
-            json.dump({"docs": [[d[k:k + chunk] for k in range(0, len(d), chunk)] for d in docs]}, f)
+            json.dump({"docs": [[d[:f0]] + [d[k:k + chunk] for k in range(f0, len(d), chunk)] for d in docs]}, f)
         p = subprocess.run([node, "--max-old-space-size=16384", "--max-semi-space-size=64",
                             os.path.join(here, "tools", "bench_node.js"), fn, ",".join(legs)],
                            capture_output=True, text=True, timeout=timeout)
@@ -643,6 +647,17 @@ def _node_e2e(args):
             r["gpu_async_vs_js"] = r["gpu_async"]["changes_per_s"] / r["cpu"]["changes_per_s"]
             r["sample"] = f"{name}: {bx.n_docs} {desc}; rounds of 16 changes per document"
         out[name] = r
+    # live arrivals: the same C2 documents loaded with their first 48 changes (init), then
+    # applyRemoteChanges rounds of 2 changes — the granularity hypercore blocks arrive at
+    # (Actor.onDownload / syncChanges per block) — which the store routes to the incremental kernels
+    if args.node_arrival_docs > 0:
+        ba = synth.generate(synth.config("C2", n_docs=args.node_arrival_docs), threads=th)
+        r = _node_run(node, [decode_doc(ba, i) for i in range(ba.n_docs)], ["cpu", "gpu_async"], chunk=2, first=48)
+        if "error" not in r:
+            r["gpu_async_vs_js"] = r["gpu_async"]["changes_per_s"] / r["cpu"]["changes_per_s"]
+            r["sample"] = (f"C2 arrivals: {ba.n_docs} docs x 4 actors x 64 changes, init with 48, then 8 "
+                           f"applyRemoteChanges rounds of 2 changes per document")
+        out["C2_arrivals"] = r
     return out
 
 

@@ -146,7 +146,7 @@ class RoundReader {
     skipClock(); skipClock()
     const c = rdClock()
     this.leave()
-    return { patch: { clock, deps: state.deps, canUndo: false, canRedo: false, diffs: this.diffs(d) }, c }
+    return { patch: { clock, deps: state.deps, canUndo: state.canUndo, canRedo: state.canRedo, diffs: this.diffs(d) }, c }
   }
 
   diffs(d) {
@@ -244,7 +244,9 @@ class JsonRoundReader {
     Object.assign(state.backClock, this.j.b[d])
     return true
   }
-  message(d, state) { return { patch: Object.assign({}, this.j.p[d], { deps: state.deps }), c: this.j.c[d] } }
+  message(d, state) {
+    return { patch: Object.assign({}, this.j.p[d], { deps: state.deps, canUndo: state.canUndo, canRedo: state.canRedo }), c: this.j.c[d] }
+  }
 }
 
 function decodeRound(buf, n) {
@@ -326,7 +328,15 @@ class GpuBackendState {
     this.clock = {}
     this.deps = {}
     this.backClock = {}              // max seq per actor over the whole log (queued included)
+    // Automerge's local undo history (applyLocalChange, SURVEY Appendix A.4): undoStack of op
+    // lists, undoPos, redoStack; canUndo = undoPos > 0, canRedo = redoStack not empty
+    this.undoStack = []
+    this.undoPos = 0
+    this.redoStack = []
   }
+
+  get canUndo() { return this.undoPos > 0 }
+  get canRedo() { return this.redoStack.length > 0 }
 
   change(i) {
     const c = this.log[i]
@@ -397,12 +407,24 @@ class GpuEngine {
 
   // leading callbacks run; each document's head GPU job forms the round
   collectRound() {
+    const prepErrors = []            // (requests whose preparation threw: raised with the round)
     for (;;) {
       const round = []
+      round.prepErrors = prepErrors
       for (const [state, q] of Array.from(this.queues)) {
         while (q.length && q[0].entries === null) q.shift().done(null)
-        if (q.length) round.push([state, q.shift()])
-        else this.queues.delete(state)
+        if (!q.length) { this.queues.delete(state); continue }
+        const job = q.shift()
+        if (job.prepare) {
+          // (a local undo / redo request: its ops from the document as every earlier round left it)
+          try {
+            job.prepare()
+          } catch (e) {
+            prepErrors.push([job, e])
+            continue
+          }
+        }
+        round.push([state, job])
       }
       if (round.length || this.queues.size === 0) return round
     }
@@ -415,7 +437,7 @@ class GpuEngine {
     try {
       for (;;) {
         const round = this.collectRound()
-        if (!round.length) break
+        if (!round.length) { this.raise(round.prepErrors); break }
         this.runRound(round)
       }
     } finally {
@@ -433,7 +455,7 @@ class GpuEngine {
       this.flushing = false
       throw e
     }
-    if (!round.length) { this.flushing = false; return }
+    if (!round.length) { this.flushing = false; this.raise(round.prepErrors); return }
     this.runRoundAsync(round, () => { this.flushing = false; this.flushAsync() })
   }
 
@@ -488,7 +510,7 @@ class GpuEngine {
 
   // One applyChanges per document of the round, one docset call per device
   runRound(round) {
-    const errors = []
+    const errors = round.prepErrors ? round.prepErrors.slice() : []
     for (const g of this.groups(round, 0)) {
       GpuEngine.prepare(g)
       this.finish(g, addon.docsetApplyPacked(g.ds, g.ids, g.data, g.ends, g.docBlock), errors)
@@ -504,7 +526,7 @@ class GpuEngine {
       done()
       throw e
     }
-    const errors = []
+    const errors = round.prepErrors ? round.prepErrors.slice() : []
     let left = gs.length
     const finish = () => { try { this.raise(errors) } finally { done() } }
     for (const g of gs) {
@@ -665,11 +687,83 @@ function fullPatch(state) {
     for (const [key, e] of ov.keys) diffs.push(Object.assign({ action: 'set', type: ov.type, obj: uuid, key }, e))
     ov.elems.forEach(([elemId, e], index) => diffs.push(Object.assign({ action: 'insert', type: ov.type, obj: uuid, index, elemId }, e)))
   }
-  return { clock: Object.assign({}, state.clock), deps: Object.assign({}, state.deps), canUndo: false, canRedo: false, diffs }
+  return { clock: Object.assign({}, state.clock), deps: Object.assign({}, state.deps), canUndo: state.canUndo,
+    canRedo: state.canRedo, diffs }
 }
 
-const emptyPatch = (state) => ({ clock: Object.assign({}, state.clock), deps: Object.assign({}, state.deps), canUndo: false,
-  canRedo: false, diffs: [] })
+const emptyPatch = (state) => ({ clock: Object.assign({}, state.clock), deps: Object.assign({}, state.deps),
+  canUndo: state.canUndo, canRedo: state.canRedo, diffs: [] })
+
+// ---------------- local undo / redo (Backend.applyLocalChange, src/DocBackend.ts:187-205) ----------------
+// Automerge 0.12 records, for every set / del / link / inc of an undoable local change, the ops
+// that restore the field it touches: an inc's negation, else the field's current ops (action,
+// obj, key, value, datatype) or a del when it has none; the list goes on undoStack at undoPos
+// (the redo stack is cleared).  An 'undo' request applies undoStack[undoPos - 1] as its ops and
+// pushes the ops that restore the fields they touch onto redoStack; a 'redo' request applies the
+// top of redoStack.  (SURVEY Appendix A.4 [R]: recollected, parity unpinned.)  The field
+// states come from the merged document (the docset's view, read when the request reaches the
+// head of its document's queue: every earlier round of the document has applied); the fields a
+// request touches twice see its own earlier ops, which are concurrent with later ones of the same
+// change (so a later set keeps the earlier one as a conflict).
+function viewField(view, obj, key) {
+  const ov = view[obj]
+  if (!ov) return []
+  let e = null
+  if (ov.type === 'list' || ov.type === 'text') { for (const [id, x] of ov.elems) if (id === key) { e = x; break } } else {
+    for (const [k, x] of ov.keys) if (k === key) { e = x; break }
+  }
+  if (!e) return []
+  const one = (x) => {
+    const o = { action: x.link ? 'link' : 'set', obj, key, value: x.value }
+    if (x.datatype) o.datatype = x.datatype
+    return o
+  }
+  return [one(e)].concat((e.conflicts || []).map(one))
+}
+
+const UNDO_ACTIONS = new Set(['set', 'del', 'link', 'inc'])
+
+// the undo ops of an undoable local change's ops, in op order
+function undoOpsOf(view, ops) {
+  const sim = new Map()                       // obj \0 key -> {prior: [...], own: [...]}
+  const out = []
+  for (const op of ops || []) {
+    if (!UNDO_ACTIONS.has(op.action)) continue
+    const k = op.obj + '\u0000' + op.key
+    let f = sim.get(k)
+    if (!f) { f = { prior: viewField(view, op.obj, op.key), own: [] }; sim.set(k, f) }
+    if (op.action === 'inc') {
+      out.push({ action: 'inc', obj: op.obj, key: op.key, value: -op.value })
+      // the inc adds to the counters it causally follows: the field's earlier ops, not this change's
+      f.prior = f.prior.map((o) => (o.datatype === 'counter' && typeof o.value === 'number' ? Object.assign({}, o, { value: o.value + op.value }) : o))
+      continue
+    }
+    const cur = f.own.concat(f.prior)
+    if (cur.length) for (const o of cur) out.push(Object.assign({}, o))
+    else out.push({ action: 'del', obj: op.obj, key: op.key })
+    // set / link / del remove the field's earlier ops (this change causally follows them) and keep
+    // this change's own (concurrent with each other: one change)
+    f.prior = []
+    if (op.action === 'set' || op.action === 'link') {
+      const o = { action: op.action, obj: op.obj, key: op.key, value: op.value }
+      if (op.datatype) o.datatype = op.datatype
+      f.own.unshift(o)
+    }
+  }
+  return out
+}
+
+// the ops that restore the fields an undo change's ops touch (the redo ops), from the fields before it
+function redoOpsOf(view, ops) {
+  const out = []
+  for (const op of ops) {
+    if (op.action === 'inc') { out.push({ action: 'inc', obj: op.obj, key: op.key, value: -op.value }); continue }
+    const cur = viewField(view, op.obj, op.key)
+    if (cur.length) for (const o of cur) out.push(o)
+    else out.push({ action: 'del', obj: op.obj, key: op.key })
+  }
+  return out
+}
 
 function makeBackend(engine) {
   return {
@@ -785,12 +879,52 @@ class DocBackend {
       // Backend.applyLocalChange: the change must extend its actor's sequence
       const cur = this.back.clock[change.actor] || 0
       if (change.seq <= cur) throw new Error(`Change request has already been applied: ${change.actor}:${change.seq}`)
-      this.engine.enqueue(this.back, { entries: [change], done: (r) => {
+      // requestType 'change' (a request without one is taken as a change), 'undo' or 'redo'
+      const type = change.requestType === undefined ? 'change' : change.requestType
+      if (type !== 'change' && type !== 'undo' && type !== 'redo') throw new RangeError(`Unknown requestType: ${type}`)
+      const state = this.back
+      let after = null
+      const job = { entries: [change], done: (r) => {
+        if (after) after()
         this.updateClock(r.roundClock)
-        const patch = Object.assign(r.patch, { actor: change.actor, seq: change.seq })
+        const patch = Object.assign(r.patch, { actor: change.actor, seq: change.seq, canUndo: state.canUndo,
+          canRedo: state.canRedo })
         this.notify({ type: 'LocalPatchMsg', id: this.id, actorId: this.actorId,
           minimumClockSatisfied: this.minimumClockSatisfied, change, patch, history: this.back.histLen })
-      } })
+      } }
+      const undoable = type === 'change' && change.undoable !== false
+      if (undoable || type !== 'change') {
+        // run when the request heads its document's queue (every earlier round applied)
+        job.prepare = () => {
+          const view = JSON.parse(addon.docsetView(state.ds, state.id))
+          if (type === 'change') {
+            const ops = undoOpsOf(view, change.ops)
+            after = () => {
+              state.undoStack = state.undoStack.slice(0, state.undoPos).concat([ops])
+              state.undoPos++
+              state.redoStack = []
+            }
+            return
+          }
+          let ops
+          if (type === 'undo') {
+            ops = state.undoPos > 0 ? state.undoStack[state.undoPos - 1] : undefined
+            if (!ops) throw new RangeError('Cannot undo: there is nothing to be undone')
+            const redo = redoOpsOf(view, ops)
+            after = () => { state.undoPos--; state.redoStack = state.redoStack.concat([redo]) }
+          } else {
+            ops = state.redoStack[state.redoStack.length - 1]
+            if (!ops) throw new RangeError('Cannot redo: the last change was not an undo')
+            after = () => { state.undoPos++; state.redoStack = state.redoStack.slice(0, -1) }
+          }
+          // the change the engine applies: the request's actor / seq / deps / message with these ops
+          const c = { actor: change.actor, seq: change.seq, deps: change.deps || {} }
+          if (change.message !== undefined) c.message = change.message
+          c.ops = ops
+          job.entries = [c]
+        }
+      }
+      this.engine.enqueue(this.back, job)
     })
   }
 }

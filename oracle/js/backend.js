@@ -33,7 +33,33 @@ class OpSet {
     this.history = []
     this.queue = []
     this.objs = new Map([[ROOT, { type: 'map', keys: new Map(), following: new Map(), insertion: new Map(), elemIds: [] }]])
+    // local undo history (Backend.applyLocalChange, Appendix A.4 [R]): undoLocal collects the undo
+    // ops of the change being applied undoably
+    this.undoStack = []
+    this.undoPos = 0
+    this.redoStack = []
+    this.undoLocal = null
   }
+}
+
+// a field's current ops as undo / redo ops: action, obj, key, value, datatype
+function fieldOps(s, objId, key) {
+  const obj = s.objs.get(objId)
+  const ops = obj ? obj.keys.get(key) || [] : []
+  return ops.map((o) => {
+    const r = { action: o.action, obj: o.obj, key: o.key, value: o.value }
+    if (o.datatype) r.datatype = o.datatype
+    return r
+  })
+}
+
+// recordUndoHistory: the ops that restore the field an op of an undoable local change touches
+function recordUndo(s, op) {
+  if (!s.undoLocal) return
+  if (op.action === 'inc') { s.undoLocal.push({ action: 'inc', obj: op.obj, key: op.key, value: -op.value }); return }
+  const f = fieldOps(s, op.obj, op.key)
+  if (f.length) s.undoLocal.push(...f)
+  else s.undoLocal.push({ action: 'del', obj: op.obj, key: op.key })
 }
 
 function allDepsOf(s, actor, seq) { return s.states.get(actor)[seq - 1].allDeps }
@@ -126,6 +152,7 @@ function updateListElement(s, obj, elemId, diffs, objId) {
 function applyAssign(s, op, diffs) {
   const obj = s.objs.get(op.obj)
   if (!obj) throw new Error(`Modification of unknown object ${op.obj}`)
+  recordUndo(s, op)
   const prior = obj.keys.get(op.key) || []
   let remaining
   if (op.action === 'inc') {
@@ -201,11 +228,65 @@ const Backend = {
   applyChanges(s, changes) {
     const diffs = []
     for (const c of changes) { s.queue.push(c); applyQueuedOps(s, diffs) }
-    const clock = {}, deps = {}
-    for (const [a, q] of s.clock) clock[a] = q
-    for (const [a, q] of s.deps) deps[a] = q
-    return [s, { clock, deps, canUndo: false, canRedo: false, diffs }]
+    return [s, makePatch(s, diffs)]
   },
+  // applyLocalChange(state, request) -> [state, patch]: requestType 'change' (undoable unless
+  // `undoable: false`; a request without a type is taken as a change), 'undo', 'redo'
+  applyLocalChange(s, change) {
+    if (change.seq <= (s.clock.get(change.actor) || 0)) throw new RangeError('Change request has already been applied')
+    const type = change.requestType === undefined ? 'change' : change.requestType
+    const diffs = []
+    if (type === 'change') {
+      const undoable = change.undoable !== false
+      if (undoable) s.undoLocal = []
+      s.queue.push(change)
+      applyQueuedOps(s, diffs)
+      if (undoable) {
+        s.undoStack = s.undoStack.slice(0, s.undoPos).concat([s.undoLocal])
+        s.undoPos++
+        s.redoStack = []
+        s.undoLocal = null
+      }
+    } else if (type === 'undo' || type === 'redo') {
+      let ops
+      if (type === 'undo') {
+        ops = s.undoPos > 0 ? s.undoStack[s.undoPos - 1] : undefined
+        if (!ops) throw new RangeError('Cannot undo: there is nothing to be undone')
+        const redo = []
+        for (const op of ops) {
+          if (op.action === 'inc') { redo.push({ action: 'inc', obj: op.obj, key: op.key, value: -op.value }); continue }
+          const f = fieldOps(s, op.obj, op.key)
+          if (f.length) redo.push(...f)
+          else redo.push({ action: 'del', obj: op.obj, key: op.key })
+        }
+        s.undoPos--
+        s.redoStack = s.redoStack.concat([redo])
+      } else {
+        ops = s.redoStack[s.redoStack.length - 1]
+        if (!ops) throw new RangeError('Cannot redo: the last change was not an undo')
+        s.undoPos++
+        s.redoStack = s.redoStack.slice(0, -1)
+      }
+      const c = { actor: change.actor, seq: change.seq, deps: change.deps || {} }
+      if (change.message !== undefined) c.message = change.message
+      c.ops = ops
+      s.queue.push(c)
+      applyQueuedOps(s, diffs)
+    } else {
+      throw new RangeError(`Unknown requestType: ${type}`)
+    }
+    const patch = makePatch(s, diffs)
+    patch.actor = change.actor
+    patch.seq = change.seq
+    return [s, patch]
+  },
+}
+
+function makePatch(s, diffs) {
+  const clock = {}, deps = {}
+  for (const [a, q] of s.clock) clock[a] = q
+  for (const [a, q] of s.deps) deps[a] = q
+  return { clock, deps, canUndo: s.undoPos > 0, canRedo: s.redoStack.length > 0, diffs }
 }
 
 // DocBackend (src/DocBackend.ts:46-213) over the restatement, synchronous Queue semantics
@@ -233,11 +314,14 @@ class DocBackend {
       this.ready.subscribe((f) => f())
       this.minimumClockSatisfied = true
       this.subscribeToRemoteChanges()
+      this.subscribeToLocalChanges()
       this.notify({ type: 'ReadyMsg', id: this.id, minimumClockSatisfied: true, actorId: this.actorId, history: back.history.length })
     }
   }
 
   applyRemoteChanges(changes) { this.remoteChangesQ.push(changes) }
+
+  applyLocalChange(change) { this.localChangeQ.push(change) }
 
   updateClock(changes) {
     for (const c of changes) this.clock[c.actor] = Math.max(this.clock[c.actor] || 0, c.seq)
@@ -250,9 +334,21 @@ class DocBackend {
     this.updateClock(changes)
     this.minimumClockSatisfied = changes.length > 0
     this.ready.subscribe((f) => f())
+    this.subscribeToLocalChanges()
     this.subscribeToRemoteChanges()
     this.notify({ type: 'ReadyMsg', id: this.id, minimumClockSatisfied: this.minimumClockSatisfied, actorId: this.actorId,
       patch, history: back.history.length })
+  }
+
+  // src/DocBackend.ts:187-205
+  subscribeToLocalChanges() {
+    this.localChangeQ.subscribe((change) => {
+      const [back, patch] = Backend.applyLocalChange(this.back, change)
+      this.back = back
+      this.updateClock([change])
+      this.notify({ type: 'LocalPatchMsg', id: this.id, actorId: this.actorId, minimumClockSatisfied: this.minimumClockSatisfied,
+        change, patch, history: back.history.length })
+    })
   }
 
   subscribeToRemoteChanges() {

@@ -53,3 +53,27 @@ def test_js_restatement_matches_oracle(name, n, kw):
         clock = {actors[a]: int(v) for a, v in enumerate(r.clock[i * S:(i + 1) * S]) if v}
         assert j["clock"] == clock
         assert j["doc"] == plain(doc_state(cold, r, i)), i
+
+
+def test_restatement_local_undo_redo_known_answers():
+    """Backend.applyLocalChange of the JS restatement (oracle/js/backend.js; SURVEY Appendix A.4
+    [R], parity unpinned: Automerge 0.12 is not vendored): undo restores a set field, a new
+    key (a del), a counter (the inc's negation) and a list element (removed); redo re-applies;
+    `undoable: false` records nothing; a new change clears the redo stack; the throws.  The
+    expected answers are hand-checked and kept in tests/golden/undo_kats.json."""
+    import json
+    import shutil
+    import subprocess
+    node = shutil.which("node")
+    if node is None:
+        pytest.skip("node not installed")
+    p = subprocess.run([node, os.path.join(ROOT, "tests", "js", "run_undo_kat.js")], capture_output=True, text=True,
+                       timeout=60)
+    assert p.returncode == 0, p.stderr
+    got = json.loads(p.stdout)
+    want = json.load(open(os.path.join(ROOT, "tests", "golden", "undo_kats.json")))
+    assert got == want
+    assert want["set_undo_redo"][1][0]["x"] == 1 and want["set_undo_redo"][1][1:3] == [False, True]
+    assert "y" not in want["new_key_undo_is_del"][1][0]
+    assert want["inc_undo"][1][0]["n"] == 5 and want["list_insert_undo"][1][0]["l"] == []
+    assert want["nothing_to_undo"][0] == ["throw", "Cannot undo: there is nothing to be undone"]

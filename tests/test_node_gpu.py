@@ -302,3 +302,26 @@ def test_documents_open_while_an_async_round_is_in_flight():
     for i, g in enumerate(got["docs"]):
         s = doc_summary(cold, o, i)
         assert g["clock"] == s["backend_clock"] and g["hist"] == len(s["history"]) and g["stored"] == s["backend_clock"], i
+
+
+@pytest.mark.parametrize("mode", ["sync", "batched", "async"])
+def test_local_undo_redo_matches_restatement(mode):
+    """applyLocalChange with requestType change / undo / redo (src/DocBackend.ts:187-205,
+    Automerge's undo stack, SURVEY Appendix A.4 [R]) through the GPU drop-in and through the JS
+    restatement: the same messages, canUndo / canRedo on every patch, the same throws ('Cannot
+    undo: there is nothing to be undone', 'Cannot redo: ...') and the same document after every
+    step, on seeded documents with counters, lists, deletes and concurrent remote sets."""
+    p = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "run_undo.js"), mode, "24"],
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr
+    got = json.loads(p.stdout.strip().splitlines()[-1])
+    assert len(got["gpu"]) == len(got["cpu"]) == 24
+    undos = redos = throws = 0
+    for d, (g, c) in enumerate(zip(got["gpu"], got["cpu"])):
+        assert g["trace"] == c["trace"], d
+        assert g["msgs"] == c["msgs"], d
+        for kind, err, _ in c["trace"]:
+            throws += err is not None
+        undos += sum(1 for m in c["msgs"] if m[0] == "LocalPatchMsg" and m[3])
+        redos += sum(1 for m in c["msgs"] if m[0] == "LocalPatchMsg" and m[2])
+    assert throws > 0 and undos > 0 and redos > 0, (throws, undos, redos)

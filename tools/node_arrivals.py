@@ -1,0 +1,36 @@
+"""The bench's Node live-arrival leg alone (dev): C2 documents loaded with their first `first`
+changes through DocBackend.init, then applyRemoteChanges rounds of `chunk` changes, JS restatement
+vs the GPU drop-in (async).  Prints the run's JSON (routing included)."""
+import argparse
+import importlib.util
+import json
+import os
+import shutil
+import sys
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, HERE)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--docs", type=int, default=10000)
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--first", type=int, default=48)
+    ap.add_argument("--chunk", type=int, default=2)
+    a = ap.parse_args()
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(HERE, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    from hypermerge_amd import synth
+    from hypermerge_amd.columnar import decode_doc
+    b = synth.generate(synth.config(a.config, n_docs=a.docs), threads=16)
+    r = bench._node_run(shutil.which("node"), [decode_doc(b, i) for i in range(b.n_docs)], ["cpu", "gpu_async"],
+                        chunk=a.chunk, first=a.first)
+    if "error" not in r:
+        r["gpu_async_vs_js"] = r["gpu_async"]["changes_per_s"] / r["cpu"]["changes_per_s"]
+    print(json.dumps(r))
+
+
+if __name__ == "__main__":
+    main()
