@@ -42,10 +42,16 @@ def build_gpu(force: bool = False) -> str:
         flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
                  "-mllvm", "-amdgpu-atomic-optimizer-strategy=DPP"]
         objs = [os.path.join(objdir, s + ".o") for s in GPU_SRCS]
-        with ThreadPoolExecutor(min(8, len(GPU_SRCS))) as ex:
-            list(ex.map(lambda so: _run([HIPCC] + flags + ["-c", "-o", so[1], os.path.join(CSRC, so[0])]),
-                        zip(GPU_SRCS, objs)))
+        # plus the check build's merge_kernels object (tests only: HM_ASYNC_CHECK re-reads every
+        # asynchronously loaded row set with counted loads; libhmgpu_check.so shares the other objects)
+        chk_o = os.path.join(objdir, "merge_kernels_check.hip.o")
+        jobs = [[HIPCC] + flags + ["-c", "-o", o, os.path.join(CSRC, src)] for src, o in zip(GPU_SRCS, objs)]
+        jobs.append([HIPCC] + flags + ["-DHM_ASYNC_CHECK=1", "-c", "-o", chk_o, os.path.join(CSRC, "merge_kernels.hip")])
+        with ThreadPoolExecutor(min(8, len(jobs))) as ex:
+            list(ex.map(_run, jobs))
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs + ["-ldl"])
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", os.path.join(LIBDIR, "libhmgpu_check.so"), chk_o] +
+             [o for o in objs if not o.endswith(os.sep + "merge_kernels.hip.o")] + ["-ldl"])
     return out
 
 

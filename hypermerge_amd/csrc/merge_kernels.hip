@@ -114,6 +114,10 @@
 #ifndef HM_ASYNC_STORES
 #define HM_ASYNC_STORES 10  // store instructions an OK document's write_outputs issues at least (padded)
 #endif
+#ifndef HM_ASYNC_CHECK
+#define HM_ASYNC_CHECK 0    // check builds (libhmgpu_check.so): every asynchronously loaded set of rows is re-read
+                            // with counted loads and compared (hm_debug_async_check counts the differences)
+#endif
 #ifndef HM_OPAQUE_LANE
 #define HM_OPAQUE_LANE 1    // per-document lane index the compiler cannot hoist out of the document loop
 #endif
@@ -612,6 +616,26 @@ __device__ __forceinline__ Rows load_rows(const SmallParams &p, const hm_doc_row
     if (lane + WAVE < doc.n_deps) r.d1 = *reinterpret_cast<const uint2 *>(dp + lane + WAVE);
     return r;
 }
+#if HM_ASYNC_CHECK
+__device__ unsigned long long hm_async_checked, hm_async_bad;
+// the rows the counted loads return against the asynchronously loaded ones (lane-wise, every field)
+template <int OPL>
+__device__ __forceinline__ void async_check(const SmallParams &p, const hm_doc_row &doc, const Rows &got) {
+    const Rows want = load_rows<OPL>(p, doc);
+    auto ne4 = [](uint4 a, uint4 b) { return a.x != b.x || a.y != b.y || a.z != b.z || a.w != b.w; };
+    auto ne2 = [](uint2 a, uint2 b) { return a.x != b.x || a.y != b.y; };
+    bool bad = ne4(want.c01, got.c01) || ne2(want.c2, got.c2) || ne4(want.a0, got.a0) || ne4(want.b0, got.b0) ||
+               ne2(want.d0, got.d0) || ne2(want.d1, got.d1);
+    if (OPL > 1) bad = bad || ne4(want.a1, got.a1) || ne4(want.b1, got.b1);
+    if (OPL > 2) bad = bad || ne4(want.a2, got.a2) || ne4(want.b2, got.b2);
+    if (OPL > 3) bad = bad || ne4(want.a3, got.a3) || ne4(want.b3, got.b3);
+    const unsigned long long m = __ballot(bad);
+    if (threadIdx.x == 0) {
+        atomicAdd(&hm_async_checked, 1ull);
+        if (m) atomicAdd(&hm_async_bad, 1ull);
+    }
+}
+#endif
 #if HM_ASYNC_NEXT
 // The next document's rows issued as inline-asm loads: hipcc does not count them, so the staging
 // waits with an explicit vmcnt(N) — N the store instructions write_outputs is certain to issue
@@ -1874,7 +1898,12 @@ void merge_small_kernel(SmallParams p) {
         STAMP(L, 10);
         if (!more) break;
 #if HM_ASYNC_NEXT
-        if constexpr (ASY) next = take_rows_async<OPL>(anext, docn, oc == OUT_OK);
+        if constexpr (ASY) {
+            next = take_rows_async<OPL>(anext, docn, oc == OUT_OK);
+#if HM_ASYNC_CHECK
+            async_check<OPL>(p, docn, next);
+#endif
+        }
 #endif
         stage_rows<OPL, LISTS>(p, L, docn, next, C::ND);
         if (HM_PRIO_IO) __builtin_amdgcn_s_setprio(0);
@@ -1920,6 +1949,24 @@ __global__ void clock_intersection_kernel(const uint32_t *a, const uint32_t *b, 
 }  // namespace hm
 
 // ---------------- host-side launchers ----------------
+// (check builds) documents whose rows were loaded asynchronously and checked, and those whose
+// asynchronous rows differed from the counted loads' (both since the last reset)
+extern "C" int hm_debug_async_check(unsigned long long *out2, int reset) {
+#if HM_ASYNC_CHECK && HM_ASYNC_NEXT
+    if (!out2 || hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(&out2[0], HIP_SYMBOL(hm::hm_async_checked), 8) != hipSuccess ||
+        hipMemcpyFromSymbol(&out2[1], HIP_SYMBOL(hm::hm_async_bad), 8) != hipSuccess) return -1;
+    if (reset) {
+        const unsigned long long z = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(hm::hm_async_checked), &z, 8) != hipSuccess ||
+            hipMemcpyToSymbol(HIP_SYMBOL(hm::hm_async_bad), &z, 8) != hipSuccess) return -1;
+    }
+    return 1;
+#else
+    (void)out2; (void)reset;
+    return 0;                        // not a check build
+#endif
+}
 #if HM_STAMPS
 extern "C" int hm_debug_stamps(unsigned long long *out, int n, int reset) {
     if (n > HM_NSTAMP) n = HM_NSTAMP;

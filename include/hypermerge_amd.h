@@ -359,6 +359,12 @@ int hm_store_last_routing(const hm_store *s, uint32_t *out3);
  * has returned for that submit (the submit itself does not wait for its kernels). */
 int hm_store_last_kernel_ms(const hm_store *s, float *out2);
 
+/* Diagnostics of check builds (libhmgpu_check.so, built beside libhmgpu.so): out2[0] = documents
+ * whose next rows merge_small_kernel loaded asynchronously and re-read with counted loads,
+ * out2[1] = those whose two reads differed (the asynchronous wait was too short); reset zeroes
+ * both.  Returns 1 in a check build, 0 in the product build (out2 untouched), < 0 on a HIP error. */
+int hm_debug_async_check(unsigned long long *out2, int reset);
+
 /* Sizes of a document's log and merged state. */
 typedef struct {
     uint32_t n_changes, n_deps, n_ops, n_regs, n_objs, n_actors;
