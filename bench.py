@@ -352,17 +352,34 @@ def main() -> int:
     # ClockStore feed across the node (off the merge's critical path, timed separately):
     # every rank's changed DocBackend.clock rows, keyed by (docId hash, actorId hash), gathered
     # over RCCL through the C-ABI (hm_clock_allgather), plus the replica min-clock
+    value = applied_all * args.steps / wall_max
+    ms_per_step = wall_max * 1000.0 / args.steps
     xchg = None
     if ws > 1:
         # off the merge's critical path and outside `value`: a failure here is reported in the
-        # line instead of costing the whole scaling measurement
+        # line instead of costing the whole scaling measurement.  It has not run on a multi-GPU
+        # node yet, so a watchdog bounds it: past XCHG_TIMEOUT_S rank 0 prints the line with the
+        # exchange marked timed out and every rank exits (a hung collective must not cost the
+        # scaling measurement either)
+        import threading
+
+        def _expired():
+            if rank == 0:
+                _progress(f"clock exchange timed out after {XCHG_TIMEOUT_S} s")
+                fb = _line(args, ws, value, ms_per_step, nd, nc, no, batch, kern, None, ev_ms,
+                           {"error": f"timed out after {XCHG_TIMEOUT_S} s"})
+                print(dump_line(fb), flush=True)
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0)
+        dog = threading.Timer(XCHG_TIMEOUT_S, _expired)
+        dog.daemon = True
+        dog.start()
         try:
             xchg = _clock_exchange(eng, batch, run, dev, rank, ws, cfg)
         except Exception as ex:                       # noqa: BLE001 (reported, not hidden)
             xchg = {"error": f"{type(ex).__name__}: {ex}"[:300]}
-
-    value = applied_all * args.steps / wall_max
-    ms_per_step = wall_max * 1000.0 / args.steps
+        dog.cancel()
 
     # spot parity against the oracle on a sample (checker only; not timed)
     parity = None
@@ -503,32 +520,16 @@ def main() -> int:
                 ro["traffic_vs_alg"] = it["bytes_per_doc"] / ro["alg_bytes_per_doc"]
 
     if rank == 0:
-        line = {
-            "metric": "merged changes/sec (1M docs×8 actors) at 1/2/4/8 GPUs + % HBM roofline",
-            "value": value, "unit": "changes/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "u32", "data": "synthetic (seeded gossip feeds, hypermerge_amd/csrc/synth.cpp)",
-            "config": {"workload": f"{args.config}: {nd} docs/GPU x {batch.docs['n_actors'].max()} actors x "
-                                   f"{nc / max(nd, 1):.0f} changes/doc, {WORKLOAD_KIND.get(args.config, '')}"
-                                   + ("" if args.arrival is None else f", arrival order {ARRIVAL[args.arrival]}"), "docs_per_gpu": nd,
-                       "changes_per_gpu": nc, "ops_per_gpu": no, "parallelism": f"doc-shard{ws}"},
-            "roofline": {"bound": "hbm", "achieved": kern["achieved"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": kern["frac"], "traffic": traffic["bytes"] if traffic else None,
-                         "kernel": kern["kernel"], "kernel_ms": kern["kernel_ms"], "alg_bytes": kern["alg_bytes"],
-                         "kernels": kern["kernels"], "traffic_detail": traffic},
+        line = _line(args, ws, value, ms_per_step, nd, nc, no, batch, kern, traffic, ev_ms, xchg)
+        line.update({
             "cpu_baseline": cpu, "cpu_parallel": cpu_mt, "end_to_end": e2e, "from_blocks": from_blocks,
             "resident_incremental": incremental, "resident_incremental_text": incremental_text,
             "resident_incremental_c5": incremental_c5, "node_docbackend": node,
             "arrival_orders": orders,
             "host": _host_info(),
             "parity_sample_ok": parity, "unsupported_docs": unsupported, "error_docs": errors,
-            "gen_s": round(gen_s, 2), "event_ms_per_step": ev_ms / args.steps,
-            "clock_exchange": xchg,
-        }
-        if ws > 1:
-            line["ranks_note"] = (f"{ws} ranks, one per GPU, each merging its own {nd}-document shard (FNV-1a64(docId) % "
-                                  f"{ws}); value = changes of all ranks / max-over-ranks time. cpu_baseline, the side legs "
-                                  "and roofline.traffic (PMC passes) are measured at N=1 only; roofline is rank 0's kernel")
+            "gen_s": round(gen_s, 2),
+        })
 
         line["detail_file"] = None
         try:
@@ -544,6 +545,35 @@ def main() -> int:
     if ws > 1:
         dist.destroy_process_group()
     return 0
+
+
+XCHG_TIMEOUT_S = 120
+
+
+def _line(args, ws, value, ms_per_step, nd, nc, no, batch, kern, traffic, ev_ms, xchg) -> dict:
+    """The bench record's headline part (the side legs are added by the caller)."""
+    line = {
+        "metric": "merged changes/sec (1M docs×8 actors) at 1/2/4/8 GPUs + % HBM roofline",
+        "value": value, "unit": "changes/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u32", "data": "synthetic (seeded gossip feeds, hypermerge_amd/csrc/synth.cpp)",
+        "config": {"workload": f"{args.config}: {nd} docs/GPU x {batch.docs['n_actors'].max()} actors x "
+                               f"{nc / max(nd, 1):.0f} changes/doc, {WORKLOAD_KIND.get(args.config, '')}"
+                               + ("" if args.arrival is None else f", arrival order {ARRIVAL[args.arrival]}"), "docs_per_gpu": nd,
+                   "changes_per_gpu": nc, "ops_per_gpu": no, "parallelism": f"doc-shard{ws}"},
+        "roofline": {"bound": "hbm", "achieved": kern["achieved"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": kern["frac"], "traffic": traffic["bytes"] if traffic else None,
+                     "kernel": kern["kernel"], "kernel_ms": kern["kernel_ms"], "alg_bytes": kern["alg_bytes"],
+                     "kernels": kern["kernels"], "traffic_detail": traffic},
+        "cpu_baseline": None, "cpu_parallel": None,
+        "event_ms_per_step": ev_ms / args.steps,
+        "clock_exchange": xchg,
+    }
+    if ws > 1:
+        line["ranks_note"] = (f"{ws} ranks, one per GPU, each merging its own {nd}-document shard (FNV-1a64(docId) % "
+                              f"{ws}); value = changes of all ranks / max-over-ranks time. cpu_baseline, the side legs "
+                              "and roofline.traffic (PMC passes) are measured at N=1 only; roofline is rank 0's kernel")
+    return line
 
 
 def _from_blocks(eng, batch, cfg, args):
