@@ -114,6 +114,12 @@
 #ifndef HM_ASYNC_STORES
 #define HM_ASYNC_STORES 10  // store instructions an OK document's write_outputs issues at least (padded)
 #endif
+#ifndef HM_NT_OUT
+#define HM_NT_OUT 0         // dev A/B: the output rows (allDeps, history, registers, survivors) as non-temporal stores
+#endif
+#ifndef HM_NT_IN
+#define HM_NT_IN 0          // dev A/B: the next document's rows as non-temporal loads (read once)
+#endif
 #ifndef HM_ASYNC_CHECK
 #define HM_ASYNC_CHECK 0    // check builds (libhmgpu_check.so): every asynchronously loaded set of rows is re-read
                             // with counted loads and compared (hm_debug_async_check counts the differences)
@@ -647,14 +653,19 @@ __device__ __forceinline__ void async_check(const SmallParams &p, const hm_doc_r
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 struct AsyncRows { u32x2 c0, c1, c2; u32x4 a0, b0, a1, b1, a2, b2, a3, b3; u32x2 d0, d1; };
+#if HM_NT_IN
+#define HM_AL_POL " nt"
+#else
+#define HM_AL_POL ""
+#endif
 __device__ __forceinline__ u32x2 aload2(const void *p) {
     u32x2 v;
-    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    asm volatile("global_load_dwordx2 %0, %1, off" HM_AL_POL : "=v"(v) : "v"(p) : "memory");
     return v;
 }
 __device__ __forceinline__ u32x4 aload4(const void *p) {
     u32x4 v;
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    asm volatile("global_load_dwordx4 %0, %1, off" HM_AL_POL : "=v"(v) : "v"(p) : "memory");
     return v;
 }
 template <int OPL>
@@ -1651,6 +1662,23 @@ __device__ __forceinline__ SurvRows<OPL> surv_rows(const SmallParams &p, const S
     return o;
 }
 
+// one 16-byte output row (non-temporal under HM_NT_OUT: written once, never read by this kernel)
+__device__ __forceinline__ void st16(void *dst, uint4 v) {
+#if HM_NT_OUT
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<v4u *>(dst));
+#else
+    *reinterpret_cast<uint4 *>(dst) = v;
+#endif
+}
+__device__ __forceinline__ void st4(void *dst, uint32_t v) {
+#if HM_NT_OUT
+    __builtin_nontemporal_store(v, reinterpret_cast<uint32_t *>(dst));
+#else
+    *reinterpret_cast<uint32_t *>(dst) = v;
+#endif
+}
 template <int OPL, bool LISTS>
 __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallLds &L, uint32_t d, uint32_t ds,
                                               const hm_doc_row &doc, Outcome oc, const DocState &st, uint32_t mcmp,
@@ -1699,10 +1727,8 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
         return;
     }
     for (uint32_t r = lane; r < R; r += WAVE) {
-        hm_reg_result rr;
-        rr.n_surv = L.survcnt[r]; rr.surv_off = L.regoff[r]; rr.obj = L.regobj[r];
-        rr.list_index = (LISTS && st.doc_lists) ? (int32_t)L.insmin[r] : -1;
-        p.res_regs[doc.reg_off + r] = rr;
+        const int32_t li = (LISTS && st.doc_lists) ? (int32_t)L.insmin[r] : -1;
+        st16(p.res_regs + doc.reg_off + r, make_uint4(L.survcnt[r], L.regoff[r], (uint32_t)li, L.regobj[r]));
     }
     // allDeps rows: lane = arrival index writes its change's row (zeros if not applied;
     // chain[a] is empty for a >= A)
@@ -1713,8 +1739,8 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
             uint32_t v[NA_MAX];
 #pragma unroll
             for (int a = 0; a < NA_MAX; a++) v[a] = (uint32_t)__popcll(an & L.chain[a]);
-            reinterpret_cast<uint4 *>(row)[0] = make_uint4(v[0], v[1], v[2], v[3]);
-            if (S == 8) reinterpret_cast<uint4 *>(row)[1] = make_uint4(v[4], v[5], v[6], v[7]);
+            st16(row, make_uint4(v[0], v[1], v[2], v[3]));
+            if (S == 8) st16(row + 4, make_uint4(v[4], v[5], v[6], v[7]));
         } else {
             for (uint32_t a = 0; a < S; a++) row[a] = a < NA_MAX ? (uint32_t)__popcll(an & L.chain[a]) : 0u;
         }
@@ -1730,7 +1756,7 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
     }
     const bool act = lane < n;
     const u64 q = __ballot(act && st.hist == -1);
-    if (act) p.res_hist[doc.change_off + lane] = st.hist;
+    if (act) st4(p.res_hist + doc.change_off + lane, (uint32_t)st.hist);
     if (lane == 0) {
         hm_doc_result r = {};
         r.status = HM_OK; r.err_change = HM_NONE; r.err_op = HM_NONE;
@@ -1741,7 +1767,8 @@ __device__ __forceinline__ void write_outputs(const SmallParams &p, const SmallL
 #pragma unroll
     for (int t = 0; t < OPL; t++) {
         const uint32_t q = lane + WAVE * t;
-        if (q < st.total) p.res_surv[doc.op_off + q] = sv.r[t];
+        if (q < st.total) st16(p.res_surv + doc.op_off + q, make_uint4(sv.r[t].op, sv.r[t].vtag, (uint32_t)sv.r[t].value,
+                                                                       (uint32_t)(sv.r[t].value >> 32)));
     }
 }
 
