@@ -1309,32 +1309,24 @@ __device__ __forceinline__ uint32_t change_of_op(const hm_change_row *ch, uint32
 // directory ldir = (object, elements) per list.
 // Documents that are not clean (an error, queued changes) get flags = 0: their next submit
 // re-merges.
-__device__ __forceinline__ bool meta_skip(const MetaArgs &a, const DevDoc &m, const hm_doc_result &r) {
-    // (mode 1: a small document with lists re-merges every round — one small-kernel wave either
-    // way — so it keeps no incremental state at all)
-    return r.status != HM_OK || r.n_queued != 0 || r.n_surv > m.o_cap ||
-           ((m.flags & HM_DOC_HAS_LISTS) && m.n_o <= a.small_lists);
-}
-
 __global__ __launch_bounds__(256) void inc_meta_kernel(MetaArgs a) {
     const uint32_t lane = threadIdx.x & 63;
-    // a wave takes 64 listed documents: one lane each decides whether the document keeps state
-    // (the documents that keep none — errors, queued changes, mode 1's small list documents,
-    // often every document of a C5 round — cost one lane, not a wave), then the wave builds the
-    // state of the others one after the other
-    for (uint32_t q0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 64; q0 < a.n; q0 += gridDim.x * 4 * 64) {
-        const uint32_t qi = q0 + lane;
-        bool keep = false;
-        uint32_t hl = 0;
-        if (qi < a.n) {
-            hl = a.list[qi];
-            keep = !meta_skip(a, a.dm[hl], a.res_docs[hl]);
-            if (!keep) { IncState z = {}; a.ist[hl] = z; }
-        }
-        for (unsigned long long km = __ballot(keep); km; km &= km - 1) {
-        const uint32_t h = (uint32_t)__shfl((int)hl, (int)__builtin_ctzll(km));
+    // one wave per listed document: the re-merged documents of a submit are few and large (their
+    // state is rebuilt from whole logs) or many and small (a few loads each, then skipped), and a
+    // wave per document keeps the large ones in parallel (a round-6 variant that let one lane per
+    // document decide first and a wave build the kept ones serially cost a C3 round the sum of its
+    // few re-merged documents' rebuilds: 0.35 -> 1.07 ms)
+    for (uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6); q < a.n; q += gridDim.x * 4) {
+        const uint32_t h = a.list[q];
         const DevDoc m = a.dm[h];
         const hm_doc_result r = a.res_docs[h];
+        // (mode 1: a small document with lists re-merges every round — one small-kernel wave either
+        // way — so it keeps no incremental state at all)
+        if (r.status != HM_OK || r.n_queued != 0 || r.n_surv > m.o_cap ||
+            ((m.flags & HM_DOC_HAS_LISTS) && m.n_o <= a.small_lists)) {
+            if (lane == 0) { IncState z = {}; a.ist[h] = z; }
+            continue;
+        }
         const hm_change_row *ch = a.changes + m.c_off;
         for (uint32_t i = lane; i < r.n_surv; i += 64) {
             const uint32_t op = a.surv[m.o_off + i].op;
@@ -1452,7 +1444,6 @@ __global__ __launch_bounds__(256) void inc_meta_kernel(MetaArgs a) {
             st.pad[0] = (flags & HM_IST_LIST) ? n_el : 0u; st.pad[1] = (flags & HM_IST_LIST) ? nlst : 0u;
             a.ist[h] = st;
         }
-        }
     }
 }
 
@@ -1502,7 +1493,7 @@ hipError_t hm_launch_inc_apply(const IncArgs &A, hipStream_t s) {
 
 hipError_t hm_launch_inc_meta(const MetaArgs &a, hipStream_t s) {
     if (!a.n) return hipSuccess;
-    const uint32_t waves = (a.n + 63) / 64, grid = (waves + 3) / 4 < 65535u ? (waves + 3) / 4 : 65535u;
+    const uint32_t grid = (a.n + 3) / 4 < 65535u ? (a.n + 3) / 4 : 65535u;
     hipLaunchKernelGGL(hmi::inc_meta_kernel, dim3(grid), dim3(256), 0, s, a);
     return hipGetLastError();
 }
