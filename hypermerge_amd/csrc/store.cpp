@@ -86,6 +86,7 @@ struct hm_store {
     DBuf<AppendDesc> descs, bdescs;
     DBuf<uint32_t> list;                          // re-merge list (cold, then handed back)
     DBuf<uint32_t> blist;                         // rollback list
+    DBuf<uint32_t> klist;                         // a re-merge's documents that may keep incremental state
     DBuf<uint32_t> alist;                         // append list (batch rows with append work)
     DBuf<uint8_t> remap, inv;
     DBuf<hm_doc_row> rows;
@@ -107,6 +108,10 @@ struct hm_store {
     DBuf<uint32_t> undo_handles;
     // incremental applyRemoteChanges (inc_apply_kernel) and the last submit's routing
     bool incremental = true;
+    // some document may hold incremental state (an IncState with HM_IST_VALID): set when a re-merge
+    // lists a document that may keep one, or the path is switched on over old state; until then no
+    // document can route to the incremental kernels and a submit does not launch them
+    bool any_state = false;
     uint32_t inc_mode = 1;                        // 1: small list documents re-merge (cost policy); 2: every one
     uint32_t st_inc = 0, st_cold = 0, st_bail = 0;
     // HIP events around the last submit's incremental kernels and its re-merge (engine stream)
@@ -292,9 +297,11 @@ int launch_list_merge(hm_store *s, const uint32_t *dev_list, uint32_t n) {
     if (!n) return HM_OK;
     hipStream_t st = hm_engine_stream(s->e);
     int rc;
-    if ((rc = ensure_buf(s, s->rows, n))) return rc;
+    if ((rc = ensure_buf(s, s->rows, n)) || (rc = ensure_buf(s, s->klist, n))) return rc;
     if ((rc = reset_stats(s))) return rc;
-    SCHK(s, hm_launch_doc_rows(dev_list, n, s->dm, s->rows.p, s->st, st));
+    const uint32_t small_lists = s->inc_mode == 1 ? HM_INC_SMALL_LIST_OPS : 0u;
+    SCHK(s, hm_launch_doc_rows(dev_list, n, s->dm, s->rows.p, s->st, small_lists, s->incremental ? s->ist : nullptr,
+                               s->klist.p, st));
     rc = HM_OK;
     const PlanStats P = read_stats(s, &rc);
     if (rc) return rc;
@@ -317,14 +324,18 @@ int launch_list_merge(hm_store *s, const uint32_t *dev_list, uint32_t n) {
     // the incremental path keeps list documents' element order: positions written by the merge
     // (mode 1: when every listed document holds <= HM_INC_SMALL_LIST_OPS ops, none with lists keeps
     // incremental state — inc_meta skips them — so no positions are needed)
-    const bool positions = s->incremental && (P.flags & HM_DOC_HAS_LISTS) &&
-                           !(s->inc_mode == 1 && P.max_o <= HM_INC_SMALL_LIST_OPS);
-    if (positions) SCHK(s, hm_launch_epos_clear(dev_list, n, s->dm, s->epos, st));
+    // (P.mx[3]: listed list documents that may keep incremental state)
+    const bool positions = s->incremental && (P.flags & HM_DOC_HAS_LISTS) && P.mx[3] != 0;
+    if (positions) SCHK(s, hm_launch_epos_clear(s->klist.p, P.mx[2], s->dm, s->epos, st));     // (the keep list)
     rc = hm_engine_launch_merge(s->e, &b, &o, dev_list, &ext, positions ? s->epos : nullptr);
-    // the incremental path's survivor metadata of the re-merged documents (packed survivors)
-    if (rc == HM_OK && s->incremental) {
+    // the incremental path's survivor metadata of the re-merged documents that may keep state (the
+    // keep list doc_rows_kernel built; it cleared the others' IncState).  A store none of whose
+    // documents ever kept state (any_state: e.g. mode 1 with only small list documents) launches
+    // no incremental kernel in its submits
+    if (P.mx[2]) s->any_state = true;
+    if (rc == HM_OK && s->incremental && P.mx[2]) {
         MetaArgs M;
-        M.list = dev_list; M.n = n; M.dm = s->dm; M.res_docs = s->res_docs; M.changes = s->changes; M.hist = s->hist;
+        M.list = s->klist.p; M.n = P.mx[2]; M.dm = s->dm; M.res_docs = s->res_docs; M.changes = s->changes; M.hist = s->hist;
         M.ckey = s->ckey; M.ops = s->ops; M.surv = s->surv; M.smeta = s->smeta; M.ist = s->ist;
         M.epos = s->epos; M.epar = s->epar; M.ekey = s->ekey; M.lorder = s->lorder; M.ldir = s->ldir;
         M.small_lists = s->inc_mode == 1 ? HM_INC_SMALL_LIST_OPS : 0u;
@@ -438,7 +449,7 @@ void hm_store_destroy(hm_store *s) {
     void *bufs[] = {s->changes, s->hist, s->ckey, s->all_deps, s->deps, s->ops, s->surv, s->smeta, s->ist, s->ldir, s->regs, s->epos,
                     s->epar, s->ekey, s->lorder, s->res_docs, s->clock,
                     s->back_clock, s->heads, s->min_clock, s->stored, s->stage.p, s->dm, s->seen, s->plan.p, s->descs.p,
-                    s->bdescs.p, s->list.p, s->blist.p, s->alist.p, s->remap.p, s->inv.p, s->rows.p, s->undo_handles.p, s->st};
+                    s->bdescs.p, s->list.p, s->blist.p, s->alist.p, s->remap.p, s->inv.p, s->rows.p, s->undo_handles.p, s->klist.p, s->st};
     for (void *b : bufs) if (b) (void)hipFree(b);
     for (hipEvent_t e : s->ev) if (e) (void)hipEventDestroy(e);
     if (s->h_st) (void)hipHostFree(s->h_st);
@@ -587,7 +598,7 @@ static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handl
             SCHK(s, hm_launch_append(s->descs.p, n, ar, ar, A.changes, t_dp, t_op, A.remap, S, st, s->alist.p, &s->st->n_app));
             T.mark("alloc+append");
             SCHK(s, hipEventRecord(s->ev[0], st));
-            if (A.incremental) {
+            if (A.incremental && s->any_state) {
                 IncArgs IA;
                 IA.descs = s->descs.p; IA.n = n; IA.list = nullptr; IA.S = S;
                 IA.st_changes = A.changes; IA.st_deps = t_dp; IA.st_ops = t_op;

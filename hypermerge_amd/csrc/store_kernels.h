@@ -45,7 +45,8 @@ struct PlanStats {
     uint32_t err;                              // HM_PLAN_* bits of the failed checks
     uint32_t n_inc, n_cold, n_back, n_app;       // (n_app: batch rows append_kernel has work for)
     uint32_t mx[6];                            // mx[0]: documents routed to the lane pass; mx[1] = 1: alloc_kernel
-                                               //   found no room for the growth and moved nothing (the rest unused)
+                                               //   found no room for the growth and moved nothing; mx[2] / mx[3]:
+                                               //   doc_rows_kernel's may-keep-state counts (all / with lists)
     uint32_t max_c, max_o, max_r, max_objs, max_d, flags;   // launch hints of a merge list
     unsigned long long need[4];                // rows the submit's growing segments take, per space
     unsigned long long tot_c, tot_d, tot_o, tot_r;
@@ -178,8 +179,11 @@ struct PlanArgs {
 hipError_t hm_launch_plan(const PlanArgs &a, hipStream_t s);
 hipError_t hm_launch_alloc(const PlanArgs &a, hipStream_t s);
 // hm_doc_row of each listed handle from its device meta (+ the launch hints in st)
+// (mx[2] / mx[3] of the stats: listed documents that may keep incremental state after their re-merge —
+// all but the list documents of at most small_lists ops — and those of them with lists; keep (if
+// not NULL) lists the former's handles, ist (if not NULL) has the others' IncState cleared)
 hipError_t hm_launch_doc_rows(const uint32_t *list, uint32_t n, const DevDoc *dm, hm_doc_row *rows, PlanStats *st,
-                              hipStream_t s);
+                              uint32_t small_lists, IncState *ist, uint32_t *keep, hipStream_t s);
 // documents of a batch whose merge failed (every = all of the batch's documents): totals restored,
 // rows re-ranked back, listed for re-merge
 hipError_t hm_launch_rollback(const uint32_t *handles, uint32_t n, const hm_doc_result *res_docs, PlanRow *plan,

@@ -500,16 +500,28 @@ __global__ __launch_bounds__(ALLOC_WG) void alloc_kernel(PlanArgs a) {
 }
 
 __global__ __launch_bounds__(PLAN_WG) void doc_rows_kernel(const uint32_t *list, uint32_t n, const DevDoc *dm, hm_doc_row *rows,
-                                                          PlanStats *st) {
-    // per workgroup: 5 maxima, the flags OR, 4 sums -> LDS, then one atomic each
-    __shared__ uint32_t s_mx[6];
+                                                          PlanStats *st, uint32_t small_lists, IncState *ist, uint32_t *keep) {
+    // per workgroup: 5 maxima, the flags OR, 4 sums, the keep counts -> LDS, then one atomic each
+    __shared__ uint32_t s_mx[8];
     __shared__ unsigned long long s_tot[4];
-    if (threadIdx.x < 6) s_mx[threadIdx.x] = 0;
+    __shared__ uint32_t s_kw[PLAN_WG / 64], s_kbase;
+    if (threadIdx.x < 8) s_mx[threadIdx.x] = 0;
     if (threadIdx.x < 4) s_tot[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    bool kp = false;
+    uint32_t h = 0;
     if (i < n) {
-        const DevDoc m = dm[list[i]];
+        h = list[i];
+        const DevDoc m = dm[h];
+        // documents that may keep incremental state after this re-merge (inc_meta_kernel decides;
+        // mode 1's small list documents never do), and those of them with lists; the others'
+        // state is cleared here (incremental stores)
+        const bool lists = (m.flags & HM_DOC_HAS_LISTS) != 0;
+        kp = !(lists && m.n_o <= small_lists);
+        if (kp && lists) atomicAdd(&s_mx[7], 1u);
+        if (!kp && ist) { IncState z = {}; ist[h] = z; }
         hm_doc_row r;
         r.change_off = m.c_off; r.n_changes = m.n_c; r.dep_off = m.d_off; r.n_deps = m.n_d;
         r.op_off = m.o_off; r.n_ops = m.n_o; r.reg_off = m.r_off; r.n_regs = m.n_r;
@@ -520,7 +532,21 @@ __global__ __launch_bounds__(PLAN_WG) void doc_rows_kernel(const uint32_t *list,
         atomicAdd(&s_tot[0], (unsigned long long)m.n_c); atomicAdd(&s_tot[1], (unsigned long long)m.n_d);
         atomicAdd(&s_tot[2], (unsigned long long)m.n_o); atomicAdd(&s_tot[3], (unsigned long long)m.n_r);
     }
+    // the keep list (inc_meta's and the position clear's work list): one slot atomic per workgroup
+    const unsigned long long km = __ballot(kp);
+    if (ln == 0) s_kw[wv] = (uint32_t)__popcll(km);
     __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (uint32_t w = 0; w < PLAN_WG / 64; w++) t += s_kw[w];
+        s_kbase = t ? atomicAdd(&st->mx[2], t) : 0u;
+    }
+    __syncthreads();
+    if (kp && keep) {
+        uint32_t off = s_kbase + (uint32_t)__popcll(km & ((1ull << ln) - 1));
+        for (uint32_t w = 0; w < wv; w++) off += s_kw[w];
+        keep[off] = h;
+    }
     switch (threadIdx.x) {
     case 0: atomicMax(&st->max_c, s_mx[0]); break;
     case 1: atomicMax(&st->max_o, s_mx[1]); break;
@@ -532,6 +558,7 @@ __global__ __launch_bounds__(PLAN_WG) void doc_rows_kernel(const uint32_t *list,
     case 7: atomicAdd(&st->tot_d, s_tot[1]); break;
     case 8: atomicAdd(&st->tot_o, s_tot[2]); break;
     case 9: atomicAdd(&st->tot_r, s_tot[3]); break;
+    case 11: if (s_mx[7]) atomicAdd(&st->mx[3], s_mx[7]); break;
     default: break;
     }
 }
@@ -651,9 +678,10 @@ hipError_t hm_launch_alloc(const PlanArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t hm_launch_doc_rows(const uint32_t *list, uint32_t n, const DevDoc *dm, hm_doc_row *rows, PlanStats *st,
-                              hipStream_t s) {
+                              uint32_t small_lists, IncState *ist, uint32_t *keep, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(hms::doc_rows_kernel, dim3((n + PLAN_WG - 1) / PLAN_WG), dim3(PLAN_WG), 0, s, list, n, dm, rows, st);
+    hipLaunchKernelGGL(hms::doc_rows_kernel, dim3((n + PLAN_WG - 1) / PLAN_WG), dim3(PLAN_WG), 0, s, list, n, dm, rows, st,
+                       small_lists, ist, keep);
     return hipGetLastError();
 }
 hipError_t hm_launch_rollback(const uint32_t *handles, uint32_t n, const hm_doc_result *res_docs, PlanRow *plan,
