@@ -137,14 +137,17 @@ def test_docset_failed_call_is_undone_everywhere(where, monkeypatch):
     info0, view0 = [ds.info(x) for x in (d, d + 1)], [ds.view(x) for x in (d, d + 1)]
     r2 = [narrow[2:] + [{"actor": "n0", "seq": 2, "deps": {"n1": 1, "n2": 1}, "ops": [{"action": "del", "obj": R, "key": "k"}]}],
           wide[10:] + [{"actor": "w00", "seq": 2, "deps": {"w05": 1}, "ops": [{"action": "set", "obj": R, "key": "k1", "value": 7}]}]]
+    routed0 = ds.routing()
     monkeypatch.setenv("HM_DOCSET_INJECT_FAIL", where)
     with pytest.raises(EngineError):
         ds.apply([d, d + 1], [_blocks(r2[0]), _blocks(r2[1])])
     monkeypatch.delenv("HM_DOCSET_INJECT_FAIL")
     assert [ds.info(x) for x in (d, d + 1)] == info0
     assert [ds.view(x) for x in (d, d + 1)] == view0
+    assert ds.routing() == routed0                            # the undone call's rounds are not counted
     res, js = ds.apply([d, d + 1], [_blocks(r2[0]), _blocks(r2[1])])
     assert (res["status"] == 0).all()
+    assert sum(ds.routing().values()) == sum(routed0.values()) + 2
     for k, (x, log) in enumerate(((d, narrow + r2[0][1:]), (d + 1, wide + r2[1][2:]))):
         s = _oracle(log)
         assert js["p"][k]["clock"] == s["clock"] and js["b"][k] == s["backend_clock"]
