@@ -697,9 +697,10 @@ def _incremental(eng, batch, args, tail=4, oracle_docs=0):
     its next 1-2 changes (DocBackend.ts:169-185).  `value`: the rounds' new rows already in HBM
     (hm_batch_submit_device + hm_batch_wait_device: plan, append, the incremental kernels, the
     gathered per-document results), the same convention as the headline.  The same rounds run on
-    a second store with the incremental path off (whole-log re-merge) for the comparison and an
-    equality check of every round's results, and on a third through the host entry points
-    (hm_batch_submit / hm_batch_wait from page-locked buffers: PCIe included, never `value`)."""
+    stores with the incremental path off (whole-log re-merge) for the comparison and an equality
+    check of every round's results — two of each kind, timed in both orders every round — and on
+    one more through the host entry points (hm_batch_submit / hm_batch_wait from page-locked
+    buffers: PCIe included, never `value`)."""
     import torch
     from hypermerge_amd.store import RowStore, slice_changes, BatchResult
     from hypermerge_amd.columnar import DOC_RESULT_DT
@@ -720,7 +721,11 @@ def _incremental(eng, batch, args, tail=4, oracle_docs=0):
     first = slice_changes(batch, np.zeros(n, np.int64), start)
     fc, ft = to_dev(first, np.arange(n))
     stores = []
-    for inc in (True, False, True):
+    # [0] incremental and [1] re-merge timed in that order each round, [3] incremental and [4] re-merge
+    # in the other order (a leg that goes first meets the host's work between rounds, ~0.1 ms: each
+    # leg's time is the mean of one first and one second run, whatever the rounds' sizes); [2] the
+    # PCIe leg
+    for inc in (True, False, True, True, False):
         st = RowStore(eng, a_stride=S)
         st.set_incremental(inc)
         h0 = st.open_n(n)
@@ -741,7 +746,7 @@ def _incremental(eng, batch, args, tail=4, oracle_docs=0):
         cnt, t = to_dev(sub, sel)
         rounds_in.append((sub, sel.astype(np.uint32), cnt, t))
         pos = np.maximum(pos, hi)
-    out = [torch.empty(n * (32 + 12 * S), dtype=torch.uint8, device=dev) for _ in range(2)]
+    out = [torch.empty(n * (32 + 12 * S), dtype=torch.uint8, device=dev) for _ in range(4)]
     keep = BatchResult(pinned((n,), DOC_RESULT_DT), pinned((n, S), np.uint32), pinned((n, S), np.uint32),
                        pinned((n, S), np.uint32))
     rounds, same, routing_ok = [], True, True
@@ -749,19 +754,24 @@ def _incremental(eng, batch, args, tail=4, oracle_docs=0):
         r = {"docs": int(len(sel)), "changes": int(len(sub.changes)), "ops": int(len(sub.ops)),
              "alg_bytes": inc_alg_bytes(sub, S), "survey_bytes": inc_survey_bytes(sub, S)}
         nb = len(sel) * (32 + 12 * S)
-        legs = list(zip(stores[:2], ("incremental", "remerge"), out))
-        # the two legs take turns going first (the first submit after the host's work between
-        # rounds meets an idle, down-clocked GPU)
-        for st, tag, o in (legs if ri % 2 == 0 else legs[::-1]):
+        runs = {"incremental": [], "remerge": []}
+        order = [(stores[0], "incremental", out[0]), (stores[1], "remerge", out[1]),
+                 (stores[4], "remerge", out[3]), (stores[3], "incremental", out[2])]
+        for st, tag, o in (order if ri % 2 == 0 else order[2:] + order[:2]):
             torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
             st.submit_device(len(sel), cnt, *t)
             nf = st.wait_device(o)
             torch.cuda.synchronize(dev)
             dt = time.perf_counter() - t0
-            r[tag] = {"ms": dt * 1e3, "changes_per_s": len(sub.changes) / dt, "routing": st.last_routing(), "failed": nf,
-                      **st.last_kernel_ms()}
-        same &= bool(torch.equal(out[0][:nb], out[1][:nb]))
+            runs[tag].append({"ms": dt * 1e3, "routing": st.last_routing(), "failed": nf, **st.last_kernel_ms()})
+        for tag, rs in runs.items():
+            ms = sum(x["ms"] for x in rs) / len(rs)
+            r[tag] = dict(rs[0], ms=ms, changes_per_s=len(sub.changes) / (ms * 1e-3), ms_runs=[x["ms"] for x in rs],
+                          incremental_ms=sum(x["incremental_ms"] for x in rs) / len(rs),
+                          remerge_ms=sum(x["remerge_ms"] for x in rs) / len(rs))
+        same &= bool(torch.equal(out[0][:nb], out[1][:nb])) and bool(torch.equal(out[2][:nb], out[3][:nb])) and \
+            bool(torch.equal(out[0][:nb], out[2][:nb]))
         routing_ok &= r["incremental"]["routing"]["incremental"] == len(sel)
         # PCIe leg: host tables in page-locked memory, results into kept page-locked arrays
         pb = _pinned_rows(sub)
