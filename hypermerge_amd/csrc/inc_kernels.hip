@@ -92,7 +92,8 @@ constexpr unsigned long long TWO53 = 1ull << 53;
 // insert after an element not inserted yet, a duplicate elemId) goes to the re-merge.  Sets /
 // deletes on elements are applyAssign as for map keys; the visible indices (per list) are then
 // rewritten from the first position that changed.
-constexpr uint32_t LSCR = 192;                 // per document: anchors (64), cumulative block sizes (64), subtree sizes (64)
+// per document (a group of G lanes): anchors (G), cumulative block sizes (G), subtree sizes (G)
+template <int G> constexpr uint32_t lscr_words() { return 3u * (uint32_t)G; }
 constexpr uint32_t LMAX = HM_INC_LISTS;
 
 struct ListPlan {
@@ -103,15 +104,17 @@ struct ListPlan {
     uint32_t bnew, cnew;                       // lane k < nl: list k's base and elements after the submit
 };
 
+template <int G>
 __device__ __forceinline__ uint32_t list_shift(const uint32_t *lscr, uint32_t na, uint32_t i) {
     uint32_t s = 0;
     for (uint32_t k = 0; k < na; k++)
-        if ((int)lscr[k] - 1 < (int)i) s = lscr[64 + k];     // blocks of the anchors at or before position i
+        if ((int)lscr[k] - 1 < (int)i) s = lscr[G + k];      // blocks of the anchors at or before position i
     return s;
 }
 
 // the list (directory index) holding global position i, from the lanes' (base, count)
-__device__ __forceinline__ uint32_t list_at(const Grp<64> &g, uint32_t nl, uint32_t b, uint32_t c, uint32_t i) {
+template <int G>
+__device__ __forceinline__ uint32_t list_at(const Grp<G> &g, uint32_t nl, uint32_t b, uint32_t c, uint32_t i) {
     uint32_t l = HM_NONE;
     for (uint32_t k = 0; k < nl; k++) {
         const uint32_t bk = g.sh(b, k), ck = g.sh(c, k);
@@ -122,7 +125,8 @@ __device__ __forceinline__ uint32_t list_at(const Grp<64> &g, uint32_t nl, uint3
 
 // li: the op's list (directory index; HM_NONE for other ops); dir: lane k < nl holds list k's
 // directory entry (object, elements)
-__device__ int list_plan(const Grp<64> &g, const AppendDesc &D, const IncArgs &A, const IncState &I, uint32_t nno,
+template <int G>
+__device__ int list_plan(const Grp<G> &g, const AppendDesc &D, const IncArgs &A, const IncState &I, uint32_t nno,
                          uint32_t o_act, uint32_t o_reg, uint32_t o_par, uint32_t o_elem, bool lst, uint32_t li,
                          uint32_t opactor, uint2 dir, uint32_t *lscr, ListPlan &lp) {
     const uint32_t gl = g.gl, n_el = I.pad[0], nl = I.pad[1];
@@ -171,7 +175,7 @@ __device__ int list_plan(const Grp<64> &g, const AppendDesc &D, const IncArgs &A
     if (g.bits(bad)) return INC_BAIL;
 
     // subtree sizes in the round's forest: every element counts itself at each of its ancestors
-    uint32_t *sz = lscr + 128;
+    uint32_t *sz = lscr + 2 * G;
     sz[gl] = 0;
     __builtin_amdgcn_wave_barrier();
     {
@@ -222,10 +226,10 @@ __device__ int list_plan(const Grp<64> &g, const AppendDesc &D, const IncArgs &A
         if (leader && ak < akey) idx++;
         if (leader && ak <= akey) cum += bk2;
     }
-    if (leader) { lscr[idx] = ins_at; lscr[64 + idx] = cum; }
+    if (leader) { lscr[idx] = ins_at; lscr[G + idx] = cum; }
     __builtin_amdgcn_wave_barrier();
     uint32_t pmin = ins ? (ranc >> 4) : HM_NONE;
-    for (uint32_t d = 1; d < 64; d <<= 1) { const uint32_t y = g.sh(pmin, gl ^ d); pmin = y < pmin ? y : pmin; }
+    for (uint32_t d = 1; d < (uint32_t)G; d <<= 1) { const uint32_t y = g.sh(pmin, gl ^ d); pmin = y < pmin ? y : pmin; }
     lp.n_el0 = n_el; lp.n_el = n_el + nins; lp.na = na; lp.pmin = nins ? pmin : n_el;
     lp.key = key;
     lp.npos = ins ? (ranc >> 4) + before + rank : HM_NONE;
@@ -244,27 +248,28 @@ __device__ int list_plan(const Grp<64> &g, const AppendDesc &D, const IncArgs &A
     uint32_t qe = HM_NONE;
     {
         const uint32_t cnp = g.sh(lp.npos, ecr == HM_NONE ? 0u : ecr);
-        const uint32_t sh = list_shift(lscr, na, eold == HM_NONE ? 0u : eold);
+        const uint32_t sh = list_shift<G>(lscr, na, eold == HM_NONE ? 0u : eold);
         if (eop) qe = ecr != HM_NONE ? cnp : eold + sh;
     }
     uint32_t q0 = qe < lp.pmin ? qe : lp.pmin;
-    for (uint32_t d = 1; d < 64; d <<= 1) { const uint32_t y = g.sh(q0, gl ^ d); q0 = y < q0 ? y : q0; }
+    for (uint32_t d = 1; d < (uint32_t)G; d <<= 1) { const uint32_t y = g.sh(q0, gl ^ d); q0 = y < q0 ? y : q0; }
     lp.q0 = q0;
     return INC_DONE;
 }
 
 // the order rewritten: old elements from pmin on shift right (from the end, 64 at a time: every
 // move goes up, so nothing is overwritten before it is read), then the new elements land
-__device__ void list_insert(const Grp<64> &g, const AppendDesc &D, const IncArgs &A, const IncState &I, uint32_t o_act,
+template <int G>
+__device__ void list_insert(const Grp<G> &g, const AppendDesc &D, const IncArgs &A, const IncState &I, uint32_t o_act,
                             uint32_t o_reg, uint32_t o_par, const uint32_t *lscr, const ListPlan &lp) {
     const uint32_t gl = g.gl;
     if (lp.n_el > lp.n_el0)
-        for (int top = (int)lp.n_el0 - 1; top >= (int)lp.pmin; top -= 64) {
+        for (int top = (int)lp.n_el0 - 1; top >= (int)lp.pmin; top -= G) {
             const int i = top - (int)gl;
             const bool v = i >= (int)lp.pmin;
             const uint32_t e = v ? A.lorder[D.dst_r + i] : 0u;
             if (v) {
-                const uint32_t np = (uint32_t)i + list_shift(lscr, lp.na, (uint32_t)i);
+                const uint32_t np = (uint32_t)i + list_shift<G>(lscr, lp.na, (uint32_t)i);
                 A.lorder[D.dst_r + np] = e;
                 A.epos[D.dst_r + e] = np;
             }
@@ -279,14 +284,15 @@ __device__ void list_insert(const Grp<64> &g, const AppendDesc &D, const IncArgs
 
 // visible indices (hm_reg_result.list_index, counted per list) from the first position that
 // changed to the end of the last list
-__device__ void list_indices(const Grp<64> &g, const AppendDesc &D, const IncArgs &A, const ListPlan &lp) {
+template <int G>
+__device__ void list_indices(const Grp<G> &g, const AppendDesc &D, const IncArgs &A, const ListPlan &lp) {
     const uint32_t gl = g.gl, nl = lp.nl, bn = lp.bnew, cn = lp.cnew;
     if (lp.q0 >= lp.n_el) return;
     const uint32_t l0 = list_at(g, nl, bn, cn, lp.q0);
     const uint32_t b0 = g.sh(bn, l0 < nl ? l0 : 0u);
     const uint32_t start = l0 < nl ? b0 : lp.q0;
     uint32_t c = 0;                                           // visible elements of q0's list before q0
-    for (int top = (int)lp.q0 - 1; top >= (int)start; top -= 64) {
+    for (int top = (int)lp.q0 - 1; top >= (int)start; top -= G) {
         const int i = top - (int)gl;
         bool v = false;
         int32_t li = -1;
@@ -298,7 +304,7 @@ __device__ void list_indices(const Grp<64> &g, const AppendDesc &D, const IncArg
         const uint64_t m = g.bits(v);
         if (m) { c = (uint32_t)g.sh((uint32_t)li, (uint32_t)__builtin_ctzll(m)) + 1u; break; }
     }
-    for (uint32_t q = lp.q0; q < lp.n_el; q += 64) {
+    for (uint32_t q = lp.q0; q < lp.n_el; q += G) {
         const uint32_t i = q + gl;
         hm_reg_result *r = nullptr;
         bool v = false;
@@ -322,7 +328,7 @@ __device__ void list_indices(const Grp<64> &g, const AppendDesc &D, const IncArg
         const int32_t li = v ? (int32_t)((cont ? c : 0u) + (uint32_t)__popcll(mine)) : -1;
         if (r && li != old) r->list_index = li;
         // the carry: the visible elements of the chunk's last list, this chunk's included
-        const uint32_t last = lp.n_el - 1u - q < 63u ? lp.n_el - 1u - q : 63u;
+        const uint32_t last = lp.n_el - 1u - q < (uint32_t)G - 1u ? lp.n_el - 1u - q : (uint32_t)G - 1u;
         const uint32_t sl = g.sh(s, last);
         const bool cl = g.sh(cont ? 1u : 0u, last) != 0u;
         const uint64_t tail = m & (last >= 63 ? ~0ull : ((1ull << (last + 1)) - 1)) & ~((1ull << sl) - 1);
@@ -362,13 +368,14 @@ __device__ __forceinline__ void inc_append(const Grp<G> &g, const AppendDesc &D,
     for (uint32_t i = gl; i < 2 * nno; i += G) do4[i] = so4[i];
 }
 
-template <int G>
+template <int G, bool LS = false>
 __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 *smt, uint32_t *lscr, bool appended = false,
                         uint32_t bi = HM_NONE) {
     const Grp<G> g;
     const uint32_t gl = g.gl;
     const uint32_t S = A.S, h = D.handle, NA = D.n_actors, nnc = D.n_new_c, nno = D.n_new_o, nnd = D.n_new_d;
     constexpr int FAILG = G < 64 ? INC_DEFER : INC_BAIL;     // a limit of this group size only
+    constexpr bool LST = G == 64 || (HM_INC_LIST_GROUPS && LS);   // list / text ops taken by this instantiation
     constexpr uint32_t KT = G >= 32 ? 1u : 32u / G;           // the log's last KT * G rows are searched first
     // the new rows: a document whose segments did not move gets them appended here — before
     // anything can hand the document over, since the re-merge reads them from the log
@@ -380,9 +387,9 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
     // ---- level 2: everything that depends only on the descriptor ----
     const IncState I = A.ist[h];
     const hm_doc_result R0 = A.res_docs[h];
-    // the list directory (one document per wave only: lane k < HM_INC_LISTS holds entry k)
+    // the list directory (lane k < HM_INC_LISTS holds entry k)
     uint2 dir = make_uint2(HM_NONE, 0u);
-    if constexpr (G == 64) { if (A.ldir && gl < LMAX) dir = A.ldir[(size_t)h * LMAX + gl]; }
+    if constexpr (LST) { if (A.ldir && gl < LMAX) dir = A.ldir[(size_t)h * LMAX + gl]; }
     uint32_t ck = 0, hd = 0, mc = 0;
     if (gl < S) {
         ck = A.clock[(size_t)h * S + gl];
@@ -430,11 +437,12 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
     const bool bad_c = gl < nnc && (ca >= NA || cq == 0 || cq >= (1u << 24) || cdo != xd || coo != xo);
     const int64_t oval = (int64_t)(((uint64_t)o_vhi << 32) | o_vlo);
     // an op on one of the document's list / text objects (their order is resident: HM_IST_LIST);
-    // li = its list in the directory.  A group of 8 / 16 lanes has no directory: an op on an
-    // object that is not a map of the log marks the document for the one-document-per-wave pass
+    // li = its list in the directory.  (Without HM_INC_LIST_GROUPS a group of 8 / 16 lanes has no
+    // directory: an op on an object that is not a map of the log marks the document for the
+    // one-document-per-wave pass)
     const uint32_t nl = (I.flags & HM_IST_LIST) ? (I.pad[1] < LMAX ? I.pad[1] : LMAX) : 0u;
     uint32_t li = HM_NONE;
-    if constexpr (G == 64) {
+    if constexpr (LST) {
         for (uint32_t k = 0; k < nl; k++) li = g.sh(dir.x, k) == o_obj ? k : li;
     } else {
         li = nl && o_obj != 0 && (o_obj >= 64 || !((I.mapmask >> o_obj) & 1ull)) ? 0u : HM_NONE;
@@ -466,7 +474,7 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
                                     (!mk && !lst && o_obj != 0 && (o_obj >= 64 || !((known >> o_obj) & 1ull))));
     if (g.bits(bad_c || bad_o) || total_o != nno || total_d != nnd) return INC_BAIL;
     const bool any_list = g.bits(lst) != 0;
-    if (G < 64 && any_list) return INC_DEFER;                 // list / text ops: one document per wave
+    if (!LST && any_list) return INC_DEFER;                   // list / text ops: one document per wave
     // integer counters: |base| + sum|inc| of every counter stays <= 2^53 (the re-merge's exact rule)
     unsigned long long cadd = (gl < nno && o_vt == HM_V_INT &&
                                (o_act == HM_INC || (o_act == HM_SET && o_dt == HM_DT_COUNTER))) ? abs64(oval) : 0ull;
@@ -597,7 +605,7 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
 
     // ---- list / text ops (applyInsert, A.3): the new elements' places in the resident order ----
     ListPlan lp;
-    if constexpr (G == 64) {
+    if constexpr (LST) {
         if (any_list) {
             // an inserted element's register was never touched: a fresh id, or one the document's
             // declared register count reserved (untouched registers have no object)
@@ -652,7 +660,7 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
     }
     if (mv) __threadfence_block();                            // the copies land before the writes below
     __builtin_amdgcn_wave_barrier();
-    if constexpr (G == 64) {
+    if constexpr (LST) {
         if (any_list) list_insert(g, D, A, I, o_act, o_reg, o_par, lscr, lp);
     }
 
@@ -758,7 +766,7 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
         }
     }
 
-    if constexpr (G == 64) {
+    if constexpr (LST) {
         if (any_list) {
             __threadfence_block();                            // the register rows above, then the visible indices
             __builtin_amdgcn_wave_barrier();
@@ -790,10 +798,10 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
         if (bi != HM_NONE) gather_result(A, bi, r);
         IncState s = I;
         s.s_used = I.s_used + acc; s.cabs = cabs; s.mapmask = I.mapmask | made_all;
-        if (G == 64 && any_list) s.pad[0] = lp.n_el;
+        if (LST && any_list) s.pad[0] = lp.n_el;
         A.ist[h] = s;
     }
-    if constexpr (G == 64) {
+    if constexpr (LST) {
         if (any_list && gl < lp.nl) A.ldir[(size_t)h * LMAX + gl] = make_uint2(dir.x, lp.cnew);   // the lists' new lengths
     }
     return INC_DONE;
@@ -804,7 +812,7 @@ __device__ int inc_doc(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 
 // round of its own on the state the previous tile left (the rows before it are old rows to it).
 // A tile after the first that cannot go incremental sends the document to the re-merge, which
 // rewrites every row the earlier tiles wrote.
-template <int G>
+template <int G, bool LS = false>
 __device__ int inc_doc_tiled(const AppendDesc &D, const IncArgs &A, uint4 *ssv, uint2 *smt, uint32_t *lscr, uint32_t bi) {
     const Grp<G> g;
     const uint32_t gl = g.gl;
@@ -838,7 +846,7 @@ __device__ int inc_doc_tiled(const AppendDesc &D, const IncArgs &A, uint4 *ssv, 
                 T.n_old_r = D.n_r;                            // (the first tile wrote every new register's row)
             }
         }
-        const int rc = inc_doc<G>(T, A, ssv, smt, lscr, tiled, bi);
+        const int rc = inc_doc<G, LS>(T, A, ssv, smt, lscr, tiled, bi);
         if (rc != INC_DONE) return first ? rc : INC_BAIL;
         c0 += k; d0 += td; o0 += to;
         if (c0 >= D.n_new_c) return INC_DONE;
@@ -855,14 +863,19 @@ __device__ int inc_doc_tiled(const AppendDesc &D, const IncArgs &A, uint4 *ssv, 
 #ifndef HM_INC_WAVES
 #define HM_INC_WAVES 1       // dev A/B: waves per SIMD the G = 8 / 16 instantiations are compiled for
 #endif
-template <int G, bool TL>
+// LS (G = 8 / 16, HM_INC_LIST_GROUPS): the instantiation for documents with lists (HM_DINC_LISTS);
+// the other takes the map documents at the register budget the list code would cost them (116 vs
+// 141 VGPRs: 4 waves per SIMD instead of 3)
+template <int G, bool TL, bool LS = false>
 __global__ __launch_bounds__(256, (G < 64 ? HM_INC_WAVES : 1)) void inc_group_kernel(IncArgs A_in) {
     constexpr uint32_t NG = 256 / G;
     __shared__ uint4 s_sv[NG][2 * G];
     __shared__ uint2 s_mt[NG][2 * G];
-    __shared__ uint32_t s_ls[G == 64 ? NG : 1][G == 64 ? LSCR : 1];   // the list phase's anchors
+    constexpr bool LST = G == 64 || (HM_INC_LIST_GROUPS && LS);
+    __shared__ uint32_t s_ls[LST ? NG : 1][LST ? lscr_words<G>() : 1];   // the list phase's anchors
     const uint32_t grp = threadIdx.x / G, gl = threadIdx.x & (G - 1);
     if (!A_in.list && A_in.pst && A_in.pst->n_inc == 0) return;     // (a submit with nothing incremental)
+    if (LS && A_in.pst && A_in.pst->mx[4] == 0) return;              // (no list document routed to the groups)
     const uint32_t n = A_in.list ? A_in.list[0] : A_in.n;
     // the loop reads the launch parameters through an opaque pointer to the kernarg segment: a
     // document re-loads the fields it uses (scalar loads) rather than holding them in SGPRs
@@ -878,9 +891,10 @@ __global__ __launch_bounds__(256, (G < 64 ? HM_INC_WAVES : 1)) void inc_group_ke
         if (!route || route == 3 || (G < 64 && route == 2)) continue;   // (2: listed for the wave pass, 3: the lane pass)
         const bool tl = D.n_new_c > NC || D.n_new_o > (uint32_t)G || D.n_new_d > (uint32_t)G;
         if (G == 64 && tl != TL) continue;                             // (the other launch's document)
+        if (G < 64 && ((D.inc & HM_DINC_LISTS) != 0) != LS) continue;   // (the other instantiation's document)
         int rc;
-        if constexpr (TL) rc = inc_doc_tiled<G>(D, A, s_sv[grp], s_mt[grp], s_ls[G == 64 ? grp : 0], di);
-        else rc = inc_doc<G>(D, A, s_sv[grp], s_mt[grp], s_ls[G == 64 ? grp : 0], false, di);
+        if constexpr (TL) rc = inc_doc_tiled<G, LS>(D, A, s_sv[grp], s_mt[grp], s_ls[LST ? grp : 0], di);
+        else rc = inc_doc<G, LS>(D, A, s_sv[grp], s_mt[grp], s_ls[LST ? grp : 0], false, di);
         if (rc == INC_DONE && gl == 0 && A.gdone) A.gdone[di] = 1;
         if (rc != INC_DONE && gl == 0) {
             if (rc == INC_DEFER && A.defer) A.defer[1 + atomicAdd(&A.defer[0], 1u)] = di;
@@ -1473,6 +1487,11 @@ hipError_t hm_launch_inc_apply(const IncArgs &A, hipStream_t s) {
     }
     if (S <= 8) hipLaunchKernelGGL((hmi::inc_group_kernel<8, false>), dim3(grid(A.n, 32)), dim3(256), 0, s, A);
     else if (S <= 16) hipLaunchKernelGGL((hmi::inc_group_kernel<16, false>), dim3(grid(A.n, 16)), dim3(256), 0, s, A);
+    if (HM_INC_LIST_GROUPS) {
+        // the documents with lists (the launch returns at once when the plan routed none here)
+        if (S <= 8) hipLaunchKernelGGL((hmi::inc_group_kernel<8, false, true>), dim3(grid(A.n, 32)), dim3(256), 0, s, A);
+        else if (S <= 16) hipLaunchKernelGGL((hmi::inc_group_kernel<16, false, true>), dim3(grid(A.n, 16)), dim3(256), 0, s, A);
+    }
     if (S <= 16 && A.defer) {
         // the documents handed over, one per wave (their count is read on the device); rounds that
         // need tiles in a launch of their own

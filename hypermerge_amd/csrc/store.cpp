@@ -299,7 +299,7 @@ int launch_list_merge(hm_store *s, const uint32_t *dev_list, uint32_t n) {
     int rc;
     if ((rc = ensure_buf(s, s->rows, n)) || (rc = ensure_buf(s, s->klist, n))) return rc;
     if ((rc = reset_stats(s))) return rc;
-    const uint32_t small_lists = s->inc_mode == 1 ? HM_INC_SMALL_LIST_OPS : 0u;
+    const uint32_t small_lists = hm_small_list_ops(s->S, s->inc_mode);
     SCHK(s, hm_launch_doc_rows(dev_list, n, s->dm, s->rows.p, s->st, small_lists, s->incremental ? s->ist : nullptr,
                                s->klist.p, st));
     rc = HM_OK;
@@ -338,7 +338,7 @@ int launch_list_merge(hm_store *s, const uint32_t *dev_list, uint32_t n) {
         M.list = s->klist.p; M.n = P.mx[2]; M.dm = s->dm; M.res_docs = s->res_docs; M.changes = s->changes; M.hist = s->hist;
         M.ckey = s->ckey; M.ops = s->ops; M.surv = s->surv; M.smeta = s->smeta; M.ist = s->ist;
         M.epos = s->epos; M.epar = s->epar; M.ekey = s->ekey; M.lorder = s->lorder; M.ldir = s->ldir;
-        M.small_lists = s->inc_mode == 1 ? HM_INC_SMALL_LIST_OPS : 0u;
+        M.small_lists = small_lists;
         SCHK(s, hm_launch_inc_meta(M, st));
     }
     SCHK(s, hipStreamSynchronize(st));

@@ -46,7 +46,8 @@ struct PlanStats {
     uint32_t n_inc, n_cold, n_back, n_app;       // (n_app: batch rows append_kernel has work for)
     uint32_t mx[6];                            // mx[0]: documents routed to the lane pass; mx[1] = 1: alloc_kernel
                                                //   found no room for the growth and moved nothing; mx[2] / mx[3]:
-                                               //   doc_rows_kernel's may-keep-state counts (all / with lists)
+                                               //   doc_rows_kernel's may-keep-state counts (all / with lists);
+                                               //   mx[4]: list documents the plan routed to the group passes
     uint32_t max_c, max_o, max_r, max_objs, max_d, flags;   // launch hints of a merge list
     unsigned long long need[4];                // rows the submit's growing segments take, per space
     unsigned long long tot_c, tot_d, tot_o, tot_r;
@@ -97,6 +98,24 @@ static_assert(sizeof(IncState) == 32, "IncState is 32 B");
 // the cost policy of incremental mode 1: a list document of at most this many ops re-merges (one
 // small-kernel wave, all in LDS) rather than taking the one-document-per-wave incremental pass
 #define HM_INC_SMALL_LIST_OPS 256u
+// dev A/B (round 6, off): the G = 8 / 16 group passes take list / text ops too (list_plan /
+// list_insert / list_indices in groups of G lanes, a separate instantiation at 143 VGPRs), list
+// documents of strides <= 16 route there and mode 1 stops re-merging small list documents.
+// Measured (profiles/r06/ab_list_groups): C5 resident 51 % incremental but 0.84x the re-merge (the
+// list instantiation's ~5 ns per document, 10 % handed back, the re-merge of the rest as costly as
+// re-merging all), C3 resident 1.56x instead of 2.2x (long lists shifted and re-indexed G
+// elements at a time)
+#ifndef HM_INC_LIST_GROUPS
+#define HM_INC_LIST_GROUPS 0
+#endif
+// the small-list bound a store of stride S applies in incremental mode `mode`: with the group
+// passes taking lists (strides <= 16) a list document's round is as cheap as a map document's, so
+// none re-merges for being small; the one-document-per-wave pass (wider strides) costs as much as
+// the small kernel's re-merge of such a document, which keeps mode 1's bound
+__host__ __device__ inline uint32_t hm_small_list_ops(uint32_t S, uint32_t mode) {
+    if (mode != 1u) return 0u;
+    return (HM_INC_LIST_GROUPS && S <= 16u) ? 0u : HM_INC_SMALL_LIST_OPS;
+}
 // ... and a round of more than 1 / HM_INC_COST of the log's rows (changes + ops, the new ones
 // included) re-merges: the per-row cost ratio of the incremental passes to the merge kernels,
 // measured on C4 (profiles/r05/inc: inc_lane_kernel 25.5 ms for a 60-change first load of 1M

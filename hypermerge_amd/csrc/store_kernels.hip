@@ -263,11 +263,13 @@ __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
     __shared__ unsigned long long s_need[4][PLAN_WG / 64];
     __shared__ uint32_t s_inc[PLAN_WG / 64];
     __shared__ uint32_t s_lane[PLAN_WG / 64];
+    __shared__ uint32_t s_glst[PLAN_WG / 64];
     const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
     if (ln == 0) {
         for (int k = 0; k < 4; k++) s_need[k][wv] = 0;
         s_inc[wv] = 0;
         s_lane[wv] = 0;
+        s_glst[wv] = 0;
     }
     const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
     const bool live = i0 < a.n;
@@ -350,7 +352,8 @@ __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
                (small || longr) && m.n_r <= r.n_regs && r.n_actors <= a.S;
     // mode 1: a small list document keeps no incremental state (inc_meta_kernel), so it re-merges
     // before any of the reads below
-    if (inc && lists && a.incremental == 1u && m.n_o + r.n_ops <= HM_INC_SMALL_LIST_OPS) inc = false;
+    const uint32_t small_lists = hm_small_list_ops(a.S, a.incremental);
+    if (inc && lists && m.n_o + r.n_ops <= small_lists) inc = false;
     bool wave = false;                                             // list ops: the one-document-per-wave pass
     if (inc && a.ist) {
         // what inc_group_kernel would hand straight back (its state checks, and for documents with
@@ -397,18 +400,24 @@ __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
     // kernels take a log row ~HM_INC_COST times faster than the incremental passes take a new
     // one (C4: 37 ps per change merged vs 0.43-0.53 ns per change applied), so that round is
     // cheaper re-merged (this also sends a first load into a document re-merged empty to the merge)
-    if (inc && wave && a.incremental == 1u && m.n_o + r.n_ops <= HM_INC_SMALL_LIST_OPS) inc = false;
+    if (inc && wave && m.n_o + r.n_ops <= small_lists) inc = false;
+    // list documents of strides <= 16 whose round fits a group take the group passes' list
+    // instantiation (a longer round goes straight to the wave pass)
+    const uint32_t GS = a.S <= 8 ? 8u : 16u;
+    if (HM_INC_LIST_GROUPS && a.S <= 16 && r.n_ops <= GS && r.n_deps <= GS && r.n_changes <= HM_INC_MAX_NEW_C)
+        wave = false;
+    const bool glist = inc && !wave && lists;
     if (inc && a.incremental == 1u &&
         (unsigned long long)HM_INC_COST * (r.n_changes + r.n_ops) > (unsigned long long)m.n_c + m.n_o + r.n_changes + r.n_ops)
         inc = false;
     p.inc = inc ? (wave ? 2u : (lane ? 3u : 1u)) : 0u;
     p.remapped = remapped ? 1u : 0u;
     if (live) a.plan[i] = p;
-    const unsigned long long im = __ballot(inc), lm = __ballot(inc && p.inc == 3u);
-    if (ln == 0) { s_inc[wv] = (uint32_t)__popcll(im); s_lane[wv] = (uint32_t)__popcll(lm); }
+    const unsigned long long im = __ballot(inc), lm = __ballot(inc && p.inc == 3u), gm = __ballot(glist && p.inc == 1u);
+    if (ln == 0) { s_inc[wv] = (uint32_t)__popcll(im); s_lane[wv] = (uint32_t)__popcll(lm); s_glst[wv] = (uint32_t)__popcll(gm); }
     }
     __syncthreads();
-    if (threadIdx.x < 6) {                                         // one lane per reduced value
+    if (threadIdx.x < 7) {                                         // one lane per reduced value
         const uint32_t k = threadIdx.x, nw = PLAN_WG / 64;
         if (k < 4) {
             unsigned long long g = 0;
@@ -416,8 +425,8 @@ __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
             if (g) atomicAdd(&a.st->need[k], g);
         } else {
             uint32_t c = 0;
-            for (uint32_t w = 0; w < nw; w++) c += k == 4 ? s_inc[w] : s_lane[w];
-            if (c) atomicAdd(k == 4 ? &a.st->n_inc : &a.st->mx[0], c);
+            for (uint32_t w = 0; w < nw; w++) c += k == 4 ? s_inc[w] : (k == 5 ? s_lane[w] : s_glst[w]);
+            if (c) atomicAdd(k == 4 ? &a.st->n_inc : (k == 5 ? &a.st->mx[0] : &a.st->mx[4]), c);
         }
     }
 }
