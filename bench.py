@@ -615,9 +615,20 @@ def _node_run(node, docs, legs, chunk=16, timeout=900, first=None):
         fn = os.path.join(td, "docs.json")
         with open(fn, "w") as f:
             json.dump({"docs": [[d[:f0]] + [d[k:k + chunk] for k in range(f0, len(d), chunk)] for d in docs]}, f)
-        p = subprocess.run([node, "--max-old-space-size=16384", "--max-semi-space-size=64",
-                            os.path.join(here, "tools", "bench_node.js"), fn, ",".join(legs)],
-                           capture_output=True, text=True, timeout=timeout)
+        import threading
+        t0, done = time.perf_counter(), threading.Event()
+
+        def beat():                      # (a heartbeat in the progress file while Node runs)
+            while not done.wait(30):
+                _progress(f"node legs {','.join(legs[:2])}...: {time.perf_counter() - t0:.0f} s")
+        hb = threading.Thread(target=beat, daemon=True)
+        hb.start()
+        try:
+            p = subprocess.run([node, "--max-old-space-size=16384", "--max-semi-space-size=64",
+                                os.path.join(here, "tools", "bench_node.js"), fn, ",".join(legs)],
+                               capture_output=True, text=True, timeout=timeout)
+        finally:
+            done.set()
     if p.returncode != 0:
         return {"error": p.stderr[-800:]}
     out = json.loads(p.stdout.strip().splitlines()[-1])

@@ -891,7 +891,7 @@ __global__ __launch_bounds__(256, (G < 64 ? HM_INC_WAVES : 1)) void inc_group_ke
         if (!route || route == 3 || (G < 64 && route == 2)) continue;   // (2: listed for the wave pass, 3: the lane pass)
         const bool tl = D.n_new_c > NC || D.n_new_o > (uint32_t)G || D.n_new_d > (uint32_t)G;
         if (G == 64 && tl != TL) continue;                             // (the other launch's document)
-        if (G < 64 && ((D.inc & HM_DINC_LISTS) != 0) != LS) continue;   // (the other instantiation's document)
+        if (HM_INC_LIST_GROUPS && G < 64 && ((D.inc & HM_DINC_LISTS) != 0) != LS) continue;   // (the other instantiation's)
         int rc;
         if constexpr (TL) rc = inc_doc_tiled<G, LS>(D, A, s_sv[grp], s_mt[grp], s_ls[LST ? grp : 0], di);
         else rc = inc_doc<G, LS>(D, A, s_sv[grp], s_mt[grp], s_ls[LST ? grp : 0], false, di);
