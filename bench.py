@@ -604,17 +604,46 @@ def _from_blocks(eng, batch, cfg, args):
             "path": "JSON blocks -> hm_decode_blocks (native, multi-threaded) -> hm_merge_host (PCIe included)"}
 
 
+def _node_docs(name, n, th):
+    """`n` synthetic `name` documents as Change JSON texts, per document: for map documents the
+    texts the native block renderer writes (synth.blocks: Block.pack's raw-JSON form, realistic
+    base58 actor ids) — the documents decode_doc restates, without a Python object per op (1.28M
+    C2 changes: ~9 s instead of ~60 s of decode_doc + json.dump)."""
+    from hypermerge_amd import synth
+    cfg = synth.config(name, n_docs=n)
+    b = synth.generate(cfg, threads=th)
+    if name not in ("C2", "C4"):
+        # (the renderer writes list / text ops in a simplified form the JS restatement cannot
+        # apply: documents with lists go through decode_doc)
+        from hypermerge_amd.columnar import decode_doc
+        return b, [[json.dumps(c).encode() for c in decode_doc(b, i)] for i in range(b.n_docs)]
+    data, bo, db = synth.blocks(cfg, b)
+    raw = data.tobytes()
+    bo = bo.tolist()
+    docs = []
+    for d in range(len(db) - 1):
+        blk = [raw[bo[i]:bo[i + 1]] for i in range(int(db[d]), int(db[d + 1]))]
+        if any(x[:2] != b'{"' for x in blk):
+            raise RuntimeError("node legs: a compressed block (the renderer's raw JSON form expected)")
+        docs.append(blk)
+    return b, docs
+
+
 def _node_run(node, docs, legs, chunk=16, timeout=900, first=None):
-    """tools/bench_node.js over `docs` (each document's changes, fed in chunks of `chunk`; with
-    `first`, the first chunk — DocBackend.init — holds that many changes)."""
+    """tools/bench_node.js over `docs` (each document's changes as JSON texts, fed in chunks of
+    `chunk`; with `first`, the first chunk — DocBackend.init — holds that many changes)."""
     import subprocess
     import tempfile
     here = os.path.dirname(os.path.abspath(__file__))
     f0 = chunk if first is None else first
+
+    def arr(xs):
+        return b"[" + b",".join(xs) + b"]"
     with tempfile.TemporaryDirectory() as td:
         fn = os.path.join(td, "docs.json")
-        with open(fn, "w") as f:
-            json.dump({"docs": [[d[:f0]] + [d[k:k + chunk] for k in range(f0, len(d), chunk)] for d in docs]}, f)
+        with open(fn, "wb") as f:
+            f.write(b'{"docs":' + arr([arr([arr(d[:f0])] + [arr(d[k:k + chunk]) for k in range(f0, len(d), chunk)])
+                                       for d in docs]) + b"}")
         import threading
         t0, done = time.perf_counter(), threading.Event()
 
@@ -652,11 +681,8 @@ def _node_e2e(args):
     node = shutil.which("node")
     if node is None:
         return {"skipped": "node not installed"}
-    from hypermerge_amd import synth
-    from hypermerge_amd.columnar import decode_doc
     th = min(16, os.cpu_count() or 1)
-    b = synth.generate(synth.config("C2", n_docs=args.node_docs), threads=th)
-    docs = [decode_doc(b, i) for i in range(b.n_docs)]
+    b, docs = _node_docs("C2", args.node_docs, th)
     legs = ["cpu", "cpu_blocks", "gpu", "gpu_async", "gpu_objects", "gpu_async_net"]
     # cpu and gpu_async run twice more, interleaved with the others: the ratio is taken between
     # their median runs (single runs of either leg vary by +-20% on a shared host)
@@ -682,8 +708,9 @@ def _node_e2e(args):
                                  "nested maps / lists x 4 actors x 8 changes, 20% delivered before their deps, 3% duplicates")):
         if n <= 0:
             continue
-        bx = synth.generate(synth.config(name, n_docs=n, **over), threads=th)
-        r = _node_run(node, [decode_doc(bx, i) for i in range(bx.n_docs)], ["cpu", "gpu_async"])
+        bx, dx = _node_docs(name, n, th)
+        r = _node_run(node, dx, ["cpu", "gpu_async"])
+        del dx
         if "error" not in r:
             r["gpu_async_vs_js"] = r["gpu_async"]["changes_per_s"] / r["cpu"]["changes_per_s"]
             r["sample"] = f"{name}: {bx.n_docs} {desc}; rounds of 16 changes per document"
@@ -692,8 +719,9 @@ def _node_e2e(args):
     # applyRemoteChanges rounds of 2 changes — the granularity hypercore blocks arrive at
     # (Actor.onDownload / syncChanges per block) — which the store routes to the incremental kernels
     if args.node_arrival_docs > 0:
-        ba = synth.generate(synth.config("C2", n_docs=args.node_arrival_docs), threads=th)
-        r = _node_run(node, [decode_doc(ba, i) for i in range(ba.n_docs)], ["cpu", "gpu_async"], chunk=2, first=48)
+        ba, da = _node_docs("C2", args.node_arrival_docs, th)
+        r = _node_run(node, da, ["cpu", "gpu_async"], chunk=2, first=48)
+        del da
         if "error" not in r:
             r["gpu_async_vs_js"] = r["gpu_async"]["changes_per_s"] / r["cpu"]["changes_per_s"]
             r["sample"] = (f"C2 arrivals: {ba.n_docs} docs x 4 actors x 64 changes, init with 48, then 8 "
