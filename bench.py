@@ -262,10 +262,10 @@ def main() -> int:
                     help="skip the resident-store leg (1-2 new changes per resident document per round)")
     ap.add_argument("--no-node", action="store_true",
                     help="skip the Node DocBackend leg (C2 sample: JS restatement vs the GPU drop-in)")
-    ap.add_argument("--node-docs", type=int, default=20000)
-    ap.add_argument("--node-text-docs", type=int, default=1000, help="C3 documents of the Node leg (0: skip)")
+    ap.add_argument("--node-docs", type=int, default=10000)
+    ap.add_argument("--node-text-docs", type=int, default=500, help="C3 documents of the Node leg (0: skip)")
     ap.add_argument("--node-c5-docs", type=int, default=5000, help="C5 documents of the Node leg (0: skip)")
-    ap.add_argument("--node-arrival-docs", type=int, default=10000,
+    ap.add_argument("--node-arrival-docs", type=int, default=5000,
                     help="C2 documents of the Node live-arrival leg (init 48 changes, then rounds of 2; 0: skip)")
     ap.add_argument("--text-docs", type=int, default=10000, help="C3 documents in the resident text leg")
     ap.add_argument("--c5-docs", type=int, default=100000, help="C5 documents in the resident nested-document leg (0: skip)")
@@ -698,7 +698,8 @@ def _node_e2e(args):
         out[m] = dict(runs[1], runs_changes_per_s=[r["changes_per_s"] for r in runs])   # the median run
     out["same_diff_count"] = len({out[k]["diffs"] for k in legs if k != "gpu_async_net"}) == 1
     out["sample"] = (f"C2: {b.n_docs} docs x 4 actors x 64 changes, 4 rounds of 16 changes per document "
-                     f"(init + 3 applyRemoteChanges), one Node thread; blocks = JSON Change texts")
+                     f"(init + 3 applyRemoteChanges), one Node thread; blocks = JSON Change texts with base58 actor ids "
+                     f"(SURVEY 8(d); rounds <= 5 used 8-character ids: both sides ran ~2x faster)")
     out["gpu_async_vs_js"] = out["gpu_async"]["changes_per_s"] / out["cpu"]["changes_per_s"]
     out["gpu_async_vs_js_blocks"] = out["gpu_async"]["changes_per_s"] / out["cpu_blocks"]["changes_per_s"]
     out["gpu_vs_js"] = out["gpu"]["changes_per_s"] / out["cpu"]["changes_per_s"]

@@ -1325,6 +1325,11 @@ __device__ __forceinline__ uint32_t change_of_op(const hm_change_row *ch, uint32
 // re-merges.
 __global__ __launch_bounds__(256) void inc_meta_kernel(MetaArgs a) {
     const uint32_t lane = threadIdx.x & 63;
+    // the change in PlanStats.n_valid, summed per wave, then per workgroup into part[], then by
+    // valid_sum_kernel: device-scope atomics on one word from every document (or workgroup)
+    // serialize across the XCDs (~10 ns each: 0.3-1.8 ms for 65k-1M of them)
+    __shared__ int s_dv[4];
+    int dv = 0;
     // one wave per listed document: the re-merged documents of a submit are few and large (their
     // state is rebuilt from whole logs) or many and small (a few loads each, then skipped), and a
     // wave per document keeps the large ones in parallel (a round-6 variant that let one lane per
@@ -1334,11 +1339,16 @@ __global__ __launch_bounds__(256) void inc_meta_kernel(MetaArgs a) {
         const uint32_t h = a.list[q];
         const DevDoc m = a.dm[h];
         const hm_doc_result r = a.res_docs[h];
+        const bool was = HM_IST_COUNTS(a.ist[h].flags);      // (PlanStats.n_valid follows the change)
         // (mode 1: a small document with lists re-merges every round — one small-kernel wave either
         // way — so it keeps no incremental state at all)
         if (r.status != HM_OK || r.n_queued != 0 || r.n_surv > m.o_cap ||
             ((m.flags & HM_DOC_HAS_LISTS) && m.n_o <= a.small_lists)) {
-            if (lane == 0) { IncState z = {}; a.ist[h] = z; }
+            if (lane == 0) {
+                IncState z = {};
+                a.ist[h] = z;
+            }
+            dv -= was ? 1 : 0;
             continue;
         }
         const hm_change_row *ch = a.changes + m.c_off;
@@ -1458,6 +1468,25 @@ __global__ __launch_bounds__(256) void inc_meta_kernel(MetaArgs a) {
             st.pad[0] = (flags & HM_IST_LIST) ? n_el : 0u; st.pad[1] = (flags & HM_IST_LIST) ? nlst : 0u;
             a.ist[h] = st;
         }
+        dv += (HM_IST_COUNTS(flags) ? 1 : 0) - (was ? 1 : 0);
+    }
+    if (lane == 0) s_dv[threadIdx.x >> 6] = dv;
+    __syncthreads();
+    if (threadIdx.x == 0 && a.part) a.part[blockIdx.x] = s_dv[0] + s_dv[1] + s_dv[2] + s_dv[3];
+}
+
+// n_valid += the sum of inc_meta_kernel's per-workgroup changes (one workgroup, one atomic)
+__global__ __launch_bounds__(1024) void valid_sum_kernel(const int *part, uint32_t n, uint32_t *n_valid) {
+    __shared__ int s[16];
+    int t = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += 1024) t += part[i];
+    for (int d = 32; d >= 1; d >>= 1) t += __shfl_xor(t, d);
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int u = 0;
+        for (int w = 0; w < 16; w++) u += s[w];
+        if (u) atomicAdd(n_valid, (uint32_t)u);
     }
 }
 
@@ -1512,8 +1541,9 @@ hipError_t hm_launch_inc_apply(const IncArgs &A, hipStream_t s) {
 
 hipError_t hm_launch_inc_meta(const MetaArgs &a, hipStream_t s) {
     if (!a.n) return hipSuccess;
-    const uint32_t grid = (a.n + 3) / 4 < 65535u ? (a.n + 3) / 4 : 65535u;
+    const uint32_t grid = (a.n + 3) / 4 < HM_META_GRID ? (a.n + 3) / 4 : HM_META_GRID;
     hipLaunchKernelGGL(hmi::inc_meta_kernel, dim3(grid), dim3(256), 0, s, a);
+    if (a.part && a.n_valid) hipLaunchKernelGGL(hmi::valid_sum_kernel, dim3(1), dim3(1024), 0, s, a.part, grid, a.n_valid);
     return hipGetLastError();
 }
 

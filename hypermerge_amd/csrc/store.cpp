@@ -87,6 +87,7 @@ struct hm_store {
     DBuf<uint32_t> list;                          // re-merge list (cold, then handed back)
     DBuf<uint32_t> blist;                         // rollback list
     DBuf<uint32_t> klist;                         // a re-merge's documents that may keep incremental state
+    DBuf<int> mpart;                              // inc_meta_kernel's per-workgroup n_valid changes
     DBuf<uint32_t> alist;                         // append list (batch rows with append work)
     DBuf<uint8_t> remap, inv;
     DBuf<hm_doc_row> rows;
@@ -108,9 +109,9 @@ struct hm_store {
     DBuf<uint32_t> undo_handles;
     // incremental applyRemoteChanges (inc_apply_kernel) and the last submit's routing
     bool incremental = true;
-    // some document may hold incremental state (an IncState with HM_IST_VALID): set when a re-merge
-    // lists a document that may keep one, or the path is switched on over old state; until then no
-    // document can route to the incremental kernels and a submit does not launch them
+    // some document holds incremental state a submit can use (PlanStats.n_valid > 0, read back after
+    // every re-merge): without one no document can route to the incremental kernels and a submit
+    // does not launch them
     bool any_state = false;
     uint32_t inc_mode = 1;                        // 1: small list documents re-merge (cost policy); 2: every one
     uint32_t st_inc = 0, st_cold = 0, st_bail = 0;
@@ -300,7 +301,8 @@ int launch_list_merge(hm_store *s, const uint32_t *dev_list, uint32_t n) {
     if ((rc = ensure_buf(s, s->rows, n)) || (rc = ensure_buf(s, s->klist, n))) return rc;
     if ((rc = reset_stats(s))) return rc;
     const uint32_t small_lists = hm_small_list_ops(s->S, s->inc_mode);
-    SCHK(s, hm_launch_doc_rows(dev_list, n, s->dm, s->rows.p, s->st, small_lists, s->incremental ? s->ist : nullptr,
+    // (the states of the documents that keep none are cleared — unless no document holds one)
+    SCHK(s, hm_launch_doc_rows(dev_list, n, s->dm, s->rows.p, s->st, small_lists, s->incremental && s->any_state ? s->ist : nullptr,
                                s->klist.p, st));
     rc = HM_OK;
     const PlanStats P = read_stats(s, &rc);
@@ -329,19 +331,25 @@ int launch_list_merge(hm_store *s, const uint32_t *dev_list, uint32_t n) {
     if (positions) SCHK(s, hm_launch_epos_clear(s->klist.p, P.mx[2], s->dm, s->epos, st));     // (the keep list)
     rc = hm_engine_launch_merge(s->e, &b, &o, dev_list, &ext, positions ? s->epos : nullptr);
     // the incremental path's survivor metadata of the re-merged documents that may keep state (the
-    // keep list doc_rows_kernel built; it cleared the others' IncState).  A store none of whose
-    // documents ever kept state (any_state: e.g. mode 1 with only small list documents) launches
-    // no incremental kernel in its submits
-    if (P.mx[2]) s->any_state = true;
+    // keep list doc_rows_kernel built; it cleared the others' IncState)
     if (rc == HM_OK && s->incremental && P.mx[2]) {
         MetaArgs M;
         M.list = s->klist.p; M.n = P.mx[2]; M.dm = s->dm; M.res_docs = s->res_docs; M.changes = s->changes; M.hist = s->hist;
         M.ckey = s->ckey; M.ops = s->ops; M.surv = s->surv; M.smeta = s->smeta; M.ist = s->ist;
         M.epos = s->epos; M.epar = s->epar; M.ekey = s->ekey; M.lorder = s->lorder; M.ldir = s->ldir;
         M.small_lists = small_lists;
+        M.n_valid = &s->st->n_valid;
+        if ((rc = ensure_buf(s, s->mpart, HM_META_GRID))) return rc;
+        M.part = s->mpart.p;
         SCHK(s, hm_launch_inc_meta(M, st));
     }
+    // documents whose state can route them to the incremental kernels, after this re-merge (the
+    // only step that adds or drops states): none (e.g. mode 1 with only small list documents, or
+    // every document with queued changes) = the next submits launch no incremental kernel
+    const bool count = s->incremental && (s->any_state || P.mx[2]);
+    if (count) SCHK(s, hipMemcpyAsync(&s->h_cnt[4], &s->st->n_valid, 4, hipMemcpyDeviceToHost, st));
     SCHK(s, hipStreamSynchronize(st));
+    if (count) s->any_state = s->h_cnt[4] != 0;
     return rc;
 }
 
@@ -449,7 +457,7 @@ void hm_store_destroy(hm_store *s) {
     void *bufs[] = {s->changes, s->hist, s->ckey, s->all_deps, s->deps, s->ops, s->surv, s->smeta, s->ist, s->ldir, s->regs, s->epos,
                     s->epar, s->ekey, s->lorder, s->res_docs, s->clock,
                     s->back_clock, s->heads, s->min_clock, s->stored, s->stage.p, s->dm, s->seen, s->plan.p, s->descs.p,
-                    s->bdescs.p, s->list.p, s->blist.p, s->alist.p, s->remap.p, s->inv.p, s->rows.p, s->undo_handles.p, s->klist.p, s->st};
+                    s->bdescs.p, s->list.p, s->blist.p, s->alist.p, s->remap.p, s->inv.p, s->rows.p, s->undo_handles.p, s->klist.p, s->mpart.p, s->st};
     for (void *b : bufs) if (b) (void)hipFree(b);
     for (hipEvent_t e : s->ev) if (e) (void)hipEventDestroy(e);
     if (s->h_st) (void)hipHostFree(s->h_st);
@@ -500,7 +508,7 @@ int hm_doc_reset(hm_store *s, const uint32_t *doc_handles, uint32_t n) {
         hipStream_t st = hm_engine_stream(s->e);
         SCHK(s, hipMemcpyAsync(s->blist.p, hs.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
         SCHK(s, hm_launch_reset_docs(s->blist.p, n, s->dm, s->res_docs, s->ist, s->clock, s->back_clock, s->heads, s->min_clock,
-                                     s->stored, s->S, st));
+                                     s->stored, s->S, &s->st->n_valid, st));
         SCHK(s, hipStreamSynchronize(st));
         s->undo_id = 0;                               // the last batch's undo no longer applies
         return HM_OK;
@@ -554,7 +562,9 @@ static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handl
         A.docs = t_docs; A.changes = t_ch;
         A.handles = t_hand; A.remap = nremap ? t_remap : nullptr;
         A.n = n; A.n_changes = b->n_changes; A.n_deps = b->n_deps; A.n_ops = b->n_ops; A.n_handles = s->n_handles;
-        A.S = S; A.stamp = ++s->stamp ? s->stamp : ++s->stamp; A.incremental = s->incremental && S <= 64 ? s->inc_mode : 0u;
+        A.S = S; A.stamp = ++s->stamp ? s->stamp : ++s->stamp; A.incremental = s->incremental && S <= 64 && s->any_state ? s->inc_mode : 0u;
+        // (no document holds a usable state: the plan routes every document to the re-merge and no
+        // incremental kernel is launched)
         A.dm = s->dm; A.res_docs = s->res_docs; A.seen = s->seen; A.plan = s->plan.p; A.descs = s->descs.p;
         A.list = s->list.p; A.st = s->st;
         A.ist = A.incremental ? s->ist : nullptr; A.ops = t_op; A.deps = t_dp; A.clock = s->clock;
@@ -598,7 +608,7 @@ static int submit_impl(hm_store *s, const hm_batch *b, const uint32_t *doc_handl
             SCHK(s, hm_launch_append(s->descs.p, n, ar, ar, A.changes, t_dp, t_op, A.remap, S, st, s->alist.p, &s->st->n_app));
             T.mark("alloc+append");
             SCHK(s, hipEventRecord(s->ev[0], st));
-            if (A.incremental && s->any_state) {
+            if (A.incremental) {
                 IncArgs IA;
                 IA.descs = s->descs.p; IA.n = n; IA.list = nullptr; IA.S = S;
                 IA.st_changes = A.changes; IA.st_deps = t_dp; IA.st_ops = t_op;
@@ -805,8 +815,11 @@ int hm_store_set_incremental(hm_store *s, int on) {
     if (s->pending) return hm_engine_fail(s->e, HM_ERR_INVALID, "batch in flight");
     // re-merges while the path was off kept no survivor metadata: every document's next submit
     // re-merges (and rebuilds it)
-    if (on && !s->incremental && s->cap_h)
+    if (on && !s->incremental && s->cap_h) {
         SCHK(s, hipMemsetAsync(s->ist, 0, s->cap_h * sizeof(IncState), hm_engine_stream(s->e)));
+        SCHK(s, hipMemsetAsync(&s->st->n_valid, 0, 4, hm_engine_stream(s->e)));
+        s->any_state = false;
+    }
     s->incremental = on != 0;
     s->inc_mode = on == 2 ? 2u : 1u;
     return HM_OK;
@@ -815,6 +828,16 @@ int hm_store_set_incremental(hm_store *s, int on) {
 int hm_store_last_routing(const hm_store *s, uint32_t *out3) {
     if (!s || !out3) return HM_ERR_INVALID;
     out3[0] = s->st_inc; out3[1] = s->st_cold; out3[2] = s->st_bail;
+    return HM_OK;
+}
+
+int hm_store_inc_states(hm_store *s, uint32_t *out) {
+    if (!s || !out) return HM_ERR_INVALID;
+    if (s->pending) return hm_engine_fail(s->e, HM_ERR_INVALID, "batch in flight");
+    hipStream_t st = hm_engine_stream(s->e);
+    SCHK(s, hipMemcpyAsync(&s->h_cnt[5], &s->st->n_valid, 4, hipMemcpyDeviceToHost, st));
+    SCHK(s, hipStreamSynchronize(st));
+    *out = s->h_cnt[5];
     return HM_OK;
 }
 

@@ -52,7 +52,10 @@ struct PlanStats {
     unsigned long long need[4];                // rows the submit's growing segments take, per space
     unsigned long long tot_c, tot_d, tot_o, tot_r;
     unsigned long long bump[4];                // arena bump pointers (device-side segment allocation;
-};                                             //   last: one memset clears every per-phase field)
+                                               //   last: one memset clears every per-phase field)
+    uint32_t n_valid, pad_v;                   // documents whose IncState can route a submit to the incremental
+};                                             //   kernels (HM_IST_VALID without NOCKEY): kept by every writer
+#define HM_IST_COUNTS(f) (((f) & (HM_IST_VALID | HM_IST_NOCKEY)) == HM_IST_VALID)
 #define HM_PLAN_BAD_HANDLE 1u
 #define HM_PLAN_REPEATED 2u
 #define HM_PLAN_ROWS 4u
@@ -211,7 +214,7 @@ hipError_t hm_launch_rollback(const uint32_t *handles, uint32_t n, const hm_doc_
 hipError_t hm_launch_init_docs(DevDoc *dm, uint32_t h0, uint32_t n, hipStream_t s);
 hipError_t hm_launch_reset_docs(const uint32_t *handles, uint32_t n, DevDoc *dm, hm_doc_result *res, IncState *ist,
                                 uint32_t *clock, uint32_t *back, uint32_t *heads, uint32_t *minc, uint32_t *stored,
-                                uint32_t S, hipStream_t s);
+                                uint32_t S, uint32_t *n_valid, hipStream_t s);
 // chosen registers of resident documents by (handle, register): validated on the device
 hipError_t hm_launch_read_hist(uint32_t n, const uint32_t *handles, const uint32_t *from, const uint32_t *to,
                                const uint32_t *out_off, const DevDoc *dm, uint32_t n_handles, const int32_t *hist,
@@ -241,7 +244,10 @@ struct MetaArgs {
     uint32_t *epos, *epar, *ekey, *lorder;
     uint2 *ldir;
     uint32_t small_lists;                      // list documents of at most this many ops keep no list state
+    uint32_t *n_valid;                         // PlanStats.n_valid (the documents' states that count)
+    int *part;                                 // [HM_META_GRID] per-workgroup changes of n_valid (scratch)
 };
+#define HM_META_GRID 65535u                    // inc_meta_kernel's largest grid
 hipError_t hm_launch_inc_meta(const MetaArgs &a, hipStream_t s);
 // element positions of the listed list documents reset (HM_NONE) before their re-merge writes them
 hipError_t hm_launch_epos_clear(const uint32_t *list, uint32_t n, const DevDoc *dm, uint32_t *epos, hipStream_t s);

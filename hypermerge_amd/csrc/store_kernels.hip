@@ -519,7 +519,7 @@ __global__ __launch_bounds__(PLAN_WG) void doc_rows_kernel(const uint32_t *list,
     __syncthreads();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-    bool kp = false;
+    bool kp = false, drop = false;
     uint32_t h = 0;
     if (i < n) {
         h = list[i];
@@ -530,7 +530,11 @@ __global__ __launch_bounds__(PLAN_WG) void doc_rows_kernel(const uint32_t *list,
         const bool lists = (m.flags & HM_DOC_HAS_LISTS) != 0;
         kp = !(lists && m.n_o <= small_lists);
         if (kp && lists) atomicAdd(&s_mx[7], 1u);
-        if (!kp && ist) { IncState z = {}; ist[h] = z; }
+        if (!kp && ist) {
+            drop = HM_IST_COUNTS(ist[h].flags);                // (PlanStats.n_valid follows every state cleared)
+            IncState z = {};
+            ist[h] = z;
+        }
         hm_doc_row r;
         r.change_off = m.c_off; r.n_changes = m.n_c; r.dep_off = m.d_off; r.n_deps = m.n_d;
         r.op_off = m.o_off; r.n_ops = m.n_o; r.reg_off = m.r_off; r.n_regs = m.n_r;
@@ -541,6 +545,8 @@ __global__ __launch_bounds__(PLAN_WG) void doc_rows_kernel(const uint32_t *list,
         atomicAdd(&s_tot[0], (unsigned long long)m.n_c); atomicAdd(&s_tot[1], (unsigned long long)m.n_d);
         atomicAdd(&s_tot[2], (unsigned long long)m.n_o); atomicAdd(&s_tot[3], (unsigned long long)m.n_r);
     }
+    const uint32_t nd = (uint32_t)__popcll(__ballot(drop));
+    if (ln == 0 && nd) atomicSub(&st->n_valid, nd);
     // the keep list (inc_meta's and the position clear's work list): one slot atomic per workgroup
     const unsigned long long km = __ballot(kp);
     if (ln == 0) s_kw[wv] = (uint32_t)__popcll(km);
@@ -617,7 +623,7 @@ __global__ void init_docs_kernel(DevDoc *dm, uint32_t h0, uint32_t n) {
 // Backend.init() result row, zero clocks and incremental state); one thread per handle
 __global__ void reset_docs_kernel(const uint32_t *handles, uint32_t n, DevDoc *dm, hm_doc_result *res, IncState *ist,
                                   uint32_t *clock, uint32_t *back, uint32_t *heads, uint32_t *minc, uint32_t *stored,
-                                  uint32_t S) {
+                                  uint32_t S, uint32_t *n_valid) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t h = handles[i];
@@ -627,6 +633,7 @@ __global__ void reset_docs_kernel(const uint32_t *handles, uint32_t n, DevDoc *d
     hm_doc_result r = {};
     r.err_change = HM_NONE; r.err_op = HM_NONE;
     res[h] = r;
+    if (HM_IST_COUNTS(ist[h].flags)) atomicSub(n_valid, 1u);
     ist[h] = IncState{};
     for (uint32_t a = 0; a < S; a++) {
         const size_t k = (size_t)h * S + a;
@@ -708,10 +715,10 @@ hipError_t hm_launch_init_docs(DevDoc *dm, uint32_t h0, uint32_t n, hipStream_t 
 }
 hipError_t hm_launch_reset_docs(const uint32_t *handles, uint32_t n, DevDoc *dm, hm_doc_result *res, IncState *ist,
                                 uint32_t *clock, uint32_t *back, uint32_t *heads, uint32_t *minc, uint32_t *stored,
-                                uint32_t S, hipStream_t s) {
+                                uint32_t S, uint32_t *n_valid, hipStream_t s) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(hms::reset_docs_kernel, dim3((n + 255) / 256), dim3(256), 0, s, handles, n, dm, res, ist, clock, back,
-                       heads, minc, stored, S);
+                       heads, minc, stored, S, n_valid);
     return hipGetLastError();
 }
 hipError_t hm_launch_read_regs_h(uint32_t n, const uint32_t *handles, const uint32_t *regs, const DevDoc *dm,

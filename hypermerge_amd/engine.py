@@ -30,7 +30,7 @@ EXPORTS = ("hm_abi_version", "hm_status_message", "hm_engine_create", "hm_engine
            "hm_clock_allgather", "hm_clock_min_allreduce", "hm_comm_create_local", "hm_clock_exchange_host",
            "hm_clock_min_host", "hm_decode_blocks", "hm_decoded_batch", "hm_decoded_status", "hm_decoded_n_strings",
            "hm_decoded_string", "hm_decoded_actor", "hm_decoded_obj", "hm_decoded_reg", "hm_decoded_free",
-           "hm_store_set_incremental", "hm_store_last_routing", "hm_store_last_kernel_ms", "hm_debug_async_check", "hm_doc_open_n", "hm_doc_reset", "hm_store_read_regs", "hm_store_read_history",
+           "hm_store_set_incremental", "hm_store_last_routing", "hm_store_last_kernel_ms", "hm_store_inc_states", "hm_debug_async_check", "hm_doc_open_n", "hm_doc_reset", "hm_store_read_regs", "hm_store_read_history",
            "hm_cursors_create", "hm_cursors_destroy", "hm_cursors_reserve", "hm_cursors_update", "hm_cursors_get",
            "hm_cursors_entry", "hm_cursors_docs_with_actors", "hm_docset_create", "hm_docset_destroy",
            "hm_docset_engine", "hm_docset_open", "hm_docset_apply", "hm_text_data", "hm_text_results", "hm_text_free",
@@ -97,7 +97,7 @@ def lib():
             "hm_decoded_status": [vp], "hm_decoded_n_strings": [vp], "hm_decoded_string": [vp, u32, vp],
             "hm_decoded_actor": [vp, u32, u32, vp], "hm_decoded_free": [vp],
             "hm_decoded_obj": [vp, u32, u32, vp], "hm_decoded_reg": [vp, u32, u32, vp, vp],
-            "hm_store_set_incremental": [vp, ctypes.c_int], "hm_store_last_routing": [vp, vp], "hm_store_last_kernel_ms": [vp, vp], "hm_debug_async_check": [vp, ctypes.c_int],
+            "hm_store_set_incremental": [vp, ctypes.c_int], "hm_store_last_routing": [vp, vp], "hm_store_last_kernel_ms": [vp, vp], "hm_store_inc_states": [vp, vp], "hm_debug_async_check": [vp, ctypes.c_int],
             "hm_doc_open_n": [vp, u32, vp], "hm_doc_reset": [vp, vp, u32], "hm_store_read_regs": [vp, u32, vp, vp, vp, vp, u32, vp],
             "hm_store_read_history": [vp, u32, vp, vp, vp, vp, vp, vp],
             "hm_cursors_create": [vp, u32, vp], "hm_cursors_destroy": [vp], "hm_cursors_reserve": [vp, u32],

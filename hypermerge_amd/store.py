@@ -244,6 +244,12 @@ class DocStore:
         self._check(self._L.hm_store_last_routing(self._h, _p(out)), "hm_store_last_routing")
         return {"incremental": int(out[0]), "remerged": int(out[1]), "handed_back": int(out[2])}
 
+    def inc_states(self) -> int:
+        """Documents whose resident incremental state a submit can use (hm_store_inc_states)."""
+        out = np.zeros(1, np.uint32)
+        self._check(self._L.hm_store_inc_states(self._h, _p(out)), "hm_store_inc_states")
+        return int(out[0])
+
     def last_kernel_ms(self) -> Dict[str, float]:
         """Device time of the last submit (HIP events): the incremental kernels and the re-merge."""
         out = np.zeros(2, np.float32)

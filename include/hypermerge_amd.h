@@ -358,6 +358,10 @@ int hm_store_last_routing(const hm_store *s, uint32_t *out3);
  * they did not take (row build, merge kernels, metadata), in ms; read once hm_batch_wait(_device)
  * has returned for that submit (the submit itself does not wait for its kernels). */
 int hm_store_last_kernel_ms(const hm_store *s, float *out2);
+/* Documents whose resident incremental state a submit can use (kept on the device by every step
+ * that builds or drops a state; a store with none plans its submits as whole re-merges and
+ * launches no incremental kernel).  Synchronous; no batch may be in flight. */
+int hm_store_inc_states(hm_store *s, uint32_t *out);
 
 /* Diagnostics of check builds (libhmgpu_check.so, built beside libhmgpu.so): out2[0] = documents
  * whose next rows merge_small_kernel loaded asynchronously and re-read with counted loads,

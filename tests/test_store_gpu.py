@@ -623,3 +623,57 @@ def test_default_cost_rule_on_long_c4_rounds_matches_oracle(engine):
     assert routed["incremental"] > 0 and routed["remerged"] > 0, routed
     for h in hs:
         assert_doc_matches_oracle(store, h)
+
+
+def test_inc_state_count_follows_every_writer(engine):
+    """hm_store_inc_states: the documents whose resident state a submit can use, kept on the
+    device by inc_meta (built / dropped after a re-merge), doc_rows (cleared for documents that keep
+    none), hm_doc_reset and hm_store_set_incremental; a store with none plans whole re-merges and
+    launches no incremental kernel, with results equal to a re-merge-only store."""
+    b = synth.generate(synth.config("C4", n_docs=120))
+    docs = [decode_doc(b, i) for i in range(b.n_docs)]
+    A, B = DocStore(engine, a_stride=8), DocStore(engine, a_stride=8)
+    B.set_incremental(False)
+    ha = [A.open() for _ in docs]
+    hb = [B.open() for _ in docs]
+    assert A.inc_states() == 0
+    pos = [len(c) - 6 for c in docs]
+    A.apply([(h, docs[i][:pos[i]]) for i, h in enumerate(ha)])
+    B.apply([(h, docs[i][:pos[i]]) for i, h in enumerate(hb)])
+    assert A.inc_states() == len(docs)                      # clean map documents: every one
+    A.reset(ha[:10])
+    B.reset(hb[:10])
+    assert A.inc_states() == len(docs) - 10
+    for i in range(10):
+        pos[i] = 0
+    # switched off and on: every state dropped; the next submit re-merges all and rebuilds them
+    A.set_incremental(False)
+    A.set_incremental(True)
+    assert A.inc_states() == 0
+    for rnd in range(3):
+        items = [(i, docs[i][pos[i]:pos[i] + 2 if rnd else len(docs[i]) - 4]) for i in range(len(docs))]
+        ra = A.apply([(ha[i], c) for i, c in items])
+        rb = B.apply([(hb[i], c) for i, c in items])
+        for f in ("docs", "clock", "back_clock", "heads"):
+            np.testing.assert_array_equal(getattr(ra, f), getattr(rb, f), err_msg=f"{f} round {rnd}")
+        r = A.last_routing()
+        if rnd == 0:
+            assert r["incremental"] == 0 and r["remerged"] == len(docs), r
+        else:
+            assert r["incremental"] >= 0.9 * len(docs), r
+        assert A.inc_states() == len(docs)
+        for i, c in items:
+            pos[i] += len(c)
+    # mode 1: small list documents keep no state (C5: none routes incremental, none is counted)
+    b5 = synth.generate(synth.config("C5", n_docs=60))
+    d5 = [decode_doc(b5, i) for i in range(b5.n_docs)]
+    small = bool((b5.docs["n_ops"] <= 256).all())
+    C5 = DocStore(engine, a_stride=8)
+    h5 = [C5.open() for _ in d5]
+    C5.apply([(h, d5[i][:len(d5[i]) - 2]) for i, h in enumerate(h5)])
+    if small:
+        assert C5.inc_states() == 0
+    C5.set_incremental(2)
+    C5.apply([(h, d5[i][len(d5[i]) - 2:len(d5[i]) - 1]) for i, h in enumerate(h5)])
+    n2 = C5.inc_states()
+    assert 0 < n2 <= len(d5)

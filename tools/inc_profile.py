@@ -47,7 +47,7 @@ def main():
     st.submit_device(n, cnt, *tt)
     st.wait_device(out)
     del tt
-    print(f"initial {time.perf_counter() - t:.3f}s", flush=True)
+    print(f"initial {time.perf_counter() - t:.3f}s inc_states {st.inc_states()}", flush=True)
     rng = np.random.default_rng(5)
     os.environ["HM_STORE_PROFILE"] = "1"
     r = 0
@@ -70,7 +70,7 @@ def main():
             st.wait()
             t2 = time.perf_counter()
         print(f"round {r}: {len(sel)} docs {len(sub.changes)} changes submit {1e3 * (t1 - t0):.2f} ms "
-              f"wait {1e3 * (t2 - t1):.2f} ms routing {st.last_routing()}", flush=True, file=sys.stderr)
+              f"wait {1e3 * (t2 - t1):.2f} ms routing {st.last_routing()} inc_states {st.inc_states()}", flush=True, file=sys.stderr)
         pos = np.maximum(pos, hi)
         r += 1
 
