@@ -74,10 +74,40 @@ const ACTIONS = ['create', 'set', 'remove', 'insert']
 // makes millions of small objects per round, and the garbage collector is the JS thread's
 // largest cost)
 const R = { w: null, nums: null, strs: null, p: 0, sb: 0, nb: 0, tag: 0, dt: 0 }
+// Clock objects ({actorId: seq}).  Hypermerge mints an actor per document, so a process holds
+// thousands of distinct actor ids; object literals keyed by them give V8 a hidden-class
+// transition per new key from the empty shape, and past its transition limit every clock built
+// falls to the slow path (C2 with base58 ids: clocks 4x slower than in dictionary mode, and the
+// maps' garbage).  Once more than 1024 distinct actor ids have been seen, clocks start in
+// dictionary mode (an object literal whose two placeholder keys are deleted: Object.prototype
+// stays, insertion order stays); with a few shared actors the literal form is faster (3x) and stays.
+const CK = { dict: false, seen: new Set(), probes: 0 }
+function noteActor(a) {
+  const s = CK.seen
+  if (!s) return
+  s.add(a)
+  if (s.size > 1024) { CK.dict = true; CK.seen = null } else if (++CK.probes > 65536) CK.seen = null
+}
+function newClock() {
+  if (!CK.dict) return {}
+  const c = { _a: 0, _b: 0 }
+  delete c._a
+  delete c._b
+  return c
+}
+// a long-lived clock made before the switch, moved to the dictionary form (once per object)
+function dictCopy(o) {
+  const c = newClock()
+  for (const k in o) c[k] = o[k]
+  return c
+}
 function rdClock() {
   const w = R.w, strs = R.strs, sb = R.sb
-  const c = {}
+  const c = newClock()
   let p = R.p
+  if (CK.seen) {
+    for (let k = w[p]; k > 0; k--) noteActor(strs[sb + w[p + 2 * k - 1]])
+  }
   for (let k = w[p++]; k > 0; k--) { c[strs[sb + w[p]]] = w[p + 1]; p += 2 }
   R.p = p
   return c
@@ -129,6 +159,11 @@ class RoundReader {
   // collection are promoted, and the old generation's collections cost the JS thread most)
   advance(d, state) {
     if (this.woff[d] === this.woff[d + 1]) return false
+    if (CK.dict && !state.dictClocks) {
+      state.clock = dictCopy(state.clock)
+      state.backClock = dictCopy(state.backClock)
+      state.dictClocks = true
+    }
     this.enter(d, this.woff[d])
     rdClockInto(state.clock)
     state.deps = rdClock()
@@ -325,9 +360,10 @@ class GpuBackendState {
     this.log = []
     this.histLen = 0
     this.nQueued = 0
-    this.clock = {}
-    this.deps = {}
-    this.backClock = {}              // max seq per actor over the whole log (queued included)
+    this.clock = newClock()
+    this.deps = newClock()
+    this.backClock = newClock()      // max seq per actor over the whole log (queued included)
+    this.dictClocks = CK.dict
     // Automerge's local undo history (applyLocalChange, SURVEY Appendix A.4): undoStack of op
     // lists, undoPos, redoStack; canUndo = undoPos > 0, canRedo = redoStack not empty
     this.undoStack = []
@@ -687,11 +723,11 @@ function fullPatch(state) {
     for (const [key, e] of ov.keys) diffs.push(Object.assign({ action: 'set', type: ov.type, obj: uuid, key }, e))
     ov.elems.forEach(([elemId, e], index) => diffs.push(Object.assign({ action: 'insert', type: ov.type, obj: uuid, index, elemId }, e)))
   }
-  return { clock: Object.assign({}, state.clock), deps: Object.assign({}, state.deps), canUndo: state.canUndo,
+  return { clock: dictCopy(state.clock), deps: dictCopy(state.deps), canUndo: state.canUndo,
     canRedo: state.canRedo, diffs }
 }
 
-const emptyPatch = (state) => ({ clock: Object.assign({}, state.clock), deps: Object.assign({}, state.deps),
+const emptyPatch = (state) => ({ clock: dictCopy(state.clock), deps: dictCopy(state.deps),
   canUndo: state.canUndo, canRedo: state.canRedo, diffs: [] })
 
 // ---------------- local undo / redo (Backend.applyLocalChange, src/DocBackend.ts:187-205) ----------------
@@ -780,7 +816,8 @@ class DocBackend {
   constructor(documentId, notify, back, engine) {
     this.id = documentId
     this.actorId = undefined
-    this.clock = {}
+    this.clock = newClock()
+    this.dictClock = CK.dict
     this.back = undefined
     this.changes = new Map()
     this.ready = new Channel('doc:back:readyQ')
@@ -838,6 +875,7 @@ class DocBackend {
   // DocBackend.updateClock (src/DocBackend.ts:135-142) from the max seq per actor of the
   // handed changes (queued ones included), which the docset reports per round
   updateClock(roundClock) {
+    if (CK.dict && !this.dictClock) { this.clock = dictCopy(this.clock); this.dictClock = true }
     for (const a in roundClock) {
       const old = this.clock[a] || 0
       this.clock[a] = Math.max(old, roundClock[a])

@@ -282,8 +282,27 @@ const Backend = {
   },
 }
 
+// Clock objects keyed by actor id: the same rule as the GPU drop-in (GpuDocBackend.js newClock),
+// so the baseline does not pay V8's per-key hidden-class transitions when every document has its
+// own actors (hypermerge mints an actor per document): past 1024 distinct actor ids seen, clocks
+// start in dictionary mode
+const CK = { dict: false, seen: new Set(), probes: 0 }
+function noteActor(a) {
+  const s = CK.seen
+  if (!s) return
+  s.add(a)
+  if (s.size > 1024) { CK.dict = true; CK.seen = null } else if (++CK.probes > 65536) CK.seen = null
+}
+function newClock() {
+  if (!CK.dict) return {}
+  const c = { _a: 0, _b: 0 }
+  delete c._a
+  delete c._b
+  return c
+}
+
 function makePatch(s, diffs) {
-  const clock = {}, deps = {}
+  const clock = newClock(), deps = newClock()
   for (const [a, q] of s.clock) clock[a] = q
   for (const [a, q] of s.deps) deps[a] = q
   return { clock, deps, canUndo: s.undoPos > 0, canRedo: s.redoStack.length > 0, diffs }
@@ -300,7 +319,8 @@ class DocBackend {
   constructor(documentId, notify, back) {
     this.id = documentId
     this.actorId = undefined
-    this.clock = {}
+    this.clock = newClock()
+    this.dictClock = CK.dict
     this.back = back
     this.changes = new Map()
     this.ready = new Queue()
@@ -324,7 +344,16 @@ class DocBackend {
   applyLocalChange(change) { this.localChangeQ.push(change) }
 
   updateClock(changes) {
-    for (const c of changes) this.clock[c.actor] = Math.max(this.clock[c.actor] || 0, c.seq)
+    if (CK.dict && !this.dictClock) {
+      const c = newClock()
+      for (const k in this.clock) c[k] = this.clock[k]
+      this.clock = c
+      this.dictClock = true
+    }
+    for (const c of changes) {
+      if (CK.seen) noteActor(c.actor)
+      this.clock[c.actor] = Math.max(this.clock[c.actor] || 0, c.seq)
+    }
   }
 
   init(changes, actorId) {
