@@ -1323,8 +1323,33 @@ __device__ __forceinline__ uint32_t change_of_op(const hm_change_row *ch, uint32
 // directory ldir = (object, elements) per list.
 // Documents that are not clean (an error, queued changes) get flags = 0: their next submit
 // re-merges.
+// a document of at most META_LCH changes keeps its changes' first ops (and applied bits) in LDS
+// for the op -> change searches: from HBM / L2 each of their ~8 steps is a dependent round trip,
+// which made one 3.7k-op text document's rebuild 236 us (a C3 round re-merging one or two
+// documents spent that on top of the merge)
+constexpr uint32_t META_LCH = 1024;
+#ifndef HM_META_STAMPS
+#define HM_META_STAMPS 0     // diagnostic builds: inc_meta_kernel's per-phase wave time (hm_debug_meta_stamps)
+#endif
+#if HM_META_STAMPS
+__device__ unsigned long long hm_meta_st[8];
+#define MSTAMP(k) do { const unsigned long long t_ = wall_clock64(); if (lane == 0) atomicAdd(&hm_meta_st[k], t_ - t_ms); t_ms = t_; } while (0)
+#else
+#define MSTAMP(k) do { } while (0)
+#endif
+__device__ __forceinline__ uint32_t change_of_op_lds(const uint32_t *s_of, uint32_t n_c, uint32_t k) {
+    uint32_t lo = 0, hi = n_c;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((s_of[mid] & 0x7FFFFFFFu) <= k) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
 __global__ __launch_bounds__(256) void inc_meta_kernel(MetaArgs a) {
     const uint32_t lane = threadIdx.x & 63;
+    __shared__ uint32_t s_of4[4][META_LCH];                  // per wave: op_first - o_off | applied << 31
+    uint32_t *s_of = s_of4[threadIdx.x >> 6];
     // the change in PlanStats.n_valid, summed per wave, then per workgroup into part[], then by
     // valid_sum_kernel: device-scope atomics on one word from every document (or workgroup)
     // serialize across the XCDs (~10 ns each: 0.3-1.8 ms for 65k-1M of them)
@@ -1336,6 +1361,9 @@ __global__ __launch_bounds__(256) void inc_meta_kernel(MetaArgs a) {
     // document decide first and a wave build the kept ones serially cost a C3 round the sum of its
     // few re-merged documents' rebuilds: 0.35 -> 1.07 ms)
     for (uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6); q < a.n; q += gridDim.x * 4) {
+#if HM_META_STAMPS
+        unsigned long long t_ms = wall_clock64();
+#endif
         const uint32_t h = a.list[q];
         const DevDoc m = a.dm[h];
         const hm_doc_result r = a.res_docs[h];
@@ -1352,30 +1380,47 @@ __global__ __launch_bounds__(256) void inc_meta_kernel(MetaArgs a) {
             continue;
         }
         const hm_change_row *ch = a.changes + m.c_off;
-        for (uint32_t i = lane; i < r.n_surv; i += 64) {
-            const uint32_t op = a.surv[m.o_off + i].op;
-            const uint32_t c = change_of_op(ch, m.n_c, m.o_off, op);
-            const uint2 kw = *reinterpret_cast<const uint2 *>(ch + c);
-            const hm_op_row &o = a.ops[m.o_off + op];
-            const uint32_t cset = (o.action == HM_SET && o.datatype == HM_DT_COUNTER) ? 0x100u : 0u;
-            a.smeta[m.o_off + i] = make_uint2(kw.y, (kw.x & 0xFFu) | cset);
-        }
+        const bool lch = m.n_c <= META_LCH;
         bool wide = false;                                   // a seq the packed keys cannot hold
         for (uint32_t i = lane; i < m.n_c; i += 64) {
-            const uint2 kw = *reinterpret_cast<const uint2 *>(ch + i);
-            wide |= kw.y >= (1u << 24);
-            a.ckey[m.c_off + i] = hm_ckey(kw.x & 0xFFFFu, kw.y, a.hist[m.c_off + i] >= 0);
+            const hm_change_row c = ch[i];
+            const bool app = a.hist[m.c_off + i] >= 0;
+            wide |= c.seq >= (1u << 24);
+            a.ckey[m.c_off + i] = hm_ckey(c.actor, c.seq, app);
+            if (lch) s_of[i] = (c.op_first - m.o_off) | (app ? 0x80000000u : 0u);
         }
         wide = __ballot(wide) != 0;
+        __threadfence_block();                               // (s_of: this wave's writes, then its reads)
+        __builtin_amdgcn_wave_barrier();
+        MSTAMP(0);
+        // (the next chunk's survivor rows are loaded before this chunk's lookups)
+        uint32_t sop = lane < r.n_surv ? a.surv[m.o_off + lane].op : 0u;
+        for (uint32_t i = lane; i < r.n_surv; i += 64) {
+            const uint32_t op = sop;
+            if (i + 64 < r.n_surv) sop = a.surv[m.o_off + i + 64].op;
+            const uint32_t ow = reinterpret_cast<const uint4 *>(a.ops + m.o_off + op)[1].x;   // action | datatype << 8
+            const uint32_t c = lch ? change_of_op_lds(s_of, m.n_c, op) : change_of_op(ch, m.n_c, m.o_off, op);
+            const uint2 kw = *reinterpret_cast<const uint2 *>(ch + c);
+            const uint32_t cset = ((ow & 0xFFu) == HM_SET && ((ow >> 8) & 0xFFu) == HM_DT_COUNTER) ? 0x100u : 0u;
+            a.smeta[m.o_off + i] = make_uint2(kw.y, (kw.x & 0xFFu) | cset);
+        }
+        MSTAMP(1);
         unsigned long long mask = 1ull, cabs = 0;
-        // the list / text objects created: distinct, ascending, at most LMAX (lane k holds list k)
-        uint32_t lobj = HM_NONE, nlst = 0;
-        bool over = false;
-        for (uint32_t i0 = 0; i0 < m.n_o; i0 += 64) {
-            const uint32_t i = i0 + lane;
+        // the op scans below load the next chunk's rows before working on this one (a large
+        // document's scans are dozens of chunks, each otherwise waiting on its loads)
+        auto ldop = [&](uint32_t i) -> hm_op_row {
             hm_op_row o = {};
             o.action = 0xFF;
             if (i < m.n_o) o = a.ops[m.o_off + i];
+            return o;
+        };
+        // the list / text objects created: distinct, ascending, at most LMAX (lane k holds list k)
+        uint32_t lobj = HM_NONE, nlst = 0;
+        bool over = false;
+        hm_op_row nx = ldop(lane);
+        for (uint32_t i0 = 0; i0 < m.n_o; i0 += 64) {
+            const hm_op_row o = nx;
+            nx = ldop(i0 + 64 + lane);
             if ((o.action == HM_MAKE_MAP || o.action == HM_MAKE_TABLE) && o.obj < 64) mask |= 1ull << o.obj;
             if (o.vtag == HM_V_INT && (o.action == HM_INC || (o.action == HM_SET && o.datatype == HM_DT_COUNTER))) {
                 const unsigned long long v = abs64((int64_t)o.value);
@@ -1398,10 +1443,77 @@ __global__ __launch_bounds__(256) void inc_meta_kernel(MetaArgs a) {
             const unsigned long long y = (unsigned long long)__shfl_xor((long long)cabs, d);
             cabs = cabs + y > (1ull << 62) ? (1ull << 62) : cabs + y;
         }
+        MSTAMP(2);
         // the lists' order from the element positions of the merge (within each list), laid end
         // to end: every applied insert counted per list, then placed at its list's base
         uint32_t flags = HM_IST_VALID | (wide ? HM_IST_NOCKEY : 0u), n_el = 0;
-        if (nlst && !over && a.lorder && a.ldir) {
+        if (nlst == 1 && !over && a.lorder && a.ldir) {
+            // one list (a text document): its base is 0, so the element positions the merge wrote
+            // are already global — one pass counts the applied inserts, places each at its
+            // position, and checks every insert's position against the count (the two counting /
+            // placing passes and the hole check of the general case below, fused: C3's rebuild)
+            const uint32_t lo0 = (uint32_t)__shfl((int)lobj, 0);
+            bool bad = false, any_ins = false;
+            uint32_t cnt1 = 0, maxpos = 0, c_lo = 0;                  // c_lo: the change of the chunk's first op
+            hm_op_row px = ldop(lane);
+            for (uint32_t i0 = 0; i0 < m.n_o; i0 += 64) {
+                const uint32_t i = i0 + lane;
+                const hm_op_row o = px;
+                px = ldop(i0 + 64 + lane);
+                // the changes that start inside the chunk (ops are grouped by change): lane j holds
+                // the first op of change c_lo + 1 + j; an op's change is c_lo plus those starting at
+                // or before it — one LDS read and a readlane per such change, no dependent search
+                uint32_t cc = 0;
+                bool chunk_ok = false;
+                if (lch) {
+                    const uint32_t cj = c_lo + 1 + lane;
+                    const uint32_t ofj = cj < m.n_c ? (s_of[cj] & 0x7FFFFFFFu) : 0xFFFFFFFFu;
+                    const unsigned long long in = __ballot(ofj <= i0 + 63);
+                    chunk_ok = ~in != 0;                                  // (64 changes starting: search instead)
+                    if (chunk_ok) {
+                        cc = c_lo;
+                        for (uint32_t j = 0, K = (uint32_t)__popcll(in); j < K; j++)
+                            cc += (uint32_t)__builtin_amdgcn_readlane((int)ofj, (int)j) <= i ? 1u : 0u;
+                    }
+                }
+                bool applied_ins = false;
+                uint32_t c = 0;
+                if (o.action == HM_INS) {
+                    if (lch) {
+                        c = chunk_ok ? cc : change_of_op_lds(s_of, m.n_c, i);
+                        applied_ins = (s_of[c] >> 31) != 0;              // (a duplicate's copy: its twin counts)
+                    } else {
+                        c = change_of_op(ch, m.n_c, m.o_off, i);
+                        applied_ins = a.hist[m.c_off + c] >= 0;
+                    }
+                }
+                if (lch) {                                                // the next chunk's first change
+                    const uint32_t cl = chunk_ok ? cc : change_of_op_lds(s_of, m.n_c, i < m.n_o ? i : m.n_o - 1);
+                    c_lo = (uint32_t)__builtin_amdgcn_readlane((int)cl, 63);
+                }
+                const bool mine = o.obj == lo0;
+                bad |= applied_ins && !(mine && o.elem < (1u << 24));
+                cnt1 += (uint32_t)__popcll(__ballot(applied_ins && mine));
+                if (o.action == HM_INS && o.reg < m.n_r) {
+                    const uint32_t pos = a.epos[m.r_off + o.reg];
+                    any_ins = true;
+                    maxpos = pos > maxpos ? pos : maxpos;               // (HM_NONE: a hole)
+                    if (applied_ins && mine && pos < m.n_r) {
+                        a.lorder[m.r_off + pos] = o.reg;
+                        a.epar[m.r_off + o.reg] = o.parent;
+                        a.ekey[m.r_off + o.reg] = (o.elem << 8) | (ch[c].actor & 0xFFu);
+                    }
+                }
+            }
+            for (uint32_t d = 1; d < 64; d <<= 1) maxpos = max(maxpos, (uint32_t)__shfl_xor((int)maxpos, d));
+            MSTAMP(3);
+            n_el = cnt1;
+            // every applied insert in the list, every insert's element placed inside it
+            if (__ballot(bad) == 0 && (__ballot(any_ins) == 0 || maxpos < cnt1)) {
+                flags |= HM_IST_LIST;
+                if (lane == 0) a.ldir[(size_t)h * LMAX] = make_uint2(lo0, cnt1);
+            }
+        } else if (nlst && !over && a.lorder && a.ldir) {
             bool ok = true;
             uint32_t cnt = 0;                                  // lane k < nlst: list k's elements
             for (uint32_t pass = 0; pass < 2 && ok; pass++) {
@@ -1411,16 +1523,21 @@ __global__ __launch_bounds__(256) void inc_meta_kernel(MetaArgs a) {
                         const uint32_t x = (uint32_t)__shfl((int)cnt, (int)k);     // (every lane shuffles)
                         bk += k < lane ? x : 0u;
                     }
+                hm_op_row px = ldop(lane);
                 for (uint32_t i0 = 0; i0 < m.n_o; i0 += 64) {
                     const uint32_t i = i0 + lane;
-                    hm_op_row o = {};
-                    o.action = 0xFF;
-                    if (i < m.n_o) o = a.ops[m.o_off + i];
+                    const hm_op_row o = px;
+                    px = ldop(i0 + 64 + lane);
                     bool applied_ins = false;
                     uint32_t c = 0, lk = HM_NONE;
                     if (o.action == HM_INS) {
-                        c = change_of_op(ch, m.n_c, m.o_off, i);
-                        applied_ins = a.hist[m.c_off + c] >= 0;          // (a duplicate's copy: its twin counts)
+                        if (lch) {
+                            c = change_of_op_lds(s_of, m.n_c, i);
+                            applied_ins = (s_of[c] >> 31) != 0;          // (a duplicate's copy: its twin counts)
+                        } else {
+                            c = change_of_op(ch, m.n_c, m.o_off, i);
+                            applied_ins = a.hist[m.c_off + c] >= 0;
+                        }
                     }
                     for (uint32_t k = 0; k < nlst; k++) lk = (uint32_t)__shfl((int)lobj, (int)k) == o.obj ? k : lk;
                     // (every lane shuffles: a lane that places nothing still serves as a source)
@@ -1444,6 +1561,7 @@ __global__ __launch_bounds__(256) void inc_meta_kernel(MetaArgs a) {
                     }
                 }
                 ok = __ballot(!ok) == 0;
+                MSTAMP(3 + pass);
             }
             for (uint32_t k = 0; k < nlst; k++) n_el += (uint32_t)__shfl((int)cnt, (int)k);
             // every element placed, at positions 0 .. n_el - 1 (detached elements have none)
@@ -1451,12 +1569,15 @@ __global__ __launch_bounds__(256) void inc_meta_kernel(MetaArgs a) {
             __builtin_amdgcn_wave_barrier();
             if (ok) {
                 bool hole = false;
-                for (uint32_t i = lane; i < m.n_o; i += 64) {
-                    const hm_op_row o = a.ops[m.o_off + i];
+                hm_op_row hx = ldop(lane);
+                for (uint32_t i0 = 0; i0 < m.n_o; i0 += 64) {
+                    const hm_op_row o = hx;
+                    hx = ldop(i0 + 64 + lane);
                     if (o.action == HM_INS && o.reg < m.n_r) hole |= a.epos[m.r_off + o.reg] >= n_el;
                 }
                 ok = __ballot(hole) == 0;
             }
+            MSTAMP(5);
             if (ok) {
                 flags |= HM_IST_LIST;
                 if (lane < nlst) a.ldir[(size_t)h * LMAX + lane] = make_uint2(lobj, cnt);
@@ -1537,6 +1658,21 @@ hipError_t hm_launch_inc_apply(const IncArgs &A, hipStream_t s) {
         hipLaunchKernelGGL((hmi::inc_group_kernel<64, true>), dim3(grid(A.n, 4) < 1024u ? grid(A.n, 4) : 1024u), dim3(256), 0, s, B);
     }
     return hipGetLastError();
+}
+
+extern "C" int hm_debug_meta_stamps(unsigned long long *out8, int reset) {
+#if HM_META_STAMPS
+    if (!out8 || hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(hmi::hm_meta_st), 64) != hipSuccess) return -1;
+    if (reset) {
+        const unsigned long long z[8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(hmi::hm_meta_st), z, 64) != hipSuccess) return -1;
+    }
+    return 1;
+#else
+    (void)out8; (void)reset;
+    return 0;
+#endif
 }
 
 hipError_t hm_launch_inc_meta(const MetaArgs &a, hipStream_t s) {

@@ -24,7 +24,7 @@ def main():
     import torch
     torch.cuda.init()
     from hypermerge_amd import synth
-    from hypermerge_amd.engine import Engine
+    from hypermerge_amd.engine import Engine, lib
     from hypermerge_amd.store import RowStore, slice_changes
     b = synth.generate(synth.config(a.config, n_docs=a.docs), threads=16)
     eng = Engine(0)
@@ -50,6 +50,16 @@ def main():
     print(f"initial {time.perf_counter() - t:.3f}s inc_states {st.inc_states()}", flush=True)
     rng = np.random.default_rng(5)
     os.environ["HM_STORE_PROFILE"] = "1"
+    # diagnostic builds (-DHM_META_STAMPS=1, via HMGPU_LIB): inc_meta_kernel's per-phase wave time
+    # over the rounds below
+    import ctypes
+    L = lib()
+    stamps = np.zeros(8, np.uint64)
+    meta = getattr(L, "hm_debug_meta_stamps", None)
+    if meta is not None:
+        meta.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        meta.restype = ctypes.c_int
+        meta(stamps.ctypes.data, 1)
     r = 0
     while (pos < nch).any():
         hi = np.minimum(pos + rng.integers(1, 3, n), nch)
@@ -73,6 +83,11 @@ def main():
               f"wait {1e3 * (t2 - t1):.2f} ms routing {st.last_routing()} inc_states {st.inc_states()}", flush=True, file=sys.stderr)
         pos = np.maximum(pos, hi)
         r += 1
+    if meta is not None and meta(stamps.ctypes.data, 0) == 1:
+        names = ["changes+keys", "survivors", "op scan", "list pass 0", "list pass 1", "hole check"]
+        tot = float(stamps[:6].sum()) or 1.0
+        for k, nm in enumerate(names):
+            print(f"inc_meta {nm:14s} {int(stamps[k]):>14d} ticks {100 * stamps[k] / tot:5.1f}%", flush=True)
 
 
 if __name__ == "__main__":
