@@ -424,6 +424,7 @@ class GpuEngine {
     const t = { calls: 0, docs: 0, moves: 0, hitPatches: 0, fullPatches: 0, opPatches: 0, replayMismatch: 0,
       incremental: 0, remerged: 0, handedBack: 0 }
     for (const ds of this.docsets) { const s = addon.docsetStats(ds); for (const k in t) t[k] += s[k] }
+    t.dictClocks = CK.dict                      // (clocks in dictionary form: > 1024 actor ids seen)
     return t
   }
 

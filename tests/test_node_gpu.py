@@ -112,7 +112,11 @@ def test_patch_diffs_rebuild_the_merged_document(name, n, mode, binary):
                                                       ("C2", 80, "batched", True, "arrival"),
                                                       ("C3", 10, "batched", True, "arrival"),
                                                       ("C3", 10, "async", True, "shuffled"),
-                                                      ("C4", 200, "async", True, "shuffled")])
+                                                      ("C4", 200, "async", True, "shuffled"),
+                                                      # every document with its own actors (as hypermerge mints
+                                                      # them): past 1024 distinct ids both sides' clocks switch
+                                                      # to V8's dictionary form mid-run
+                                                      ("C2", 400, "async", True, "unique")])
 def test_patch_diff_sequence_equals_js_restatement(name, n, mode, binary, order):
     """f2 / a12: every RemotePatchMsg / ReadyMsg patch of the GPU
     drop-in — clock, deps and the diffs, one per applied op in application order (create,
@@ -128,6 +132,12 @@ def test_patch_diff_sequence_equals_js_restatement(name, n, mode, binary, order)
     b = synth.generate(synth.config(name, n_docs=n, **over))
     docs = [decode_doc(b, i) for i in range(b.n_docs)]
     rng = np.random.default_rng(29)
+    if order == "unique":
+        def own(c, i):
+            r = dict(c, actor=f"{c['actor']}-{i:05d}")
+            r["deps"] = {f"{a}-{i:05d}": q for a, q in c["deps"].items()}
+            return r
+        docs = [[own(c, i) for c in chs] for i, chs in enumerate(docs)]
     chunked = []
     for chs in docs:
         chs = list(chs)
@@ -141,6 +151,7 @@ def test_patch_diff_sequence_equals_js_restatement(name, n, mode, binary, order)
     assert p.returncode == 0, p.stderr[-3000:]
     got = json.loads(p.stdout)
     assert got["stats"]["replayMismatch"] == 0 and got["stats"]["opPatches"] > 0
+    assert got["stats"]["dictClocks"] == (order == "unique")
     n_diffs = 0
     for i, d in enumerate(got["docs"]):
         assert len(d["gpu"]) == len(d["cpu"]), i
