@@ -105,6 +105,16 @@ def _routing(r):
     return None if not isinstance(r, dict) else f"{r.get('incremental', 0)}/{r.get('remerged', 0)}"
 
 
+def _side(name, fn):
+    """A side leg: its failure (an exception: a Node timeout, a missing tool) is reported in the
+    detail and the line instead of costing the run its headline."""
+    try:
+        return fn()
+    except Exception as ex:                                   # noqa: BLE001 (reported, not hidden)
+        _progress(f"{name} failed: {type(ex).__name__}: {ex}")
+        return {"error": f"{type(ex).__name__}: {ex}"[:300]}
+
+
 def compact_line(full: dict) -> dict:
     """The one JSON line the driver parses: the headline, its roofline and CPU baseline, and a
     one-level summary of every side leg.  The whole record (per-round tables, Node run lists,
@@ -130,13 +140,18 @@ def compact_line(full: dict) -> dict:
         legs["end_to_end"] = {"value": _r(e2e.get("value"), 3), "pinned": _r((e2e.get("pinned") or {}).get("value"), 3),
                               "same": e2e.get("same_as_device_path")}
     fb = full.get("from_blocks")
-    if fb:
+    if fb and "error" in fb:
+        legs["from_blocks"] = {"error": str(fb["error"])[:120]}
+    elif fb:
         legs["from_blocks"] = {"value": _r(fb.get("value"), 3), "decode_MBps": _r((fb.get("decode") or {}).get("MB_per_s"), 3),
                                "same": fb.get("same_as_generated_rows")}
     for name, key in (("resident_c4", "resident_incremental"), ("resident_c3", "resident_incremental_text"),
                       ("resident_c5", "resident_incremental_c5")):
         r = full.get(key)
         if not r:
+            continue
+        if "error" in r:
+            legs[name] = {"error": str(r["error"])[:120]}
             continue
         ro = r.get("roofline") or {}
         legs[name] = {"value": _r(r.get("value"), 3), "us_round": _r(r.get("us_per_round"), 3),
@@ -164,8 +179,9 @@ def compact_line(full: dict) -> dict:
             legs["node"] = n
     ao = (full.get("arrival_orders") or {}).get("actor_major")
     if ao:
-        legs["actor_major"] = {"value": _r(ao.get("value")), "frac": _r(ao.get("roofline_frac"), 3),
-                               "ms_per_step": _r(ao.get("ms_per_step"))}
+        legs["actor_major"] = ({"error": str(ao["error"])[:120]} if "error" in ao else
+                               {"value": _r(ao.get("value")), "frac": _r(ao.get("roofline_frac"), 3),
+                                "ms_per_step": _r(ao.get("ms_per_step"))})
     line["legs"] = {k: {a: b for a, b in v.items() if b is not None} for k, v in legs.items()}
     if full.get("ranks_note"):
         line["ranks_note"] = full["ranks_note"]
@@ -446,18 +462,18 @@ def main() -> int:
     # multi-threaded decoder (hm_decode_blocks) -> hm_merge_host; reported beside `value`
     from_blocks = None
     if rank == 0 and ws == 1 and not args.no_e2e and args.config in ("C1", "C2", "C4") and args.block_docs > 0:
-        from_blocks = _from_blocks(eng, batch, cfg, args)
+        from_blocks = _side("from_blocks", lambda: _from_blocks(eng, batch, cfg, args))
     # applyRemoteChanges on resident documents: every document of the shard resident in the
     # store, then rounds in which each receives its next 1-2 changes (DocBackend.ts:169-185)
     incremental = None
     incremental_text = None
     incremental_c5 = None
     if rank == 0 and ws == 1 and not args.no_incremental and args.config == "C4" and args.arrival is None:
-        incremental = _incremental(eng, batch, args, oracle_docs=200)
+        incremental = _side("resident C4", lambda: _incremental(eng, batch, args, oracle_docs=200))
         _progress("resident C4 leg done")
         # the same event on text documents (C3: RGA inserts / deletes on the resident element order)
         c3 = synth.generate(synth.config("C3", n_docs=args.text_docs), threads=min(16, os.cpu_count() or 1))
-        incremental_text = _incremental(eng, c3, args, tail=8, oracle_docs=200)
+        incremental_text = _side("resident C3", lambda: _incremental(eng, c3, args, tail=8, oracle_docs=200))
         _progress("resident C3 leg done")
         incremental_text["workload"] = f"C3: {c3.n_docs} text docs x 8 actors, the last 8 changes of each in rounds of 1-2"
         del c3
@@ -466,10 +482,11 @@ def main() -> int:
         # changes, object creation, a second list per document)
         if args.c5_docs > 0:
             c5 = synth.generate(synth.config("C5", n_docs=args.c5_docs), threads=min(16, os.cpu_count() or 1))
-            incremental_c5 = _incremental(eng, c5, args, tail=4, oracle_docs=200)
+            incremental_c5 = _side("resident C5", lambda: _incremental(eng, c5, args, tail=4, oracle_docs=200))
             incremental_c5["workload"] = (f"C5: {c5.n_docs} nested map / list docs x 4 actors, 20% delivered before "
                                           f"their deps, 3% duplicates; the last 4 changes of each in rounds of 1-2")
-            incremental_c5["bail_share"] = 1.0 - incremental_c5["incremental_share"]
+            if "incremental_share" in incremental_c5:
+                incremental_c5["bail_share"] = 1.0 - incremental_c5["incremental_share"]
             _progress("resident C5 leg done")
             incremental_c5["policy"] = ("incremental mode 1 (the default): a document with lists and <= 256 ops re-merges "
                                         "(one small-kernel wave either way) and keeps no incremental state")
@@ -477,35 +494,40 @@ def main() -> int:
     # the Node host path end to end through the DocBackend message API (C2 sample)
     node = None
     if rank == 0 and ws == 1 and not args.no_node:
-        node = _node_e2e(args)
+        node = _side("node legs", lambda: _node_e2e(args))
         _progress("node legs done")
     # the same workload in RepoBackend.loadDocument's arrival order (actor-major concatenation,
     # src/RepoBackend.ts:242-248): changes whose deps come later in the array wait in the queue
     orders = None
     if rank == 0 and ws == 1 and args.arrival is None and args.config == "C4" and not args.no_orders:
-        del run
-        torch.cuda.empty_cache()
-        cfg_am = synth.config(args.config, n_docs=args.docs, shard=rank, n_shards=ws, arrival=1)
-        b_am = synth.generate(cfg_am, threads=min(16, os.cpu_count() or 1))
-        r_am = _Resident(eng, b_am, dev, stream)
-        for _ in range(2):
-            r_am.step()
-        torch.cuda.synchronize(dev)
-        k_am = max(3, args.steps // 2)
-        t = time.perf_counter()
-        for _ in range(k_am):
-            r_am.step()
-        torch.cuda.synchronize(dev)
-        dt = (time.perf_counter() - t) / k_am
-        kr = r_am.kernel_roofline(3)
-        ap = int(r_am.docs_res["hist_len"].astype(np.int64).sum())
-        _progress("actor-major leg done")
-        orders = {"actor_major": {"value": ap / dt, "unit": "changes/s", "ms_per_step": dt * 1e3,
-                                  "roofline_frac": kr["frac"], "kernel": kr["kernel"],
-                                  "unsupported_docs": int((r_am.docs_res["status"] == 16).sum()),
-                                  "order": "RepoBackend.loadDocument (actor-major, src/RepoBackend.ts:242-248)"},
-                  "generation": {"value": value, "order": "generation (every change ready on arrival)"}}
-        del r_am, b_am
+        try:
+            del run
+            torch.cuda.empty_cache()
+            cfg_am = synth.config(args.config, n_docs=args.docs, shard=rank, n_shards=ws, arrival=1)
+            b_am = synth.generate(cfg_am, threads=min(16, os.cpu_count() or 1))
+            r_am = _Resident(eng, b_am, dev, stream)
+            for _ in range(2):
+                r_am.step()
+            torch.cuda.synchronize(dev)
+            k_am = max(3, args.steps // 2)
+            t = time.perf_counter()
+            for _ in range(k_am):
+                r_am.step()
+            torch.cuda.synchronize(dev)
+            dt = (time.perf_counter() - t) / k_am
+            kr = r_am.kernel_roofline(3)
+            ap = int(r_am.docs_res["hist_len"].astype(np.int64).sum())
+            _progress("actor-major leg done")
+            orders = {"actor_major": {"value": ap / dt, "unit": "changes/s", "ms_per_step": dt * 1e3,
+                                      "roofline_frac": kr["frac"], "kernel": kr["kernel"],
+                                      "unsupported_docs": int((r_am.docs_res["status"] == 16).sum()),
+                                      "order": "RepoBackend.loadDocument (actor-major, src/RepoBackend.ts:242-248)"},
+                      "generation": {"value": value, "order": "generation (every change ready on arrival)"}}
+            del r_am, b_am
+        except Exception as ex:                                # noqa: BLE001 (reported, not hidden)
+            _progress(f"actor-major leg failed: {type(ex).__name__}: {ex}")
+            orders = {"actor_major": {"error": f"{type(ex).__name__}: {ex}"[:300]}}
+
     traffic = None
     if rank == 0 and ws == 1 and not args.no_traffic:
         traffic = _pmc_traffic(args, kern["kernel"])

@@ -130,3 +130,24 @@ def test_compact_line_from_the_round5_record():
     full["legs_padding"] = "x" * 10
     big = dict(full, resident_incremental=dict(full["resident_incremental"], value=1.0))
     assert len(b.dump_line(big)) < 4096
+
+
+def test_failed_side_legs_keep_the_headline():
+    """A side leg that raises (a Node timeout, a missing tool) is reported as an error in the
+    line, and the headline, roofline and the other legs still print."""
+    import json
+    b = _bench()
+    full = json.load(open(os.path.join(ROOT, "profiles", "r05", "final4", "bench_line.json")))
+    err = b._side("node legs", lambda: (_ for _ in ()).throw(TimeoutError("node ran 900 s")))
+    assert err == {"error": "TimeoutError: node ran 900 s"}
+    full["node_docbackend"] = err
+    full["resident_incremental_text"] = {"error": "RuntimeError: x"}
+    full["from_blocks"] = {"error": "OSError: y"}
+    full["arrival_orders"] = {"actor_major": {"error": "MemoryError: z"}}
+    line = json.loads(b.dump_line(full))
+    assert line["value"] == full["value"] and line["roofline"]["frac"] is not None
+    assert line["legs"]["node"]["error"].startswith("TimeoutError")
+    assert line["legs"]["resident_c3"] == {"error": "RuntimeError: x"}
+    assert line["legs"]["from_blocks"] == {"error": "OSError: y"}
+    assert line["legs"]["actor_major"] == {"error": "MemoryError: z"}
+    assert line["legs"]["resident_c4"]["speedup"] > 1
