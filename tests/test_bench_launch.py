@@ -145,7 +145,7 @@ def test_failed_side_legs_keep_the_headline():
     full["from_blocks"] = {"error": "OSError: y"}
     full["arrival_orders"] = {"actor_major": {"error": "MemoryError: z"}}
     line = json.loads(b.dump_line(full))
-    assert line["value"] == full["value"] and line["roofline"]["frac"] is not None
+    assert abs(line["value"] - full["value"]) / full["value"] < 1e-5 and line["roofline"]["frac"] is not None
     assert line["legs"]["node"]["error"].startswith("TimeoutError")
     assert line["legs"]["resident_c3"] == {"error": "RuntimeError: x"}
     assert line["legs"]["from_blocks"] == {"error": "OSError: y"}
