@@ -362,12 +362,23 @@ __global__ __launch_bounds__(PLAN_WG) void plan_kernel(PlanArgs a) {
         const IncState I = a.ist[h];
         if ((I.flags & (HM_IST_VALID | HM_IST_NOCKEY)) != HM_IST_VALID) inc = false;
         else if ((r.flags | m.flags) & HM_DOC_HAS_LISTS)
-            for (uint32_t k = r.op_off; k < r.op_off + r.n_ops && inc; k++) {
-                const uint4 w = reinterpret_cast<const uint4 *>(a.ops + k)[0];
-                const uint32_t act = reinterpret_cast<const uint4 *>(a.ops + k)[1].x & 0xFFu, obj = w.x;
-                const bool other = obj != 0 && (obj >= 64 || !((I.mapmask >> obj) & 1ull));   // not ROOT / a map
-                if (act <= HM_MAKE_TEXT || (other && !(I.flags & HM_IST_LIST))) inc = false;
-                wave |= other;
+            // (four op rows in flight per step: the lane's loads are otherwise one round trip each)
+            for (uint32_t k0 = r.op_off; k0 < r.op_off + r.n_ops && inc; k0 += 4) {
+                uint32_t ob[4], ac[4];
+#pragma unroll
+                for (uint32_t u = 0; u < 4; u++) {
+                    const uint32_t k = k0 + u < r.op_off + r.n_ops ? k0 + u : r.op_off;
+                    ob[u] = reinterpret_cast<const uint4 *>(a.ops + k)[0].x;
+                    ac[u] = reinterpret_cast<const uint4 *>(a.ops + k)[1].x & 0xFFu;
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < 4; u++) {
+                    if (k0 + u >= r.op_off + r.n_ops) break;
+                    const uint32_t obj = ob[u];
+                    const bool other = obj != 0 && (obj >= 64 || !((I.mapmask >> obj) & 1ull));   // not ROOT / a map
+                    if (ac[u] <= HM_MAKE_TEXT || (other && !(I.flags & HM_IST_LIST))) inc = false;
+                    wave |= other;
+                }
             }
         // causallyReady in arrival order against the resident clock (small strides: the clock in
         // registers): a change the queue would hold, or a duplicate, goes to the re-merge at once.
