@@ -162,17 +162,59 @@ __device__ int list_plan(const Grp<G> &g, const AppendDesc &D, const IncArgs &A,
     // key that orders anchors by insertion point, then an element's before the '_head's at the same
     // point (the end of one list is the start of the next), then '_head's by list (empty lists
     // share their base with the next list): insertion point << 4 | head << 3 | list
-    const uint32_t ins_at = root ? (o_par == HM_HEAD ? lb : pold + 1u) : 0u;
-    const uint32_t akey = root ? (ins_at << 4) | (o_par == HM_HEAD ? 8u | lix : 0u) : 0u;
+    uint32_t ins_at = root ? (o_par == HM_HEAD ? lb : pold + 1u) : 0u;
     // the positions read back name the registers (a register that is no element has a stale slot)
     uint32_t at_p = HM_NONE, at_e = HM_NONE, nxt = HM_NONE;
     if (root && o_par != HM_HEAD) at_p = A.lorder[D.src_r + pold];
     if (root && ins_at < lb + lc) nxt = A.lorder[D.src_r + ins_at];
     if (eop && ecr == HM_NONE) at_e = A.lorder[D.src_r + eold];
     bad = (root && o_par != HM_HEAD && at_p != o_par) || (eop && ecr == HM_NONE && at_e != o_reg);
-    // under an old parent (or '_head') the new element must sort before the parent's first child
-    if (root && nxt != HM_NONE && A.epar[D.src_r + nxt] == o_par && !(key > A.ekey[D.src_r + nxt])) bad = true;
     if (g.bits(bad)) return INC_BAIL;
+    // under an old parent (or '_head') a new element that does not sort before the parent's first
+    // child (a concurrent insert at the same place with a smaller lamport key) goes before the
+    // parent's first child with a smaller key, or at the end of the parent's subtree: the group
+    // scans the order from the parent on, G positions a step — an element whose parent is the
+    // parent and whose key is smaller stops it, and so does one whose parent sits before the
+    // parent (or is '_head'): the first element after the parent's subtree in pre-order
+    const bool hard = root && nxt != HM_NONE && A.epar[D.src_r + nxt] == o_par && !(key > A.ekey[D.src_r + nxt]);
+    for (uint64_t hm = g.bits(hard); hm; hm &= hm - 1) {
+        const uint32_t k = (uint32_t)__builtin_ctzll(hm);
+        const uint32_t p = g.sh(o_par, k), kk = g.sh(key, k), pp = g.sh(pold, k);
+        const uint32_t start = g.sh(ins_at, k), end = g.sh(lb, k) + g.sh(lc, k);
+        uint32_t found = end;
+        bool dup = false;
+        for (uint32_t j0 = start; j0 < end && found == end; j0 += G) {
+            const uint32_t j = j0 + gl;
+            bool stop = false;
+            if (j < end) {
+                const uint32_t y = A.lorder[D.src_r + j];
+                const uint32_t py = A.epar[D.src_r + y];
+                if (py == p) {
+                    const uint32_t ky = A.ekey[D.src_r + y];
+                    dup |= ky == kk;
+                    stop = ky < kk;
+                } else if (p != HM_HEAD) {
+                    stop = py == HM_HEAD || A.epos[D.src_r + py] < pp;
+                }
+            }
+            const uint64_t sm = g.bits(stop);
+            if (sm) found = j0 + (uint32_t)__builtin_ctzll(sm);
+        }
+        if (g.bits(dup)) return INC_BAIL;                     // (the same elemId twice: the re-merge reports it)
+        if (gl == k) ins_at = found;
+    }
+    const uint32_t akey = root ? (ins_at << 4) | (o_par == HM_HEAD ? 8u | lix : 0u) : 0u;
+    // an insertion point the scan found may coincide with another anchor's (a deeper element's
+    // child placed at the same point): the anchors' order there is not the key order — re-merge
+    {
+        bool clash = false;
+        for (uint64_t rm = g.bits(root); rm; rm &= rm - 1) {
+            const uint32_t k = (uint32_t)__builtin_ctzll(rm);
+            const uint32_t ak = g.sh(akey, k), pk = g.sh(o_par, k);
+            clash |= root && ak == akey && pk != o_par;
+        }
+        if (g.bits(clash)) return INC_BAIL;
+    }
 
     // subtree sizes in the round's forest: every element counts itself at each of its ancestors
     uint32_t *sz = lscr + 2 * G;

@@ -471,16 +471,18 @@ def test_device_submit_equals_host_submit(engine):
 
 def _text_rounds():
     """A text object edited round by round: typing at the end, at the head, in the middle after an
-    element that already has children (a larger elem counter: first child), a concurrent insert
-    that sorts after an existing child (the re-merge's case), deletes, an insert after a deleted
-    element, a value overwrite, a run of inserts in one change, and a map key beside the text."""
+    element that already has children (a larger elem counter: first child), a child under that
+    child, a concurrent insert that sorts after the existing child (placed after its subtree: the
+    wave pass's scan), deletes, an insert after a deleted element, a value overwrite, a run of
+    inserts in one change, and a map key beside the text."""
     T = "text-1"
-    A, B = "aaaa", "bbbb"
+    A, B, C = "aaaa", "bbbb", "cccc"
     rounds = [[ch(A, 1, {}, mk("makeText", T), link("t", T), ins(T, "_head", 1), s(f"{A}:1", "h", T),
                   ins(T, f"{A}:1", 2), s(f"{A}:2", "e", T))]]
     rounds.append([ch(A, 2, {}, ins(T, f"{A}:2", 3), s(f"{A}:3", "y", T))])                    # typing at the end
     rounds.append([ch(B, 1, {A: 2}, ins(T, "_head", 4), s(f"{B}:4", "<", T))])                 # at the head
     rounds.append([ch(B, 2, {A: 2}, ins(T, f"{A}:1", 5), s(f"{B}:5", "+", T))])                # after h: first child
+    rounds.append([ch(C, 1, {B: 2}, ins(T, f"{B}:5", 6), s(f"{C}:6", "c", T))])                # under that child
     rounds.append([ch(A, 3, {A: 2}, ins(T, f"{A}:1", 4), s(f"{A}:4", "x", T))])                # concurrent, sorts later
     rounds.append([ch(A, 4, {B: 2}, d(f"{A}:2", T)), ch(B, 3, {A: 3}, s(f"{A}:3", "Y", T))])    # delete, overwrite
     rounds.append([ch(B, 4, {A: 4, B: 3}, ins(T, f"{A}:2", 9), s(f"{B}:9", "!", T),             # after a deleted one
@@ -532,7 +534,7 @@ def test_incremental_edits_on_several_lists(engine):
         bb, g = assert_doc_matches_oracle(A, ha)
         _, gb = B.read(hb)
         np.testing.assert_array_equal(g.regs, gb.regs, err_msg=f"round {i}")
-    assert sum(routed[1:]) >= len(rounds) - 2, routed          # the sorts-later insert re-merges
+    assert sum(routed[1:]) == len(rounds) - 1, routed          # every round after the load: incremental
 
 
 def test_rowstore_text_rounds_with_declared_registers(engine):
@@ -593,7 +595,7 @@ def test_incremental_text_edits_equal_remerge_and_oracle(engine):
         bb, g = assert_doc_matches_oracle(A, ha)
         _, gb = B.read(hb)
         np.testing.assert_array_equal(g.regs, gb.regs, err_msg=f"round {i}")
-    assert sum(routed[1:]) >= len(rounds) - 3, routed          # the sorts-later insert re-merges
+    assert sum(routed[1:]) == len(rounds) - 1, routed          # every round after the load: incremental
 
 
 def test_default_cost_rule_on_long_c4_rounds_matches_oracle(engine):
