@@ -83,13 +83,15 @@ constexpr unsigned long long TWO53 = 1ull << 53;
 // directory, HM_IST_LIST): the lists end to end in object-id order, so an element's position is
 // global and list k occupies [base_k, base_k + count_k).  A round's `ins` ops take the fast path
 // of applyInsert when every new element hangs off an element of its own list that exists (or
-// one this round inserted earlier) or off the list's '_head', and, under an old parent, sorts
-// before that parent's current first child (lamportCompare (elem, actor) DESCENDING: the typing
-// case, a new element with the largest elem counter): the new elements then form blocks, one per
-// old anchor, in pre-order of their own forest, placed at the anchor's insertion point; every
-// old element after an insertion point (later lists' included) shifts by the blocks before it.
-// Anything else (concurrent inserts under one parent that sort after an existing child, an
-// insert after an element not inserted yet, a duplicate elemId) goes to the re-merge.  Sets /
+// one this round inserted earlier) or off the list's '_head'.  Under an old parent its insertion
+// point is right after the parent when it sorts before the parent's current first child
+// (lamportCompare (elem, actor) DESCENDING: the typing case, a new element with the largest elem
+// counter), else before the parent's first child with a smaller key or after the parent's
+// subtree (a group scan of the order).  The new elements then form blocks, one per anchor, in
+// pre-order of their own forest, placed at the anchor's insertion point; every old element after
+// an insertion point (later lists' included) shifts by the blocks before it.  Anything else (an
+// insert after an element not inserted yet, a duplicate elemId, anchors of different parents at
+// one point) goes to the re-merge.  Sets /
 // deletes on elements are applyAssign as for map keys; the visible indices (per list) are then
 // rewritten from the first position that changed.
 // per document (a group of G lanes): anchors (G), cumulative block sizes (G), subtree sizes (G)
